@@ -1,0 +1,232 @@
+// Memory-bound vision kernels for gfx950: frame pre-processing, pooling, classifier head.
+// All NHWC, bf16 activations, 16-byte vectorised where the layout allows (Guideline 13).
+#include "common.h"
+
+namespace aiko {
+
+// ---------------------------------------------------------------------------------------------
+// uint8 RGB frames [B, Hin, Win, 3] -> bf16 [B, Hp, Wp, 4] normalised ((x/255 - mean) / std),
+// bilinearly resized to (Ho, Wo) (half-pixel centres, like cv2.INTER_LINEAR) and written into
+// the interior of a zero-bordered buffer at offset (pad_t, pad_l).  The 4th channel is zero.
+// This is the fused resize + colour-normalise + layout kernel feeding the ResNet-50 stem.
+// One thread per padded output pixel (8-byte store), border pixels written as zeros so the
+// buffer never needs a separate memset.
+__global__ void preprocess_kernel(const uint8_t* __restrict__ in, bf16_t* __restrict__ out,
+                                  int B, int Hin, int Win, int Ho, int Wo, int Hp, int Wp,
+                                  int pad_t, int pad_l, float m0, float m1, float m2,
+                                  float is0, float is1, float is2, int bgr) {
+  const long total = (long)B * Hp * Wp;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int b = idx / (Hp * Wp);
+    const int rem = idx - (long)b * Hp * Wp;
+    const int yp = rem / Wp;
+    const int xp = rem - yp * Wp;
+    const int yo = yp - pad_t, xo = xp - pad_l;
+    uint2 o = {0u, 0u};
+    if (yo >= 0 && yo < Ho && xo >= 0 && xo < Wo) {
+      float c[3];
+      if (Hin == Ho && Win == Wo) {
+        const uint8_t* px = in + (((long)b * Hin + yo) * Win + xo) * 3;
+        c[0] = px[0]; c[1] = px[1]; c[2] = px[2];
+      } else {
+        const float sy = fmaxf(((yo + 0.5f) * Hin) / Ho - 0.5f, 0.f);
+        const float sx = fmaxf(((xo + 0.5f) * Win) / Wo - 0.5f, 0.f);
+        int y0 = (int)sy, x0 = (int)sx;
+        y0 = min(y0, Hin - 1); x0 = min(x0, Win - 1);
+        const int y1 = min(y0 + 1, Hin - 1), x1 = min(x0 + 1, Win - 1);
+        const float fy = sy - y0, fx = sx - x0;
+        const uint8_t* base = in + (long)b * Hin * Win * 3;
+        const uint8_t* p00 = base + ((long)y0 * Win + x0) * 3;
+        const uint8_t* p01 = base + ((long)y0 * Win + x1) * 3;
+        const uint8_t* p10 = base + ((long)y1 * Win + x0) * 3;
+        const uint8_t* p11 = base + ((long)y1 * Win + x1) * 3;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const float top = p00[k] + (p01[k] - (float)p00[k]) * fx;
+          const float bot = p10[k] + (p11[k] - (float)p10[k]) * fx;
+          c[k] = top + (bot - top) * fy;
+        }
+      }
+      if (bgr) { const float t = c[0]; c[0] = c[2]; c[2] = t; }
+      const float v0 = (c[0] * (1.f / 255.f) - m0) * is0;
+      const float v1 = (c[1] * (1.f / 255.f) - m1) * is1;
+      const float v2 = (c[2] * (1.f / 255.f) - m2) * is2;
+      o.x = pack2(v0, v1);
+      o.y = pack2(v2, 0.f);
+    }
+    *reinterpret_cast<uint2*>(out + idx * 4) = o;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Max pool (k x k, stride s, pad p) NHWC bf16, C % 8 == 0: one thread per 8 channels of one
+// output pixel (16-byte loads/stores).  Padding never wins (-inf).
+__global__ void maxpool_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int B,
+                               int H, int W, int C, int Ho, int Wo, int k, int s, int p) {
+  const int C8 = C >> 3;
+  const long total = (long)B * Ho * Wo * C8;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int c8 = idx % C8;
+    long t = idx / C8;
+    const int wo = t % Wo; t /= Wo;
+    const int ho = t % Ho;
+    const int b = t / Ho;
+    float m[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
+    for (int dy = 0; dy < k; ++dy) {
+      const int ih = ho * s - p + dy;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int dx = 0; dx < k; ++dx) {
+        const int iw = wo * s - p + dx;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(
+            x + (((long)b * H + ih) * W + iw) * C + c8 * 8);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          m[2 * e] = fmaxf(m[2 * e], __uint_as_float(v[e] << 16));
+          m[2 * e + 1] = fmaxf(m[2 * e + 1], __uint_as_float(v[e] & 0xffff0000u));
+        }
+      }
+    }
+    u32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = pack2(m[2 * e], m[2 * e + 1]);
+    *reinterpret_cast<u32x4*>(y + idx * 8) = o;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Global average pool NHWC bf16 [B, HW, C] -> bf16 [B, C]; one thread per 8 channels.
+__global__ void avgpool_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int B,
+                               int HW, int C) {
+  const int C8 = C >> 3;
+  const long total = (long)B * C8;
+  const float inv = 1.f / HW;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int c8 = idx % C8;
+    const int b = idx / C8;
+    float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const bf16_t* src = x + (long)b * HW * C + c8 * 8;
+    for (int i = 0; i < HW; ++i) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(src + (long)i * C);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[2 * e] += __uint_as_float(v[e] << 16);
+        a[2 * e + 1] += __uint_as_float(v[e] & 0xffff0000u);
+      }
+    }
+    u32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = pack2(a[2 * e] * inv, a[2 * e + 1] * inv);
+    *reinterpret_cast<u32x4*>(y + idx * 8) = o;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Row softmax + top-k (k <= 8) over bf16 logits [B, N]: one wave per row.  Each lane keeps
+// its strided slice in registers (N <= 64 * 32), the wave reduces max / sum-exp with
+// shuffles, then k rounds of wave-wide argmax extract the top-k (ties -> lowest index).
+template <int PER_LANE>
+__global__ void softmax_topk_kernel(const bf16_t* __restrict__ logits, float* __restrict__ prob,
+                                    int* __restrict__ index, int B, int N, int k) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const bf16_t* src = logits + (long)row * N;
+  float v[PER_LANE];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < PER_LANE; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = c < N ? bf2f(src[c]) : -INFINITY;
+    mx = fmaxf(mx, v[i]);
+  }
+  mx = wave_max(mx);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER_LANE; ++i) {
+    const int c = lane + 64 * i;
+    s += c < N ? __expf(v[i] - mx) : 0.f;
+  }
+  s = wave_sum(s);
+  const float inv = 1.f / s;
+  for (int t = 0; t < k; ++t) {
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int i = 0; i < PER_LANE; ++i) {
+      const int c = lane + 64 * i;
+      if (v[i] > best || (v[i] == best && c < bi)) { best = v[i]; bi = c; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    if (lane == 0) {
+      prob[(long)row * k + t] = __expf(best - mx) * inv;
+      index[(long)row * k + t] = bi;
+    }
+#pragma unroll
+    for (int i = 0; i < PER_LANE; ++i)
+      if (lane + 64 * i == bi) v[i] = -INFINITY;
+  }
+}
+
+}  // namespace aiko
+
+static inline int grid_for(long total, int block) {
+  long g = (total + block - 1) / block;
+  if (g > 256 * 16) g = 256 * 16;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+extern "C" int aiko_preprocess(const void* in, void* out, int B, int Hin, int Win, int Ho,
+                               int Wo, int Hp, int Wp, int pad_t, int pad_l, const float* mean,
+                               const float* std, int bgr, hipStream_t stream) {
+  const long total = (long)B * Hp * Wp;
+  hipLaunchKernelGGL(aiko::preprocess_kernel, dim3(grid_for(total, 256)), dim3(256), 0, stream,
+                     static_cast<const uint8_t*>(in), static_cast<aiko::bf16_t*>(out), B, Hin,
+                     Win, Ho, Wo, Hp, Wp, pad_t, pad_l, mean[0], mean[1], mean[2],
+                     1.f / std[0], 1.f / std[1], 1.f / std[2], bgr);
+  return (int)hipGetLastError();
+}
+
+extern "C" int aiko_maxpool(const void* x, void* y, int B, int H, int W, int C, int Ho, int Wo,
+                            int k, int s, int p, hipStream_t stream) {
+  const long total = (long)B * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(aiko::maxpool_kernel, dim3(grid_for(total, 256)), dim3(256), 0, stream,
+                     static_cast<const aiko::bf16_t*>(x), static_cast<aiko::bf16_t*>(y), B, H, W,
+                     C, Ho, Wo, k, s, p);
+  return (int)hipGetLastError();
+}
+
+extern "C" int aiko_avgpool(const void* x, void* y, int B, int HW, int C, hipStream_t stream) {
+  const long total = (long)B * (C / 8);
+  hipLaunchKernelGGL(aiko::avgpool_kernel, dim3(grid_for(total, 256)), dim3(256), 0, stream,
+                     static_cast<const aiko::bf16_t*>(x), static_cast<aiko::bf16_t*>(y), B, HW, C);
+  return (int)hipGetLastError();
+}
+
+extern "C" int aiko_softmax_topk(const void* logits, float* prob, int* index, int B, int N, int k,
+                                 hipStream_t stream) {
+  const int rows_per_block = 4;
+  dim3 grid((B + rows_per_block - 1) / rows_per_block), block(64 * rows_per_block);
+  const aiko::bf16_t* l = static_cast<const aiko::bf16_t*>(logits);
+  if (N <= 64 * 4) {
+    aiko::softmax_topk_kernel<4><<<grid, block, 0, stream>>>(l, prob, index, B, N, k);
+  } else if (N <= 64 * 16) {
+    aiko::softmax_topk_kernel<16><<<grid, block, 0, stream>>>(l, prob, index, B, N, k);
+  } else if (N <= 64 * 32) {
+    aiko::softmax_topk_kernel<32><<<grid, block, 0, stream>>>(l, prob, index, B, N, k);
+  } else {
+    return -1;
+  }
+  return (int)hipGetLastError();
+}

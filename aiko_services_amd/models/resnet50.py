@@ -1,0 +1,196 @@
+"""ResNet-50 (v1.5) inference on aiko_services_amd's HIP kernels — NHWC bf16, BN folded.
+
+Not present in the reference (which delegates every model to third-party libraries, SURVEY
+§2.4 K12); it is the model of BASELINE config 2/3 and the bench headline.  Architecture as
+torchvision ``resnet50``: 7x7/2 stem, 3x3/2 max-pool, bottleneck stages [3, 4, 6, 3] with the
+stride on the 3x3 conv, global average pool, 2048 -> 1000 classifier.
+
+Execution plan per forward (B frames, all on one HIP stream, graph-capturable):
+
+  preprocess (u8 resize/normalise -> padded 4-ch)  -> stem igemm (+bias+ReLU)
+  -> maxpool -> 16 bottlenecks (3 igemm convs each; the 3rd fuses bias + residual + ReLU,
+     the projection shortcut is one more igemm) -> avgpool -> FC igemm -> softmax/top-k
+
+Weights are random-init (no checkpoints offline) with deterministic seeds; BatchNorm running
+statistics are random too and folded into the conv weights at construction.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+from ..ops import conv as C
+from ..ops import vision as V
+
+STAGES = ((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2))
+EXPANSION = 4
+
+
+def _rand_bn(g: torch.Generator, c: int, gamma_range=(0.5, 1.0)):
+    lo, hi = gamma_range
+    gamma = lo + (hi - lo) * torch.rand(c, generator=g)
+    beta = 0.1 * torch.randn(c, generator=g)
+    mean = 0.1 * torch.randn(c, generator=g)
+    var = 0.5 + torch.rand(c, generator=g)
+    return gamma, beta, mean, var
+
+
+def _rand_conv(g: torch.Generator, cout: int, cin: int, k: int) -> torch.Tensor:
+    fan_in = cin * k * k
+    return torch.randn(cout, cin, k, k, generator=g) * math.sqrt(2.0 / fan_in)
+
+
+@dataclass
+class Bottleneck:
+    conv1: C.ConvSpec
+    conv2: C.ConvSpec
+    conv3: C.ConvSpec
+    down: C.ConvSpec | None
+
+
+class ResNet50:
+    """Packed ResNet-50 for inference.  ``forward(frames_u8) -> (top-k probs, top-k ids)``."""
+
+    def __init__(self, num_classes: int = 1000, seed: int = 0, device="cuda", image_size=224,
+                 topk: int = 5):
+        self.device = torch.device(device)
+        self.image_size = image_size
+        self.num_classes = num_classes
+        self.topk = topk
+        g = torch.Generator().manual_seed(seed)
+        w = _rand_conv(g, 64, 3, 7)
+        wf, b = C.fold_bn(w, *_rand_bn(g, 64))
+        self.stem = C.make_stem_spec(wf, b, act="relu", device=self.device)
+        self.blocks: list[Bottleneck] = []
+        cin = 64
+        for width, nblocks, stride in STAGES:
+            for i in range(nblocks):
+                s = stride if i == 0 else 1
+                cout = width * EXPANSION
+                c1 = C.make_conv_spec(*C.fold_bn(_rand_conv(g, width, cin, 1), *_rand_bn(g, width)),
+                                      act="relu", device=self.device)
+                c2 = C.make_conv_spec(*C.fold_bn(_rand_conv(g, width, width, 3), *_rand_bn(g, width)),
+                                      stride=s, pad=1, act="relu", device=self.device)
+                # small gamma on the last BN keeps the random residual stream bounded
+                c3 = C.make_conv_spec(*C.fold_bn(_rand_conv(g, cout, width, 1),
+                                                 *_rand_bn(g, cout, (0.1, 0.3))),
+                                      act="relu", device=self.device)
+                down = None
+                if i == 0:
+                    down = C.make_conv_spec(*C.fold_bn(_rand_conv(g, cout, cin, 1), *_rand_bn(g, cout)),
+                                            stride=s, act=None, device=self.device)
+                self.blocks.append(Bottleneck(c1, c2, c3, down))
+                cin = cout
+        fc_w = 0.01 * torch.randn(num_classes, 2048, generator=g)
+        fc_b = torch.zeros(num_classes)
+        self.fc = C.make_linear_spec(fc_w, fc_b, device=self.device)
+        self._ws: dict = {}
+
+    # ---- workspace: every activation buffer allocated once per batch size ----------------
+    def _buf(self, key: str, shape, dtype=torch.bfloat16) -> torch.Tensor:
+        k = (key, tuple(shape), dtype)
+        t = self._ws.get(k)
+        if t is None:
+            t = torch.empty(shape, dtype=dtype, device=self.device)
+            self._ws[k] = t
+        return t
+
+    def release_workspace(self) -> None:
+        self._ws.clear()
+
+    # ---- forward ------------------------------------------------------------------------
+    def features(self, frames: torch.Tensor) -> torch.Tensor:
+        """uint8 [B, H, W, 3] -> pooled features bf16 [B, 2048]."""
+        B = frames.shape[0]
+        S = self.image_size
+        Hp, Wp = C.stem_geometry(S, S)
+        x = V.preprocess_frames(frames, (S, S), out=self._buf("pre", (B, Hp, Wp, 4)))
+        Ho, Wo = C.stem_out_hw(S, S)
+        x = C.conv2d(x, self.stem, out=self._buf("stem", (B, Ho, Wo, 64)), image_hw=(S, S))
+        Hm, Wm = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
+        x = V.maxpool2d(x, 3, 2, 1, out=self._buf("pool", (B, Hm, Wm, 64)))
+        for bi, blk in enumerate(self.blocks):
+            H, W = x.shape[1], x.shape[2]
+            t1 = C.conv2d(x, blk.conv1, out=self._buf("t1", (B, H, W, blk.conv1.cout)))
+            Ho, Wo = blk.conv2.out_hw(H, W)
+            t2 = C.conv2d(t1, blk.conv2, out=self._buf("t2", (B, Ho, Wo, blk.conv2.cout)))
+            if blk.down is not None:
+                idn = C.conv2d(x, blk.down, out=self._buf("ds", (B, Ho, Wo, blk.down.cout)))
+            else:
+                idn = x
+            key = "xa" if bi % 2 == 0 else "xb"
+            x = C.conv2d(t2, blk.conv3, residual=idn, out=self._buf(key, (B, Ho, Wo, blk.conv3.cout)))
+        return V.avgpool(x, out=self._buf("gap", (B, x.shape[3])))
+
+    def logits(self, frames: torch.Tensor) -> torch.Tensor:
+        f = self.features(frames)
+        return C.linear(f, self.fc, out=self._buf("logits", (f.shape[0], self.num_classes)))
+
+    def forward(self, frames: torch.Tensor):
+        lg = self.logits(frames)
+        B = lg.shape[0]
+        return V.softmax_topk(lg, self.topk,
+                              prob=self._buf("prob", (B, self.topk), torch.float32),
+                              index=self._buf("index", (B, self.topk), torch.int32))
+
+    __call__ = forward
+
+    # ---- bookkeeping ----------------------------------------------------------------------
+    def conv_specs(self):
+        yield "stem", self.stem
+        for i, b in enumerate(self.blocks):
+            yield f"b{i}.conv1", b.conv1
+            yield f"b{i}.conv2", b.conv2
+            yield f"b{i}.conv3", b.conv3
+            if b.down is not None:
+                yield f"b{i}.down", b.down
+        yield "fc", self.fc
+
+    def flops_per_image(self) -> int:
+        """Multiply-adds x 2 of every conv/FC at the configured resolution (≈ 8.2 GFLOP)."""
+        total = 0
+        S = self.image_size
+        H, W = C.stem_out_hw(S, S)
+        total += 2 * H * W * 64 * 3 * 49
+        H, W = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        for b in self.blocks:
+            total += b.conv1.flops(1, H, W)
+            Ho, Wo = b.conv2.out_hw(H, W)
+            total += b.conv2.flops(1, H, W)
+            total += b.conv3.flops(1, Ho, Wo)
+            if b.down is not None:
+                total += b.down.flops(1, H, W)
+            H, W = Ho, Wo
+        total += 2 * 2048 * self.num_classes
+        return total
+
+    def state_dict(self) -> dict:
+        """Packed weights (bf16 [Cout, K]) and fp32 biases, for save/load of random inits."""
+        sd = {}
+        for name, spec in self.conv_specs():
+            sd[f"{name}.weight"] = spec.weight.detach().cpu()
+            if spec.bias is not None:
+                sd[f"{name}.bias"] = spec.bias.detach().cpu()
+        return sd
+
+    def load_state_dict(self, sd: dict) -> None:
+        for name, spec in self.conv_specs():
+            spec.weight.copy_(sd[f"{name}.weight"].to(spec.weight.device))
+            if spec.bias is not None:
+                spec.bias.copy_(sd[f"{name}.bias"].to(spec.bias.device))
+
+    # ---- fp32 torch reference (tests only) -------------------------------------------------
+    def reference_logits(self, frames: torch.Tensor) -> torch.Tensor:
+        from ..ops import reference as R
+        x = R.preprocess_ref(frames, (self.image_size, self.image_size))
+        x = R.conv_ref(x, self.stem)
+        x = torch.nn.functional.max_pool2d(x, 3, 2, 1)
+        for b in self.blocks:
+            t = R.conv_ref(x, b.conv1)
+            t = R.conv_ref(t, b.conv2)
+            idn = R.conv_ref(x, b.down) if b.down is not None else x
+            x = R.conv_ref(t, b.conv3, residual_nchw=idn)
+        x = x.mean(dim=(2, 3))
+        return R.linear_ref(x, self.fc)

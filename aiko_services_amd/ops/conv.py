@@ -1,0 +1,208 @@
+"""Convolution / linear layers on the implicit-GEMM MFMA kernel (``csrc/kernels/conv_igemm.hip``).
+
+Layouts (MI355X-first, chosen for the kernel, not for torch):
+
+* activations are NHWC bf16 (``[B, H, W, C]`` contiguous) so an output pixel's channels are a
+  contiguous GEMM row and every conv becomes ``[B*Ho*Wo, K] x [K, Cout]``;
+* weights are packed once to ``[Cout, K]`` bf16 with K ordered (r, s, c) — the "B^T" layout
+  whose rows the kernel stages into LDS exactly like the activation rows;
+* BatchNorm is folded into the weights and an fp32 bias at pack time (inference), and the
+  bias / residual add / ReLU|SiLU run in the kernel epilogue.
+
+The ResNet stem (7x7/s2, 3 input channels) uses a pre-padded 4-channel input written by the
+fused pre-processing kernel: with 4 channels per pixel a 32-element chunk of one input row
+covers the 7 horizontal taps of one filter row, so the stem is an implicit GEMM with K = 8x32
+(see :func:`make_stem_spec`).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+
+ACT_NONE, ACT_RELU, ACT_SILU = 0, 1, 2
+_ACTS = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "silu": ACT_SILU}
+
+
+@dataclass
+class ConvSpec:
+    """A packed, inference-ready conv (or linear) layer."""
+
+    weight: torch.Tensor            # [Cout, K] bf16
+    bias: torch.Tensor | None       # [Cout] fp32
+    cin: int
+    cout: int
+    R: int
+    S: int
+    stride: int
+    pad: int
+    Cc: int                         # contiguous channel run per tap (multiple of 8)
+    act: int = ACT_NONE
+    kind: str = "conv"              # conv | stem | linear
+    ref_weight: torch.Tensor | None = field(default=None, repr=False)  # fp32 OIHW (folded)
+    ref_bias: torch.Tensor | None = field(default=None, repr=False)
+
+    def to(self, device) -> "ConvSpec":
+        self.weight = self.weight.to(device)
+        if self.bias is not None:
+            self.bias = self.bias.to(device)
+        return self
+
+    @property
+    def K(self) -> int:
+        return self.weight.shape[1]
+
+    def out_hw(self, H: int, W: int) -> tuple[int, int]:
+        if self.kind == "stem":
+            return stem_out_hw(H, W)
+        return ((H + 2 * self.pad - self.R) // self.stride + 1,
+                (W + 2 * self.pad - self.S) // self.stride + 1)
+
+    def flops(self, B: int, H: int, W: int) -> int:
+        Ho, Wo = self.out_hw(H, W)
+        k_real = self.cin * self.R * self.S if self.kind != "stem" else 3 * 49
+        return 2 * B * Ho * Wo * self.cout * k_real
+
+
+def _act(act) -> int:
+    return act if isinstance(act, int) else _ACTS[act]
+
+
+def fold_bn(w: torch.Tensor, gamma, beta, mean, var, eps=1e-5, conv_bias=None):
+    """Fold inference BatchNorm into (weight, bias) — fp32."""
+    scale = gamma / torch.sqrt(var + eps)
+    wf = w * scale.reshape(-1, *([1] * (w.dim() - 1)))
+    b = beta - mean * scale
+    if conv_bias is not None:
+        b = b + conv_bias * scale
+    return wf, b
+
+
+def make_conv_spec(w_oihw: torch.Tensor, bias: torch.Tensor | None, stride=1, pad=0, act=None,
+                   device=None, cin_pitch: int | None = None) -> ConvSpec:
+    """Pack an fp32 OIHW conv weight into the kernel's ``[Cout, K]`` bf16 layout.
+
+    K is ordered (r, s, c) with the channel run padded to a multiple of 8 (``Cc``) and the
+    total padded to a multiple of 64 with zero weights.  ``cin_pitch`` is the channel pitch
+    of the input activation (defaults to ``Cc``).
+    """
+    cout, cin, R, S = w_oihw.shape
+    cc = _round_up(cin, 8)
+    k_real = R * S * cc
+    K = _round_up(k_real, 64)
+    w = torch.zeros(cout, R, S, cc, dtype=torch.float32)
+    w[..., :cin] = w_oihw.permute(0, 2, 3, 1).float()
+    packed = torch.zeros(cout, K, dtype=torch.float32)
+    packed[:, :k_real] = w.reshape(cout, k_real)
+    packed = packed.to(torch.bfloat16).contiguous()
+    ref_w = w_oihw.to(torch.bfloat16).float().contiguous()
+    spec = ConvSpec(weight=packed, bias=None if bias is None else bias.float().contiguous(),
+                    cin=cin_pitch or cc, cout=cout, R=R, S=S, stride=stride, pad=pad, Cc=cc,
+                    act=_act(act), kind="conv", ref_weight=ref_w,
+                    ref_bias=None if bias is None else bias.float().clone())
+    return spec.to(device) if device is not None else spec
+
+
+def make_linear_spec(w_oi: torch.Tensor, bias: torch.Tensor | None, act=None, device=None) -> ConvSpec:
+    cout, cin = w_oi.shape
+    spec = make_conv_spec(w_oi.reshape(cout, cin, 1, 1), bias, act=act, device=device)
+    spec.kind = "linear"
+    return spec
+
+
+# ---- stem (7x7 / stride 2 / pad 3 over 3 channels) ----------------------------------------
+
+STEM_PAD = 3
+
+
+def stem_out_hw(H: int, W: int) -> tuple[int, int]:
+    return (H + 2 * STEM_PAD - 7) // 2 + 1, (W + 2 * STEM_PAD - 7) // 2 + 1
+
+
+def stem_geometry(H: int, W: int) -> tuple[int, int]:
+    """(Hp, Wp) of the zero-bordered 4-channel stem input for an HxW image."""
+    Ho, Wo = stem_out_hw(H, W)
+    Hp = max(2 * (Ho - 1) + 8, H + STEM_PAD)
+    Wp = _round_up(max(2 * (Wo - 1) + 8, W + STEM_PAD), 8)
+    return Hp, Wp
+
+
+def make_stem_spec(w_oihw: torch.Tensor, bias: torch.Tensor | None, act="relu", device=None) -> ConvSpec:
+    """Pack a [Cout, 3, 7, 7] stem weight: K = 8 rows x 32 (= 8 pixels x 4 channels)."""
+    cout, cin, R, S = w_oihw.shape
+    assert (cin, R, S) == (3, 7, 7), "stem packing expects a 7x7 conv over 3 channels"
+    w = torch.zeros(cout, 8, 8, 4, dtype=torch.float32)  # [o][r][s(pixel)][c]
+    w[:, :7, :7, :3] = w_oihw.permute(0, 2, 3, 1).float()
+    packed = w.reshape(cout, 256).to(torch.bfloat16).contiguous()
+    ref_w = w_oihw.to(torch.bfloat16).float().contiguous()
+    spec = ConvSpec(weight=packed, bias=None if bias is None else bias.float().contiguous(),
+                    cin=3, cout=cout, R=8, S=1, stride=2, pad=0, Cc=32, act=_act(act),
+                    kind="stem", ref_weight=ref_w,
+                    ref_bias=None if bias is None else bias.float().clone())
+    return spec.to(device) if device is not None else spec
+
+
+def _round_up(v: int, m: int) -> int:
+    return (v + m - 1) // m * m
+
+
+def pick_tile(M: int, cout: int) -> tuple[int, int]:
+    """Block tile (BM, BN) for the igemm kernel: fill 256 CUs x 2 blocks first, then reuse."""
+    bn = 128 if cout % 128 == 0 else 64
+    bm = 128
+    tiles = math.ceil(M / bm) * math.ceil(cout / bn)
+    if tiles < 512:
+        bm = 64
+        tiles = math.ceil(M / bm) * math.ceil(cout / bn)
+        if tiles < 512 and bn == 128:
+            bn = 64
+    return bm, bn
+
+
+def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None,
+           out: torch.Tensor | None = None, tile: tuple[int, int] | None = None,
+           image_hw: tuple[int, int] | None = None) -> torch.Tensor:
+    """NHWC bf16 conv with fused bias / residual / activation on the MFMA igemm kernel.
+
+    ``x`` is ``[B, H, W, C]`` — possibly a channel-slice view of a wider buffer (the pixel
+    pitch is ``x.stride(2)``).  For a stem spec ``x`` is the zero-bordered ``[B, Hp, Wp, 4]``
+    buffer from :func:`aiko_services_amd.ops.preprocess_frames` and ``image_hw`` the original
+    image size.  ``residual`` (optional) has the output's shape.  ``out`` may be a channel
+    slice of a concat buffer.  Returns ``out`` ``[B, Ho, Wo, Cout]``.
+    """
+    B, H, W, C = x.shape
+    pitch = x.stride(2)
+    if x.stride(3) != 1 or x.stride(1) != W * pitch or x.stride(0) != H * W * pitch:
+        raise ValueError("conv2d: x must be NHWC with unit channel stride (a channel slice is fine)")
+    if spec.kind == "stem":
+        if image_hw is None:
+            raise ValueError("conv2d: stem conv needs image_hw")
+        Ho, Wo = stem_out_hw(*image_hw)
+    else:
+        if C < spec.Cc and pitch < spec.Cc:
+            raise ValueError(f"conv2d: input has {C} channels, spec expects {spec.Cc}")
+        Ho, Wo = spec.out_hw(H, W)
+    M = B * Ho * Wo
+    if out is None:
+        out = torch.empty(B, Ho, Wo, spec.cout, dtype=torch.bfloat16, device=x.device)
+    bm, bn = tile or pick_tile(M, spec.cout)
+    geom = [H, W, pitch, spec.Cc, spec.R, spec.S, spec.stride, spec.pad, Ho, Wo, M,
+            spec.act, out.stride(2) if out.dim() == 4 else out.stride(0),
+            0 if residual is None else (residual.stride(2) if residual.dim() == 4 else residual.stride(0)),
+            bm, bn]
+    torch.ops.aiko.conv_igemm_out(x, spec.weight, spec.bias, residual, out, geom)
+    return out
+
+
+def linear(x: torch.Tensor, spec: ConvSpec, out: torch.Tensor | None = None,
+           residual: torch.Tensor | None = None) -> torch.Tensor:
+    """``[B, K] @ W^T + b`` on the same kernel (1x1 "image")."""
+    B, K = x.shape
+    if out is None:
+        out = torch.empty(B, spec.cout, dtype=torch.bfloat16, device=x.device)
+    bm, bn = pick_tile(B, spec.cout)
+    geom = [1, 1, x.stride(0), spec.Cc, 1, 1, 1, 0, 1, 1, B, spec.act, out.stride(0),
+            0 if residual is None else residual.stride(0), bm, bn]
+    torch.ops.aiko.conv_igemm_out(x, spec.weight, spec.bias, residual, out, geom)
+    return out

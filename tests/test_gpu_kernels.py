@@ -1,0 +1,148 @@
+"""Numerics of the HIP kernels vs plain PyTorch fp32 references (run on MI355X: -m gpu)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rel_err(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _nhwc(x_nchw):
+    return x_nchw.permute(0, 2, 3, 1).contiguous()
+
+
+@pytest.mark.parametrize("B,H,W,cin,cout,k,stride,pad,act,res,tile", [
+    (2, 56, 56, 64, 64, 1, 1, 0, "relu", False, None),
+    (2, 56, 56, 64, 256, 1, 1, 0, "relu", True, None),
+    (2, 56, 56, 64, 64, 3, 1, 1, "relu", False, None),
+    (2, 56, 56, 128, 128, 3, 2, 1, "relu", False, None),
+    (3, 14, 14, 256, 1024, 1, 1, 0, None, True, (128, 128)),
+    (3, 14, 14, 256, 1024, 1, 1, 0, None, True, (64, 64)),
+    (1, 7, 7, 512, 2048, 1, 1, 0, "relu", True, (128, 64)),
+    (2, 28, 28, 256, 512, 1, 2, 0, None, False, (64, 128)),
+    (2, 20, 20, 16, 32, 3, 1, 1, "silu", False, None),    # Cin=16: 4 taps per K block
+    (2, 20, 20, 48, 64, 3, 2, 1, "silu", False, None),    # Cin=48: padded chunk
+    (1, 9, 11, 40, 24, 3, 1, 1, None, False, None),       # odd spatial, Cout=24 (N tail)
+])
+def test_conv_igemm_matches_torch(native, B, H, W, cin, cout, k, stride, pad, act, res, tile):
+    from aiko_services_amd.ops import conv as C
+    from aiko_services_amd.ops import reference as R
+    g = torch.Generator().manual_seed(1234)
+    w = torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    spec = C.make_conv_spec(w, b, stride=stride, pad=pad, act=act, device=DEV)
+    x = torch.randn(B, cin, H, W, generator=g).to(torch.bfloat16)
+    x_nhwc = torch.zeros(B, H, W, spec.Cc, dtype=torch.bfloat16)
+    x_nhwc[..., :cin] = _nhwc(x)
+    x_nhwc = x_nhwc.to(DEV)
+    Ho, Wo = spec.out_hw(H, W)
+    r = torch.randn(B, cout, Ho, Wo, generator=g).to(torch.bfloat16) if res else None
+    y = C.conv2d(x_nhwc, spec, residual=None if r is None else _nhwc(r).to(DEV), tile=tile)
+    torch.cuda.synchronize()
+    ref = R.conv_ref(x.float().to(DEV), spec, None if r is None else r.float().to(DEV))
+    err = _rel_err(y.permute(0, 3, 1, 2), ref)
+    assert err < 1e-2, err
+
+
+def test_conv_writes_into_channel_slice(native):
+    """Output into a slice of a concat buffer and input from a channel slice (pitch != Cc)."""
+    from aiko_services_amd.ops import conv as C
+    from aiko_services_amd.ops import reference as R
+    g = torch.Generator().manual_seed(7)
+    B, H, W = 2, 16, 16
+    big = torch.randn(B, H, W, 96, generator=g).to(torch.bfloat16).to(DEV)
+    xin = big[..., 32:64]                      # 32-channel slice, pitch 96
+    w = torch.randn(64, 32, 3, 3, generator=g) / 17
+    spec = C.make_conv_spec(w, None, pad=1, act="silu", device=DEV)
+    cat = torch.zeros(B, H, W, 128, dtype=torch.bfloat16, device=DEV)
+    C.conv2d(xin, spec, out=cat[..., 64:128])
+    torch.cuda.synchronize()
+    ref = R.conv_ref(xin.permute(0, 3, 1, 2).float(), spec)
+    assert _rel_err(cat[..., 64:].permute(0, 3, 1, 2), ref) < 1e-2
+    assert cat[..., :64].abs().max().item() == 0
+
+
+def test_stem_and_preprocess(native):
+    from aiko_services_amd.ops import conv as C
+    from aiko_services_amd.ops import reference as R
+    from aiko_services_amd.ops import vision as V
+    g = torch.Generator().manual_seed(3)
+    B = 3
+    frames = torch.randint(0, 256, (B, 224, 224, 3), generator=g, dtype=torch.uint8)
+    w = torch.randn(64, 3, 7, 7, generator=g) / (3 * 49) ** 0.5
+    b = torch.randn(64, generator=g) * 0.1
+    spec = C.make_stem_spec(w, b, act="relu", device=DEV)
+    pre = V.preprocess_frames(frames.to(DEV))
+    y = C.conv2d(pre, spec, image_hw=(224, 224))
+    torch.cuda.synchronize()
+    xr = R.preprocess_ref(frames.to(DEV))
+    # the pre-processed image (interior) must match
+    assert _rel_err(pre[:, 3:227, 3:227, :3].permute(0, 3, 1, 2), xr) < 5e-3
+    assert pre[:, :3].abs().max().item() == 0 and pre[..., 3].abs().max().item() == 0
+    ref = R.conv_ref(xr.to(torch.bfloat16).float(), spec)
+    assert y.shape == (B, 112, 112, 64)
+    assert _rel_err(y.permute(0, 3, 1, 2), ref) < 1e-2
+
+
+def test_preprocess_resize(native):
+    from aiko_services_amd.ops import reference as R
+    from aiko_services_amd.ops import vision as V
+    frames = torch.randint(0, 256, (2, 480, 640, 3), dtype=torch.uint8)
+    pre = V.preprocess_frames(frames.to(DEV), (224, 224))
+    ref = R.preprocess_ref(frames.to(DEV), (224, 224))
+    assert _rel_err(pre[:, 3:227, 3:227, :3].permute(0, 3, 1, 2), ref) < 1e-2
+
+
+def test_linear_with_n_tail(native):
+    from aiko_services_amd.ops import conv as C
+    from aiko_services_amd.ops import reference as R
+    g = torch.Generator().manual_seed(5)
+    for B in (1, 7, 256):
+        w = torch.randn(1000, 2048, generator=g) * 0.02
+        b = torch.randn(1000, generator=g)
+        spec = C.make_linear_spec(w, b, device=DEV)
+        x = torch.randn(B, 2048, generator=g).to(torch.bfloat16).to(DEV)
+        y = C.linear(x, spec)
+        torch.cuda.synchronize()
+        assert _rel_err(y, R.linear_ref(x.float(), spec)) < 1e-2
+
+
+def test_pools_and_topk(native):
+    from aiko_services_amd.ops import vision as V
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(2, 112, 112, 64, generator=g).to(torch.bfloat16).to(DEV)
+    y = V.maxpool2d(x, 3, 2, 1)
+    ref = torch.nn.functional.max_pool2d(x.permute(0, 3, 1, 2).float(), 3, 2, 1)
+    assert torch.equal(y.permute(0, 3, 1, 2).float(), ref)
+    x = torch.randn(4, 7, 7, 2048, generator=g).to(torch.bfloat16).to(DEV)
+    a = V.avgpool(x)
+    assert _rel_err(a, x.float().mean(dim=(1, 2))) < 5e-3
+    lg = torch.randn(37, 1000, generator=g).to(torch.bfloat16).to(DEV)
+    p, i = V.softmax_topk(lg, 5)
+    torch.cuda.synchronize()
+    rp, ri = torch.softmax(lg.float(), -1).topk(5, -1)
+    # bf16 logits can tie: compare the selected logit values, not tie-broken indices
+    assert torch.equal(lg.float().gather(1, i.long()), lg.float().gather(1, ri))
+    assert torch.allclose(p, rp, rtol=1e-3, atol=1e-5)
+
+
+def test_resnet50_matches_fp32_reference(native):
+    from aiko_services_amd.models.resnet50 import ResNet50
+    m = ResNet50(seed=0, device=DEV)
+    frames = torch.randint(0, 256, (4, 224, 224, 3), dtype=torch.uint8,
+                           generator=torch.Generator().manual_seed(0)).to(DEV)
+    lg = m.logits(frames).float()
+    ref = m.reference_logits(frames)
+    torch.cuda.synchronize()
+    cos = torch.nn.functional.cosine_similarity(lg, ref, dim=1)
+    assert cos.min().item() > 0.995, cos
+    p, i = m(frames)
+    torch.cuda.synchronize()
+    assert p.shape == (4, 5) and i.shape == (4, 5)
+    assert (i[:, 0].long() == lg.argmax(1)).all()
