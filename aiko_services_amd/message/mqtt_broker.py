@@ -1,0 +1,298 @@
+"""In-repo MQTT 3.1.1 broker (single thread, ``selectors``) — replaces the external mosquitto.
+
+Supports what the aiko control plane relies on: QoS 0 and 1, retained
+messages (empty retained payload clears), last-will-and-testament on abnormal disconnect or
+keep-alive expiry, ``+``/``#`` subscriptions through a topic trie, session takeover on a
+duplicate client id.  Messages are routed with one trie lookup per publish and queued to
+per-connection output buffers flushed when writable, so one slow subscriber never blocks the
+broker loop.
+
+Run standalone:  ``python -m aiko_services_amd.message.mqtt_broker --port 1883``
+"""
+from __future__ import annotations
+
+import argparse
+import itertools
+import selectors
+import socket
+import struct
+import threading
+import time
+
+from . import mqtt_codec as C
+
+__all__ = ["Broker", "start_broker_thread"]
+
+
+class _Conn:
+    __slots__ = ("sock", "reader", "out", "client_id", "will", "keepalive", "last_rx",
+                 "connected", "subs", "closing", "pid")
+
+    def __init__(self, sock):
+        self.sock = sock
+        self.reader = C.PacketReader()
+        self.out = bytearray()
+        self.client_id = None
+        self.will = None
+        self.keepalive = 0
+        self.last_rx = time.monotonic()
+        self.connected = False
+        self.subs: dict = {}
+        self.closing = False
+        self.pid = itertools.count(1)
+
+
+class Broker:
+    def __init__(self, host: str = "127.0.0.1", port: int = 1883):
+        self.host = host
+        self.port = port
+        self.sel = selectors.DefaultSelector()
+        self.lsock: socket.socket | None = None
+        self.conns: dict = {}            # sock -> _Conn
+        self.by_client: dict = {}        # client_id -> _Conn
+        self.trie = C.TopicTrie()        # filter -> {conn: qos}
+        self.retained: dict = {}         # topic -> (payload, qos)
+        self._running = False
+        self._wake_r, self._wake_w = socket.socketpair()
+        self.stats = {"published": 0, "delivered": 0, "connections": 0}
+
+    # ---- lifecycle -------------------------------------------------------------------------
+    def bind(self):
+        s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        s.bind((self.host, self.port))
+        s.listen(256)
+        s.setblocking(False)
+        self.port = s.getsockname()[1]
+        self.lsock = s
+        self.sel.register(s, selectors.EVENT_READ, "listen")
+        self._wake_r.setblocking(False)
+        self.sel.register(self._wake_r, selectors.EVENT_READ, "wake")
+        return self.port
+
+    def stop(self):
+        self._running = False
+        try:
+            self._wake_w.send(b"x")
+        except OSError:
+            pass
+
+    def serve_forever(self):
+        if self.lsock is None:
+            self.bind()
+        self._running = True
+        last_sweep = time.monotonic()
+        try:
+            while self._running:
+                for key, mask in self.sel.select(timeout=1.0):
+                    if key.data == "listen":
+                        self._accept()
+                    elif key.data == "wake":
+                        try:
+                            self._wake_r.recv(4096)
+                        except OSError:
+                            pass
+                    else:
+                        conn = key.data
+                        if mask & selectors.EVENT_READ:
+                            self._read(conn)
+                        if mask & selectors.EVENT_WRITE and not conn.closing:
+                            self._flush(conn)
+                now = time.monotonic()
+                if now - last_sweep > 1.0:
+                    last_sweep = now
+                    self._sweep_keepalive(now)
+        finally:
+            for conn in list(self.conns.values()):
+                self._close(conn, send_will=False)
+            self.sel.close()
+            if self.lsock:
+                self.lsock.close()
+
+    # ---- connection handling ----------------------------------------------------------------
+    def _accept(self):
+        try:
+            sock, _ = self.lsock.accept()
+        except OSError:
+            return
+        sock.setblocking(False)
+        sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        conn = _Conn(sock)
+        self.conns[sock] = conn
+        self.sel.register(sock, selectors.EVENT_READ, conn)
+        self.stats["connections"] += 1
+
+    def _close(self, conn: _Conn, send_will: bool):
+        if conn.sock not in self.conns:
+            return
+        if send_will and conn.will is not None:
+            topic, payload, qos, retain = conn.will
+            self._route(topic, payload, qos, retain)
+        for f in list(conn.subs):
+            self.trie.remove(f, conn)
+        conn.subs.clear()
+        if conn.client_id is not None and self.by_client.get(conn.client_id) is conn:
+            del self.by_client[conn.client_id]
+        try:
+            self.sel.unregister(conn.sock)
+        except (KeyError, ValueError):
+            pass
+        del self.conns[conn.sock]
+        try:
+            conn.sock.close()
+        except OSError:
+            pass
+
+    def _send(self, conn: _Conn, data: bytes):
+        if conn.closing:
+            return
+        was_empty = not conn.out
+        conn.out += data
+        if was_empty:
+            self._flush(conn)
+
+    def _flush(self, conn: _Conn):
+        if not conn.out:
+            return
+        try:
+            n = conn.sock.send(conn.out)
+            del conn.out[:n]
+        except BlockingIOError:
+            pass
+        except OSError:
+            self._close(conn, send_will=True)
+            return
+        try:
+            self.sel.modify(conn.sock, selectors.EVENT_READ | (selectors.EVENT_WRITE if conn.out else 0), conn)
+        except (KeyError, ValueError):
+            pass
+
+    def _read(self, conn: _Conn):
+        try:
+            data = conn.sock.recv(65536)
+        except BlockingIOError:
+            return
+        except OSError:
+            data = b""
+        if not data:
+            self._close(conn, send_will=True)
+            return
+        conn.last_rx = time.monotonic()
+        conn.reader.feed(data)
+        try:
+            for ptype, flags, body in conn.reader.packets():
+                self._handle(conn, ptype, flags, body)
+                if conn.sock not in self.conns:
+                    return
+        except (ValueError, struct.error, UnicodeDecodeError, IndexError):
+            self._close(conn, send_will=True)
+
+    def _sweep_keepalive(self, now):
+        for conn in list(self.conns.values()):
+            if conn.keepalive and now - conn.last_rx > 1.5 * conn.keepalive:
+                self._close(conn, send_will=True)
+
+    # ---- protocol ---------------------------------------------------------------------------
+    def _handle(self, conn: _Conn, ptype, flags, body):
+        if ptype == C.CONNECT:
+            info = C.decode_connect(body)
+            if info["level"] != C.PROTOCOL_LEVEL:
+                self._send(conn, C.packet(C.CONNACK, 0, bytes([0, 1])))
+                self._close(conn, send_will=False)
+                return
+            cid = info["client_id"] or f"auto-{id(conn):x}"
+            old = self.by_client.get(cid)
+            if old is not None and old is not conn:
+                self._close(old, send_will=False)   # session takeover
+            conn.client_id = cid
+            conn.keepalive = info["keepalive"]
+            conn.will = info["will"]
+            conn.connected = True
+            self.by_client[cid] = conn
+            self._send(conn, C.packet(C.CONNACK, 0, bytes([0, 0])))
+        elif not conn.connected:
+            self._close(conn, send_will=False)
+        elif ptype == C.PUBLISH:
+            topic, payload, qos, retain, pid = C.decode_publish(flags, body)
+            if qos == 1:
+                self._send(conn, C.packet(C.PUBACK, 0, struct.pack("!H", pid)))
+            elif qos == 2:  # not supported: treat as QoS 1 delivery semantics
+                qos = 1
+            self._route(topic, payload, qos, retain)
+        elif ptype == C.SUBSCRIBE:
+            (pid,) = struct.unpack_from("!H", body, 0)
+            off = 2
+            granted = []
+            filters = []
+            while off < len(body):
+                f, off = C.decode_str(body, off)
+                q = min(body[off], 1)
+                off += 1
+                conn.subs[f] = q
+                self.trie.add(f, conn, q)
+                granted.append(q)
+                filters.append((f, q))
+            self._send(conn, C.packet(C.SUBACK, 0, struct.pack("!H", pid) + bytes(granted)))
+            for f, q in filters:
+                for topic, (payload, rq) in list(self.retained.items()):
+                    if C.topic_matches(f, topic):
+                        self._deliver(conn, topic, payload, min(q, rq), True)
+        elif ptype == C.UNSUBSCRIBE:
+            (pid,) = struct.unpack_from("!H", body, 0)
+            off = 2
+            while off < len(body):
+                f, off = C.decode_str(body, off)
+                conn.subs.pop(f, None)
+                self.trie.remove(f, conn)
+            self._send(conn, C.packet(C.UNSUBACK, 0, struct.pack("!H", pid)))
+        elif ptype == C.PINGREQ:
+            self._send(conn, C.packet(C.PINGRESP, 0, b""))
+        elif ptype == C.DISCONNECT:
+            conn.will = None
+            self._close(conn, send_will=False)
+        elif ptype == C.PUBACK:
+            pass
+
+    def _route(self, topic: str, payload: bytes, qos: int, retain: bool):
+        self.stats["published"] += 1
+        if retain:
+            if payload:
+                self.retained[topic] = (bytes(payload), qos)
+            else:
+                self.retained.pop(topic, None)
+        for conn, sq in self.trie.match(topic).items():
+            self._deliver(conn, topic, payload, min(qos, sq), False)
+
+    def _deliver(self, conn: _Conn, topic, payload, qos, retain):
+        pid = 0
+        if qos:
+            pid = next(conn.pid) & 0xFFFF or 1
+        self.stats["delivered"] += 1
+        self._send(conn, C.publish_packet(topic, payload, qos, retain, pid))
+
+
+def start_broker_thread(host="127.0.0.1", port=0):
+    """Start a broker on a background thread; returns (broker, port)."""
+    broker = Broker(host, port)
+    port = broker.bind()
+    t = threading.Thread(target=broker.serve_forever, name="aiko-mqtt-broker", daemon=True)
+    t.start()
+    return broker, port
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="aiko MQTT 3.1.1 broker")
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--port", type=int, default=1883)
+    a = ap.parse_args(argv)
+    b = Broker(a.host, a.port)
+    port = b.bind()
+    print(f"aiko MQTT broker listening on {a.host}:{port}", flush=True)
+    try:
+        b.serve_forever()
+    except KeyboardInterrupt:
+        pass
+
+
+if __name__ == "__main__":
+    main()

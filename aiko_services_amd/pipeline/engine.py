@@ -1,0 +1,804 @@
+"""Dataflow engine: Pipeline, PipelineElement, PipelineRemote (reference ``main/pipeline.py``).
+
+A :class:`PipelineImpl` is an Actor owning a DAG of elements built from a PipelineDefinition.
+Frames enter through ``process_frame(stream_dict, frame_data)`` (posted by MQTT, by a frame
+generator thread, or called directly by an embedding such as ``bench.py``) and run through
+the graph path in topological order; each element's ``process_frame(stream, **inputs)``
+returns ``(StreamEvent, outputs)`` and the outputs are merged into the frame's ``swag``.
+
+Semantics kept from the reference: input selection by declared input names
+with ``(from: to)`` mapping properties on graph edges; per-element metrics; DROP_FRAME /
+STOP (graceful destroy) / ERROR (immediate destroy) handling; streams with a grace lease
+extended per frame; the default stream ``"*"`` auto-created; thread-local "current stream";
+remote elements pause the frame (``paused_pe_name``) and ``process_frame_response``
+continues after it; output routed to ``queue_response``, ``topic_response`` or ``/out``;
+4-level ``get_parameter`` precedence; ``set_parameter(s)``.
+
+MI355X additions: swag values may be device tensors, handed between local elements by
+reference (the data plane never touches MQTT); elements can declare a ``device`` in their
+deploy block (``GpuPipelineElement`` binds it); ``frame.metrics`` optionally carries GPU
+event timings (``AIKO_GPU_TIMING=1``); graph paths are cached.
+"""
+from __future__ import annotations
+
+import os
+import threading
+import time
+import traceback
+from abc import abstractmethod
+from collections import OrderedDict
+from typing import Tuple
+
+from ..control.share import services_cache_create_singleton
+from ..control.transport import get_actor_mqtt
+from ..runtime import event
+from ..runtime.actor import Actor, ActorTopic
+from ..runtime.context import Interface, compose_instance, pipeline_args, pipeline_element_args
+from ..runtime.lease import Lease
+from ..runtime.process import aiko
+from ..runtime.service import ServiceFilter, ServiceProtocol
+from ..utils.graph import Graph, Node
+from ..utils.misc import load_module
+from ..utils.sexpr import generate, parse
+from .definition import (PipelineDefinition, PipelineElementDeployLocal, PipelineElementDeployRemote,
+                         parse_pipeline_definition)
+from .stream import (DEFAULT_STREAM_ID, FIRST_FRAME_ID, Frame, Stream, StreamEvent, StreamEventName,
+                     StreamState)
+
+__all__ = ["Pipeline", "PipelineElement", "PipelineElementImpl", "PipelineImpl", "PipelineRemote",
+           "PipelineGraph", "PROTOCOL_PIPELINE", "PROTOCOL_ELEMENT", "GRACE_TIME"]
+
+_VERSION = 0
+ACTOR_TYPE_PIPELINE = "pipeline"
+ACTOR_TYPE_ELEMENT = "pipeline_element"
+PROTOCOL_PIPELINE = f"{ServiceProtocol.AIKO}/{ACTOR_TYPE_PIPELINE}:{_VERSION}"
+PROTOCOL_ELEMENT = f"{ServiceProtocol.AIKO}/{ACTOR_TYPE_ELEMENT}:{_VERSION}"
+GRACE_TIME = 60
+STATUS_UPDATE_PERIOD = 3.0
+_GPU_TIMING = os.environ.get("AIKO_GPU_TIMING", "0") == "1"
+
+_LOGGER = aiko.logger(__name__)
+
+
+class PipelineError(SystemExit):
+    pass
+
+
+# ---- graph -----------------------------------------------------------------------------------
+
+class PipelineGraph(Graph):
+    def add_element(self, node: Node):
+        self.add(node)
+        node.predecessors = OrderedDict()
+
+    @property
+    def element_count(self):
+        return len(self._graph)
+
+    @classmethod
+    def get_element(cls, node):
+        element = node.element
+        if type(element).__name__ == "ServiceRemoteProxy":
+            return element, node.name, False, "ready"
+        lifecycle = element.share["lifecycle"]
+        local = element.is_local()
+        name = node.name if isinstance(element, PipelineRemote) else type(element).__name__
+        return element, name, local, lifecycle
+
+    def validate(self, definition, head_node_name):
+        """Link predecessors; warn about inputs no predecessor (or mapping) can provide."""
+        for node in self.get_path(head_node_name):
+            element, element_name, _, _ = PipelineGraph.get_element(node)
+            for succ in node.successors:
+                self.get_node(succ).predecessors[node.name] = node
+        for node in self.get_path(head_node_name):
+            if not node.predecessors:
+                continue
+            element = node.element
+            definition_e = getattr(element, "definition", None)
+            if definition_e is None:
+                continue
+            produced = set()
+            stack = list(node.predecessors.values())
+            seen = set()
+            while stack:
+                p = stack.pop()
+                if p.name in seen:
+                    continue
+                seen.add(p.name)
+                pd = getattr(p.element, "definition", None)
+                if pd is not None:
+                    produced.update(o["name"] for o in pd.output)
+                stack.extend(p.predecessors.values())
+            mapped = set()
+            for mapping in definition.map_in_nodes.get(node.name, {}).values():
+                mapped.update(mapping.values())
+            for inp in definition_e.input:
+                if inp["name"] not in produced and inp["name"] not in mapped:
+                    _LOGGER.debug(f"PipelineElement {node.name}: input \"{inp['name']}\" "
+                                  "not produced by any previous PipelineElement")
+
+
+# ---- PipelineElement -----------------------------------------------------------------------
+
+class PipelineElement(Actor):
+    Interface.default("PipelineElement", "aiko_services_amd.pipeline.engine.PipelineElementImpl")
+
+    @abstractmethod
+    def create_frame(self, stream, frame_data):
+        pass
+
+    @abstractmethod
+    def create_frames(self, stream, frame_generator, frame_id=FIRST_FRAME_ID, rate=None):
+        pass
+
+    @abstractmethod
+    def get_parameter(self, name, default=None, use_pipeline=True):
+        pass
+
+    @abstractmethod
+    def get_stream(self):
+        pass
+
+    @classmethod
+    def is_local(cls):
+        return True
+
+    @abstractmethod
+    def my_id(self, all=False):
+        pass
+
+    @abstractmethod
+    def process_frame(self, stream, **kwargs) -> Tuple[int, dict]:
+        pass
+
+    @abstractmethod
+    def start_stream(self, stream, stream_id):
+        pass
+
+    @abstractmethod
+    def stop_stream(self, stream, stream_id):
+        pass
+
+
+class PipelineElementImpl(PipelineElement):
+    def __init__(self, context):
+        self.definition = context.get_definition()
+        self.pipeline = context.get_pipeline()
+        self.is_pipeline = self.pipeline is None
+        if context.protocol == "*":
+            context.set_protocol(PROTOCOL_PIPELINE if self.is_pipeline else PROTOCOL_ELEMENT)
+        context.get_implementation("Actor").__init__(self, context)
+        log_level, found = self.get_parameter("log_level", self_share_priority=False)
+        if found:
+            try:
+                self.logger.setLevel(str(log_level).upper())
+            except ValueError:
+                pass
+        self.share["source_file"] = f"v{_VERSION}⇒ {__file__}"
+        params = getattr(self.definition, "parameters", None) or {}
+        self.share.update(params)
+
+    def create_frame(self, stream, frame_data, frame_id=None):
+        frame_id = frame_id if frame_id is not None else stream.frame_id
+        stream_copy = Stream(stream_id=stream.stream_id, frame_id=frame_id,
+                             parameters=stream.parameters, queue_response=stream.queue_response,
+                             state=stream.state, topic_response=stream.topic_response)
+        self.pipeline.create_frame(stream_copy, frame_data)
+
+    def create_frames(self, stream, frame_generator, frame_id=FIRST_FRAME_ID, rate=None):
+        t = threading.Thread(target=self._create_frames_generator,
+                             args=(stream, frame_generator, int(frame_id), rate), daemon=True,
+                             name=f"frames-{self.name}")
+        t.start()
+        return t
+
+    def _create_frames_generator(self, stream, frame_generator, frame_id, rate):
+        pipeline = self.pipeline
+        try:
+            pipeline._enable_thread_local("_create_frames_generator", stream.stream_id, frame_id)
+            stream, frame_id = self.get_stream()
+            period = 1.0 / rate if rate else 0.0
+            next_time = time.monotonic()
+            while stream.state == StreamState.RUN:
+                try:
+                    stream_event, frame_data = frame_generator(stream, frame_id)
+                except Exception:
+                    self.logger.error("Exception in frame_generator()")
+                    stream_event = StreamEvent.ERROR
+                    frame_data = {"diagnostic": traceback.format_exc()}
+                stream.state = pipeline._process_stream_event(self.name, stream_event, frame_data)
+                if stream.state == StreamState.RUN and frame_data:
+                    if isinstance(frame_data, dict):
+                        frame_data = [frame_data]
+                    if isinstance(frame_data, list):
+                        for fd in frame_data:
+                            self.create_frame(stream, fd, frame_id)
+                            frame_id += 1
+                    else:
+                        self.logger.warning("Frame generator must return either {frame_data} or [{frame_data}]")
+                else:
+                    frame_id += 1
+                if stream.state in (StreamState.DROP_FRAME, StreamState.RUN):
+                    stream.state = StreamState.RUN
+                    if period:
+                        next_time += period
+                        delay = next_time - time.monotonic()
+                        if delay > 0:
+                            time.sleep(delay)
+                        else:
+                            next_time = time.monotonic()
+                    pipeline.thread_local.frame_id = frame_id
+        finally:
+            pipeline._disable_thread_local("_create_frames_generator")
+
+    def get_parameter(self, name, default=None, use_pipeline=True, self_share_priority=True):
+        value, found = None, False
+        definition = self.definition
+        element_params = getattr(definition, "parameters", None) or {}
+        stream_params = self._get_stream_parameters()
+        qualified = f"{getattr(definition, 'name', self.name)}.{name}"
+        if qualified in stream_params:
+            value, found = stream_params[qualified], True
+        elif name in element_params:
+            value = self.share[name] if self_share_priority and name in self.share else element_params[name]
+            found = True
+        if not found and use_pipeline and not self.is_pipeline:
+            if name in stream_params:
+                value, found = stream_params[name], True
+            else:
+                pparams = getattr(self.pipeline.definition, "parameters", None) or {}
+                if name in pparams:
+                    value = (self.pipeline.share[name] if self_share_priority and name in self.pipeline.share
+                             else pparams[name])
+                    found = True
+        if not found and default is not None:
+            value = default
+        return value, found
+
+    def get_stream(self):
+        return self.pipeline.get_stream()
+
+    def _get_stream_parameters(self):
+        try:
+            stream, _ = self.get_stream()
+            if stream:
+                return stream.parameters
+        except (AttributeError, AssertionError):
+            pass
+        return {}
+
+    def my_id(self, all=False):
+        name = self.name if all else ""
+        try:
+            stream, frame_id = self.get_stream()
+            return f"{name}<{stream.stream_id}:{frame_id}>"
+        except (AttributeError, AssertionError):
+            return f"{name}<?>"
+
+    def start_stream(self, stream, stream_id):
+        return StreamEvent.OKAY, None
+
+    def stop_stream(self, stream, stream_id):
+        return StreamEvent.OKAY, None
+
+    def process_frame(self, stream, **kwargs):
+        return StreamEvent.OKAY, {}
+
+
+# ---- Pipeline -------------------------------------------------------------------------------
+
+class Pipeline(PipelineElement):
+    Interface.default("Pipeline", "aiko_services_amd.pipeline.engine.PipelineImpl")
+
+    @abstractmethod
+    def create_stream(self, stream_id, graph_path=None, parameters=None, grace_time=GRACE_TIME,
+                      queue_response=None, topic_response=None):
+        pass
+
+    @abstractmethod
+    def destroy_stream(self, stream_id, graceful=False):
+        pass
+
+    @abstractmethod
+    def process_frame_response(self, stream, frame_data):
+        pass
+
+    @abstractmethod
+    def set_parameter(self, stream_id, name, value):
+        pass
+
+    @abstractmethod
+    def set_parameters(self, stream_id, parameters):
+        pass
+
+
+class PipelineImpl(Pipeline):
+    def __init__(self, context):
+        context.get_implementation("PipelineElement").__init__(self, context)
+        self.share["definition_pathname"] = context.definition_pathname
+        self.share["lifecycle"] = "waiting"
+        self.share["graph_path"] = context.graph_path
+        self.remote_pipelines: dict = {}
+        self.services_cache = None
+        self.stream_leases: dict = {}
+        self.thread_local = threading.local()
+        self.frames_completed = 0
+        self.pipeline_graph = self._create_pipeline_graph(context.definition)
+        self.share["element_count"] = self.pipeline_graph.element_count
+        self.share["streams"] = 0
+        self.share["streams_frames"] = 0
+        self._update_lifecycle_state()
+        event.add_timer_handler(self._status_update_timer, STATUS_UPDATE_PERIOD)
+
+    # ---- lifecycle / status ------------------------------------------------------------------
+    def _update_lifecycle_state(self):
+        ready = all(PipelineGraph.get_element(n)[3] == "ready"
+                    for n in self.pipeline_graph.get_path(self.share["graph_path"]))
+        self.ec_producer.update("lifecycle", "ready" if ready else "waiting")
+
+    def _status_update_timer(self):
+        frames = sum(len(l.stream.frames) for l in self.stream_leases.values())
+        self.ec_producer.update("streams", len(self.stream_leases))
+        self.ec_producer.update("streams_frames", frames)
+        self.ec_producer.update("frames_completed", self.frames_completed)
+
+    def _add_node_properties(self, node_name, properties, predecessor_name):
+        d = self.definition
+        d.map_in_nodes.setdefault(node_name, {})[predecessor_name] = properties
+        d.map_out_nodes.setdefault(predecessor_name, {})[node_name] = properties
+
+    # ---- thread-local current stream ----------------------------------------------------------
+    def _enable_thread_local(self, function_name, stream_id, frame_id=None):
+        assert not getattr(self.thread_local, "stream", None), "thread_local.stream already assigned"
+        self.thread_local.stream = self.stream_leases[stream_id].stream
+        self.thread_local.frame_id = frame_id if frame_id is not None else self.thread_local.stream.frame_id
+
+    def _disable_thread_local(self, function_name):
+        self.thread_local.stream = None
+        self.thread_local.frame_id = None
+
+    def get_stream(self):
+        stream = getattr(self.thread_local, "stream", None)
+        assert stream, "thread_local.stream must be assigned"
+        return stream, self.thread_local.frame_id
+
+    # ---- construction ----------------------------------------------------------------------------
+    def create_frame(self, stream_dict, frame_data):
+        if isinstance(stream_dict, Stream):
+            stream_dict = stream_dict.as_dict()
+        self._post_message(ActorTopic.IN, "process_frame", [stream_dict, frame_data])
+
+    @classmethod
+    def create_pipeline(cls, definition_pathname, pipeline_definition, name, graph_path, stream_id,
+                        parameters, frame_id, frame_data, grace_time, queue_response=None,
+                        stream_reset=False):
+        name = name or pipeline_definition.name
+        init_args = pipeline_args(name, protocol=PROTOCOL_PIPELINE, definition=pipeline_definition,
+                                  definition_pathname=definition_pathname, graph_path=graph_path)
+        pipeline = compose_instance(PipelineImpl, init_args)
+        stream_dict = {"frame_id": int(frame_id or 0), "parameters": {}}
+        parameters = dict(parameters or {})
+        if stream_id is not None:
+            stream_dict["stream_id"] = stream_id
+            if stream_reset:
+                pipeline.destroy_stream(stream_id)
+            pipeline.create_stream(stream_id, graph_path=None, parameters=parameters,
+                                   grace_time=grace_time, queue_response=queue_response)
+        else:
+            pipeline.set_parameters(None, list(parameters.items()))
+        if frame_data is not None:
+            _, arguments = parse(f"(process_frame {frame_data})")
+            if not arguments:
+                raise SystemExit("Error: Frame data must be provided")
+            pipeline.create_frame(stream_dict, arguments[0])
+        return pipeline
+
+    def _error_pipeline(self, header, diagnostic):
+        PipelineImpl._exit(header, diagnostic)
+
+    @classmethod
+    def _exit(cls, header, diagnostic):
+        _LOGGER.error(f"{header}\n{diagnostic}")
+        raise PipelineError(-1)
+
+    def _load_element_class(self, module_descriptor, class_name, header):
+        try:
+            module = load_module(module_descriptor)
+            return getattr(module, class_name)
+        except FileNotFoundError:
+            self._error_pipeline(header, f"PipelineDefinition: PipelineElement {class_name}: "
+                                 f"Module {module_descriptor} could not be found")
+        except Exception:
+            self._error_pipeline(header, f"PipelineDefinition: PipelineElement {class_name}: "
+                                 f"Module {module_descriptor} could not be loaded\n{traceback.format_exc()}")
+
+    def _create_pipeline_graph(self, definition: PipelineDefinition):
+        header = f"Error: Creating Pipeline: {definition.name}"
+        if not definition.elements:
+            self._error_pipeline(header, "PipelineDefinition: Doesn't define any PipelineElements")
+        definition.map_in_nodes = {}
+        definition.map_out_nodes = {}
+        heads, successors = Graph.traverse(definition.graph, self._add_node_properties)
+        graph = PipelineGraph(heads)
+        for ed in definition.elements:
+            if ed.name not in successors:
+                _LOGGER.debug(f"Skipping PipelineElement {ed.name}: not used within the graph")
+                continue
+            deploy = ed.deploy
+            if isinstance(deploy, PipelineElementDeployLocal):
+                element_class = self._load_element_class(deploy.module, deploy.class_name, header)
+            elif isinstance(deploy, PipelineElementDeployRemote):
+                element_class = PipelineRemote
+            else:
+                self._error_pipeline(header, f"PipelineElement type unknown: {type(deploy).__name__}")
+            init_args = pipeline_element_args(ed.name, definition=ed, pipeline=self)
+            instance = compose_instance(element_class, init_args)
+            instance.parameters = ed.parameters
+            if element_class is PipelineRemote:
+                service_name = deploy.service_filter["name"]
+                if service_name in self.remote_pipelines:
+                    self._error_pipeline(header, f"PipelineElement {ed.name}: re-uses remote service_filter "
+                                         f"name: {service_name}")
+                self.remote_pipelines[service_name] = (ed.name, instance, None)
+                if self.services_cache is None:
+                    self.services_cache = services_cache_create_singleton(self)
+                self.services_cache.add_handler(self._pipeline_element_change_handler,
+                                                ServiceFilter.with_topic_path(**deploy.service_filter))
+            graph.add_element(Node(ed.name, instance, successors[ed.name]))
+        missing = [n for n in successors if n not in graph._graph]
+        if missing:
+            self._error_pipeline(header, f"PipelineDefinition: graph references undefined "
+                                 f"PipelineElements: {', '.join(missing)}")
+        graph.validate(definition, self.share["graph_path"])
+        return graph
+
+    def _pipeline_element_change_handler(self, command, service_details):
+        if command not in ("add", "remove") or not service_details:
+            return
+        topic_path = f"{service_details[0]}/in"
+        service_name = service_details[1]
+        if service_name not in self.remote_pipelines:
+            return
+        element_name, element_instance, element_topic_path = self.remote_pipelines[service_name]
+        node = self.pipeline_graph.get_node(element_name)
+        definition = element_instance.definition
+        if command == "add":
+            element_instance.set_remote_absent(False)
+            proxy = get_actor_mqtt(topic_path, PipelineRemote)
+            proxy.definition = definition
+            new_instance, new_tp = proxy, topic_path
+        elif topic_path == element_topic_path:
+            element_instance.set_remote_absent(True)
+            new_instance, new_tp = element_instance, None
+        else:
+            return
+        self.remote_pipelines[service_name] = (element_name, element_instance, new_tp)
+        node.element = new_instance
+        self._update_lifecycle_state()
+
+    # ---- streams -------------------------------------------------------------------------------
+    def create_stream(self, stream_id, graph_path=None, parameters=None, grace_time=GRACE_TIME,
+                      queue_response=None, topic_response=None):
+        if queue_response and topic_response:
+            self.logger.error("Create stream: use either queue_response or topic_response")
+            return False
+        if self.share["lifecycle"] != "ready":
+            self._post_message(ActorTopic.IN, "create_stream",
+                               [stream_id, graph_path, parameters, grace_time, queue_response, topic_response],
+                               delay=1.0)
+            self.logger.warning(f"Create stream: {stream_id}: remote Pipeline not yet discovered ... will retry")
+            return False
+        stream_id = str(stream_id)
+        if stream_id in self.stream_leases:
+            self.logger.error(f"Create stream: {stream_id} already exists")
+            return False
+        graph_path = graph_path or self.share["graph_path"]
+        if graph_path and Graph.path_local(graph_path) not in self.pipeline_graph.head_nodes:
+            self.logger.error(f"Create stream: Unknown Pipeline Graph Path: {graph_path}")
+            return False
+        lease = Lease(int(float(grace_time)), stream_id, lease_expired_handler=self.destroy_stream)
+        lease.stream = Stream(stream_id=stream_id, graph_path=graph_path,
+                              parameters=parameters if isinstance(parameters, dict) else {},
+                              queue_response=queue_response, topic_response=topic_response)
+        self.stream_leases[stream_id] = lease
+        try:
+            self._enable_thread_local("create_stream", stream_id)
+            stream, _ = self.get_stream()
+            for node in self.pipeline_graph.get_path(Graph.path_local(stream.graph_path)):
+                element, element_name, local, _ = PipelineGraph.get_element(node)
+                if local:
+                    try:
+                        stream_event, diagnostic = element.start_stream(stream, stream_id)
+                    except Exception:
+                        self.logger.error("Exception in pipeline.create_stream() --> start_stream()")
+                        stream_event, diagnostic = StreamEvent.ERROR, {"diagnostic": traceback.format_exc()}
+                    self._process_stream_event(element_name, stream_event, diagnostic)
+                    if stream_id not in self.stream_leases:
+                        break   # start_stream failed -> stream destroyed
+                else:
+                    element.create_stream(stream_id, Graph.path_remote(stream.graph_path), parameters,
+                                          grace_time, None, self.topic_in)
+        finally:
+            self._disable_thread_local("create_stream")
+        return True
+
+    def destroy_stream(self, stream_id, graceful=False, use_thread_local=True):
+        stream_id = str(stream_id)
+        if isinstance(graceful, str):
+            graceful = graceful.lower() == "true"
+        if self.share["lifecycle"] == "ready":
+            for node in self.pipeline_graph.get_path(self.share["graph_path"]):
+                element, _, local, _ = PipelineGraph.get_element(node)
+                if not local:
+                    element.destroy_stream(stream_id, True)
+        else:
+            self._post_message(ActorTopic.IN, "destroy_stream", [stream_id, graceful, use_thread_local],
+                               delay=1.0)
+            return False
+        lease = self.stream_leases.get(stream_id)
+        if lease is None:
+            return False
+        enabled = False
+        try:
+            if use_thread_local and not getattr(self.thread_local, "stream", None):
+                self._enable_thread_local("destroy_stream", stream_id)
+                enabled = True
+            stream = lease.stream
+            if graceful and stream.frames:
+                self._post_message(ActorTopic.IN, "destroy_stream", [stream_id, graceful, use_thread_local],
+                                   delay=1.0)
+                return False
+            for node in self.pipeline_graph.get_path(Graph.path_local(stream.graph_path)):
+                element, element_name, local, _ = PipelineGraph.get_element(node)
+                if local:
+                    try:
+                        stream_event, diagnostic = element.stop_stream(stream, stream_id)
+                    except Exception:
+                        self.logger.error("Exception in pipeline.destroy_stream() --> stop_stream()")
+                        stream_event, diagnostic = StreamEvent.ERROR, {"diagnostic": traceback.format_exc()}
+                    self._process_stream_event(element_name, stream_event, diagnostic, in_destroy_stream=True)
+        finally:
+            if enabled:
+                self._disable_thread_local("destroy_stream")
+        lease = self.stream_leases.pop(stream_id, None)
+        if lease is not None:
+            lease.terminate()
+            lease.stream.state = StreamState.STOP if lease.stream.state != StreamState.ERROR else StreamState.ERROR
+        return True
+
+    # ---- frames ----------------------------------------------------------------------------------
+    def process_frame(self, stream_dict, frame_data):
+        return self._process_frame_common(stream_dict, frame_data, True)
+
+    def process_frame_response(self, stream_dict, frame_data):
+        return self._process_frame_common(stream_dict, frame_data, False)
+
+    def _process_initialize(self, stream_dict, frame_data_in, new_frame):
+        stream = Stream()
+        if not stream.update(stream_dict):
+            self.logger.warning("Process frame: stream_dict must be a dictionary")
+            return None, None
+        if frame_data_in == [] or frame_data_in is None:
+            frame_data_in = {}
+        if not isinstance(frame_data_in, dict):
+            self.logger.warning("Process frame: frame data must be a dictionary")
+            return None, None
+        stream_id = stream.stream_id
+        if stream_id == DEFAULT_STREAM_ID and DEFAULT_STREAM_ID not in self.stream_leases:
+            if not self.create_stream(DEFAULT_STREAM_ID, graph_path=stream.graph_path,
+                                      parameters=stream.parameters):
+                return None, None
+        frame_id = stream.frame_id
+        header = f"Process frame <{stream_id}:{frame_id}>:"
+        lease = self.stream_leases.get(stream_id)
+        if lease is None:
+            self.logger.warning(f"{header} stream not found")
+            return None, None
+        lease.extend()
+        stream = lease.stream
+        stream.frame_id = frame_id
+        stream.state = int(stream_dict.get("state", StreamState.RUN)) if stream.state != StreamState.ERROR \
+            else StreamState.ERROR
+        graph = None
+        if new_frame:
+            if frame_id in stream.frames:
+                self.logger.warning(f"{header} new frame id already exists")
+                return None, None
+            frame = stream.frames[frame_id] = Frame()
+            graph = self.pipeline_graph.get_path(Graph.path_local(stream.graph_path))
+        elif frame_id in stream.frames:
+            frame = stream.frames[frame_id]
+            graph = self.pipeline_graph.iterate_after(frame.paused_pe_name, Graph.path_local(stream.graph_path))
+        else:
+            self.logger.warning(f"{header} paused frame id doesn't exist")
+            return None, None
+        frame.swag.update(frame_data_in)
+        return graph, stream
+
+    def _process_frame_common(self, stream_dict, frame_data_in, new_frame):
+        graph, stream = self._process_initialize(stream_dict, frame_data_in, new_frame)
+        if graph is None:
+            return False
+        frame_complete = True
+        frame_id = stream.frame_id
+        try:
+            self._enable_thread_local("process_frame", stream.stream_id)
+            frame = stream.frames[frame_id]
+            metrics = frame.metrics
+            if not metrics:
+                metrics["pipeline_elements"] = {}
+                metrics["time_pipeline_start"] = time.time()
+            frame_data_out = {} if new_frame else frame_data_in
+            definition_pathname = self.share["definition_pathname"]
+            for node in graph:
+                if stream.state in (StreamState.DROP_FRAME, StreamState.ERROR):
+                    break
+                element, element_name, local, _ = PipelineGraph.get_element(node)
+                header = (f'Error: Invoking Pipeline "{definition_pathname}": '
+                          f'PipelineElement "{element_name}": process_frame()')
+                inputs = self._process_map_in(header, element, node.name, frame.swag)
+                if local:
+                    start = time.time()
+                    gpu_t = element.gpu_timer_start() if _GPU_TIMING and hasattr(element, "gpu_timer_start") else None
+                    try:
+                        stream_event, frame_data_out = element.process_frame(stream, **inputs)
+                    except Exception:
+                        self.logger.error("Exception in pipeline.process_frame() --> element.process_frame()")
+                        stream_event = StreamEvent.ERROR
+                        frame_data_out = {"diagnostic": traceback.format_exc()}
+                    if frame_data_out is None:
+                        frame_data_out = {}
+                    stream.state = self._process_stream_event(element_name, stream_event, frame_data_out)
+                    self._process_map_out(node.name, frame_data_out)
+                    t = time.time()
+                    metrics["pipeline_elements"][f"time_{element.name}"] = t - start
+                    metrics["time_pipeline"] = t - metrics["time_pipeline_start"]
+                    if gpu_t is not None:
+                        metrics.setdefault("gpu_events", {})[element.name] = gpu_t
+                        element.gpu_timer_stop(gpu_t)
+                    frame.swag.update(frame_data_out)
+                else:
+                    if self.share["lifecycle"] != "ready":
+                        stream.state = self._process_stream_event(
+                            element_name, StreamEvent.ERROR,
+                            {"diagnostic": "process_frame() invoked when remote Pipeline hasn't been discovered"})
+                    else:
+                        frame_complete = False
+                        frame_data_out = {}
+                        frame.paused_pe_name = node.name
+                        element.process_frame({"stream_id": stream.stream_id, "frame_id": frame_id}, **inputs)
+                    break
+            if frame_complete:
+                self.frames_completed += 1
+                stream_info = {"stream_id": stream.stream_id, "frame_id": frame_id, "state": stream.state}
+                if stream.queue_response is not None:
+                    stream.queue_response.put((stream_info, frame_data_out))
+                elif stream.topic_response:
+                    get_actor_mqtt(stream.topic_response, Pipeline).process_frame_response(stream_info, frame_data_out)
+                else:
+                    aiko.message.publish(self.topic_out, generate("process_frame", (stream_info, frame_data_out)))
+        finally:
+            if frame_complete:
+                stream.frames.pop(frame_id, None)
+            self._disable_thread_local("process_frame")
+            if stream.state == StreamState.DROP_FRAME:
+                stream.state = StreamState.RUN
+        return True
+
+    def _process_map_in(self, header, element, node_name, swag):
+        map_in = {}
+        for mapping in self.definition.map_in_nodes.get(node_name, {}).values():
+            if mapping:
+                _from, to = next(iter(mapping.items()))
+                map_in[to] = f"{node_name}.{to}"
+        inputs = {}
+        definition = getattr(element, "definition", None)
+        for inp in (definition.input if definition is not None else []):
+            name = inp["name"]
+            key = map_in.get(name, name)
+            if key in swag:
+                inputs[name] = swag[key]
+            elif name in swag:
+                inputs[name] = swag[name]
+            else:
+                self._error_pipeline(header, f'Function parameter "{name}" not found')
+        return inputs
+
+    def _process_map_out(self, node_name, frame_data_out):
+        for out_element, mapping in self.definition.map_out_nodes.get(node_name, {}).items():
+            if mapping:
+                from_name, to_name = next(iter(mapping.items()))
+                if from_name in frame_data_out:
+                    frame_data_out[f"{out_element}.{to_name}"] = frame_data_out.pop(from_name)
+
+    def _process_stream_event(self, element_name, stream_event, diagnostic, in_destroy_stream=False):
+        def get_diagnostic():
+            name = StreamEventName.get(stream_event, str(stream_event))
+            d = diagnostic.get("diagnostic", "No diagnostic provided") if isinstance(diagnostic, dict) \
+                else "No diagnostic provided"
+            return f"{element_name.upper()}: {name} stream {self.my_id()} {d}"
+
+        def current_stream_id():
+            stream, _ = self.get_stream()
+            return stream.stream_id
+
+        if stream_event == StreamEvent.DROP_FRAME:
+            return StreamState.DROP_FRAME
+        if stream_event == StreamEvent.STOP:
+            self.logger.debug(get_diagnostic())
+            if not in_destroy_stream:
+                self._post_message(ActorTopic.IN, "destroy_stream", [current_stream_id(), True])
+            return StreamState.STOP
+        if stream_event == StreamEvent.ERROR:
+            self.logger.error(get_diagnostic())
+            if not in_destroy_stream:
+                stream, _ = self.get_stream()
+                stream.state = StreamState.ERROR
+                self.destroy_stream(current_stream_id(), use_thread_local=False)
+            return StreamState.ERROR
+        return StreamState.RUN
+
+    # ---- parameters ------------------------------------------------------------------------------
+    def set_parameter(self, stream_id, name, value):
+        if stream_id is None:
+            names = str(name).split(".")
+            if len(names) == 1:
+                self.ec_producer.update(names[0], value)
+            else:
+                try:
+                    element = self.pipeline_graph.get_node(names[0]).element
+                    element.ec_producer.update(names[1], value)
+                except (KeyError, AttributeError):
+                    pass
+        else:
+            lease = self.stream_leases.get(str(stream_id))
+            if lease is not None:
+                lease.stream.parameters[name] = value
+
+    def set_parameters(self, stream_id, parameters):
+        for p in parameters or []:
+            self.set_parameter(stream_id, p[0], p[1])
+
+    def get_element(self, name):
+        return self.pipeline_graph.get_node(name).element
+
+
+# ---- remote element placeholder --------------------------------------------------------------
+
+class PipelineRemote(PipelineElement):
+
+    def __init__(self, context):
+        context.get_implementation("PipelineElement").__init__(self, context)
+        self.set_remote_absent(True)
+
+    def create_stream(self, stream_id, graph_path=None, parameters=None, grace_time=GRACE_TIME,
+                      queue_response=None, topic_response=None):
+        if self.absent:
+            self.log_error("create_stream")
+        return not self.absent
+
+    def destroy_stream(self, stream_id, graceful=False):
+        if self.absent:
+            self.log_error("destroy_stream")
+        return not self.absent
+
+    @classmethod
+    def is_local(cls):
+        return False
+
+    def log_error(self, function_name):
+        self.logger.error(f"PipelineElement.{function_name}(): {self.definition.name}: invoked when "
+                          "remote Pipeline hasn't been discovered")
+
+    def process_frame(self, stream, **kwargs):
+        if self.absent:
+            self.log_error("process_frame")
+        return not self.absent
+
+    def process_frame_response(self, stream, frame_data):
+        pass
+
+    def set_remote_absent(self, absent):
+        self.absent = absent
+        self.share["lifecycle"] = "absent" if absent else "ready"

@@ -1,0 +1,274 @@
+"""Local pipeline engine: definitions, graph paths, name mapping, stream events, parameters.
+
+Where the reference checkout is present its example PipelineDefinitions (``examples/pipeline/
+*.json``, ``elements/media/text_pipeline_*.json``) are run unchanged as golden inputs;
+otherwise equivalent inline definitions are used.
+"""
+import json
+import os
+import queue
+import time
+from pathlib import Path
+
+import pytest
+
+from aiko_services_amd.pipeline.definition import (DefinitionError, parse_pipeline_definition,
+                                                   parse_pipeline_definition_dict)
+from aiko_services_amd.runtime import event
+
+REF = Path("/root/reference/src/aiko_services")
+needs_ref = pytest.mark.skipif(not REF.exists(), reason="reference checkout not present")
+
+
+@pytest.fixture(scope="module")
+def aiko_process():
+    import aiko_services_amd as aiko
+    from aiko_services_amd.message import Loopback, LoopbackBus
+    if not aiko.process.initialized:
+        aiko.process.run_in_thread(loop_when_no_handlers=True, message=Loopback(bus=LoopbackBus()))
+    deadline = time.time() + 5
+    while not event.is_running() and time.time() < deadline:
+        time.sleep(0.01)
+    return aiko
+
+
+def _create(definition, name=None, stream_id="1", parameters=None, graph_path=None, frame_data=None,
+            pathname="<inline>"):
+    from aiko_services_amd.pipeline.engine import PipelineImpl
+    q = queue.Queue()
+    if isinstance(definition, dict):
+        definition = parse_pipeline_definition_dict(definition)
+
+    def build():
+        return PipelineImpl.create_pipeline(pathname, definition, name, graph_path, stream_id,
+                                            list((parameters or {}).items()), 0, frame_data, 60,
+                                            queue_response=q)
+    return event.call_on_loop(build), q
+
+
+def _elem(name, inputs, outputs, cls=None, params=None):
+    e = {"name": name, "input": [{"name": n, "type": "int"} for n in inputs],
+         "output": [{"name": n, "type": "int"} for n in outputs],
+         "deploy": {"local": {"module": "aiko_services_amd.examples.pipeline.elements"}}}
+    if cls:
+        e["deploy"]["local"]["class_name"] = cls
+    if params:
+        e["parameters"] = params
+    return e
+
+
+DIAMOND = {
+    "version": 0, "name": "p_diamond", "runtime": "python",
+    "graph": ["(PE_1 (PE_2 PE_4) (PE_3 PE_4) PE_Metrics)"],
+    "parameters": {"p_0": None, "p_1": True, "p_2": 0, "p_3": "test"},
+    "elements": [_elem("PE_1", ["b"], ["c"], params={"pe_1_inc": 1}), _elem("PE_2", ["c"], ["d"]),
+                 _elem("PE_3", ["c"], ["e"]), _elem("PE_4", ["d", "e"], ["f"]),
+                 _elem("PE_Metrics", [], ["f"])],
+}
+
+
+def test_definition_validation_errors():
+    bad = dict(DIAMOND, version=1)
+    with pytest.raises(DefinitionError):
+        parse_pipeline_definition_dict(bad)
+    bad = dict(DIAMOND, runtime="go")
+    with pytest.raises(DefinitionError):
+        parse_pipeline_definition_dict(bad)
+    bad = json.loads(json.dumps(DIAMOND))
+    bad["elements"][0]["deploy"] = {"local": {"module": "m"}, "remote": {"module": "m", "service_filter": {}}}
+    with pytest.raises(DefinitionError):
+        parse_pipeline_definition_dict(bad)
+    bad = json.loads(json.dumps(DIAMOND))
+    del bad["graph"]
+    with pytest.raises(DefinitionError):
+        parse_pipeline_definition_dict(bad)
+    d = parse_pipeline_definition_dict(DIAMOND)
+    assert d.elements[0].deploy.class_name == "PE_1"
+
+
+def test_diamond_pipeline_frames(aiko_process):
+    pipeline, q = _create(DIAMOND)
+    for i in range(5):
+        pipeline.create_frame({"stream_id": "1", "frame_id": i}, {"b": i})
+    outs = [q.get(timeout=5) for _ in range(5)]
+    for i, (info, data) in enumerate(outs):
+        assert info["frame_id"] == i and info["state"] == 0
+        # PE_1: c=b+1; PE_2: d=c+1; PE_3: e=c+1; PE_4: f=d+e
+        assert data["f"] == 2 * (i + 2)
+    frame_metrics_ok = pipeline.frames_completed >= 5
+    assert frame_metrics_ok
+
+
+def test_name_mapping_and_graph_path(aiko_process):
+    d = {
+        "version": 0, "name": "p_map", "runtime": "python",
+        "graph": ["(PE_0 (PE_1 PE_3) (PE_2 PE_3))", "(PE_IN PE_TEXT PE_OUT)"],
+        "elements": [_elem("PE_0", ["a"], ["b"]), _elem("PE_1", ["b"], ["c"]),
+                     _elem("PE_2", ["c"], ["d"], cls="PE_2"), _elem("PE_3", ["c"], ["e"], cls="PE_3"),
+                     {"name": "PE_IN", "input": [{"name": "in_a", "type": "str"}],
+                      "output": [{"name": "text_b", "type": "str"}],
+                      "deploy": {"local": {"module": "aiko_services_amd.examples.pipeline.elements"}}},
+                     {"name": "PE_TEXT", "input": [{"name": "text_b", "type": "str"}],
+                      "output": [{"name": "text_b", "type": "str"}],
+                      "deploy": {"local": {"module": "aiko_services_amd.examples.pipeline.elements"}}},
+                     {"name": "PE_OUT", "input": [{"name": "text_b", "type": "str"}],
+                      "output": [{"name": "out_c", "type": "str"}],
+                      "deploy": {"local": {"module": "aiko_services_amd.examples.pipeline.elements"}}}],
+    }
+    pipeline, q = _create(d, graph_path="PE_IN", stream_id="s1")
+    pipeline.create_frame({"stream_id": "s1", "frame_id": 0}, {"in_a": "x"})
+    info, data = q.get(timeout=5)
+    assert data["out_c"] == "x:in:text:out"
+
+
+def test_input_mapping_properties(aiko_process):
+    # "(PE_0 (PE_1 PE_4 (c: d)) ...": PE_1 outputs c, PE_4 expects d and e
+    d = {
+        "version": 0, "name": "p_props", "runtime": "python",
+        "graph": ["(PE_1 (PE_2 PE_4) (PE_3 PE_4 (e: e)))"],
+        "elements": [_elem("PE_1", ["b"], ["c"]), _elem("PE_2", ["c"], ["d"]), _elem("PE_3", ["c"], ["e"]),
+                     _elem("PE_4", ["d", "e"], ["f"])],
+    }
+    pipeline, q = _create(d, stream_id="m1")
+    pipeline.create_frame({"stream_id": "m1", "frame_id": 0}, {"b": 1})
+    info, data = q.get(timeout=5)
+    assert data["f"] == 3 + 3
+
+
+def test_drop_frame_stop_and_error(aiko_process):
+    from aiko_services_amd.pipeline.stream import StreamState
+    d = {
+        "version": 0, "name": "p_text_sample", "runtime": "python",
+        "graph": ["(TextTransform TextSample TextOutput)"],
+        "elements": [
+            {"name": "TextTransform", "parameters": {"transform": "uppercase"},
+             "input": [{"name": "texts", "type": "[str]"}], "output": [{"name": "texts", "type": "[str]"}],
+             "deploy": {"local": {"module": "aiko_services_amd.elements.media.text_io"}}},
+            {"name": "TextSample", "parameters": {"sample_rate": 2},
+             "input": [{"name": "texts", "type": "[str]"}], "output": [{"name": "texts", "type": "[str]"}],
+             "deploy": {"local": {"module": "aiko_services_amd.elements.media.text_io"}}},
+            {"name": "TextOutput", "input": [{"name": "texts", "type": "[str]"}],
+             "output": [{"name": "texts", "type": "[str]"}],
+             "deploy": {"local": {"module": "aiko_services_amd.elements.media.text_io"}}}],
+    }
+    pipeline, q = _create(d, stream_id="t1")
+    for i in range(4):
+        pipeline.create_frame({"stream_id": "t1", "frame_id": i}, {"texts": [f"hello {i}"]})
+    outs = [q.get(timeout=5) for _ in range(4)]
+    states = [info["state"] for info, _ in outs]
+    assert states == [StreamState.RUN, StreamState.DROP_FRAME, StreamState.RUN, StreamState.DROP_FRAME]
+    assert outs[0][1]["texts"] == ["HELLO 0"]
+    # unknown transform -> ERROR -> stream destroyed immediately
+    pipeline2, q2 = _create(json.loads(json.dumps(d).replace('"uppercase"', '"bogus"')), stream_id="t2")
+    pipeline2.create_frame({"stream_id": "t2", "frame_id": 0}, {"texts": ["x"]})
+    info, data = q2.get(timeout=5)
+    assert info["state"] == StreamState.ERROR
+    deadline = time.time() + 2
+    while "t2" in pipeline2.stream_leases and time.time() < deadline:
+        time.sleep(0.01)
+    assert "t2" not in pipeline2.stream_leases
+
+
+def test_text_files_data_source_target(aiko_process, tmp_path):
+    src = tmp_path / "in"
+    src.mkdir()
+    for i in range(3):
+        (src / f"in_{i:02d}.txt").write_text(f"text number {i}")
+    out = tmp_path / "out"
+    out.mkdir()
+    d = {
+        "version": 0, "name": "p_text_files", "runtime": "python",
+        "graph": ["(TextReadFile TextTransform TextWriteFile)"],
+        "elements": [
+            {"name": "TextReadFile", "parameters": {"data_sources": f"(file://{src}/in_{{}}.txt)",
+                                                    "data_batch_size": 1},
+             "input": [{"name": "paths", "type": "[Path]"}], "output": [{"name": "texts", "type": "[str]"}],
+             "deploy": {"local": {"module": "aiko_services_amd.elements.media.text_io"}}},
+            {"name": "TextTransform", "parameters": {"transform": "titlecase"},
+             "input": [{"name": "texts", "type": "[str]"}], "output": [{"name": "texts", "type": "[str]"}],
+             "deploy": {"local": {"module": "aiko_services_amd.elements.media.text_io"}}},
+            {"name": "TextWriteFile", "parameters": {"data_targets": f"file://{out}/out_{{:02d}}.txt"},
+             "input": [{"name": "texts", "type": "[str]"}], "output": [],
+             "deploy": {"local": {"module": "aiko_services_amd.elements.media.text_io"}}}],
+    }
+    pipeline, q = _create(d, stream_id="f1")
+    outs = [q.get(timeout=10) for _ in range(3)]
+    assert len(outs) == 3
+    texts = sorted(p.read_text() for p in out.glob("out_*.txt"))
+    assert texts == ["Text Number 0", "Text Number 1", "Text Number 2"]
+    deadline = time.time() + 5   # STOP after the last frame -> graceful destroy
+    while "f1" in pipeline.stream_leases and time.time() < deadline:
+        time.sleep(0.05)
+    assert "f1" not in pipeline.stream_leases
+
+
+def test_get_parameter_precedence(aiko_process):
+    from aiko_services_amd.pipeline.engine import PipelineElementImpl
+    pipeline, q = _create(DIAMOND, stream_id="pp", parameters={"PE_1.pe_1_inc": 7, "p_3": "stream"})
+    pe_1 = pipeline.get_element("PE_1")
+
+    def check():
+        pipeline._enable_thread_local("test", "pp")
+        try:
+            return (pe_1.get_parameter("pe_1_inc"), pe_1.get_parameter("p_3"), pe_1.get_parameter("p_2"),
+                    pe_1.get_parameter("missing", default=5))
+        finally:
+            pipeline._disable_thread_local("test")
+    a, b, c, d = event.call_on_loop(check)
+    assert a == (7, True)               # stream "Element.name" wins
+    assert b == ("stream", True)        # then element, then stream "name"
+    assert c == (0, True)               # then pipeline definition
+    assert d == (5, False)              # default, found=False
+    pipeline.create_frame({"stream_id": "pp", "frame_id": 0}, {"b": 1})
+    info, data = q.get(timeout=5)
+    assert data["f"] == 2 * (1 + 7 + 1)
+
+
+def test_process_frame_over_message_bus(aiko_process):
+    """MQTT-style ingress: S-expression on the pipeline's /in topic, output on /out."""
+    aiko = aiko_process
+    pipeline, q = _create(DIAMOND, stream_id=None)
+    outputs = queue.Queue()
+    event.call_on_loop(lambda: aiko.process.add_message_handler(
+        lambda _a, topic, payload: outputs.put(payload), pipeline.topic_out))
+    aiko.aiko.message.publish(pipeline.topic_in, "(process_frame (stream_id: 9 frame_id: 3) (b: 0))")
+    # stream 9 does not exist -> warn, no output; default stream "*" auto-creates
+    aiko.aiko.message.publish(pipeline.topic_in, "(process_frame (stream_id: * frame_id: 4) (b: 1))")
+    payload = outputs.get(timeout=5)
+    from aiko_services_amd.utils.sexpr import parse
+    cmd, (info, data) = parse(payload)
+    assert cmd == "process_frame" and info["frame_id"] == "4" and data["f"] == "6"
+
+
+@needs_ref
+@pytest.mark.parametrize("name", ["pipeline_local.json", "pipeline_paths.json", "pipeline_example.json"])
+def test_reference_definitions_parse(name):
+    d = parse_pipeline_definition(str(REF / "examples" / "pipeline" / name))
+    assert d.elements
+
+
+@needs_ref
+def test_reference_pipeline_local_runs(aiko_process, tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)   # PE_Inspect writes z_inspect.txt in cwd
+    path = REF / "examples" / "pipeline" / "pipeline_local.json"
+    d = parse_pipeline_definition(str(path))
+    pipeline, q = _create(d, stream_id="r1", pathname=str(path))
+    pipeline.create_frame({"stream_id": "r1", "frame_id": 0}, {"b": 0})
+    info, data = q.get(timeout=5)
+    assert data["f"] == 4
+    assert (tmp_path / "z_inspect.txt").exists()
+
+
+@needs_ref
+def test_reference_text_pipeline_runs(aiko_process, tmp_path, monkeypatch):
+    media = REF / "elements" / "media"
+    (tmp_path / "data_in").symlink_to(media / "data_in")
+    (tmp_path / "data_out").mkdir()
+    monkeypatch.chdir(tmp_path)
+    d = parse_pipeline_definition(str(media / "text_pipeline_0.json"))
+    pipeline, q = _create(d, stream_id="rt")
+    outs = [q.get(timeout=10) for _ in range(3)]
+    assert len(outs) == 3
+    written = sorted((tmp_path / "data_out").glob("out_*.txt"))
+    assert len(written) == 3
+    assert written[0].read_text() == (media / "data_in" / "in_00.txt").read_text().title()
