@@ -17,7 +17,7 @@ extern "C" {
 int aiko_conv_igemm(const void* x, const void* w, const float* bias, const void* res, void* y,
                     int H, int W, int C, int Cc, int R, int S, int stride, int pad, int Ho,
                     int Wo, int M, int Cout, int K, int act, int ldy, int ldr, int bm, int bn,
-                    hipStream_t stream);
+                    const void* x2, int K1, int H2, int W2, int C2, int stride2, hipStream_t stream);
 int aiko_preprocess(const void* in, void* out, int B, int Hin, int Win, int Ho, int Wo, int Hp,
                     int Wp, int pad_t, int pad_l, const float* mean, const float* std, int bgr,
                     hipStream_t stream);
@@ -46,13 +46,16 @@ void check_launch(int rc, const char* what) {
               rc < 0 ? "unsupported configuration" : hipGetErrorString((hipError_t)rc));
 }
 
-// geom = [H, W, C, Cc, R, S, stride, pad, Ho, Wo, M, act, ldy, ldr, bm, bn]
-void conv_igemm_out(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
-                    const c10::optional<at::Tensor>& res, at::Tensor& y, at::IntArrayRef geom) {
-  TORCH_CHECK(geom.size() == 16, "aiko.conv_igemm_out: geom needs 16 ints");
+// geom = [H, W, C, Cc, R, S, stride, pad, Ho, Wo, M, act, ldy, ldr, bm, bn,
+//         K1, H2, W2, C2, stride2]   (the last five describe the optional second source x2)
+void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, const at::Tensor& w,
+                    const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& res,
+                    at::Tensor& y, at::IntArrayRef geom) {
+  TORCH_CHECK(geom.size() == 21, "aiko.conv_igemm_out: geom needs 21 ints");
   const int64_t H = geom[0], W = geom[1], C = geom[2], Cc = geom[3], R = geom[4], S = geom[5];
   const int64_t stride = geom[6], pad = geom[7], Ho = geom[8], Wo = geom[9], M = geom[10];
   const int64_t act = geom[11], ldy = geom[12], ldr = geom[13], bm = geom[14], bn = geom[15];
+  const int64_t K1 = geom[16], H2 = geom[17], W2 = geom[18], C2 = geom[19], stride2 = geom[20];
   check_cuda(x, "x");
   check_cuda(w, "w");
   check_cuda(y, "y");
@@ -61,8 +64,22 @@ void conv_igemm_out(const at::Tensor& x, const at::Tensor& w, const c10::optiona
               "aiko.conv_igemm_out: x, w, y must be bfloat16");
   TORCH_CHECK(w.dim() == 2 && w.is_contiguous(), "aiko.conv_igemm_out: w must be [Cout, K] contiguous");
   const int64_t Cout = w.size(0), K = w.size(1);
-  TORCH_CHECK(K >= R * S * Cc && K % 64 == 0 && K - R * S * Cc < 64, "aiko.conv_igemm_out: K=", K,
-              " must be R*S*Cc rounded up to a multiple of 64");
+  const bool dual = x2.has_value() && x2->defined();
+  const int64_t Kmain = dual ? K1 : K;
+  TORCH_CHECK(Kmain >= R * S * Cc && Kmain % 64 == 0 && Kmain - R * S * Cc < 64, "aiko.conv_igemm_out: K=",
+              Kmain, " must be R*S*Cc rounded up to a multiple of 64");
+  const void* x2ptr = nullptr;
+  if (dual) {
+    check_cuda(*x2, "x2");
+    TORCH_CHECK(x2->scalar_type() == at::kBFloat16, "aiko.conv_igemm_out: x2 must be bf16");
+    TORCH_CHECK((K - K1) % 64 == 0 && K - K1 <= C2 && C2 % 8 == 0 && K1 > 0,
+                "aiko.conv_igemm_out: second source needs K-K1 (multiple of 64) <= C2");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(x2->data_ptr()) % 16 == 0, "aiko.conv_igemm_out: x2 alignment");
+    TORCH_CHECK(M % (Ho * Wo) == 0 && (Ho - 1) * stride2 < H2 && (Wo - 1) * stride2 < W2 &&
+                    avail_elems(*x2) >= (M / (Ho * Wo)) * H2 * W2 * C2,
+                "aiko.conv_igemm_out: x2 too small for the output geometry");
+    x2ptr = x2->data_ptr();
+  }
   TORCH_CHECK(Cc % 8 == 0 && Cc <= C || (C == 4 && Cc == 32), "aiko.conv_igemm_out: Cc must be a multiple of 8 within the pixel pitch");
   TORCH_CHECK(Cout % 8 == 0, "aiko.conv_igemm_out: Cout must be a multiple of 8");
   TORCH_CHECK(C % 8 == 0 || (C == 4 && Cc % 8 == 0), "aiko.conv_igemm_out: pixel pitch must keep 16-B alignment");
@@ -95,7 +112,7 @@ void conv_igemm_out(const at::Tensor& x, const at::Tensor& w, const c10::optiona
   }
   const int rc = aiko_conv_igemm(x.data_ptr(), w.data_ptr(), bptr, rptr, y.data_ptr(), H, W, C,
                                  Cc, R, S, stride, pad, Ho, Wo, M, Cout, K, act, ldy,
-                                 ldr, bm, bn, cur_stream());
+                                 ldr, bm, bn, x2ptr, K1, H2, W2, C2, stride2, cur_stream());
   check_launch(rc, "conv_igemm");
 }
 
@@ -165,7 +182,7 @@ void softmax_topk_out(const at::Tensor& logits, at::Tensor& prob, at::Tensor& in
 }  // namespace
 
 TORCH_LIBRARY(aiko, m) {
-  m.def("conv_igemm_out(Tensor x, Tensor w, Tensor? bias, Tensor? res, Tensor(a!) y, int[] geom) -> ()");
+  m.def("conv_igemm_out(Tensor x, Tensor? x2, Tensor w, Tensor? bias, Tensor? res, Tensor(a!) y, int[] geom) -> ()");
   m.def("preprocess_out(Tensor frames, Tensor(a!) out, int Ho, int Wo, int pad_t, int pad_l, float[] mean, float[] std, bool bgr) -> ()");
   m.def("maxpool_out(Tensor x, Tensor(a!) y, int k, int s, int p) -> ()");
   m.def("avgpool_out(Tensor x, Tensor(a!) y) -> ()");

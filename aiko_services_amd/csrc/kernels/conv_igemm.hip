@@ -35,6 +35,10 @@ struct ConvParams {
   int Ho, Wo, M, Cout, K;
   int act;              // 0 none, 1 relu, 2 silu
   int ldy, ldr;
+  // optional second A source (K columns [K1, K)): a 1x1 / stride-s2 conv over x2, used to
+  // fuse a ResNet projection shortcut into the block's last conv (K-concatenation)
+  const bf16_t* x2;
+  int K1, H2, W2, C2, stride2;
 };
 
 template <int BM, int BN>
@@ -84,6 +88,54 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvParams p) {
       a_base[i] = 0;
     }
   }
+  int a2_base[APT];
+  if (p.x2) {
+#pragma unroll
+    for (int i = 0; i < APT; ++i) {
+      const int m = m0 + prow + 32 * i;
+      if (m < p.M) {
+        const int img = m / HoWo;
+        const int rem = m - img * HoWo;
+        const int oh = rem / p.Wo;
+        const int ow = rem - oh * p.Wo;
+        a2_base[i] = ((img * p.H2 + oh * p.stride2) * p.W2 + ow * p.stride2) * p.C2;
+      } else {
+        a2_base[i] = -1;
+      }
+    }
+  }
+
+  // ---- epilogue operands prefetched now: their HBM latency hides under the K loop ----
+  constexpr int CPR = BN / 8;             // 8-wide chunks per output row
+  constexpr int CHUNKS = BM * CPR;
+  constexpr int CPT = CHUNKS / 256;       // chunks per thread
+  static_assert(CHUNKS % 256 == 0, "tile must give every thread whole chunks");
+  const int e_cc = tid % CPR;             // this thread's column chunk (fixed: 256 % CPR == 0)
+  const int e_row0 = tid / CPR;
+  constexpr int E_ROWS = 256 / CPR;       // row stride between a thread's chunks
+  const int e_n = n0 + e_cc * 8;
+  float e_bias[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) e_bias[e] = 0.f;
+  if (p.bias && e_n < p.Cout) {
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(p.bias + e_n);
+    const f32x4 b1 = *reinterpret_cast<const f32x4*>(p.bias + e_n + 4);
+    e_bias[0] = b0[0]; e_bias[1] = b0[1]; e_bias[2] = b0[2]; e_bias[3] = b0[3];
+    e_bias[4] = b1[0]; e_bias[5] = b1[1]; e_bias[6] = b1[2]; e_bias[7] = b1[3];
+  }
+  u32x4 e_res[CPT];
+  if (p.res) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int m = m0 + e_row0 + E_ROWS * i;
+      if (m < p.M && e_n < p.Cout) {
+        e_res[i] = *reinterpret_cast<const u32x4*>(p.res + (size_t)m * p.ldr + e_n);
+      } else {
+        e_res[i] = u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+  }
+
   int b_off[BPT];
   bool b_ok[BPT];
 #pragma unroll
@@ -95,6 +147,22 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvParams p) {
 
   u32x4 ra[APT], rb[BPT];
   auto load_global = [&](int kb) {
+    if (p.x2 && kb * BK >= p.K1) {          // block-uniform: second source (1x1 shortcut)
+      const int c2 = kb * BK - p.K1 + piece * 8;
+#pragma unroll
+      for (int i = 0; i < APT; ++i) {
+        if (a2_base[i] >= 0) {
+          ra[i] = *reinterpret_cast<const u32x4*>(p.x2 + (a2_base[i] + c2));
+        } else {
+          ra[i] = u32x4{0u, 0u, 0u, 0u};
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < BPT; ++i) {
+        rb[i] = b_ok[i] ? *reinterpret_cast<const u32x4*>(p.w + (b_off[i] + kb * BK)) : u32x4{0u, 0u, 0u, 0u};
+      }
+      return;
+    }
     const int koff = kb * BK + piece * 8;
     const int tap = koff / p.Cc;  // K may be zero-padded past R*S*Cc: taps >= R*S meet zero weights
     const int c = koff - tap * p.Cc;
@@ -195,29 +263,21 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvParams p) {
     }
   __syncthreads();
 
-  constexpr int CPR = BN / 8;  // 8-wide chunks per row
-  constexpr int CHUNKS = BM * CPR;
-  for (int q = tid; q < CHUNKS; q += 256) {
-    const int row = q / CPR;
-    const int cc = q - row * CPR;
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int row = e_row0 + E_ROWS * i;
     const int m = m0 + row;
-    const int n = n0 + cc * 8;
-    if (m >= p.M || n >= p.Cout) continue;
-    const f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + cc * 8);
-    const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + cc * 8 + 4);
+    if (m >= p.M || e_n >= p.Cout) continue;
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + e_cc * 8);
+    const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + e_cc * 8 + 4);
     float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-    if (p.bias) {
-      const f32x4 b0 = *reinterpret_cast<const f32x4*>(p.bias + n);
-      const f32x4 b1 = *reinterpret_cast<const f32x4*>(p.bias + n + 4);
-      v[0] += b0[0]; v[1] += b0[1]; v[2] += b0[2]; v[3] += b0[3];
-      v[4] += b1[0]; v[5] += b1[1]; v[6] += b1[2]; v[7] += b1[3];
-    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += e_bias[e];
     if (p.res) {
-      const u32x4 r = *reinterpret_cast<const u32x4*>(p.res + (size_t)m * p.ldr + n);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        v[2 * e] += __uint_as_float(r[e] << 16);
-        v[2 * e + 1] += __uint_as_float(r[e] & 0xffff0000u);
+        v[2 * e] += __uint_as_float(e_res[i][e] << 16);
+        v[2 * e + 1] += __uint_as_float(e_res[i][e] & 0xffff0000u);
       }
     }
     if (p.act == 1) {
@@ -230,7 +290,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvParams p) {
     u32x4 o;
 #pragma unroll
     for (int e = 0; e < 4; ++e) o[e] = pack2(v[2 * e], v[2 * e + 1]);
-    *reinterpret_cast<u32x4*>(p.y + (size_t)m * p.ldy + n) = o;
+    *reinterpret_cast<u32x4*>(p.y + (size_t)m * p.ldy + e_n) = o;
   }
 }
 
@@ -239,7 +299,8 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvParams p) {
 extern "C" int aiko_conv_igemm(const void* x, const void* w, const float* bias, const void* res,
                                void* y, int H, int W, int C, int Cc, int R, int S,
                                int stride, int pad, int Ho, int Wo, int M, int Cout, int K,
-                               int act, int ldy, int ldr, int bm, int bn, hipStream_t stream) {
+                               int act, int ldy, int ldr, int bm, int bn, const void* x2, int K1,
+                               int H2, int W2, int C2, int stride2, hipStream_t stream) {
   using namespace aiko;
   ConvParams p;
   p.x = static_cast<const bf16_t*>(x);
@@ -250,6 +311,8 @@ extern "C" int aiko_conv_igemm(const void* x, const void* w, const float* bias, 
   p.H = H; p.W = W; p.C = C; p.Cc = Cc; p.R = R; p.S = S;
   p.stride = stride; p.pad = pad; p.Ho = Ho; p.Wo = Wo; p.M = M; p.Cout = Cout; p.K = K;
   p.act = act; p.ldy = ldy; p.ldr = ldr;
+  p.x2 = static_cast<const bf16_t*>(x2);
+  p.K1 = x2 ? K1 : K; p.H2 = H2; p.W2 = W2; p.C2 = C2; p.stride2 = stride2;
   const int ntm = (M + bm - 1) / bm;
   const int ntn = (Cout + bn - 1) / bn;
   dim3 grid(ntm * ntn), block(256);

@@ -1,0 +1,165 @@
+"""GPU-resident vision PipelineElements (MI355X): the ResNet-50 pipeline of BASELINE configs 2/3.
+
+    "(SyntheticFrames ResNet50Classifier ClassifierTopK)"                    config 2 / bench
+    "(SyntheticFrames ImagePreprocess ResNet50Classifier ClassifierTopK)"    config 3 stages
+
+* ``SyntheticFrames`` — the "decode" stage: a batch of ``batch`` uint8 RGB frames of
+  ``height`` x ``width`` produced directly in HBM (a rotating pool of ``pool`` random batches,
+  like a hardware decoder writing into device memory; no host upload on the hot path).  In a
+  stream it can also run as a frame generator (``frames``, ``rate``).
+* ``ImagePreprocess`` — fused bilinear resize + ImageNet normalise + NHWC->padded-4-channel
+  layout in one HIP kernel (output: the ResNet stem buffer).
+* ``ResNet50Classifier`` — ResNet-50 on the igemm MFMA kernels; accepts uint8 frames (then
+  pre-processes itself) or a stem buffer; emits logits; optional hipGraph capture.
+* ``ClassifierTopK`` — softmax + top-k kernel; with data parallelism (torch.distributed over
+  RCCL) all-gathers the results to every rank; copies them to pinned host memory without
+  synchronising and emits a :class:`DeviceResult`.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+from ...gpu.element import DeviceResult, GpuPipelineElement
+from ...pipeline.stream import StreamEvent
+
+__all__ = ["SyntheticFrames", "ImagePreprocess", "ResNet50Classifier", "ClassifierTopK"]
+
+
+def _int(v, d):
+    try:
+        return int(v)
+    except (TypeError, ValueError):
+        return d
+
+
+class SyntheticFrames(GpuPipelineElement):
+    def __init__(self, context):
+        context.set_protocol("synthetic_frames:0")
+        super().__init__(context)
+        self._pool = None
+        self._cursor = 0
+
+    def _frames(self):
+        if self._pool is None:
+            B = _int(self.get_parameter("batch", 1)[0], 1)
+            H = _int(self.get_parameter("height", 224)[0], 224)
+            W = _int(self.get_parameter("width", 224)[0], 224)
+            n = _int(self.get_parameter("pool", 2)[0], 2)
+            seed = _int(self.get_parameter("seed", 0)[0], 0)
+            g = torch.Generator(device=self.device).manual_seed(seed)
+            self._pool = [torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=self.device,
+                                        generator=g) for _ in range(max(1, n))]
+        frames = self._pool[self._cursor % len(self._pool)]
+        self._cursor += 1
+        return frames
+
+    def start_stream(self, stream, stream_id):
+        limit, found = self.get_parameter("frames")
+        if found and limit:
+            stream.variables["synthetic_left"] = int(limit)
+            rate, _ = self.get_parameter("rate", None)
+            self.create_frames(stream, self.frame_generator, rate=float(rate) if rate else None)
+        return StreamEvent.OKAY, None
+
+    def frame_generator(self, stream, frame_id):
+        left = stream.variables.get("synthetic_left", 0)
+        if left <= 0:
+            return StreamEvent.STOP, {"diagnostic": "All frames generated"}
+        stream.variables["synthetic_left"] = left - 1
+        return StreamEvent.OKAY, {"t_submit": time.perf_counter()}
+
+    def process_frame(self, stream, **kwargs):
+        return StreamEvent.OKAY, {"images": self._frames(), "t_submit": kwargs.get("t_submit", time.perf_counter())}
+
+
+class ImagePreprocess(GpuPipelineElement):
+    def __init__(self, context):
+        context.set_protocol("image_preprocess:0")
+        super().__init__(context)
+        self.size = _int(self.get_parameter("image_size", 224)[0], 224)
+        self._out = {}
+
+    def process_frame(self, stream, images):
+        from ...ops import conv as C
+        from ...ops import vision as V
+        B = images.shape[0]
+        Hp, Wp = C.stem_geometry(self.size, self.size)
+        out = self._out.get(B)
+        if out is None:
+            out = self._out[B] = torch.empty(B, Hp, Wp, 4, dtype=torch.bfloat16, device=self.device)
+        return StreamEvent.OKAY, {"images": V.preprocess_frames(images, (self.size, self.size), out=out)}
+
+
+class ResNet50Classifier(GpuPipelineElement):
+    def __init__(self, context):
+        context.set_protocol("resnet50:0")
+        super().__init__(context)
+        from ...models.resnet50 import ResNet50
+        from ...ops import require_native
+        require_native()
+        seed = _int(self.get_parameter("seed", 0)[0], 0)
+        self.model = ResNet50(seed=seed, device=self.device,
+                              image_size=_int(self.get_parameter("image_size", 224)[0], 224))
+
+    def _run(self, images):
+        if images.dtype == torch.uint8:
+            x = self.model.preprocess(images)
+        else:
+            x = images
+        return self.model.logits_from_stem(x)
+
+    def process_frame(self, stream, images):
+        key = (tuple(images.shape), images.dtype)
+        logits = self.run_maybe_captured(key, self._run, images)
+        return StreamEvent.OKAY, {"logits": logits}
+
+
+class ClassifierTopK(GpuPipelineElement):
+    def __init__(self, context):
+        context.set_protocol("classifier_topk:0")
+        super().__init__(context)
+        self.k = _int(self.get_parameter("k", 5)[0], 5)
+        gather, _ = self.get_parameter("gather", default=True)
+        self.gather = str(gather).lower() in ("true", "1", "yes")
+        self._bufs = {}
+
+    def _buffers(self, B, world):
+        key = (B, world)
+        b = self._bufs.get(key)
+        if b is None:
+            dev = self.device
+            b = {"prob": torch.empty(B, self.k, dtype=torch.float32, device=dev),
+                 "index": torch.empty(B, self.k, dtype=torch.int32, device=dev),
+                 "all_prob": torch.empty(world * B, self.k, dtype=torch.float32, device=dev),
+                 "all_index": torch.empty(world * B, self.k, dtype=torch.int32, device=dev),
+                 "host_prob": [torch.empty(world * B, self.k, dtype=torch.float32, pin_memory=True)
+                               for _ in range(4)],
+                 "host_index": [torch.empty(world * B, self.k, dtype=torch.int32, pin_memory=True)
+                                for _ in range(4)],
+                 "slot": 0}
+            self._bufs[key] = b
+        return b
+
+    def process_frame(self, stream, logits, t_submit=None):
+        from ...ops import vision as V
+        from ...parallel import dist as D
+        B = logits.shape[0]
+        world = D.world_size() if self.gather else 1
+        b = self._buffers(B, world)
+        prob, index = V.softmax_topk(logits, self.k, prob=b["prob"], index=b["index"])
+        if world > 1:
+            D.all_gather_into(b["all_prob"], prob)
+            D.all_gather_into(b["all_index"], index)
+            prob, index = b["all_prob"], b["all_index"]
+        slot = b["slot"]
+        b["slot"] = (slot + 1) % len(b["host_prob"])
+        hp, hi = b["host_prob"][slot], b["host_index"][slot]
+        hp.copy_(prob, non_blocking=True)
+        hi.copy_(index, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        result = DeviceResult({"top_prob": hp, "top_index": hi}, ev,
+                              t_submit=t_submit if isinstance(t_submit, float) else None)
+        return StreamEvent.OKAY, {"topk": result}

@@ -1,0 +1,164 @@
+"""GPU-resident PipelineElements and frame-buffer pools.
+
+``GpuPipelineElement`` is a PipelineElement bound to one MI355X (its ``deploy.local.device``,
+else this process's GPU) that launches HIP work asynchronously on the current stream and
+hands device tensors to its successors through the frame ``swag`` (no copies, no
+serialisation).  Optional hipGraph capture (parameter ``graph: true``) replays the element's
+whole launch sequence per input shape, removing per-kernel launch cost; inputs are copied
+into the captured static buffers when their address differs.
+
+``DeviceResult`` is what a GPU pipeline emits at its output: device/pinned-host tensors plus
+the HIP event that completes them — the consumer calls ``wait()`` (or ``ready()``) instead of
+the pipeline synchronising the device per frame.
+
+``FramePool`` wraps the native HBM slab pool (``csrc/runtime/frame_pool.cpp``).
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+from ..pipeline.engine import PipelineElement
+from ..pipeline.stream import StreamEvent
+from .device import parse_device, require_gpu
+
+__all__ = ["GpuPipelineElement", "DeviceResult", "FramePool", "CapturedCall"]
+
+_DTYPE_CODES = {torch.uint8: 0, torch.int8: 1, torch.int16: 2, torch.int32: 3, torch.int64: 4,
+                torch.float16: 5, torch.float32: 6, torch.float64: 7, torch.bool: 11,
+                torch.bfloat16: 15}
+
+
+class FramePool:
+    """Fixed-size HBM slots with blocking acquire (back-pressure) — native implementation."""
+
+    def __init__(self, num_slots: int, slot_bytes: int, device=None):
+        from ..ops import require_native
+        require_native()
+        dev = parse_device(device) if device is not None else None
+        self._pool = torch.classes.aiko.FramePool(int(num_slots), int(slot_bytes),
+                                                  dev.index if dev is not None and dev.type == "cuda" else -1)
+
+    def acquire(self, timeout: float | None = None) -> int:
+        return self._pool.acquire(-1 if timeout is None else int(timeout * 1000))
+
+    def release(self, slot: int) -> None:
+        self._pool.release(int(slot))
+
+    def view(self, slot: int, shape, dtype=torch.uint8) -> torch.Tensor:
+        return self._pool.view(int(slot), list(shape), _DTYPE_CODES[dtype])
+
+    def close(self):
+        self._pool.close()
+
+    @property
+    def capacity(self):
+        return self._pool.capacity()
+
+    @property
+    def slot_bytes(self):
+        return self._pool.slot_bytes()
+
+    def free_count(self):
+        return self._pool.free_count()
+
+    def stats(self) -> dict:
+        cap, used, hw, acq, exh = self._pool.stats()
+        return {"capacity": cap, "in_use": used, "high_water": hw, "acquired": acq, "exhausted": exh}
+
+
+class DeviceResult:
+    """Tensors produced asynchronously on the GPU plus the event that completes them."""
+
+    __slots__ = ("tensors", "event", "t_submit", "t_done", "meta")
+
+    def __init__(self, tensors: dict, event: torch.cuda.Event | None, t_submit: float | None = None, meta=None):
+        self.tensors = tensors
+        self.event = event
+        self.t_submit = t_submit if t_submit is not None else time.perf_counter()
+        self.t_done = None
+        self.meta = meta or {}
+
+    def ready(self) -> bool:
+        return self.event is None or self.event.query()
+
+    def wait(self) -> dict:
+        if self.event is not None:
+            self.event.synchronize()
+        if self.t_done is None:
+            self.t_done = time.perf_counter()
+        return self.tensors
+
+    @property
+    def latency(self):
+        return None if self.t_done is None else self.t_done - self.t_submit
+
+    def __repr__(self):
+        shapes = {k: tuple(v.shape) if hasattr(v, "shape") else v for k, v in self.tensors.items()}
+        return f"DeviceResult({shapes}, ready={self.ready()})"
+
+
+class CapturedCall:
+    """hipGraph capture of ``fn(*static_inputs)`` for one input signature."""
+
+    def __init__(self, fn, example_inputs, warmup: int = 1):
+        self.static_inputs = [t.clone() for t in example_inputs]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                fn(*self.static_inputs)
+        torch.cuda.current_stream().wait_stream(s)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.static_outputs = fn(*self.static_inputs)
+
+    def __call__(self, *inputs):
+        for dst, src in zip(self.static_inputs, inputs):
+            if dst.data_ptr() != src.data_ptr():
+                dst.copy_(src, non_blocking=True)
+        self.graph.replay()
+        return self.static_outputs
+
+
+class GpuPipelineElement(PipelineElement):
+    """Base class: resolves the device, offers ``run_maybe_captured(key, fn, *inputs)``."""
+
+    def __init__(self, context):
+        context.get_implementation("PipelineElement").__init__(self, context)
+        require_gpu()
+        deploy = getattr(self.definition, "deploy", None)
+        device_spec = getattr(deploy, "device", None)
+        device_param, found = self.get_parameter("device")
+        if found:
+            device_spec = device_param
+        self.device = parse_device(device_spec)
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        graph, _ = self.get_parameter("graph", default=False)
+        self.use_graph = str(graph).lower() in ("true", "1", "yes")
+        self._captured: dict = {}
+        self.share["device"] = str(self.device)
+
+    def run_maybe_captured(self, key, fn, *inputs):
+        if not self.use_graph:
+            return fn(*inputs)
+        call = self._captured.get(key)
+        if call is None:
+            call = CapturedCall(fn, inputs)
+            self._captured[key] = call
+        return call(*inputs)
+
+    def gpu_timer_start(self):
+        start = torch.cuda.Event(enable_timing=True)
+        start.record()
+        return start
+
+    def gpu_timer_stop(self, start):
+        end = torch.cuda.Event(enable_timing=True)
+        end.record()
+        start._aiko_end = end
+
+    def start_stream(self, stream, stream_id):
+        return StreamEvent.OKAY, None

@@ -48,6 +48,7 @@ class Bottleneck:
     conv2: C.ConvSpec
     conv3: C.ConvSpec
     down: C.ConvSpec | None
+    fused: C.ConvSpec | None = None   # conv3 + projection shortcut as one K-concatenated igemm
 
 
 class ResNet50:
@@ -81,12 +82,14 @@ class ResNet50:
                 if i == 0:
                     down = C.make_conv_spec(*C.fold_bn(_rand_conv(g, cout, cin, 1), *_rand_bn(g, cout)),
                                             stride=s, act=None, device=self.device)
-                self.blocks.append(Bottleneck(c1, c2, c3, down))
+                fused = C.fuse_shortcut(c3, down) if down is not None else None
+                self.blocks.append(Bottleneck(c1, c2, c3, down, fused))
                 cin = cout
         fc_w = 0.01 * torch.randn(num_classes, 2048, generator=g)
         fc_b = torch.zeros(num_classes)
         self.fc = C.make_linear_spec(fc_w, fc_b, device=self.device)
         self._ws: dict = {}
+        self.fuse_shortcut = True
 
     # ---- workspace: every activation buffer allocated once per batch size ----------------
     def _buf(self, key: str, shape, dtype=torch.bfloat16) -> torch.Tensor:
@@ -101,12 +104,17 @@ class ResNet50:
         self._ws.clear()
 
     # ---- forward ------------------------------------------------------------------------
-    def features(self, frames: torch.Tensor) -> torch.Tensor:
-        """uint8 [B, H, W, 3] -> pooled features bf16 [B, 2048]."""
+    def preprocess(self, frames: torch.Tensor) -> torch.Tensor:
+        """uint8 [B, H, W, 3] (any H, W) -> zero-bordered bf16 stem buffer [B, Hp, Wp, 4]."""
         B = frames.shape[0]
         S = self.image_size
         Hp, Wp = C.stem_geometry(S, S)
-        x = V.preprocess_frames(frames, (S, S), out=self._buf("pre", (B, Hp, Wp, 4)))
+        return V.preprocess_frames(frames, (S, S), out=self._buf("pre", (B, Hp, Wp, 4)))
+
+    def features_from_stem(self, x: torch.Tensor) -> torch.Tensor:
+        """Stem buffer -> pooled features bf16 [B, 2048]."""
+        B = x.shape[0]
+        S = self.image_size
         Ho, Wo = C.stem_out_hw(S, S)
         x = C.conv2d(x, self.stem, out=self._buf("stem", (B, Ho, Wo, 64)), image_hw=(S, S))
         Hm, Wm = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
@@ -116,13 +124,30 @@ class ResNet50:
             t1 = C.conv2d(x, blk.conv1, out=self._buf("t1", (B, H, W, blk.conv1.cout)))
             Ho, Wo = blk.conv2.out_hw(H, W)
             t2 = C.conv2d(t1, blk.conv2, out=self._buf("t2", (B, Ho, Wo, blk.conv2.cout)))
-            if blk.down is not None:
-                idn = C.conv2d(x, blk.down, out=self._buf("ds", (B, Ho, Wo, blk.down.cout)))
-            else:
-                idn = x
             key = "xa" if bi % 2 == 0 else "xb"
-            x = C.conv2d(t2, blk.conv3, residual=idn, out=self._buf(key, (B, Ho, Wo, blk.conv3.cout)))
+            out = self._buf(key, (B, Ho, Wo, blk.conv3.cout))
+            if blk.fused is not None and self.fuse_shortcut:
+                x = C.conv2d(t2, blk.fused, x2=x, out=out)
+            elif blk.down is not None:
+                idn = C.conv2d(x, blk.down, out=self._buf("ds", (B, Ho, Wo, blk.down.cout)))
+                x = C.conv2d(t2, blk.conv3, residual=idn, out=out)
+            else:
+                x = C.conv2d(t2, blk.conv3, residual=x, out=out)
         return V.avgpool(x, out=self._buf("gap", (B, x.shape[3])))
+
+    def features(self, frames: torch.Tensor) -> torch.Tensor:
+        """uint8 [B, H, W, 3] -> pooled features bf16 [B, 2048]."""
+        return self.features_from_stem(self.preprocess(frames))
+
+    def logits_from_stem(self, x: torch.Tensor) -> torch.Tensor:
+        f = self.features_from_stem(x)
+        return C.linear(f, self.fc, out=self._buf("logits", (f.shape[0], self.num_classes)))
+
+    def topk_from_logits(self, lg: torch.Tensor):
+        B = lg.shape[0]
+        return V.softmax_topk(lg, self.topk,
+                              prob=self._buf("prob", (B, self.topk), torch.float32),
+                              index=self._buf("index", (B, self.topk), torch.int32))
 
     def logits(self, frames: torch.Tensor) -> torch.Tensor:
         f = self.features(frames)

@@ -42,6 +42,9 @@ class ConvSpec:
     kind: str = "conv"              # conv | stem | linear
     ref_weight: torch.Tensor | None = field(default=None, repr=False)  # fp32 OIHW (folded)
     ref_bias: torch.Tensor | None = field(default=None, repr=False)
+    # second A source (fused 1x1 projection shortcut): K columns [K1, K) read x2
+    K1: int | None = None
+    stride2: int = 1
 
     def to(self, device) -> "ConvSpec":
         self.weight = self.weight.to(device)
@@ -104,6 +107,21 @@ def make_conv_spec(w_oihw: torch.Tensor, bias: torch.Tensor | None, stride=1, pa
     return spec.to(device) if device is not None else spec
 
 
+def fuse_shortcut(main: ConvSpec, down: ConvSpec) -> ConvSpec:
+    """Fuse a 1x1 projection shortcut into a block's last 1x1 conv by K-concatenation:
+    ``act(main(x) + down(x2) + b_main + b_down)`` becomes ONE igemm over ``[x | x2]`` with
+    weights ``[W_main | W_down]`` — the shortcut activation is never written to HBM and the
+    residual is never read back."""
+    assert main.R == main.S == 1 and down.R == down.S == 1 and main.cout == down.cout
+    assert main.stride == 1 and down.pad == 0
+    bias = None
+    if main.bias is not None or down.bias is not None:
+        bias = (main.bias if main.bias is not None else 0) + (down.bias if down.bias is not None else 0)
+    return ConvSpec(weight=torch.cat([main.weight, down.weight], dim=1).contiguous(), bias=bias,
+                    cin=main.cin, cout=main.cout, R=1, S=1, stride=1, pad=0, Cc=main.Cc, act=main.act,
+                    kind="conv", K1=main.K, stride2=down.stride)
+
+
 def make_linear_spec(w_oi: torch.Tensor, bias: torch.Tensor | None, act=None, device=None) -> ConvSpec:
     cout, cin = w_oi.shape
     spec = make_conv_spec(w_oi.reshape(cout, cin, 1, 1), bias, act=act, device=device)
@@ -162,14 +180,15 @@ def pick_tile(M: int, cout: int) -> tuple[int, int]:
 
 def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None,
            out: torch.Tensor | None = None, tile: tuple[int, int] | None = None,
-           image_hw: tuple[int, int] | None = None) -> torch.Tensor:
+           image_hw: tuple[int, int] | None = None, x2: torch.Tensor | None = None) -> torch.Tensor:
     """NHWC bf16 conv with fused bias / residual / activation on the MFMA igemm kernel.
 
     ``x`` is ``[B, H, W, C]`` — possibly a channel-slice view of a wider buffer (the pixel
     pitch is ``x.stride(2)``).  For a stem spec ``x`` is the zero-bordered ``[B, Hp, Wp, 4]``
     buffer from :func:`aiko_services_amd.ops.preprocess_frames` and ``image_hw`` the original
-    image size.  ``residual`` (optional) has the output's shape.  ``out`` may be a channel
-    slice of a concat buffer.  Returns ``out`` ``[B, Ho, Wo, Cout]``.
+    image size.  ``residual`` (optional) has the output's shape.  ``x2`` is the second source of
+    a :func:`fuse_shortcut` spec.  ``out`` may be a channel slice of a concat buffer.
+    Returns ``out`` ``[B, Ho, Wo, Cout]``.
     """
     B, H, W, C = x.shape
     pitch = x.stride(2)
@@ -187,11 +206,18 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None
     if out is None:
         out = torch.empty(B, Ho, Wo, spec.cout, dtype=torch.bfloat16, device=x.device)
     bm, bn = tile or pick_tile(M, spec.cout)
+    if spec.K1 is not None:
+        if x2 is None or not x2.is_contiguous():
+            raise ValueError("conv2d: fused-shortcut spec needs a contiguous x2")
+        src2 = [spec.K1, x2.shape[1], x2.shape[2], x2.shape[3], spec.stride2]
+    else:
+        x2 = None
+        src2 = [spec.K, 1, 1, 8, 1]
     geom = [H, W, pitch, spec.Cc, spec.R, spec.S, spec.stride, spec.pad, Ho, Wo, M,
             spec.act, out.stride(2) if out.dim() == 4 else out.stride(0),
             0 if residual is None else (residual.stride(2) if residual.dim() == 4 else residual.stride(0)),
-            bm, bn]
-    torch.ops.aiko.conv_igemm_out(x, spec.weight, spec.bias, residual, out, geom)
+            bm, bn] + src2
+    torch.ops.aiko.conv_igemm_out(x, x2, spec.weight, spec.bias, residual, out, geom)
     return out
 
 
@@ -203,6 +229,6 @@ def linear(x: torch.Tensor, spec: ConvSpec, out: torch.Tensor | None = None,
         out = torch.empty(B, spec.cout, dtype=torch.bfloat16, device=x.device)
     bm, bn = pick_tile(B, spec.cout)
     geom = [1, 1, x.stride(0), spec.Cc, 1, 1, 1, 0, 1, 1, B, spec.act, out.stride(0),
-            0 if residual is None else residual.stride(0), bm, bn]
-    torch.ops.aiko.conv_igemm_out(x, spec.weight, spec.bias, residual, out, geom)
+            0 if residual is None else residual.stride(0), bm, bn, spec.K, 1, 1, 8, 1]
+    torch.ops.aiko.conv_igemm_out(x, None, spec.weight, spec.bias, residual, out, geom)
     return out

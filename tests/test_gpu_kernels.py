@@ -146,3 +146,26 @@ def test_resnet50_matches_fp32_reference(native):
     torch.cuda.synchronize()
     assert p.shape == (4, 5) and i.shape == (4, 5)
     assert (i[:, 0].long() == lg.argmax(1)).all()
+
+
+@pytest.mark.parametrize("B,H,cin_main,cin_sc,cout,stride", [(2, 28, 64, 64, 256, 1), (2, 28, 128, 256, 512, 2),
+                                                              (1, 14, 512, 1024, 2048, 2)])
+def test_fused_projection_shortcut(native, B, H, cin_main, cin_sc, cout, stride):
+    """conv3(t) + down(x) (+bias, ReLU) as one K-concatenated igemm with two A sources."""
+    from aiko_services_amd.ops import conv as C
+    from aiko_services_amd.ops import reference as R
+    g = torch.Generator().manual_seed(21)
+    Ho = H // stride
+    w3 = torch.randn(cout, cin_main, 1, 1, generator=g) / cin_main ** 0.5
+    wd = torch.randn(cout, cin_sc, 1, 1, generator=g) / cin_sc ** 0.5
+    b3, bd = torch.randn(cout, generator=g), torch.randn(cout, generator=g)
+    main = C.make_conv_spec(w3, b3, act="relu", device=DEV)
+    down = C.make_conv_spec(wd, bd, stride=stride, device=DEV)
+    fused = C.fuse_shortcut(main, down)
+    t = torch.randn(B, Ho, Ho, cin_main, generator=g).to(torch.bfloat16).to(DEV)
+    x = torch.randn(B, H, H, cin_sc, generator=g).to(torch.bfloat16).to(DEV)
+    y = C.conv2d(t, fused, x2=x)
+    torch.cuda.synchronize()
+    idn = R.conv_ref(x.permute(0, 3, 1, 2).float(), down)
+    ref = R.conv_ref(t.permute(0, 3, 1, 2).float(), main, idn)
+    assert _rel_err(y.permute(0, 3, 1, 2), ref) < 1e-2
