@@ -102,6 +102,9 @@ class ResNet50Classifier(GpuPipelineElement):
         seed = _int(self.get_parameter("seed", 0)[0], 0)
         self.model = ResNet50(seed=seed, device=self.device,
                               image_size=_int(self.get_parameter("image_size", 224)[0], 224))
+        tune, _ = self.get_parameter("autotune", default=True)
+        self.autotune = str(tune).lower() in ("true", "1", "yes")
+        self._tuned = set()
 
     def _run(self, images):
         if images.dtype == torch.uint8:
@@ -112,6 +115,13 @@ class ResNet50Classifier(GpuPipelineElement):
 
     def process_frame(self, stream, images):
         key = (tuple(images.shape), images.dtype)
+        if key not in self._tuned:
+            # first frame of a new shape: pick each conv's tile by measurement, then capture
+            from ...ops import conv as C
+            if self.autotune:
+                with C.autotune():
+                    self._run(images)
+            self._tuned.add(key)
         logits = self.run_maybe_captured(key, self._run, images)
         return StreamEvent.OKAY, {"logits": logits}
 
@@ -135,9 +145,9 @@ class ClassifierTopK(GpuPipelineElement):
                  "all_prob": torch.empty(world * B, self.k, dtype=torch.float32, device=dev),
                  "all_index": torch.empty(world * B, self.k, dtype=torch.int32, device=dev),
                  "host_prob": [torch.empty(world * B, self.k, dtype=torch.float32, pin_memory=True)
-                               for _ in range(4)],
+                               for _ in range(8)],
                  "host_index": [torch.empty(world * B, self.k, dtype=torch.int32, pin_memory=True)
-                                for _ in range(4)],
+                                for _ in range(8)],
                  "slot": 0}
             self._bufs[key] = b
         return b

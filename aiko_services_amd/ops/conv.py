@@ -165,6 +165,51 @@ def _round_up(v: int, m: int) -> int:
     return (v + m - 1) // m * m
 
 
+TILES = ((128, 128), (128, 64), (64, 128), (64, 64))
+_tile_cache: dict = {}          # geometry key -> (bm, bn), filled by autotune()
+_tuning = False
+
+
+class autotune:
+    """Context manager: while active, every conv whose geometry has no cached tile times each
+    candidate tile on the GPU (3 runs, HIP events) and keeps the fastest — like a conv
+    "benchmark mode".  Wave quantisation (tiles vs 256 CUs x 2 blocks) makes the best tile
+    shape-dependent; measuring beats modelling it."""
+
+    def __enter__(self):
+        global _tuning
+        self._prev = _tuning
+        _tuning = True
+        return self
+
+    def __exit__(self, *exc):
+        global _tuning
+        _tuning = self._prev
+
+
+def tile_cache() -> dict:
+    return dict(_tile_cache)
+
+
+def _tune(key, M, cout, launch):
+    cands = TILES
+    best, best_t = None, None
+    for t in cands:
+        launch(t)  # warm
+        start = torch.cuda.Event(enable_timing=True)
+        end = torch.cuda.Event(enable_timing=True)
+        start.record()
+        for _ in range(3):
+            launch(t)
+        end.record()
+        end.synchronize()
+        ms = start.elapsed_time(end)
+        if best_t is None or ms < best_t:
+            best, best_t = t, ms
+    _tile_cache[key] = best
+    return best
+
+
 def pick_tile(M: int, cout: int) -> tuple[int, int]:
     """Block tile (BM, BN) for the igemm kernel: fill 256 CUs x 2 blocks first, then reuse."""
     bn = 128 if cout % 128 == 0 else 64
@@ -205,7 +250,6 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None
     M = B * Ho * Wo
     if out is None:
         out = torch.empty(B, Ho, Wo, spec.cout, dtype=torch.bfloat16, device=x.device)
-    bm, bn = tile or pick_tile(M, spec.cout)
     if spec.K1 is not None:
         if x2 is None or not x2.is_contiguous():
             raise ValueError("conv2d: fused-shortcut spec needs a contiguous x2")
@@ -213,11 +257,19 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None
     else:
         x2 = None
         src2 = [spec.K, 1, 1, 8, 1]
-    geom = [H, W, pitch, spec.Cc, spec.R, spec.S, spec.stride, spec.pad, Ho, Wo, M,
+    head = [H, W, pitch, spec.Cc, spec.R, spec.S, spec.stride, spec.pad, Ho, Wo, M,
             spec.act, out.stride(2) if out.dim() == 4 else out.stride(0),
-            0 if residual is None else (residual.stride(2) if residual.dim() == 4 else residual.stride(0)),
-            bm, bn] + src2
-    torch.ops.aiko.conv_igemm_out(x, x2, spec.weight, spec.bias, residual, out, geom)
+            0 if residual is None else (residual.stride(2) if residual.dim() == 4 else residual.stride(0))]
+
+    def launch(t):
+        torch.ops.aiko.conv_igemm_out(x, x2, spec.weight, spec.bias, residual, out, head + list(t) + src2)
+
+    if tile is None:
+        key = (M, spec.cout, spec.K, spec.R, spec.S, spec.stride, pitch, spec.K1, residual is not None)
+        tile = _tile_cache.get(key)
+        if tile is None:
+            tile = _tune(key, M, spec.cout, launch) if _tuning else pick_tile(M, spec.cout)
+    launch(tile)
     return out
 
 

@@ -1,0 +1,262 @@
+"""aiko_dashboard: terminal UI over the registrar and the services' EC shares
+(reference ``main/dashboard.py`` + ``dashboard_plugins.py``, asciimatics -> stdlib curses).
+
+Pages: the live services table (ServicesCache) with the selected service's shared variables
+(ECConsumer on its ``/control`` topic) underneath; service history; the selected process's log
+(``{process}/0/log``).  Keys: Up/Down select service, Tab/Enter move between panes, ``e`` edit
+the selected variable (publishes ``(update name value)``), ``L`` cycle the service log level,
+``l`` log page, ``h`` history, ``K`` kill the selected (local) process, ``q`` quit.  GPU
+services show their device, HBM frame-pool occupancy and frames/s when they share them.
+
+``--snapshot`` prints the services (and optionally one service's variables) once and exits —
+the scriptable / testable mode.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import signal
+import threading
+import time
+from collections import deque
+
+from ..control.share import ECConsumer, services_cache_create_singleton
+from ..runtime.process import aiko
+from ..runtime.service import ServiceTopicPath
+from ..utils.sexpr import generate
+
+__all__ = ["Dashboard", "main", "format_services"]
+
+LOG_LEVELS = ["DEBUG", "INFO", "WARNING", "ERROR"]
+HISTORY_LIMIT = 32
+LOG_RING = 128
+
+
+def _field(details, i, key):
+    return details[key] if isinstance(details, dict) else details[i]
+
+
+def format_services(services, width=120):
+    rows = ["Topic                          Name                 Protocol                    Transport Owner    Tags"]
+    for d in services:
+        tp = ServiceTopicPath.parse(_field(d, 0, "topic_path"))
+        topic = tp.terse if tp else str(_field(d, 0, "topic_path"))
+        protocol = str(_field(d, 2, "protocol")).rsplit("/", 1)[-1]
+        tags = _field(d, 5, "tags")
+        tags = " ".join(tags) if isinstance(tags, list) else str(tags)
+        rows.append(f"{topic:30.30} {str(_field(d, 1, 'name')):20.20} {protocol:27.27} "
+                    f"{str(_field(d, 3, 'transport')):9.9} {str(_field(d, 4, 'owner')):8.8} {tags}"[:width])
+    return rows
+
+
+class Dashboard:
+    def __init__(self, history_limit=HISTORY_LIMIT):
+        self.cache = services_cache_create_singleton(aiko.process, True, history_limit)
+        self.selected = 0
+        self.consumer = None
+        self.variables: dict = {}
+        self.selected_topic = None
+        self.log_topic = None
+        self.log: deque = deque(maxlen=LOG_RING)
+        self.lock = threading.Lock()
+        self.page = "services"
+        self.focus = "services"
+        self.var_index = 0
+        self.status = ""
+
+    # ---- data ------------------------------------------------------------------------------
+    def services(self):
+        return list(self.cache.get_services())
+
+    def select(self, details):
+        topic_path = _field(details, 0, "topic_path")
+        if topic_path == self.selected_topic:
+            return
+        if self.consumer is not None:
+            self.consumer.terminate()
+            self.consumer = None
+        self.variables = {}
+        self.selected_topic = topic_path
+        tags = _field(details, 5, "tags")
+        if "ec=true" in (tags if isinstance(tags, list) else str(tags).split()):
+            self.consumer = ECConsumer(aiko.process, 0, self.variables, f"{topic_path}/control")
+        self._follow_log(topic_path)
+
+    def _follow_log(self, topic_path):
+        tp = ServiceTopicPath.parse(topic_path)
+        new = f"{tp.topic_path_process}/0/log" if tp else None
+        if new == self.log_topic:
+            return
+        if self.log_topic:
+            aiko.process.remove_message_handler(self._log_handler, self.log_topic)
+        self.log.clear()
+        self.log_topic = new
+        if new:
+            aiko.process.add_message_handler(self._log_handler, new)
+
+    def _log_handler(self, _aiko, topic, payload):
+        with self.lock:
+            self.log.append(str(payload))
+
+    def edit_variable(self, name, value):
+        if self.selected_topic:
+            aiko.message.publish(f"{self.selected_topic}/control", generate("update", [name, value]))
+
+    def cycle_log_level(self):
+        current = str(self.variables.get("log_level", "INFO")).upper()
+        nxt = LOG_LEVELS[(LOG_LEVELS.index(current) + 1) % len(LOG_LEVELS)] if current in LOG_LEVELS else "INFO"
+        self.edit_variable("log_level", nxt)
+        return nxt
+
+    def kill_selected(self):
+        tp = ServiceTopicPath.parse(self.selected_topic or "")
+        if tp is None:
+            return "no service selected"
+        from ..utils.configuration import get_hostname
+        if tp.hostname != get_hostname():
+            return "can only kill local processes"
+        try:
+            os.kill(int(tp.process_id), signal.SIGKILL)
+            return f"killed {tp.process_id}"
+        except (OSError, ValueError) as exc:
+            return str(exc)
+
+    def flat_variables(self):
+        out = []
+        for k, v in sorted(self.variables.items()):
+            if isinstance(v, dict):
+                out.extend((f"{k}.{sk}", sv) for sk, sv in sorted(v.items()))
+            else:
+                out.append((k, v))
+        return out
+
+    # ---- curses UI -------------------------------------------------------------------------
+    def run_curses(self):
+        import curses
+        curses.wrapper(self._main)
+
+    def _main(self, scr):
+        import curses
+        curses.curs_set(0)
+        scr.timeout(250)
+        while True:
+            self._draw(scr)
+            ch = scr.getch()
+            if ch == -1:
+                continue
+            if ch in (ord("q"), 27):
+                return
+            services = self.services()
+            if ch == curses.KEY_DOWN:
+                if self.focus == "services":
+                    self.selected = min(self.selected + 1, max(0, len(services) - 1))
+                else:
+                    self.var_index = min(self.var_index + 1, max(0, len(self.flat_variables()) - 1))
+            elif ch == curses.KEY_UP:
+                if self.focus == "services":
+                    self.selected = max(0, self.selected - 1)
+                else:
+                    self.var_index = max(0, self.var_index - 1)
+            elif ch in (9, 10, 13):
+                self.focus = "variables" if self.focus == "services" else "services"
+            elif ch == ord("l"):
+                self.page = "log" if self.page != "log" else "services"
+            elif ch == ord("h"):
+                self.page = "history" if self.page != "history" else "services"
+            elif ch == ord("L"):
+                self.status = f"log_level -> {self.cycle_log_level()}"
+            elif ch == ord("K"):
+                self.status = self.kill_selected()
+            elif ch == ord("e") and self.focus == "variables":
+                vars_ = self.flat_variables()
+                if vars_:
+                    name = vars_[self.var_index][0]
+                    value = self._prompt(scr, f"{name} = ")
+                    if value is not None:
+                        self.edit_variable(name, value)
+                        self.status = f"update {name} {value}"
+            if services and self.selected < len(services):
+                from ..runtime import event
+                event.call_soon(self.select, services[self.selected])
+
+    def _prompt(self, scr, text):
+        import curses
+        h, w = scr.getmaxyx()
+        curses.echo()
+        scr.timeout(-1)
+        scr.addstr(h - 1, 0, text[: w - 1])
+        scr.clrtoeol()
+        try:
+            value = scr.getstr(h - 1, len(text), 200).decode()
+        except Exception:
+            value = None
+        curses.noecho()
+        scr.timeout(250)
+        return value or None
+
+    def _draw(self, scr):
+        scr.erase()
+        h, w = scr.getmaxyx()
+        title = f" aiko dashboard (MI355X)  state={self.cache.get_state()}  {aiko.topic_path_process} "
+        scr.addstr(0, 0, title[: w - 1])
+        if self.page == "log":
+            with self.lock:
+                lines = list(self.log)[-(h - 3):]
+            scr.addstr(1, 0, f"log: {self.log_topic}"[: w - 1])
+            for i, line in enumerate(lines):
+                scr.addstr(2 + i, 0, line[: w - 1])
+        elif self.page == "history":
+            rows = format_services(list(self.cache.get_history()), w - 1)
+            for i, row in enumerate(rows[: h - 2]):
+                scr.addstr(1 + i, 0, row[: w - 1])
+        else:
+            rows = format_services(self.services(), w - 1)
+            top = max(3, h // 2)
+            for i, row in enumerate(rows[:top]):
+                attr = 0
+                if i - 1 == self.selected and self.focus == "services":
+                    import curses
+                    attr = curses.A_REVERSE
+                scr.addstr(1 + i, 0, row[: w - 1], attr)
+            scr.addstr(top + 1, 0, "-" * (w - 1))
+            for i, (k, v) in enumerate(self.flat_variables()[: h - top - 4]):
+                import curses
+                attr = curses.A_REVERSE if (self.focus == "variables" and i == self.var_index) else 0
+                scr.addstr(top + 2 + i, 0, f"{k:40.40} {v}"[: w - 1], attr)
+        scr.addstr(h - 1, 0, (f"{self.status}  " + "q quit  arrows select  tab pane  e edit  L level  "
+                              "l log  h history  K kill")[: w - 1])
+        scr.refresh()
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="aiko dashboard")
+    ap.add_argument("--history_limit", "-hl", type=int, default=HISTORY_LIMIT)
+    ap.add_argument("--snapshot", action="store_true", help="print services once and exit")
+    ap.add_argument("--service", default=None, help="(snapshot) also print this service's variables")
+    ap.add_argument("--timeout", type=float, default=5.0)
+    a = ap.parse_args(argv)
+    dash = Dashboard(a.history_limit)
+    if not a.snapshot:
+        dash.run_curses()
+        aiko.process.terminate()
+        return
+    if not dash.cache.wait_ready(a.timeout):
+        print(f"registrar not ready (state={dash.cache.get_state()})")
+    services = dash.services()
+    for row in format_services(services):
+        print(row)
+    if a.service:
+        from ..runtime import event
+        for d in services:
+            if _field(d, 1, "name") == a.service:
+                event.call_soon(dash.select, d).result(5)
+                deadline = time.time() + a.timeout
+                while (dash.consumer is None or dash.consumer.cache_state != "ready") and time.time() < deadline:
+                    time.sleep(0.05)
+                for k, v in dash.flat_variables():
+                    print(f"  {k} = {v}")
+    aiko.process.terminate()
+
+
+if __name__ == "__main__":
+    main()
