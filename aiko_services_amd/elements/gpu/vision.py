@@ -171,5 +171,5 @@ class ClassifierTopK(GpuPipelineElement):
         ev = torch.cuda.Event()
         ev.record()
         result = DeviceResult({"top_prob": hp, "top_index": hi}, ev,
-                              t_submit=t_submit if isinstance(t_submit, float) else None)
+                              t_submit=t_submit if isinstance(t_submit, (float, torch.Tensor)) else None)
         return StreamEvent.OKAY, {"topk": result}

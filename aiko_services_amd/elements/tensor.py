@@ -1,0 +1,70 @@
+"""Device-agnostic tensor PipelineElements: building blocks for data-plane tests and examples
+(pipeline/data parallel runners on CPU with gloo, or on MI355X with RCCL).
+
+* ``TensorSource``  — emits ``x`` = frame_id + arange(size) (float32, shape [batch, size]);
+* ``TensorAffine``  — ``x * scale + offset``;
+* ``TensorReduce``  — ``sum`` over the last dim -> ``y`` [batch];
+* ``TensorDrop``    — DROP_FRAME every ``every``-th frame (stream-state propagation tests).
+"""
+from __future__ import annotations
+
+import torch
+
+from ..pipeline.engine import PipelineElement
+from ..pipeline.stream import StreamEvent
+
+__all__ = ["TensorSource", "TensorAffine", "TensorReduce", "TensorDrop"]
+
+
+class _TensorElement(PipelineElement):
+    PROTOCOL = "tensor:0"
+
+    def __init__(self, context):
+        context.set_protocol(self.PROTOCOL)
+        context.get_implementation("PipelineElement").__init__(self, context)
+        dev, _ = self.get_parameter("device", default=None)
+        deploy = getattr(self.definition, "deploy", None)
+        dev = dev or getattr(deploy, "device", None)
+        if dev is None:
+            dev = f"cuda:{torch.cuda.current_device()}" if torch.cuda.is_available() else "cpu"
+        self.device = torch.device(str(dev).replace("gpu:", "cuda:"))
+
+    def start_stream(self, stream, stream_id):
+        return StreamEvent.OKAY, None
+
+
+class TensorSource(_TensorElement):
+    PROTOCOL = "tensor_source:0"
+
+    def process_frame(self, stream, **kwargs):
+        batch = int(self.get_parameter("batch", 2)[0])
+        size = int(self.get_parameter("size", 8)[0])
+        base = torch.arange(size, dtype=torch.float32, device=self.device)
+        x = (base + float(stream.frame_id)).expand(batch, size).contiguous()
+        return StreamEvent.OKAY, {"x": x}
+
+
+class TensorAffine(_TensorElement):
+    PROTOCOL = "tensor_affine:0"
+
+    def process_frame(self, stream, x):
+        scale = float(self.get_parameter("scale", 1.0)[0])
+        offset = float(self.get_parameter("offset", 0.0)[0])
+        return StreamEvent.OKAY, {"x": x * scale + offset}
+
+
+class TensorReduce(_TensorElement):
+    PROTOCOL = "tensor_reduce:0"
+
+    def process_frame(self, stream, x):
+        return StreamEvent.OKAY, {"y": x.sum(dim=-1)}
+
+
+class TensorDrop(_TensorElement):
+    PROTOCOL = "tensor_drop:0"
+
+    def process_frame(self, stream, x):
+        every = int(self.get_parameter("every", 0)[0])
+        if every and stream.frame_id % every == every - 1:
+            return StreamEvent.DROP_FRAME, {"x": x}
+        return StreamEvent.OKAY, {"x": x}

@@ -92,7 +92,12 @@ class DeviceResult:
 
     @property
     def latency(self):
-        return None if self.t_done is None else self.t_done - self.t_submit
+        if self.t_done is None:
+            return None
+        t = self.t_submit
+        if isinstance(t, torch.Tensor):      # int64 ns stamp carried through a PP stage header
+            t = int(t.reshape(-1)[0]) * 1e-9
+        return self.t_done - t
 
     def __repr__(self):
         shapes = {k: tuple(v.shape) if hasattr(v, "shape") else v for k, v in self.tensors.items()}

@@ -673,6 +673,8 @@ class PipelineImpl(Pipeline):
                 self.frames_completed += 1
                 stream_info = {"stream_id": stream.stream_id, "frame_id": frame_id, "state": stream.state}
                 if stream.queue_response is not None:
+                    if getattr(self, "response_swag", False):   # pipeline-parallel stage hand-off
+                        frame_data_out = dict(frame.swag)
                     stream.queue_response.put((stream_info, frame_data_out))
                 elif stream.topic_response:
                     get_actor_mqtt(stream.topic_response, Pipeline).process_frame_response(stream_info, frame_data_out)

@@ -56,6 +56,22 @@ def definition(batch: int, graph: bool, height: int, width: int) -> dict:
     }
 
 
+def pp_definition(batch: int, graph: bool, height: int, width: int, world: int) -> dict:
+    """BASELINE config 3: decode -> resize/normalise -> ResNet-50 -> post-process, one stage per
+    GPU (``deploy.local.stage`` = i * world // 4, so fewer GPUs fold neighbouring stages)."""
+    d = definition(batch, graph, height, width)
+    d["name"] = "p_resnet50_pp"
+    d["graph"] = ["(SyntheticFrames ImagePreprocess ResNet50Classifier ClassifierTopK)"]
+    pre = {"name": "ImagePreprocess", "input": [{"name": "images", "type": "tensor"}],
+           "output": [{"name": "images", "type": "tensor"}], "parameters": {"image_size": 224},
+           "deploy": {"local": {"module": ELEMENTS}}}
+    d["elements"].insert(1, pre)
+    d["elements"][3]["parameters"]["gather"] = False
+    for i, e in enumerate(d["elements"]):
+        e["deploy"]["local"]["stage"] = i * world // 4
+    return d
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
@@ -66,7 +82,12 @@ def main(argv=None):
     ap.add_argument("--width", type=int, default=224)
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture")
     ap.add_argument("--depth", type=int, default=2, help="batches in flight")
+    ap.add_argument("--parallel", choices=["dp", "pp"], default="dp",
+                    help="dp: every GPU runs the whole pipeline (config 2/headline); "
+                         "pp: one pipeline stage per GPU over RCCL P2P (config 3)")
     a = ap.parse_args(argv)
+    if a.parallel == "pp" and a.height == 224 and a.width == 224 and "--height" not in (argv or sys.argv):
+        a.height, a.width = 480, 640          # config 3 decodes VGA video frames
 
     from aiko_services_amd.parallel import dist as D
     D.init()
@@ -81,6 +102,8 @@ def main(argv=None):
     from aiko_services_amd.pipeline.definition import parse_pipeline_definition_dict
     from aiko_services_amd.pipeline.engine import PipelineImpl
 
+    if a.parallel == "pp":
+        return run_pp(a, device)
     d = parse_pipeline_definition_dict(definition(a.batch, not a.no_graph, a.height, a.width))
     responses: queue.Queue = queue.Queue()
     pipeline = PipelineImpl.create_pipeline("<bench>", d, None, None, "bench", [], 0, None, 3600,
@@ -144,6 +167,77 @@ def main(argv=None):
                        "pipeline": "(SyntheticFrames ResNet50Classifier ClassifierTopK)"},
         }
         print(json.dumps(out), flush=True)
+    D.barrier()
+    D.destroy()
+
+
+def run_pp(a, device):
+    """Config 3: the stages of one pipeline spread over the GPUs; frames/s counted at the last
+    stage (each frame batch is processed once by the whole node)."""
+    from aiko_services_amd.parallel import dist as D
+    from aiko_services_amd.parallel.pipeline_parallel import PipelineParallelRunner
+    from aiko_services_amd.pipeline.definition import parse_pipeline_definition_dict
+    ws, rank = D.world_size(), D.rank()
+    d = parse_pipeline_definition_dict(pp_definition(a.batch, not a.no_graph, a.height, a.width, ws))
+    D.barrier()
+    runner = PipelineParallelRunner(d, device=device, depth=2, stream_id="bench")
+    inflight: deque = deque()
+    latencies: list = []
+
+    def step(record):
+        r = runner.step({})
+        if r is None:
+            return
+        info, out = r
+        if info["state"] != 0:
+            raise RuntimeError(f"pipeline frame failed: {info} {out}")
+        inflight.append((out["topk"], record))
+        while len(inflight) > a.depth:
+            res, rec = inflight.popleft()
+            res.wait()
+            if rec:
+                latencies.append(res.latency)
+
+    def drain(record=True):
+        while inflight:
+            res, rec = inflight.popleft()
+            res.wait()
+            if rec and record:
+                latencies.append(res.latency)
+
+    for _ in range(a.warmup):
+        step(False)
+    drain(False)
+    torch.cuda.synchronize()
+    D.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(True)
+    runner.finish()
+    drain()
+    torch.cuda.synchronize()
+    D.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed, statistics.median(latencies) if latencies else 0.0],
+                     dtype=torch.float64, device=device)
+    D.all_reduce_max(t)
+    elapsed, p50 = float(t[0]), float(t[1])
+    fps = a.batch * a.steps / elapsed
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": round(fps, 1), "unit": "frames/s", "n_gpus": ws,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
+            "data": f"synthetic (random uint8 {a.height}x{a.width} frames generated in HBM; random-init weights)",
+            "p50_latency_ms": round(p50 * 1e3, 3),
+            "config": {"model": "resnet50", "global_batch": a.batch, "seq_len": None,
+                       "image_size": [224, 224], "frame_size": [a.height, a.width],
+                       "per_gpu_batch": a.batch, "parallelism": f"pp{ws}", "hipgraph": not a.no_graph,
+                       "stages": runner.stages,
+                       "pipeline": "(SyntheticFrames ImagePreprocess ResNet50Classifier ClassifierTopK)"},
+        }), flush=True)
     D.barrier()
     D.destroy()
 
