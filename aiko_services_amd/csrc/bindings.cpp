@@ -19,10 +19,19 @@ int aiko_conv_igemm(const void* x, const void* w, const float* bias, const void*
                     int Wo, int M, int Cout, int K, int act, int ldy, int ldr, int bm, int bn,
                     const void* x2, int K1, int H2, int W2, int C2, int stride2, hipStream_t stream);
 int aiko_preprocess(const void* in, void* out, int B, int Hin, int Win, int Ho, int Wo, int Hp,
-                    int Wp, int pad_t, int pad_l, const float* mean, const float* std, int bgr,
-                    hipStream_t stream);
+                    int Wp, int pad_t, int pad_l, int Hc, int Wc, int off_t, int off_l, float fill,
+                    const float* mean, const float* std, int bgr, hipStream_t stream);
 int aiko_maxpool(const void* x, void* y, int B, int H, int W, int C, int Ho, int Wo, int k,
-                 int s, int p, hipStream_t stream);
+                 int s, int p, int ldx, int ldy, hipStream_t stream);
+int aiko_upsample2x(const void* x, void* y, int B, int H, int W, int C, int ldx, int ldy,
+                    hipStream_t stream);
+int aiko_yolo_decode(const void* const* feats, const int* H, const int* W, const int* strides,
+                     const int* ld, int nlev, int B, int nc, int reg_max, void* boxes,
+                     float* scores, int* cls, hipStream_t stream);
+int aiko_topk_nms(const void* boxes, const float* scores, const int* cls, int B, int A,
+                  int max_cand, int max_det, float conf, float iou, float max_wh, float gain,
+                  float pad_l, float pad_t, float img_w, float img_h, float* det, int* count,
+                  hipStream_t stream);
 int aiko_avgpool(const void* x, void* y, int B, int HW, int C, hipStream_t stream);
 int aiko_softmax_topk(const void* logits, float* prob, int* index, int B, int N, int k,
                       hipStream_t stream);
@@ -80,7 +89,7 @@ void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, co
                 "aiko.conv_igemm_out: x2 too small for the output geometry");
     x2ptr = x2->data_ptr();
   }
-  TORCH_CHECK(Cc % 8 == 0 && Cc <= C || (C == 4 && Cc == 32), "aiko.conv_igemm_out: Cc must be a multiple of 8 within the pixel pitch");
+  TORCH_CHECK(Cc % 8 == 0 && (Cc <= C || C == 4), "aiko.conv_igemm_out: Cc must be a multiple of 8 within the pixel pitch (or span pixels of a 4-channel stem input)");
   TORCH_CHECK(Cout % 8 == 0, "aiko.conv_igemm_out: Cout must be a multiple of 8");
   TORCH_CHECK(C % 8 == 0 || (C == 4 && Cc % 8 == 0), "aiko.conv_igemm_out: pixel pitch must keep 16-B alignment");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 &&
@@ -116,9 +125,11 @@ void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, co
   check_launch(rc, "conv_igemm");
 }
 
+// canvas = [Hc, Wc, off_t, off_l, fill]: the frame is resized to (Ho, Wo) and placed at
+// (off_t, off_l) inside an Hc x Wc canvas of colour ``fill`` at (pad_t, pad_l) of ``out``.
 void preprocess_out(const at::Tensor& frames, at::Tensor& out, int64_t Ho, int64_t Wo,
                     int64_t pad_t, int64_t pad_l, at::ArrayRef<double> mean,
-                    at::ArrayRef<double> std, bool bgr) {
+                    at::ArrayRef<double> std, bool bgr, at::ArrayRef<double> canvas) {
   check_cuda(frames, "frames");
   check_cuda(out, "out");
   TORCH_CHECK(frames.scalar_type() == at::kByte && frames.dim() == 4 && frames.size(3) == 3 &&
@@ -128,27 +139,121 @@ void preprocess_out(const at::Tensor& frames, at::Tensor& out, int64_t Ho, int64
                   out.is_contiguous() && out.size(0) == frames.size(0),
               "aiko.preprocess_out: out must be bf16 [B, Hp, Wp, 4] contiguous");
   TORCH_CHECK(mean.size() == 3 && std.size() == 3, "aiko.preprocess_out: mean/std need 3 values");
-  TORCH_CHECK(pad_t + Ho <= out.size(1) && pad_l + Wo <= out.size(2), "aiko.preprocess_out: out too small");
+  int64_t Hc = Ho, Wc = Wo, off_t = 0, off_l = 0;
+  double fill = 0.0;
+  if (!canvas.empty()) {
+    TORCH_CHECK(canvas.size() == 5, "aiko.preprocess_out: canvas = [Hc, Wc, off_t, off_l, fill]");
+    Hc = (int64_t)canvas[0]; Wc = (int64_t)canvas[1];
+    off_t = (int64_t)canvas[2]; off_l = (int64_t)canvas[3]; fill = canvas[4];
+  }
+  TORCH_CHECK(off_t >= 0 && off_l >= 0 && off_t + Ho <= Hc && off_l + Wo <= Wc,
+              "aiko.preprocess_out: image must lie inside the canvas");
+  TORCH_CHECK(pad_t + Hc <= out.size(1) && pad_l + Wc <= out.size(2), "aiko.preprocess_out: out too small");
   float m[3] = {(float)mean[0], (float)mean[1], (float)mean[2]};
   float s[3] = {(float)std[0], (float)std[1], (float)std[2]};
   const int rc = aiko_preprocess(frames.data_ptr(), out.data_ptr(), frames.size(0), frames.size(1),
-                                 frames.size(2), Ho, Wo, out.size(1), out.size(2), pad_t, pad_l, m,
-                                 s, bgr ? 1 : 0, cur_stream());
+                                 frames.size(2), Ho, Wo, out.size(1), out.size(2), pad_t, pad_l,
+                                 Hc, Wc, off_t, off_l, (float)fill, m, s, bgr ? 1 : 0, cur_stream());
   check_launch(rc, "preprocess");
+}
+
+// NHWC bf16 tensor whose channels may be a slice of a wider buffer: returns the pixel pitch
+int64_t pixel_pitch(const at::Tensor& t, const char* op) {
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 && t.dim() == 4, "aiko.", op, ": NHWC bf16 tensors required");
+  const int64_t C = t.size(3), ld = t.stride(2);
+  TORCH_CHECK(t.stride(3) == 1 && t.stride(1) == t.size(2) * ld && t.stride(0) == t.size(1) * t.stride(1) &&
+                  ld % 8 == 0 && C % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              "aiko.", op, ": tensor must be NHWC with unit channel stride, C and pitch multiples of 8");
+  TORCH_CHECK(avail_elems(t) >= (t.size(0) * t.size(1) * t.size(2) - 1) * ld + C, "aiko.", op, ": storage too small");
+  return ld;
 }
 
 void maxpool_out(const at::Tensor& x, at::Tensor& y, int64_t k, int64_t s, int64_t p) {
   check_cuda(x, "x");
   check_cuda(y, "y");
-  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16 &&
-                  x.dim() == 4 && y.dim() == 4 && x.is_contiguous() && y.is_contiguous(),
-              "aiko.maxpool_out: NHWC bf16 contiguous tensors required");
+  const int64_t ldx = pixel_pitch(x, "maxpool_out"), ldy = pixel_pitch(y, "maxpool_out");
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
-  TORCH_CHECK(C % 8 == 0 && y.size(0) == B && y.size(3) == C, "aiko.maxpool_out: bad shapes");
+  TORCH_CHECK(y.size(0) == B && y.size(3) == C, "aiko.maxpool_out: bad shapes");
   const int64_t Ho = (H + 2 * p - k) / s + 1, Wo = (W + 2 * p - k) / s + 1;
   TORCH_CHECK(y.size(1) == Ho && y.size(2) == Wo, "aiko.maxpool_out: y must be [B, ", Ho, ", ", Wo, ", C]");
-  check_launch(aiko_maxpool(x.data_ptr(), y.data_ptr(), B, H, W, C, Ho, Wo, k, s, p, cur_stream()),
+  check_launch(aiko_maxpool(x.data_ptr(), y.data_ptr(), B, H, W, C, Ho, Wo, k, s, p, ldx, ldy,
+                            cur_stream()),
                "maxpool");
+}
+
+void upsample2x_out(const at::Tensor& x, at::Tensor& y) {
+  check_cuda(x, "x");
+  check_cuda(y, "y");
+  const int64_t ldx = pixel_pitch(x, "upsample2x_out"), ldy = pixel_pitch(y, "upsample2x_out");
+  TORCH_CHECK(y.size(0) == x.size(0) && y.size(1) == 2 * x.size(1) && y.size(2) == 2 * x.size(2) &&
+                  y.size(3) == x.size(3),
+              "aiko.upsample2x_out: y must be [B, 2H, 2W, C]");
+  check_launch(aiko_upsample2x(x.data_ptr(), y.data_ptr(), x.size(0), x.size(1), x.size(2), x.size(3),
+                               ldx, ldy, cur_stream()),
+               "upsample2x");
+}
+
+// feats: per level [B, H, W, 4*reg_max + nc] bf16 (channel slices allowed), strides per level
+void yolo_decode_out(at::TensorList feats, at::IntArrayRef strides, int64_t nc, int64_t reg_max,
+                     at::Tensor& boxes, at::Tensor& scores, at::Tensor& cls) {
+  const int nlev = (int)feats.size();
+  TORCH_CHECK(nlev >= 1 && nlev <= 4 && (int)strides.size() == nlev, "aiko.yolo_decode_out: 1..4 levels");
+  TORCH_CHECK(reg_max == 16 && nc % 8 == 0, "aiko.yolo_decode_out: reg_max 16, nc % 8 == 0");
+  const void* ptrs[4] = {nullptr, nullptr, nullptr, nullptr};
+  int H[4] = {0, 0, 0, 0}, W[4] = {1, 1, 1, 1}, st[4] = {1, 1, 1, 1}, ld[4] = {0, 0, 0, 0};
+  const int64_t B = feats[0].size(0);
+  int64_t A = 0;
+  for (int i = 0; i < nlev; ++i) {
+    check_cuda(feats[i], "feat");
+    ld[i] = (int)pixel_pitch(feats[i], "yolo_decode_out");
+    TORCH_CHECK(feats[i].size(0) == B && feats[i].size(3) == 4 * reg_max + nc,
+                "aiko.yolo_decode_out: level channels must be 4*reg_max + nc");
+    ptrs[i] = feats[i].data_ptr();
+    H[i] = feats[i].size(1); W[i] = feats[i].size(2); st[i] = strides[i];
+    A += H[i] * W[i];
+  }
+  check_cuda(boxes, "boxes");
+  check_cuda(scores, "scores");
+  check_cuda(cls, "cls");
+  TORCH_CHECK(boxes.scalar_type() == at::kFloat && boxes.is_contiguous() && boxes.numel() == B * A * 4 &&
+                  scores.scalar_type() == at::kFloat && scores.is_contiguous() && scores.numel() == B * A &&
+                  cls.scalar_type() == at::kInt && cls.is_contiguous() && cls.numel() == B * A,
+              "aiko.yolo_decode_out: outputs boxes fp32 [B, A, 4], scores fp32 [B, A], cls int32 [B, A]");
+  check_launch(aiko_yolo_decode(ptrs, H, W, st, ld, nlev, B, nc, reg_max, boxes.data_ptr(),
+                                scores.data_ptr<float>(), cls.data_ptr<int>(), cur_stream()),
+               "yolo_decode");
+}
+
+// params = [conf, iou, max_wh, gain, pad_l, pad_t, img_w, img_h]
+void topk_nms_out(const at::Tensor& boxes, const at::Tensor& scores, const at::Tensor& cls,
+                  int64_t max_cand, at::ArrayRef<double> params, at::Tensor& det, at::Tensor& count) {
+  check_cuda(boxes, "boxes");
+  check_cuda(scores, "scores");
+  check_cuda(cls, "cls");
+  check_cuda(det, "det");
+  check_cuda(count, "count");
+  TORCH_CHECK(params.size() == 8, "aiko.topk_nms_out: params = [conf, iou, max_wh, gain, pad_l, pad_t, img_w, img_h]");
+  TORCH_CHECK(scores.scalar_type() == at::kFloat && scores.dim() == 2 && scores.is_contiguous(),
+              "aiko.topk_nms_out: scores fp32 [B, A]");
+  const int64_t B = scores.size(0), A = scores.size(1);
+  TORCH_CHECK(A <= 32768, "aiko.topk_nms_out: at most 32768 anchors per image");
+  TORCH_CHECK(boxes.scalar_type() == at::kFloat && boxes.is_contiguous() && boxes.numel() == B * A * 4,
+              "aiko.topk_nms_out: boxes fp32 [B, A, 4]");
+  TORCH_CHECK(cls.scalar_type() == at::kInt && cls.is_contiguous() && cls.numel() == B * A,
+              "aiko.topk_nms_out: cls int32 [B, A]");
+  TORCH_CHECK(det.scalar_type() == at::kFloat && det.dim() == 3 && det.size(0) == B && det.size(2) == 6 &&
+                  det.is_contiguous(),
+              "aiko.topk_nms_out: det fp32 [B, max_det, 6]");
+  const int64_t max_det = det.size(1);
+  TORCH_CHECK(max_cand >= 1 && max_cand <= 1024 && max_det >= 1 && max_det <= 1024,
+              "aiko.topk_nms_out: 1 <= max_candidates, max_det <= 1024");
+  TORCH_CHECK(count.scalar_type() == at::kInt && count.numel() == B && count.is_contiguous(),
+              "aiko.topk_nms_out: count int32 [B]");
+  check_launch(aiko_topk_nms(boxes.data_ptr(), scores.data_ptr<float>(), cls.data_ptr<int>(), B, A,
+                             max_cand, max_det, params[0], params[1], params[2], params[3], params[4],
+                             params[5], params[6], params[7], det.data_ptr<float>(),
+                             count.data_ptr<int>(), cur_stream()),
+               "topk_nms");
 }
 
 void avgpool_out(const at::Tensor& x, at::Tensor& y) {
@@ -183,7 +288,10 @@ void softmax_topk_out(const at::Tensor& logits, at::Tensor& prob, at::Tensor& in
 
 TORCH_LIBRARY(aiko, m) {
   m.def("conv_igemm_out(Tensor x, Tensor? x2, Tensor w, Tensor? bias, Tensor? res, Tensor(a!) y, int[] geom) -> ()");
-  m.def("preprocess_out(Tensor frames, Tensor(a!) out, int Ho, int Wo, int pad_t, int pad_l, float[] mean, float[] std, bool bgr) -> ()");
+  m.def("preprocess_out(Tensor frames, Tensor(a!) out, int Ho, int Wo, int pad_t, int pad_l, float[] mean, float[] std, bool bgr, float[] canvas=[]) -> ()");
+  m.def("upsample2x_out(Tensor x, Tensor(a!) y) -> ()");
+  m.def("yolo_decode_out(Tensor[] feats, int[] strides, int nc, int reg_max, Tensor(a!) boxes, Tensor(b!) scores, Tensor(c!) cls) -> ()");
+  m.def("topk_nms_out(Tensor boxes, Tensor scores, Tensor cls, int max_cand, float[] params, Tensor(a!) det, Tensor(b!) count) -> ()");
   m.def("maxpool_out(Tensor x, Tensor(a!) y, int k, int s, int p) -> ()");
   m.def("avgpool_out(Tensor x, Tensor(a!) y) -> ()");
   m.def("softmax_topk_out(Tensor logits, Tensor(a!) prob, Tensor(b!) index, int k) -> ()");
@@ -193,6 +301,9 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("conv_igemm_out", &conv_igemm_out);
   m.impl("preprocess_out", &preprocess_out);
   m.impl("maxpool_out", &maxpool_out);
+  m.impl("upsample2x_out", &upsample2x_out);
+  m.impl("yolo_decode_out", &yolo_decode_out);
+  m.impl("topk_nms_out", &topk_nms_out);
   m.impl("avgpool_out", &avgpool_out);
   m.impl("softmax_topk_out", &softmax_topk_out);
 }

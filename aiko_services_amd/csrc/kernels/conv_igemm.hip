@@ -33,7 +33,8 @@ struct ConvParams {
   int Cc;               // contiguous channel run per tap (multiple of 8)
   int R, S, stride, pad;
   int Ho, Wo, M, Cout, K;
-  int act;              // 0 none, 1 relu, 2 silu
+  int act;              // bits 0-3: 0 none, 1 relu, 2 silu; bit 4: residual added AFTER the
+                        // activation (YOLO/CSP bottleneck x + silu(conv)) instead of before
   int ldy, ldr;
   // optional second A source (K columns [K1, K)): a 1x1 / stride-s2 conv over x2, used to
   // fuse a ResNet projection shortcut into the block's last conv (K-concatenation)
@@ -273,19 +274,28 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvParams p) {
     float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] += e_bias[e];
-    if (p.res) {
+    const bool post = (p.act & 16) != 0;
+    if (p.res && !post) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         v[2 * e] += __uint_as_float(e_res[i][e] << 16);
         v[2 * e + 1] += __uint_as_float(e_res[i][e] & 0xffff0000u);
       }
     }
-    if (p.act == 1) {
+    const int act = p.act & 15;
+    if (act == 1) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-    } else if (p.act == 2) {
+    } else if (act == 2) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = v[e] / (1.f + __expf(-v[e]));
+    }
+    if (p.res && post) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[2 * e] += __uint_as_float(e_res[i][e] << 16);
+        v[2 * e + 1] += __uint_as_float(e_res[i][e] & 0xffff0000u);
+      }
     }
     u32x4 o;
 #pragma unroll
@@ -324,6 +334,10 @@ extern "C" int aiko_conv_igemm(const void* x, const void* w, const float* bias, 
     conv_igemm_kernel<64, 64><<<grid, block, 0, stream>>>(p);
   } else if (bm == 64 && bn == 128) {
     conv_igemm_kernel<64, 128><<<grid, block, 0, stream>>>(p);
+  } else if (bm == 128 && bn == 32) {
+    conv_igemm_kernel<128, 32><<<grid, block, 0, stream>>>(p);
+  } else if (bm == 256 && bn == 32) {
+    conv_igemm_kernel<256, 32><<<grid, block, 0, stream>>>(p);
   } else {
     return -1;
   }

@@ -1,0 +1,450 @@
+// Detection kernels for gfx950 (YOLOv8 family): nearest upsample into concat slices, the
+// anchor-free DFL box decode, and a fused per-image "top-k candidates + class-aware NMS".
+//
+// topk_nms_kernel — one 1024-thread workgroup per image, everything resident in LDS (160 KB):
+//   1. scores above the confidence threshold -> 32-bit keys (float bits are monotone for
+//      positive floats) in LDS;
+//   2. radix select (4 x 8-bit passes, 256-bin LDS histograms, one wave resolves each pass
+//      with a suffix scan) finds the K-th largest key, K = min(max_candidates, #above conf);
+//   3. deterministic compaction (block-wide exclusive scan, ties -> lowest anchor index) and a
+//      bitonic sort of the <= 1024 candidates by (score desc, index asc);
+//   4. the IoU suppression bitmask (n x ceil(n/64) 64-bit words) is built in LDS by all 16
+//      waves — boxes are offset by class * max_wh so one pass is class-aware — overlaying the
+//      key array that is no longer needed;
+//   5. one wave scans the bitmask 64 candidates at a time: inside a word the suppression chain
+//      is resolved from the diagonal words with wave shuffles, then the kept rows' words are
+//      OR-ed into the later words lane-parallel; stops at max_det;
+//   6. kept boxes are mapped back from letterbox to frame coordinates, clipped, and written
+//      as fixed-size [max_det, 6] rows (x1, y1, x2, y2, score, class) + a count, so results can
+//      be all-gathered over RCCL without a size exchange.
+#include "common.h"
+
+namespace aiko {
+
+// ---------------------------------------------------------------------------------------------
+// Nearest 2x upsample, NHWC bf16 (C % 8 == 0), x / y may be channel slices (pixel pitches
+// ldx / ldy): one thread per 8 channels of an input pixel, one 16-B load -> four 16-B stores.
+__global__ void upsample2x_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int B,
+                                  int H, int W, int C, int ldx, int ldy) {
+  const int C8 = C >> 3;
+  const long total = (long)B * H * W * C8;
+  const int Wo = 2 * W;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int c8 = idx % C8;
+    long t = idx / C8;
+    const int w = t % W; t /= W;
+    const int h = t % H;
+    const int b = t / H;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(x + (((long)b * H + h) * W + w) * ldx + c8 * 8);
+    bf16_t* o = y + (((long)b * 2 * H + 2 * h) * Wo + 2 * w) * ldy + c8 * 8;
+    *reinterpret_cast<u32x4*>(o) = v;
+    *reinterpret_cast<u32x4*>(o + ldy) = v;
+    *reinterpret_cast<u32x4*>(o + (long)Wo * ldy) = v;
+    *reinterpret_cast<u32x4*>(o + (long)Wo * ldy + ldy) = v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// DFL decode: per anchor (all levels, all images) read the 4 x reg_max box logits and the nc
+// class logits of its head pixel -> box xyxy (letterbox pixels), max class score, class id.
+constexpr int kMaxLevels = 4;
+constexpr int kRegMax = 16;   // DFL bins per box side (YOLOv8)
+
+struct DecodeParams {
+  const bf16_t* feat[kMaxLevels];  // [B, H, W, ld] bf16: box logits [0, 4*reg_max), cls after
+  int H[kMaxLevels], W[kMaxLevels], stride[kMaxLevels], ld[kMaxLevels], start[kMaxLevels];
+  int nlev, B, A, nc, reg_max;
+  float4* boxes;   // [B, A]
+  float* scores;   // [B, A]
+  int* cls;        // [B, A]
+};
+
+__global__ void yolo_decode_kernel(DecodeParams p) {
+  const long total = (long)p.B * p.A;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int b = idx / p.A;
+    const int a = idx - (long)b * p.A;
+    int l = 0;
+#pragma unroll
+    for (int i = 1; i < kMaxLevels; ++i)
+      if (i < p.nlev && a >= p.start[i]) l = i;
+    const int r = a - p.start[l];
+    const int h = r / p.W[l], w = r - h * p.W[l];
+    const bf16_t* f = p.feat[l] + (((long)b * p.H[l] + h) * p.W[l] + w) * p.ld[l];
+    float dist[4];
+#pragma unroll
+    for (int side = 0; side < 4; ++side) {
+      const bf16_t* q = f + side * kRegMax;
+      float v[kRegMax];
+#pragma unroll
+      for (int k = 0; k < kRegMax; k += 8) {
+        const u32x4 u = *reinterpret_cast<const u32x4*>(q + k);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[k + 2 * e] = __uint_as_float(u[e] << 16);
+          v[k + 2 * e + 1] = __uint_as_float(u[e] & 0xffff0000u);
+        }
+      }
+      float m = v[0];
+#pragma unroll
+      for (int k = 1; k < kRegMax; ++k) m = fmaxf(m, v[k]);
+      float se = 0.f, sk = 0.f;
+#pragma unroll
+      for (int k = 0; k < kRegMax; ++k) {
+        const float e = __expf(v[k] - m);
+        se += e;
+        sk += e * k;
+      }
+      dist[side] = sk / se;
+    }
+    const bf16_t* c = f + 4 * kRegMax;
+    float best = -INFINITY;
+    int bi = 0;
+    for (int k = 0; k < p.nc; k += 8) {
+      const u32x4 u = *reinterpret_cast<const u32x4*>(c + k);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v0 = __uint_as_float(u[e] << 16), v1 = __uint_as_float(u[e] & 0xffff0000u);
+        if (v0 > best) { best = v0; bi = k + 2 * e; }
+        if (v1 > best) { best = v1; bi = k + 2 * e + 1; }
+      }
+    }
+    const float s = (float)p.stride[l];
+    const float ax = w + 0.5f, ay = h + 0.5f;
+    p.boxes[idx] = make_float4((ax - dist[0]) * s, (ay - dist[1]) * s, (ax + dist[2]) * s,
+                               (ay + dist[3]) * s);
+    p.scores[idx] = 1.f / (1.f + __expf(-best));
+    p.cls[idx] = bi;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+constexpr int kNmsThreads = 1024;
+constexpr int kMaxCand = 1024;
+constexpr int kMaxAnchors = 32768;
+constexpr int kMaskWords = kMaxCand / 64;  // 16
+
+struct NmsParams {
+  const float4* boxes;
+  const float* scores;
+  const int* cls;
+  int A, max_cand, max_det;
+  float conf, iou, max_wh;
+  float gain, pad_l, pad_t, img_w, img_h;  // letterbox -> frame mapping
+  float* det;   // [B, max_det, 6]
+  int* count;   // [B]
+};
+
+__device__ __forceinline__ unsigned long long shfl64(unsigned long long v, int src) {
+  const unsigned lo = __shfl((unsigned)(v & 0xffffffffull), src, 64);
+  const unsigned hi = __shfl((unsigned)(v >> 32), src, 64);
+  return ((unsigned long long)hi << 32) | lo;
+}
+
+__device__ __forceinline__ float box_iou(float4 a, float4 b) {
+  const float iw = fmaxf(0.f, fminf(a.z, b.z) - fmaxf(a.x, b.x));
+  const float ih = fmaxf(0.f, fminf(a.w, b.w) - fmaxf(a.y, b.y));
+  const float inter = iw * ih;
+  const float area_a = (a.z - a.x) * (a.w - a.y), area_b = (b.z - b.x) * (b.w - b.y);
+  return inter / (area_a + area_b - inter);
+}
+
+// block-wide exclusive scan of one int per thread (1024 threads = 16 waves)
+__device__ int block_exclusive_scan(int v, int* sh) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(x, o, 64);
+    if (lane >= o) x += t;
+  }
+  if (lane == 63) sh[wave] = x;
+  __syncthreads();
+  if (wave == 0) {
+    int y = lane < 16 ? sh[lane] : 0;
+    const int own = y;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const int t = __shfl_up(y, o, 64);
+      if (lane >= o) y += t;
+    }
+    if (lane < 16) sh[16 + lane] = y - own;
+  }
+  __syncthreads();
+  return x - v + sh[16 + wave];
+}
+
+__global__ __launch_bounds__(kNmsThreads) void topk_nms_kernel(NmsParams p) {
+  constexpr int REGION0 = kMaxCand * kMaskWords * 8;  // 128 KB: keys, later the IoU bitmask
+  static_assert(REGION0 >= kMaxAnchors * 4, "key array must fit the mask region");
+  __shared__ __attribute__((aligned(16))) unsigned char region0[REGION0];
+  __shared__ unsigned long long ckey[kMaxCand];
+  __shared__ float4 cbox[kMaxCand];
+  __shared__ unsigned hist[256];
+  __shared__ int kept[kMaxCand];
+  __shared__ int sh[40];
+
+  unsigned* keys = reinterpret_cast<unsigned*>(region0);
+  unsigned long long* masks = reinterpret_cast<unsigned long long*>(region0);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x;
+  const int A = p.A;
+  const float* sc = p.scores + (long)b * A;
+  const float4* bx = p.boxes + (long)b * A;
+  const int* cl = p.cls + (long)b * A;
+
+  // 1. keys
+  if (tid == 0) sh[32] = 0;
+  __syncthreads();
+  int cnt = 0;
+  for (int i = tid; i < A; i += kNmsThreads) {
+    const float s = sc[i];
+    const unsigned k = s > p.conf ? __float_as_uint(s) : 0u;
+    keys[i] = k;
+    cnt += k != 0u;
+  }
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+  if (lane == 0) atomicAdd(&sh[32], cnt);
+  __syncthreads();
+  const int total = sh[32];
+  const int K = min(p.max_cand, total);
+
+  int nk = 0;
+  if (K > 0) {
+    // 2. radix select of the K-th largest key
+    unsigned prefix = 0u, pmask = 0u;
+    int remaining = K;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      if (tid < 256) hist[tid] = 0u;
+      __syncthreads();
+      for (int i = tid; i < A; i += kNmsThreads) {
+        const unsigned k = keys[i];
+        if (k != 0u && (k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
+      }
+      __syncthreads();
+      if (wave == 0) {
+        const int s_l = hist[4 * lane] + hist[4 * lane + 1] + hist[4 * lane + 2] + hist[4 * lane + 3];
+        int suf = s_l;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int t = __shfl_down(suf, o, 64);
+          if (lane + o < 64) suf += t;
+        }
+        const int above = suf - s_l;
+        if (above < remaining && suf >= remaining) {
+          int acc = above;
+          for (int j = 3; j >= 0; --j) {
+            const int h = hist[4 * lane + j];
+            acc += h;
+            if (acc >= remaining) {
+              sh[34] = 4 * lane + j;
+              sh[35] = remaining - (acc - h);
+              break;
+            }
+          }
+        }
+      }
+      __syncthreads();
+      prefix |= (unsigned)sh[34] << shift;
+      pmask |= 255u << shift;
+      remaining = sh[35];
+      __syncthreads();
+    }
+    const unsigned T = prefix;
+    const int n_gt = K - remaining;
+
+    // 3. deterministic compaction (contiguous chunks + block scan) and bitonic sort
+    const int chunk = (A + kNmsThreads - 1) / kNmsThreads;
+    const int i0 = tid * chunk, i1 = min(A, i0 + chunk);
+    int gt = 0, eq = 0;
+    for (int i = i0; i < i1; ++i) {
+      const unsigned k = keys[i];
+      gt += k > T;
+      eq += k == T;
+    }
+    const int base = block_exclusive_scan(gt | (eq << 16), sh);
+    int gpos = base & 0xffff, epos = base >> 16;
+    for (int i = i0; i < i1; ++i) {
+      const unsigned k = keys[i];
+      const unsigned long long ck = ((unsigned long long)k << 32) | (0xffffffffu - (unsigned)i);
+      if (k > T) {
+        ckey[gpos++] = ck;
+      } else if (k == T) {
+        if (epos < remaining) ckey[n_gt + epos] = ck;
+        ++epos;
+      }
+    }
+    int NP = 1;
+    while (NP < K) NP <<= 1;
+    if (tid >= K && tid < NP) ckey[tid] = 0ull;
+    __syncthreads();
+    for (int size = 2; size <= NP; size <<= 1) {
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        const int i = tid, j = tid ^ stride;
+        if (i < NP && j > i) {
+          const unsigned long long a = ckey[i], c = ckey[j];
+          const bool desc = (i & size) == 0;
+          if (desc ? (a < c) : (a > c)) {
+            ckey[i] = c;
+            ckey[j] = a;
+          }
+        }
+        __syncthreads();
+      }
+    }
+
+    // 4. class-offset candidate boxes + IoU bitmask (overlays the key array)
+    const int n = K;
+    for (int i = tid; i < n; i += kNmsThreads) {
+      const int idx = (int)(0xffffffffu - (unsigned)(ckey[i] & 0xffffffffull));
+      const float off = cl[idx] * p.max_wh;
+      const float4 q = bx[idx];
+      cbox[i] = make_float4(q.x + off, q.y + off, q.z + off, q.w + off);
+    }
+    __syncthreads();
+    const int W = (n + 63) >> 6;
+    for (int t = tid; t < n * W; t += kNmsThreads) {
+      const int i = t / W, w = t - (t / W) * W;
+      const float4 bi = cbox[i];
+      unsigned long long bits = 0ull;
+      const int j0 = w * 64;
+      for (int jj = 0; jj < 64; ++jj) {
+        const int j = j0 + jj;
+        if (j > i && j < n && box_iou(bi, cbox[j]) > p.iou) bits |= 1ull << jj;
+      }
+      masks[i * kMaskWords + w] = bits;
+    }
+    __syncthreads();
+
+    // 5. greedy scan, 64 candidates per step
+    if (wave == 0) {
+      unsigned long long removed = 0ull;
+      int nkept = 0;
+      for (int w = 0; w < W && nkept < p.max_det; ++w) {
+        unsigned long long cur = shfl64(removed, w);
+        const int row = w * 64 + lane;
+        const unsigned long long diag = row < n ? masks[row * kMaskWords + w] : 0ull;
+        const int left = n - w * 64;
+        const unsigned long long valid = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
+        unsigned long long keep = 0ull;
+        for (int bb = 0; bb < 64; ++bb) {
+          if (!((valid >> bb) & 1ull)) break;
+          const unsigned long long d = shfl64(diag, bb);
+          if (!((cur >> bb) & 1ull)) {
+            keep |= 1ull << bb;
+            cur |= d;
+          }
+        }
+        const int room = p.max_det - nkept;
+        if (__popcll(keep) > room) {
+          unsigned long long trimmed = 0ull, kk = keep;
+          for (int r = 0; r < room; ++r) {
+            const unsigned long long low = kk & (~kk + 1ull);
+            trimmed |= low;
+            kk ^= low;
+          }
+          keep = trimmed;
+        }
+        if ((keep >> lane) & 1ull) {
+          const unsigned long long below = lane ? (keep & ((1ull << lane) - 1ull)) : 0ull;
+          kept[nkept + __popcll(below)] = row;
+        }
+        nkept += __popcll(keep);
+        unsigned long long kk = keep;
+        while (kk) {
+          const int bb = __ffsll((long long)kk) - 1;
+          kk &= kk - 1ull;
+          if (lane > w && lane < W) removed |= masks[(w * 64 + bb) * kMaskWords + lane];
+        }
+      }
+      if (lane == 0) sh[36] = nkept;
+    }
+    __syncthreads();
+    nk = sh[36];
+  }
+
+  // 6. fixed-size output rows in frame coordinates
+  const float inv = 1.f / p.gain;
+  for (int r = tid; r < p.max_det; r += kNmsThreads) {
+    float* o = p.det + ((long)b * p.max_det + r) * 6;
+    if (r < nk) {
+      const unsigned long long ck = ckey[kept[r]];
+      const int idx = (int)(0xffffffffu - (unsigned)(ck & 0xffffffffull));
+      const float4 q = bx[idx];
+      o[0] = fminf(fmaxf((q.x - p.pad_l) * inv, 0.f), p.img_w);
+      o[1] = fminf(fmaxf((q.y - p.pad_t) * inv, 0.f), p.img_h);
+      o[2] = fminf(fmaxf((q.z - p.pad_l) * inv, 0.f), p.img_w);
+      o[3] = fminf(fmaxf((q.w - p.pad_t) * inv, 0.f), p.img_h);
+      o[4] = __uint_as_float((unsigned)(ck >> 32));
+      o[5] = (float)cl[idx];
+    } else {
+      o[0] = o[1] = o[2] = o[3] = o[4] = 0.f;
+      o[5] = -1.f;
+    }
+  }
+  if (tid == 0) p.count[b] = nk;
+}
+
+}  // namespace aiko
+
+static inline int grid_for_d(long total, int block) {
+  long g = (total + block - 1) / block;
+  if (g > 256 * 16) g = 256 * 16;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+extern "C" int aiko_upsample2x(const void* x, void* y, int B, int H, int W, int C, int ldx,
+                               int ldy, hipStream_t stream) {
+  const long total = (long)B * H * W * (C / 8);
+  aiko::upsample2x_kernel<<<grid_for_d(total, 256), 256, 0, stream>>>(
+      static_cast<const aiko::bf16_t*>(x), static_cast<aiko::bf16_t*>(y), B, H, W, C, ldx, ldy);
+  return (int)hipGetLastError();
+}
+
+// levels: nlev entries of (feat ptr, H, W, stride, ld); outputs [B, A]
+extern "C" int aiko_yolo_decode(const void* const* feats, const int* H, const int* W,
+                                const int* strides, const int* ld, int nlev, int B, int nc,
+                                int reg_max, void* boxes, float* scores, int* cls,
+                                hipStream_t stream) {
+  if (nlev < 1 || nlev > aiko::kMaxLevels || reg_max != aiko::kRegMax || nc % 8) return -1;
+  aiko::DecodeParams p;
+  int A = 0;
+  for (int i = 0; i < aiko::kMaxLevels; ++i) {
+    p.feat[i] = i < nlev ? static_cast<const aiko::bf16_t*>(feats[i]) : nullptr;
+    p.H[i] = i < nlev ? H[i] : 0;
+    p.W[i] = i < nlev ? W[i] : 1;
+    p.stride[i] = i < nlev ? strides[i] : 1;
+    p.ld[i] = i < nlev ? ld[i] : 0;
+    p.start[i] = A;
+    if (i < nlev) A += H[i] * W[i];
+  }
+  p.nlev = nlev; p.B = B; p.A = A; p.nc = nc; p.reg_max = reg_max;
+  p.boxes = static_cast<float4*>(boxes);
+  p.scores = scores;
+  p.cls = cls;
+  aiko::yolo_decode_kernel<<<grid_for_d((long)B * A, 256), 256, 0, stream>>>(p);
+  return (int)hipGetLastError();
+}
+
+extern "C" int aiko_topk_nms(const void* boxes, const float* scores, const int* cls, int B, int A,
+                             int max_cand, int max_det, float conf, float iou, float max_wh,
+                             float gain, float pad_l, float pad_t, float img_w, float img_h,
+                             float* det, int* count, hipStream_t stream) {
+  if (A > aiko::kMaxAnchors || max_cand < 1 || max_cand > aiko::kMaxCand || max_det < 1 ||
+      max_det > aiko::kMaxCand)
+    return -1;
+  aiko::NmsParams p;
+  p.boxes = static_cast<const float4*>(boxes);
+  p.scores = scores;
+  p.cls = cls;
+  p.A = A; p.max_cand = max_cand; p.max_det = max_det;
+  p.conf = conf; p.iou = iou; p.max_wh = max_wh;
+  p.gain = gain; p.pad_l = pad_l; p.pad_t = pad_t; p.img_w = img_w; p.img_h = img_h;
+  p.det = det;
+  p.count = count;
+  aiko::topk_nms_kernel<<<B, aiko::kNmsThreads, 0, stream>>>(p);
+  return (int)hipGetLastError();
+}

@@ -5,15 +5,17 @@
 namespace aiko {
 
 // ---------------------------------------------------------------------------------------------
-// uint8 RGB frames [B, Hin, Win, 3] -> bf16 [B, Hp, Wp, 4] normalised ((x/255 - mean) / std),
-// bilinearly resized to (Ho, Wo) (half-pixel centres, like cv2.INTER_LINEAR) and written into
-// the interior of a zero-bordered buffer at offset (pad_t, pad_l).  The 4th channel is zero.
-// This is the fused resize + colour-normalise + layout kernel feeding the ResNet-50 stem.
-// One thread per padded output pixel (8-byte store), border pixels written as zeros so the
-// buffer never needs a separate memset.
+// uint8 RGB frames [B, Hin, Win, 3] -> bf16 [B, Hp, Wp, 4] normalised ((x/255 - mean) / std).
+// The padded buffer holds a "canvas" of Hc x Wc at offset (pad_t, pad_l) — everything outside
+// it is zero (the first conv's zero padding).  Inside the canvas the frame, bilinearly resized
+// to (Ho, Wo) (half-pixel centres, like cv2.INTER_LINEAR), sits at (off_t, off_l); the rest of
+// the canvas is the constant colour ``fill`` (letterbox bars, e.g. 114 for YOLO).  The 4th
+// channel is zero.  ResNet: canvas == image, YOLO: 640x640 canvas with an aspect-preserving
+// image.  One thread per padded output pixel (8-byte store): the buffer never needs a memset.
 __global__ void preprocess_kernel(const uint8_t* __restrict__ in, bf16_t* __restrict__ out,
                                   int B, int Hin, int Win, int Ho, int Wo, int Hp, int Wp,
-                                  int pad_t, int pad_l, float m0, float m1, float m2,
+                                  int pad_t, int pad_l, int Hc, int Wc, int off_t, int off_l,
+                                  float fill, float m0, float m1, float m2,
                                   float is0, float is1, float is2, int bgr) {
   const long total = (long)B * Hp * Wp;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
@@ -22,33 +24,36 @@ __global__ void preprocess_kernel(const uint8_t* __restrict__ in, bf16_t* __rest
     const int rem = idx - (long)b * Hp * Wp;
     const int yp = rem / Wp;
     const int xp = rem - yp * Wp;
-    const int yo = yp - pad_t, xo = xp - pad_l;
+    const int yc = yp - pad_t, xc = xp - pad_l;
     uint2 o = {0u, 0u};
-    if (yo >= 0 && yo < Ho && xo >= 0 && xo < Wo) {
-      float c[3];
-      if (Hin == Ho && Win == Wo) {
-        const uint8_t* px = in + (((long)b * Hin + yo) * Win + xo) * 3;
-        c[0] = px[0]; c[1] = px[1]; c[2] = px[2];
-      } else {
-        const float sy = fmaxf(((yo + 0.5f) * Hin) / Ho - 0.5f, 0.f);
-        const float sx = fmaxf(((xo + 0.5f) * Win) / Wo - 0.5f, 0.f);
-        int y0 = (int)sy, x0 = (int)sx;
-        y0 = min(y0, Hin - 1); x0 = min(x0, Win - 1);
-        const int y1 = min(y0 + 1, Hin - 1), x1 = min(x0 + 1, Win - 1);
-        const float fy = sy - y0, fx = sx - x0;
-        const uint8_t* base = in + (long)b * Hin * Win * 3;
-        const uint8_t* p00 = base + ((long)y0 * Win + x0) * 3;
-        const uint8_t* p01 = base + ((long)y0 * Win + x1) * 3;
-        const uint8_t* p10 = base + ((long)y1 * Win + x0) * 3;
-        const uint8_t* p11 = base + ((long)y1 * Win + x1) * 3;
+    if (yc >= 0 && yc < Hc && xc >= 0 && xc < Wc) {
+      const int yo = yc - off_t, xo = xc - off_l;
+      float c[3] = {fill, fill, fill};
+      if (yo >= 0 && yo < Ho && xo >= 0 && xo < Wo) {
+        if (Hin == Ho && Win == Wo) {
+          const uint8_t* px = in + (((long)b * Hin + yo) * Win + xo) * 3;
+          c[0] = px[0]; c[1] = px[1]; c[2] = px[2];
+        } else {
+          const float sy = fmaxf(((yo + 0.5f) * Hin) / Ho - 0.5f, 0.f);
+          const float sx = fmaxf(((xo + 0.5f) * Win) / Wo - 0.5f, 0.f);
+          int y0 = (int)sy, x0 = (int)sx;
+          y0 = min(y0, Hin - 1); x0 = min(x0, Win - 1);
+          const int y1 = min(y0 + 1, Hin - 1), x1 = min(x0 + 1, Win - 1);
+          const float fy = sy - y0, fx = sx - x0;
+          const uint8_t* base = in + (long)b * Hin * Win * 3;
+          const uint8_t* p00 = base + ((long)y0 * Win + x0) * 3;
+          const uint8_t* p01 = base + ((long)y0 * Win + x1) * 3;
+          const uint8_t* p10 = base + ((long)y1 * Win + x0) * 3;
+          const uint8_t* p11 = base + ((long)y1 * Win + x1) * 3;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const float top = p00[k] + (p01[k] - (float)p00[k]) * fx;
-          const float bot = p10[k] + (p11[k] - (float)p10[k]) * fx;
-          c[k] = top + (bot - top) * fy;
+          for (int k = 0; k < 3; ++k) {
+            const float top = p00[k] + (p01[k] - (float)p00[k]) * fx;
+            const float bot = p10[k] + (p11[k] - (float)p10[k]) * fx;
+            c[k] = top + (bot - top) * fy;
+          }
         }
+        if (bgr) { const float t = c[0]; c[0] = c[2]; c[2] = t; }
       }
-      if (bgr) { const float t = c[0]; c[0] = c[2]; c[2] = t; }
       const float v0 = (c[0] * (1.f / 255.f) - m0) * is0;
       const float v1 = (c[1] * (1.f / 255.f) - m1) * is1;
       const float v2 = (c[2] * (1.f / 255.f) - m2) * is2;
@@ -61,9 +66,11 @@ __global__ void preprocess_kernel(const uint8_t* __restrict__ in, bf16_t* __rest
 
 // ---------------------------------------------------------------------------------------------
 // Max pool (k x k, stride s, pad p) NHWC bf16, C % 8 == 0: one thread per 8 channels of one
-// output pixel (16-byte loads/stores).  Padding never wins (-inf).
+// output pixel (16-byte loads/stores).  Padding never wins (-inf).  ``ldx`` / ``ldy`` are the
+// pixel pitches, so input and output may be channel slices of concat buffers (YOLO SPPF).
 __global__ void maxpool_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int B,
-                               int H, int W, int C, int Ho, int Wo, int k, int s, int p) {
+                               int H, int W, int C, int Ho, int Wo, int k, int s, int p,
+                               int ldx, int ldy) {
   const int C8 = C >> 3;
   const long total = (long)B * Ho * Wo * C8;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
@@ -83,7 +90,7 @@ __global__ void maxpool_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict_
         const int iw = wo * s - p + dx;
         if ((unsigned)iw >= (unsigned)W) continue;
         const u32x4 v = *reinterpret_cast<const u32x4*>(
-            x + (((long)b * H + ih) * W + iw) * C + c8 * 8);
+            x + (((long)b * H + ih) * W + iw) * ldx + c8 * 8);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           m[2 * e] = fmaxf(m[2 * e], __uint_as_float(v[e] << 16));
@@ -94,7 +101,7 @@ __global__ void maxpool_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict_
     u32x4 o;
 #pragma unroll
     for (int e = 0; e < 4; ++e) o[e] = pack2(m[2 * e], m[2 * e + 1]);
-    *reinterpret_cast<u32x4*>(y + idx * 8) = o;
+    *reinterpret_cast<u32x4*>(y + (((long)b * Ho + ho) * Wo + wo) * ldy + c8 * 8) = o;
   }
 }
 
@@ -188,22 +195,23 @@ static inline int grid_for(long total, int block) {
 }
 
 extern "C" int aiko_preprocess(const void* in, void* out, int B, int Hin, int Win, int Ho,
-                               int Wo, int Hp, int Wp, int pad_t, int pad_l, const float* mean,
+                               int Wo, int Hp, int Wp, int pad_t, int pad_l, int Hc, int Wc,
+                               int off_t, int off_l, float fill, const float* mean,
                                const float* std, int bgr, hipStream_t stream) {
   const long total = (long)B * Hp * Wp;
   hipLaunchKernelGGL(aiko::preprocess_kernel, dim3(grid_for(total, 256)), dim3(256), 0, stream,
                      static_cast<const uint8_t*>(in), static_cast<aiko::bf16_t*>(out), B, Hin,
-                     Win, Ho, Wo, Hp, Wp, pad_t, pad_l, mean[0], mean[1], mean[2],
-                     1.f / std[0], 1.f / std[1], 1.f / std[2], bgr);
+                     Win, Ho, Wo, Hp, Wp, pad_t, pad_l, Hc, Wc, off_t, off_l, fill, mean[0],
+                     mean[1], mean[2], 1.f / std[0], 1.f / std[1], 1.f / std[2], bgr);
   return (int)hipGetLastError();
 }
 
 extern "C" int aiko_maxpool(const void* x, void* y, int B, int H, int W, int C, int Ho, int Wo,
-                            int k, int s, int p, hipStream_t stream) {
+                            int k, int s, int p, int ldx, int ldy, hipStream_t stream) {
   const long total = (long)B * Ho * Wo * (C / 8);
   hipLaunchKernelGGL(aiko::maxpool_kernel, dim3(grid_for(total, 256)), dim3(256), 0, stream,
                      static_cast<const aiko::bf16_t*>(x), static_cast<aiko::bf16_t*>(y), B, H, W,
-                     C, Ho, Wo, k, s, p);
+                     C, Ho, Wo, k, s, p, ldx, ldy);
   return (int)hipGetLastError();
 }
 

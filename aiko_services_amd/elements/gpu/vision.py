@@ -6,7 +6,8 @@
 * ``SyntheticFrames`` — the "decode" stage: a batch of ``batch`` uint8 RGB frames of
   ``height`` x ``width`` produced directly in HBM (a rotating pool of ``pool`` random batches,
   like a hardware decoder writing into device memory; no host upload on the hot path).  In a
-  stream it can also run as a frame generator (``frames``, ``rate``).
+  stream it can also run as a frame generator (``frames``, ``rate``).  With ``global: true``
+  only rank ``src`` produces frames — ``world x batch`` of them — for a FrameFanout.
 * ``ImagePreprocess`` — fused bilinear resize + ImageNet normalise + NHWC->padded-4-channel
   layout in one HIP kernel (output: the ResNet stem buffer).
 * ``ResNet50Classifier`` — ResNet-50 on the igemm MFMA kernels; accepts uint8 frames (then
@@ -42,8 +43,18 @@ class SyntheticFrames(GpuPipelineElement):
         self._cursor = 0
 
     def _frames(self):
+        glob = str(self.get_parameter("global", False)[0]).lower() in ("true", "1", "yes")
+        if glob:
+            # data-parallel ingest: rank ``src`` decodes the node's whole batch (N x batch),
+            # the other ranks get theirs from FrameFanout
+            from ...parallel import dist as D
+            if D.rank() != _int(self.get_parameter("src", 0)[0], 0):
+                return None
         if self._pool is None:
             B = _int(self.get_parameter("batch", 1)[0], 1)
+            if glob:
+                from ...parallel import dist as D
+                B *= D.world_size()
             H = _int(self.get_parameter("height", 224)[0], 224)
             W = _int(self.get_parameter("width", 224)[0], 224)
             n = _int(self.get_parameter("pool", 2)[0], 2)

@@ -13,7 +13,7 @@ import torch
 from ..pipeline.engine import PipelineElement
 from ..pipeline.stream import StreamEvent
 
-__all__ = ["TensorSource", "TensorAffine", "TensorReduce", "TensorDrop"]
+__all__ = ["TensorSource", "TensorAffine", "TensorReduce", "TensorDrop", "FrameStats"]
 
 
 class _TensorElement(PipelineElement):
@@ -68,3 +68,18 @@ class TensorDrop(_TensorElement):
         if every and stream.frame_id % every == every - 1:
             return StreamEvent.DROP_FRAME, {"x": x}
         return StreamEvent.OKAY, {"x": x}
+
+
+class FrameStats(_TensorElement):
+    """Stand-in detector for data-plane tests: uint8 frames [B, H, W, 3] -> fixed-size
+    "detections" [B, 1, 6] (per-frame channel means, frame mean, 0) + counts [B] (= 1)."""
+    PROTOCOL = "frame_stats:0"
+
+    def process_frame(self, stream, images):
+        f = images.float()
+        ch = f.mean(dim=(1, 2))                                   # [B, 3]
+        det = torch.zeros(images.shape[0], 1, 6, device=images.device)
+        det[:, 0, :3] = ch
+        det[:, 0, 3] = f.mean(dim=(1, 2, 3))
+        counts = torch.ones(images.shape[0], dtype=torch.int32, device=images.device)
+        return StreamEvent.OKAY, {"detections": det, "counts": counts}

@@ -132,12 +132,13 @@ class GpuPipelineElement(PipelineElement):
 
     def __init__(self, context):
         context.get_implementation("PipelineElement").__init__(self, context)
-        require_gpu()
         deploy = getattr(self.definition, "deploy", None)
         device_spec = getattr(deploy, "device", None)
         device_param, found = self.get_parameter("device")
         if found:
             device_spec = device_param
+        if str(device_spec) != "cpu":       # CPU only when asked for explicitly (gloo tests)
+            require_gpu()
         self.device = parse_device(device_spec)
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)

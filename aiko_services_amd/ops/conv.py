@@ -22,6 +22,7 @@ from dataclasses import dataclass, field
 import torch
 
 ACT_NONE, ACT_RELU, ACT_SILU = 0, 1, 2
+ACT_RESIDUAL_AFTER = 16          # epilogue flag: y = act(acc + b) + residual (CSP bottlenecks)
 _ACTS = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "silu": ACT_SILU}
 
 
@@ -45,6 +46,9 @@ class ConvSpec:
     # second A source (fused 1x1 projection shortcut): K columns [K1, K) read x2
     K1: int | None = None
     stride2: int = 1
+    # stem geometry (kind == "stem"): the real kernel size / padding over the image
+    stem_k: int = 7
+    stem_pad: int = 3
 
     def to(self, device) -> "ConvSpec":
         self.weight = self.weight.to(device)
@@ -58,13 +62,13 @@ class ConvSpec:
 
     def out_hw(self, H: int, W: int) -> tuple[int, int]:
         if self.kind == "stem":
-            return stem_out_hw(H, W)
+            return stem_out_hw(H, W, self.stem_k, self.stride, self.stem_pad)
         return ((H + 2 * self.pad - self.R) // self.stride + 1,
                 (W + 2 * self.pad - self.S) // self.stride + 1)
 
     def flops(self, B: int, H: int, W: int) -> int:
         Ho, Wo = self.out_hw(H, W)
-        k_real = self.cin * self.R * self.S if self.kind != "stem" else 3 * 49
+        k_real = self.cin * self.R * self.S if self.kind != "stem" else 3 * self.stem_k ** 2
         return 2 * B * Ho * Wo * self.cout * k_real
 
 
@@ -129,35 +133,54 @@ def make_linear_spec(w_oi: torch.Tensor, bias: torch.Tensor | None, act=None, de
     return spec
 
 
-# ---- stem (7x7 / stride 2 / pad 3 over 3 channels) ----------------------------------------
+# ---- stems: k x k / stride s over 3 channels, on a pre-padded 4-channel input ------------------
+#
+# The pre-processing kernel writes the image into a zero-bordered [B, Hp, Wp, 4] bf16 buffer.
+# With 4 channels per pixel a run of P pixels of one input row is 4P contiguous elements, so
+# one filter row (k taps) is a single contiguous "channel run" Cc = 4P (P = k rounded up to an
+# even count, keeping Cc a multiple of 8): the stem becomes an implicit GEMM with R = k filter
+# rows, S = 1, pad 0 (the padding is in the buffer) and K = k * Cc.  ResNet 7x7/2: Cc = 32;
+# YOLOv8 3x3/2: Cc = 16, K = 48 -> one 64-wide K block.
 
 STEM_PAD = 3
 
 
-def stem_out_hw(H: int, W: int) -> tuple[int, int]:
-    return (H + 2 * STEM_PAD - 7) // 2 + 1, (W + 2 * STEM_PAD - 7) // 2 + 1
+def stem_out_hw(H: int, W: int, k: int = 7, s: int = 2, p: int = STEM_PAD) -> tuple[int, int]:
+    return (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
 
 
-def stem_geometry(H: int, W: int) -> tuple[int, int]:
-    """(Hp, Wp) of the zero-bordered 4-channel stem input for an HxW image."""
-    Ho, Wo = stem_out_hw(H, W)
-    Hp = max(2 * (Ho - 1) + 8, H + STEM_PAD)
-    Wp = _round_up(max(2 * (Wo - 1) + 8, W + STEM_PAD), 8)
+def _stem_pixels(k: int) -> int:
+    return k + (k & 1)
+
+
+def stem_geometry(H: int, W: int, k: int = 7, s: int = 2, p: int = STEM_PAD) -> tuple[int, int]:
+    """(Hp, Wp) of the zero-bordered 4-channel stem input for an HxW image (image at (p, p))."""
+    Ho, Wo = stem_out_hw(H, W, k, s, p)
+    Hp = max(s * (Ho - 1) + k, H + 2 * p)
+    Wp = _round_up(max(s * (Wo - 1) + _stem_pixels(k), W + 2 * p), 8)
     return Hp, Wp
 
 
-def make_stem_spec(w_oihw: torch.Tensor, bias: torch.Tensor | None, act="relu", device=None) -> ConvSpec:
-    """Pack a [Cout, 3, 7, 7] stem weight: K = 8 rows x 32 (= 8 pixels x 4 channels)."""
+def make_stem_spec(w_oihw: torch.Tensor, bias: torch.Tensor | None, act="relu", device=None,
+                   stride: int = 2, pad: int | None = None) -> ConvSpec:
+    """Pack a [Cout, 3, k, k] stem weight as k filter rows x (P pixels x 4 channels)."""
     cout, cin, R, S = w_oihw.shape
-    assert (cin, R, S) == (3, 7, 7), "stem packing expects a 7x7 conv over 3 channels"
-    w = torch.zeros(cout, 8, 8, 4, dtype=torch.float32)  # [o][r][s(pixel)][c]
-    w[:, :7, :7, :3] = w_oihw.permute(0, 2, 3, 1).float()
-    packed = w.reshape(cout, 256).to(torch.bfloat16).contiguous()
+    assert cin == 3 and R == S, "stem packing expects a square conv over 3 channels"
+    k = R
+    P = _stem_pixels(k)
+    cc = 4 * P
+    K = _round_up(k * cc, 64)
+    w = torch.zeros(cout, k, P, 4, dtype=torch.float32)  # [o][r][s(pixel)][c]
+    w[:, :, :k, :3] = w_oihw.permute(0, 2, 3, 1).float()
+    packed = torch.zeros(cout, K, dtype=torch.float32)
+    packed[:, :k * cc] = w.reshape(cout, k * cc)
+    packed = packed.to(torch.bfloat16).contiguous()
     ref_w = w_oihw.to(torch.bfloat16).float().contiguous()
     spec = ConvSpec(weight=packed, bias=None if bias is None else bias.float().contiguous(),
-                    cin=3, cout=cout, R=8, S=1, stride=2, pad=0, Cc=32, act=_act(act),
+                    cin=3, cout=cout, R=k, S=1, stride=stride, pad=0, Cc=cc, act=_act(act),
                     kind="stem", ref_weight=ref_w,
-                    ref_bias=None if bias is None else bias.float().clone())
+                    ref_bias=None if bias is None else bias.float().clone(),
+                    stem_k=k, stem_pad=(k // 2) if pad is None else pad)
     return spec.to(device) if device is not None else spec
 
 
@@ -166,6 +189,7 @@ def _round_up(v: int, m: int) -> int:
 
 
 TILES = ((128, 128), (128, 64), (64, 128), (64, 64))
+NARROW_TILES = ((128, 32), (256, 32), (64, 64), (128, 64))   # Cout <= 32 (YOLO stems / heads)
 _tile_cache: dict = {}          # geometry key -> (bm, bn), filled by autotune()
 _tuning = False
 
@@ -192,7 +216,7 @@ def tile_cache() -> dict:
 
 
 def _tune(key, M, cout, launch):
-    cands = TILES
+    cands = NARROW_TILES if cout <= 32 else TILES
     best, best_t = None, None
     for t in cands:
         launch(t)  # warm
@@ -212,6 +236,8 @@ def _tune(key, M, cout, launch):
 
 def pick_tile(M: int, cout: int) -> tuple[int, int]:
     """Block tile (BM, BN) for the igemm kernel: fill 256 CUs x 2 blocks first, then reuse."""
+    if cout <= 32:
+        return (256, 32) if math.ceil(M / 256) >= 512 else (128, 32)
     bn = 128 if cout % 128 == 0 else 64
     bm = 128
     tiles = math.ceil(M / bm) * math.ceil(cout / bn)
@@ -225,7 +251,8 @@ def pick_tile(M: int, cout: int) -> tuple[int, int]:
 
 def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None,
            out: torch.Tensor | None = None, tile: tuple[int, int] | None = None,
-           image_hw: tuple[int, int] | None = None, x2: torch.Tensor | None = None) -> torch.Tensor:
+           image_hw: tuple[int, int] | None = None, x2: torch.Tensor | None = None,
+           residual_after_act: bool = False) -> torch.Tensor:
     """NHWC bf16 conv with fused bias / residual / activation on the MFMA igemm kernel.
 
     ``x`` is ``[B, H, W, C]`` — possibly a channel-slice view of a wider buffer (the pixel
@@ -242,7 +269,7 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None
     if spec.kind == "stem":
         if image_hw is None:
             raise ValueError("conv2d: stem conv needs image_hw")
-        Ho, Wo = stem_out_hw(*image_hw)
+        Ho, Wo = spec.out_hw(*image_hw)
     else:
         if C < spec.Cc and pitch < spec.Cc:
             raise ValueError(f"conv2d: input has {C} channels, spec expects {spec.Cc}")
@@ -257,15 +284,16 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None
     else:
         x2 = None
         src2 = [spec.K, 1, 1, 8, 1]
+    act = spec.act | (ACT_RESIDUAL_AFTER if (residual is not None and residual_after_act) else 0)
     head = [H, W, pitch, spec.Cc, spec.R, spec.S, spec.stride, spec.pad, Ho, Wo, M,
-            spec.act, out.stride(2) if out.dim() == 4 else out.stride(0),
+            act, out.stride(2) if out.dim() == 4 else out.stride(0),
             0 if residual is None else (residual.stride(2) if residual.dim() == 4 else residual.stride(0))]
 
     def launch(t):
         torch.ops.aiko.conv_igemm_out(x, x2, spec.weight, spec.bias, residual, out, head + list(t) + src2)
 
     if tile is None:
-        key = (M, spec.cout, spec.K, spec.R, spec.S, spec.stride, pitch, spec.K1, residual is not None)
+        key = (M, spec.cout, spec.K, spec.R, spec.S, spec.stride, pitch, spec.K1, residual is not None, spec.Cc)
         tile = _tile_cache.get(key)
         if tile is None:
             tile = _tune(key, M, spec.cout, launch) if _tuning else pick_tile(M, spec.cout)

@@ -5,22 +5,43 @@ import torch
 
 from .conv import STEM_PAD, stem_geometry
 
+YOLO_MEAN = (0.0, 0.0, 0.0)
+YOLO_STD = (1.0, 1.0, 1.0)
+
 IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)
 
 
 def preprocess_frames(frames: torch.Tensor, size: tuple[int, int] = (224, 224),
                       mean=IMAGENET_MEAN, std=IMAGENET_STD, bgr: bool = False,
-                      out: torch.Tensor | None = None) -> torch.Tensor:
+                      out: torch.Tensor | None = None, stem: tuple[int, int, int] = (7, 2, STEM_PAD),
+                      canvas: tuple | None = None) -> torch.Tensor:
     """uint8 ``[B, H, W, 3]`` frames -> bilinear resize to ``size`` + normalise -> the
-    zero-bordered ``[B, Hp, Wp, 4]`` bf16 stem buffer (image at offset (3, 3))."""
+    zero-bordered ``[B, Hp, Wp, 4]`` bf16 input of a ``stem`` = (k, stride, pad) conv.
+
+    ``canvas`` = (Hc, Wc, off_t, off_l, fill): place the resized frame at (off_t, off_l) of an
+    Hc x Wc canvas filled with colour ``fill`` (letterbox, see :func:`letterbox_geometry`);
+    by default the canvas is the resized frame itself.  The canvas sits at (pad, pad)."""
     B = frames.shape[0]
     Ho, Wo = size
-    Hp, Wp = stem_geometry(Ho, Wo)
+    k, s, p = stem
+    Hc, Wc = (canvas[0], canvas[1]) if canvas else (Ho, Wo)
+    Hp, Wp = stem_geometry(Hc, Wc, k, s, p)
     if out is None:
         out = torch.empty(B, Hp, Wp, 4, dtype=torch.bfloat16, device=frames.device)
-    torch.ops.aiko.preprocess_out(frames, out, Ho, Wo, STEM_PAD, STEM_PAD, list(mean), list(std), bgr)
+    torch.ops.aiko.preprocess_out(frames, out, Ho, Wo, p, p, list(mean), list(std), bgr,
+                                  [float(v) for v in canvas] if canvas else [])
     return out
+
+
+def letterbox_geometry(h: int, w: int, new_shape: int | tuple[int, int] = 640):
+    """Aspect-preserving resize into a ``new_shape`` canvas, centred (YOLO "letterbox",
+    auto=False, scale-up allowed): returns (Ho, Wo, off_t, off_l, gain)."""
+    nh, nw = (new_shape, new_shape) if isinstance(new_shape, int) else new_shape
+    r = min(nh / h, nw / w)
+    Wo, Ho = int(round(w * r)), int(round(h * r))
+    dw, dh = (nw - Wo) / 2, (nh - Ho) / 2
+    return Ho, Wo, int(round(dh - 0.1)), int(round(dw - 0.1)), r
 
 
 def maxpool2d(x: torch.Tensor, k: int = 3, s: int = 2, p: int = 1,

@@ -56,6 +56,30 @@ def definition(batch: int, graph: bool, height: int, width: int) -> dict:
     }
 
 
+DETECT = "aiko_services_amd.elements.gpu.detect"
+
+
+def yolo_definition(batch: int, graph: bool, height: int, width: int, fanout: str) -> dict:
+    """BASELINE config 4: ingest rank decodes the node's frames, RCCL fan-out, YOLOv8-n +
+    NMS kernels per GPU, RCCL all-gather of fixed-size detections."""
+    def el(name, module, inputs, outputs, params):
+        return {"name": name, "input": [{"name": n, "type": "tensor"} for n in inputs],
+                "output": [{"name": n, "type": "tensor"} for n in outputs],
+                "parameters": params, "deploy": {"local": {"module": module}}}
+    return {
+        "version": 0, "name": "p_yolov8n_dp", "runtime": "python",
+        "graph": ["(SyntheticFrames FrameFanout YoloDetector DetectionsGather)"], "parameters": {},
+        "elements": [
+            el("SyntheticFrames", ELEMENTS, [], ["images", "t_submit"],
+               {"batch": batch, "height": height, "width": width, "pool": 2, "global": True}),
+            el("FrameFanout", DETECT, ["images"], ["images"],
+               {"mode": fanout, "batch": batch, "height": height, "width": width}),
+            el("YoloDetector", DETECT, ["images"], ["detections", "counts"], {"graph": graph, "scale": "n"}),
+            el("DetectionsGather", DETECT, ["detections", "counts", "t_submit"], ["detections"], {}),
+        ],
+    }
+
+
 def pp_definition(batch: int, graph: bool, height: int, width: int, world: int) -> dict:
     """BASELINE config 3: decode -> resize/normalise -> ResNet-50 -> post-process, one stage per
     GPU (``deploy.local.stage`` = i * world // 4, so fewer GPUs fold neighbouring stages)."""
@@ -82,12 +106,19 @@ def main(argv=None):
     ap.add_argument("--width", type=int, default=224)
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture")
     ap.add_argument("--depth", type=int, default=2, help="batches in flight")
+    ap.add_argument("--model", choices=["resnet50", "yolov8n"], default="resnet50",
+                    help="resnet50: headline ResNet-50 pipeline (config 2/3); yolov8n: config 4")
+    ap.add_argument("--fanout", choices=["scatter", "broadcast"], default="scatter",
+                    help="(yolov8n) RCCL fan-out of the ingest rank's frame batch")
     ap.add_argument("--parallel", choices=["dp", "pp"], default="dp",
                     help="dp: every GPU runs the whole pipeline (config 2/headline); "
                          "pp: one pipeline stage per GPU over RCCL P2P (config 3)")
     a = ap.parse_args(argv)
-    if a.parallel == "pp" and a.height == 224 and a.width == 224 and "--height" not in (argv or sys.argv):
-        a.height, a.width = 480, 640          # config 3 decodes VGA video frames
+    explicit_hw = "--height" in (argv or sys.argv)
+    if (a.parallel == "pp" or a.model == "yolov8n") and not explicit_hw:
+        a.height, a.width = 480, 640          # configs 3/4 decode VGA video frames
+    if a.model == "yolov8n" and "--batch" not in (argv or sys.argv):
+        a.batch = 64
 
     from aiko_services_amd.parallel import dist as D
     D.init()
@@ -104,7 +135,15 @@ def main(argv=None):
 
     if a.parallel == "pp":
         return run_pp(a, device)
-    d = parse_pipeline_definition_dict(definition(a.batch, not a.no_graph, a.height, a.width))
+    if a.model == "yolov8n":
+        d = parse_pipeline_definition_dict(yolo_definition(a.batch, not a.no_graph, a.height, a.width, a.fanout))
+        result_key, model_cfg = "detections", {"model": "yolov8n", "image_size": [640, 640],
+                                               "frame_size": [a.height, a.width], "fanout": a.fanout,
+                                               "pipeline": d.graph[0]}
+    else:
+        d = parse_pipeline_definition_dict(definition(a.batch, not a.no_graph, a.height, a.width))
+        result_key, model_cfg = "topk", {"model": "resnet50", "image_size": [a.height, a.width],
+                                         "pipeline": "(SyntheticFrames ResNet50Classifier ClassifierTopK)"}
     responses: queue.Queue = queue.Queue()
     pipeline = PipelineImpl.create_pipeline("<bench>", d, None, None, "bench", [], 0, None, 3600,
                                             queue_response=responses)
@@ -119,7 +158,7 @@ def main(argv=None):
         info, out = responses.get_nowait()
         if info["state"] != 0:
             raise RuntimeError(f"pipeline frame failed: {info} {out}")
-        inflight.append((out["topk"], record))
+        inflight.append((out[result_key], record))
         while len(inflight) > a.depth:
             res, rec = inflight.popleft()
             res.wait()
@@ -159,12 +198,10 @@ def main(argv=None):
             "metric": METRIC, "value": round(fps, 1), "unit": "frames/s", "n_gpus": ws,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-            "data": "synthetic (random uint8 224x224 frames generated in HBM; random-init weights)",
+            "data": f"synthetic (random uint8 {a.height}x{a.width} frames generated in HBM; random-init weights)",
             "p50_latency_ms": round(p50 * 1e3, 3),
-            "config": {"model": "resnet50", "global_batch": ws * a.batch, "seq_len": None,
-                       "image_size": [a.height, a.width], "per_gpu_batch": a.batch,
-                       "parallelism": f"dp{ws}", "hipgraph": not a.no_graph,
-                       "pipeline": "(SyntheticFrames ResNet50Classifier ClassifierTopK)"},
+            "config": dict({"global_batch": ws * a.batch, "seq_len": None, "per_gpu_batch": a.batch,
+                            "parallelism": f"dp{ws}", "hipgraph": not a.no_graph}, **model_cfg),
         }
         print(json.dumps(out), flush=True)
     D.barrier()

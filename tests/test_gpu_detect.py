@@ -1,0 +1,139 @@
+"""Detection kernels + YOLOv8 on MI355X vs plain PyTorch fp32 references (BASELINE config 4)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def test_upsample2x_into_slice(native):
+    from aiko_services_amd.ops import detect as DT
+    x = torch.randn(2, 5, 7, 48, device=DEV).to(torch.bfloat16)
+    big = torch.zeros(2, 10, 14, 80, dtype=torch.bfloat16, device=DEV)
+    DT.upsample2x(x[..., 16:48], out=big[..., 48:80])
+    ref = torch.nn.functional.interpolate(x[..., 16:48].permute(0, 3, 1, 2).float(), scale_factor=2,
+                                          mode="nearest").permute(0, 2, 3, 1)
+    assert torch.equal(big[..., 48:].float(), ref)
+    assert big[..., :48].abs().max().item() == 0
+
+
+def test_maxpool_slices(native):
+    from aiko_services_amd.ops import vision as V
+    cat = torch.randn(3, 20, 20, 128, device=DEV).to(torch.bfloat16)
+    V.maxpool2d(cat[..., :32], 5, 1, 2, out=cat[..., 32:64])
+    ref = torch.nn.functional.max_pool2d(cat[..., :32].permute(0, 3, 1, 2).float(), 5, 1, 2)
+    assert torch.equal(cat[..., 32:64].permute(0, 3, 1, 2).float(), ref)
+
+
+@pytest.mark.parametrize("cout", [16, 32, 144])
+def test_conv_narrow_tiles_and_post_act_residual(native, cout):
+    from aiko_services_amd.ops import conv as C
+    from aiko_services_amd.ops import reference as R
+    g = torch.Generator().manual_seed(cout)
+    x = torch.randn(2, 40, 40, 48, generator=g).to(DEV, torch.bfloat16)
+    w = torch.randn(cout, 32, 3, 3, generator=g) / 17
+    b = torch.randn(cout, generator=g) * 0.1
+    spec = C.make_conv_spec(w, b, pad=1, act="silu", device=DEV)
+    res = torch.randn(2, 40, 40, cout, generator=g).to(DEV, torch.bfloat16)
+    ref = R.conv_ref(x[..., 8:40].permute(0, 3, 1, 2).float(), spec, res.permute(0, 3, 1, 2).float(),
+                     residual_after_act=True)
+    tiles = [(128, 32), (256, 32), (64, 64)] if cout <= 32 else [(128, 64), (64, 128)]
+    for t in tiles:
+        y = C.conv2d(x[..., 8:40], spec, residual=res, residual_after_act=True, tile=t)
+        assert _rel_err(y.permute(0, 3, 1, 2), ref) < 1e-2, t
+
+
+def test_letterbox_stem(native):
+    from aiko_services_amd.models.yolov8 import YOLOv8
+    from aiko_services_amd.ops import reference as R
+    m = YOLOv8("n", device=DEV)
+    frames = torch.randint(0, 256, (2, 480, 640, 3), dtype=torch.uint8, device=DEV)
+    pre = m.preprocess(frames)
+    Ho, Wo, top, left, gain = m.letterbox((480, 640))
+    assert (Ho, Wo, top, left) == (480, 640, 80, 0)
+    canvas = torch.full((2, 3, 640, 640), 114.0 / 255, device=DEV)
+    canvas[:, :, top:top + Ho, left:left + Wo] = frames.permute(0, 3, 1, 2).float() / 255
+    assert _rel_err(pre[:, 1:641, 1:641, :3].permute(0, 3, 1, 2), canvas) < 5e-3
+    assert pre[:, 0].abs().max().item() == 0 and pre[:, :, 0].abs().max().item() == 0
+    y = torch.ops.aiko  # noqa: F841
+    from aiko_services_amd.ops import conv as C
+    a0 = C.conv2d(pre, m.l0, image_hw=(640, 640))
+    ref = R.conv_ref(canvas.to(torch.bfloat16).float(), m.l0)
+    assert a0.shape == (2, 320, 320, 16)
+    assert _rel_err(a0.permute(0, 3, 1, 2), ref) < 1e-2
+
+
+def test_yolo_decode(native):
+    from aiko_services_amd.ops import detect as DT
+    from aiko_services_amd.ops import reference as R
+    g = torch.Generator().manual_seed(5)
+    feats = [(torch.randn(2, s, s, 144, generator=g) * 2).to(DEV, torch.bfloat16) for s in (16, 8, 4)]
+    boxes, scores, cls = DT.yolo_decode(feats, (8, 16, 32), 80)
+    rb, rs, rc = R.yolo_decode_ref([f.permute(0, 3, 1, 2) for f in feats], (8, 16, 32), 80)
+    assert torch.allclose(boxes, rb, atol=1e-2, rtol=1e-4)
+    assert torch.allclose(scores, rs, atol=1e-5)
+    assert (cls == rc).float().mean().item() > 0.999
+
+
+def _random_dets(B, A, g, n_centers=40):
+    centers = torch.rand(B, n_centers, 2, generator=g) * 600
+    pick = torch.randint(0, n_centers, (B, A), generator=g)
+    c = torch.gather(centers, 1, pick[..., None].expand(B, A, 2)) + torch.randn(B, A, 2, generator=g) * 6
+    wh = 20 + torch.rand(B, A, 2, generator=g) * 60
+    boxes = torch.cat([c - wh / 2, c + wh / 2], -1)
+    scores = (torch.rand(B, A, generator=g) * 256).floor() / 256      # many exact ties
+    cls = torch.randint(0, 3, (B, A), generator=g, dtype=torch.int32)
+    return boxes.to(DEV), scores.to(DEV), cls.to(DEV)
+
+
+@pytest.mark.parametrize("A,conf,max_cand,max_det", [(8400, 0.25, 1024, 300), (8400, 0.97, 1024, 300),
+                                                     (2000, 0.1, 256, 50), (33, 0.0, 1024, 300)])
+def test_topk_nms_matches_reference(native, A, conf, max_cand, max_det):
+    from aiko_services_amd.ops import detect as DT
+    from aiko_services_amd.ops import reference as R
+    g = torch.Generator().manual_seed(A + max_det)
+    B = 3
+    boxes, scores, cls = _random_dets(B, A, g)
+    det, count = DT.topk_nms(boxes, scores, cls, conf=conf, iou=0.5, max_candidates=max_cand,
+                             max_det=max_det)
+    torch.cuda.synchronize()
+    for b in range(B):
+        keep = R.nms_ref(boxes[b], scores[b], cls[b], conf, 0.5, max_cand, max_det)
+        n = int(count[b])
+        assert n == keep.numel(), (b, n, keep.numel())
+        ref = torch.cat([boxes[b][keep].clamp(min=0), scores[b][keep, None], cls[b][keep, None].float()], 1)
+        assert torch.allclose(det[b, :n], ref, atol=1e-4), b
+        assert (det[b, n:, 5] == -1).all()
+
+
+def test_yolov8n_heads_match_reference(native):
+    from aiko_services_amd.models.yolov8 import YOLOv8
+    m = YOLOv8("n", device=DEV)
+    frames = torch.randint(0, 256, (2, 480, 640, 3), dtype=torch.uint8, device=DEV)
+    outs = m.head_outputs(m.preprocess(frames))
+    refs = m.reference_head_outputs(frames)
+    for o, r in zip(outs, refs):
+        o = o.permute(0, 3, 1, 2).float()
+        cos = torch.nn.functional.cosine_similarity(o.flatten(), r.flatten(), dim=0).item()
+        assert cos > 0.99, cos
+
+
+def test_yolov8n_detect_end_to_end(native):
+    from aiko_services_amd.models.yolov8 import YOLOv8
+    m = YOLOv8("n", device=DEV)
+    frames = torch.randint(0, 256, (4, 480, 640, 3), dtype=torch.uint8, device=DEV)
+    det, count = m.detect(frames)
+    torch.cuda.synchronize()
+    assert det.shape == (4, 300, 6) and count.shape == (4,)
+    for b in range(4):
+        n = int(count[b])
+        assert 0 <= n <= 300
+        d = det[b, :n]
+        if n:
+            assert (d[:, 4] > 0.25).all() and (d[:, 4][:-1] >= d[:, 4][1:]).all()
+            assert (d[:, 0] >= 0).all() and (d[:, 2] <= 640).all() and (d[:, 3] <= 480).all()
