@@ -28,6 +28,15 @@ int aiko_upsample2x(const void* x, void* y, int B, int H, int W, int C, int ldx,
 int aiko_yolo_decode(const void* const* feats, const int* H, const int* W, const int* strides,
                      const int* ld, int nlev, int B, int nc, int reg_max, void* boxes,
                      float* scores, int* cls, hipStream_t stream);
+int aiko_gemm_fp8(const void* a, const void* b, const float* sa, const float* sb, const float* bias,
+                  const void* res, void* y, int M, int N, int K, int lda, int ldy, int ldr, int act,
+                  int bm, int bn, hipStream_t stream);
+int aiko_rownorm_quant(const void* x, int ldx, const float* gamma, const float* beta, float eps,
+                       void* yb, int ldyb, void* q, int ldq, float* qs, int M, int D, hipStream_t stream);
+int aiko_attn_fwd(const void* q, const void* k, const void* v, void* o, int ldq, int ldk, int ldv,
+                  int ldo, int B, int H, int T, int Tpad, int dh, float scale, hipStream_t stream);
+int aiko_logmel(const float* audio, int B, int N, const float* mel, int n_mels, int n_fft, int hop,
+                int F, float* logmel, int* gmax, void* dst, int rows, int pad, int ld, hipStream_t stream);
 int aiko_topk_nms(const void* boxes, const float* scores, const int* cls, int B, int A,
                   int max_cand, int max_det, float conf, float iou, float max_wh, float gain,
                   float pad_l, float pad_t, float img_w, float img_h, float* det, int* count,
@@ -284,6 +293,137 @@ void softmax_topk_out(const at::Tensor& logits, at::Tensor& prob, at::Tensor& in
                "softmax_topk");
 }
 
+// ---- transformer / fp8 ------------------------------------------------------------------------
+
+int64_t row_pitch(const at::Tensor& t, int64_t cols, const char* op, const char* name) {
+  TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1 && t.size(1) == cols && t.stride(0) >= cols,
+              "aiko.", op, ": ", name, " must be a row-major [rows, ", cols, "] matrix (row slices / column slices allowed)");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0 && (t.stride(0) * t.element_size()) % 16 == 0,
+              "aiko.", op, ": ", name, " rows must be 16-byte aligned");
+  TORCH_CHECK(avail_elems(t) >= (t.size(0) - 1) * t.stride(0) + cols, "aiko.", op, ": ", name, " storage too small");
+  return t.stride(0);
+}
+
+// y = act(sa[m] * sb[n] * (A @ B^T) + bias) + residual ; A fp8 [M, K] (uint8 storage), B fp8 [N, K]
+void gemm_fp8_out(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& b, const at::Tensor& sb,
+                  const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& res,
+                  at::Tensor& y, int64_t act, int64_t bm, int64_t bn) {
+  for (const at::Tensor* t : {&a, &sa, &b, &sb, (const at::Tensor*)&y}) check_cuda(*t, "operand");
+  TORCH_CHECK(a.element_size() == 1 && b.element_size() == 1, "aiko.gemm_fp8_out: A and B must be 1-byte fp8 storage");
+  TORCH_CHECK(y.scalar_type() == at::kBFloat16, "aiko.gemm_fp8_out: y must be bf16");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(K % 128 == 0 && b.dim() == 2 && b.size(1) == K && b.is_contiguous(),
+              "aiko.gemm_fp8_out: K must be a multiple of 128 and B [N, K] contiguous");
+  TORCH_CHECK(N % 8 == 0, "aiko.gemm_fp8_out: N must be a multiple of 8");
+  const int64_t lda = row_pitch(a, K, "gemm_fp8_out", "A");
+  const int64_t ldy = row_pitch(y, N, "gemm_fp8_out", "y");
+  TORCH_CHECK(y.size(0) == M, "aiko.gemm_fp8_out: y must have M rows");
+  TORCH_CHECK(sa.scalar_type() == at::kFloat && sa.numel() >= M && sa.is_contiguous() &&
+                  sb.scalar_type() == at::kFloat && sb.numel() == N && sb.is_contiguous(),
+              "aiko.gemm_fp8_out: scales fp32 sa [M], sb [N]");
+  const float* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    check_cuda(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == N && bias->is_contiguous(), "aiko.gemm_fp8_out: bias fp32 [N]");
+    bp = bias->data_ptr<float>();
+  }
+  const void* rp = nullptr;
+  int64_t ldr = 0;
+  if (res.has_value() && res->defined()) {
+    check_cuda(*res, "residual");
+    TORCH_CHECK(res->scalar_type() == at::kBFloat16 && res->size(0) == M, "aiko.gemm_fp8_out: residual bf16 [M, N]");
+    ldr = row_pitch(*res, N, "gemm_fp8_out", "residual");
+    rp = res->data_ptr();
+  }
+  TORCH_CHECK(lda * M < INT_MAX * 2L, "aiko.gemm_fp8_out: A too large");
+  check_launch(aiko_gemm_fp8(a.data_ptr(), b.data_ptr(), sa.data_ptr<float>(), sb.data_ptr<float>(), bp, rp,
+                             y.data_ptr(), M, N, K, lda, ldy, ldr, act, bm, bn, cur_stream()),
+               "gemm_fp8");
+}
+
+// LayerNorm (gamma/beta given) and/or per-row fp8 quantisation of bf16 rows x [M, D]
+void rownorm_quant_out(const at::Tensor& x, const c10::optional<at::Tensor>& gamma,
+                       const c10::optional<at::Tensor>& beta, double eps,
+                       const c10::optional<at::Tensor>& yb, const c10::optional<at::Tensor>& q,
+                       const c10::optional<at::Tensor>& qs) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16, "aiko.rownorm_quant_out: x must be bf16");
+  const int64_t M = x.size(0), D = x.size(1);
+  TORCH_CHECK(D % 8 == 0 && D <= 8192, "aiko.rownorm_quant_out: D % 8 == 0, D <= 8192");
+  const int64_t ldx = row_pitch(x, D, "rownorm_quant_out", "x");
+  const float *g = nullptr, *be = nullptr;
+  if (gamma.has_value() && gamma->defined()) {
+    TORCH_CHECK(beta.has_value() && beta->defined(), "aiko.rownorm_quant_out: gamma needs beta");
+    check_cuda(*gamma, "gamma");
+    check_cuda(*beta, "beta");
+    TORCH_CHECK(gamma->scalar_type() == at::kFloat && beta->scalar_type() == at::kFloat && gamma->numel() == D &&
+                    beta->numel() == D && gamma->is_contiguous() && beta->is_contiguous(),
+                "aiko.rownorm_quant_out: gamma/beta fp32 [D]");
+    g = gamma->data_ptr<float>();
+    be = beta->data_ptr<float>();
+  }
+  void* yp = nullptr;
+  int64_t ldyb = 0;
+  if (yb.has_value() && yb->defined()) {
+    check_cuda(*yb, "yb");
+    TORCH_CHECK(yb->scalar_type() == at::kBFloat16 && yb->size(0) == M, "aiko.rownorm_quant_out: yb bf16 [M, D]");
+    ldyb = row_pitch(*yb, D, "rownorm_quant_out", "yb");
+    yp = yb->data_ptr();
+  }
+  void* qp = nullptr;
+  float* sp = nullptr;
+  int64_t ldq = 0;
+  if (q.has_value() && q->defined()) {
+    TORCH_CHECK(qs.has_value() && qs->defined(), "aiko.rownorm_quant_out: q needs qs");
+    check_cuda(*q, "q");
+    check_cuda(*qs, "qs");
+    TORCH_CHECK(q->element_size() == 1 && q->size(0) == M, "aiko.rownorm_quant_out: q fp8 [M, D]");
+    ldq = row_pitch(*q, D, "rownorm_quant_out", "q");
+    TORCH_CHECK(qs->scalar_type() == at::kFloat && qs->numel() >= M && qs->is_contiguous(), "aiko.rownorm_quant_out: qs fp32 [M]");
+    qp = q->data_ptr();
+    sp = qs->data_ptr<float>();
+  }
+  TORCH_CHECK(yp || qp, "aiko.rownorm_quant_out: nothing to write");
+  check_launch(aiko_rownorm_quant(x.data_ptr(), ldx, g, be, (float)eps, yp, ldyb, qp, ldq, sp, M, D, cur_stream()),
+               "rownorm_quant");
+}
+
+// q/k/v/o: [B*Tpad, >= H*64] row-major (column slices of a fused QKV buffer allowed)
+void attn_fwd_out(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& o,
+                  int64_t B, int64_t H, int64_t T, int64_t Tpad, double scale) {
+  for (const at::Tensor* t : {&q, &k, &v, (const at::Tensor*)&o}) {
+    check_cuda(*t, "q/k/v/o");
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16, "aiko.attn_fwd_out: bf16 tensors required");
+    TORCH_CHECK(t->size(0) == B * Tpad, "aiko.attn_fwd_out: tensors need B*Tpad rows");
+    row_pitch(*t, H * 64, "attn_fwd_out", "q/k/v/o");
+  }
+  TORCH_CHECK(T >= 1 && T <= Tpad, "aiko.attn_fwd_out: 1 <= T <= Tpad");
+  check_launch(aiko_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), q.stride(0), k.stride(0),
+                             v.stride(0), o.stride(0), B, H, T, Tpad, 64, (float)scale, cur_stream()),
+               "attn_fwd");
+}
+
+// audio fp32 [B, N] -> bf16 log-mel rows [B*rows, n_mels] (frame t at row b*rows + pad + t)
+void logmel_out(const at::Tensor& audio, const at::Tensor& mel, int64_t n_fft, int64_t hop, int64_t F,
+                at::Tensor& work, at::Tensor& gmax, at::Tensor& dst, int64_t rows, int64_t pad) {
+  for (const at::Tensor* t : {&audio, &mel, (const at::Tensor*)&work, (const at::Tensor*)&gmax, (const at::Tensor*)&dst})
+    check_cuda(*t, "logmel operand");
+  TORCH_CHECK(audio.scalar_type() == at::kFloat && audio.dim() == 2 && audio.is_contiguous(), "aiko.logmel_out: audio fp32 [B, N]");
+  const int64_t B = audio.size(0), N = audio.size(1), n_mels = mel.size(0);
+  TORCH_CHECK(mel.scalar_type() == at::kFloat && mel.is_contiguous() && mel.size(1) == n_fft / 2 + 1,
+              "aiko.logmel_out: mel filters fp32 [n_mels, n_fft/2+1]");
+  TORCH_CHECK(N > n_fft / 2 && F >= 1 && (F - 1) * hop - n_fft / 2 < N, "aiko.logmel_out: bad frame count");
+  TORCH_CHECK(work.scalar_type() == at::kFloat && work.numel() >= B * F * n_mels, "aiko.logmel_out: work fp32 [B*F*n_mels]");
+  TORCH_CHECK(gmax.scalar_type() == at::kInt && gmax.numel() >= B, "aiko.logmel_out: gmax int32 [B]");
+  TORCH_CHECK(dst.scalar_type() == at::kBFloat16 && dst.dim() == 2 && dst.size(1) == n_mels && dst.stride(1) == 1 &&
+                  dst.size(0) == B * rows && rows >= F + pad,
+              "aiko.logmel_out: dst bf16 [B*rows, n_mels]");
+  check_launch(aiko_logmel(audio.data_ptr<float>(), B, N, mel.data_ptr<float>(), n_mels, n_fft, hop, F,
+                           work.data_ptr<float>(), gmax.data_ptr<int>(), dst.data_ptr(), rows, pad, dst.stride(0),
+                           cur_stream()),
+               "logmel");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(aiko, m) {
@@ -294,6 +434,10 @@ TORCH_LIBRARY(aiko, m) {
   m.def("topk_nms_out(Tensor boxes, Tensor scores, Tensor cls, int max_cand, float[] params, Tensor(a!) det, Tensor(b!) count) -> ()");
   m.def("maxpool_out(Tensor x, Tensor(a!) y, int k, int s, int p) -> ()");
   m.def("avgpool_out(Tensor x, Tensor(a!) y) -> ()");
+  m.def("gemm_fp8_out(Tensor a, Tensor sa, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!) y, int act, int bm, int bn) -> ()");
+  m.def("rownorm_quant_out(Tensor x, Tensor? gamma, Tensor? beta, float eps, Tensor(a!)? yb, Tensor(b!)? q, Tensor(c!)? qs) -> ()");
+  m.def("attn_fwd_out(Tensor q, Tensor k, Tensor v, Tensor(a!) o, int B, int H, int T, int Tpad, float scale) -> ()");
+  m.def("logmel_out(Tensor audio, Tensor mel, int n_fft, int hop, int F, Tensor(a!) work, Tensor(b!) gmax, Tensor(c!) dst, int rows, int pad) -> ()");
   m.def("softmax_topk_out(Tensor logits, Tensor(a!) prob, Tensor(b!) index, int k) -> ()");
 }
 
@@ -306,4 +450,8 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("topk_nms_out", &topk_nms_out);
   m.impl("avgpool_out", &avgpool_out);
   m.impl("softmax_topk_out", &softmax_topk_out);
+  m.impl("gemm_fp8_out", &gemm_fp8_out);
+  m.impl("rownorm_quant_out", &rownorm_quant_out);
+  m.impl("attn_fwd_out", &attn_fwd_out);
+  m.impl("logmel_out", &logmel_out);
 }

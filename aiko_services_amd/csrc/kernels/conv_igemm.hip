@@ -33,7 +33,7 @@ struct ConvParams {
   int Cc;               // contiguous channel run per tap (multiple of 8)
   int R, S, stride, pad;
   int Ho, Wo, M, Cout, K;
-  int act;              // bits 0-3: 0 none, 1 relu, 2 silu; bit 4: residual added AFTER the
+  int act;              // bits 0-3: 0 none, 1 relu, 2 silu, 3 gelu(erf); bit 4: residual added AFTER the
                         // activation (YOLO/CSP bottleneck x + silu(conv)) instead of before
   int ldy, ldr;
   // optional second A source (K columns [K1, K)): a 1x1 / stride-s2 conv over x2, used to
@@ -42,8 +42,16 @@ struct ConvParams {
   int K1, H2, W2, C2, stride2;
 };
 
+// Occupancy per tile shape (waves per SIMD = resident 256-thread blocks per CU), bounded by LDS
+// (2-deep ring + epilogue tile) and by the VGPR cap the launch bound imposes (512 / w):
+// narrow / small tiles are latency-bound on low-K layers and need more resident blocks.
 template <int BM, int BN>
-__global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvParams p) {
+constexpr int conv_occupancy() {
+  return (BM * BN <= 64 * 64 || (BM == 128 && BN == 32)) ? 4 : (BM * BN <= 128 * 64 ? 3 : 2);
+}
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256, (conv_occupancy<BM, BN>())) void conv_igemm_kernel(ConvParams p) {
   constexpr int BK = 64;
   constexpr int WM = BM / 2, WN = BN / 2;      // per-wave tile
   constexpr int MI = WM / 16, NI = WN / 16;    // 16x16 MFMA tiles per wave
@@ -289,6 +297,9 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(ConvParams p) {
     } else if (act == 2) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = v[e] / (1.f + __expf(-v[e]));
+    } else if (act == 3) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
     }
     if (p.res && post) {
 #pragma unroll

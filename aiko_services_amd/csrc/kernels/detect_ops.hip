@@ -219,9 +219,23 @@ __global__ __launch_bounds__(kNmsThreads) void topk_nms_kernel(NmsParams p) {
     for (int shift = 24; shift >= 0; shift -= 8) {
       if (tid < 256) hist[tid] = 0u;
       __syncthreads();
-      for (int i = tid; i < A; i += kNmsThreads) {
-        const unsigned k = keys[i];
-        if (k != 0u && (k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
+      for (int i0 = 0; i0 < A; i0 += kNmsThreads) {   // wave-uniform trip count (ballots below)
+        const int i = i0 + tid;
+        const unsigned k = i < A ? keys[i] : 0u;
+        const bool live = k != 0u && (k & pmask) == prefix;
+        const unsigned bin = (k >> shift) & 255u;
+        // scores cluster: most live keys of a wave share a bin -> one aggregated LDS atomic
+        const unsigned long long lm = __ballot(live);
+        if (lm) {
+          const int leader = __ffsll((long long)lm) - 1;
+          const unsigned lbin = __shfl(bin, leader, 64);
+          const unsigned long long same = __ballot(live && bin == lbin);
+          if (same == lm) {
+            if (lane == leader) atomicAdd(&hist[lbin], (unsigned)__popcll(lm));
+          } else if (live) {
+            atomicAdd(&hist[bin], 1u);
+          }
+        }
       }
       __syncthreads();
       if (wave == 0) {
@@ -305,14 +319,17 @@ __global__ __launch_bounds__(kNmsThreads) void topk_nms_kernel(NmsParams p) {
     }
     __syncthreads();
     const int W = (n + 63) >> 6;
+    // lanes of a wave take consecutive ROWS of one word column: the inner loop's cbox[j] read
+    // is then a broadcast (consecutive words per lane would be 1 KB apart: one LDS bank)
     for (int t = tid; t < n * W; t += kNmsThreads) {
-      const int i = t / W, w = t - (t / W) * W;
-      const float4 bi = cbox[i];
+      const int w = t / n, i = t - (t / n) * n;
       unsigned long long bits = 0ull;
       const int j0 = w * 64;
-      for (int jj = 0; jj < 64; ++jj) {
-        const int j = j0 + jj;
-        if (j > i && j < n && box_iou(bi, cbox[j]) > p.iou) bits |= 1ull << jj;
+      if (j0 + 63 > i) {                       // words left of the diagonal stay zero
+        const float4 bi = cbox[i];
+        const int jb = max(j0, i + 1), je = min(j0 + 64, n);
+        for (int j = jb; j < je; ++j)
+          if (box_iou(bi, cbox[j]) > p.iou) bits |= 1ull << (j - j0);
       }
       masks[i * kMaskWords + w] = bits;
     }

@@ -1,0 +1,348 @@
+// FP8 (OCP e4m3fn) GEMM for CDNA4 (gfx950) on the block-scaled MFMA
+// v_mfma_scale_f32_16x16x128_f8f6f4 — twice the bf16 MFMA rate per clock.
+//
+//   y[m, n] = act( sa[m] * sb[n] * sum_k A[m, k] * B[n, k] + bias[n] ) (+ residual[m, n])
+//
+// A: activations [M][lda] fp8, one fp32 scale per row (dynamic per-token quantisation, written
+// by the LayerNorm / quantise kernels); B: weights [N][K] fp8, one fp32 scale per output
+// channel (quantised once at load).  The MX block scales of the instruction are set to 1.0
+// (E8M0 127): per-row/per-channel scales are exact in the fp32 epilogue and keep the MX rate.
+//
+// Tiling mirrors the bf16 igemm: 256 threads = 4 waves (2 x 2), block tile BM x BN x 128
+// (one 128-byte K block = 8 16-B pieces per row), register-staged 2-deep LDS ring, pieces
+// XOR-swizzled by (row & 7) so each lane's two ds_read_b128 per fragment are conflict-free,
+// XCD-aware block remap, fp32 epilogue staged through padded LDS (bias, GELU, residual add,
+// 16-byte bf16 stores).  For 16x16x128 every lane holds 32 consecutive K bytes of one row
+// (row = lane & 15, K range 32 * (lane >> 4)) for both operands, so A and B pair element for
+// element whatever the instruction's internal k order within the range.
+#include "common.h"
+
+namespace aiko {
+
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+
+struct Fp8GemmParams {
+  const uint8_t* a;     // [M][lda]
+  const uint8_t* b;     // [N][K]
+  const float* sa;      // [M]
+  const float* sb;      // [N]
+  const float* bias;    // [N] or nullptr
+  const bf16_t* res;    // [M][ldr] or nullptr (added after the activation)
+  bf16_t* y;            // [M][ldy]
+  int M, N, K, lda, ldy, ldr;
+  int act;              // 0 none, 1 relu, 2 silu, 3 gelu (erf)
+};
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+}
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256, 2) void gemm_fp8_kernel(Fp8GemmParams p) {
+  constexpr int BK = 128;                      // bytes == fp8 elements
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int MI = WM / 16, NI = WN / 16;
+  constexpr int APT = BM / 32, BPT = BN / 32;  // 16-B pieces per thread per K block
+  constexpr int STAGE_BYTES = (BM + BN) * BK;
+  constexpr int CPAD = 4;
+  constexpr int EPI_BYTES = BM * (BN + CPAD) * 4;
+  constexpr int RING_BYTES = 2 * STAGE_BYTES;
+  constexpr int LDS_BYTES = EPI_BYTES > RING_BYTES ? EPI_BYTES : RING_BYTES;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int ntn = (p.N + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
+
+  const int piece = tid & 7, prow = tid >> 3;
+  long a_off[APT];
+  bool a_ok[APT];
+#pragma unroll
+  for (int i = 0; i < APT; ++i) {
+    const int m = m0 + prow + 32 * i;
+    a_ok[i] = m < p.M;
+    a_off[i] = (long)(a_ok[i] ? m : 0) * p.lda + piece * 16;
+  }
+  long b_off[BPT];
+  bool b_ok[BPT];
+#pragma unroll
+  for (int i = 0; i < BPT; ++i) {
+    const int n = n0 + prow + 32 * i;
+    b_ok[i] = n < p.N;
+    b_off[i] = (long)(b_ok[i] ? n : 0) * p.K + piece * 16;
+  }
+
+  u32x4 ra[APT], rb[BPT];
+  auto load_global = [&](int kb) {
+    const int k0 = kb * BK;
+#pragma unroll
+    for (int i = 0; i < APT; ++i)
+      ra[i] = a_ok[i] ? *reinterpret_cast<const u32x4*>(p.a + a_off[i] + k0) : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < BPT; ++i)
+      rb[i] = b_ok[i] ? *reinterpret_cast<const u32x4*>(p.b + b_off[i] + k0) : u32x4{0u, 0u, 0u, 0u};
+  };
+  auto store_lds = [&](int slot) {
+    unsigned char* As = smem + slot * STAGE_BYTES;
+    unsigned char* Bs = As + BM * BK;
+#pragma unroll
+    for (int i = 0; i < APT; ++i) {
+      const int row = prow + 32 * i;
+      *reinterpret_cast<u32x4*>(As + row * BK + ((piece ^ (row & 7)) << 4)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      const int row = prow + 32 * i;
+      *reinterpret_cast<u32x4*>(Bs + row * BK + ((piece ^ (row & 7)) << 4)) = rb[i];
+    }
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nkb = p.K / BK;
+  load_global(0);
+  store_lds(0);
+  __syncthreads();
+  const int fr = lane & 15, fg = lane >> 4;   // fragment row, K group (32 bytes each)
+
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int cur = kb & 1;
+    if (kb + 1 < nkb) load_global(kb + 1);
+    const unsigned char* As = smem + cur * STAGE_BYTES;
+    const unsigned char* Bs = As + BM * BK;
+    i32x8 af[MI], bfr[NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int row = wr * WM + i * 16 + fr;
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(As + row * BK + (((2 * fg) ^ (row & 7)) << 4));
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(As + row * BK + (((2 * fg + 1) ^ (row & 7)) << 4));
+      af[i] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int row = wc * WN + j * 16 + fr;
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(Bs + row * BK + (((2 * fg) ^ (row & 7)) << 4));
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(Bs + row * BK + (((2 * fg + 1) ^ (row & 7)) << 4));
+      bfr[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0,
+                                                                      0, 127, 0, 127);
+    if (kb + 1 < nkb) store_lds(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue ----
+  float* Cs = reinterpret_cast<float*>(smem);
+  constexpr int LDC = BN + CPAD;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int col = wc * WN + j * 16 + fr;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Cs[(wr * WM + i * 16 + fg * 4 + e) * LDC + col] = acc[i][j][e];
+    }
+  __syncthreads();
+  constexpr int CPR = BN / 8, CHUNKS = BM * CPR, CPT = CHUNKS / 256, E_ROWS = 256 / CPR;
+  static_assert(CHUNKS % 256 == 0, "whole chunks per thread");
+  const int e_cc = tid % CPR, e_row0 = tid / CPR;
+  const int e_n = n0 + e_cc * 8;
+  if (e_n >= p.N) return;
+  float cs[8], cb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    cs[e] = p.sb[e_n + e];
+    cb[e] = p.bias ? p.bias[e_n + e] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int row = e_row0 + E_ROWS * i;
+    const int m = m0 + row;
+    if (m >= p.M) continue;
+    const float rs = p.sa[m];
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = Cs[row * LDC + e_cc * 8 + e] * rs * cs[e] + cb[e];
+    if (p.act == 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    } else if (p.act == 2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = v[e] / (1.f + __expf(-v[e]));
+    } else if (p.act == 3) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+    }
+    if (p.res) {
+      const u32x4 r = *reinterpret_cast<const u32x4*>(p.res + (long)m * p.ldr + e_n);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[2 * e] += __uint_as_float(r[e] << 16);
+        v[2 * e + 1] += __uint_as_float(r[e] & 0xffff0000u);
+      }
+    }
+    u32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = pack2(v[2 * e], v[2 * e + 1]);
+    *reinterpret_cast<u32x4*>(p.y + (long)m * p.ldy + e_n) = o;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Row-wise LayerNorm and/or fp8 quantisation, one wave per row (wave64 reductions):
+//   z = gamma ? (x - mean) * rstd * gamma + beta : x
+//   yb (optional) = bf16(z);  q (optional) = e4m3(z / s), s = amax(|z|) / 448 per row.
+// Rows are read once with 16-byte loads and kept in registers (D <= 64 * 8 * MAXC).
+template <int MAXC>
+__global__ __launch_bounds__(256) void rownorm_quant_kernel(
+    const bf16_t* __restrict__ x, int ldx, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, bf16_t* __restrict__ yb, int ldyb,
+    uint8_t* __restrict__ q, int ldq, float* __restrict__ qs, int M, int D) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int nchunk = D >> 3;
+  const bf16_t* src = x + (long)row * ldx;
+  float v[MAXC][8];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nchunk) {
+      const u32x4 u = *reinterpret_cast<const u32x4*>(src + ch * 8);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[c][2 * e] = __uint_as_float(u[e] << 16);
+        v[c][2 * e + 1] = __uint_as_float(u[e] & 0xffff0000u);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[c][e] = 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += v[c][e];
+  }
+  if (gamma) {
+    const float mean = wave_sum(s) / D;
+    float ss = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      if (lane + 64 * c < nchunk) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = v[c][e] - mean;
+          ss += d * d;
+        }
+      }
+    }
+    const float rstd = rsqrtf(wave_sum(ss) / D + eps);
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < nchunk) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          v[c][e] = (v[c][e] - mean) * rstd * gamma[ch * 8 + e] + beta[ch * 8 + e];
+      }
+    }
+  }
+  if (yb) {
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < nchunk) {
+        u32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = pack2(v[c][2 * e], v[c][2 * e + 1]);
+        *reinterpret_cast<u32x4*>(yb + (long)row * ldyb + ch * 8) = o;
+      }
+    }
+  }
+  if (q) {
+    float amax = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+      if (lane + 64 * c < nchunk) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[c][e]));
+      }
+    amax = wave_max(amax);
+    const float scale = amax > 0.f ? amax / 448.f : 1.f;
+    const float inv = 1.f / scale;
+    if (lane == 0) qs[row] = scale;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < nchunk) {
+        unsigned w0 = 0u, w1 = 0u;
+        w0 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[c][0] * inv, -448.f), 448.f),
+                                             fminf(fmaxf(v[c][1] * inv, -448.f), 448.f), w0, false);
+        w0 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[c][2] * inv, -448.f), 448.f),
+                                             fminf(fmaxf(v[c][3] * inv, -448.f), 448.f), w0, true);
+        w1 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[c][4] * inv, -448.f), 448.f),
+                                             fminf(fmaxf(v[c][5] * inv, -448.f), 448.f), w1, false);
+        w1 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[c][6] * inv, -448.f), 448.f),
+                                             fminf(fmaxf(v[c][7] * inv, -448.f), 448.f), w1, true);
+        *reinterpret_cast<uint2*>(q + (long)row * ldq + ch * 8) = make_uint2(w0, w1);
+      }
+    }
+  }
+}
+
+}  // namespace aiko
+
+extern "C" int aiko_gemm_fp8(const void* a, const void* b, const float* sa, const float* sb,
+                             const float* bias, const void* res, void* y, int M, int N, int K,
+                             int lda, int ldy, int ldr, int act, int bm, int bn, hipStream_t stream) {
+  using namespace aiko;
+  Fp8GemmParams p;
+  p.a = static_cast<const uint8_t*>(a);
+  p.b = static_cast<const uint8_t*>(b);
+  p.sa = sa; p.sb = sb; p.bias = bias;
+  p.res = static_cast<const bf16_t*>(res);
+  p.y = static_cast<bf16_t*>(y);
+  p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldy = ldy; p.ldr = ldr; p.act = act;
+  dim3 grid(((M + bm - 1) / bm) * ((N + bn - 1) / bn)), block(256);
+  if (bm == 128 && bn == 128) {
+    gemm_fp8_kernel<128, 128><<<grid, block, 0, stream>>>(p);
+  } else if (bm == 128 && bn == 64) {
+    gemm_fp8_kernel<128, 64><<<grid, block, 0, stream>>>(p);
+  } else if (bm == 64 && bn == 64) {
+    gemm_fp8_kernel<64, 64><<<grid, block, 0, stream>>>(p);
+  } else if (bm == 64 && bn == 128) {
+    gemm_fp8_kernel<64, 128><<<grid, block, 0, stream>>>(p);
+  } else {
+    return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int aiko_rownorm_quant(const void* x, int ldx, const float* gamma, const float* beta,
+                                  float eps, void* yb, int ldyb, void* q, int ldq, float* qs,
+                                  int M, int D, hipStream_t stream) {
+  using namespace aiko;
+  dim3 grid((M + 3) / 4), block(256);
+  const bf16_t* xp = static_cast<const bf16_t*>(x);
+  bf16_t* yp = static_cast<bf16_t*>(yb);
+  uint8_t* qp = static_cast<uint8_t*>(q);
+  if (D <= 64 * 8 * 2) {
+    rownorm_quant_kernel<2><<<grid, block, 0, stream>>>(xp, ldx, gamma, beta, eps, yp, ldyb, qp, ldq, qs, M, D);
+  } else if (D <= 64 * 8 * 6) {
+    rownorm_quant_kernel<6><<<grid, block, 0, stream>>>(xp, ldx, gamma, beta, eps, yp, ldyb, qp, ldq, qs, M, D);
+  } else if (D <= 64 * 8 * 16) {
+    rownorm_quant_kernel<16><<<grid, block, 0, stream>>>(xp, ldx, gamma, beta, eps, yp, ldyb, qp, ldq, qs, M, D);
+  } else {
+    return -1;
+  }
+  return (int)hipGetLastError();
+}

@@ -21,9 +21,9 @@ from dataclasses import dataclass, field
 
 import torch
 
-ACT_NONE, ACT_RELU, ACT_SILU = 0, 1, 2
+ACT_NONE, ACT_RELU, ACT_SILU, ACT_GELU = 0, 1, 2, 3
 ACT_RESIDUAL_AFTER = 16          # epilogue flag: y = act(acc + b) + residual (CSP bottlenecks)
-_ACTS = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "silu": ACT_SILU}
+_ACTS = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "silu": ACT_SILU, "gelu": ACT_GELU}
 
 
 @dataclass

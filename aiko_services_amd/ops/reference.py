@@ -8,7 +8,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
-from .conv import ACT_RELU, ACT_SILU, ConvSpec
+from .conv import ACT_GELU, ACT_RELU, ACT_SILU, ConvSpec
 from .vision import IMAGENET_MEAN, IMAGENET_STD
 
 
@@ -17,6 +17,8 @@ def act_ref(x: torch.Tensor, act: int) -> torch.Tensor:
         return F.relu(x)
     if act == ACT_SILU:
         return F.silu(x)
+    if act == ACT_GELU:
+        return F.gelu(x)
     return x
 
 

@@ -1,0 +1,111 @@
+"""Transformer ops on the CDNA4 kernels: fp8 (OCP e4m3fn) linear layers on the block-scaled
+MFMA, fused LayerNorm + per-token fp8 quantisation, flash attention forward
+(``csrc/kernels/gemm_fp8.hip``, ``csrc/kernels/attention.hip``).
+
+Quantisation scheme (inference):
+* weights: per output channel, ``s_w[n] = amax(|W[n, :]|) / 448``, stored e4m3fn [N, K]
+  (K zero-padded to a multiple of 128), quantised once at load;
+* activations: per row (token), ``s_x[m] = amax(|x[m, :]|) / 448``, produced by the kernel that
+  writes the activation (LayerNorm, or the quantise pass over attention / MLP outputs);
+* the GEMM multiplies e4m3 x e4m3 on ``v_mfma_scale_f32_16x16x128_f8f6f4`` and applies
+  ``s_x[m] * s_w[n]`` (+ bias, GELU, residual) in its fp32 epilogue.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+
+__all__ = ["Fp8Linear", "make_fp8_linear", "quantize_rows_ref", "linear_fp8", "rownorm",
+           "attention", "ACT_NONE", "ACT_RELU", "ACT_SILU", "ACT_GELU", "FP8_MAX", "pick_tile"]
+
+ACT_NONE, ACT_RELU, ACT_SILU, ACT_GELU = 0, 1, 2, 3
+FP8_MAX = 448.0
+FP8 = torch.float8_e4m3fn
+
+
+def _round_up(v, m):
+    return (v + m - 1) // m * m
+
+
+@dataclass
+class Fp8Linear:
+    weight: torch.Tensor            # uint8 view of e4m3fn [N, Kp]
+    scale: torch.Tensor             # fp32 [N]
+    bias: torch.Tensor | None       # fp32 [N]
+    n: int
+    k: int
+    ref_weight: torch.Tensor | None = field(default=None, repr=False)   # dequantised fp32 [N, K]
+
+    def to(self, device):
+        self.weight = self.weight.to(device)
+        self.scale = self.scale.to(device)
+        if self.bias is not None:
+            self.bias = self.bias.to(device)
+        return self
+
+    @property
+    def K(self):
+        return self.weight.shape[1]
+
+
+def make_fp8_linear(w: torch.Tensor, bias: torch.Tensor | None = None, device=None) -> Fp8Linear:
+    """Quantise an fp32 [N, K] weight per output channel to e4m3fn."""
+    n, k = w.shape
+    w = w.float()
+    amax = w.abs().amax(dim=1).clamp(min=1e-12)
+    scale = amax / FP8_MAX
+    q = (w / scale[:, None]).clamp(-FP8_MAX, FP8_MAX).to(FP8)
+    kp = _round_up(k, 128)
+    qp = torch.zeros(n, kp, dtype=torch.uint8)
+    qp[:, :k] = q.view(torch.uint8)
+    ref = q.float() * scale[:, None]
+    lin = Fp8Linear(qp.contiguous(), scale.contiguous(), None if bias is None else bias.float().contiguous(),
+                    n, k, ref)
+    return lin.to(device) if device is not None else lin
+
+
+def quantize_rows_ref(x: torch.Tensor):
+    """Reference per-row e4m3 quantisation: (q as uint8, scale fp32 [M])."""
+    x = x.float()
+    amax = x.abs().amax(dim=1)
+    s = torch.where(amax > 0, amax / FP8_MAX, torch.ones_like(amax))
+    q = (x / s[:, None]).clamp(-FP8_MAX, FP8_MAX).to(FP8)
+    return q.view(torch.uint8), s
+
+
+def pick_tile(M: int, N: int) -> tuple[int, int]:
+    bn = 128 if N % 128 == 0 else 64
+    bm = 128
+    if -(-M // bm) * -(-N // bn) < 512:
+        bm = 64
+    return bm, bn
+
+
+def linear_fp8(xq: torch.Tensor, xs: torch.Tensor, lin: Fp8Linear, out: torch.Tensor | None = None,
+               residual: torch.Tensor | None = None, act: int = ACT_NONE, tile=None) -> torch.Tensor:
+    """``act(xs[m] * s_w[n] * (xq @ Wq^T) + bias) + residual`` -> bf16 [M, N].
+    ``xq`` uint8 [M, K] (row pitch may exceed K), ``xs`` fp32 [M]."""
+    M = xq.shape[0]
+    if xq.shape[1] != lin.K:
+        raise ValueError(f"linear_fp8: activation K {xq.shape[1]} != weight K {lin.K}")
+    if out is None:
+        out = torch.empty(M, lin.n, dtype=torch.bfloat16, device=xq.device)
+    bm, bn = tile or pick_tile(M, lin.n)
+    torch.ops.aiko.gemm_fp8_out(xq, xs, lin.weight, lin.scale, lin.bias, residual, out, act, bm, bn)
+    return out
+
+
+def rownorm(x: torch.Tensor, gamma=None, beta=None, eps: float = 1e-5, out: torch.Tensor | None = None,
+            q: torch.Tensor | None = None, qs: torch.Tensor | None = None):
+    """LayerNorm (when ``gamma``/``beta`` are given) of bf16 rows, writing bf16 ``out`` and/or
+    per-row e4m3 ``q`` + scales ``qs`` in one pass."""
+    torch.ops.aiko.rownorm_quant_out(x, gamma, beta, float(eps), out, q, qs)
+    return out, q, qs
+
+
+def attention(q, k, v, out, batch: int, heads: int, T: int, Tpad: int, scale: float):
+    """Non-causal multi-head attention (head dim 64) over sequences of ``T`` tokens stored
+    every ``Tpad`` rows; q/k/v may be column slices of one fused QKV buffer."""
+    torch.ops.aiko.attn_fwd_out(q, k, v, out, batch, heads, T, Tpad, float(scale))
+    return out

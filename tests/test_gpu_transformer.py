@@ -1,0 +1,117 @@
+"""fp8 GEMM, LayerNorm/quantise, flash attention, log-mel and the Whisper encoder on MI355X
+vs plain PyTorch fp32 references (BASELINE config 5)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("tile", [(128, 128), (128, 64), (64, 64), (64, 128)])
+@pytest.mark.parametrize("act", [0, 3])
+def test_gemm_fp8(native, tile, act):
+    from aiko_services_amd.ops import transformer as TR
+    g = torch.Generator().manual_seed(1)
+    M, N, K = 333, 384, 768
+    x = torch.randn(M, K, generator=g)
+    lin = TR.make_fp8_linear(torch.randn(N, K, generator=g) / 30, torch.randn(N, generator=g) * 0.1, DEV)
+    xq, xs = TR.quantize_rows_ref(x)
+    res = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    y = TR.linear_fp8(xq.to(DEV), xs.to(DEV), lin, residual=res, act=act, tile=tile)
+    xd = xq.view(torch.float8_e4m3fn).float() * xs[:, None]
+    ref = xd.to(DEV) @ lin.ref_weight.T.to(DEV) + lin.bias
+    if act == 3:
+        ref = F.gelu(ref)
+    ref = ref + res.float()
+    assert _rel(y, ref) < 5e-3
+
+
+def test_rownorm_quant(native):
+    from aiko_services_amd.ops import transformer as TR
+    g = torch.Generator().manual_seed(2)
+    M, D = 100, 768
+    big = torch.randn(M, 2 * D, generator=g).to(DEV, torch.bfloat16)
+    x = big[:, D:]                                    # column slice, pitch 2D
+    gamma = (1 + 0.1 * torch.randn(D, generator=g)).to(DEV)
+    beta = (0.1 * torch.randn(D, generator=g)).to(DEV)
+    out = torch.empty(M, D, dtype=torch.bfloat16, device=DEV)
+    q = torch.empty(M, D, dtype=torch.uint8, device=DEV)
+    qs = torch.empty(M, dtype=torch.float32, device=DEV)
+    TR.rownorm(x, gamma, beta, 1e-5, out=out, q=q, qs=qs)
+    ref = F.layer_norm(x.float(), (D,), gamma, beta, 1e-5)
+    assert _rel(out, ref) < 5e-3
+    rq, rs = TR.quantize_rows_ref(ref)
+    assert torch.allclose(qs, rs.to(DEV), rtol=1e-5)
+    deq = q.view(torch.float8_e4m3fn).float() * qs[:, None]
+    rdeq = rq.to(DEV).view(torch.float8_e4m3fn).float() * rs.to(DEV)[:, None]
+    assert _rel(deq, rdeq) < 2e-2
+    assert (q == rq.to(DEV)).float().mean().item() > 0.97
+    # quantise-only (no LayerNorm) on a 3072-wide row
+    u = torch.randn(50, 3072, generator=g).to(DEV, torch.bfloat16)
+    uq = torch.empty(50, 3072, dtype=torch.uint8, device=DEV)
+    us = torch.empty(50, dtype=torch.float32, device=DEV)
+    TR.rownorm(u, q=uq, qs=us)
+    rq, rs = TR.quantize_rows_ref(u.float())
+    assert torch.allclose(us, rs.to(DEV), rtol=1e-5)
+    assert (uq == rq.to(DEV)).float().mean().item() > 0.97
+
+
+@pytest.mark.parametrize("B,T,Tpad,H", [(2, 1500, 1501, 12), (3, 77, 80, 4)])
+def test_flash_attention(native, B, T, Tpad, H):
+    from aiko_services_amd.ops import transformer as TR
+    g = torch.Generator().manual_seed(T)
+    d = H * 64
+    qkv = (torch.randn(B * Tpad, 3 * d, generator=g) * 1.5).to(DEV, torch.bfloat16)
+    out = torch.zeros(B * Tpad, d, dtype=torch.bfloat16, device=DEV)
+    TR.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], out, B, H, T, Tpad, 0.125)
+    x = qkv.float().view(B, Tpad, 3, H, 64)[:, :T]
+    q, k, v = (x[:, :, i].transpose(1, 2) for i in range(3))
+    ref = F.scaled_dot_product_attention(q, k, v, scale=0.125).transpose(1, 2).reshape(B, T, d)
+    got = out.view(B, Tpad, d)[:, :T]
+    assert _rel(got, ref) < 1e-2
+    assert out.view(B, Tpad, d)[:, T:].abs().max().item() == 0
+
+
+def test_log_mel(native):
+    from aiko_services_amd.ops import audio as AU
+    g = torch.Generator().manual_seed(3)
+    B, N = 2, 16000 * 5
+    t = torch.arange(N) / 16000
+    audio = (0.3 * torch.sin(2 * torch.pi * 440 * t) + 0.05 * torch.randn(B, N, generator=g)).float()
+    filters = AU.mel_filters().to(DEV)
+    F_ = N // AU.HOP
+    rows = F_ + 2
+    out = torch.full((B * rows, 80), 7.0, dtype=torch.bfloat16, device=DEV)
+    AU.log_mel(audio.to(DEV), filters, out, rows, 1, frames=F_)
+    ref = AU.log_mel_ref(audio.to(DEV), filters, frames=F_)         # [B, 80, F]
+    got = out.view(B, rows, 80)
+    assert (got[:, 0] == 0).all() and (got[:, -1] == 0).all()
+    assert (got[:, 1:-1].float().transpose(1, 2) - ref).abs().max().item() < 2e-2
+
+
+def test_whisper_tiny_matches_reference(native):
+    from aiko_services_amd.models.whisper import WhisperEncoder
+    enc = WhisperEncoder("tiny", device=DEV)
+    g = torch.Generator().manual_seed(4)
+    audio = (0.1 * torch.randn(2, 16000 * 4, generator=g)).to(DEV)
+    y = enc.encode(audio)
+    ref = enc.reference_encode(audio)
+    assert y.shape == ref.shape == (2, 200, 384)
+    cos = F.cosine_similarity(y.float().flatten(), ref.flatten(), dim=0).item()
+    assert cos > 0.99, cos
+
+
+def test_whisper_small_30s(native):
+    from aiko_services_amd.models.whisper import WhisperEncoder
+    enc = WhisperEncoder("small", device=DEV)
+    audio = (0.1 * torch.randn(1, 480000)).to(DEV)
+    y = enc.encode(audio)
+    torch.cuda.synchronize()
+    assert y.shape == (1, 1500, 768)
+    assert torch.isfinite(y.float()).all()
