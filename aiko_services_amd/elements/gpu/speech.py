@@ -1,0 +1,145 @@
+"""GPU speech PipelineElements — BASELINE config 5, Whisper encoder on streamed audio chunks.
+
+    "(AudioChunks AudioWindow WhisperEncoder FeatureSink)"
+
+* ``AudioChunks``   — ``streams`` concurrent audio streams, each producing a ``chunk``-second
+  16 kHz chunk per frame directly in HBM (synthetic: tones + noise from a rotating pool), or
+  uploads host chunks (numpy / CPU tensors from ``AudioReadFile`` / ``AudioSynthetic``) through
+  pinned staging buffers;
+* ``AudioWindow``   — per-stream sliding window of the last ``window`` seconds kept on the GPU
+  (the reference's ``PE_AudioFraming`` LRU of chunks, ``examples/speech/speech_elements.py:
+  60-83``, as one device ring per stream: shift + append, no host copies);
+* ``WhisperEncoder`` — log-mel + Whisper encoder (fp8 linear layers) over the windows,
+  optional hipGraph capture; emits encoder features [B, T, d] on the device;
+* ``FeatureSink``   — mean-pooled features to pinned host memory as a DeviceResult (a
+  stand-in consumer; decoding is not part of the encoder config).
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+
+from ...gpu.element import DeviceResult, GpuPipelineElement
+from ...pipeline.stream import StreamEvent
+
+__all__ = ["AudioChunks", "AudioWindow", "WhisperEncoder", "FeatureSink"]
+
+RATE = 16000
+
+
+def _p(el, name, default):
+    return el.get_parameter(name, default)[0]
+
+
+class AudioChunks(GpuPipelineElement):
+    def __init__(self, context):
+        context.set_protocol("audio_chunks:0")
+        super().__init__(context)
+        self._pool = None
+        self._cursor = 0
+        self._pinned = None
+
+    def _synthetic(self):
+        if self._pool is None:
+            B = int(_p(self, "streams", 8))
+            n = int(float(_p(self, "chunk", 5.0)) * RATE)
+            g = torch.Generator(device=self.device).manual_seed(int(_p(self, "seed", 0)))
+            t = torch.arange(n, device=self.device, dtype=torch.float32) / RATE
+            self._pool = []
+            for _ in range(int(_p(self, "pool", 4))):
+                f = 100 + 900 * torch.rand(B, 1, device=self.device, generator=g)
+                noise = 0.02 * torch.randn(B, n, device=self.device, generator=g)
+                self._pool.append((0.3 * torch.sin(2 * torch.pi * f * t) + noise).contiguous())
+        x = self._pool[self._cursor % len(self._pool)]
+        self._cursor += 1
+        return x
+
+    def _upload(self, audio):
+        x = torch.as_tensor(np.asarray(audio, dtype=np.float32)) if not isinstance(audio, torch.Tensor) else audio
+        if x.dim() == 1:
+            x = x[None]
+        if x.device.type == "cuda":
+            return x.float()
+        if self._pinned is None or self._pinned.shape != x.shape:
+            self._pinned = torch.empty(x.shape, dtype=torch.float32, pin_memory=True)
+        self._pinned.copy_(x)
+        return self._pinned.to(self.device, non_blocking=True)
+
+    def process_frame(self, stream, audio_samples=None, **kwargs):
+        audio = self._synthetic() if audio_samples is None else self._upload(audio_samples)
+        return StreamEvent.OKAY, {"audio": audio, "t_submit": time.perf_counter()}
+
+
+class AudioWindow(GpuPipelineElement):
+    def __init__(self, context):
+        context.set_protocol("audio_window:0")
+        super().__init__(context)
+        self.window = int(float(_p(self, "window", 30.0)) * RATE)
+        self._ring = None
+
+    def process_frame(self, stream, audio):
+        B, n = audio.shape
+        W = self.window
+        if self._ring is None or self._ring[0].shape[0] != B:
+            self._ring = [torch.zeros(B, W, dtype=torch.float32, device=self.device) for _ in range(2)]
+            self._cur = 0
+        src, dst = self._ring[self._cur], self._ring[self._cur ^ 1]
+        if n >= W:
+            dst.copy_(audio[:, n - W:])
+        else:
+            dst[:, :W - n].copy_(src[:, n:])
+            dst[:, W - n:].copy_(audio)
+        self._cur ^= 1
+        return StreamEvent.OKAY, {"audio": dst}
+
+
+class WhisperEncoder(GpuPipelineElement):
+    def __init__(self, context):
+        context.set_protocol("whisper_encoder:0")
+        super().__init__(context)
+        from ...models.whisper import WhisperEncoder as Model
+        from ...ops import require_native
+        require_native()
+        self.model = Model(size=str(_p(self, "size", "small")), seed=int(_p(self, "seed", 0)),
+                           device=self.device)
+        self._tuned = set()
+
+    def _run(self, audio):
+        return self.model.encode(audio)
+
+    def process_frame(self, stream, audio):
+        key = (tuple(audio.shape),)
+        if key not in self._tuned:
+            from ...ops import conv as C
+            with C.autotune():
+                self._run(audio)
+            self._tuned.add(key)
+        return StreamEvent.OKAY, {"features": self.run_maybe_captured(key, self._run, audio)}
+
+
+class FeatureSink(GpuPipelineElement):
+    def __init__(self, context):
+        context.set_protocol("feature_sink:0")
+        super().__init__(context)
+        self._host = []
+        self._slot = 0
+        self._pooled = None
+
+    def process_frame(self, stream, features, t_submit=None):
+        B, T, d = features.shape
+        if self._pooled is None or self._pooled.shape != (B, d):
+            self._pooled = torch.empty(B, d, dtype=torch.float32, device=self.device)
+            pin = self.device.type == "cuda"
+            self._host = [torch.empty(B, d, dtype=torch.float32, pin_memory=pin) for _ in range(8)]
+        torch.mean(features, dim=1, dtype=torch.float32, out=self._pooled)
+        h = self._host[self._slot]
+        self._slot = (self._slot + 1) % len(self._host)
+        h.copy_(self._pooled, non_blocking=True)
+        ev = None
+        if self.device.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+        return StreamEvent.OKAY, {"embedding": DeviceResult({"pooled": h}, ev,
+                                                            t_submit=t_submit if isinstance(t_submit, float) else None)}

@@ -80,6 +80,29 @@ def yolo_definition(batch: int, graph: bool, height: int, width: int, fanout: st
     }
 
 
+SPEECH = "aiko_services_amd.elements.gpu.speech"
+WHISPER_METRIC = "30 s audio windows/sec (whole node) + p50 latency, Whisper encoder fp8 on streamed chunks"
+
+
+def whisper_definition(streams: int, graph: bool, size: str, chunk: float, window: float) -> dict:
+    """BASELINE config 5: streamed audio chunks -> per-stream sliding window on the GPU ->
+    log-mel + Whisper encoder (fp8 linears) -> pooled features to the host."""
+    def el(name, inputs, outputs, params):
+        return {"name": name, "input": [{"name": n, "type": "tensor"} for n in inputs],
+                "output": [{"name": n, "type": "tensor"} for n in outputs],
+                "parameters": params, "deploy": {"local": {"module": SPEECH}}}
+    return {
+        "version": 0, "name": "p_whisper_encoder", "runtime": "python",
+        "graph": ["(AudioChunks AudioWindow WhisperEncoder FeatureSink)"], "parameters": {},
+        "elements": [
+            el("AudioChunks", [], ["audio", "t_submit"], {"streams": streams, "chunk": chunk}),
+            el("AudioWindow", ["audio"], ["audio"], {"window": window}),
+            el("WhisperEncoder", ["audio"], ["features"], {"size": size, "graph": graph}),
+            el("FeatureSink", ["features", "t_submit"], ["embedding"], {}),
+        ],
+    }
+
+
 def pp_definition(batch: int, graph: bool, height: int, width: int, world: int) -> dict:
     """BASELINE config 3: decode -> resize/normalise -> ResNet-50 -> post-process, one stage per
     GPU (``deploy.local.stage`` = i * world // 4, so fewer GPUs fold neighbouring stages)."""
@@ -106,8 +129,12 @@ def main(argv=None):
     ap.add_argument("--width", type=int, default=224)
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture")
     ap.add_argument("--depth", type=int, default=2, help="batches in flight")
-    ap.add_argument("--model", choices=["resnet50", "yolov8n"], default="resnet50",
-                    help="resnet50: headline ResNet-50 pipeline (config 2/3); yolov8n: config 4")
+    ap.add_argument("--model", choices=["resnet50", "yolov8n", "whisper-small", "whisper-tiny", "whisper-base"],
+                    default="resnet50",
+                    help="resnet50: headline ResNet-50 pipeline (config 2/3); yolov8n: config 4; "
+                         "whisper-*: config 5 (--batch = concurrent audio streams)")
+    ap.add_argument("--chunk", type=float, default=5.0, help="(whisper) seconds of audio per chunk")
+    ap.add_argument("--window", type=float, default=30.0, help="(whisper) encoder window seconds")
     ap.add_argument("--fanout", choices=["scatter", "broadcast"], default="scatter",
                     help="(yolov8n) RCCL fan-out of the ingest rank's frame batch")
     ap.add_argument("--parallel", choices=["dp", "pp"], default="dp",
@@ -119,6 +146,8 @@ def main(argv=None):
         a.height, a.width = 480, 640          # configs 3/4 decode VGA video frames
     if a.model == "yolov8n" and "--batch" not in (argv or sys.argv):
         a.batch = 64
+    if a.model.startswith("whisper") and "--batch" not in (argv or sys.argv):
+        a.batch = 16
 
     from aiko_services_amd.parallel import dist as D
     D.init()
@@ -135,7 +164,15 @@ def main(argv=None):
 
     if a.parallel == "pp":
         return run_pp(a, device)
-    if a.model == "yolov8n":
+    metric, unit = METRIC, "frames/s"
+    if a.model.startswith("whisper"):
+        size = a.model.split("-", 1)[1]
+        d = parse_pipeline_definition_dict(whisper_definition(a.batch, not a.no_graph, size, a.chunk, a.window))
+        result_key, model_cfg = "embedding", {"model": f"whisper-{size}-encoder", "weights": "fp8 e4m3 (per-channel)",
+                                              "chunk_s": a.chunk, "window_s": a.window, "streams": a.batch,
+                                              "pipeline": d.graph[0]}
+        metric, unit = WHISPER_METRIC, "windows/s"
+    elif a.model == "yolov8n":
         d = parse_pipeline_definition_dict(yolo_definition(a.batch, not a.no_graph, a.height, a.width, a.fanout))
         result_key, model_cfg = "detections", {"model": "yolov8n", "image_size": [640, 640],
                                                "frame_size": [a.height, a.width], "fanout": a.fanout,
@@ -195,14 +232,19 @@ def main(argv=None):
     fps = frames / elapsed
     if rank == 0:
         out = {
-            "metric": METRIC, "value": round(fps, 1), "unit": "frames/s", "n_gpus": ws,
+            "metric": metric, "value": round(fps, 1), "unit": unit, "n_gpus": ws,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-            "data": f"synthetic (random uint8 {a.height}x{a.width} frames generated in HBM; random-init weights)",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp8 linears / bf16 conv+attention" if a.model.startswith("whisper") else "bf16",
+            "data": (f"synthetic ({a.batch} streams of {a.chunk:g} s 16 kHz chunks generated in HBM; random-init weights)"
+                     if a.model.startswith("whisper") else
+                     f"synthetic (random uint8 {a.height}x{a.width} frames generated in HBM; random-init weights)"),
             "p50_latency_ms": round(p50 * 1e3, 3),
             "config": dict({"global_batch": ws * a.batch, "seq_len": None, "per_gpu_batch": a.batch,
                             "parallelism": f"dp{ws}", "hipgraph": not a.no_graph}, **model_cfg),
         }
+        if a.model.startswith("whisper"):
+            out["audio_seconds_per_s"] = round(ws * a.batch * a.chunk * a.steps / elapsed, 1)
         print(json.dumps(out), flush=True)
     D.barrier()
     D.destroy()
