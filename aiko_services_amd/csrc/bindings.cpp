@@ -23,6 +23,9 @@ int aiko_preprocess(const void* in, void* out, int B, int Hin, int Win, int Ho, 
                     const float* mean, const float* std, int bgr, hipStream_t stream);
 int aiko_maxpool(const void* x, void* y, int B, int H, int W, int C, int Ho, int Wo, int k,
                  int s, int p, int ldx, int ldy, hipStream_t stream);
+int aiko_resize_u8(const void* in, void* out, int B, int Hin, int Win, int Ho, int Wo, hipStream_t stream);
+int aiko_batchnorm(const void* x, void* y, const float* scale, const float* shift, long P, int C, int ldx,
+                   int ldy, int act, hipStream_t stream);
 int aiko_upsample2x(const void* x, void* y, int B, int H, int W, int C, int ldx, int ldy,
                     hipStream_t stream);
 int aiko_yolo_decode(const void* const* feats, const int* H, const int* W, const int* strides,
@@ -188,6 +191,33 @@ void maxpool_out(const at::Tensor& x, at::Tensor& y, int64_t k, int64_t s, int64
   check_launch(aiko_maxpool(x.data_ptr(), y.data_ptr(), B, H, W, C, Ho, Wo, k, s, p, ldx, ldy,
                             cur_stream()),
                "maxpool");
+}
+
+void resize_u8_out(const at::Tensor& x, at::Tensor& y) {
+  check_cuda(x, "x");
+  check_cuda(y, "y");
+  TORCH_CHECK(x.scalar_type() == at::kByte && y.scalar_type() == at::kByte && x.dim() == 4 && y.dim() == 4 &&
+                  x.size(3) == 3 && y.size(3) == 3 && x.is_contiguous() && y.is_contiguous() && x.size(0) == y.size(0),
+              "aiko.resize_u8_out: uint8 [B, H, W, 3] contiguous tensors required");
+  check_launch(aiko_resize_u8(x.data_ptr(), y.data_ptr(), x.size(0), x.size(1), x.size(2), y.size(1), y.size(2),
+                              cur_stream()),
+               "resize_u8");
+}
+
+void batchnorm_out(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& shift, at::Tensor& y, int64_t act) {
+  check_cuda(x, "x");
+  check_cuda(y, "y");
+  check_cuda(scale, "scale");
+  check_cuda(shift, "shift");
+  const int64_t ldx = pixel_pitch(x, "batchnorm_out"), ldy = pixel_pitch(y, "batchnorm_out");
+  const int64_t C = x.size(3);
+  TORCH_CHECK(y.sizes() == x.sizes(), "aiko.batchnorm_out: y must match x");
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && shift.scalar_type() == at::kFloat && scale.numel() == C &&
+                  shift.numel() == C && scale.is_contiguous() && shift.is_contiguous(),
+              "aiko.batchnorm_out: scale/shift fp32 [C]");
+  check_launch(aiko_batchnorm(x.data_ptr(), y.data_ptr(), scale.data_ptr<float>(), shift.data_ptr<float>(),
+                              x.size(0) * x.size(1) * x.size(2), C, ldx, ldy, act, cur_stream()),
+               "batchnorm");
 }
 
 void upsample2x_out(const at::Tensor& x, at::Tensor& y) {
@@ -430,6 +460,8 @@ TORCH_LIBRARY(aiko, m) {
   m.def("conv_igemm_out(Tensor x, Tensor? x2, Tensor w, Tensor? bias, Tensor? res, Tensor(a!) y, int[] geom) -> ()");
   m.def("preprocess_out(Tensor frames, Tensor(a!) out, int Ho, int Wo, int pad_t, int pad_l, float[] mean, float[] std, bool bgr, float[] canvas=[]) -> ()");
   m.def("upsample2x_out(Tensor x, Tensor(a!) y) -> ()");
+  m.def("resize_u8_out(Tensor x, Tensor(a!) y) -> ()");
+  m.def("batchnorm_out(Tensor x, Tensor scale, Tensor shift, Tensor(a!) y, int act) -> ()");
   m.def("yolo_decode_out(Tensor[] feats, int[] strides, int nc, int reg_max, Tensor(a!) boxes, Tensor(b!) scores, Tensor(c!) cls) -> ()");
   m.def("topk_nms_out(Tensor boxes, Tensor scores, Tensor cls, int max_cand, float[] params, Tensor(a!) det, Tensor(b!) count) -> ()");
   m.def("maxpool_out(Tensor x, Tensor(a!) y, int k, int s, int p) -> ()");
@@ -446,6 +478,8 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("preprocess_out", &preprocess_out);
   m.impl("maxpool_out", &maxpool_out);
   m.impl("upsample2x_out", &upsample2x_out);
+  m.impl("resize_u8_out", &resize_u8_out);
+  m.impl("batchnorm_out", &batchnorm_out);
   m.impl("yolo_decode_out", &yolo_decode_out);
   m.impl("topk_nms_out", &topk_nms_out);
   m.impl("avgpool_out", &avgpool_out);

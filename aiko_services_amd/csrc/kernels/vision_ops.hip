@@ -185,6 +185,96 @@ __global__ void softmax_topk_kernel(const bf16_t* __restrict__ logits, float* __
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// uint8 RGB bilinear resize [B, Hin, Win, 3] -> [B, Ho, Wo, 3] (half-pixel centres, like
+// cv2.INTER_LINEAR; ImageResize on the GPU path).  One thread per output pixel.
+__global__ void resize_u8_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, int B,
+                                 int Hin, int Win, int Ho, int Wo) {
+  const long total = (long)B * Ho * Wo;
+  const float sy_scale = (float)Hin / Ho, sx_scale = (float)Win / Wo;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int b = idx / ((long)Ho * Wo);
+    const int rem = idx - (long)b * Ho * Wo;
+    const int yo = rem / Wo, xo = rem - (rem / Wo) * Wo;
+    const float sy = fmaxf((yo + 0.5f) * sy_scale - 0.5f, 0.f);
+    const float sx = fmaxf((xo + 0.5f) * sx_scale - 0.5f, 0.f);
+    const int y0 = min((int)sy, Hin - 1), x0 = min((int)sx, Win - 1);
+    const int y1 = min(y0 + 1, Hin - 1), x1 = min(x0 + 1, Win - 1);
+    const float fy = sy - y0, fx = sx - x0;
+    const uint8_t* base = in + (long)b * Hin * Win * 3;
+    const uint8_t* p00 = base + ((long)y0 * Win + x0) * 3;
+    const uint8_t* p01 = base + ((long)y0 * Win + x1) * 3;
+    const uint8_t* p10 = base + ((long)y1 * Win + x0) * 3;
+    const uint8_t* p11 = base + ((long)y1 * Win + x1) * 3;
+    uint8_t* o = out + idx * 3;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float top = p00[k] + (p01[k] - (float)p00[k]) * fx;
+      const float bot = p10[k] + (p11[k] - (float)p10[k]) * fx;
+      o[k] = (uint8_t)fminf(fmaxf(rintf(top + (bot - top) * fy), 0.f), 255.f);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Inference BatchNorm as a standalone op (normally folded into the preceding conv):
+// y = act(x * scale[c] + shift[c]) on NHWC bf16, 8 channels per thread, pixel pitches ldx/ldy.
+__global__ void batchnorm_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                 const float* __restrict__ scale, const float* __restrict__ shift,
+                                 long P, int C, int ldx, int ldy, int act) {
+  const int C8 = C >> 3;
+  const long total = P * C8;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int c8 = idx % C8;
+    const long pix = idx / C8;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(x + pix * ldx + c8 * 8);
+    float f[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      f[2 * e] = __uint_as_float(v[e] << 16);
+      f[2 * e + 1] = __uint_as_float(v[e] & 0xffff0000u);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float t = f[e] * scale[c8 * 8 + e] + shift[c8 * 8 + e];
+      if (act == 1) t = fmaxf(t, 0.f);
+      else if (act == 2) t = t / (1.f + __expf(-t));
+      f[e] = t;
+    }
+    u32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = pack2(f[2 * e], f[2 * e + 1]);
+    *reinterpret_cast<u32x4*>(y + pix * ldy + c8 * 8) = o;
+  }
+}
+
+}  // namespace aiko
+
+extern "C" int aiko_resize_u8(const void* in, void* out, int B, int Hin, int Win, int Ho, int Wo,
+                              hipStream_t stream) {
+  const long total = (long)B * Ho * Wo;
+  long g = (total + 255) / 256;
+  if (g > 4096) g = 4096;
+  aiko::resize_u8_kernel<<<(int)g, 256, 0, stream>>>(static_cast<const uint8_t*>(in),
+                                                     static_cast<uint8_t*>(out), B, Hin, Win, Ho, Wo);
+  return (int)hipGetLastError();
+}
+
+extern "C" int aiko_batchnorm(const void* x, void* y, const float* scale, const float* shift, long P,
+                              int C, int ldx, int ldy, int act, hipStream_t stream) {
+  const long total = P * (C / 8);
+  long g = (total + 255) / 256;
+  if (g > 4096) g = 4096;
+  aiko::batchnorm_kernel<<<(int)g, 256, 0, stream>>>(static_cast<const aiko::bf16_t*>(x),
+                                                     static_cast<aiko::bf16_t*>(y), scale, shift, P,
+                                                     C, ldx, ldy, act);
+  return (int)hipGetLastError();
+}
+
+namespace aiko {
 }  // namespace aiko
 
 static inline int grid_for(long total, int block) {

@@ -71,3 +71,29 @@ def softmax_topk(logits: torch.Tensor, k: int = 5, prob: torch.Tensor | None = N
         index = torch.empty(B, k, dtype=torch.int32, device=logits.device)
     torch.ops.aiko.softmax_topk_out(logits, prob, index, k)
     return prob, index
+
+
+def resize_u8(frames: torch.Tensor, size: tuple[int, int], out: torch.Tensor | None = None) -> torch.Tensor:
+    """Bilinear resize of uint8 ``[B, H, W, 3]`` frames to ``size`` = (H', W') on the GPU."""
+    if frames.dim() == 3:
+        return resize_u8(frames[None], size, None if out is None else out[None])[0]
+    B = frames.shape[0]
+    if out is None:
+        out = torch.empty(B, size[0], size[1], 3, dtype=torch.uint8, device=frames.device)
+    torch.ops.aiko.resize_u8_out(frames.contiguous(), out)
+    return out
+
+
+def batchnorm(x: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor, act: int = 0,
+              out: torch.Tensor | None = None) -> torch.Tensor:
+    """Standalone inference BatchNorm ``act(x * scale + shift)`` over NHWC bf16 (channel
+    slices allowed); ``scale = gamma / sqrt(var + eps)``, ``shift = beta - mean * scale``."""
+    if out is None:
+        out = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+    torch.ops.aiko.batchnorm_out(x, scale, shift, out, act)
+    return out
+
+
+def bn_scale_shift(gamma, beta, mean, var, eps=1e-5):
+    scale = gamma / torch.sqrt(var + eps)
+    return scale.float().contiguous(), (beta - mean * scale).float().contiguous()

@@ -169,3 +169,27 @@ def test_fused_projection_shortcut(native, B, H, cin_main, cin_sc, cout, stride)
     idn = R.conv_ref(x.permute(0, 3, 1, 2).float(), down)
     ref = R.conv_ref(t.permute(0, 3, 1, 2).float(), main, idn)
     assert _rel_err(y.permute(0, 3, 1, 2), ref) < 1e-2
+
+
+def test_resize_u8(native):
+    from aiko_services_amd.ops import vision as V
+    frames = torch.randint(0, 256, (2, 37, 53, 3), dtype=torch.uint8, device=DEV)
+    y = V.resize_u8(frames, (64, 80))
+    ref = torch.nn.functional.interpolate(frames.permute(0, 3, 1, 2).float(), size=(64, 80), mode="bilinear",
+                                          align_corners=False).round().clamp(0, 255).permute(0, 2, 3, 1)
+    assert (y.float() - ref).abs().max().item() <= 1
+
+
+def test_batchnorm_standalone(native):
+    from aiko_services_amd.ops import vision as V
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(2, 9, 11, 64, generator=g).to(DEV, torch.bfloat16)
+    gamma, beta = torch.rand(32, generator=g) + 0.5, torch.randn(32, generator=g)
+    mean, var = torch.randn(32, generator=g), torch.rand(32, generator=g) + 0.5
+    scale, shift = V.bn_scale_shift(gamma, beta, mean, var)
+    out = torch.zeros(2, 9, 11, 64, dtype=torch.bfloat16, device=DEV)
+    V.batchnorm(x[..., 32:], scale.to(DEV), shift.to(DEV), act=1, out=out[..., :32])
+    ref = torch.nn.functional.batch_norm(x[..., 32:].permute(0, 3, 1, 2).float(), mean.to(DEV), var.to(DEV),
+                                         gamma.to(DEV), beta.to(DEV), False, 0.0, 1e-5).relu()
+    assert _rel_err(out[..., :32].permute(0, 3, 1, 2), ref) < 1e-2
+    assert out[..., 32:].abs().max().item() == 0
