@@ -137,3 +137,31 @@ def test_yolov8n_detect_end_to_end(native):
         if n:
             assert (d[:, 4] > 0.25).all() and (d[:, 4][:-1] >= d[:, 4][1:]).all()
             assert (d[:, 0] >= 0).all() and (d[:, 2] <= 640).all() and (d[:, 3] <= 480).all()
+
+
+def test_example_yolo_element_overlay(native):
+    """Reference-compatible YoloDetector (examples/yolo): list of numpy images -> overlay dict."""
+    import queue
+
+    import numpy as np
+
+    from aiko_services_amd.pipeline.definition import parse_pipeline_definition_dict
+    from aiko_services_amd.pipeline.engine import PipelineImpl
+    d = {"version": 0, "name": "p_yolo_example", "runtime": "python", "graph": ["(YoloDetector)"],
+         "parameters": {}, "elements": [
+             {"name": "YoloDetector", "input": [{"name": "images", "type": "[image]"}],
+              "output": [{"name": "overlay", "type": "[overlay]"}], "parameters": {"class_filter": "all"},
+              "deploy": {"local": {"module": "aiko_services_amd.examples.yolo.yolo"}}}]}
+    q = queue.Queue()
+    p = PipelineImpl.create_pipeline("<t>", parse_pipeline_definition_dict(d), None, None, "s", [], 0, None, 60,
+                                     queue_response=q)
+    rng = np.random.default_rng(0)
+    images = [rng.integers(0, 256, (480, 640, 3), dtype=np.uint8) for _ in range(3)] + \
+             [rng.integers(0, 256, (240, 320, 3), dtype=np.uint8)]
+    p.process_frame({"stream_id": "s", "frame_id": 0}, {"images": images})
+    info, out = q.get(timeout=60)
+    assert info["state"] == 0, out
+    ov = out["overlay"]
+    assert len(ov["objects"]) == len(ov["rectangles"])
+    for r in ov["rectangles"]:
+        assert r["w"] >= 0 and r["h"] >= 0 and 0 <= r["x"] <= 640

@@ -97,3 +97,24 @@ def test_storage_request_response(cluster):
     cluster["spawn"]("-m", "aiko_services_amd.tools.storage", "start", ":memory:")
     res = cluster["run"]("-m", "aiko_services_amd.tools.storage", "test_request", "hello_world", timeout=30)
     assert "Response: [('hello_world', [])]" in res.stdout, res.stdout + res.stderr
+
+
+def test_aloha_honua_actor_over_mqtt(cluster):
+    """Hello-world actor (X1): remote call published as an S-expression on its /in topic."""
+    cluster["spawn"]("-m", "aiko_services_amd.tools.registrar")
+    time.sleep(0.8)
+    actor = cluster["spawn"]("-m", "aiko_services_amd.examples.aloha_honua.aloha_honua_0")
+    topic = None
+    deadline = time.time() + 15
+    while time.time() < deadline and topic is None:
+        line = actor.stdout.readline()
+        if line.startswith("MQTT topic:"):
+            topic = line.split(":", 1)[1].strip()
+    assert topic, "actor did not report its topic"
+    out = _snapshot(cluster, expect=("aloha_honua",))
+    assert "aloha_honua" in out
+    for name in ("Pele", "Hiiaka"):
+        r = cluster["run"]("-m", "aiko_services_amd.tools.mqtt", "pub", topic, f"(aloha {name})")
+        assert r.returncode == 0, r.stderr
+    out = _snapshot(cluster, service="aloha_honua", expect=("greetings = 2",))
+    assert "greetings = 2" in out, out
