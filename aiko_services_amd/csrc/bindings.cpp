@@ -18,6 +18,11 @@ int aiko_conv_igemm(const void* x, const void* w, const float* bias, const void*
                     int H, int W, int C, int Cc, int R, int S, int stride, int pad, int Ho,
                     int Wo, int M, int Cout, int K, int act, int ldy, int ldr, int bm, int bn,
                     const void* x2, int K1, int H2, int W2, int C2, int stride2, hipStream_t stream);
+int aiko_conv_glds(const void* x, const void* w, const float* bias, const void* res, void* y,
+                   int H, int W, int C, int Cc, int R, int S, int stride, int pad, int Ho,
+                   int Wo, int M, int Cout, int K, int act, int ldy, int ldr, int bm, int bn,
+                   const void* x2, int K1, int H2, int W2, int C2, int stride2, const void* zero,
+                   hipStream_t stream);
 int aiko_preprocess(const void* in, void* out, int B, int Hin, int Win, int Ho, int Wo, int Hp,
                     int Wp, int pad_t, int pad_l, int Hc, int Wc, int off_t, int off_l, float fill,
                     const float* mean, const float* std, int bgr, hipStream_t stream);
@@ -68,11 +73,14 @@ void check_launch(int rc, const char* what) {
 }
 
 // geom = [H, W, C, Cc, R, S, stride, pad, Ho, Wo, M, act, ldy, ldr, bm, bn,
-//         K1, H2, W2, C2, stride2]   (the last five describe the optional second source x2)
+//         K1, H2, W2, C2, stride2 (the optional second source x2), [variant]]
+// variant 0: register-staged kernel (conv_igemm.hip); 1: LDS-DMA kernel (conv_glds.hip), which
+// needs ``zero`` (>= 16 B of zeros on the device) as the source of conv padding.
 void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, const at::Tensor& w,
                     const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& res,
-                    at::Tensor& y, at::IntArrayRef geom) {
-  TORCH_CHECK(geom.size() == 21, "aiko.conv_igemm_out: geom needs 21 ints");
+                    at::Tensor& y, at::IntArrayRef geom, const c10::optional<at::Tensor>& zero) {
+  TORCH_CHECK(geom.size() == 21 || geom.size() == 22, "aiko.conv_igemm_out: geom needs 21 or 22 ints");
+  const int64_t variant = geom.size() == 22 ? geom[21] : 0;
   const int64_t H = geom[0], W = geom[1], C = geom[2], Cc = geom[3], R = geom[4], S = geom[5];
   const int64_t stride = geom[6], pad = geom[7], Ho = geom[8], Wo = geom[9], M = geom[10];
   const int64_t act = geom[11], ldy = geom[12], ldr = geom[13], bm = geom[14], bn = geom[15];
@@ -131,9 +139,19 @@ void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, co
     TORCH_CHECK(ldr % 8 == 0 && avail_elems(*res) >= (M - 1) * ldr + Cout, "aiko.conv_igemm_out: bad residual");
     rptr = res->data_ptr();
   }
-  const int rc = aiko_conv_igemm(x.data_ptr(), w.data_ptr(), bptr, rptr, y.data_ptr(), H, W, C,
-                                 Cc, R, S, stride, pad, Ho, Wo, M, Cout, K, act, ldy,
-                                 ldr, bm, bn, x2ptr, K1, H2, W2, C2, stride2, cur_stream());
+  int rc;
+  if (variant == 1) {
+    TORCH_CHECK(zero.has_value() && zero->defined() && zero->is_cuda() && zero->nbytes() >= 16 &&
+                    reinterpret_cast<uintptr_t>(zero->data_ptr()) % 16 == 0,
+                "aiko.conv_igemm_out: the LDS-DMA variant needs a zero page tensor (>= 16 B)");
+    rc = aiko_conv_glds(x.data_ptr(), w.data_ptr(), bptr, rptr, y.data_ptr(), H, W, C, Cc, R, S, stride,
+                        pad, Ho, Wo, M, Cout, K, act, ldy, ldr, bm, bn, x2ptr, K1, H2, W2, C2, stride2,
+                        zero->data_ptr(), cur_stream());
+  } else {
+    rc = aiko_conv_igemm(x.data_ptr(), w.data_ptr(), bptr, rptr, y.data_ptr(), H, W, C, Cc, R, S, stride,
+                         pad, Ho, Wo, M, Cout, K, act, ldy, ldr, bm, bn, x2ptr, K1, H2, W2, C2, stride2,
+                         cur_stream());
+  }
   check_launch(rc, "conv_igemm");
 }
 
@@ -457,7 +475,7 @@ void logmel_out(const at::Tensor& audio, const at::Tensor& mel, int64_t n_fft, i
 }  // namespace
 
 TORCH_LIBRARY(aiko, m) {
-  m.def("conv_igemm_out(Tensor x, Tensor? x2, Tensor w, Tensor? bias, Tensor? res, Tensor(a!) y, int[] geom) -> ()");
+  m.def("conv_igemm_out(Tensor x, Tensor? x2, Tensor w, Tensor? bias, Tensor? res, Tensor(a!) y, int[] geom, Tensor? zero=None) -> ()");
   m.def("preprocess_out(Tensor frames, Tensor(a!) out, int Ho, int Wo, int pad_t, int pad_l, float[] mean, float[] std, bool bgr, float[] canvas=[]) -> ()");
   m.def("upsample2x_out(Tensor x, Tensor(a!) y) -> ()");
   m.def("resize_u8_out(Tensor x, Tensor(a!) y) -> ()");

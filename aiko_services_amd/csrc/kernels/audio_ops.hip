@@ -1,6 +1,6 @@
 // Whisper front end for gfx950: log-mel spectrogram of 16 kHz audio, fully on the GPU.
 //
-// logmel_kernel: one 256-thread workgroup per 8 STFT frames of one clip.  Frames (n_fft 400,
+// logmel_kernel: one 256-thread workgroup per 16 STFT frames of one clip.  Frames (n_fft 400,
 // hop 160, centred with reflect padding, periodic Hann window) are staged in LDS; the 201-bin
 // power spectrum is a direct DFT against an LDS twiddle table (0.26 MFLOP per frame: a few
 // microseconds for a 30 s clip, not worth an FFT's passes at this size); the mel filterbank
@@ -12,7 +12,7 @@
 
 namespace aiko {
 
-constexpr int kFPB = 8;          // frames per workgroup
+constexpr int kFPB = 16;         // frames per workgroup
 constexpr int kMaxFFT = 400;
 constexpr int kMaxBins = kMaxFFT / 2 + 1;
 
@@ -56,18 +56,26 @@ __global__ __launch_bounds__(256) void logmel_kernel(const float* __restrict__ a
     frame[f][n] = v;
   }
   __syncthreads();
-  for (int pr = tid; pr < kFPB * nbins; pr += 256) {
-    const int f = pr / nbins, k = pr - f * nbins;
-    float re = 0.f, im = 0.f;
+  // one thread per frequency bin, all kFPB frames at once: each twiddle gather from LDS feeds
+  // 2 * kFPB FMAs and the frame samples are wave-wide broadcasts
+  for (int k = tid; k < nbins; k += 256) {
+    float re[kFPB], im[kFPB];
+#pragma unroll
+    for (int f = 0; f < kFPB; ++f) re[f] = im[f] = 0.f;
     int t = 0;
     for (int n = 0; n < n_fft; ++n) {
-      const float v = frame[f][n];
-      re += v * tw_c[t];
-      im -= v * tw_s[t];
+      const float c = tw_c[t], sn = tw_s[t];
+#pragma unroll
+      for (int f = 0; f < kFPB; ++f) {
+        const float v = frame[f][n];
+        re[f] += v * c;
+        im[f] -= v * sn;
+      }
       t += k;
       if (t >= n_fft) t -= n_fft;
     }
-    power[f][k] = re * re + im * im;
+#pragma unroll
+    for (int f = 0; f < kFPB; ++f) power[f][k] = re[f] * re[f] + im[f] * im[f];
   }
   __syncthreads();
   float mx = -INFINITY;

@@ -1,0 +1,295 @@
+// Implicit-GEMM convolution, global_load_lds variant (gfx950 LDS-DMA staging).
+//
+// Same math, tiles, epilogue and LDS image as conv_igemm.hip, but operands go HBM -> LDS with
+// `global_load_lds_dwordx4` (no VGPR staging, no ds_write pass) through a 3-slot ring: stage
+// kb+2 is issued right after the barrier that retires stage kb, so two K-blocks stay in flight
+// across the barrier.  Synchronisation follows the LDS-DMA rules:
+//   * RAW: each wave retires its own DMAs for stage kb with a COUNTED `s_waitcnt vmcnt(PER)`
+//     (PER = DMA instructions per stage), then a raw `s_barrier`; only then is the slot read;
+//   * WAR: a slot is re-issued one iteration after its last ds_read, behind a barrier that
+//     every wave reaches after `s_waitcnt lgkmcnt(0)` (its reads of that slot have landed);
+//   * never `__syncthreads()` inside the loop: its fence would drain vmcnt to 0 (the in-flight
+//     stage), one LDS array only (a second __shared__ object makes hipcc drain before reads).
+// The DMA destination is lane-linear (wave base + lane * 16 B), so the XOR swizzle moves to
+// the SOURCE: lane l of a row group fetches logical 16-B piece (l & 7) ^ (row & 7) into
+// physical slot l & 7 — exactly the image the fragment reads of the register-staged kernel
+// expect.  Conv zero padding (and rows / channels past the edge) are fetched from a zeroed
+// 16-B global page instead of being predicated away.
+#include "conv_common.h"
+
+namespace aiko {
+
+// ring slots: 3 (two stages in flight) where 2 workgroups still fit the 160 KB LDS, else 2
+template <int BM, int BN>
+constexpr int glds_slots() {
+  return (BM + BN) * 64 * 2 * 3 <= 80 * 1024 ? 3 : 2;
+}
+template <int BM, int BN>
+constexpr int glds_occupancy() {
+  return (BM == 64 && BN == 64) ? 3 : 2;
+}
+
+__device__ __forceinline__ void glds16(const void* g, bf16_t* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(g, reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                          reinterpret_cast<uintptr_t>(lds_wave_base)),
+                                   16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256, (glds_occupancy<BM, BN>())) void conv_glds_kernel(ConvParams p,
+                                                                                 const bf16_t* zero) {
+  constexpr int BK = 64;
+  constexpr int NS = glds_slots<BM, BN>();     // LDS ring slots
+  constexpr int D = NS - 1;                    // stages in flight
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int MI = WM / 16, NI = WN / 16;
+  constexpr int APT = BM / 32, BPT = BN / 32;  // DMA instructions per thread per stage
+  constexpr int PER = APT + BPT;
+  constexpr int STAGE_ELEMS = (BM + BN) * BK;
+  constexpr int CPAD = 4;
+  constexpr int EPI_BYTES = BM * (BN + CPAD) * 4;
+  constexpr int RING_BYTES = NS * STAGE_ELEMS * 2;
+  constexpr int LDS_BYTES = EPI_BYTES > RING_BYTES ? EPI_BYTES : RING_BYTES;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
+  bf16_t* ring = reinterpret_cast<bf16_t*>(smem);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int ntn = (p.Cout + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile_n = bid % ntn, tile_m = bid / ntn;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+
+  // DMA lane mapping: instruction i of wave w covers rows i*32 + w*8 .. +7, lane l -> row
+  // (l >> 3) of that group, physical slot (l & 7), logical piece lp = (l & 7) ^ (l >> 3)
+  const int lrow = wave * 8 + (lane >> 3);
+  const int lp = (lane & 7) ^ (lane >> 3);
+  const int HoWo = p.Ho * p.Wo;
+  int a_base[APT], a_ih[APT], a_iw[APT], a2_base[APT];
+#pragma unroll
+  for (int i = 0; i < APT; ++i) {
+    const int m = m0 + lrow + 32 * i;
+    if (m < p.M) {
+      const int img = m / HoWo;
+      const int rem = m - img * HoWo;
+      const int oh = rem / p.Wo;
+      const int ow = rem - oh * p.Wo;
+      a_ih[i] = oh * p.stride - p.pad;
+      a_iw[i] = ow * p.stride - p.pad;
+      a_base[i] = ((img * p.H + a_ih[i]) * p.W + a_iw[i]) * p.C;
+      a2_base[i] = ((img * p.H2 + oh * p.stride2) * p.W2 + ow * p.stride2) * p.C2;
+    } else {
+      a_ih[i] = -(1 << 28);
+      a_iw[i] = 0;
+      a_base[i] = 0;
+      a2_base[i] = -1;
+    }
+  }
+  const bf16_t* b_src[BPT];
+#pragma unroll
+  for (int i = 0; i < BPT; ++i) {
+    const int n = n0 + lrow + 32 * i;
+    b_src[i] = n < p.Cout ? p.w + (long)n * p.K + lp * 8 : nullptr;
+  }
+
+  // epilogue operands, prefetched before the K loop (ordinary loads, older than every DMA)
+  constexpr int CPR = BN / 8, CHUNKS = BM * CPR, CPT = CHUNKS / 256, E_ROWS = 256 / CPR;
+  static_assert(CHUNKS % 256 == 0, "tile must give every thread whole chunks");
+  const int e_cc = tid % CPR, e_row0 = tid / CPR;
+  const int e_n = n0 + e_cc * 8;
+  float e_bias[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) e_bias[e] = 0.f;
+  if (p.bias && e_n < p.Cout) {
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(p.bias + e_n);
+    const f32x4 b1 = *reinterpret_cast<const f32x4*>(p.bias + e_n + 4);
+    e_bias[0] = b0[0]; e_bias[1] = b0[1]; e_bias[2] = b0[2]; e_bias[3] = b0[3];
+    e_bias[4] = b1[0]; e_bias[5] = b1[1]; e_bias[6] = b1[2]; e_bias[7] = b1[3];
+  }
+  u32x4 e_res[CPT];
+  if (p.res) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int m = m0 + e_row0 + E_ROWS * i;
+      const bool ok = m < p.M && e_n < p.Cout;
+      e_res[i] = *reinterpret_cast<const u32x4*>(p.res + (ok ? (size_t)m * p.ldr + e_n : 0));
+    }
+  }
+
+  const bf16_t* zp = zero;
+  auto issue = [&](int kb, int slot) {
+    bf16_t* As = ring + slot * STAGE_ELEMS;
+    bf16_t* Bs = As + BM * BK;
+    if (p.x2 && kb * BK >= p.K1) {
+      const int c2 = kb * BK - p.K1 + lp * 8;
+#pragma unroll
+      for (int i = 0; i < APT; ++i) {
+        const bf16_t* g = a2_base[i] >= 0 ? p.x2 + (a2_base[i] + c2) : zp;
+        glds16(g, As + (i * 32 + wave * 8) * BK);
+      }
+    } else {
+      const int koff = kb * BK + lp * 8;
+      const int tap = koff / p.Cc;
+      const int c = koff - tap * p.Cc;
+      const int r = tap / p.S;
+      const int s = tap - r * p.S;
+      const int tap_off = (r * p.W + s) * p.C + c;
+#pragma unroll
+      for (int i = 0; i < APT; ++i) {
+        const int ih = a_ih[i] + r, iw = a_iw[i] + s;
+        const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        const bf16_t* g = ok ? p.x + (a_base[i] + tap_off) : zp;
+        glds16(g, As + (i * 32 + wave * 8) * BK);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      const bf16_t* g = b_src[i] ? b_src[i] + kb * BK : zp;
+      glds16(g, Bs + (i * 32 + wave * 8) * BK);
+    }
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nkb = p.K / BK;
+#pragma unroll
+  for (int j = 0; j < D; ++j)
+    if (j < nkb) issue(j, j);
+  const int fr = lane & 15, fq = lane >> 4;
+
+  int slot = 0;
+  for (int kb = 0; kb < nkb; ++kb) {
+    // retire stage kb (this wave's DMAs), keep the younger ones in flight, then barrier
+    if (D == 2 && kb + 1 < nkb) {
+      wait_vm_barrier<PER>();
+    } else {
+      wait_vm_barrier<0>();
+    }
+    if (kb + D < nkb) issue(kb + D, slot == 0 ? NS - 1 : slot - 1);   // the slot of stage kb-1
+    const bf16_t* As = ring + slot * STAGE_ELEMS;
+    const bf16_t* Bs = As + BM * BK;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[MI], bfr[NI];
+      const int pc = fq + 4 * kk;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int row = wr * WM + i * 16 + fr;
+        af[i] = *reinterpret_cast<const bf16x8*>(As + row * BK + ((pc ^ (row & 7)) << 3));
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int row = wc * WN + j * 16 + fr;
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + ((pc ^ (row & 7)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    slot = slot == NS - 1 ? 0 : slot + 1;
+  }
+  wait_vm_barrier<0>();                // every wave's last fragment reads done before Cs reuse
+
+  // ---- epilogue (as conv_igemm) ----
+  float* Cs = reinterpret_cast<float*>(smem);
+  constexpr int LDC = BN + CPAD;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int col = wc * WN + j * 16 + fr;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Cs[(wr * WM + i * 16 + fq * 4 + e) * LDC + col] = acc[i][j][e];
+    }
+  __syncthreads();
+  const bool post = (p.act & 16) != 0;
+  const int act = p.act & 15;
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int row = e_row0 + E_ROWS * i;
+    const int m = m0 + row;
+    if (m >= p.M || e_n >= p.Cout) continue;
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + e_cc * 8);
+    const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + e_cc * 8 + 4);
+    float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += e_bias[e];
+    if (p.res && !post) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[2 * e] += __uint_as_float(e_res[i][e] << 16);
+        v[2 * e + 1] += __uint_as_float(e_res[i][e] & 0xffff0000u);
+      }
+    }
+    if (act == 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    } else if (act == 2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = v[e] / (1.f + __expf(-v[e]));
+    } else if (act == 3) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
+    }
+    if (p.res && post) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[2 * e] += __uint_as_float(e_res[i][e] << 16);
+        v[2 * e + 1] += __uint_as_float(e_res[i][e] & 0xffff0000u);
+      }
+    }
+    u32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = pack2(v[2 * e], v[2 * e + 1]);
+    *reinterpret_cast<u32x4*>(p.y + (size_t)m * p.ldy + e_n) = o;
+  }
+}
+
+}  // namespace aiko
+
+// Same arguments as aiko_conv_igemm plus the zero page (>= 16 B of zeros in device memory).
+extern "C" int aiko_conv_glds(const void* x, const void* w, const float* bias, const void* res,
+                              void* y, int H, int W, int C, int Cc, int R, int S, int stride,
+                              int pad, int Ho, int Wo, int M, int Cout, int K, int act, int ldy,
+                              int ldr, int bm, int bn, const void* x2, int K1, int H2, int W2,
+                              int C2, int stride2, const void* zero, hipStream_t stream) {
+  using namespace aiko;
+  ConvParams p;
+  p.x = static_cast<const bf16_t*>(x);
+  p.w = static_cast<const bf16_t*>(w);
+  p.bias = bias;
+  p.res = static_cast<const bf16_t*>(res);
+  p.y = static_cast<bf16_t*>(y);
+  p.H = H; p.W = W; p.C = C; p.Cc = Cc; p.R = R; p.S = S;
+  p.stride = stride; p.pad = pad; p.Ho = Ho; p.Wo = Wo; p.M = M; p.Cout = Cout; p.K = K;
+  p.act = act; p.ldy = ldy; p.ldr = ldr;
+  p.x2 = static_cast<const bf16_t*>(x2);
+  p.K1 = x2 ? K1 : K; p.H2 = H2; p.W2 = W2; p.C2 = C2; p.stride2 = stride2;
+  const bf16_t* z = static_cast<const bf16_t*>(zero);
+  dim3 grid(((M + bm - 1) / bm) * ((Cout + bn - 1) / bn)), block(256);
+  if (bm == 128 && bn == 128) {
+    conv_glds_kernel<128, 128><<<grid, block, 0, stream>>>(p, z);
+  } else if (bm == 128 && bn == 64) {
+    conv_glds_kernel<128, 64><<<grid, block, 0, stream>>>(p, z);
+  } else if (bm == 64 && bn == 64) {
+    conv_glds_kernel<64, 64><<<grid, block, 0, stream>>>(p, z);
+  } else if (bm == 64 && bn == 128) {
+    conv_glds_kernel<64, 128><<<grid, block, 0, stream>>>(p, z);
+  } else {
+    return -1;
+  }
+  return (int)hipGetLastError();
+}

@@ -215,8 +215,23 @@ def tile_cache() -> dict:
     return dict(_tile_cache)
 
 
+_ZERO: dict = {}
+
+
+def zero_page(device) -> torch.Tensor:
+    """64 zero bytes on ``device``: the global source of conv zero padding for the LDS-DMA
+    kernel variant (allocated on first use, outside any graph capture)."""
+    z = _ZERO.get(device)
+    if z is None:
+        z = _ZERO[device] = torch.zeros(32, dtype=torch.bfloat16, device=device)
+    return z
+
+
 def _tune(key, M, cout, launch):
-    cands = NARROW_TILES if cout <= 32 else TILES
+    if cout <= 32:
+        cands = [t + (0,) for t in NARROW_TILES]
+    else:
+        cands = [t + (0,) for t in TILES] + [t + (1,) for t in TILES]
     best, best_t = None, None
     for t in cands:
         launch(t)  # warm
@@ -290,7 +305,10 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None
             0 if residual is None else (residual.stride(2) if residual.dim() == 4 else residual.stride(0))]
 
     def launch(t):
-        torch.ops.aiko.conv_igemm_out(x, x2, spec.weight, spec.bias, residual, out, head + list(t) + src2)
+        # t = (BM, BN) or (BM, BN, variant): variant 1 = LDS-DMA kernel (needs the zero page)
+        v = t[2] if len(t) > 2 else 0
+        torch.ops.aiko.conv_igemm_out(x, x2, spec.weight, spec.bias, residual, out,
+                                      head + [t[0], t[1]] + src2 + [v], zero_page(x.device) if v else None)
 
     if tile is None:
         key = (M, spec.cout, spec.K, spec.R, spec.S, spec.stride, pitch, spec.K1, residual is not None, spec.Cc)

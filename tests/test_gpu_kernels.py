@@ -29,6 +29,14 @@ def _nhwc(x_nchw):
     (2, 20, 20, 16, 32, 3, 1, 1, "silu", False, None),    # Cin=16: 4 taps per K block
     (2, 20, 20, 48, 64, 3, 2, 1, "silu", False, None),    # Cin=48: padded chunk
     (1, 9, 11, 40, 24, 3, 1, 1, None, False, None),       # odd spatial, Cout=24 (N tail)
+    # LDS-DMA variant (global_load_lds ring, zero-page padding)
+    (2, 56, 56, 64, 256, 1, 1, 0, "relu", True, (128, 128, 1)),
+    (2, 56, 56, 64, 64, 3, 1, 1, "relu", False, (128, 64, 1)),
+    (2, 28, 28, 128, 128, 3, 2, 1, "relu", True, (64, 64, 1)),
+    (3, 14, 14, 256, 1024, 1, 1, 0, None, True, (64, 128, 1)),
+    (1, 9, 11, 40, 24, 3, 1, 1, "silu", False, (64, 64, 1)),
+    (2, 20, 20, 48, 64, 3, 2, 1, "silu", False, (128, 64, 1)),
+    (2, 20, 20, 16, 64, 3, 1, 1, "relu", False, (128, 128, 1)),
 ])
 def test_conv_igemm_matches_torch(native, B, H, W, cin, cout, k, stride, pad, act, res, tile):
     from aiko_services_amd.ops import conv as C
@@ -148,9 +156,10 @@ def test_resnet50_matches_fp32_reference(native):
     assert (i[:, 0].long() == lg.argmax(1)).all()
 
 
+@pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("B,H,cin_main,cin_sc,cout,stride", [(2, 28, 64, 64, 256, 1), (2, 28, 128, 256, 512, 2),
                                                               (1, 14, 512, 1024, 2048, 2)])
-def test_fused_projection_shortcut(native, B, H, cin_main, cin_sc, cout, stride):
+def test_fused_projection_shortcut(native, B, H, cin_main, cin_sc, cout, stride, variant):
     """conv3(t) + down(x) (+bias, ReLU) as one K-concatenated igemm with two A sources."""
     from aiko_services_amd.ops import conv as C
     from aiko_services_amd.ops import reference as R
@@ -164,7 +173,7 @@ def test_fused_projection_shortcut(native, B, H, cin_main, cin_sc, cout, stride)
     fused = C.fuse_shortcut(main, down)
     t = torch.randn(B, Ho, Ho, cin_main, generator=g).to(torch.bfloat16).to(DEV)
     x = torch.randn(B, H, H, cin_sc, generator=g).to(torch.bfloat16).to(DEV)
-    y = C.conv2d(t, fused, x2=x)
+    y = C.conv2d(t, fused, x2=x, tile=(64, 128, variant))
     torch.cuda.synchronize()
     idn = R.conv_ref(x.permute(0, 3, 1, 2).float(), down)
     ref = R.conv_ref(t.permute(0, 3, 1, 2).float(), main, idn)
