@@ -38,7 +38,7 @@ int aiko_yolo_decode(const void* const* feats, const int* H, const int* W, const
                      float* scores, int* cls, hipStream_t stream);
 int aiko_gemm_fp8(const void* a, const void* b, const float* sa, const float* sb, const float* bias,
                   const void* res, void* y, int M, int N, int K, int lda, int ldy, int ldr, int act,
-                  int bm, int bn, hipStream_t stream);
+                  int bm, int bn, int variant, const void* zero, hipStream_t stream);
 int aiko_rownorm_quant(const void* x, int ldx, const float* gamma, const float* beta, float eps,
                        void* yb, int ldyb, void* q, int ldq, float* qs, int M, int D, hipStream_t stream);
 int aiko_attn_fwd(const void* q, const void* k, const void* v, void* o, int ldq, int ldk, int ldv,
@@ -355,7 +355,8 @@ int64_t row_pitch(const at::Tensor& t, int64_t cols, const char* op, const char*
 // y = act(sa[m] * sb[n] * (A @ B^T) + bias) + residual ; A fp8 [M, K] (uint8 storage), B fp8 [N, K]
 void gemm_fp8_out(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& b, const at::Tensor& sb,
                   const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& res,
-                  at::Tensor& y, int64_t act, int64_t bm, int64_t bn) {
+                  at::Tensor& y, int64_t act, int64_t bm, int64_t bn, int64_t variant,
+                  const c10::optional<at::Tensor>& zero) {
   for (const at::Tensor* t : {&a, &sa, &b, &sb, (const at::Tensor*)&y}) check_cuda(*t, "operand");
   TORCH_CHECK(a.element_size() == 1 && b.element_size() == 1, "aiko.gemm_fp8_out: A and B must be 1-byte fp8 storage");
   TORCH_CHECK(y.scalar_type() == at::kBFloat16, "aiko.gemm_fp8_out: y must be bf16");
@@ -384,8 +385,17 @@ void gemm_fp8_out(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& b
     rp = res->data_ptr();
   }
   TORCH_CHECK(lda * M < INT_MAX * 2L, "aiko.gemm_fp8_out: A too large");
+  const void* zp = nullptr;
+  if (variant == 1) {
+    TORCH_CHECK(zero.has_value() && zero->defined() && zero->is_cuda() && zero->nbytes() >= 16 &&
+                    reinterpret_cast<uintptr_t>(zero->data_ptr()) % 16 == 0,
+                "aiko.gemm_fp8_out: the LDS-DMA variant needs a zero page tensor (>= 16 B)");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0,
+                "aiko.gemm_fp8_out: operands must be 16-byte aligned");
+    zp = zero->data_ptr();
+  }
   check_launch(aiko_gemm_fp8(a.data_ptr(), b.data_ptr(), sa.data_ptr<float>(), sb.data_ptr<float>(), bp, rp,
-                             y.data_ptr(), M, N, K, lda, ldy, ldr, act, bm, bn, cur_stream()),
+                             y.data_ptr(), M, N, K, lda, ldy, ldr, act, bm, bn, (int)variant, zp, cur_stream()),
                "gemm_fp8");
 }
 
@@ -484,7 +494,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("topk_nms_out(Tensor boxes, Tensor scores, Tensor cls, int max_cand, float[] params, Tensor(a!) det, Tensor(b!) count) -> ()");
   m.def("maxpool_out(Tensor x, Tensor(a!) y, int k, int s, int p) -> ()");
   m.def("avgpool_out(Tensor x, Tensor(a!) y) -> ()");
-  m.def("gemm_fp8_out(Tensor a, Tensor sa, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!) y, int act, int bm, int bn) -> ()");
+  m.def("gemm_fp8_out(Tensor a, Tensor sa, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!) y, int act, int bm, int bn, int variant=0, Tensor? zero=None) -> ()");
   m.def("rownorm_quant_out(Tensor x, Tensor? gamma, Tensor? beta, float eps, Tensor(a!)? yb, Tensor(b!)? q, Tensor(c!)? qs) -> ()");
   m.def("attn_fwd_out(Tensor q, Tensor k, Tensor v, Tensor(a!) o, int B, int H, int T, int Tpad, float scale) -> ()");
   m.def("logmel_out(Tensor audio, Tensor mel, int n_fft, int hop, int F, Tensor(a!) work, Tensor(b!) gmax, Tensor(c!) dst, int rows, int pad) -> ()");

@@ -48,9 +48,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
     const int q = q0 + qt * 16 + fr;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      u32x4 u = {0u, 0u, 0u, 0u};
-      if (q < p.T) u = *reinterpret_cast<const u32x4*>(p.q + (seq0 + q) * p.ldq + hc + ks * 32 + 8 * g);
-      qf[qt][ks] = as_bf16x8(u);
+      // rows past T are clamped to T-1 (their outputs are never written): no predicated loads
+      const int qc = q < p.T ? q : p.T - 1;
+      qf[qt][ks] = as_bf16x8(*reinterpret_cast<const u32x4*>(p.q + (seq0 + qc) * p.ldq + hc + ks * 32 + 8 * g));
     }
   }
 
@@ -60,14 +60,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
   auto load_tile = [&](int t0) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int key = t0 + prow + 32 * i;
-      if (key < p.T) {
-        rk[i] = *reinterpret_cast<const u32x4*>(p.k + (seq0 + key) * p.ldk + hc + piece * 8);
-        rv[i] = *reinterpret_cast<const u32x4*>(p.v + (seq0 + key) * p.ldv + hc + piece * 8);
-      } else {
-        rk[i] = u32x4{0u, 0u, 0u, 0u};
-        rv[i] = u32x4{0u, 0u, 0u, 0u};
-      }
+      // keys past T read row T-1 (finite data): their scores are masked to -inf, so P = 0 and
+      // the V rows contribute exactly 0 — unconditional loads keep the prefetch pipelined
+      const int key = min(t0 + prow + 32 * i, p.T - 1);
+      rk[i] = *reinterpret_cast<const u32x4*>(p.k + (seq0 + key) * p.ldk + hc + piece * 8);
+      rv[i] = *reinterpret_cast<const u32x4*>(p.v + (seq0 + key) * p.ldv + hc + piece * 8);
     }
   };
   auto store_tile = [&](int slot) {

@@ -38,6 +38,68 @@ __device__ __forceinline__ float gelu_erf(float x) {
 }
 
 template <int BM, int BN>
+__device__ __forceinline__ void fp8_epilogue(const Fp8GemmParams& p, f32x4 (&acc)[BM / 32][BN / 32],
+                                             unsigned char* smem, int m0, int n0) {
+  constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NI = WN / 16, CPAD = 4;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1, fr = lane & 15, fg = lane >> 4;
+  float* Cs = reinterpret_cast<float*>(smem);
+  constexpr int LDC = BN + CPAD;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int col = wc * WN + j * 16 + fr;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Cs[(wr * WM + i * 16 + fg * 4 + e) * LDC + col] = acc[i][j][e];
+    }
+  __syncthreads();
+  constexpr int CPR = BN / 8, CHUNKS = BM * CPR, CPT = CHUNKS / 256, E_ROWS = 256 / CPR;
+  static_assert(CHUNKS % 256 == 0, "whole chunks per thread");
+  const int e_cc = tid % CPR, e_row0 = tid / CPR;
+  const int e_n = n0 + e_cc * 8;
+  if (e_n >= p.N) return;
+  float cs[8], cb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    cs[e] = p.sb[e_n + e];
+    cb[e] = p.bias ? p.bias[e_n + e] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int row = e_row0 + E_ROWS * i;
+    const int m = m0 + row;
+    if (m >= p.M) continue;
+    const float rs = p.sa[m];
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = Cs[row * LDC + e_cc * 8 + e] * rs * cs[e] + cb[e];
+    if (p.act == 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    } else if (p.act == 2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = v[e] / (1.f + __expf(-v[e]));
+    } else if (p.act == 3) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+    }
+    if (p.res) {
+      const u32x4 r = *reinterpret_cast<const u32x4*>(p.res + (long)m * p.ldr + e_n);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[2 * e] += __uint_as_float(r[e] << 16);
+        v[2 * e + 1] += __uint_as_float(r[e] & 0xffff0000u);
+      }
+    }
+    u32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = pack2(v[2 * e], v[2 * e + 1]);
+    *reinterpret_cast<u32x4*>(p.y + (long)m * p.ldy + e_n) = o;
+  }
+}
+
+template <int BM, int BN>
 __global__ __launch_bounds__(256, 2) void gemm_fp8_kernel(Fp8GemmParams p) {
   constexpr int BK = 128;                      // bytes == fp8 elements
   constexpr int WM = BM / 2, WN = BN / 2;
@@ -141,61 +203,122 @@ __global__ __launch_bounds__(256, 2) void gemm_fp8_kernel(Fp8GemmParams p) {
     __syncthreads();
   }
 
-  // ---- epilogue ----
-  float* Cs = reinterpret_cast<float*>(smem);
-  constexpr int LDC = BN + CPAD;
+  fp8_epilogue<BM, BN>(p, acc, smem, m0, n0);
+}
+
+// ---------------------------------------------------------------------------------------------
+// LDS-DMA variant: the same tile / MFMA / epilogue with operands staged by
+// global_load_lds_dwordx4 through a ring of NS slots (see conv_glds.hip for the protocol:
+// counted vmcnt + raw barrier, source-side swizzle, lane-linear DMA destination).  Rows past
+// M / N read a zeroed 16-B page.
+template <int BM, int BN>
+constexpr int fp8_glds_slots() {
+  return (BM + BN) * 128 * 3 <= 80 * 1024 ? 3 : 2;
+}
+
+__device__ __forceinline__ void glds16_u8(const void* g, unsigned char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(g, reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                          reinterpret_cast<uintptr_t>(lds_wave_base)),
+                                   16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void fp8_wait_vm_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN>
+__global__ __launch_bounds__(256, 2) void gemm_fp8_glds_kernel(Fp8GemmParams p, const uint8_t* zero) {
+  constexpr int BK = 128;
+  constexpr int NS = fp8_glds_slots<BM, BN>();
+  constexpr int D = NS - 1;
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int MI = WM / 16, NI = WN / 16;
+  constexpr int APT = BM / 32, BPT = BN / 32;
+  constexpr int PER = APT + BPT;
+  constexpr int STAGE_BYTES = (BM + BN) * BK;
+  constexpr int CPAD = 4;
+  constexpr int EPI_BYTES = BM * (BN + CPAD) * 4;
+  constexpr int RING_BYTES = NS * STAGE_BYTES;
+  constexpr int LDS_BYTES = EPI_BYTES > RING_BYTES ? EPI_BYTES : RING_BYTES;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int ntn = (p.N + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
+  const int lrow = wave * 8 + (lane >> 3);
+  const int lp = (lane & 7) ^ (lane >> 3);
+
+  const uint8_t* a_src[APT];
+#pragma unroll
+  for (int i = 0; i < APT; ++i) {
+    const int m = m0 + lrow + 32 * i;
+    a_src[i] = m < p.M ? p.a + (long)m * p.lda + lp * 16 : nullptr;
+  }
+  const uint8_t* b_src[BPT];
+#pragma unroll
+  for (int i = 0; i < BPT; ++i) {
+    const int n = n0 + lrow + 32 * i;
+    b_src[i] = n < p.N ? p.b + (long)n * p.K + lp * 16 : nullptr;
+  }
+  auto issue = [&](int kb, int slot) {
+    unsigned char* As = smem + slot * STAGE_BYTES;
+    unsigned char* Bs = As + BM * BK;
+    const int k0 = kb * BK;
+#pragma unroll
+    for (int i = 0; i < APT; ++i) glds16_u8(a_src[i] ? a_src[i] + k0 : zero, As + (i * 32 + wave * 8) * BK);
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) glds16_u8(b_src[i] ? b_src[i] + k0 : zero, Bs + (i * 32 + wave * 8) * BK);
+  };
+
+  f32x4 acc[MI][NI];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nkb = p.K / BK;
+#pragma unroll
+  for (int j = 0; j < D; ++j)
+    if (j < nkb) issue(j, j);
+  const int fr = lane & 15, fg = lane >> 4;
+  int slot = 0;
+  for (int kb = 0; kb < nkb; ++kb) {
+    if (D == 2 && kb + 1 < nkb) {
+      fp8_wait_vm_barrier<PER>();
+    } else {
+      fp8_wait_vm_barrier<0>();
+    }
+    if (kb + D < nkb) issue(kb + D, slot == 0 ? NS - 1 : slot - 1);
+    const unsigned char* As = smem + slot * STAGE_BYTES;
+    const unsigned char* Bs = As + BM * BK;
+    i32x8 af[MI], bfr[NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int row = wr * WM + i * 16 + fr;
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(As + row * BK + (((2 * fg) ^ (row & 7)) << 4));
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(As + row * BK + (((2 * fg + 1) ^ (row & 7)) << 4));
+      af[i] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+#pragma unroll
     for (int j = 0; j < NI; ++j) {
-      const int col = wc * WN + j * 16 + fr;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) Cs[(wr * WM + i * 16 + fg * 4 + e) * LDC + col] = acc[i][j][e];
+      const int row = wc * WN + j * 16 + fr;
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(Bs + row * BK + (((2 * fg) ^ (row & 7)) << 4));
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(Bs + row * BK + (((2 * fg + 1) ^ (row & 7)) << 4));
+      bfr[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
     }
-  __syncthreads();
-  constexpr int CPR = BN / 8, CHUNKS = BM * CPR, CPT = CHUNKS / 256, E_ROWS = 256 / CPR;
-  static_assert(CHUNKS % 256 == 0, "whole chunks per thread");
-  const int e_cc = tid % CPR, e_row0 = tid / CPR;
-  const int e_n = n0 + e_cc * 8;
-  if (e_n >= p.N) return;
-  float cs[8], cb[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    cs[e] = p.sb[e_n + e];
-    cb[e] = p.bias ? p.bias[e_n + e] : 0.f;
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0,
+                                                                      0, 127, 0, 127);
+    slot = slot == NS - 1 ? 0 : slot + 1;
   }
-#pragma unroll
-  for (int i = 0; i < CPT; ++i) {
-    const int row = e_row0 + E_ROWS * i;
-    const int m = m0 + row;
-    if (m >= p.M) continue;
-    const float rs = p.sa[m];
-    float v[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = Cs[row * LDC + e_cc * 8 + e] * rs * cs[e] + cb[e];
-    if (p.act == 1) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-    } else if (p.act == 2) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = v[e] / (1.f + __expf(-v[e]));
-    } else if (p.act == 3) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
-    }
-    if (p.res) {
-      const u32x4 r = *reinterpret_cast<const u32x4*>(p.res + (long)m * p.ldr + e_n);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[2 * e] += __uint_as_float(r[e] << 16);
-        v[2 * e + 1] += __uint_as_float(r[e] & 0xffff0000u);
-      }
-    }
-    u32x4 o;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = pack2(v[2 * e], v[2 * e + 1]);
-    *reinterpret_cast<u32x4*>(p.y + (long)m * p.ldy + e_n) = o;
-  }
+  fp8_wait_vm_barrier<0>();
+  fp8_epilogue<BM, BN>(p, acc, smem, m0, n0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -303,7 +426,8 @@ __global__ __launch_bounds__(256) void rownorm_quant_kernel(
 
 extern "C" int aiko_gemm_fp8(const void* a, const void* b, const float* sa, const float* sb,
                              const float* bias, const void* res, void* y, int M, int N, int K,
-                             int lda, int ldy, int ldr, int act, int bm, int bn, hipStream_t stream) {
+                             int lda, int ldy, int ldr, int act, int bm, int bn, int variant,
+                             const void* zero, hipStream_t stream) {
   using namespace aiko;
   Fp8GemmParams p;
   p.a = static_cast<const uint8_t*>(a);
@@ -313,6 +437,22 @@ extern "C" int aiko_gemm_fp8(const void* a, const void* b, const float* sa, cons
   p.y = static_cast<bf16_t*>(y);
   p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldy = ldy; p.ldr = ldr; p.act = act;
   dim3 grid(((M + bm - 1) / bm) * ((N + bn - 1) / bn)), block(256);
+  if (variant == 1) {
+    const uint8_t* z = static_cast<const uint8_t*>(zero);
+    if (!z) return -1;
+    if (bm == 128 && bn == 128) {
+      gemm_fp8_glds_kernel<128, 128><<<grid, block, 0, stream>>>(p, z);
+    } else if (bm == 128 && bn == 64) {
+      gemm_fp8_glds_kernel<128, 64><<<grid, block, 0, stream>>>(p, z);
+    } else if (bm == 64 && bn == 64) {
+      gemm_fp8_glds_kernel<64, 64><<<grid, block, 0, stream>>>(p, z);
+    } else if (bm == 64 && bn == 128) {
+      gemm_fp8_glds_kernel<64, 128><<<grid, block, 0, stream>>>(p, z);
+    } else {
+      return -1;
+    }
+    return (int)hipGetLastError();
+  }
   if (bm == 128 && bn == 128) {
     gemm_fp8_kernel<128, 128><<<grid, block, 0, stream>>>(p);
   } else if (bm == 128 && bn == 64) {

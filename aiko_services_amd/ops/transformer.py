@@ -16,6 +16,8 @@ from dataclasses import dataclass, field
 
 import torch
 
+from . import conv as _conv
+
 __all__ = ["Fp8Linear", "make_fp8_linear", "quantize_rows_ref", "linear_fp8", "rownorm",
            "attention", "ACT_NONE", "ACT_RELU", "ACT_SILU", "ACT_GELU", "FP8_MAX", "pick_tile"]
 
@@ -91,9 +93,44 @@ def linear_fp8(xq: torch.Tensor, xs: torch.Tensor, lin: Fp8Linear, out: torch.Te
         raise ValueError(f"linear_fp8: activation K {xq.shape[1]} != weight K {lin.K}")
     if out is None:
         out = torch.empty(M, lin.n, dtype=torch.bfloat16, device=xq.device)
-    bm, bn = tile or pick_tile(M, lin.n)
-    torch.ops.aiko.gemm_fp8_out(xq, xs, lin.weight, lin.scale, lin.bias, residual, out, act, bm, bn)
+    if tile is None:
+        key = (M, lin.n, lin.K, xq.stride(0), residual is not None, act)
+        tile = _tile_cache.get(key)
+        if tile is None:
+            if _conv._tuning:
+                tile = _tune_fp8(key, lambda t: _launch(xq, xs, lin, out, residual, act, t))
+            else:
+                tile = pick_tile(M, lin.n) + (1,)
+    _launch(xq, xs, lin, out, residual, act, tile)
     return out
+
+
+def _launch(xq, xs, lin, out, residual, act, t):
+    v = t[2] if len(t) > 2 else 0
+    torch.ops.aiko.gemm_fp8_out(xq, xs, lin.weight, lin.scale, lin.bias, residual, out, act, t[0], t[1], v,
+                                _conv.zero_page(xq.device) if v else None)
+
+
+_tile_cache: dict = {}
+FP8_TILES = ((128, 128), (128, 64), (64, 128), (64, 64))
+
+
+def _tune_fp8(key, launch):
+    """Pick (BM, BN, variant) by measurement, like ``ops.conv.autotune`` (shares its switch)."""
+    best, best_t = None, None
+    for t in [tt + (v,) for tt in FP8_TILES for v in (0, 1)]:
+        launch(t)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(3):
+            launch(t)
+        e1.record()
+        e1.synchronize()
+        ms = e0.elapsed_time(e1)
+        if best_t is None or ms < best_t:
+            best, best_t = t, ms
+    _tile_cache[key] = best
+    return best
 
 
 def rownorm(x: torch.Tensor, gamma=None, beta=None, eps: float = 1e-5, out: torch.Tensor | None = None,
