@@ -104,6 +104,18 @@ class DeviceResult:
         return f"DeviceResult({shapes}, ready={self.ready()})"
 
 
+_STREAMS: dict = {}
+
+
+def named_stream(name: str, device) -> "torch.cuda.Stream":
+    """One HIP stream per (device, name), shared by the elements that name it."""
+    key = (str(device), name)
+    st = _STREAMS.get(key)
+    if st is None:
+        st = _STREAMS[key] = torch.cuda.Stream(device=device)
+    return st
+
+
 class CapturedCall:
     """hipGraph capture of ``fn(*static_inputs)`` for one input signature."""
 
@@ -144,8 +156,14 @@ class GpuPipelineElement(PipelineElement):
             torch.cuda.set_device(self.device)
         graph, _ = self.get_parameter("graph", default=False)
         self.use_graph = str(graph).lower() in ("true", "1", "yes")
+        # optional dedicated HIP stream (parameter "hip_stream": name): independent graph branches
+        # on different streams run concurrently on the GPU; joins use events
+        stream_name, found = self.get_parameter("hip_stream")
+        self.hip_stream = named_stream(str(stream_name), self.device) if found and stream_name \
+            and self.device.type == "cuda" else None
         self._captured: dict = {}
         self.share["device"] = str(self.device)
+        self._telemetry = {"frames": 0, "t0": time.perf_counter(), "t_last": 0.0, "n_last": 0}
 
     def run_maybe_captured(self, key, fn, *inputs):
         if not self.use_graph:
@@ -155,6 +173,64 @@ class GpuPipelineElement(PipelineElement):
             call = CapturedCall(fn, inputs)
             self._captured[key] = call
         return call(*inputs)
+
+    def stream_enter(self, frame):
+        """Engine hook before process_frame: order this element after the producers of its
+        inputs (events recorded by side-stream elements) and switch to its own stream."""
+        events = getattr(frame, "_hip_events", None)
+        target = self.hip_stream
+        if events:
+            wait_on = target if target is not None else torch.cuda.current_stream(self.device)
+            for io in self.definition.input or []:
+                ev = events.get(io["name"])
+                if ev is not None:
+                    wait_on.wait_event(ev)
+        if target is None:
+            return None
+        target.wait_stream(torch.cuda.current_stream(self.device))   # fork point: prior work
+        ctx = torch.cuda.stream(target)
+        ctx.__enter__()
+        return ctx
+
+    def stream_exit(self, frame, outputs, ctx):
+        if ctx is None:
+            return
+        ev = torch.cuda.Event()
+        ev.record(self.hip_stream)
+        ctx.__exit__(None, None, None)
+        if not hasattr(frame, "_hip_events"):
+            frame._hip_events = {}
+            frame._hip_pending = []
+            device = self.device
+
+            def join():   # end of frame: the default stream sees every side stream's work
+                cur = torch.cuda.current_stream(device)
+                for e in frame._hip_pending:
+                    cur.wait_event(e)
+            frame._hip_join = join
+        for name in (outputs or {}):
+            frame._hip_events[name] = ev
+        frame._hip_pending.append(ev)
+
+    def frame_done(self, seconds: float) -> None:
+        """Engine hook after each local process_frame: GPU telemetry in the EC share (at most
+        once a second, so dashboards see frames/s, host-side ms/frame and HBM use per element)."""
+        t = self._telemetry
+        t["frames"] += 1
+        now = time.perf_counter()
+        if now - t["t_last"] < 1.0:
+            return
+        if t["t_last"]:
+            self.share["gpu_fps"] = round((t["frames"] - t["n_last"]) / (now - t["t_last"]), 1)
+        t["t_last"], t["n_last"] = now, t["frames"]
+        self.share["gpu_frames"] = t["frames"]
+        self.share["gpu_host_ms"] = round(seconds * 1e3, 3)
+        if self.device.type == "cuda":
+            self.share["hbm_allocated_mb"] = round(torch.cuda.memory_allocated(self.device) / 2**20, 1)
+            self.share["hbm_reserved_mb"] = round(torch.cuda.memory_reserved(self.device) / 2**20, 1)
+        pool = getattr(self, "frame_pool", None)
+        if pool is not None:
+            self.share["frame_pool_free"] = pool.free_count()
 
     def gpu_timer_start(self):
         start = torch.cuda.Event(enable_timing=True)

@@ -641,6 +641,8 @@ class PipelineImpl(Pipeline):
                 if local:
                     start = time.time()
                     gpu_t = element.gpu_timer_start() if _GPU_TIMING and hasattr(element, "gpu_timer_start") else None
+                    enter = getattr(element, "stream_enter", None)
+                    hip_ctx = enter(frame) if enter is not None else None
                     try:
                         stream_event, frame_data_out = element.process_frame(stream, **inputs)
                     except Exception:
@@ -649,6 +651,8 @@ class PipelineImpl(Pipeline):
                         frame_data_out = {"diagnostic": traceback.format_exc()}
                     if frame_data_out is None:
                         frame_data_out = {}
+                    if enter is not None:
+                        element.stream_exit(frame, frame_data_out, hip_ctx)
                     stream.state = self._process_stream_event(element_name, stream_event, frame_data_out)
                     self._process_map_out(node.name, frame_data_out)
                     t = time.time()
@@ -657,6 +661,9 @@ class PipelineImpl(Pipeline):
                     if gpu_t is not None:
                         metrics.setdefault("gpu_events", {})[element.name] = gpu_t
                         element.gpu_timer_stop(gpu_t)
+                    hook = getattr(element, "frame_done", None)
+                    if hook is not None:
+                        hook(t - start)
                     frame.swag.update(frame_data_out)
                 else:
                     if self.share["lifecycle"] != "ready":
@@ -670,6 +677,9 @@ class PipelineImpl(Pipeline):
                         element.process_frame({"stream_id": stream.stream_id, "frame_id": frame_id}, **inputs)
                     break
             if frame_complete:
+                join = getattr(stream.frames.get(frame_id), "_hip_join", None)
+                if join is not None:
+                    join()
                 self.frames_completed += 1
                 stream_info = {"stream_id": stream.stream_id, "frame_id": frame_id, "state": stream.state}
                 if stream.queue_response is not None:

@@ -47,3 +47,49 @@ def test_frame_pool_on_device(native):
     assert pool.acquire(0.1) == slots[1]
     st = pool.stats()
     assert st["capacity"] == 3 and st["high_water"] == 3 and st["exhausted"] == 1
+
+
+def _diamond(streams: bool, repeat=12, size=2048):
+    M = "aiko_services_amd.elements.gpu.tensor_ops"
+
+    def el(name, cls_in, cls_out, params):
+        return {"name": name, "input": [{"name": n, "type": "tensor"} for n in cls_in],
+                "output": [{"name": n, "type": "tensor"} for n in cls_out], "parameters": params,
+                "deploy": {"local": {"module": M, "class_name": name.rstrip("AB")}}}
+    pa = {"repeat": repeat, "seed": 1}
+    pb = {"repeat": repeat, "seed": 2}
+    if streams:
+        pa["hip_stream"], pb["hip_stream"] = "branch_a", "branch_b"
+    return {"version": 0, "name": "p_diamond", "runtime": "python",
+            "graph": ["(GpuTensorSource (GpuMatChainA GpuAdd) (GpuMatChainB GpuAdd))"], "parameters": {},
+            "elements": [el("GpuTensorSource", [], ["x"], {"size": size}),
+                         el("GpuMatChainA", ["x"], ["ya"], pa),
+                         el("GpuMatChainB", ["x"], ["yb"], pb),
+                         el("GpuAdd", ["ya", "yb"], ["z"], {})]}
+
+
+def test_branches_on_hip_streams_match_sequential(native):
+    """Diamond graph: branches on two HIP streams (concurrent) give the sequential result."""
+    import queue
+    import time
+    from aiko_services_amd.pipeline.definition import parse_pipeline_definition_dict
+    from aiko_services_amd.pipeline.engine import PipelineImpl
+    results, times = {}, {}
+    for streams in (False, True):
+        q = queue.Queue()
+        p = PipelineImpl.create_pipeline("<t>", parse_pipeline_definition_dict(_diamond(streams)), None, None,
+                                         f"s{int(streams)}", [], 0, None, 60, queue_response=q)
+        for i in range(3):          # warm-up
+            p.process_frame({"stream_id": f"s{int(streams)}", "frame_id": i}, {})
+            q.get(timeout=60)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(3, 13):
+            p.process_frame({"stream_id": f"s{int(streams)}", "frame_id": i}, {})
+            info, out = q.get(timeout=60)
+            assert info["state"] == 0, out
+        torch.cuda.synchronize()
+        times[streams] = time.perf_counter() - t0
+        results[streams] = out["z"].float().clone()
+    assert torch.allclose(results[False], results[True], atol=1e-2)
+    print(f"diamond sequential {times[False]*1e3:.1f} ms, two streams {times[True]*1e3:.1f} ms")
