@@ -1,15 +1,21 @@
 // Flash-attention forward (non-causal, head dim 64) for CDNA4 (gfx950), bf16 in / fp32 softmax.
 //
-// Built for the Whisper encoder (1500 tokens x 12 heads x 64): one 256-thread workgroup per
-// (128-query block, head, sequence); each of the 4 waves owns 32 queries and streams the
-// sequence's keys in 64-key tiles through a 2-deep LDS ring (K as [key][dh] with 16-B XOR
-// swizzle, V transposed to [dh][key] with 8-B chunk swizzle).  The products are computed
+// Built for the Whisper encoder (1500 tokens x 12 heads x 64): one workgroup of NW waves per
+// (32*NW-query block, head, sequence); each wave owns 32 queries and streams the sequence's
+// keys in 64-key tiles through a 3-slot LDS ring filled by LDS-DMA (global_load_lds, two
+// tiles in flight behind a counted vmcnt + raw barrier).  K and V are both stored row-major
+// ([key][dh]; the DMA destination is lane-linear, so the swizzles are applied to the source
+// rows): K with a 16-B XOR swizzle for ds_read_b128, V with a 32-B chunk swizzle
+// (chunk ^ ((key >> 1) & 3)) read by the gfx950 hardware-transpose ds_read_b64_tr_b16
+// (conflict-free per 32-lane half), which hands every lane a 4-key column of V.  The
+// products are computed
 // TRANSPOSED — S^T = K Q^T and O^T = V^T P^T with v_mfma_f32_16x16x32_bf16 — so that:
 //   * each lane's accumulator column is one query: the online-softmax rescale of O^T is a
 //     per-lane scalar, and row statistics need only 2 cross-lane shuffles (xor 16, 32);
 //   * the bf16 probabilities P^T are consumed as the B operand straight from the S^T
 //     accumulator registers (no LDS round trip): element j of lane group g of k-step s is key
-//     32s + 16(j>>2) + 4g + (j&3), and the V^T fragment is read in that same key order.
+//     32s + 16(j>>2) + 4g + (j&3), and the V^T fragment is two transposed reads of rows
+//     32s + 4g .. +3 and 32s + 16 + 4g .. +3 — that same key order.
 // Q stays in registers for the whole key loop.  Sequences are rows b*Tpad .. b*Tpad+T-1 of
 // q/k/v (any row pitch: q, k, v may be column slices of one fused QKV buffer).
 #include "common.h"
@@ -26,19 +32,34 @@ struct AttnParams {
   float scale_log2;     // softmax scale * log2(e)
 };
 
-constexpr int kQB = 128, kKB = 64, kDH = 64;
+constexpr int kKB = 64, kDH = 64;
+constexpr float kRescale = 8.f;   // lazy-rescale threshold (log2 units): P <= 2^8, safe in bf16/fp32
 
 __device__ __forceinline__ bf16x8 as_bf16x8(u32x4 u) { return __builtin_bit_cast(bf16x8, u); }
 
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[2][kKB * kDH];
-  __shared__ __attribute__((aligned(16))) bf16_t Vt[2][kDH * kKB];
+typedef __attribute__((ext_vector_type(4))) short v4i16;
+
+// byte offset of 16-bit column `col` (multiple of 4) of key row `row` in the V image
+__device__ __forceinline__ int v_off(int row, int col) {
+  return row * (kDH * 2) + (((col >> 4) ^ ((row >> 1) & 3)) << 5) + ((col & 15) << 1);
+}
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnParams p) {
+  constexpr int NT = 64 * NW;
+  constexpr int QB = 32 * NW;
+  constexpr int TILE = kKB * kDH;                // elements
+  constexpr int PIECES = TILE / 8;               // 16-B pieces per tile (512)
+  constexpr int PPT = PIECES / NT;               // DMA pieces per thread per operand
+  constexpr int NS = 3;                          // LDS ring slots: tiles it+1, it+2 in flight
+  constexpr int PER = 2 * PPT;                   // DMA instructions per thread per tile
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NS * 2 * TILE];   // one array: [slot][K|V]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, g = lane >> 4;
   const int h = blockIdx.y, b = blockIdx.z;
   const long seq0 = (long)b * p.Tpad;
-  const int q0 = blockIdx.x * kQB + wave * 32;
+  const int q0 = blockIdx.x * QB + wave * 32;
   const int hc = h * kDH;
 
   // Q^T fragments (B operand): lane holds Q[q][ks*32 + 8g .. +7] for q = q0 + qt*16 + fr
@@ -46,39 +67,33 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int q = q0 + qt * 16 + fr;
+    const int qc = q < p.T ? q : p.T - 1;     // rows past T: clamped, never written
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      // rows past T are clamped to T-1 (their outputs are never written): no predicated loads
-      const int qc = q < p.T ? q : p.T - 1;
+    for (int ks = 0; ks < 2; ++ks)
       qf[qt][ks] = as_bf16x8(*reinterpret_cast<const u32x4*>(p.q + (seq0 + qc) * p.ldq + hc + ks * 32 + 8 * g));
-    }
   }
 
-  // staging: 2 x 16-B pieces of K and of V per thread per tile
-  const int piece = tid & 7, prow = tid >> 3;  // rows prow, prow + 32
-  u32x4 rk[2], rv[2];
-  auto load_tile = [&](int t0) {
+  // K / V tiles by LDS-DMA (lane-linear destination, swizzle on the SOURCE): instruction i of
+  // wave w fills rows (NT/8)*i + 8w .. +7; lane l -> row (l >> 3), physical 16-B slot (l & 7)
+  const int drow = wave * 8 + (lane >> 3);
+  const int ps = lane & 7;
+  const int k_lp = ps ^ (lane >> 3);                                   // K: piece ^ (row & 7)
+  auto issue = [&](int t0, int slot) {
+    bf16_t* Ks = smem + slot * 2 * TILE;
+    bf16_t* Vs = Ks + TILE;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      // keys past T read row T-1 (finite data): their scores are masked to -inf, so P = 0 and
-      // the V rows contribute exactly 0 — unconditional loads keep the prefetch pipelined
-      const int key = min(t0 + prow + 32 * i, p.T - 1);
-      rk[i] = *reinterpret_cast<const u32x4*>(p.k + (seq0 + key) * p.ldk + hc + piece * 8);
-      rv[i] = *reinterpret_cast<const u32x4*>(p.v + (seq0 + key) * p.ldv + hc + piece * 8);
-    }
-  };
-  auto store_tile = [&](int slot) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = prow + 32 * i;
-      *reinterpret_cast<u32x4*>(&Ks[slot][row * kDH + ((piece ^ (row & 7)) << 3)]) = rk[i];
-      const int chunk = row >> 2, within = row & 3;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int d0 = piece * 8 + 2 * e, d1 = d0 + 1;
-        Vt[slot][d0 * kKB + ((chunk ^ (d0 & 15)) << 2) + within] = (bf16_t)(rv[i][e] & 0xffffu);
-        Vt[slot][d1 * kKB + ((chunk ^ (d1 & 15)) << 2) + within] = (bf16_t)(rv[i][e] >> 16);
-      }
+    for (int i = 0; i < PPT; ++i) {
+      const int row = drow + (NT / 8) * i;
+      const int key = min(t0 + row, p.T - 1);   // keys past T: finite row T-1, masked later
+      const int v_lp = ((((ps >> 1) ^ ((row >> 1) & 3))) << 1) | (ps & 1);
+      __builtin_amdgcn_global_load_lds(
+          p.k + (seq0 + key) * p.ldk + hc + k_lp * 8,
+          reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(
+              Ks + ((NT / 8) * i + wave * 8) * kDH)), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(
+          p.v + (seq0 + key) * p.ldv + hc + v_lp * 8,
+          reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(
+              Vs + ((NT / 8) * i + wave * 8) * kDH)), 16, 0, 0);
     }
   };
 
@@ -89,17 +104,25 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
     for (int qt = 0; qt < 2; ++qt) o[d][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
 
+  // transposed-read lane geometry: lane 4q'+p' of its 16-lane group addresses row q', cols 4p'
+  const int trq = fr >> 2, trp = fr & 3;
+
   const int ntiles = (p.T + kKB - 1) / kKB;
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
-
+  issue(0, 0);
+  if (ntiles > 1) issue(kKB, 1);
+  int slot = 0;
   for (int it = 0; it < ntiles; ++it) {
-    const int cur = it & 1;
     const int t0 = it * kKB;
-    if (it + 1 < ntiles) load_tile(t0 + kKB);
+    if (it + 1 < ntiles) {
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(PER) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    if (it + 2 < ntiles) issue(t0 + 2 * kKB, slot == 0 ? NS - 1 : slot - 1);
+    const bf16_t* Kc = smem + slot * 2 * TILE;
+    const bf16_t* Vc = Kc + TILE;
 
-    // S^T = K Q^T : 4 key tiles x 2 query tiles
+  // S^T = K Q^T : 4 key tiles x 2 query tiles
     f32x4 s[4][2];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
@@ -109,44 +132,55 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const bf16x8 kf = *reinterpret_cast<const bf16x8*>(
-            &Ks[cur][row * kDH + (((ks * 4 + g) ^ (row & 7)) << 3)]);
+            &Kc[row * kDH + (((ks * 4 + g) ^ (row & 7)) << 3)]);
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt)
           s[kt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt][ks], s[kt][qt], 0, 0, 0);
       }
     }
 
-    // online softmax per query column; P^T packed to bf16 B fragments
+    // online softmax per query column (scores kept unscaled: p = exp2(s*c - m*c), one FMA per
+    // score; key masking only on the ragged last tile; the running max is only raised — and O,
+    // l rescaled — when it grows by more than kRescale (log2 units): otherwise exp2 stays
+    // bounded by 2^kRescale and the stale max is exact for the final normalisation)
+    const bool ragged = t0 + kKB > p.T;
+    const float c = p.scale_log2;
     bf16x8 pf[2][2];
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       float mloc = -INFINITY;
+      if (ragged) {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (t0 + kt * 16 + 4 * g + j >= p.T) s[kt][qt][j] = -INFINITY;
+      }
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int key = t0 + kt * 16 + 4 * g + j;
-          const float v = key < p.T ? s[kt][qt][j] * p.scale_log2 : -INFINITY;
-          s[kt][qt][j] = v;
-          mloc = fmaxf(mloc, v);
-        }
+        for (int j = 0; j < 4; ++j) mloc = fmaxf(mloc, s[kt][qt][j]);
       mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
       mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-      const float m_new = fmaxf(m_run[qt], mloc);
-      const float alpha = exp2f(m_run[qt] - m_new);
-      m_run[qt] = m_new;
+      if (mloc * c > m_run[qt] * c + kRescale || m_run[qt] == -INFINITY) {   // wave-uniform per column group
+        const float m_new = fmaxf(m_run[qt], mloc);
+        const float alpha = fast_exp2((m_run[qt] - m_new) * c);
+        m_run[qt] = m_new;
+        l_run[qt] *= alpha;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) o[d][qt] *= alpha;
+      }
+      const float mc = m_run[qt] * c;
       float lsum = 0.f;
       float pv[4][4];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          pv[kt][j] = exp2f(s[kt][qt][j] - m_new);
+          pv[kt][j] = fast_exp2(fmaf(s[kt][qt][j], c, -mc));
           lsum += pv[kt][j];
         }
-      l_run[qt] = l_run[qt] * alpha + lsum;
-#pragma unroll
-      for (int d = 0; d < 4; ++d) o[d][qt] *= alpha;
+      l_run[qt] += lsum;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         u32x4 u;
@@ -158,24 +192,25 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
       }
     }
 
-    // O^T += V^T P^T
+    // O^T += V^T P^T, V^T fragments by hardware-transposed reads of the row-major V tile
+    const unsigned char* vb = reinterpret_cast<const unsigned char*>(Vc);
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-      const int dh = d * 16 + fr;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const int c0 = 8 * ks + g, c1 = 8 * ks + 4 + g;
-        const uint2 lo = *reinterpret_cast<const uint2*>(&Vt[cur][dh * kKB + ((c0 ^ (dh & 15)) << 2)]);
-        const uint2 hi = *reinterpret_cast<const uint2*>(&Vt[cur][dh * kKB + ((c1 ^ (dh & 15)) << 2)]);
-        const bf16x8 vf = as_bf16x8(u32x4{lo.x, lo.y, hi.x, hi.y});
+        const int r0 = 32 * ks + 4 * g + trq;
+        const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4i16*)(vb + v_off(r0, d * 16 + 4 * trp)));
+        const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4i16*)(vb + v_off(r0 + 16, d * 16 + 4 * trp)));
+        const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt)
           o[d][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qt][ks], o[d][qt], 0, 0, 0);
       }
     }
 
-    if (it + 1 < ntiles) store_tile(cur ^ 1);
-    __syncthreads();
+    slot = slot == NS - 1 ? 0 : slot + 1;
   }
 
   // normalise and write O[q][dh]: lane holds dh = d*16 + 4g + j for its query
@@ -212,7 +247,8 @@ extern "C" int aiko_attn_fwd(const void* q, const void* k, const void* v, void* 
   p.ldq = ldq; p.ldk = ldk; p.ldv = ldv; p.ldo = ldo;
   p.T = T; p.Tpad = Tpad; p.H = H;
   p.scale_log2 = scale * 1.4426950408889634f;
-  dim3 grid((T + aiko::kQB - 1) / aiko::kQB, H, B), block(256);
-  aiko::attn_fwd_kernel<<<grid, block, 0, stream>>>(p);
+  constexpr int NW = 8;
+  dim3 grid((T + 32 * NW - 1) / (32 * NW), H, B), block(64 * NW);
+  aiko::attn_fwd_kernel<NW><<<grid, block, 0, stream>>>(p);
   return (int)hipGetLastError();
 }

@@ -25,9 +25,17 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, b);
 }
 
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+
+// two floats -> packed bf16 pair with ONE v_cvt_pk_bf16_f32 (RNE, NaN-preserving)
 __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, bf16x2));
 }
+
+// raw v_exp_f32 (2^x): no denormal-range fix-up sequence; results below 2^-126 flush to 0,
+// which is what softmax wants
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll

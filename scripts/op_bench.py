@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Run one op repeatedly at Whisper-small encoder shapes (for rocprofv3 --pmc / timing).
+
+    python scripts/op_bench.py attn|gemm_qkv|gemm_fc2 [--batch 16] [--iters 20]
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("op")
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--tile", default=None)
+    a = ap.parse_args()
+    from aiko_services_amd.ops import require_native
+    from aiko_services_amd.ops import transformer as TR
+    require_native()
+    dev = "cuda"
+    B, T, Tp, H, d = a.batch, 1500, 1501, 12, 768
+    M = B * Tp
+    if a.op == "attn":
+        qkv = (torch.randn(M, 3 * d, device=dev) * 1.5).to(torch.bfloat16)
+        out = torch.empty(M, d, dtype=torch.bfloat16, device=dev)
+        fn = lambda: TR.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], out, B, H, T, Tp, 0.125)  # noqa: E731
+        flops = 4 * B * H * T * T * 64
+    else:
+        K, N = {"gemm_qkv": (d, 3 * d), "gemm_fc1": (d, 4 * d), "gemm_fc2": (4 * d, d), "gemm_out": (d, d)}[a.op]
+        x = torch.randn(M, K, device=dev)
+        xq, xs = TR.quantize_rows_ref(x.cpu())
+        xq, xs = xq.to(dev), xs.to(dev)
+        lin = TR.make_fp8_linear(torch.randn(N, K) / K ** 0.5, torch.zeros(N), dev)
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+        tile = tuple(int(v) for v in a.tile.split(",")) if a.tile else None
+        fn = lambda: TR.linear_fp8(xq, xs, lin, out=out, tile=tile)  # noqa: E731
+        flops = 2 * M * N * K
+    for _ in range(3):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.iters):
+        fn()
+    e1.record()
+    e1.synchronize()
+    us = e0.elapsed_time(e1) / a.iters * 1e3
+    print(f"{a.op}: {us:.1f} us  {flops / us / 1e6:.1f} TFLOP/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
