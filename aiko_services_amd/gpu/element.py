@@ -161,6 +161,7 @@ class GpuPipelineElement(PipelineElement):
         stream_name, found = self.get_parameter("hip_stream")
         self.hip_stream = named_stream(str(stream_name), self.device) if found and stream_name \
             and self.device.type == "cuda" else None
+        self.hip_stream_name = str(stream_name) if self.hip_stream is not None else "default"
         self._captured: dict = {}
         self.share["device"] = str(self.device)
         self._telemetry = {"frames": 0, "t0": time.perf_counter(), "t_last": 0.0, "n_last": 0}
@@ -220,9 +221,15 @@ class GpuPipelineElement(PipelineElement):
         now = time.perf_counter()
         if now - t["t_last"] < 1.0:
             return
+        from ..parallel import dist as D
+        comm = D.comm_bytes_total()
         if t["t_last"]:
-            self.share["gpu_fps"] = round((t["frames"] - t["n_last"]) / (now - t["t_last"]), 1)
-        t["t_last"], t["n_last"] = now, t["frames"]
+            dt = now - t["t_last"]
+            self.share["gpu_fps"] = round((t["frames"] - t["n_last"]) / dt, 1)
+            if comm:
+                self.share["rccl_mb"] = round(comm / 2**20, 1)
+                self.share["rccl_gbps"] = round((comm - t.get("comm_last", 0)) / dt / 1e9, 3)
+        t["t_last"], t["n_last"], t["comm_last"] = now, t["frames"], comm
         self.share["gpu_frames"] = t["frames"]
         self.share["gpu_host_ms"] = round(seconds * 1e3, 3)
         if self.device.type == "cuda":
@@ -233,6 +240,9 @@ class GpuPipelineElement(PipelineElement):
             self.share["frame_pool_free"] = pool.free_count()
 
     def gpu_timer_start(self):
+        """HIP event on the element's stream (the engine calls this after ``stream_enter``)."""
+        if self.device.type != "cuda":
+            return None
         start = torch.cuda.Event(enable_timing=True)
         start.record()
         return start
@@ -241,6 +251,7 @@ class GpuPipelineElement(PipelineElement):
         end = torch.cuda.Event(enable_timing=True)
         end.record()
         start._aiko_end = end
+        return end
 
     def start_stream(self, stream, stream_id):
         return StreamEvent.OKAY, None

@@ -13,8 +13,10 @@ from __future__ import annotations
 
 import os
 import threading
+import time
 from abc import ABC, abstractmethod
 
+from ..utils import fault as _fault
 from ..utils.configuration import get_mqtt_configuration
 from . import mqtt_codec as C
 from .mqtt_client import MQTTClient, MQTTMessage
@@ -107,6 +109,9 @@ class Loopback(Message):
             self.message_handler(self, None, MQTTMessage(topic, payload, 0, retain))
 
     def publish(self, topic, payload, retain=False, wait=False):
+        plan = _fault.active()
+        if plan is not None and plan.should_drop(topic):
+            return
         if isinstance(payload, str):
             payload = payload.encode("utf-8")
         self.bus.route(topic, bytes(payload or b""), retain)
@@ -168,10 +173,12 @@ class MQTT(Message):
         if not server_up:
             raise SystemError(f"Couldn't connect to MQTT server {self.host}:{self.port}")
         self.client = None
+        self._terminating = False
+        self.reconnects = 0
         self._connect()
 
     def _connect(self):
-        client = MQTTClient(on_message=self._on_message)
+        client = MQTTClient(on_message=self._on_message, on_disconnect=self._on_disconnect)
         if self.lwt:
             client.will_set(self.lwt[0], self.lwt[1], self.lwt[2])
         try:
@@ -183,9 +190,28 @@ class MQTT(Message):
         with self._lock:
             topics = list(self.topics_subscribe) if not isinstance(self.topics_subscribe, str) \
                 else [self.topics_subscribe]
+            topics += [t for t in self._subscribed if t not in topics]   # replay after a reconnect
             self._subscribed.clear()
         if topics:
             self.subscribe(topics)
+
+    def _on_disconnect(self, client, userdata, rc):
+        """Broker lost (rc != 0): reconnect in the background with capped exponential backoff
+        and replay every subscription (the reference left this as a TODO)."""
+        if rc == 0 or self._terminating or client is not self.client:
+            return
+        threading.Thread(target=self._reconnect_loop, name="aiko-mqtt-reconnect", daemon=True).start()
+
+    def _reconnect_loop(self):
+        delay = 0.2
+        while not self._terminating:
+            time.sleep(delay)
+            try:
+                self._connect()
+                self.reconnects += 1
+                return
+            except SystemError:
+                delay = min(delay * 2, 5.0)
 
     def _on_message(self, client, userdata, message):
         if self.message_handler:
@@ -195,6 +221,9 @@ class MQTT(Message):
         return self.client is not None and self.client.is_connected()
 
     def publish(self, topic, payload, retain=False, wait=False):
+        plan = _fault.active()
+        if plan is not None and plan.should_drop(topic):
+            return
         if self.client is None:
             return
         try:
@@ -230,6 +259,7 @@ class MQTT(Message):
         self._connect()
 
     def terminate(self):
+        self._terminating = True
         if self.client is not None:
             self.client.disconnect()
             self.client = None

@@ -12,6 +12,10 @@ otherwise (CPU tests).  The collectives used by the pipeline engines:
 
 xGMI on MI355X is point-to-point (7 links per GPU), so fan-out/fan-in is issued as grouped
 P2P (one transfer per link) rather than ring algorithms wherever only the root needs data.
+
+Every call is accounted in per-operation counters (calls, bytes moved by this rank) —
+``comm_stats()`` — which GPU elements publish in their EC share (``rccl_mb``, ``rccl_gbps``)
+and the tracer records as counter tracks (SURVEY §5.1 "RCCL bytes/latency counters").
 """
 from __future__ import annotations
 
@@ -23,9 +27,39 @@ import torch.distributed as tdist
 
 __all__ = ["init", "is_initialized", "world_size", "rank", "local_rank", "barrier", "broadcast",
            "all_gather_into", "send", "recv", "batch_p2p", "scatter_frames", "all_reduce_max",
-           "destroy", "backend"]
+           "destroy", "backend", "comm_stats", "comm_bytes_total", "reset_comm_stats"]
 
 _backend = None
+_comm: dict = {}          # op -> [calls, bytes]
+
+
+def _account(op: str, nbytes: int):
+    c = _comm.get(op)
+    if c is None:
+        c = _comm[op] = [0, 0]
+    c[0] += 1
+    c[1] += int(nbytes)
+    from ..utils.trace import get_tracer
+    tracer = get_tracer()
+    if tracer is not None:
+        tracer.counter("rccl_bytes", {op: c[1]})
+
+
+def _nbytes(t: torch.Tensor) -> int:
+    return t.numel() * t.element_size()
+
+
+def comm_stats() -> dict:
+    """{op: {"calls": n, "bytes": b}} for this rank since start / the last reset."""
+    return {op: {"calls": c, "bytes": b} for op, (c, b) in _comm.items()}
+
+
+def comm_bytes_total() -> int:
+    return sum(b for _, b in _comm.values())
+
+
+def reset_comm_stats():
+    _comm.clear()
 
 
 def is_initialized() -> bool:
@@ -80,6 +114,7 @@ def barrier():
 
 def broadcast(t: torch.Tensor, src: int = 0):
     if is_initialized():
+        _account("broadcast", _nbytes(t))
         tdist.broadcast(t, src)
     return t
 
@@ -89,21 +124,25 @@ def all_gather_into(out: torch.Tensor, t: torch.Tensor):
     if not is_initialized():
         out.copy_(t)
         return out
+    _account("all_gather", _nbytes(out))
     tdist.all_gather_into_tensor(out, t.contiguous())
     return out
 
 
 def all_reduce_max(t: torch.Tensor):
     if is_initialized():
+        _account("all_reduce", _nbytes(t))
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
     return t
 
 
 def send(t: torch.Tensor, dst: int):
+    _account("send", _nbytes(t))
     tdist.send(t, dst)
 
 
 def recv(t: torch.Tensor, src: int):
+    _account("recv", _nbytes(t))
     tdist.recv(t, src)
     return t
 
@@ -112,6 +151,8 @@ def batch_p2p(ops):
     """``ops`` = [("send"|"recv", tensor, peer), ...] issued as one grouped launch."""
     if not ops:
         return []
+    for kind, t, _ in ops:
+        _account(kind, _nbytes(t))
     p2p = [tdist.P2POp(tdist.isend if kind == "send" else tdist.irecv, t, peer) for kind, t, peer in ops]
     return tdist.batch_isend_irecv(p2p)
 

@@ -212,6 +212,14 @@ class StageLink:
             self._retire(slot)
 
 
+class StageFailure(RuntimeError):
+    """A neighbouring stage rank is gone (transport error on its link)."""
+
+    def __init__(self, peer: int, cause: BaseException):
+        super().__init__(f"pipeline-parallel stage rank {peer} failed: {cause}")
+        self.peer = peer
+
+
 class PipelineParallelRunner:
     """This rank's stage of a pipeline-parallel PipelineDefinition.
 
@@ -246,6 +254,8 @@ class PipelineParallelRunner:
         self._host_hdr = None
         self._host_slot = 0
         self._state_hdr = torch.zeros(HEADER, dtype=torch.int64, device=self.device)
+        self.healthy = True
+        self.failed_peer = None
 
     @property
     def is_first(self):
@@ -267,13 +277,36 @@ class PipelineParallelRunner:
         h.copy_(hdr, non_blocking=True)
         return h
 
-    def step(self, frame_data=None):
-        frame_data = dict(frame_data or {})
-        in_hdr = upstream = None
-        if self.prev is not None:
+    def _link_failed(self, peer: int, exc: BaseException):
+        """Health: a transport error on a stage link marks the peer absent — the
+        stage pipeline's lifecycle drops to "waiting" and its share names the failed rank — and
+        surfaces as ``StageFailure`` to the caller (which ends or re-forms the stream).  On RCCL
+        a dead peer shows up as a communicator error / watchdog timeout on the next wait; on
+        gloo as a closed connection."""
+        self.healthy = False
+        self.failed_peer = peer
+        share = getattr(self.pipeline, "ec_producer", None)
+        if share is not None:
+            share.update("lifecycle", "waiting")
+            share.update("stage_failed", peer)
+        raise StageFailure(peer, exc) from exc
+
+    def _recv_next(self):
+        try:
             slot = self._posted if self._posted is not None else self.prev.post_recv()
             in_hdr, bufs = self.prev.wait(slot)
             self._posted = self.prev.post_recv()      # next frame's transfer overlaps our compute
+        except RuntimeError as exc:
+            self._link_failed(self.rank - 1, exc)
+        return in_hdr, bufs
+
+    def step(self, frame_data=None):
+        if not self.healthy:
+            raise StageFailure(self.failed_peer, RuntimeError("stage link already failed"))
+        frame_data = dict(frame_data or {})
+        in_hdr = upstream = None
+        if self.prev is not None:
+            in_hdr, bufs = self._recv_next()
             frame_data.update(bufs)
             if self.is_last:
                 host = self._host_header(in_hdr)
@@ -293,7 +326,10 @@ class PipelineParallelRunner:
                 header.copy_(in_hdr, non_blocking=True)
                 if int(info["state"]) != 0:
                     header[1] = int(info["state"])
-            self.next.send(header, tensors)
+            try:
+                self.next.send(header, tensors)
+            except RuntimeError as exc:
+                self._link_failed(self.rank + 1, exc)
             return None
         if upstream is not None:
             # pinned int64 [frame_id, state, t_submit_ns, 0] of the frame as sent by stage 0 and

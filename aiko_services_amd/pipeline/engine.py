@@ -26,7 +26,7 @@ import threading
 import time
 import traceback
 from abc import abstractmethod
-from collections import OrderedDict
+from collections import OrderedDict, deque
 from typing import Tuple
 
 from ..control.share import services_cache_create_singleton
@@ -37,6 +37,8 @@ from ..runtime.context import Interface, compose_instance, pipeline_args, pipeli
 from ..runtime.lease import Lease
 from ..runtime.process import aiko
 from ..runtime.service import ServiceFilter, ServiceProtocol
+from ..utils import fault as _fault
+from ..utils import trace as _trace
 from ..utils.graph import Graph, Node
 from ..utils.misc import load_module
 from ..utils.sexpr import generate, parse
@@ -324,6 +326,7 @@ class PipelineImpl(Pipeline):
         self.stream_leases: dict = {}
         self.thread_local = threading.local()
         self.frames_completed = 0
+        self._latencies: deque = deque(maxlen=1024)     # recent frame latencies (s) -> p50 / p99
         self.pipeline_graph = self._create_pipeline_graph(context.definition)
         self.share["element_count"] = self.pipeline_graph.element_count
         self.share["streams"] = 0
@@ -342,6 +345,19 @@ class PipelineImpl(Pipeline):
         self.ec_producer.update("streams", len(self.stream_leases))
         self.ec_producer.update("streams_frames", frames)
         self.ec_producer.update("frames_completed", self.frames_completed)
+        stats = self.latency_stats()
+        if stats:
+            self.ec_producer.update("latency_p50_ms", stats["p50_ms"])
+            self.ec_producer.update("latency_p99_ms", stats["p99_ms"])
+
+    def latency_stats(self) -> dict:
+        """p50 / p99 / max over the last 1024 completed frames (first element to last)."""
+        lat = sorted(self._latencies)
+        if not lat:
+            return {}
+        pick = lambda q: lat[min(len(lat) - 1, int(q * len(lat)))] * 1e3
+        return {"frames": len(lat), "p50_ms": round(pick(0.50), 3), "p99_ms": round(pick(0.99), 3),
+                "max_ms": round(lat[-1] * 1e3, 3)}
 
     def _add_node_properties(self, node_name, properties, predecessor_name):
         d = self.definition
@@ -629,6 +645,8 @@ class PipelineImpl(Pipeline):
             if not metrics:
                 metrics["pipeline_elements"] = {}
                 metrics["time_pipeline_start"] = time.time()
+            tracer = _trace.get_tracer()
+            faults = _fault.active()
             frame_data_out = {} if new_frame else frame_data_in
             definition_pathname = self.share["definition_pathname"]
             for node in graph:
@@ -640,10 +658,14 @@ class PipelineImpl(Pipeline):
                 inputs = self._process_map_in(header, element, node.name, frame.swag)
                 if local:
                     start = time.time()
-                    gpu_t = element.gpu_timer_start() if _GPU_TIMING and hasattr(element, "gpu_timer_start") else None
+                    p_start = time.perf_counter() if tracer is not None else 0.0
                     enter = getattr(element, "stream_enter", None)
                     hip_ctx = enter(frame) if enter is not None else None
+                    gpu_t = element.gpu_timer_start() if (_GPU_TIMING or tracer is not None) \
+                        and hasattr(element, "gpu_timer_start") else None
                     try:
+                        if faults is not None:
+                            faults.before_element(element_name, frame_id)
                         stream_event, frame_data_out = element.process_frame(stream, **inputs)
                     except Exception:
                         self.logger.error("Exception in pipeline.process_frame() --> element.process_frame()")
@@ -651,6 +673,7 @@ class PipelineImpl(Pipeline):
                         frame_data_out = {"diagnostic": traceback.format_exc()}
                     if frame_data_out is None:
                         frame_data_out = {}
+                    gpu_end = element.gpu_timer_stop(gpu_t) if gpu_t is not None else None
                     if enter is not None:
                         element.stream_exit(frame, frame_data_out, hip_ctx)
                     stream.state = self._process_stream_event(element_name, stream_event, frame_data_out)
@@ -660,7 +683,13 @@ class PipelineImpl(Pipeline):
                     metrics["time_pipeline"] = t - metrics["time_pipeline_start"]
                     if gpu_t is not None:
                         metrics.setdefault("gpu_events", {})[element.name] = gpu_t
-                        element.gpu_timer_stop(gpu_t)
+                        if tracer is not None:
+                            tracer.gpu_span(element_name, gpu_t, gpu_end,
+                                            args={"frame_id": frame_id},
+                                            stream_name=getattr(element, "hip_stream_name", None) or "default")
+                    if tracer is not None:
+                        tracer.span(element_name, p_start, time.perf_counter(),
+                                    args={"stream_id": stream.stream_id, "frame_id": frame_id})
                     hook = getattr(element, "frame_done", None)
                     if hook is not None:
                         hook(t - start)
@@ -681,6 +710,14 @@ class PipelineImpl(Pipeline):
                 if join is not None:
                     join()
                 self.frames_completed += 1
+                latency = time.time() - metrics["time_pipeline_start"]
+                self._latencies.append(latency)
+                if faults is not None:
+                    faults.frame_completed()
+                if tracer is not None:
+                    end = time.perf_counter()
+                    tracer.span(f"frame {self.name}", end - latency, end, cat="frame",
+                                args={"stream_id": stream.stream_id, "frame_id": frame_id})
                 stream_info = {"stream_id": stream.stream_id, "frame_id": frame_id, "state": stream.state}
                 if stream.queue_response is not None:
                     if getattr(self, "response_swag", False):   # pipeline-parallel stage hand-off

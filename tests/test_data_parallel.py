@@ -63,7 +63,7 @@ def _worker(rank, world, port, mode, frames, results):
             assert info["state"] == 0, data
             r = data["detections"].wait()
             out.append((r["det"].tolist(), r["count"].tolist()))   # plain data: workers exit first
-        results.put((rank, out))
+        results.put((rank, (out, D.comm_stats())))
         D.barrier()
     finally:
         D.destroy()
@@ -76,6 +76,17 @@ def test_dp_fanout_gather(mode, world):
     results = ctx.SimpleQueue()
     mp.spawn(_worker, args=(world, _free_port(), mode, frames, results), nprocs=world, join=True)
     got = dict(results.get() for _ in range(world))
+    stats = {r: v[1] for r, v in got.items()}
+    got = {r: v[0] for r, v in got.items()}
+    frame_bytes = B * H * W * 3
+    for r, st in stats.items():   # RCCL byte counters: exact per-rank accounting
+        assert st["all_gather"]["calls"] >= frames
+        if mode == "broadcast":
+            assert st["broadcast"] == {"calls": frames, "bytes": frames * world * frame_bytes}
+        elif r == 0:
+            assert st["send"] == {"calls": frames * (world - 1), "bytes": frames * (world - 1) * frame_bytes}
+        else:
+            assert st["recv"] == {"calls": frames, "bytes": frames * frame_bytes}
     g = torch.Generator(device="cpu").manual_seed(SEED)
     pool = [torch.randint(0, 256, (world * B, H, W, 3), dtype=torch.uint8, generator=g) for _ in range(2)]
     for i in range(frames):

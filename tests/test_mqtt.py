@@ -1,12 +1,13 @@
 """In-repo MQTT 3.1.1 broker + client: pub/sub, wildcards, retained, LWT, QoS 1, topic trie."""
 import queue
 import socket
+import threading
 import time
 
 import pytest
 
 from aiko_services_amd.message import mqtt_codec as C
-from aiko_services_amd.message.mqtt_broker import start_broker_thread
+from aiko_services_amd.message.mqtt_broker import Broker, start_broker_thread
 from aiko_services_amd.message.mqtt_client import MQTTClient
 
 
@@ -122,3 +123,42 @@ def test_broker_throughput(broker):
     assert rate > 2000, rate
     sub.disconnect()
     pub.disconnect()
+
+
+def test_transport_reconnects_after_broker_loss(monkeypatch):
+    """Broker restart: the process transport reconnects with backoff and replays subscriptions
+    (the reference's MQTT class leaves reconnection as a TODO)."""
+    from aiko_services_amd.message.message import MQTT
+
+    b1, port = start_broker_thread("127.0.0.1", 0)
+    monkeypatch.setenv("AIKO_MQTT_HOST", "127.0.0.1")
+    monkeypatch.setenv("AIKO_MQTT_PORT", str(port))
+    got = queue.Queue()
+    t = MQTT(message_handler=lambda cl, ud, m: got.put(m.payload), topics_subscribe=["a/b"])
+    t.subscribe(["late/#"])
+    try:
+        b1.stop()
+        deadline = time.time() + 5
+        while t.is_connected() and time.time() < deadline:
+            time.sleep(0.05)
+        assert not t.is_connected()
+        b2 = Broker("127.0.0.1", port)
+        b2.bind()
+        threading.Thread(target=b2.serve_forever, daemon=True).start()
+        try:
+            deadline = time.time() + 10
+            while not t.is_connected() and time.time() < deadline:
+                time.sleep(0.05)
+            assert t.is_connected() and t.reconnects == 1
+            time.sleep(0.2)
+            pub, _ = _client(port)
+            pub.connect("127.0.0.1", port)
+            pub.publish("a/b", b"one")
+            pub.publish("late/x", b"two")
+            assert {got.get(timeout=5), got.get(timeout=5)} == {b"one", b"two"}
+            pub.disconnect()
+        finally:
+            t.terminate()
+            b2.stop()
+    finally:
+        t.terminate()

@@ -272,3 +272,63 @@ def test_reference_text_pipeline_runs(aiko_process, tmp_path, monkeypatch):
     written = sorted((tmp_path / "data_out").glob("out_*.txt"))
     assert len(written) == 3
     assert written[0].read_text() == (media / "data_in" / "in_00.txt").read_text().title()
+
+
+def test_trace_export_and_latency_stats(aiko_process, tmp_path):
+    """Chrome-trace export of frame / element spans and p50 / p99 latency."""
+    from aiko_services_amd.utils import trace
+    tracer = trace.enable_tracing()
+    try:
+        pipeline, q = _create(dict(DIAMOND, name="p_traced"), stream_id="7")
+        for i in range(4):
+            pipeline.create_frame({"stream_id": "7", "frame_id": i}, {"b": i})
+        for _ in range(4):
+            q.get(timeout=5)
+        path = tracer.export(str(tmp_path / "trace.json"))
+    finally:
+        trace.disable_tracing()
+    evs = json.load(open(path))["traceEvents"]
+    spans = [e for e in evs if e.get("ph") == "X"]
+    frames = [e for e in spans if e["cat"] == "frame" and e["args"]["stream_id"] == "7"]
+    elems = [e for e in spans if e["cat"] == "element" and e["args"]["stream_id"] == "7"]
+    assert len(frames) == 4 and len(elems) == 4 * 5
+    for f in frames:   # element spans nest inside their frame's span
+        inner = [e for e in elems if e["args"]["frame_id"] == f["args"]["frame_id"]]
+        assert all(f["ts"] - 1 <= e["ts"] and e["ts"] + e["dur"] <= f["ts"] + f["dur"] + 1 for e in inner)
+    stats = pipeline.latency_stats()
+    assert stats["frames"] >= 4 and 0 <= stats["p50_ms"] <= stats["p99_ms"] <= stats["max_ms"]
+    summary = tracer.summary()
+    assert summary["element:PE_1"]["count"] >= 4, summary
+
+
+def test_fault_injection_element_error_and_message_drop(aiko_process):
+    """Fault hooks (SURVEY §5.3): an injected element error takes the StreamEvent.ERROR path;
+    control messages matching a topic filter are dropped reproducibly."""
+    from aiko_services_amd.message import Loopback, LoopbackBus
+    from aiko_services_amd.pipeline.stream import StreamState
+    from aiko_services_amd.utils import fault
+    plan = fault.inject("error=PE_2@2")
+    try:
+        pipeline, q = _create(dict(DIAMOND, name="p_fault"), stream_id="5")
+        pipeline.create_frame({"stream_id": "5", "frame_id": 1}, {"b": 1})
+        info, data = q.get(timeout=5)
+        assert info["state"] == 0 and data["f"] == 6
+        pipeline.create_frame({"stream_id": "5", "frame_id": 2}, {"b": 2})
+        info, data = q.get(timeout=5)
+        assert info["state"] == StreamState.ERROR and "injected fault" in data["diagnostic"]
+        assert plan.frames_seen >= 2
+    finally:
+        fault.clear()
+    bus = LoopbackBus()
+    got = []
+    rx = Loopback(message_handler=lambda c, u, m: got.append(m.topic), topics_subscribe=["t/#"], bus=bus)
+    tx = Loopback(bus=bus)
+    plan = fault.inject("drop=0.5@t/lossy", seed=3)
+    try:
+        for _ in range(200):
+            tx.publish("t/lossy", "x")
+            tx.publish("t/safe", "x")
+    finally:
+        fault.clear()
+    assert got.count("t/safe") == 200
+    assert got.count("t/lossy") == 200 - plan.dropped and 60 < plan.dropped < 140

@@ -96,3 +96,49 @@ def test_pipeline_parallel_gloo(world, drop_every):
         assert stamped
         dropped = drop_every and fid % drop_every == drop_every - 1
         assert state == (1 if dropped else 0), (fid, state)
+
+
+def _fault_worker(rank, world, port, results):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                       "AIKO_MQTT_DISABLE": "1", "AIKO_LOG_MQTT": "false", "AIKO_LOG_LEVEL": "ERROR"})
+    from aiko_services_amd.parallel import dist as D
+    from aiko_services_amd.parallel.pipeline_parallel import PipelineParallelRunner, StageFailure
+    from aiko_services_amd.utils import fault
+    D.init("gloo", timeout_s=30)
+    if rank == 1:
+        fault.inject("kill=3")            # the middle stage dies after its 3rd frame
+    d = parse_pipeline_definition_dict(_definition(batch=64, size=64))
+    runner = PipelineParallelRunner(d, device="cpu", depth=2)
+    ok = 0
+    try:
+        for _ in range(200):
+            runner.step({})
+            ok += 1
+        results.put((rank, "no failure", ok))
+    except StageFailure as exc:
+        share = runner.pipeline.share
+        results.put((rank, exc.peer, ok, share["lifecycle"], share.get("stage_failed")))
+    os._exit(0)                          # the group is broken: skip the collective teardown
+
+
+def test_stage_rank_failure_detected():
+    """Fault injection (kill a stage rank): both neighbours observe StageFailure naming it."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    results = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fault_worker, args=(r, world, port, results)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    from aiko_services_amd.utils.fault import KILL_EXIT_CODE
+    assert procs[1].exitcode == KILL_EXIT_CODE
+    got = {}
+    while not results.empty():
+        r = results.get()
+        got[r[0]] = r[1:]
+    assert got[0][0] == 1 and got[0][2:] == ("waiting", 1), got
+    assert got[2][0] == 1 and got[2][2:] == ("waiting", 1), got
+    assert got[2][1] <= 3
