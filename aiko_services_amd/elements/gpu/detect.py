@@ -89,7 +89,8 @@ class YoloDetector(GpuPipelineElement):
                             conf=float(p("conf", 0.25)), iou=float(p("iou", 0.7)),
                             max_det=_int(p("max_det", 300), 300),
                             max_candidates=_int(p("max_candidates", 1024), 1024))
-        self.autotune = _bool(p("autotune", True))
+        self.load_model_weights(self.model)
+        self.autotune = _bool(p("autotune", self.gpu_config.autotune))
         self._tuned = set()
 
     def _run(self, images):

@@ -104,6 +104,7 @@ class WhisperEncoder(GpuPipelineElement):
         require_native()
         self.model = Model(size=str(_p(self, "size", "small")), seed=int(_p(self, "seed", 0)),
                            device=self.device)
+        self.load_model_weights(self.model)
         self._tuned = set()
 
     def _run(self, audio):
@@ -113,7 +114,10 @@ class WhisperEncoder(GpuPipelineElement):
         key = (tuple(audio.shape),)
         if key not in self._tuned:
             from ...ops import conv as C
-            with C.autotune():
+            if str(_p(self, "autotune", self.gpu_config.autotune)).lower() in ("true", "1", "yes"):
+                with C.autotune():
+                    self._run(audio)
+            else:
                 self._run(audio)
             self._tuned.add(key)
         return StreamEvent.OKAY, {"features": self.run_maybe_captured(key, self._run, audio)}

@@ -113,7 +113,8 @@ class ResNet50Classifier(GpuPipelineElement):
         seed = _int(self.get_parameter("seed", 0)[0], 0)
         self.model = ResNet50(seed=seed, device=self.device,
                               image_size=_int(self.get_parameter("image_size", 224)[0], 224))
-        tune, _ = self.get_parameter("autotune", default=True)
+        self.load_model_weights(self.model)
+        tune, _ = self.get_parameter("autotune", default=self.gpu_config.autotune)
         self.autotune = str(tune).lower() in ("true", "1", "yes")
         self._tuned = set()
 

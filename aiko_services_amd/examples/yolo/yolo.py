@@ -47,6 +47,7 @@ class YoloDetector(GpuPipelineElement):
             self.model = YOLOv8(scale=str(p("scale", "n")), device=self.device,
                                 image_size=int(p("image_size", 640)), conf=float(p("conf", 0.25)),
                                 iou=float(p("iou", 0.7)), max_det=int(p("max_det", 300)))
+            self.load_model_weights(self.model)
         return self.model
 
     def start_stream(self, stream, stream_id):

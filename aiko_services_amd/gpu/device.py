@@ -1,7 +1,8 @@
 """GPU device binding for GPU-resident actors: one process per MI355X.
 
 ``select_device()`` resolves the device of this process (``AIKO_GPU_DEVICE`` >
-``LOCAL_RANK`` > 0), binds it, and returns a ``torch.device``.  ``require_gpu()`` fails loudly
+``AIKO_GPU_DEVICE_MAP[LOCAL_RANK]`` > ``LOCAL_RANK`` > 0), binds it, applies
+``AIKO_GPU_MEMORY_FRACTION`` and returns a ``torch.device``.  ``require_gpu()`` fails loudly
 when no HIP device is visible — GPU elements never silently fall back to the CPU.
 """
 from __future__ import annotations
@@ -9,6 +10,8 @@ from __future__ import annotations
 import os
 
 import torch
+
+from ..utils.configuration import get_gpu_configuration
 
 __all__ = ["select_device", "require_gpu", "gpu_available", "parse_device", "device_info"]
 
@@ -41,9 +44,12 @@ def select_device() -> torch.device:
     global _selected
     if _selected is None:
         require_gpu()
-        idx = os.environ.get("AIKO_GPU_DEVICE", os.environ.get("LOCAL_RANK", "0"))
-        idx = int(idx) % max(1, torch.cuda.device_count())
+        cfg = get_gpu_configuration()
+        idx = cfg.device_for_local_rank(int(os.environ.get("LOCAL_RANK", "0")))
+        idx = idx % max(1, torch.cuda.device_count())
         torch.cuda.set_device(idx)
+        if cfg.memory_fraction < 1.0:
+            torch.cuda.set_per_process_memory_fraction(cfg.memory_fraction, idx)
         _selected = torch.device("cuda", idx)
     return _selected
 

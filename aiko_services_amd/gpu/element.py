@@ -21,6 +21,7 @@ import torch
 
 from ..pipeline.engine import PipelineElement
 from ..pipeline.stream import StreamEvent
+from ..utils.configuration import get_gpu_configuration
 from .device import parse_device, require_gpu
 
 __all__ = ["GpuPipelineElement", "DeviceResult", "FramePool", "CapturedCall"]
@@ -154,7 +155,8 @@ class GpuPipelineElement(PipelineElement):
         self.device = parse_device(device_spec)
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
-        graph, _ = self.get_parameter("graph", default=False)
+        self.gpu_config = get_gpu_configuration()
+        graph, _ = self.get_parameter("graph", default=self.gpu_config.graph)
         self.use_graph = str(graph).lower() in ("true", "1", "yes")
         # optional dedicated HIP stream (parameter "hip_stream": name): independent graph branches
         # on different streams run concurrently on the GPU; joins use events
@@ -165,6 +167,15 @@ class GpuPipelineElement(PipelineElement):
         self._captured: dict = {}
         self.share["device"] = str(self.device)
         self._telemetry = {"frames": 0, "t0": time.perf_counter(), "t_last": 0.0, "n_last": 0}
+
+    def load_model_weights(self, model):
+        """Element parameter ``weights``: a safetensors file written by ``model.save()`` (packed
+        weights + fp8 scale tables); without it the model keeps its seeded random init."""
+        path, found = self.get_parameter("weights")
+        if found and path:
+            model.load(str(path))
+            self.share["weights"] = str(path)
+        return model
 
     def run_maybe_captured(self, key, fn, *inputs):
         if not self.use_graph:

@@ -123,7 +123,7 @@ class Broker:
         self.stats["connections"] += 1
 
     def _close(self, conn: _Conn, send_will: bool):
-        if conn.sock not in self.conns:
+        if self.conns.pop(conn.sock, None) is None:      # also guards re-entry via the will
             return
         if send_will and conn.will is not None:
             topic, payload, qos, retain = conn.will
@@ -137,7 +137,6 @@ class Broker:
             self.sel.unregister(conn.sock)
         except (KeyError, ValueError):
             pass
-        del self.conns[conn.sock]
         try:
             conn.sock.close()
         except OSError:

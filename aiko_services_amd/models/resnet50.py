@@ -22,6 +22,7 @@ from dataclasses import dataclass
 import torch
 
 from ..ops import conv as C
+from .weights import WeightsMixin
 from ..ops import vision as V
 
 STAGES = ((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2))
@@ -51,7 +52,7 @@ class Bottleneck:
     fused: C.ConvSpec | None = None   # conv3 + projection shortcut as one K-concatenated igemm
 
 
-class ResNet50:
+class ResNet50(WeightsMixin):
     """Packed ResNet-50 for inference.  ``forward(frames_u8) -> (top-k probs, top-k ids)``."""
 
     def __init__(self, num_classes: int = 1000, seed: int = 0, device="cuda", image_size=224,
@@ -191,20 +192,23 @@ class ResNet50:
         total += 2 * 2048 * self.num_classes
         return total
 
-    def state_dict(self) -> dict:
-        """Packed weights (bf16 [Cout, K]) and fp32 biases, for save/load of random inits."""
-        sd = {}
-        for name, spec in self.conv_specs():
-            sd[f"{name}.weight"] = spec.weight.detach().cpu()
-            if spec.bias is not None:
-                sd[f"{name}.bias"] = spec.bias.detach().cpu()
-        return sd
+    def named_layers(self):
+        return self.conv_specs()
 
-    def load_state_dict(self, sd: dict) -> None:
-        for name, spec in self.conv_specs():
-            spec.weight.copy_(sd[f"{name}.weight"].to(spec.weight.device))
-            if spec.bias is not None:
-                spec.bias.copy_(sd[f"{name}.bias"].to(spec.bias.device))
+    def config(self) -> dict:
+        return {"num_classes": self.num_classes, "image_size": self.image_size, "topk": self.topk}
+
+    def _weights_loaded(self):
+        """Re-derive the K-concatenated conv3 + shortcut specs from the loaded layers."""
+        for b in self.blocks:
+            if b.fused is None:
+                continue
+            k1 = b.conv3.weight.shape[1]
+            b.fused.weight[:, :k1].copy_(b.conv3.weight)
+            b.fused.weight[:, k1:].copy_(b.down.weight)
+            if b.fused.bias is not None:
+                b.fused.bias.copy_((b.conv3.bias if b.conv3.bias is not None else 0)
+                                   + (b.down.bias if b.down.bias is not None else 0))
 
     # ---- fp32 torch reference (tests only) -------------------------------------------------
     def reference_logits(self, frames: torch.Tensor) -> torch.Tensor:

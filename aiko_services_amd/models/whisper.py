@@ -27,6 +27,7 @@ import torch
 
 from ..ops import audio as AU
 from ..ops import conv as C
+from .weights import WeightsMixin
 from ..ops import transformer as TR
 
 # name: (d_model, layers, heads)
@@ -53,7 +54,7 @@ class Block:
     fc2: TR.Fp8Linear
 
 
-class WhisperEncoder:
+class WhisperEncoder(WeightsMixin):
     """``encode(audio [B, N] fp32 16 kHz) -> bf16 [B, T, d_model]``, T = N / 320 (1500 for 30 s)."""
 
     def __init__(self, size: str = "small", seed: int = 0, device="cuda", n_ctx: int = N_CTX):
@@ -92,6 +93,22 @@ class WhisperEncoder:
         self.ln_post = ((1.0 + 0.1 * torch.randn(d, generator=g)).to(dev), small(d).to(dev))
         self._ws: dict = {}
         self._pos_ready: set = set()
+
+    # ---- weights ---------------------------------------------------------------------------------
+    def named_layers(self):
+        yield "conv1", self.conv1
+        yield "conv2", self.conv2
+        for i, b in enumerate(self.blocks):
+            yield f"blocks.{i}.ln1", b.ln1
+            yield f"blocks.{i}.qkv", b.qkv
+            yield f"blocks.{i}.out", b.out
+            yield f"blocks.{i}.ln2", b.ln2
+            yield f"blocks.{i}.fc1", b.fc1
+            yield f"blocks.{i}.fc2", b.fc2
+        yield "ln_post", self.ln_post
+
+    def config(self) -> dict:
+        return {"size": self.size, "n_ctx": self.n_ctx}
 
     # ---- workspace ------------------------------------------------------------------------------
     def _buf(self, key, shape, dtype=torch.bfloat16, zero=False):

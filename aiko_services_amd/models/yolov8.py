@@ -26,6 +26,7 @@ from dataclasses import dataclass, field
 import torch
 
 from ..ops import conv as C
+from .weights import WeightsMixin
 from ..ops import detect as DT
 from ..ops import vision as V
 
@@ -89,7 +90,7 @@ class DetectLevel:
     first: C.ConvSpec  # box[0] | cls[0] fused along Cout
 
 
-class YOLOv8:
+class YOLOv8(WeightsMixin):
     """Packed YOLOv8 detector.  ``detect(frames_u8) -> (det [B, max_det, 6], count [B])``."""
 
     def __init__(self, scale: str = "n", num_classes: int = 80, seed: int = 0, device="cuda",
@@ -266,6 +267,22 @@ class YOLOv8:
     __call__ = detect
 
     # ---- bookkeeping ----------------------------------------------------------------------------
+    def named_layers(self):
+        return self.conv_specs()
+
+    def config(self) -> dict:
+        return {"scale": self.scale, "num_classes": self.nc, "image_size": self.image_size}
+
+    def _weights_loaded(self):
+        """Re-derive each head level's fused box|cls first conv from the loaded layers."""
+        for lvl in self.heads:
+            a, b = lvl.box[0], lvl.cls[0]
+            lvl.first.weight[:a.cout].copy_(a.weight)
+            lvl.first.weight[a.cout:].copy_(b.weight)
+            if lvl.first.bias is not None:
+                lvl.first.bias[:a.cout].copy_(a.bias)
+                lvl.first.bias[a.cout:].copy_(b.bias)
+
     def conv_specs(self):
         yield "l0", self.l0
         for name in ("l1", "l3", "l5", "l7", "l16", "l19"):

@@ -82,7 +82,7 @@ def backend():
     return _backend
 
 
-def init(backend_name: str | None = None, timeout_s: float = 600.0) -> bool:
+def init(backend_name: str | None = None, timeout_s: float | None = None) -> bool:
     """Initialise from the environment when WORLD_SIZE > 1; returns True if distributed."""
     global _backend
     if is_initialized():
@@ -92,11 +92,15 @@ def init(backend_name: str | None = None, timeout_s: float = 600.0) -> bool:
         return False
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29500")
+    from ..utils.configuration import get_gpu_configuration
+    cfg = get_gpu_configuration()
     if backend_name is None:
-        backend_name = "nccl" if torch.cuda.is_available() else "gloo"
+        backend_name = cfg.comm_backend or ("nccl" if torch.cuda.is_available() else "gloo")
+    if timeout_s is None:
+        timeout_s = cfg.comm_timeout_s
     kwargs = {}
     if backend_name == "nccl":
-        dev = torch.device("cuda", local_rank() % max(1, torch.cuda.device_count()))
+        dev = torch.device("cuda", cfg.device_for_local_rank(local_rank()) % max(1, torch.cuda.device_count()))
         torch.cuda.set_device(dev)
         kwargs["device_id"] = dev
     tdist.init_process_group(backend=backend_name, timeout=datetime.timedelta(seconds=timeout_s), **kwargs)

@@ -229,10 +229,13 @@ class PipelineParallelRunner:
     one frame ahead so the xGMI transfer of frame k+1 overlaps this stage's compute of frame k.
     """
 
-    def __init__(self, definition: PipelineDefinition, device=None, depth: int = 2,
+    def __init__(self, definition: PipelineDefinition, device=None, depth: int | None = None,
                  stream_id: str = "pp"):
         from ..pipeline.engine import PipelineImpl
         self.rank, self.world = D.rank(), D.world_size()
+        if depth is None:
+            from ..utils.configuration import get_gpu_configuration
+            depth = get_gpu_configuration().pp_depth
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
                 else torch.device("cpu")

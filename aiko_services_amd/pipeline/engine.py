@@ -39,6 +39,7 @@ from ..runtime.process import aiko
 from ..runtime.service import ServiceFilter, ServiceProtocol
 from ..utils import fault as _fault
 from ..utils import trace as _trace
+from ..utils.configuration import get_gpu_configuration
 from ..utils.graph import Graph, Node
 from ..utils.misc import load_module
 from ..utils.sexpr import generate, parse
@@ -57,7 +58,7 @@ PROTOCOL_PIPELINE = f"{ServiceProtocol.AIKO}/{ACTOR_TYPE_PIPELINE}:{_VERSION}"
 PROTOCOL_ELEMENT = f"{ServiceProtocol.AIKO}/{ACTOR_TYPE_ELEMENT}:{_VERSION}"
 GRACE_TIME = 60
 STATUS_UPDATE_PERIOD = 3.0
-_GPU_TIMING = os.environ.get("AIKO_GPU_TIMING", "0") == "1"
+_GPU_TIMING = get_gpu_configuration().timing
 
 _LOGGER = aiko.logger(__name__)
 

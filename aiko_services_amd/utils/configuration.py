@@ -11,6 +11,7 @@ started on request (:func:`bootstrap_start`).
 from __future__ import annotations
 
 import getpass
+from dataclasses import dataclass
 import os
 import secrets
 import socket
@@ -19,7 +20,7 @@ import threading
 __all__ = [
     "create_password", "get_hostname", "get_mqtt_configuration", "get_mqtt_host",
     "get_mqtt_port", "get_namespace", "get_namespace_prefix", "get_pid", "get_username",
-    "bootstrap_start", "get_lan_ip_address",
+    "bootstrap_start", "get_lan_ip_address", "GpuConfiguration", "get_gpu_configuration",
 ]
 
 AIKO_BOOTSTRAP_UDP_PORT = 4149
@@ -144,3 +145,64 @@ def bootstrap_start(port: int = AIKO_BOOTSTRAP_UDP_PORT) -> socket.socket:
     sock.bind(("0.0.0.0", port))
     threading.Thread(target=_bootstrap_loop, args=(sock,), daemon=True).start()
     return sock
+
+
+# ---- GPU data-plane settings (AIKO_GPU_*; SURVEY §5.6 "add AIKO_GPU_*") ------------------
+
+@dataclass(frozen=True)
+class GpuConfiguration:
+    """Process-wide defaults for the GPU data plane; element / definition parameters override.
+
+    ========================  =========================================================  =======
+    variable                  meaning                                                    default
+    ========================  =========================================================  =======
+    AIKO_GPU_DEVICE           device index of this process (else LOCAL_RANK)             LOCAL_RANK
+    AIKO_GPU_DEVICE_MAP       comma list: local rank -> device index ("0,2,4,6")         identity
+    AIKO_GPU_MEMORY_FRACTION  cap on this process's share of HBM (0 < f <= 1)            1.0
+    AIKO_GPU_GRAPH            capture GPU elements into hipGraphs by default             false
+    AIKO_GPU_AUTOTUNE         measure kernel tiles / variants on first use               true
+    AIKO_GPU_TIMING           HIP-event timing per element into frame.metrics            false
+    AIKO_GPU_PP_DEPTH         pipeline-parallel slot-ring depth per stage link           2
+    AIKO_GPU_COMM_BACKEND     torch.distributed backend (nccl = RCCL on ROCm, or gloo)   auto
+    AIKO_GPU_COMM_TIMEOUT     collective / P2P timeout in seconds                        600
+    ========================  =========================================================  =======
+    """
+    device: int | None = None
+    device_map: tuple = ()
+    memory_fraction: float = 1.0
+    graph: bool = False
+    autotune: bool = True
+    timing: bool = False
+    pp_depth: int = 2
+    comm_backend: str | None = None
+    comm_timeout_s: float = 600.0
+
+    def device_for_local_rank(self, local_rank: int) -> int:
+        if self.device is not None:
+            return self.device
+        if self.device_map:
+            return self.device_map[local_rank % len(self.device_map)]
+        return local_rank
+
+
+def _env_bool(name: str, default: bool) -> bool:
+    v = os.environ.get(name)
+    return default if v is None else v.strip().lower() in ("1", "true", "yes", "on")
+
+
+def get_gpu_configuration() -> GpuConfiguration:
+    dev = os.environ.get("AIKO_GPU_DEVICE")
+    dmap = os.environ.get("AIKO_GPU_DEVICE_MAP", "")
+    frac = float(os.environ.get("AIKO_GPU_MEMORY_FRACTION", "1.0"))
+    if not 0.0 < frac <= 1.0:
+        raise ValueError(f"AIKO_GPU_MEMORY_FRACTION must be in (0, 1], not {frac}")
+    return GpuConfiguration(
+        device=int(dev) if dev not in (None, "") else None,
+        device_map=tuple(int(x) for x in dmap.split(",") if x.strip()),
+        memory_fraction=frac,
+        graph=_env_bool("AIKO_GPU_GRAPH", False),
+        autotune=_env_bool("AIKO_GPU_AUTOTUNE", True),
+        timing=_env_bool("AIKO_GPU_TIMING", False),
+        pp_depth=int(os.environ.get("AIKO_GPU_PP_DEPTH", "2")),
+        comm_backend=os.environ.get("AIKO_GPU_COMM_BACKEND") or None,
+        comm_timeout_s=float(os.environ.get("AIKO_GPU_COMM_TIMEOUT", "600")))

@@ -165,3 +165,18 @@ def test_example_yolo_element_overlay(native):
     assert len(ov["objects"]) == len(ov["rectangles"])
     for r in ov["rectangles"]:
         assert r["w"] >= 0 and r["h"] >= 0 and 0 <= r["x"] <= 640
+
+
+def test_yolo_weights_roundtrip_bit_exact(native, tmp_path):
+    """save() on one seed, load() into another: identical detections (packed weights + the
+    re-derived fused head convs)."""
+    from aiko_services_amd.models.yolov8 import YOLOv8
+    a = YOLOv8(scale="n", seed=0, device=DEV, image_size=320)
+    b = YOLOv8(scale="n", seed=7, device=DEV, image_size=320)
+    path = str(tmp_path / "yolo.safetensors")
+    a.save(path)
+    frames = torch.randint(0, 256, (2, 240, 320, 3), dtype=torch.uint8, device=DEV)
+    det_a, cnt_a = (t.clone() for t in a.detect(frames))
+    b.load(path)
+    det_b, cnt_b = b.detect(frames)
+    assert torch.equal(cnt_a, cnt_b) and torch.equal(det_a, det_b)

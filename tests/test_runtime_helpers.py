@@ -4,3 +4,4 @@
 class GreeterImpl:
     def greet(self, name):
         return f"default {name}"
+
