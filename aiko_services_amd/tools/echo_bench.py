@@ -28,14 +28,14 @@ from pathlib import Path
 DEFS = Path(__file__).resolve().parent.parent / "examples" / "pipeline" / "definitions"
 
 
-def _parent(frames: int, window: int, timeout: float):
+def _parent(frames: int, window: int, timeout: float, definition: str | None = None, expect: int = 3):
     import aiko_services_amd as aiko
     from aiko_services_amd.pipeline.definition import parse_pipeline_definition
     from aiko_services_amd.pipeline.engine import PipelineImpl
     from aiko_services_amd.runtime import event
 
     q: queue.Queue = queue.Queue()
-    path = str(DEFS / "echo_parent.json")
+    path = definition or str(DEFS / "echo_parent.json")
     definition = parse_pipeline_definition(path)
     pipeline = PipelineImpl.create_pipeline(path, definition, None, None, "1", [], 0, None, 600,
                                             queue_response=q)
@@ -62,7 +62,7 @@ def _parent(frames: int, window: int, timeout: float):
                 result["error"] = f"timeout after {len(rtts)} frames"
                 break
             rtts.append(time.perf_counter() - t_sent.pop(int(info["frame_id"])))
-            if int(data.get("i", -1)) != 3:
+            if int(data.get("i", -1)) != expect:
                 result["error"] = f"bad echo payload {data}"
         elapsed = time.perf_counter() - t0
         if rtts:
@@ -78,7 +78,9 @@ def _parent(frames: int, window: int, timeout: float):
     pipeline.run(mqtt_connection_required=True)
 
 
-def orchestrate(frames=2000, window=8, timeout=60.0, broker_port=None):
+def orchestrate(frames=2000, window=8, timeout=60.0, broker_port=None, parent=None, children=None,
+                expect=3):
+    """Registrar + child pipeline processes + a parent driving ``frames`` through the chain."""
     from aiko_services_amd.message.mqtt_broker import start_broker_thread
     broker = None
     if broker_port is None:
@@ -92,11 +94,15 @@ def orchestrate(frames=2000, window=8, timeout=60.0, broker_port=None):
     try:
         procs.append(subprocess.Popen([sys.executable, "-m", "aiko_services_amd.tools.registrar"], env=env))
         time.sleep(0.5)
-        procs.append(subprocess.Popen([sys.executable, "-m", "aiko_services_amd.pipeline.cli", "create",
-                                       str(DEFS / "echo_child.json")], env=env))
-        parent = subprocess.run([sys.executable, "-m", "aiko_services_amd.tools.echo_bench", "--role", "parent",
-                                 "--frames", str(frames), "--window", str(window), "--timeout", str(timeout)],
-                                env=env, capture_output=True, text=True, timeout=timeout + 30)
+        for child in children or [str(DEFS / "echo_child.json")]:
+            procs.append(subprocess.Popen([sys.executable, "-m", "aiko_services_amd.pipeline.cli", "create",
+                                           str(child)], env=env))
+        cmd = [sys.executable, "-m", "aiko_services_amd.tools.echo_bench", "--role", "parent",
+               "--frames", str(frames), "--window", str(window), "--timeout", str(timeout),
+               "--expect", str(expect)]
+        if parent:
+            cmd += ["--definition", str(parent)]
+        parent = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout + 30)
         for line in parent.stdout.splitlines():
             if line.startswith("ECHO_RESULT "):
                 return json.loads(line[len("ECHO_RESULT "):])
@@ -119,9 +125,11 @@ def main(argv=None):
     ap.add_argument("--frames", type=int, default=2000)
     ap.add_argument("--window", type=int, default=8)
     ap.add_argument("--timeout", type=float, default=60.0)
+    ap.add_argument("--definition", default=None, help="(parent role) parent pipeline definition")
+    ap.add_argument("--expect", type=int, default=3, help="(parent role) expected 'i' at the end")
     a = ap.parse_args(argv)
     if a.role == "parent":
-        _parent(a.frames, a.window, a.timeout)
+        _parent(a.frames, a.window, a.timeout, a.definition, a.expect)
     else:
         res = orchestrate(a.frames, a.window, a.timeout)
         res.update({"metric": "two-process echo pipeline frames/s over MQTT (config 1)",

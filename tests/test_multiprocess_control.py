@@ -118,3 +118,12 @@ def test_aloha_honua_actor_over_mqtt(cluster):
         assert r.returncode == 0, r.stderr
     out = _snapshot(cluster, service="aloha_honua", expect=("greetings = 2",))
     assert "greetings = 2" in out, out
+
+
+def test_multitude_chain_three_processes():
+    """The reference's multitude load test topology: a chain of pipeline processes, each
+    stage's last element remote-bound (via the registrar) to the next process."""
+    from aiko_services_amd.examples.pipeline.multitude.chain import run
+    res = run(processes=3, elements=2, frames=100, window=4, timeout=60)
+    assert "error" not in res, res
+    assert res["frames"] == 100 and res["frames_per_s"] > 50

@@ -332,3 +332,33 @@ def test_fault_injection_element_error_and_message_drop(aiko_process):
         fault.clear()
     assert got.count("t/safe") == 200
     assert got.count("t/lossy") == 200 - plan.dropped and 60 < plan.dropped < 140
+
+
+EXAMPLES = Path(__file__).resolve().parents[1] / "aiko_services_amd/examples/pipeline/definitions"
+
+
+def _load_example(name):
+    return parse_pipeline_definition_dict(json.loads((EXAMPLES / name).read_text()), str(EXAMPLES / name))
+
+
+def test_example_definitions_run(aiko_process):
+    """The shipped example definitions (no reference checkout needed)."""
+    import numpy as np
+    p, q = _create(_load_example("diamond.json"), name="ex_diamond", stream_id="11")
+    p.create_frame({"stream_id": "11", "frame_id": 0}, {"a": 1})
+    info, data = q.get(timeout=5)
+    assert info["state"] == 0 and data["f"] == 2 * (1 + 1 + 10 + 1)
+    for head, expect in (("PE_IN", "x:in:text:out"), ("PE_IN_B", "x:in:out")):
+        p, q = _create(_load_example("graph_paths.json"), name=f"ex_paths_{head}", stream_id="12",
+                       graph_path=head)
+        p.create_frame({"stream_id": "12", "frame_id": 0}, {"in_a": "x"})
+        info, data = q.get(timeout=5)
+        assert data["out_c"] == expect, (head, data)
+    p, q = _create(_load_example("name_mapping.json"), name="ex_mapping", stream_id="13")
+    outs = [q.get(timeout=10) for _ in range(5)]
+    assert all(0 <= int(d["i"]) - 1 <= 9 for _, d in outs)
+    p, q = _create(_load_example("codec.json"), name="ex_codec", stream_id="14")
+    arr = np.arange(12, dtype=np.float32).reshape(3, 4)
+    p.create_frame({"stream_id": "14", "frame_id": 0}, {"data": arr})
+    info, data = q.get(timeout=5)
+    assert np.array_equal(data["data"], arr)
