@@ -19,8 +19,8 @@ try:
 except ImportError:  # pragma: no cover
     _PIL = False
 
-__all__ = ["ImageOutput", "ImageOverlay", "ImageReadFile", "ImageResize", "ImageWriteFile",
-           "to_numpy_rgb"]
+__all__ = ["ImageOutput", "ImageOverlay", "ImageReadFile", "ImageResize", "ImageSynthetic",
+           "ImageWriteFile", "to_numpy_rgb"]
 
 
 def to_numpy_rgb(image) -> np.ndarray:
@@ -88,6 +88,35 @@ class ImageReadFile(DataSource):
                 images.append(Image.open(path))
             except Exception as exc:
                 return StreamEvent.ERROR, {"diagnostic": f"Error loading image: {exc}"}
+        return StreamEvent.OKAY, {"images": images}
+
+
+class ImageSynthetic(PipelineElement):
+    """Frame generator of random host images: parameters ``width`` / ``height`` (640 x 480),
+    ``batch`` images per frame (1), ``limit`` frames (unbounded when absent), ``rate`` frames/s,
+    ``seed``.  Stands in for a camera or video file where none is available (BASELINE frames
+    are synthetic)."""
+
+    def __init__(self, context):
+        context.set_protocol("image_synthetic:0")
+        context.get_implementation("PipelineElement").__init__(self, context)
+
+    def start_stream(self, stream, stream_id):
+        rate, _ = self.get_parameter("rate", default=None)
+        self.create_frames(stream, self._generate, rate=float(rate) if rate else None)
+        return StreamEvent.OKAY, {}
+
+    def _generate(self, stream, frame_id):
+        limit, found = self.get_parameter("limit")
+        if found and limit is not None and frame_id >= int(limit):
+            return StreamEvent.STOP, {"diagnostic": "frame limit reached"}
+        w = int(self.get_parameter("width", 640)[0])
+        h = int(self.get_parameter("height", 480)[0])
+        n = int(self.get_parameter("batch", 1)[0])
+        rng = np.random.default_rng(int(self.get_parameter("seed", 0)[0]) + frame_id)
+        return StreamEvent.OKAY, {"images": [rng.integers(0, 256, (h, w, 3), dtype=np.uint8) for _ in range(n)]}
+
+    def process_frame(self, stream, images):
         return StreamEvent.OKAY, {"images": images}
 
 

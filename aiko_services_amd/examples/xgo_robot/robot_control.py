@@ -1,0 +1,87 @@
+"""Robot controller Actor (reference ``examples/xgo_robot/robot_control.py:84-295``).
+
+Subscribes to the robot's binary video topic (``zlib(np.save(image))`` payloads, the
+reference's off-node data path), keeps the latest frame and a frame count in its EC share, and
+optionally runs a detector on each frame: ``detector="yolo"`` uses the GPU ``YOLOv8`` model on
+the HIP kernels and publishes ``(detections frame_id (name confidence x y w h) ...)`` on
+``{namespace}/detections``.  Robot commands go through a remote proxy of the ``XGORobot``
+interface (``get_actor_mqtt``), e.g. ``control.robot("turn", 30)``.
+
+    python -m aiko_services_amd.examples.xgo_robot.robot_control --robot <robot /in topic>
+"""
+from __future__ import annotations
+
+from abc import abstractmethod
+import argparse
+
+import aiko_services_amd as aiko
+from aiko_services_amd.runtime.actor import Actor
+from aiko_services_amd.runtime.context import Interface
+from aiko_services_amd.runtime.process import aiko as _aiko
+from aiko_services_amd.utils.configuration import get_namespace
+from aiko_services_amd.utils.sexpr import generate
+
+from .xgo_robot import XGORobot, decode_image, topic_video
+
+__all__ = ["RobotControl", "RobotControlImpl"]
+
+
+class RobotControl(Actor):
+    Interface.default("RobotControl", "aiko_services_amd.examples.xgo_robot.robot_control.RobotControlImpl")
+
+    @abstractmethod
+    def robot(self, command, *args): ...
+
+
+class RobotControlImpl(RobotControl):
+    def __init__(self, context, robot_topic=None, detector=None):
+        context.get_implementation("Actor").__init__(self, context)
+        self.robot_topic = robot_topic
+        self.detector = detector
+        self._model = None
+        self.last_image = None
+        self.share.update({"frames_received": 0, "robot_topic": robot_topic or "", "detections": 0})
+        _aiko.process.add_message_handler(self._video_handler, topic_video(), binary=True)
+
+    def _video_handler(self, _aiko_ctx, topic, payload):
+        image = decode_image(payload)
+        self.last_image = image
+        n = int(self.share["frames_received"]) + 1
+        self.ec_producer.update("frames_received", n)
+        if self.detector == "yolo":
+            self._detect(n, image)
+        return True
+
+    def _detect(self, frame_id, image):
+        import torch
+        if self._model is None:
+            from aiko_services_amd.models.yolov8 import YOLOv8
+            self._model = YOLOv8(scale="n", device="cuda", image_size=640)
+        det, count = self._model.detect(torch.from_numpy(image)[None].cuda())
+        rows = det[0, :int(count[0])].tolist()
+        items = [[f"class_{int(c)}", f"{s:.2f}", int(x1), int(y1), int(x2 - x1), int(y2 - y1)]
+                 for x1, y1, x2, y2, s, c in rows]
+        self.ec_producer.update("detections", int(self.share["detections"]) + len(items))
+        _aiko.message.publish(f"{get_namespace()}/detections", generate("detections", [frame_id] + items))
+
+    def robot(self, command, *args):
+        """Forward one XGORobot method call to the robot actor's /in topic."""
+        if not self.robot_topic:
+            return
+        proxy = aiko.get_actor_mqtt(self.robot_topic, XGORobot)
+        getattr(proxy, command)(*args)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="robot controller actor")
+    ap.add_argument("--robot", default=None, help="robot actor /in topic")
+    ap.add_argument("--detector", default=None, choices=[None, "yolo"])
+    a = ap.parse_args(argv)
+    args = aiko.actor_args("robot_control")
+    args.update(robot_topic=a.robot, detector=a.detector)
+    aiko.compose_instance(RobotControlImpl, args)
+    aiko.process.run()
+
+
+if __name__ == "__main__":
+    main()

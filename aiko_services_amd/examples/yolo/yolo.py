@@ -32,8 +32,10 @@ COCO_NAMES = (
 
 
 class YoloDetector(GpuPipelineElement):
+    PROTOCOL = "object_detector:0"
+
     def __init__(self, context):
-        context.set_protocol("object_detector:0")
+        context.set_protocol(self.PROTOCOL)
         super().__init__(context)
         self.model = None
         self._pinned = {}

@@ -93,3 +93,28 @@ def test_branches_on_hip_streams_match_sequential(native):
         results[streams] = out["z"].float().clone()
     assert torch.allclose(results[False], results[True], atol=1e-2)
     print(f"diamond sequential {times[False]*1e3:.1f} ms, two streams {times[True]*1e3:.1f} ms")
+
+
+def test_face_detector_example_pipeline(native):
+    """examples/face: FaceDetector (single-class YOLOv8 on the HIP kernels) + ImageOverlay."""
+    import json
+    from pathlib import Path
+    import numpy as np
+    from aiko_services_amd.pipeline.definition import parse_pipeline_definition_dict
+    from aiko_services_amd.pipeline.engine import PipelineImpl
+    d = json.loads((Path(__file__).resolve().parents[1] /
+                    "aiko_services_amd/examples/face/face_pipeline.json").read_text())
+    d["graph"] = ["(FaceDetector ImageOverlay)"]            # frames fed directly below
+    d["elements"] = d["elements"][1:]
+    d["elements"][0]["parameters"] = {"conf": 0.01, "iou": 0.5, "image_size": 320}
+    q = queue.Queue()
+    p = PipelineImpl.create_pipeline("<face>", parse_pipeline_definition_dict(d), None, None, "f", [], 0,
+                                     None, 60, queue_response=q)
+    rng = np.random.default_rng(0)
+    images = [rng.integers(0, 256, (240, 320, 3), dtype=np.uint8) for _ in range(3)]
+    p.process_frame({"stream_id": "f", "frame_id": 0}, {"images": images})
+    info, out = q.get(timeout=60)
+    assert info["state"] == 0
+    assert len(out["images"]) == 3 and out["images"][0].shape == (240, 320, 3)
+    face = p.get_element("FaceDetector")
+    assert face.model.nc == 1 and face.share["detections"] >= 0

@@ -362,3 +362,67 @@ def test_example_definitions_run(aiko_process):
     p.create_frame({"stream_id": "14", "frame_id": 0}, {"data": arr})
     info, data = q.get(timeout=5)
     assert np.array_equal(data["data"], arr)
+
+
+def test_image_synthetic_source(aiko_process):
+    M = "aiko_services_amd.elements.media.image_io"
+    d = {"version": 0, "name": "p_synth", "runtime": "python", "graph": ["(ImageSynthetic ImageOutput)"],
+         "parameters": {"width": 64, "height": 48, "batch": 2, "limit": 3},
+         "elements": [{"name": "ImageSynthetic", "input": [{"name": "images", "type": "[image]"}], "output": [{"name": "images", "type": "[image]"}],
+                       "deploy": {"local": {"module": M}}},
+                      {"name": "ImageOutput", "input": [{"name": "images", "type": "[image]"}],
+                       "output": [{"name": "images", "type": "[image]"}], "deploy": {"local": {"module": M}}}]}
+    p, q = _create(d, name="p_synth", stream_id="21")
+    outs = [q.get(timeout=10) for _ in range(3)]
+    for info, data in outs:
+        assert len(data["images"]) == 2 and data["images"][0].shape == (48, 64, 3)
+
+
+def test_speech_example_elements(aiko_process, tmp_path):
+    """examples/speech: WAV write -> LRU framing (reads + deletes the file); LLM element against
+    a local OpenAI-compatible stub server."""
+    import http.server
+    import threading
+    import numpy as np
+    M = "aiko_services_amd.examples.speech.speech_elements"
+
+    def el(name, ins, outs, params=None):
+        return {"name": name, "input": [{"name": n, "type": "any"} for n in ins],
+                "output": [{"name": n, "type": "any"} for n in outs], "parameters": params or {},
+                "deploy": {"local": {"module": M}}}
+    d = {"version": 0, "name": "p_speech", "runtime": "python", "graph": ["(PE_AudioWriteFile PE_AudioFraming)"],
+         "elements": [el("PE_AudioWriteFile", ["audio"], ["audio"],
+                         {"path_template": str(tmp_path / "chunk_{frame_id:03}.wav")}),
+                      el("PE_AudioFraming", ["audio"], ["audio"], {"window_chunks": 2, "delete_input": True})]}
+    p, q = _create(d, name="p_speech", stream_id="31")
+    chunks = [np.full(1600, 0.1 * (i + 1), np.float32) for i in range(3)]
+    for i, c in enumerate(chunks):
+        p.create_frame({"stream_id": "31", "frame_id": i}, {"audio": c})
+    outs = [q.get(timeout=5)[1]["audio"] for _ in range(3)]
+    assert [len(o) for o in outs] == [1600, 3200, 3200]
+    assert np.allclose(outs[2][:1600], 0.2, atol=1e-3) and np.allclose(outs[2][1600:], 0.3, atol=1e-3)
+    assert not list(tmp_path.glob("*.wav"))                          # inputs deleted
+
+    class Stub(http.server.BaseHTTPRequestHandler):
+        def do_POST(self):
+            body = json.loads(self.rfile.read(int(self.headers["Content-Length"])))
+            reply = json.dumps({"choices": [{"message": {"content": body["messages"][0]["content"].upper()}}]})
+            self.send_response(200)
+            self.send_header("Content-Type", "application/json")
+            self.end_headers()
+            self.wfile.write(reply.encode())
+
+        def log_message(self, *a):
+            pass
+    server = http.server.HTTPServer(("127.0.0.1", 0), Stub)
+    threading.Thread(target=server.serve_forever, daemon=True).start()
+    try:
+        d = {"version": 0, "name": "p_llm", "runtime": "python", "graph": ["(PE_SpeechFraming PE_LLM)"],
+             "elements": [el("PE_SpeechFraming", ["text"], ["text"]),
+                          el("PE_LLM", ["text"], ["text"], {"url": f"http://127.0.0.1:{server.server_port}/v1"})]}
+        p, q = _create(d, name="p_llm", stream_id="32")
+        p.create_frame({"stream_id": "32", "frame_id": 0}, {"text": "aloha honua"})
+        info, data = q.get(timeout=10)
+        assert info["state"] == 0 and data["text"] == "ALOHA HONUA"
+    finally:
+        server.shutdown()

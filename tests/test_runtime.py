@@ -270,3 +270,38 @@ def test_ec_share_producer_consumer(aiko_process):
     event.call_on_loop(consumer.terminate)
     from aiko_services_amd.runtime.connection import ConnectionState as CS
     event.call_on_loop(lambda: aiko.aiko.connection.update_state(CS.TRANSPORT))
+
+
+def test_xgo_robot_simulated_video_and_control(aiko_process):
+    """examples/xgo_robot: simulated robot actor publishes zlib(np.save) frames on a binary topic,
+    the controller decodes them and drives the robot through an XGORobot remote proxy."""
+    from aiko_services_amd.examples.xgo_robot.robot_control import RobotControlImpl
+    from aiko_services_amd.examples.xgo_robot.xgo_robot import XGORobotImpl, decode_image, encode_image
+    from aiko_services_amd.runtime.context import actor_args, compose_instance
+    import numpy as np
+    img = np.arange(24, dtype=np.uint8).reshape(2, 4, 3)
+    assert np.array_equal(decode_image(encode_image(img)), img)
+
+    def make():
+        ra = actor_args("xgo_robot")
+        ra.update(fps=50.0, width=32, height=24)
+        robot = compose_instance(XGORobotImpl, ra)
+        ca = actor_args("robot_control")
+        ca.update(robot_topic=robot.topic_in)
+        return robot, compose_instance(RobotControlImpl, ca)
+    robot, control = event.call_on_loop(make)
+    deadline = time.time() + 5
+    while int(control.share["frames_received"]) < 5 and time.time() < deadline:
+        time.sleep(0.02)
+    assert int(control.share["frames_received"]) >= 5
+    assert control.last_image.shape == (24, 32, 3)
+    control.robot("move", "x", 10)
+    control.robot("turn", 500)          # clipped to 100 deg/s
+    control.robot("claw", 128)
+    deadline = time.time() + 5
+    while (robot.share["pose"][0] == 0 or robot.share["claw"] != 128) and time.time() < deadline:
+        time.sleep(0.02)
+    assert robot.share["claw"] == 128 and robot._turn_rate == 100.0
+    assert robot.share["pose"][0] != 0 or robot.share["pose"][1] != 0
+    control.robot("stop")
+    event.call_on_loop(lambda: event.remove_timer_handler(robot._tick))
