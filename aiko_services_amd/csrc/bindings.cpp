@@ -386,10 +386,10 @@ void gemm_fp8_out(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& b
   }
   TORCH_CHECK(lda * M < INT_MAX * 2L, "aiko.gemm_fp8_out: A too large");
   const void* zp = nullptr;
-  if (variant == 1) {
+  if (variant >= 1) {
     TORCH_CHECK(zero.has_value() && zero->defined() && zero->is_cuda() && zero->nbytes() >= 16 &&
                     reinterpret_cast<uintptr_t>(zero->data_ptr()) % 16 == 0,
-                "aiko.gemm_fp8_out: the LDS-DMA variant needs a zero page tensor (>= 16 B)");
+                "aiko.gemm_fp8_out: the LDS-DMA variants need a zero page tensor (>= 16 B)");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0,
                 "aiko.gemm_fp8_out: operands must be 16-byte aligned");
     zp = zero->data_ptr();

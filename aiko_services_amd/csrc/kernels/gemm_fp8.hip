@@ -12,9 +12,11 @@
 // (one 128-byte K block = 8 16-B pieces per row), register-staged 2-deep LDS ring, pieces
 // XOR-swizzled by (row & 7) so each lane's two ds_read_b128 per fragment are conflict-free,
 // XCD-aware block remap, fp32 epilogue staged through padded LDS (bias, GELU, residual add,
-// 16-byte bf16 stores).  For 16x16x128 every lane holds 32 consecutive K bytes of one row
-// (row = lane & 15, K range 32 * (lane >> 4)) for both operands, so A and B pair element for
-// element whatever the instruction's internal k order within the range.
+// 16-byte bf16 stores).  For 16x16x128 every lane holds 32 K bytes of one row (row = lane & 15):
+// 16-B pieces g and g + 4 of the 128-B K block, g = lane >> 4 — a K permutation applied to both
+// operands alike, so A and B still pair element for element (the MX block scales are uniform).
+// With the (row & 7) XOR swizzle this makes both ds_read_b128 of a fragment bank-conflict free
+// over the instruction's lane groups (consecutive pieces 2g, 2g + 1 would be 2-way).
 #include "common.h"
 
 namespace aiko {
@@ -37,12 +39,17 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
 }
 
-template <int BM, int BN>
-__device__ __forceinline__ void fp8_epilogue(const Fp8GemmParams& p, f32x4 (&acc)[BM / 32][BN / 32],
+// Epilogue for a WGM x WGN grid of waves, each owning (BM / WGM) x (BN / WGN) of the tile: the
+// fp32 accumulators go through padded LDS so that every thread then owns whole 8-column chunks
+// (16-B bf16 stores); scales, bias, activation and residual are applied on the way out.
+template <int BM, int BN, int WGM = 2, int WGN = 2>
+__device__ __forceinline__ void fp8_epilogue(const Fp8GemmParams& p,
+                                             f32x4 (&acc)[BM / WGM / 16][BN / WGN / 16],
                                              unsigned char* smem, int m0, int n0) {
-  constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NI = WN / 16, CPAD = 4;
+  constexpr int NT = 64 * WGM * WGN;
+  constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 16, NI = WN / 16, CPAD = 4;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1, fr = lane & 15, fg = lane >> 4;
+  const int wr = wave / WGN, wc = wave % WGN, fr = lane & 15, fg = lane >> 4;
   float* Cs = reinterpret_cast<float*>(smem);
   constexpr int LDC = BN + CPAD;
 #pragma unroll
@@ -54,16 +61,32 @@ __device__ __forceinline__ void fp8_epilogue(const Fp8GemmParams& p, f32x4 (&acc
       for (int e = 0; e < 4; ++e) Cs[(wr * WM + i * 16 + fg * 4 + e) * LDC + col] = acc[i][j][e];
     }
   __syncthreads();
-  constexpr int CPR = BN / 8, CHUNKS = BM * CPR, CPT = CHUNKS / 256, E_ROWS = 256 / CPR;
-  static_assert(CHUNKS % 256 == 0, "whole chunks per thread");
+  constexpr int CPR = BN / 8, CHUNKS = BM * CPR, CPT = CHUNKS / NT, E_ROWS = NT / CPR;
+  static_assert(CHUNKS % NT == 0, "whole chunks per thread");
   const int e_cc = tid % CPR, e_row0 = tid / CPR;
   const int e_n = n0 + e_cc * 8;
   if (e_n >= p.N) return;
   float cs[8], cb[8];
+  {
+    const f32x4 s0 = *reinterpret_cast<const f32x4*>(p.sb + e_n);
+    const f32x4 s1 = *reinterpret_cast<const f32x4*>(p.sb + e_n + 4);
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    cs[e] = p.sb[e_n + e];
-    cb[e] = p.bias ? p.bias[e_n + e] : 0.f;
+    for (int e = 0; e < 4; ++e) {
+      cs[e] = s0[e];
+      cs[e + 4] = s1[e];
+    }
+    if (p.bias) {
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(p.bias + e_n);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(p.bias + e_n + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        cb[e] = b0[e];
+        cb[e + 4] = b1[e];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) cb[e] = 0.f;
+    }
   }
 #pragma unroll
   for (int i = 0; i < CPT; ++i) {
@@ -71,9 +94,14 @@ __device__ __forceinline__ void fp8_epilogue(const Fp8GemmParams& p, f32x4 (&acc
     const int m = m0 + row;
     if (m >= p.M) continue;
     const float rs = p.sa[m];
+    const f32x4 c0 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + e_cc * 8);
+    const f32x4 c1 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + e_cc * 8 + 4);
     float v[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = Cs[row * LDC + e_cc * 8 + e] * rs * cs[e] + cb[e];
+    for (int e = 0; e < 4; ++e) {
+      v[e] = c0[e] * rs * cs[e] + cb[e];
+      v[e + 4] = c1[e] * rs * cs[e + 4] + cb[e + 4];
+    }
     if (p.act == 1) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
@@ -182,15 +210,15 @@ __global__ __launch_bounds__(256, 2) void gemm_fp8_kernel(Fp8GemmParams p) {
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       const int row = wr * WM + i * 16 + fr;
-      const u32x4 lo = *reinterpret_cast<const u32x4*>(As + row * BK + (((2 * fg) ^ (row & 7)) << 4));
-      const u32x4 hi = *reinterpret_cast<const u32x4*>(As + row * BK + (((2 * fg + 1) ^ (row & 7)) << 4));
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(As + row * BK + ((fg ^ (row & 7)) << 4));
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(As + row * BK + (((fg + 4) ^ (row & 7)) << 4));
       af[i] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
     }
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const int row = wc * WN + j * 16 + fr;
-      const u32x4 lo = *reinterpret_cast<const u32x4*>(Bs + row * BK + (((2 * fg) ^ (row & 7)) << 4));
-      const u32x4 hi = *reinterpret_cast<const u32x4*>(Bs + row * BK + (((2 * fg + 1) ^ (row & 7)) << 4));
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(Bs + row * BK + ((fg ^ (row & 7)) << 4));
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(Bs + row * BK + (((fg + 4) ^ (row & 7)) << 4));
       bfr[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
     }
 #pragma unroll
@@ -298,15 +326,15 @@ __global__ __launch_bounds__(256, 2) void gemm_fp8_glds_kernel(Fp8GemmParams p, 
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       const int row = wr * WM + i * 16 + fr;
-      const u32x4 lo = *reinterpret_cast<const u32x4*>(As + row * BK + (((2 * fg) ^ (row & 7)) << 4));
-      const u32x4 hi = *reinterpret_cast<const u32x4*>(As + row * BK + (((2 * fg + 1) ^ (row & 7)) << 4));
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(As + row * BK + ((fg ^ (row & 7)) << 4));
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(As + row * BK + (((fg + 4) ^ (row & 7)) << 4));
       af[i] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
     }
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const int row = wc * WN + j * 16 + fr;
-      const u32x4 lo = *reinterpret_cast<const u32x4*>(Bs + row * BK + (((2 * fg) ^ (row & 7)) << 4));
-      const u32x4 hi = *reinterpret_cast<const u32x4*>(Bs + row * BK + (((2 * fg + 1) ^ (row & 7)) << 4));
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(Bs + row * BK + ((fg ^ (row & 7)) << 4));
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(Bs + row * BK + (((fg + 4) ^ (row & 7)) << 4));
       bfr[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
     }
 #pragma unroll
@@ -319,6 +347,111 @@ __global__ __launch_bounds__(256, 2) void gemm_fp8_glds_kernel(Fp8GemmParams p, 
   }
   fp8_wait_vm_barrier<0>();
   fp8_epilogue<BM, BN>(p, acc, smem, m0, n0);
+}
+
+// ---------------------------------------------------------------------------------------------
+// 8-wave LDS-DMA variant for long-M GEMMs: 512 threads as 4 (M) x 2 (N) waves over a 256 x BN
+// tile, each wave 64 x BN/2.  One workgroup per CU with a 3-slot ring (2 K blocks in flight
+// across every barrier): the register-staged / 2-slot kernels above retire each K block with
+// only one block of MFMA work (512 cycles per wave) to cover an L2/MALL round trip, which left
+// the 16x16x128 pipe idle most of the time (PMC: ~10 % MFMA-busy per wave at K = 768).
+// The MFMA block runs at raised wave priority so the co-resident wave's DMA issue and fragment
+// reads slot into the MFMA shadow instead of the other way round.
+template <int BN>
+__global__ __launch_bounds__(512, 1) void gemm_fp8_w8_kernel(Fp8GemmParams p, const uint8_t* zero) {
+  constexpr int BM = 256, BK = 128, NS = 3, D = NS - 1;
+  constexpr int WGM = 4, WGN = 2;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int MI = WM / 16, NI = WN / 16;
+  constexpr int APT = BM / 64, BPT = BN / 64;   // DMA instructions per thread per stage
+  constexpr int PER = APT + BPT;
+  constexpr int STAGE_BYTES = (BM + BN) * BK;
+  constexpr int CPAD = 4;
+  constexpr int EPI_BYTES = BM * (BN + CPAD) * 4;
+  constexpr int RING_BYTES = NS * STAGE_BYTES;
+  constexpr int LDS_BYTES = EPI_BYTES > RING_BYTES ? EPI_BYTES : RING_BYTES;
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave / WGN, wc = wave % WGN;
+  const int ntn = (p.N + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
+  // DMA instruction i of wave w fills rows i*64 + w*8 .. +7 (lane l: row l >> 3, slot l & 7)
+  const int lrow = wave * 8 + (lane >> 3);
+  const int lp = (lane & 7) ^ (lane >> 3);
+
+  const uint8_t* a_src[APT];
+#pragma unroll
+  for (int i = 0; i < APT; ++i) {
+    const int m = m0 + lrow + 64 * i;
+    a_src[i] = m < p.M ? p.a + (long)m * p.lda + lp * 16 : nullptr;
+  }
+  const uint8_t* b_src[BPT];
+#pragma unroll
+  for (int i = 0; i < BPT; ++i) {
+    const int n = n0 + lrow + 64 * i;
+    b_src[i] = n < p.N ? p.b + (long)n * p.K + lp * 16 : nullptr;
+  }
+  auto issue = [&](int kb, int slot) {
+    unsigned char* As = smem + slot * STAGE_BYTES;
+    unsigned char* Bs = As + BM * BK;
+    const int k0 = kb * BK;
+#pragma unroll
+    for (int i = 0; i < APT; ++i) glds16_u8(a_src[i] ? a_src[i] + k0 : zero, As + (i * 64 + wave * 8) * BK);
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) glds16_u8(b_src[i] ? b_src[i] + k0 : zero, Bs + (i * 64 + wave * 8) * BK);
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nkb = p.K / BK;
+#pragma unroll
+  for (int j = 0; j < D; ++j)
+    if (j < nkb) issue(j, j);
+  const int fr = lane & 15, fg = lane >> 4;
+  int slot = 0;
+  for (int kb = 0; kb < nkb; ++kb) {
+    if (kb + 1 < nkb) {
+      fp8_wait_vm_barrier<PER>();
+    } else {
+      fp8_wait_vm_barrier<0>();
+    }
+    if (kb + D < nkb) issue(kb + D, slot == 0 ? NS - 1 : slot - 1);
+    const unsigned char* As = smem + slot * STAGE_BYTES;
+    const unsigned char* Bs = As + BM * BK;
+    i32x8 af[MI], bfr[NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int row = wr * WM + i * 16 + fr;
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(As + row * BK + ((fg ^ (row & 7)) << 4));
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(As + row * BK + (((fg + 4) ^ (row & 7)) << 4));
+      af[i] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int row = wc * WN + j * 16 + fr;
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(Bs + row * BK + ((fg ^ (row & 7)) << 4));
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(Bs + row * BK + (((fg + 4) ^ (row & 7)) << 4));
+      bfr[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0,
+                                                                      0, 127, 0, 127);
+    __builtin_amdgcn_s_setprio(0);
+    slot = slot == NS - 1 ? 0 : slot + 1;
+  }
+  fp8_wait_vm_barrier<0>();
+  fp8_epilogue<BM, BN, WGM, WGN>(p, acc, smem, m0, n0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -437,6 +570,16 @@ extern "C" int aiko_gemm_fp8(const void* a, const void* b, const float* sa, cons
   p.y = static_cast<bf16_t*>(y);
   p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldy = ldy; p.ldr = ldr; p.act = act;
   dim3 grid(((M + bm - 1) / bm) * ((N + bn - 1) / bn)), block(256);
+  if (variant == 2) {
+    const uint8_t* z = static_cast<const uint8_t*>(zero);
+    if (!z || bm != 256) return -1;
+    if (bn == 128) {
+      gemm_fp8_w8_kernel<128><<<grid, 512, 0, stream>>>(p, z);
+    } else {
+      return -1;
+    }
+    return (int)hipGetLastError();
+  }
   if (variant == 1) {
     const uint8_t* z = static_cast<const uint8_t*>(zero);
     if (!z) return -1;

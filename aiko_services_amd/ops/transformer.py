@@ -118,7 +118,10 @@ FP8_TILES = ((128, 128), (128, 64), (64, 128), (64, 64))
 def _tune_fp8(key, launch):
     """Pick (BM, BN, variant) by measurement, like ``ops.conv.autotune`` (shares its switch)."""
     best, best_t = None, None
-    for t in [tt + (v,) for tt in FP8_TILES for v in (0, 1)]:
+    cands = [tt + (v,) for tt in FP8_TILES for v in (0, 1)]
+    if key[1] % 128 == 0:
+        cands.append((256, 128, 2))     # 8-wave LDS-DMA kernel (one workgroup per CU)
+    for t in cands:
         launch(t)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()

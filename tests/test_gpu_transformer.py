@@ -14,7 +14,7 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("tile", [(128, 128), (128, 64), (64, 64), (64, 128),
-                                  (128, 128, 1), (128, 64, 1), (64, 64, 1), (64, 128, 1)])
+                                  (128, 128, 1), (128, 64, 1), (64, 64, 1), (64, 128, 1), (256, 128, 2)])
 @pytest.mark.parametrize("act", [0, 3])
 def test_gemm_fp8(native, tile, act):
     from aiko_services_amd.ops import transformer as TR
