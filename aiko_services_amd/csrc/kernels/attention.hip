@@ -2,7 +2,7 @@
 //
 // Built for the Whisper encoder (1500 tokens x 12 heads x 64): one workgroup of NW waves per
 // (32*NW-query block, head, sequence); each wave owns 32 queries and streams the sequence's
-// keys in 64-key tiles through a 3-slot LDS ring filled by LDS-DMA (global_load_lds, two
+// keys in 64-key tiles through a 4-slot LDS ring filled by LDS-DMA (global_load_lds, three
 // tiles in flight behind a counted vmcnt + raw barrier).  K and V are both stored row-major
 // ([key][dh]; the DMA destination is lane-linear, so the swizzles are applied to the source
 // rows): K with a 16-B XOR swizzle for ds_read_b128, V with a 32-B chunk swizzle
@@ -18,6 +18,8 @@
 //     32s + 4g .. +3 and 32s + 16 + 4g .. +3 — that same key order.
 // Q stays in registers for the whole key loop.  Sequences are rows b*Tpad .. b*Tpad+T-1 of
 // q/k/v (any row pitch: q, k, v may be column slices of one fused QKV buffer).
+#include <type_traits>
+
 #include "common.h"
 
 namespace aiko {
@@ -51,15 +53,20 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnParams p) {
   constexpr int TILE = kKB * kDH;                // elements
   constexpr int PIECES = TILE / 8;               // 16-B pieces per tile (512)
   constexpr int PPT = PIECES / NT;               // DMA pieces per thread per operand
-  constexpr int NS = 3;                          // LDS ring slots: tiles it+1, it+2 in flight
+  constexpr int NS = 4;                          // LDS ring slots: tiles it+1 .. it+3 in flight
   constexpr int PER = 2 * PPT;                   // DMA instructions per thread per tile
   __shared__ __attribute__((aligned(16))) bf16_t smem[NS * 2 * TILE];   // one array: [slot][K|V]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, g = lane >> 4;
-  const int h = blockIdx.y, b = blockIdx.z;
+  // XCD-aware mapping: the query blocks of one (sequence, head) share its K/V stream, so they
+  // are placed on one XCD (one L2) instead of round-robin over all eight
+  const int nqb = gridDim.x;
+  const int lin = xcd_remap(blockIdx.x + nqb * (blockIdx.y + gridDim.y * blockIdx.z),
+                            nqb * gridDim.y * gridDim.z);
+  const int qblk = lin % nqb, h = (lin / nqb) % p.H, b = lin / (nqb * p.H);
   const long seq0 = (long)b * p.Tpad;
-  const int q0 = blockIdx.x * QB + wave * 32;
+  const int q0 = qblk * QB + wave * 32;
   const int hc = h * kDH;
 
   // Q^T fragments (B operand): lane holds Q[q][ks*32 + 8g .. +7] for q = q0 + qt*16 + fr
@@ -72,6 +79,12 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnParams p) {
     for (int ks = 0; ks < 2; ++ks)
       qf[qt][ks] = as_bf16x8(*reinterpret_cast<const u32x4*>(p.q + (seq0 + qc) * p.ldq + hc + ks * 32 + 8 * g));
   }
+  // consume Q here, before the first (asm, compiler-invisible) DMA: the compiler's own vmcnt
+  // for these loads would otherwise land inside the key loop and count the DMAs too
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) asm volatile("" : "+v"(qf[qt][ks]));
 
   // K / V tiles by LDS-DMA (lane-linear destination, swizzle on the SOURCE): instruction i of
   // wave w fills rows (NT/8)*i + 8w .. +7; lane l -> row (l >> 3), physical 16-B slot (l & 7)
@@ -86,14 +99,8 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnParams p) {
       const int row = drow + (NT / 8) * i;
       const int key = min(t0 + row, p.T - 1);   // keys past T: finite row T-1, masked later
       const int v_lp = ((((ps >> 1) ^ ((row >> 1) & 3))) << 1) | (ps & 1);
-      __builtin_amdgcn_global_load_lds(
-          p.k + (seq0 + key) * p.ldk + hc + k_lp * 8,
-          reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(
-              Ks + ((NT / 8) * i + wave * 8) * kDH)), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(
-          p.v + (seq0 + key) * p.ldv + hc + v_lp * 8,
-          reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(
-              Vs + ((NT / 8) * i + wave * 8) * kDH)), 16, 0, 0);
+      glds16_asm(p.k + (seq0 + key) * p.ldk + hc + k_lp * 8, Ks + ((NT / 8) * i + wave * 8) * kDH);
+      glds16_asm(p.v + (seq0 + key) * p.ldv + hc + v_lp * 8, Vs + ((NT / 8) * i + wave * 8) * kDH);
     }
   };
 
@@ -108,17 +115,24 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnParams p) {
   const int trq = fr >> 2, trp = fr & 3;
 
   const int ntiles = (p.T + kKB - 1) / kKB;
-  issue(0, 0);
-  if (ntiles > 1) issue(kKB, 1);
+#pragma unroll
+  for (int j = 0; j < NS - 1; ++j)
+    if (j < ntiles) issue(j * kKB, j);
   int slot = 0;
-  for (int it = 0; it < ntiles; ++it) {
+  // one key tile; MASK only for the ragged last tile (keeps the compare/select chain out of the
+  // steady-state loop, where hipcc would otherwise if-convert it into every iteration)
+  auto tile = [&](int it, auto mask_tag) {
+    constexpr bool MASK = decltype(mask_tag)::value;
     const int t0 = it * kKB;
-    if (it + 1 < ntiles) {
+    // retire tile it (this wave's DMAs; the younger tiles stay in flight), then barrier
+    if (it + 2 < ntiles) {
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(2 * PER) : "memory");
+    } else if (it + 1 < ntiles) {
       asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(PER) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
-    if (it + 2 < ntiles) issue(t0 + 2 * kKB, slot == 0 ? NS - 1 : slot - 1);
+    if (it + NS - 1 < ntiles) issue(t0 + (NS - 1) * kKB, slot == 0 ? NS - 1 : slot - 1);
     const bf16_t* Kc = smem + slot * 2 * TILE;
     const bf16_t* Vc = Kc + TILE;
 
@@ -143,13 +157,12 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnParams p) {
     // score; key masking only on the ragged last tile; the running max is only raised — and O,
     // l rescaled — when it grows by more than kRescale (log2 units): otherwise exp2 stays
     // bounded by 2^kRescale and the stale max is exact for the final normalisation)
-    const bool ragged = t0 + kKB > p.T;
     const float c = p.scale_log2;
     bf16x8 pf[2][2];
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       float mloc = -INFINITY;
-      if (ragged) {
+      if constexpr (MASK) {
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
@@ -170,24 +183,28 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnParams p) {
 #pragma unroll
         for (int d = 0; d < 4; ++d) o[d][qt] *= alpha;
       }
-      const float mc = m_run[qt] * c;
-      float lsum = 0.f;
-      float pv[4][4];
+      // packed fp32 (v_pk_fma_f32 / v_pk_add_f32): two scores per VALU issue — the softmax is
+      // VALU-issue bound beside the MFMAs, only v_exp_f32 has no packed form
+      const f32x2 c2 = {c, c};
+      const f32x2 nmc2 = {-m_run[qt] * c, -m_run[qt] * c};
+      f32x2 lsum2 = {0.f, 0.f};
+      f32x2 pv[4][2];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          pv[kt][j] = fast_exp2(fmaf(s[kt][qt][j], c, -mc));
-          lsum += pv[kt][j];
+        for (int j = 0; j < 2; ++j) {
+          const f32x2 x = f32x2{s[kt][qt][2 * j], s[kt][qt][2 * j + 1]} * c2 + nmc2;
+          pv[kt][j] = f32x2{fast_exp2(x[0]), fast_exp2(x[1])};
+          lsum2 += pv[kt][j];
         }
-      l_run[qt] += lsum;
+      l_run[qt] += lsum2[0] + lsum2[1];
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         u32x4 u;
-        u[0] = pack2(pv[2 * ks][0], pv[2 * ks][1]);
-        u[1] = pack2(pv[2 * ks][2], pv[2 * ks][3]);
-        u[2] = pack2(pv[2 * ks + 1][0], pv[2 * ks + 1][1]);
-        u[3] = pack2(pv[2 * ks + 1][2], pv[2 * ks + 1][3]);
+        u[0] = pack2(pv[2 * ks][0][0], pv[2 * ks][0][1]);
+        u[1] = pack2(pv[2 * ks][1][0], pv[2 * ks][1][1]);
+        u[2] = pack2(pv[2 * ks + 1][0][0], pv[2 * ks + 1][0][1]);
+        u[3] = pack2(pv[2 * ks + 1][1][0], pv[2 * ks + 1][1][1]);
         pf[qt][ks] = as_bf16x8(u);
       }
     }
@@ -211,7 +228,10 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnParams p) {
     }
 
     slot = slot == NS - 1 ? 0 : slot + 1;
-  }
+  };
+  const int nfull = p.T / kKB;               // tiles with every key < T
+  for (int it = 0; it < nfull; ++it) tile(it, std::false_type{});
+  if (nfull < ntiles) tile(nfull, std::true_type{});
 
   // normalise and write O[q][dh]: lane holds dh = d*16 + 4g + j for its query
 #pragma unroll

@@ -49,6 +49,19 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// 16-byte LDS-DMA (global_load_lds_dwordx4) issued through inline asm: the LDS destination is
+// M0 (wave-uniform) + lane * 16.  Hidden from the compiler's waitcnt pass on purpose — where it
+// cannot prove a later ds_read disjoint from a pending DMA it drains vmcnt to 0 before the read
+// (seen in the attention loop), collapsing the ring to zero tiles in flight.  The caller owns
+// every wait: counted `s_waitcnt vmcnt(N)` before the barrier that publishes a slot.  Only for
+// loops with no other VMEM loads whose waits the compiler would then mis-count.
+__device__ __forceinline__ void glds16_asm(const void* g, const void* lds_wave_base) {
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lds_wave_base)));
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+               :: "v"(g), "s"(lds) : "memory", "m0");
+}
+
 // Bijective XCD-aware remap of a linear workgroup id: consecutive logical ids land on the
 // same XCD (blocks b and b+8 share an XCD under round-robin dispatch), so tiles that share
 // an operand panel share an L2.  Speed only; correctness never depends on placement.
