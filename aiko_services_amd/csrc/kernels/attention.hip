@@ -18,6 +18,7 @@
 //     32s + 4g .. +3 and 32s + 16 + 4g .. +3 — that same key order.
 // Q stays in registers for the whole key loop.  Sequences are rows b*Tpad .. b*Tpad+T-1 of
 // q/k/v (any row pitch: q, k, v may be column slices of one fused QKV buffer).
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -46,8 +47,8 @@ __device__ __forceinline__ int v_off(int row, int col) {
   return row * (kDH * 2) + (((col >> 4) ^ ((row >> 1) & 3)) << 5) + ((col & 15) << 1);
 }
 
-template <int NW>
-__global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnParams p) {
+template <int NW, int VPRE>
+__global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p) {
   constexpr int NT = 64 * NW;
   constexpr int QB = 32 * NW;
   constexpr int TILE = kKB * kDH;                // elements
@@ -135,6 +136,21 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnParams p) {
     if (it + NS - 1 < ntiles) issue(t0 + (NS - 1) * kKB, slot == 0 ? NS - 1 : slot - 1);
     const bf16_t* Kc = smem + slot * 2 * TILE;
     const bf16_t* Vc = Kc + TILE;
+    // V^T fragments by hardware-transposed reads of the row-major V tile; the first VPRE
+    // d-blocks are read before the softmax so their LDS latency hides under its VALU work
+    const unsigned char* vb = reinterpret_cast<const unsigned char*>(Vc);
+    bf16x8 vfr[4][2];
+    auto read_v = [&](int d) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int r0 = 32 * ks + 4 * g + trq;
+        const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4i16*)(vb + v_off(r0, d * 16 + 4 * trp)));
+        const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4i16*)(vb + v_off(r0 + 16, d * 16 + 4 * trp)));
+        vfr[d][ks] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+    };
 
   // S^T = K Q^T : 4 key tiles x 2 query tiles
     f32x4 s[4][2];
@@ -152,6 +168,9 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnParams p) {
           s[kt][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qt][ks], s[kt][qt], 0, 0, 0);
       }
     }
+
+#pragma unroll
+    for (int d = 0; d < VPRE; ++d) read_v(d);
 
     // online softmax per query column (scores kept unscaled: p = exp2(s*c - m*c), one FMA per
     // score; key masking only on the ragged last tile; the running max is only raised — and O,
@@ -209,22 +228,15 @@ __global__ __launch_bounds__(64 * NW, 2) void attn_fwd_kernel(AttnParams p) {
       }
     }
 
-    // O^T += V^T P^T, V^T fragments by hardware-transposed reads of the row-major V tile
-    const unsigned char* vb = reinterpret_cast<const unsigned char*>(Vc);
+    // O^T += V^T P^T (fragments read above / here)
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
+      if (d >= VPRE) read_v(d);
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int r0 = 32 * ks + 4 * g + trq;
-        const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) v4i16*)(vb + v_off(r0, d * 16 + 4 * trp)));
-        const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) v4i16*)(vb + v_off(r0 + 16, d * 16 + 4 * trp)));
-        const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt)
-          o[d][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qt][ks], o[d][qt], 0, 0, 0);
-      }
+          o[d][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vfr[d][ks], pf[qt][ks], o[d][qt], 0, 0, 0);
     }
 
     slot = slot == NS - 1 ? 0 : slot + 1;
@@ -267,8 +279,23 @@ extern "C" int aiko_attn_fwd(const void* q, const void* k, const void* v, void* 
   p.ldq = ldq; p.ldk = ldk; p.ldv = ldv; p.ldo = ldo;
   p.T = T; p.Tpad = Tpad; p.H = H;
   p.scale_log2 = scale * 1.4426950408889634f;
-  constexpr int NW = 8;
-  dim3 grid((T + 32 * NW - 1) / (32 * NW), H, B), block(64 * NW);
-  aiko::attn_fwd_kernel<NW><<<grid, block, 0, stream>>>(p);
+  static const int variant = [] {
+    const char* v = getenv("AIKO_ATTN_VARIANT");
+    return v ? atoi(v) : 0;
+  }();
+  auto launch = [&](auto nw_tag, auto vpre_tag) {
+    constexpr int NW = decltype(nw_tag)::value, VPRE = decltype(vpre_tag)::value;
+    dim3 grid((T + 32 * NW - 1) / (32 * NW), H, B), block(64 * NW);
+    aiko::attn_fwd_kernel<NW, VPRE><<<grid, block, 0, stream>>>(p);
+  };
+  using I8 = std::integral_constant<int, 8>;
+  using I4 = std::integral_constant<int, 4>;
+  switch (variant) {
+    case 1: launch(I8{}, std::integral_constant<int, 2>{}); break;
+    case 2: launch(I8{}, std::integral_constant<int, 4>{}); break;
+    case 3: launch(I4{}, std::integral_constant<int, 0>{}); break;
+    case 4: launch(I4{}, std::integral_constant<int, 2>{}); break;
+    default: launch(I8{}, std::integral_constant<int, 0>{}); break;
+  }
   return (int)hipGetLastError();
 }

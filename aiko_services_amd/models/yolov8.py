@@ -101,8 +101,9 @@ class YOLOv8(WeightsMixin):
         self.nc = num_classes
         self.image_size = image_size
         self.conf, self.iou, self.max_det, self.max_candidates = conf, iou, max_det, max_candidates
-        if num_classes % 8:
-            raise ValueError("num_classes must be a multiple of 8 (16-byte epilogue chunks)")
+        # the class conv's Cout is padded to a multiple of 8 (16-byte epilogue chunks); padded
+        # classes have zero weights and a -40 logit bias, so they never pass any threshold
+        self.nc_pad = -(-num_classes // 8) * 8
         d, w, mc = SCALES[scale]
         ch = lambda x: _make_div(min(x, mc) * w)  # noqa: E731
         rep = lambda n: max(round(n * d), 1)        # noqa: E731
@@ -135,9 +136,11 @@ class YOLOv8(WeightsMixin):
             wbox = 1.0 * torch.randn(4 * REG_MAX, cb, 1, 1, generator=g)
             box.append(C.make_conv_spec(wbox, torch.ones(4 * REG_MAX), act=None, device=dev))
             cls = [_conv_bn(g, cin, cc, 3, 1, dev), _conv_bn(g, cc, cc, 3, 1, dev)]
-            wcls = 0.9 * torch.randn(num_classes, cc, 1, 1, generator=g)
-            cls.append(C.make_conv_spec(wcls, torch.full((num_classes,), float(cls_bias)), act=None,
-                                        device=dev))
+            wcls = torch.zeros(self.nc_pad, cc, 1, 1)
+            wcls[:num_classes] = 0.9 * torch.randn(num_classes, cc, 1, 1, generator=g)
+            bcls = torch.full((self.nc_pad,), -40.0)
+            bcls[:num_classes] = float(cls_bias)
+            cls.append(C.make_conv_spec(wcls, bcls, act=None, device=dev))
             self.heads.append(DetectLevel(box, cls, concat_cout(box[0], cls[0])))
         self._ws: dict = {}
 
@@ -191,7 +194,7 @@ class YOLOv8(WeightsMixin):
         cb, cc = self.cb, self.cc
         h1 = self._buf(f"h{i}.1", (B, H, W, cb + cc))
         h2 = self._buf(f"h{i}.2", (B, H, W, cb + cc))
-        out = self._buf(f"h{i}.out", (B, H, W, 4 * REG_MAX + self.nc))
+        out = self._buf(f"h{i}.out", (B, H, W, 4 * REG_MAX + self.nc_pad))
         C.conv2d(x, lvl.first, out=h1)
         C.conv2d(h1[..., :cb], lvl.box[1], out=h2[..., :cb])
         C.conv2d(h1[..., cb:], lvl.cls[1], out=h2[..., cb:])
@@ -252,7 +255,7 @@ class YOLOv8(WeightsMixin):
         B = feats[0].shape[0]
         A = sum(f.shape[1] * f.shape[2] for f in feats)
         boxes, scores, cls = DT.yolo_decode(
-            feats, STRIDES, self.nc, boxes=self._buf("boxes", (B, A, 4), torch.float32),
+            feats, STRIDES, self.nc_pad, boxes=self._buf("boxes", (B, A, 4), torch.float32),
             scores=self._buf("scores", (B, A), torch.float32), cls=self._buf("cls", (B, A), torch.int32))
         _, _, top, left, gain = self.letterbox(frame_hw)
         return DT.topk_nms(boxes, scores, cls, self.conf, self.iou, self.max_candidates, self.max_det,
