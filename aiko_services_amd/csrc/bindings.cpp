@@ -18,6 +18,10 @@ int aiko_conv_igemm(const void* x, const void* w, const float* bias, const void*
                     int H, int W, int C, int Cc, int R, int S, int stride, int pad, int Ho,
                     int Wo, int M, int Cout, int K, int act, int ldy, int ldr, int bm, int bn,
                     const void* x2, int K1, int H2, int W2, int C2, int stride2, hipStream_t stream);
+int aiko_conv_buf(const void* x, const void* w, const float* bias, const void* res, void* y,
+                  int H, int W, int C, int Cc, int R, int S, int stride, int pad, int Ho, int Wo,
+                  int M, int Cout, int K, int act, int ldy, int ldr, int bm, int bn, const void* x2,
+                  int K1, int H2, int W2, int C2, int stride2, hipStream_t stream);
 int aiko_conv_glds(const void* x, const void* w, const float* bias, const void* res, void* y,
                    int H, int W, int C, int Cc, int R, int S, int stride, int pad, int Ho,
                    int Wo, int M, int Cout, int K, int act, int ldy, int ldr, int bm, int bn,
@@ -75,7 +79,8 @@ void check_launch(int rc, const char* what) {
 // geom = [H, W, C, Cc, R, S, stride, pad, Ho, Wo, M, act, ldy, ldr, bm, bn,
 //         K1, H2, W2, C2, stride2 (the optional second source x2), [variant]]
 // variant 0: register-staged kernel (conv_igemm.hip); 1: LDS-DMA kernel (conv_glds.hip), which
-// needs ``zero`` (>= 16 B of zeros on the device) as the source of conv padding.
+// needs ``zero`` (>= 16 B of zeros on the device) as the source of conv padding; 2: buffer
+// LDS-DMA kernel (conv_buf.hip, padding by out-of-range buffer reads).
 void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, const at::Tensor& w,
                     const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& res,
                     at::Tensor& y, at::IntArrayRef geom, const c10::optional<at::Tensor>& zero) {
@@ -140,7 +145,15 @@ void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, co
     rptr = res->data_ptr();
   }
   int rc;
-  if (variant == 1) {
+  if (variant == 2) {
+    // buffer-LDS-DMA kernel: 64-channel K blocks inside one tap, byte offsets in 31 bits
+    TORCH_CHECK(Cc % 64 == 0 && R * S <= 32 && x_extent * 2 < (1LL << 31) - 64 && w.numel() * 2 < (1LL << 31),
+                "aiko.conv_igemm_out: variant 2 needs Cc % 64 == 0, R*S <= 32 and operands < 2 GiB");
+    TORCH_CHECK(!dual || avail_elems(*x2) * 2 < (1LL << 31) - 64, "aiko.conv_igemm_out: x2 too large for variant 2");
+    rc = aiko_conv_buf(x.data_ptr(), w.data_ptr(), bptr, rptr, y.data_ptr(), H, W, C, Cc, R, S, stride,
+                       pad, Ho, Wo, M, Cout, K, act, ldy, ldr, bm, bn, x2ptr, K1, H2, W2, C2, stride2,
+                       cur_stream());
+  } else if (variant == 1) {
     TORCH_CHECK(zero.has_value() && zero->defined() && zero->is_cuda() && zero->nbytes() >= 16 &&
                     reinterpret_cast<uintptr_t>(zero->data_ptr()) % 16 == 0,
                 "aiko.conv_igemm_out: the LDS-DMA variant needs a zero page tensor (>= 16 B)");

@@ -227,11 +227,26 @@ def zero_page(device) -> torch.Tensor:
     return z
 
 
-def _tune(key, M, cout, launch):
+BUF_WIDE_TILES = ((256, 128), (128, 256))   # 8-wave buffer-DMA kernels (one workgroup per CU)
+
+
+def buf_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = None) -> bool:
+    """Whether the buffer-LDS-DMA kernel (variant 2) applies: whole 64-channel K blocks per tap
+    and operands addressable with 31-bit byte offsets."""
+    def nbytes(t):
+        return t.untyped_storage().nbytes() - t.storage_offset() * t.element_size()
+    return (spec.kind != "stem" and spec.Cc % 64 == 0 and spec.R * spec.S <= 32 and spec.cout > 32
+            and nbytes(x) < 2**31 - 64 and spec.weight.numel() * 2 < 2**31
+            and (x2 is None or nbytes(x2) < 2**31 - 64))
+
+
+def _tune(key, M, cout, launch, buf_ok=False):
     if cout <= 32:
         cands = [t + (0,) for t in NARROW_TILES]
     else:
         cands = [t + (0,) for t in TILES] + [t + (1,) for t in TILES]
+        if buf_ok:
+            cands += [t + (2,) for t in TILES + BUF_WIDE_TILES]
     best, best_t = None, None
     for t in cands:
         launch(t)  # warm
@@ -305,16 +320,20 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None
             0 if residual is None else (residual.stride(2) if residual.dim() == 4 else residual.stride(0))]
 
     def launch(t):
-        # t = (BM, BN) or (BM, BN, variant): variant 1 = LDS-DMA kernel (needs the zero page)
+        # t = (BM, BN) or (BM, BN, variant): variant 1 = LDS-DMA kernel (needs the zero page),
+        # 2 = buffer-LDS-DMA kernel
         v = t[2] if len(t) > 2 else 0
         torch.ops.aiko.conv_igemm_out(x, x2, spec.weight, spec.bias, residual, out,
-                                      head + [t[0], t[1]] + src2 + [v], zero_page(x.device) if v else None)
+                                      head + [t[0], t[1]] + src2 + [v], zero_page(x.device) if v == 1 else None)
 
     if tile is None:
         key = (M, spec.cout, spec.K, spec.R, spec.S, spec.stride, pitch, spec.K1, residual is not None, spec.Cc)
         tile = _tile_cache.get(key)
         if tile is None:
-            tile = _tune(key, M, spec.cout, launch) if _tuning else pick_tile(M, spec.cout)
+            if _tuning:
+                tile = _tune(key, M, spec.cout, launch, buf_variant_ok(spec, x, x2))
+            else:
+                tile = pick_tile(M, spec.cout)
     launch(tile)
     return out
 

@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--tile", default=None, help="only this tile, e.g. 128,128,1")
     a = ap.parse_args()
     from aiko_services_amd.ops import conv as C
     from aiko_services_amd.ops import require_native
@@ -63,6 +64,8 @@ def main():
         base = C.NARROW_TILES if cout <= 32 else C.TILES
         res[name] = {}
         cands = [tt + (0,) for tt in base] + ([tt + (1,) for tt in base] if cout > 32 else [])
+        if a.tile:
+            cands = [tuple(int(v) for v in a.tile.split(","))]
         for t in cands:
             for _ in range(3):
                 C.conv2d(x, spec, residual=r, out=out, tile=t, x2=x2)

@@ -37,6 +37,17 @@ def _nhwc(x_nchw):
     (1, 9, 11, 40, 24, 3, 1, 1, "silu", False, (64, 64, 1)),
     (2, 20, 20, 48, 64, 3, 2, 1, "silu", False, (128, 64, 1)),
     (2, 20, 20, 16, 64, 3, 1, 1, "relu", False, (128, 128, 1)),
+    # buffer-LDS-DMA variant (Cc % 64 == 0: padding by out-of-range buffer reads)
+    (2, 56, 56, 64, 256, 1, 1, 0, "relu", True, (128, 128, 2)),
+    (2, 56, 56, 64, 64, 3, 1, 1, "relu", False, (128, 64, 2)),
+    (2, 28, 28, 128, 128, 3, 2, 1, "relu", True, (64, 64, 2)),
+    (3, 14, 14, 256, 1024, 1, 1, 0, None, True, (64, 128, 2)),
+    (1, 9, 11, 128, 64, 3, 1, 1, "silu", False, (64, 64, 2)),
+    (2, 7, 7, 512, 512, 3, 1, 1, "relu", False, (128, 128, 2)),
+    (1, 13, 9, 192, 72, 3, 2, 1, "gelu", True, (128, 64, 2)),
+    (2, 28, 28, 128, 256, 3, 1, 1, "relu", True, (256, 128, 2)),   # 8-wave, 3-slot ring
+    (3, 14, 14, 256, 512, 1, 1, 0, None, False, (128, 256, 2)),
+    (1, 9, 11, 128, 64, 3, 2, 1, "silu", False, (256, 128, 2)),
 ])
 def test_conv_igemm_matches_torch(native, B, H, W, cin, cout, k, stride, pad, act, res, tile):
     from aiko_services_amd.ops import conv as C
@@ -156,7 +167,7 @@ def test_resnet50_matches_fp32_reference(native):
     assert (i[:, 0].long() == lg.argmax(1)).all()
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 @pytest.mark.parametrize("B,H,cin_main,cin_sc,cout,stride", [(2, 28, 64, 64, 256, 1), (2, 28, 128, 256, 512, 2),
                                                               (1, 14, 512, 1024, 2048, 2)])
 def test_fused_projection_shortcut(native, B, H, cin_main, cin_sc, cout, stride, variant):
