@@ -42,7 +42,8 @@ int aiko_yolo_decode(const void* const* feats, const int* H, const int* W, const
                      float* scores, int* cls, hipStream_t stream);
 int aiko_gemm_fp8(const void* a, const void* b, const float* sa, const float* sb, const float* bias,
                   const void* res, void* y, int M, int N, int K, int lda, int ldy, int ldr, int act,
-                  int bm, int bn, int variant, const void* zero, hipStream_t stream);
+                  int bm, int bn, int variant, const void* zero, const void* amx, int mxr, void* yq, void* ysc, int ldq, int ysr,
+                  hipStream_t stream);
 int aiko_rownorm_quant(const void* x, int ldx, const float* gamma, const float* beta, float eps,
                        void* yb, int ldyb, void* q, int ldq, float* qs, int M, int D, hipStream_t stream);
 int aiko_attn_fwd(const void* q, const void* k, const void* v, void* o, int ldq, int ldk, int ldv,
@@ -365,24 +366,72 @@ int64_t row_pitch(const at::Tensor& t, int64_t cols, const char* op, const char*
   return t.stride(0);
 }
 
-// y = act(sa[m] * sb[n] * (A @ B^T) + bias) + residual ; A fp8 [M, K] (uint8 storage), B fp8 [N, K]
-void gemm_fp8_out(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& b, const at::Tensor& sb,
-                  const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& res,
-                  at::Tensor& y, int64_t act, int64_t bm, int64_t bn, int64_t variant,
-                  const c10::optional<at::Tensor>& zero) {
-  for (const at::Tensor* t : {&a, &sa, &b, &sb, (const at::Tensor*)&y}) check_cuda(*t, "operand");
+// y = act(sa[m] * sb[n] * (A @ B^T) + bias) + residual ; A fp8 [M, K] (uint8 storage), B fp8 [N, K].
+// MX-fp8 options (LDS-DMA kernel, variant 1): ``amx`` uint8 [K/128, R, 4] E8M0 block scales of A
+// (replaces ``sa``); ``yq`` uint8 [M, N] + ``ysc`` uint8 [N/128, R2, 4]: quantise the output to
+// MX-fp8 instead of writing bf16 ``y`` (then ``y`` may be omitted).
+void gemm_fp8_out(const at::Tensor& a, const c10::optional<at::Tensor>& sa_opt, const at::Tensor& b,
+                  const at::Tensor& sb, const c10::optional<at::Tensor>& bias,
+                  const c10::optional<at::Tensor>& res, const c10::optional<at::Tensor>& y_opt, int64_t act,
+                  int64_t bm, int64_t bn, int64_t variant, const c10::optional<at::Tensor>& zero,
+                  const c10::optional<at::Tensor>& amx, const c10::optional<at::Tensor>& yq,
+                  const c10::optional<at::Tensor>& ysc) {
+  for (const at::Tensor* t : {&a, &b, &sb}) check_cuda(*t, "operand");
   TORCH_CHECK(a.element_size() == 1 && b.element_size() == 1, "aiko.gemm_fp8_out: A and B must be 1-byte fp8 storage");
-  TORCH_CHECK(y.scalar_type() == at::kBFloat16, "aiko.gemm_fp8_out: y must be bf16");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
   TORCH_CHECK(K % 128 == 0 && b.dim() == 2 && b.size(1) == K && b.is_contiguous(),
               "aiko.gemm_fp8_out: K must be a multiple of 128 and B [N, K] contiguous");
   TORCH_CHECK(N % 8 == 0, "aiko.gemm_fp8_out: N must be a multiple of 8");
   const int64_t lda = row_pitch(a, K, "gemm_fp8_out", "A");
-  const int64_t ldy = row_pitch(y, N, "gemm_fp8_out", "y");
-  TORCH_CHECK(y.size(0) == M, "aiko.gemm_fp8_out: y must have M rows");
-  TORCH_CHECK(sa.scalar_type() == at::kFloat && sa.numel() >= M && sa.is_contiguous() &&
-                  sb.scalar_type() == at::kFloat && sb.numel() == N && sb.is_contiguous(),
-              "aiko.gemm_fp8_out: scales fp32 sa [M], sb [N]");
+  TORCH_CHECK(sb.scalar_type() == at::kFloat && sb.numel() == N && sb.is_contiguous(), "aiko.gemm_fp8_out: sb fp32 [N]");
+  const bool mx_in = amx.has_value() && amx->defined();
+  const bool mx_out = yq.has_value() && yq->defined();
+  const float* sap = nullptr;
+  if (!mx_in) {
+    TORCH_CHECK(sa_opt.has_value() && sa_opt->defined(), "aiko.gemm_fp8_out: sa needed without amx");
+    const at::Tensor& sa = *sa_opt;
+    check_cuda(sa, "sa");
+    TORCH_CHECK(sa.scalar_type() == at::kFloat && sa.numel() >= M && sa.is_contiguous(), "aiko.gemm_fp8_out: sa fp32 [M]");
+    sap = sa.data_ptr<float>();
+  }
+  const void* amxp = nullptr;
+  int64_t mxr = 0;
+  if (mx_in) {
+    check_cuda(*amx, "amx");
+    TORCH_CHECK(amx->element_size() == 1 && amx->dim() == 3 && amx->size(0) == K / 128 && amx->size(2) == 4 &&
+                    amx->is_contiguous() && amx->size(1) >= ((M + 127) / 128) * 128,
+                "aiko.gemm_fp8_out: amx must be uint8 [K/128, rows >= M rounded to 128, 4]");
+    amxp = amx->data_ptr();
+    mxr = amx->size(1);
+  }
+  void* yp = nullptr;
+  int64_t ldy = 0;
+  if (y_opt.has_value() && y_opt->defined()) {
+    check_cuda(*y_opt, "y");
+    TORCH_CHECK(y_opt->scalar_type() == at::kBFloat16 && y_opt->size(0) == M, "aiko.gemm_fp8_out: y must be bf16 [M, N]");
+    ldy = row_pitch(*y_opt, N, "gemm_fp8_out", "y");
+    yp = y_opt->data_ptr();
+  }
+  void* yqp = nullptr;
+  void* yscp = nullptr;
+  int64_t ldq = 0, ysr = 0;
+  if (mx_out) {
+    check_cuda(*yq, "yq");
+    TORCH_CHECK(ysc.has_value() && ysc->defined(), "aiko.gemm_fp8_out: yq needs ysc");
+    check_cuda(*ysc, "ysc");
+    TORCH_CHECK(yq->element_size() == 1 && yq->size(0) == M && N % 128 == 0, "aiko.gemm_fp8_out: yq uint8 [M, N], N % 128 == 0");
+    ldq = row_pitch(*yq, N, "gemm_fp8_out", "yq");
+    TORCH_CHECK(ysc->element_size() == 1 && ysc->dim() == 3 && ysc->size(0) == N / 128 && ysc->size(1) >= M &&
+                    ysc->size(2) == 4 && ysc->is_contiguous(),
+                "aiko.gemm_fp8_out: ysc must be uint8 [N/128, rows >= M, 4]");
+    TORCH_CHECK(!(res.has_value() && res->defined()), "aiko.gemm_fp8_out: no residual with MX output");
+    yqp = yq->data_ptr();
+    yscp = ysc->data_ptr();
+    ysr = ysc->size(1);
+  } else {
+    TORCH_CHECK(yp != nullptr, "aiko.gemm_fp8_out: y (or yq) required");
+  }
+  TORCH_CHECK(!(mx_in || mx_out) || (variant == 1 && bn == 128), "aiko.gemm_fp8_out: MX paths need variant 1 and BN 128");
   const float* bp = nullptr;
   if (bias.has_value() && bias->defined()) {
     check_cuda(*bias, "bias");
@@ -407,8 +456,9 @@ void gemm_fp8_out(const at::Tensor& a, const at::Tensor& sa, const at::Tensor& b
                 "aiko.gemm_fp8_out: operands must be 16-byte aligned");
     zp = zero->data_ptr();
   }
-  check_launch(aiko_gemm_fp8(a.data_ptr(), b.data_ptr(), sa.data_ptr<float>(), sb.data_ptr<float>(), bp, rp,
-                             y.data_ptr(), M, N, K, lda, ldy, ldr, act, bm, bn, (int)variant, zp, cur_stream()),
+  check_launch(aiko_gemm_fp8(a.data_ptr(), b.data_ptr(), sap, sb.data_ptr<float>(), bp, rp, yp, M, N, K, lda,
+                             ldy, ldr, act, bm, bn, (int)variant, zp, amxp, (int)mxr, yqp, yscp, (int)ldq,
+                             (int)ysr, cur_stream()),
                "gemm_fp8");
 }
 
@@ -507,7 +557,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("topk_nms_out(Tensor boxes, Tensor scores, Tensor cls, int max_cand, float[] params, Tensor(a!) det, Tensor(b!) count) -> ()");
   m.def("maxpool_out(Tensor x, Tensor(a!) y, int k, int s, int p) -> ()");
   m.def("avgpool_out(Tensor x, Tensor(a!) y) -> ()");
-  m.def("gemm_fp8_out(Tensor a, Tensor sa, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!) y, int act, int bm, int bn, int variant=0, Tensor? zero=None) -> ()");
+  m.def("gemm_fp8_out(Tensor a, Tensor? sa, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!)? y, int act, int bm, int bn, int variant=0, Tensor? zero=None, Tensor? amx=None, Tensor(b!)? yq=None, Tensor(c!)? ysc=None) -> ()");
   m.def("rownorm_quant_out(Tensor x, Tensor? gamma, Tensor? beta, float eps, Tensor(a!)? yb, Tensor(b!)? q, Tensor(c!)? qs) -> ()");
   m.def("attn_fwd_out(Tensor q, Tensor k, Tensor v, Tensor(a!) o, int B, int H, int T, int Tpad, float scale) -> ()");
   m.def("logmel_out(Tensor audio, Tensor mel, int n_fft, int hop, int F, Tensor(a!) work, Tensor(b!) gmax, Tensor(c!) dst, int rows, int pad) -> ()");

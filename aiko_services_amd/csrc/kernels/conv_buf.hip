@@ -352,6 +352,8 @@ extern "C" int aiko_conv_buf(const void* x, const void* w, const float* bias, co
     conv_buf_kernel<256, 128, 4, 2><<<grid, 512, 0, stream>>>(p);
   } else if (bm == 128 && bn == 256) {
     conv_buf_kernel<128, 256, 2, 4><<<grid, 512, 0, stream>>>(p);
+  } else if (bm == 256 && bn == 64) {      // narrow Cout (ResNet stage 1): 8 waves of 64 x 32
+    conv_buf_kernel<256, 64, 4, 2><<<grid, 512, 0, stream>>>(p);
   } else {
     return -1;
   }

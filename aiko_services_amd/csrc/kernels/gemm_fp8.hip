@@ -17,6 +17,8 @@
 // operands alike, so A and B still pair element for element (the MX block scales are uniform).
 // With the (row & 7) XOR swizzle this makes both ds_read_b128 of a fragment bank-conflict free
 // over the instruction's lane groups (consecutive pieces 2g, 2g + 1 would be 2-way).
+#include <type_traits>
+
 #include "common.h"
 
 namespace aiko {
@@ -33,7 +35,26 @@ struct Fp8GemmParams {
   bf16_t* y;            // [M][ldy]
   int M, N, K, lda, ldy, ldr;
   int act;              // 0 none, 1 relu, 2 silu, 3 gelu (erf)
+  // MX-fp8 activations (OCP microscaling: one E8M0 scale per 32 consecutive K values).  For
+  // v_mfma_scale_f32_16x16x128_f8f6f4 the A scale of lane l applies to row l % 16 and K block
+  // l / 16 of the instruction's 128 (measured: scripts/probe/mfma_scale_probe.hip — the block is
+  // the low 16 bytes of lane groups 2b', 2b'+1 or the high 16 bytes, which under this kernel's
+  // piece order g, g + 4 is exactly the natural K range [32 b, 32 b + 32)).  Scale bytes are
+  // laid out [K/128][rows][4].
+  const uint8_t* amx;   // A scales (sa unused when set), rows = mxr
+  int mxr;
+  uint8_t* yq;          // MX output instead of y: e4m3 [M][ldq] + scales [N/128][ysr][4]
+  uint8_t* ysc;
+  int ldq, ysr;
 };
+
+// E8M0 exponent for a block with absolute maximum amax (so that amax / 2^e <= 448)
+__device__ __forceinline__ int mx_exponent(float amax) {
+  const uint32_t bits = __float_as_uint(amax * (1.f / 448.f));
+  int e = (int)((bits >> 23) & 255u) - 127 + ((bits & 0x7fffffu) != 0u);
+  if (amax == 0.f) e = -126;
+  return e < -126 ? -126 : (e > 127 ? 127 : e);
+}
 
 __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
@@ -42,7 +63,7 @@ __device__ __forceinline__ float gelu_erf(float x) {
 // Epilogue for a WGM x WGN grid of waves, each owning (BM / WGM) x (BN / WGN) of the tile: the
 // fp32 accumulators go through padded LDS so that every thread then owns whole 8-column chunks
 // (16-B bf16 stores); scales, bias, activation and residual are applied on the way out.
-template <int BM, int BN, int WGM = 2, int WGN = 2>
+template <int BM, int BN, int WGM = 2, int WGN = 2, bool MXO = false>
 __device__ __forceinline__ void fp8_epilogue(const Fp8GemmParams& p,
                                              f32x4 (&acc)[BM / WGM / 16][BN / WGN / 16],
                                              unsigned char* smem, int m0, int n0) {
@@ -65,6 +86,7 @@ __device__ __forceinline__ void fp8_epilogue(const Fp8GemmParams& p,
   static_assert(CHUNKS % NT == 0, "whole chunks per thread");
   const int e_cc = tid % CPR, e_row0 = tid / CPR;
   const int e_n = n0 + e_cc * 8;
+  static_assert(!MXO || BN == 128, "MX output needs whole 128-column K chunks per tile");
   if (e_n >= p.N) return;
   float cs[8], cb[8];
   {
@@ -92,8 +114,9 @@ __device__ __forceinline__ void fp8_epilogue(const Fp8GemmParams& p,
   for (int i = 0; i < CPT; ++i) {
     const int row = e_row0 + E_ROWS * i;
     const int m = m0 + row;
-    if (m >= p.M) continue;
-    const float rs = p.sa[m];
+    const bool live = m < p.M;
+    if (!MXO && !live) continue;            // (MX output: every lane joins the block shuffles)
+    const float rs = p.sa && live ? p.sa[m] : 1.f;
     const f32x4 c0 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + e_cc * 8);
     const f32x4 c1 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + e_cc * 8 + 4);
     float v[8];
@@ -111,6 +134,32 @@ __device__ __forceinline__ void fp8_epilogue(const Fp8GemmParams& p,
     } else if (p.act == 3) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+    }
+    if constexpr (MXO) {
+      // MX block b = columns 32b .. 32b+31 of this 128-column tile row = chunks 4b .. 4b+3,
+      // held by lanes that differ in bits 0-1
+      float amax = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[e]));
+      amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+      amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+      const int ex = mx_exponent(amax);
+      const float inv = __uint_as_float((uint32_t)(127 - ex) << 23);
+      unsigned w0 = 0u, w1 = 0u;
+      w0 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[0] * inv, -448.f), 448.f),
+                                           fminf(fmaxf(v[1] * inv, -448.f), 448.f), w0, false);
+      w0 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[2] * inv, -448.f), 448.f),
+                                           fminf(fmaxf(v[3] * inv, -448.f), 448.f), w0, true);
+      w1 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[4] * inv, -448.f), 448.f),
+                                           fminf(fmaxf(v[5] * inv, -448.f), 448.f), w1, false);
+      w1 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[6] * inv, -448.f), 448.f),
+                                           fminf(fmaxf(v[7] * inv, -448.f), 448.f), w1, true);
+      if (live) {
+        *reinterpret_cast<uint2*>(p.yq + (long)m * p.ldq + e_n) = make_uint2(w0, w1);
+        if ((e_cc & 3) == 0)
+          p.ysc[((long)(n0 >> 7) * p.ysr + m) * 4 + (e_cc >> 2)] = (uint8_t)(ex + 127);
+      }
+      continue;
     }
     if (p.res) {
       const u32x4 r = *reinterpret_cast<const u32x4*>(p.res + (long)m * p.ldr + e_n);
@@ -255,7 +304,7 @@ __device__ __forceinline__ void fp8_wait_vm_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN>
+template <int BM, int BN, bool MXA = false, bool MXO = false>
 __global__ __launch_bounds__(256, 2) void gemm_fp8_glds_kernel(Fp8GemmParams p, const uint8_t* zero) {
   constexpr int BK = 128;
   constexpr int NS = fp8_glds_slots<BM, BN>();
@@ -263,8 +312,9 @@ __global__ __launch_bounds__(256, 2) void gemm_fp8_glds_kernel(Fp8GemmParams p, 
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int MI = WM / 16, NI = WN / 16;
   constexpr int APT = BM / 32, BPT = BN / 32;
-  constexpr int PER = APT + BPT;
-  constexpr int STAGE_BYTES = (BM + BN) * BK;
+  constexpr int PER = APT + BPT + (MXA ? 1 : 0);   // + one scale-tile DMA per wave
+  constexpr int TILE_BYTES = (BM + BN) * BK;
+  constexpr int STAGE_BYTES = TILE_BYTES + (MXA ? BM * 4 : 0);
   constexpr int CPAD = 4;
   constexpr int EPI_BYTES = BM * (BN + CPAD) * 4;
   constexpr int RING_BYTES = NS * STAGE_BYTES;
@@ -291,6 +341,9 @@ __global__ __launch_bounds__(256, 2) void gemm_fp8_glds_kernel(Fp8GemmParams p, 
     const int n = n0 + lrow + 32 * i;
     b_src[i] = n < p.N ? p.b + (long)n * p.K + lp * 16 : nullptr;
   }
+  // MX scale tile of a K block: rows m0 .. m0+BM-1, 4 bytes each, contiguous in the [K/128][rows][4]
+  // layout; wave w fetches rows w*BM/4 .. (w+1)*BM/4 - 1 with BM/16 lanes of 16 B
+  constexpr int SC_LANES = BM / 16;
   auto issue = [&](int kb, int slot) {
     unsigned char* As = smem + slot * STAGE_BYTES;
     unsigned char* Bs = As + BM * BK;
@@ -299,6 +352,10 @@ __global__ __launch_bounds__(256, 2) void gemm_fp8_glds_kernel(Fp8GemmParams p, 
     for (int i = 0; i < APT; ++i) glds16_u8(a_src[i] ? a_src[i] + k0 : zero, As + (i * 32 + wave * 8) * BK);
 #pragma unroll
     for (int i = 0; i < BPT; ++i) glds16_u8(b_src[i] ? b_src[i] + k0 : zero, Bs + (i * 32 + wave * 8) * BK);
+    if constexpr (MXA) {
+      const uint8_t* src = p.amx + ((long)kb * p.mxr + m0 + wave * (BM / 4)) * 4 + lane * 16;
+      if (lane < SC_LANES) glds16_u8(src, As + TILE_BYTES + wave * BM);
+    }
   };
 
   f32x4 acc[MI][NI];
@@ -322,6 +379,16 @@ __global__ __launch_bounds__(256, 2) void gemm_fp8_glds_kernel(Fp8GemmParams p, 
     if (kb + D < nkb) issue(kb + D, slot == 0 ? NS - 1 : slot - 1);
     const unsigned char* As = smem + slot * STAGE_BYTES;
     const unsigned char* Bs = As + BM * BK;
+    int asc[MI];                       // E8M0 scale of this lane's A block, in byte 0
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      if constexpr (MXA) {
+        const uint32_t w4 = *reinterpret_cast<const uint32_t*>(As + TILE_BYTES + (wr * WM + i * 16 + fr) * 4);
+        asc[i] = (int)(w4 >> (8 * fg));
+      } else {
+        asc[i] = 127;
+      }
+    }
     i32x8 af[MI], bfr[NI];
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
@@ -342,11 +409,11 @@ __global__ __launch_bounds__(256, 2) void gemm_fp8_glds_kernel(Fp8GemmParams p, 
 #pragma unroll
       for (int j = 0; j < NI; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0,
-                                                                      0, 127, 0, 127);
+                                                                      0, asc[i], 0, 127);
     slot = slot == NS - 1 ? 0 : slot + 1;
   }
   fp8_wait_vm_barrier<0>();
-  fp8_epilogue<BM, BN>(p, acc, smem, m0, n0);
+  fp8_epilogue<BM, BN, 2, 2, MXO>(p, acc, smem, m0, n0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -455,6 +522,178 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_w8_kernel(Fp8GemmParams p, co
 }
 
 // ---------------------------------------------------------------------------------------------
+// 256 x 256 tile, 8 waves as 2 (M) x 4 (N), each wave 128 x 64 (8 x 4 accumulators).  The per-
+// wave register blocking is what the 16x16x128 fp8 MFMA needs: a 64 x 64 wave tile reads 2 KB
+// of fragments per 32-cycle MFMA, so 8 such waves would demand the whole 256 B/clk of the CU's
+// LDS; 128 x 64 reads 0.75 KB per MFMA.  Double-buffered 64 KB stages (LDS-DMA, counted vmcnt +
+// raw barrier), 1024 MFMA cycles per wave per stage to cover the next stage's flight.  The fp32
+// epilogue is staged through LDS in two 128-row halves.
+__global__ __launch_bounds__(512, 1) void gemm_fp8_big_kernel(Fp8GemmParams p, const uint8_t* zero) {
+  constexpr int BM = 256, BN = 256, BK = 128, NS = 2;
+  constexpr int WGN = 4;
+  constexpr int WM = 128, WN = 64, MI = WM / 16, NI = WN / 16;
+  constexpr int APT = BM / 64, BPT = BN / 64;   // DMA instructions per thread per stage
+  constexpr int PER = APT + BPT;
+  constexpr int STAGE_BYTES = (BM + BN) * BK;  // 64 KB
+  constexpr int CPAD = 4, LDC = BN + CPAD;
+  constexpr int EPI_BYTES = 128 * LDC * 4;     // one 128-row half
+  constexpr int RING_BYTES = NS * STAGE_BYTES;
+  constexpr int LDS_BYTES = EPI_BYTES > RING_BYTES ? EPI_BYTES : RING_BYTES;
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WGN, wc = wave % WGN;
+  const int ntn = (p.N + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid / ntn) * BM, n0 = (bid % ntn) * BN;
+  const int lrow = wave * 8 + (lane >> 3);
+  const int lp = (lane & 7) ^ (lane >> 3);
+
+  const uint8_t* a_src[APT];
+#pragma unroll
+  for (int i = 0; i < APT; ++i) {
+    const int m = m0 + lrow + 64 * i;
+    a_src[i] = m < p.M ? p.a + (long)m * p.lda + lp * 16 : nullptr;
+  }
+  const uint8_t* b_src[BPT];
+#pragma unroll
+  for (int i = 0; i < BPT; ++i) {
+    const int n = n0 + lrow + 64 * i;
+    b_src[i] = n < p.N ? p.b + (long)n * p.K + lp * 16 : nullptr;
+  }
+  auto issue = [&](int kb, int slot) {
+    unsigned char* As = smem + slot * STAGE_BYTES;
+    unsigned char* Bs = As + BM * BK;
+    const int k0 = kb * BK;
+#pragma unroll
+    for (int i = 0; i < APT; ++i) glds16_u8(a_src[i] ? a_src[i] + k0 : zero, As + (i * 64 + wave * 8) * BK);
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) glds16_u8(b_src[i] ? b_src[i] + k0 : zero, Bs + (i * 64 + wave * 8) * BK);
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nkb = p.K / BK;
+  issue(0, 0);
+  const int fr = lane & 15, fg = lane >> 4;
+  const int sw = fr & 7;
+  const int off_lo = (fg ^ sw) << 4, off_hi = ((fg + 4) ^ sw) << 4;
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int slot = kb & 1;
+    fp8_wait_vm_barrier<0>();          // stage kb landed (this wave's DMAs) and slot kb-1 free
+    if (kb + 1 < nkb) issue(kb + 1, slot ^ 1);
+    const unsigned char* As = smem + slot * STAGE_BYTES + (wr * WM + fr) * BK;
+    const unsigned char* Bs = smem + slot * STAGE_BYTES + BM * BK + (wc * WN + fr) * BK;
+    i32x8 bfr[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(Bs + j * 16 * BK + off_lo);
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(Bs + j * 16 * BK + off_hi);
+      bfr[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(As + i * 16 * BK + off_lo);
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(As + i * 16 * BK + off_hi);
+      const i32x8 af = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bfr[j], acc[i][j], 0, 0, 0, 127, 0, 127);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  fp8_wait_vm_barrier<0>();
+
+  // ---- epilogue: two 128-row halves through LDS ----
+  float* Cs = reinterpret_cast<float*>(smem);
+  constexpr int CPR = BN / 8, CHUNKS = 128 * CPR, CPT = CHUNKS / 512, E_ROWS = 512 / CPR;
+  const int e_cc = tid % CPR, e_row0 = tid / CPR;
+  const int e_n = n0 + e_cc * 8;
+  float cs[8], cb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) cs[e] = cb[e] = 0.f;
+  if (e_n < p.N) {
+    const f32x4 s0 = *reinterpret_cast<const f32x4*>(p.sb + e_n);
+    const f32x4 s1 = *reinterpret_cast<const f32x4*>(p.sb + e_n + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      cs[e] = s0[e];
+      cs[e + 4] = s1[e];
+    }
+    if (p.bias) {
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(p.bias + e_n);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(p.bias + e_n + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        cb[e] = b0[e];
+        cb[e + 4] = b1[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    if (wr == half) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int col = wc * WN + j * 16 + fr;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) Cs[(i * 16 + fg * 4 + e) * LDC + col] = acc[i][j][e];
+        }
+    }
+    __syncthreads();
+    if (e_n < p.N) {
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) {
+        const int row = e_row0 + E_ROWS * i;
+        const int m = m0 + half * 128 + row;
+        if (m >= p.M) continue;
+        const float rs = p.sa[m];
+        const f32x4 c0 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + e_cc * 8);
+        const f32x4 c1 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + e_cc * 8 + 4);
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = c0[e] * rs * cs[e] + cb[e];
+          v[e + 4] = c1[e] * rs * cs[e + 4] + cb[e + 4];
+        }
+        if (p.act == 1) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+        } else if (p.act == 2) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = v[e] / (1.f + __expf(-v[e]));
+        } else if (p.act == 3) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+        }
+        if (p.res) {
+          const u32x4 r = *reinterpret_cast<const u32x4*>(p.res + (long)m * p.ldr + e_n);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[2 * e] += __uint_as_float(r[e] << 16);
+            v[2 * e + 1] += __uint_as_float(r[e] & 0xffff0000u);
+          }
+        }
+        u32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = pack2(v[2 * e], v[2 * e + 1]);
+        *reinterpret_cast<u32x4*>(p.y + (long)m * p.ldy + e_n) = o;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Row-wise LayerNorm and/or fp8 quantisation, one wave per row (wave64 reductions):
 //   z = gamma ? (x - mean) * rstd * gamma + beta : x
 //   yb (optional) = bf16(z);  q (optional) = e4m3(z / s), s = amax(|z|) / 448 per row.
@@ -560,9 +799,17 @@ __global__ __launch_bounds__(256) void rownorm_quant_kernel(
 extern "C" int aiko_gemm_fp8(const void* a, const void* b, const float* sa, const float* sb,
                              const float* bias, const void* res, void* y, int M, int N, int K,
                              int lda, int ldy, int ldr, int act, int bm, int bn, int variant,
-                             const void* zero, hipStream_t stream) {
+                             const void* zero, const void* amx, int mxr, void* yq, void* ysc,
+                             int ldq, int ysr, hipStream_t stream) {
   using namespace aiko;
   Fp8GemmParams p;
+  p.amx = static_cast<const uint8_t*>(amx);
+  p.mxr = mxr;
+  p.yq = static_cast<uint8_t*>(yq);
+  p.ysc = static_cast<uint8_t*>(ysc);
+  p.ldq = ldq;
+  p.ysr = ysr;
+  if ((amx || yq) && variant != 1) return -1;   // MX paths: LDS-DMA kernel only
   p.a = static_cast<const uint8_t*>(a);
   p.b = static_cast<const uint8_t*>(b);
   p.sa = sa; p.sb = sb; p.bias = bias;
@@ -570,6 +817,12 @@ extern "C" int aiko_gemm_fp8(const void* a, const void* b, const float* sa, cons
   p.y = static_cast<bf16_t*>(y);
   p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldy = ldy; p.ldr = ldr; p.act = act;
   dim3 grid(((M + bm - 1) / bm) * ((N + bn - 1) / bn)), block(256);
+  if (variant == 3) {
+    const uint8_t* z = static_cast<const uint8_t*>(zero);
+    if (!z || bm != 256 || bn != 256) return -1;
+    gemm_fp8_big_kernel<<<grid, 512, 0, stream>>>(p, z);
+    return (int)hipGetLastError();
+  }
   if (variant == 2) {
     const uint8_t* z = static_cast<const uint8_t*>(zero);
     if (!z || bm != 256) return -1;
@@ -583,6 +836,18 @@ extern "C" int aiko_gemm_fp8(const void* a, const void* b, const float* sa, cons
   if (variant == 1) {
     const uint8_t* z = static_cast<const uint8_t*>(zero);
     if (!z) return -1;
+    if (amx || yq) {
+      if (bn != 128 || (bm != 128 && bm != 64)) return -1;
+      auto go = [&](auto mxa, auto mxo) {
+        constexpr bool A = decltype(mxa)::value, O = decltype(mxo)::value;
+        if (bm == 128) gemm_fp8_glds_kernel<128, 128, A, O><<<grid, block, 0, stream>>>(p, z);
+        else gemm_fp8_glds_kernel<64, 128, A, O><<<grid, block, 0, stream>>>(p, z);
+      };
+      if (amx && yq) go(std::true_type{}, std::true_type{});
+      else if (amx) go(std::true_type{}, std::false_type{});
+      else go(std::false_type{}, std::true_type{});
+      return (int)hipGetLastError();
+    }
     if (bm == 128 && bn == 128) {
       gemm_fp8_glds_kernel<128, 128><<<grid, block, 0, stream>>>(p, z);
     } else if (bm == 128 && bn == 64) {

@@ -172,9 +172,13 @@ class WhisperEncoder(WeightsMixin):
         s8 = self._buf("s8", (M,), torch.float32)
         qkv = self._buf("qkv", (M, 3 * d))
         att = self._buf("att", (M, d), zero=True)
-        u = self._buf("u", (M, 4 * d))
-        u8 = self._buf("u8", (M, 4 * d), torch.uint8)
-        su = self._buf("su", (M,), torch.float32)
+        # fc1 -> fc2 hand-off in MX-fp8: the fc1 epilogue applies GELU and writes e4m3 + E8M0
+        # block scales, fc2 feeds those scales straight to the scaled MFMA (no bf16 round trip,
+        # no separate row-quantisation pass)
+        u8, usc = self._ws.get(("u_mx", M, 4 * d)) or (None, None)
+        if u8 is None:
+            u8, usc = TR.mx_buffers(M, 4 * d, self.device)
+            self._ws[("u_mx", M, 4 * d)] = (u8, usc)
         for blk in self.blocks:
             TR.rownorm(x, *blk.ln1, q=q8, qs=s8)
             TR.linear_fp8(q8, s8, blk.qkv, out=qkv)
@@ -182,9 +186,8 @@ class WhisperEncoder(WeightsMixin):
             TR.rownorm(att, q=q8, qs=s8)
             TR.linear_fp8(q8, s8, blk.out, out=x, residual=x)
             TR.rownorm(x, *blk.ln2, q=q8, qs=s8)
-            TR.linear_fp8(q8, s8, blk.fc1, out=u, act=TR.ACT_GELU)
-            TR.rownorm(u, q=u8, qs=su)
-            TR.linear_fp8(u8, su, blk.fc2, out=x, residual=x)
+            TR.linear_fp8(q8, s8, blk.fc1, act=TR.ACT_GELU, out_mx=(u8, usc))
+            TR.linear_fp8(u8, None, blk.fc2, out=x, residual=x, x_mx=usc)
         y = self._buf("y", (M, d))
         TR.rownorm(x, *self.ln_post, out=y)
         return y.view(B, Tp, d)[:, :T]

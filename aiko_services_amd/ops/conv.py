@@ -227,7 +227,7 @@ def zero_page(device) -> torch.Tensor:
     return z
 
 
-BUF_WIDE_TILES = ((256, 128), (128, 256))   # 8-wave buffer-DMA kernels (one workgroup per CU)
+BUF_WIDE_TILES = ((256, 128), (128, 256), (256, 64))   # 8-wave buffer-DMA kernels (one workgroup per CU)
 
 
 def buf_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = None) -> bool:

@@ -84,43 +84,84 @@ def pick_tile(M: int, N: int) -> tuple[int, int]:
     return bm, bn
 
 
-def linear_fp8(xq: torch.Tensor, xs: torch.Tensor, lin: Fp8Linear, out: torch.Tensor | None = None,
-               residual: torch.Tensor | None = None, act: int = ACT_NONE, tile=None) -> torch.Tensor:
+def mx_buffers(M: int, K: int, device) -> tuple[torch.Tensor, torch.Tensor]:
+    """Storage for an MX-fp8 activation: e4m3 bytes [M, K] and E8M0 scales, one per 32
+    consecutive K values, laid out [K/128, rows, 4] (rows = M rounded up to 128)."""
+    rows = -(-M // 128) * 128
+    return (torch.empty(M, K, dtype=torch.uint8, device=device),
+            torch.full((K // 128, rows, 4), 127, dtype=torch.uint8, device=device))
+
+
+def mx_dequant(q: torch.Tensor, sc: torch.Tensor) -> torch.Tensor:
+    """fp32 values of an MX-fp8 activation (test reference)."""
+    M, K = q.shape
+    v = q.view(torch.float8_e4m3fn).float().view(M, K // 128, 4, 32)          # [m, chunk, block, j]
+    e = sc[:, :M].permute(1, 0, 2).float() - 127.0                             # [m, chunk, block]
+    return (v * torch.exp2(e)[..., None]).reshape(M, K)
+
+
+def mx_quantize_ref(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """Reference MX-fp8 quantisation of fp32 [M, K] (same block layout and E8M0 rule)."""
+    M, K = x.shape
+    v = x.float().reshape(M, K // 128, 4, 32)
+    amax = v.abs().amax(dim=3)                                                 # [m, chunk, block]
+    t = (amax / FP8_MAX).clamp(min=2.0 ** -126)
+    e = torch.ceil(torch.log2(t)).clamp(-126, 127)
+    e = torch.where(amax == 0, torch.full_like(e, -126.0), e)
+    q = (v / torch.exp2(e)[..., None]).clamp(-FP8_MAX, FP8_MAX).to(FP8)
+    rows = -(-M // 128) * 128
+    sc = torch.full((K // 128, rows, 4), 127, dtype=torch.uint8)
+    sc[:, :M] = (e + 127).to(torch.uint8).permute(1, 0, 2)
+    return q.reshape(M, K).view(torch.uint8), sc
+
+
+def linear_fp8(xq: torch.Tensor, xs: torch.Tensor | None, lin: Fp8Linear, out: torch.Tensor | None = None,
+               residual: torch.Tensor | None = None, act: int = ACT_NONE, tile=None,
+               x_mx: torch.Tensor | None = None, out_mx: tuple | None = None) -> torch.Tensor | None:
     """``act(xs[m] * s_w[n] * (xq @ Wq^T) + bias) + residual`` -> bf16 [M, N].
-    ``xq`` uint8 [M, K] (row pitch may exceed K), ``xs`` fp32 [M]."""
+    ``xq`` uint8 [M, K] (row pitch may exceed K), ``xs`` fp32 [M] per-row scales, or ``x_mx``
+    (E8M0 block scales from :func:`mx_buffers`) for an MX-fp8 activation.  ``out_mx`` = (q, sc)
+    quantises the output to MX-fp8 in the epilogue instead of writing bf16 (no residual)."""
     M = xq.shape[0]
     if xq.shape[1] != lin.K:
         raise ValueError(f"linear_fp8: activation K {xq.shape[1]} != weight K {lin.K}")
-    if out is None:
+    if out is None and out_mx is None:
         out = torch.empty(M, lin.n, dtype=torch.bfloat16, device=xq.device)
+    mx = x_mx is not None or out_mx is not None
     if tile is None:
-        key = (M, lin.n, lin.K, xq.stride(0), residual is not None, act)
+        key = (M, lin.n, lin.K, xq.stride(0), residual is not None, act, x_mx is not None, out_mx is not None)
         tile = _tile_cache.get(key)
         if tile is None:
+            launch = lambda t: _launch(xq, xs, lin, out, residual, act, t, x_mx, out_mx)  # noqa: E731
             if _conv._tuning:
-                tile = _tune_fp8(key, lambda t: _launch(xq, xs, lin, out, residual, act, t))
+                tile = _tune_fp8(key, launch, mx)
             else:
-                tile = pick_tile(M, lin.n) + (1,)
-    _launch(xq, xs, lin, out, residual, act, tile)
+                tile = (128, 128, 1) if mx else pick_tile(M, lin.n) + (1,)
+    _launch(xq, xs, lin, out, residual, act, tile, x_mx, out_mx)
     return out
 
 
-def _launch(xq, xs, lin, out, residual, act, t):
+def _launch(xq, xs, lin, out, residual, act, t, x_mx=None, out_mx=None):
     v = t[2] if len(t) > 2 else 0
-    torch.ops.aiko.gemm_fp8_out(xq, xs, lin.weight, lin.scale, lin.bias, residual, out, act, t[0], t[1], v,
-                                _conv.zero_page(xq.device) if v else None)
+    yq, ysc = out_mx if out_mx is not None else (None, None)
+    torch.ops.aiko.gemm_fp8_out(xq, None if x_mx is not None else xs, lin.weight, lin.scale, lin.bias, residual,
+                                out, act, t[0], t[1], v, _conv.zero_page(xq.device) if v else None,
+                                x_mx, yq, ysc)
 
 
 _tile_cache: dict = {}
 FP8_TILES = ((128, 128), (128, 64), (64, 128), (64, 64))
 
 
-def _tune_fp8(key, launch):
+def _tune_fp8(key, launch, mx=False):
     """Pick (BM, BN, variant) by measurement, like ``ops.conv.autotune`` (shares its switch)."""
     best, best_t = None, None
-    cands = [tt + (v,) for tt in FP8_TILES for v in (0, 1)]
-    if key[1] % 128 == 0:
-        cands.append((256, 128, 2))     # 8-wave LDS-DMA kernel (one workgroup per CU)
+    if mx:                               # MX-fp8 in/out: LDS-DMA kernel, whole 128-wide K chunks
+        cands = [(128, 128, 1), (64, 128, 1)]
+    else:
+        cands = [tt + (v,) for tt in FP8_TILES for v in (0, 1)]
+        if key[1] % 128 == 0:
+            cands.append((256, 128, 2))  # 8-wave LDS-DMA kernel (one workgroup per CU)
     for t in cands:
         launch(t)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

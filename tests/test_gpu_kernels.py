@@ -48,6 +48,7 @@ def _nhwc(x_nchw):
     (2, 28, 28, 128, 256, 3, 1, 1, "relu", True, (256, 128, 2)),   # 8-wave, 3-slot ring
     (3, 14, 14, 256, 512, 1, 1, 0, None, False, (128, 256, 2)),
     (1, 9, 11, 128, 64, 3, 2, 1, "silu", False, (256, 128, 2)),
+    (2, 30, 30, 64, 64, 3, 1, 1, "relu", True, (256, 64, 2)),
 ])
 def test_conv_igemm_matches_torch(native, B, H, W, cin, cout, k, stride, pad, act, res, tile):
     from aiko_services_amd.ops import conv as C

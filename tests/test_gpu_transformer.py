@@ -14,7 +14,7 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("tile", [(128, 128), (128, 64), (64, 64), (64, 128),
-                                  (128, 128, 1), (128, 64, 1), (64, 64, 1), (64, 128, 1), (256, 128, 2)])
+                                  (128, 128, 1), (128, 64, 1), (64, 64, 1), (64, 128, 1), (256, 128, 2), (256, 256, 3)])
 @pytest.mark.parametrize("act", [0, 3])
 def test_gemm_fp8(native, tile, act):
     from aiko_services_amd.ops import transformer as TR
@@ -116,3 +116,30 @@ def test_whisper_small_30s(native):
     torch.cuda.synchronize()
     assert y.shape == (1, 1500, 768)
     assert torch.isfinite(y.float()).all()
+
+
+@pytest.mark.parametrize("bm", [128, 64])
+def test_gemm_fp8_mx_in_and_out(native, bm):
+    """MX-fp8 activations: E8M0 block scales straight into the scaled MFMA (A side), and an
+    epilogue that quantises GELU(out) to MX-fp8 (fc1 -> fc2 without a bf16 round trip)."""
+    from aiko_services_amd.ops import transformer as TR
+    g = torch.Generator().manual_seed(5)
+    M, N, K = 300, 384, 512
+    lin = TR.make_fp8_linear(torch.randn(N, K, generator=g) / 20, torch.randn(N, generator=g) * 0.1, DEV)
+    # A side: MX-quantised input with a wide dynamic range across blocks
+    x = torch.randn(M, K, generator=g) * torch.exp2(torch.randint(-6, 6, (M, K // 32), generator=g).float()
+                                                    ).repeat_interleave(32, dim=1)
+    q, sc = TR.mx_quantize_ref(x)
+    y = TR.linear_fp8(q.to(DEV), None, lin, x_mx=sc.to(DEV), tile=(bm, 128, 1))
+    ref = TR.mx_dequant(q, sc).to(DEV) @ lin.ref_weight.T.to(DEV) + lin.bias
+    assert _rel(y, ref) < 5e-3
+    # output side: GELU then MX quantisation in the epilogue
+    xq, xs = TR.quantize_rows_ref(torch.randn(M, K, generator=g))
+    oq, osc = TR.mx_buffers(M, N, DEV)
+    TR.linear_fp8(xq.to(DEV), xs.to(DEV), lin, act=TR.ACT_GELU, out_mx=(oq, osc), tile=(bm, 128, 1))
+    full = F.gelu((xq.view(torch.float8_e4m3fn).float() * xs[:, None]).to(DEV) @ lin.ref_weight.T.to(DEV) + lin.bias)
+    rq, rsc = TR.mx_quantize_ref(full.cpu())
+    got = TR.mx_dequant(oq.cpu(), osc.cpu())
+    assert (osc.cpu()[:, :M] == rsc[:, :M]).float().mean() > 0.98          # same E8M0 scales
+    assert _rel(got, full.cpu()) < 4e-2                                    # fp8 rounding only
+    assert _rel(got, TR.mx_dequant(rq, rsc)) < 1e-2
