@@ -8,6 +8,7 @@ disabled; BASELINE's north star names ``aiko pipeline create``).
     aiko recorder [filter]
     aiko storage start|test_command|test_request
     aiko lifecycle manager N | client ID TOPIC
+    aiko ec-test sc_test | ec_test [PID [SID [FILTER]]]   EC share / ServicesCache self tests
     aiko echo-bench                    BASELINE config 1 (two-process echo pipeline)
     aiko bench ...                     bench.py (ResNet-50 pipeline on MI355X)
     aiko build                         compile the HIP/C++ library for gfx950
@@ -38,6 +39,8 @@ def main(argv=None):
         from .storage import main as m
     elif cmd == "lifecycle":
         from ..control.lifecycle import main as m
+    elif cmd == "ec-test":
+        from .ec_test import main as m
     elif cmd == "echo-bench":
         from .echo_bench import main as m
     elif cmd == "bench":

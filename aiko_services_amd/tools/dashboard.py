@@ -8,6 +8,11 @@ the selected variable (publishes ``(update name value)``), ``L`` cycle the servi
 ``l`` log page, ``h`` history, ``K`` kill the selected (local) process, ``q`` quit.  GPU
 services show their device, HBM frame-pool occupancy and frames/s when they share them.
 
+Plugins (reference ``dashboard_plugins.py``): ``PLUGINS`` maps a service *name* or *protocol* to
+a page function ``page(dashboard, details, width) -> [lines]``; ``p`` shows the selected
+service's plugin page.  Built in: ``registrar`` (discovered services' topic paths) and
+``gpu`` pages for services that share GPU telemetry.  ``register_plugin(key, page)`` adds more.
+
 ``--snapshot`` prints the services (and optionally one service's variables) once and exits —
 the scriptable / testable mode.
 """
@@ -25,7 +30,7 @@ from ..runtime.process import aiko
 from ..runtime.service import ServiceTopicPath
 from ..utils.sexpr import generate
 
-__all__ = ["Dashboard", "main", "format_services"]
+__all__ = ["Dashboard", "PLUGINS", "format_services", "main", "register_plugin"]
 
 LOG_LEVELS = ["DEBUG", "INFO", "WARNING", "ERROR"]
 HISTORY_LIMIT = 32
@@ -47,6 +52,45 @@ def format_services(services, width=120):
         rows.append(f"{topic:30.30} {str(_field(d, 1, 'name')):20.20} {protocol:27.27} "
                     f"{str(_field(d, 3, 'transport')):9.9} {str(_field(d, 4, 'owner')):8.8} {tags}"[:width])
     return rows
+
+
+def registrar_page(dashboard, details, width=120):
+    """Reference ``RegistrarFrame``: the registrar's view of every discovered service."""
+    rows = ["Registrar: Discovered Services topic paths"]
+    for d in dashboard.services():
+        tp = ServiceTopicPath.parse(_field(d, 0, "topic_path"))
+        rows.append(f"{str(tp) if tp else _field(d, 0, 'topic_path'):40.40} {str(_field(d, 1, 'name')):20.20} "
+                    f"{str(_field(d, 4, 'owner')):10.10} {str(_field(d, 2, 'protocol'))}"[:width])
+    return rows
+
+
+GPU_KEYS = ("gpu", "device", "gpu_fps", "hbm", "rccl", "latency")
+
+
+def gpu_page(dashboard, details, width=120):
+    """GPU element telemetry from the selected service's share (device, HBM, RCCL, latency)."""
+    rows = [f"GPU telemetry: {_field(details, 1, 'name')}"]
+    for k, v in dashboard.flat_variables():
+        if any(g in k for g in GPU_KEYS):
+            rows.append(f"  {k:40.40} {v}"[:width])
+    return rows
+
+
+PLUGINS = {"registrar": registrar_page}
+
+
+def register_plugin(key, page):
+    """Add a plugin page for services whose name or protocol is ``key``."""
+    PLUGINS[key] = page
+
+
+def find_plugin(details):
+    name = str(_field(details, 1, "name"))
+    protocol = str(_field(details, 2, "protocol"))
+    for key in (name, protocol, protocol.rsplit("/", 1)[-1].split(":")[0]):
+        if key in PLUGINS:
+            return PLUGINS[key]
+    return None
 
 
 class Dashboard:
@@ -130,6 +174,18 @@ class Dashboard:
                 out.append((k, v))
         return out
 
+    def plugin_lines(self, width=120):
+        services = self.services()
+        if not services or self.selected >= len(services):
+            return ["no service selected"]
+        details = services[self.selected]
+        page = find_plugin(details)
+        if page is None and any(any(g in k for g in GPU_KEYS) for k, _ in self.flat_variables()):
+            page = gpu_page
+        if page is None:
+            return [f"no plugin for {_field(details, 1, 'name')}"]
+        return page(self, details, width)
+
     # ---- curses UI -------------------------------------------------------------------------
     def run_curses(self):
         import curses
@@ -163,6 +219,8 @@ class Dashboard:
                 self.page = "log" if self.page != "log" else "services"
             elif ch == ord("h"):
                 self.page = "history" if self.page != "history" else "services"
+            elif ch == ord("p"):
+                self.page = "plugin" if self.page != "plugin" else "services"
             elif ch == ord("L"):
                 self.status = f"log_level -> {self.cycle_log_level()}"
             elif ch == ord("K"):
@@ -205,6 +263,10 @@ class Dashboard:
             scr.addstr(1, 0, f"log: {self.log_topic}"[: w - 1])
             for i, line in enumerate(lines):
                 scr.addstr(2 + i, 0, line[: w - 1])
+        elif self.page == "plugin":
+            rows = self.plugin_lines(w - 1)
+            for i, row in enumerate(rows[: h - 2]):
+                scr.addstr(1 + i, 0, row[: w - 1])
         elif self.page == "history":
             rows = format_services(list(self.cache.get_history()), w - 1)
             for i, row in enumerate(rows[: h - 2]):
@@ -224,7 +286,7 @@ class Dashboard:
                 attr = curses.A_REVERSE if (self.focus == "variables" and i == self.var_index) else 0
                 scr.addstr(top + 2 + i, 0, f"{k:40.40} {v}"[: w - 1], attr)
         scr.addstr(h - 1, 0, (f"{self.status}  " + "q quit  arrows select  tab pane  e edit  L level  "
-                              "l log  h history  K kill")[: w - 1])
+                              "l log  h history  p plugin  K kill")[: w - 1])
         scr.refresh()
 
 

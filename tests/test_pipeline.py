@@ -426,3 +426,83 @@ def test_speech_example_elements(aiko_process, tmp_path):
         assert info["state"] == 0 and data["text"] == "ALOHA HONUA"
     finally:
         server.shutdown()
+
+
+def test_audio_spectrum_and_remote_elements(aiko_process):
+    """Reference dead audio elements: FFT -> filter -> bands -> XY graph; array frames sent by
+    PE_RemoteSend0 over a binary topic arrive as new frames of PE_RemoteReceive0's pipeline."""
+    import numpy as np
+    M = "aiko_services_amd.elements.media.audio_io"
+
+    def el(name, ins, outs, params=None):
+        return {"name": name, "input": [{"name": n, "type": "any"} for n in ins],
+                "output": [{"name": n, "type": "any"} for n in outs], "parameters": params or {},
+                "deploy": {"local": {"module": M}}}
+    d = {"version": 0, "name": "p_spectrum", "runtime": "python",
+         "graph": ["(PE_FFT PE_AudioFilter PE_AudioResampler PE_GraphXY)"],
+         "elements": [el("PE_FFT", ["audio_samples"], ["amplitudes", "frequencies"]),
+                      el("PE_AudioFilter", ["amplitudes", "frequencies"], ["amplitudes", "frequencies"],
+                         {"amplitude_minimum": 10, "amplitude_maximum": 1e9}),
+                      el("PE_AudioResampler", ["amplitudes", "frequencies"], ["amplitudes", "frequencies"],
+                         {"band_count": 4, "frequency_maximum": 4000}),
+                      el("PE_GraphXY", ["amplitudes", "frequencies"], ["amplitudes", "frequencies", "image"],
+                         {"width": 64, "height": 48, "frequency_maximum": 4000, "amplitude_maximum": 0})]}
+    p, q = _create(d, name="p_spectrum", stream_id="41")
+    t = np.arange(16000) / 16000.0
+    x = (np.sin(2 * np.pi * 440 * t) + 0.5 * np.sin(2 * np.pi * 2500 * t)).astype(np.float32)
+    p.create_frame({"stream_id": "41", "frame_id": 0}, {"audio_samples": x})
+    info, out = q.get(timeout=5)
+    assert info["state"] == 0 and out["image"].shape == (48, 64, 3) and out["image"].any()
+    assert len(out["amplitudes"]) == 4
+    assert np.argmax(out["amplitudes"]) == 0 and out["amplitudes"][2] > 0   # 440 Hz band, 2.5 kHz band
+
+    rx = {"version": 0, "name": "p_rx", "runtime": "python", "graph": ["(PE_RemoteReceive0)"],
+          "elements": [el("PE_RemoteReceive0", ["audio"], ["audio"], {"stream_id": "0"})]}
+    tx = {"version": 0, "name": "p_tx", "runtime": "python", "graph": ["(PE_RemoteSend0)"],
+          "elements": [el("PE_RemoteSend0", ["audio"], [])]}
+    _, qr = _create(rx, name="p_rx", stream_id="0")
+    ptx, qt = _create(tx, name="p_tx", stream_id="42")
+    for i in range(2):
+        ptx.create_frame({"stream_id": "42", "frame_id": i}, {"audio": np.full(8, i, np.int16)})
+    got = [qr.get(timeout=5)[1]["audio"] for _ in range(2)]
+    assert [g.tolist() for g in got] == [[0] * 8, [1] * 8]
+    from aiko_services_amd.elements.media.audio_io import PE_MicrophoneSD, decode_array, encode_array
+    assert decode_array(encode_array(np.array(["hi"]))).tolist() == ["hi"]
+    with pytest.raises(Exception):
+        _create({"version": 0, "name": "p_mic", "runtime": "python", "graph": ["(PE_MicrophoneSD)"],
+                 "elements": [el("PE_MicrophoneSD", [], ["audio"])]}, name="p_mic", stream_id="43")
+    assert PE_MicrophoneSD.BACKEND == "sounddevice"
+
+
+def test_aruco_example_fallback_detector(aiko_process):
+    """examples/aruco_marker: numpy fallback finds two markers (one turned 90 degrees) with
+    rotation-invariant ids and marker-frame corners; the overlay draws on the image."""
+    import numpy as np
+    from aiko_services_amd.examples.aruco_marker.aruco import make_marker
+    a, b = make_marker(0b1000_0110_0010_1101, 6), make_marker(0b0001_0000_0111_0011, 5)
+    img = np.full((120, 160, 3), 255, np.uint8)
+    img[10:10 + a.shape[0], 10:10 + a.shape[1]] = a[..., None]
+    rb = np.rot90(b, -1)                                    # turned 90 degrees clockwise
+    img[50:50 + rb.shape[0], 90:90 + rb.shape[1]] = rb[..., None]
+    M = "aiko_services_amd.examples.aruco_marker.aruco"
+    d = {"version": 0, "name": "p_aruco", "runtime": "python",
+         "graph": ["(ArucoMarkerDetector ArucoMarkerOverlay)"],
+         "elements": [{"name": "ArucoMarkerDetector", "input": [{"name": "images", "type": "[image]"}],
+                       "output": [{"name": "overlays", "type": "[overlay]"}], "deploy": {"local": {"module": M}}},
+                      {"name": "ArucoMarkerOverlay", "input": [{"name": "images", "type": "[image]"},
+                                                                {"name": "overlays", "type": "[overlay]"}],
+                       "output": [{"name": "images", "type": "[image]"}, {"name": "overlays", "type": "[overlay]"}],
+                       "deploy": {"local": {"module": M}}}]}
+    p, q = _create(d, name="p_aruco", stream_id="51")
+    p.create_frame({"stream_id": "51", "frame_id": 0}, {"images": [img]})
+    info, out = q.get(timeout=5)
+    assert info["state"] == 0
+    ov = out["overlays"][0]
+    ids = sorted(int(i) for i in ov["ids"].reshape(-1))
+    from aiko_services_amd.examples.aruco_marker.aruco import _code, GRID
+    def canon(code):
+        bits = np.array([(code >> i) & 1 for i in range(16)]).reshape(4, 4)
+        return min(_code(np.rot90(bits, -k)) for k in range(4))
+    assert ids == sorted([canon(0b1000_0110_0010_1101), canon(0b0001_0000_0111_0011)])
+    assert len(ov["corners"]) == 2 and ov["corners"][0].shape == (1, 4, 2)
+    assert (out["images"][0] != img).any()

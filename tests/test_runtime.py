@@ -305,3 +305,34 @@ def test_xgo_robot_simulated_video_and_control(aiko_process):
     assert robot.share["pose"][0] != 0 or robot.share["pose"][1] != 0
     control.robot("stop")
     event.call_on_loop(lambda: event.remove_timer_handler(robot._tick))
+
+
+def test_ec_test_services(aiko_process):
+    """tools/ec_test: ECConsumerTest mirrors ECProducerTest's share and sees live log_level edits."""
+    aiko = aiko_process
+    from aiko_services_amd.control.share import PROTOCOL_EC_CONSUMER, PROTOCOL_EC_PRODUCER
+    from aiko_services_amd.runtime.connection import ConnectionState
+    from aiko_services_amd.runtime.context import compose_instance, service_args
+    from aiko_services_amd.tools.ec_test import ECConsumerTest, ECProducerTest
+
+    def build():
+        p = compose_instance(ECProducerTest, service_args("ec_producer_test", protocol=PROTOCOL_EC_PRODUCER,
+                                                          tags=["ec=true"]))
+        args = service_args("ec_consumer_test", protocol=PROTOCOL_EC_CONSUMER, tags=["ec=true"])
+        args.update(ec_producer_pid="0", ec_producer_topic_control=p.topic_control)
+        c = compose_instance(ECConsumerTest, args)
+        aiko.aiko.connection.update_state(ConnectionState.REGISTRAR)
+        return p, c
+    producer, consumer = event.call_on_loop(build)
+    deadline = time.time() + 5
+    while consumer.ec_consumer.cache_state != "ready" and time.time() < deadline:
+        time.sleep(0.01)
+    assert consumer.share_consumer["items"]["key_1"] == ["item_1a", "item_1b"]
+    aiko.aiko.message.publish(producer.topic_control, "(update log_level DEBUG)")
+    deadline = time.time() + 5
+    while consumer.share_consumer.get("log_level") != "DEBUG" and time.time() < deadline:
+        time.sleep(0.01)
+    assert consumer.share_consumer["log_level"] == "DEBUG"
+    assert ("update", "log_level", "DEBUG") in producer.changes
+    event.call_on_loop(consumer.ec_consumer.terminate)
+    event.call_on_loop(lambda: aiko.aiko.connection.update_state(ConnectionState.TRANSPORT))

@@ -91,3 +91,26 @@ def test_graph_reference_order_chain_with_revisit():
     for name in succ:
         g.add(Node(name, None, succ[name]))
     assert [n.name for n in g.get_path()] == ["PE_0", "PE_2", "PE_1"]
+
+
+def test_dashboard_plugin_pages():
+    """tools/dashboard plugins: lookup by service name / protocol; registrar + GPU pages."""
+    from aiko_services_amd.tools import dashboard as D
+    svc = ["aiko/host/10/1", "registrar", "au/registrar:2", "mqtt", "root", []]
+    gpu = ["aiko/host/11/2", "yolo", "au/pipeline:0", "mqtt", "root", ["ec=true"]]
+
+    class Fake:
+        variables = {"gpu_fps": "20000", "hbm_pool_mb": "512", "lifecycle": "ready"}
+        flat_variables = D.Dashboard.flat_variables
+
+        def services(self):
+            return [svc, gpu]
+    assert D.find_plugin(svc) is D.registrar_page
+    assert D.find_plugin(gpu) is None
+    lines = D.registrar_page(Fake(), svc)
+    assert len(lines) == 3 and "aiko/host/11/2" in lines[2]
+    g = D.gpu_page(Fake(), gpu)
+    assert any("gpu_fps" in r for r in g) and not any("lifecycle" in r for r in g)
+    D.register_plugin("yolo", D.gpu_page)
+    assert D.find_plugin(gpu) is D.gpu_page
+    del D.PLUGINS["yolo"]
