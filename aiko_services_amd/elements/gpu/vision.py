@@ -36,6 +36,8 @@ def _int(v, d):
 
 
 class SyntheticFrames(GpuPipelineElement):
+    lane_safe = True          # read-only frame pool
+
     def __init__(self, context):
         context.set_protocol("synthetic_frames:0")
         super().__init__(context)
@@ -86,6 +88,8 @@ class SyntheticFrames(GpuPipelineElement):
 
 
 class ImagePreprocess(GpuPipelineElement):
+    lane_safe = True
+
     def __init__(self, context):
         context.set_protocol("image_preprocess:0")
         super().__init__(context)
@@ -97,13 +101,15 @@ class ImagePreprocess(GpuPipelineElement):
         from ...ops import vision as V
         B = images.shape[0]
         Hp, Wp = C.stem_geometry(self.size, self.size)
-        out = self._out.get(B)
+        out = self._out.get((B, self.lane))
         if out is None:
-            out = self._out[B] = torch.empty(B, Hp, Wp, 4, dtype=torch.bfloat16, device=self.device)
+            out = self._out[(B, self.lane)] = torch.empty(B, Hp, Wp, 4, dtype=torch.bfloat16, device=self.device)
         return StreamEvent.OKAY, {"images": V.preprocess_frames(images, (self.size, self.size), out=out)}
 
 
 class ResNet50Classifier(GpuPipelineElement):
+    lane_safe = True          # one model workspace per lane (buffer tag)
+
     def __init__(self, context):
         context.set_protocol("resnet50:0")
         super().__init__(context)
@@ -119,11 +125,12 @@ class ResNet50Classifier(GpuPipelineElement):
         self._tuned = set()
 
     def _run(self, images):
+        tag = f"lane{self.lane}." if self.lane else ""
         if images.dtype == torch.uint8:
-            x = self.model.preprocess(images)
+            x = self.model.preprocess(images, tag)
         else:
             x = images
-        return self.model.logits_from_stem(x)
+        return self.model.logits_from_stem(x, tag)
 
     def process_frame(self, stream, images):
         key = (tuple(images.shape), images.dtype)
@@ -139,6 +146,8 @@ class ResNet50Classifier(GpuPipelineElement):
 
 
 class ClassifierTopK(GpuPipelineElement):
+    lane_safe = True          # device buffers and pinned host ring per lane
+
     def __init__(self, context):
         context.set_protocol("classifier_topk:0")
         super().__init__(context)
@@ -148,7 +157,7 @@ class ClassifierTopK(GpuPipelineElement):
         self._bufs = {}
 
     def _buffers(self, B, world):
-        key = (B, world)
+        key = (B, world, self.lane)
         b = self._bufs.get(key)
         if b is None:
             dev = self.device

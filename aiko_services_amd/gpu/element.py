@@ -177,9 +177,19 @@ class GpuPipelineElement(PipelineElement):
             self.share["weights"] = str(path)
         return model
 
+    # set True by elements whose mutable device state is keyed by the frame lane
+    lane_safe = False
+
+    @property
+    def lane(self) -> int:
+        """Frame lane of the frame being processed (``gpu/lanes.py``; 0 without lanes)."""
+        from .lanes import current_lane
+        return current_lane()
+
     def run_maybe_captured(self, key, fn, *inputs):
         if not self.use_graph:
             return fn(*inputs)
+        key = (key, self.lane)
         call = self._captured.get(key)
         if call is None:
             call = CapturedCall(fn, inputs)

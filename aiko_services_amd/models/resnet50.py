@@ -105,44 +105,90 @@ class ResNet50(WeightsMixin):
         self._ws.clear()
 
     # ---- forward ------------------------------------------------------------------------
-    def preprocess(self, frames: torch.Tensor) -> torch.Tensor:
+    def preprocess(self, frames: torch.Tensor, tag: str = "") -> torch.Tensor:
         """uint8 [B, H, W, 3] (any H, W) -> zero-bordered bf16 stem buffer [B, Hp, Wp, 4]."""
         B = frames.shape[0]
         S = self.image_size
         Hp, Wp = C.stem_geometry(S, S)
-        return V.preprocess_frames(frames, (S, S), out=self._buf("pre", (B, Hp, Wp, 4)))
+        return V.preprocess_frames(frames, (S, S), out=self._buf(tag + "pre", (B, Hp, Wp, 4)))
 
-    def features_from_stem(self, x: torch.Tensor) -> torch.Tensor:
-        """Stem buffer -> pooled features bf16 [B, 2048]."""
+    def features_from_stem(self, x: torch.Tensor, tag: str = "", after_block=None) -> torch.Tensor:
+        """Stem buffer -> pooled features bf16 [B, 2048].  ``after_block`` = (index, fn): call
+        ``fn()`` once bottleneck ``index`` is enqueued (-1: after the max-pool)."""
         B = x.shape[0]
         S = self.image_size
         Ho, Wo = C.stem_out_hw(S, S)
-        x = C.conv2d(x, self.stem, out=self._buf("stem", (B, Ho, Wo, 64)), image_hw=(S, S))
+        x = C.conv2d(x, self.stem, out=self._buf(tag + "stem", (B, Ho, Wo, 64)), image_hw=(S, S))
         Hm, Wm = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
-        x = V.maxpool2d(x, 3, 2, 1, out=self._buf("pool", (B, Hm, Wm, 64)))
+        x = V.maxpool2d(x, 3, 2, 1, out=self._buf(tag + "pool", (B, Hm, Wm, 64)))
+        if after_block is not None and after_block[0] < 0:
+            after_block[1]()
         for bi, blk in enumerate(self.blocks):
             H, W = x.shape[1], x.shape[2]
-            t1 = C.conv2d(x, blk.conv1, out=self._buf("t1", (B, H, W, blk.conv1.cout)))
+            t1 = C.conv2d(x, blk.conv1, out=self._buf(tag + "t1", (B, H, W, blk.conv1.cout)))
             Ho, Wo = blk.conv2.out_hw(H, W)
-            t2 = C.conv2d(t1, blk.conv2, out=self._buf("t2", (B, Ho, Wo, blk.conv2.cout)))
+            t2 = C.conv2d(t1, blk.conv2, out=self._buf(tag + "t2", (B, Ho, Wo, blk.conv2.cout)))
             key = "xa" if bi % 2 == 0 else "xb"
-            out = self._buf(key, (B, Ho, Wo, blk.conv3.cout))
+            out = self._buf(tag + key, (B, Ho, Wo, blk.conv3.cout))
             if blk.fused is not None and self.fuse_shortcut:
                 x = C.conv2d(t2, blk.fused, x2=x, out=out)
             elif blk.down is not None:
-                idn = C.conv2d(x, blk.down, out=self._buf("ds", (B, Ho, Wo, blk.down.cout)))
+                idn = C.conv2d(x, blk.down, out=self._buf(tag + "ds", (B, Ho, Wo, blk.down.cout)))
                 x = C.conv2d(t2, blk.conv3, residual=idn, out=out)
             else:
                 x = C.conv2d(t2, blk.conv3, residual=x, out=out)
-        return V.avgpool(x, out=self._buf("gap", (B, x.shape[3])))
+            if after_block is not None and after_block[0] == bi:
+                after_block[1]()
+        return V.avgpool(x, out=self._buf(tag + "gap", (B, x.shape[3])))
+
+    def _lanes(self, n: int) -> list:
+        lanes = getattr(self, "_lane_streams", None)
+        if lanes is None or len(lanes) < n:
+            lanes = self._lane_streams = [torch.cuda.Stream(self.device) for _ in range(n)]
+        return lanes[:n]
+
+    def logits_lanes(self, x: torch.Tensor, lanes: int, frames: bool = False,
+                     stagger: int | None = None) -> torch.Tensor:
+        """Forward split into ``lanes`` batch slices, each on its own HIP stream with its own
+        workspace, forked from and joined back into the current stream.  Captured in one
+        hipGraph the slices are independent branches: one slice's kernels fill the tail
+        and launch gaps of the other's, which a single in-order chain leaves idle.  With
+        ``stagger`` = block index, lane i+1 starts only once lane i has passed that block, so
+        the memory-bound early stages of one lane overlap the compute-bound late stages of
+        the other."""
+        B = x.shape[0]
+        if lanes <= 1 or B % lanes:
+            return self.logits(x) if frames else self.logits_from_stem(x)
+        out = self._buf("logits", (B, self.num_classes))
+        cur = torch.cuda.current_stream(self.device)
+        step = B // lanes
+        gate = None
+        for i, s in enumerate(self._lanes(lanes)):
+            s.wait_stream(cur)
+            if gate is not None:
+                s.wait_event(gate)
+            with torch.cuda.stream(s):
+                xi = x[i * step:(i + 1) * step]
+                tag = f"l{i}."
+                if frames:
+                    xi = self.preprocess(xi, tag)
+                hook = None
+                if stagger is not None and i + 1 < lanes:
+                    gate = torch.cuda.Event()
+                    hook = (stagger, lambda ev=gate, st=s: ev.record(st))
+                f = self.features_from_stem(xi, tag, after_block=hook)
+                C.linear(f, self.fc, out=out[i * step:(i + 1) * step])
+        for s in self._lanes(lanes):
+            cur.wait_stream(s)
+        return out
 
     def features(self, frames: torch.Tensor) -> torch.Tensor:
         """uint8 [B, H, W, 3] -> pooled features bf16 [B, 2048]."""
         return self.features_from_stem(self.preprocess(frames))
 
-    def logits_from_stem(self, x: torch.Tensor) -> torch.Tensor:
-        f = self.features_from_stem(x)
-        return C.linear(f, self.fc, out=self._buf("logits", (f.shape[0], self.num_classes)))
+    def logits_from_stem(self, x: torch.Tensor, tag: str = "") -> torch.Tensor:
+        f = self.features_from_stem(x, tag)
+        return C.linear(f, self.fc, out=self._buf(tag + "logits", (f.shape[0], self.num_classes)))
 
     def topk_from_logits(self, lg: torch.Tensor):
         B = lg.shape[0]
@@ -150,9 +196,9 @@ class ResNet50(WeightsMixin):
                               prob=self._buf("prob", (B, self.topk), torch.float32),
                               index=self._buf("index", (B, self.topk), torch.int32))
 
-    def logits(self, frames: torch.Tensor) -> torch.Tensor:
-        f = self.features(frames)
-        return C.linear(f, self.fc, out=self._buf("logits", (f.shape[0], self.num_classes)))
+    def logits(self, frames: torch.Tensor, tag: str = "") -> torch.Tensor:
+        f = self.features_from_stem(self.preprocess(frames, tag), tag)
+        return C.linear(f, self.fc, out=self._buf(tag + "logits", (f.shape[0], self.num_classes)))
 
     def forward(self, frames: torch.Tensor):
         lg = self.logits(frames)

@@ -633,7 +633,46 @@ class PipelineImpl(Pipeline):
         frame.swag.update(frame_data_in)
         return graph, stream
 
+    def _frame_lanes(self):
+        """(lanes, device) for ``gpu_lanes`` (see ``gpu/lanes.py``); decided on first use."""
+        cached = getattr(self, "_lanes_cfg", None)
+        if cached is not None:
+            return cached
+        lanes, found = self.get_parameter("gpu_lanes")
+        if not found:
+            lanes = os.environ.get("AIKO_GPU_LANES", 1)
+        try:
+            lanes = max(1, int(lanes))
+        except (TypeError, ValueError):
+            lanes = 1
+        device = None
+        if lanes > 1:
+            for node in self.pipeline_graph:
+                element, name, local, _ = PipelineGraph.get_element(node)
+                if not local:
+                    raise ValueError(f"gpu_lanes > 1 needs a fully local pipeline ({name} is remote)")
+                if hasattr(element, "device") and hasattr(element, "run_maybe_captured"):
+                    if not getattr(element, "lane_safe", False):
+                        raise ValueError(f"gpu_lanes > 1: GPU element {name} is not lane-safe")
+                    device = device or element.device
+            if device is None or getattr(device, "type", "cpu") != "cuda":
+                lanes = 1
+        self._lanes_cfg = (lanes, device)
+        self._lane_next = 0
+        self.share["gpu_lanes"] = lanes
+        return self._lanes_cfg
+
     def _process_frame_common(self, stream_dict, frame_data_in, new_frame):
+        lanes, device = self._frame_lanes()
+        if lanes > 1:
+            from ..gpu.lanes import lane_scope
+            lane = self._lane_next
+            self._lane_next = (lane + 1) % lanes
+            with lane_scope(lane, device):
+                return self._process_frame_body(stream_dict, frame_data_in, new_frame)
+        return self._process_frame_body(stream_dict, frame_data_in, new_frame)
+
+    def _process_frame_body(self, stream_dict, frame_data_in, new_frame):
         graph, stream = self._process_initialize(stream_dict, frame_data_in, new_frame)
         if graph is None:
             return False

@@ -38,7 +38,7 @@ METRIC = "frames/sec (whole node) + p50 latency, ResNet-50 pipeline at 1/2/4/8 M
 ELEMENTS = "aiko_services_amd.elements.gpu.vision"
 
 
-def definition(batch: int, graph: bool, height: int, width: int) -> dict:
+def definition(batch: int, graph: bool, height: int, width: int, lanes: int = 1) -> dict:
     def el(name, inputs, outputs, params=None):
         return {"name": name, "input": [{"name": n, "type": "tensor"} for n in inputs],
                 "output": [{"name": n, "type": "tensor"} for n in outputs],
@@ -46,7 +46,7 @@ def definition(batch: int, graph: bool, height: int, width: int) -> dict:
     return {
         "version": 0, "name": "p_resnet50_bench", "runtime": "python",
         "graph": ["(SyntheticFrames ResNet50Classifier ClassifierTopK)"],
-        "parameters": {},
+        "parameters": {"gpu_lanes": lanes},
         "elements": [
             el("SyntheticFrames", [], ["images", "t_submit"],
                {"batch": batch, "height": height, "width": width, "pool": 4}),
@@ -129,6 +129,9 @@ def main(argv=None):
     ap.add_argument("--width", type=int, default=224)
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture")
     ap.add_argument("--depth", type=int, default=2, help="batches in flight")
+    ap.add_argument("--lanes", type=int, default=2,
+                    help="(resnet50) frame lanes: successive batches alternate over this many HIP "
+                         "streams with private workspaces (gpu/lanes.py)")
     ap.add_argument("--model", choices=["resnet50", "yolov8n", "whisper-small", "whisper-tiny", "whisper-base"],
                     default="resnet50",
                     help="resnet50: headline ResNet-50 pipeline (config 2/3); yolov8n: config 4; "
@@ -178,9 +181,10 @@ def main(argv=None):
                                                "frame_size": [a.height, a.width], "fanout": a.fanout,
                                                "pipeline": d.graph[0]}
     else:
-        d = parse_pipeline_definition_dict(definition(a.batch, not a.no_graph, a.height, a.width))
+        d = parse_pipeline_definition_dict(definition(a.batch, not a.no_graph, a.height, a.width, a.lanes))
         result_key, model_cfg = "topk", {"model": "resnet50", "image_size": [a.height, a.width],
-                                         "pipeline": "(SyntheticFrames ResNet50Classifier ClassifierTopK)"}
+                                         "pipeline": "(SyntheticFrames ResNet50Classifier ClassifierTopK)",
+                                         "gpu_lanes": a.lanes}
     responses: queue.Queue = queue.Queue()
     pipeline = PipelineImpl.create_pipeline("<bench>", d, None, None, "bench", [], 0, None, 3600,
                                             queue_response=responses)

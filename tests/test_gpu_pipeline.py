@@ -12,12 +12,12 @@ def test_resnet_pipeline_matches_direct_model(native):
     from aiko_services_amd.models.resnet50 import ResNet50
     from aiko_services_amd.pipeline.definition import parse_pipeline_definition_dict
     from aiko_services_amd.pipeline.engine import PipelineImpl
-    for graph in (False, True):
-        d = parse_pipeline_definition_dict(bench.definition(4, graph, 224, 224))
+    for graph, lanes in ((False, 1), (True, 1), (True, 2), (False, 3)):
+        d = parse_pipeline_definition_dict(bench.definition(4, graph, 224, 224, lanes))
         q = queue.Queue()
         p = PipelineImpl.create_pipeline("<t>", d, None, None, "g", [], 0, None, 60, queue_response=q)
         results = []
-        for i in range(3):
+        for i in range(5):          # frames alternate over the lanes (own streams + workspaces)
             p.process_frame({"stream_id": "g", "frame_id": i}, {})
             info, out = q.get_nowait()
             assert info["state"] == 0
@@ -31,6 +31,7 @@ def test_resnet_pipeline_matches_direct_model(native):
             assert torch.equal(got["top_index"], idx.cpu())
             assert torch.allclose(got["top_prob"], prob.cpu(), rtol=1e-4, atol=1e-6)
             assert r.latency is not None and r.latency > 0
+        assert p.share["gpu_lanes"] == lanes
 
 
 def test_frame_pool_on_device(native):
