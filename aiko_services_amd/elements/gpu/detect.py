@@ -35,6 +35,7 @@ def _bool(v):
 
 
 class FrameFanout(GpuPipelineElement):
+    lane_safe = True
     """Ingest rank's ``[N*B, H, W, 3]`` batch -> this rank's ``[B, H, W, 3]`` (RCCL)."""
 
     def __init__(self, context):
@@ -67,14 +68,16 @@ class FrameFanout(GpuPipelineElement):
         return StreamEvent.OKAY, {"images": mine}
 
     def _buf(self, key, shape):
-        t = self._bufs.get((key, shape))
+        k = (key, shape, self.lane)
+        t = self._bufs.get(k)
         if t is None:
-            t = self._bufs[(key, shape)] = torch.empty(shape, dtype=torch.uint8, device=self.device)
+            t = self._bufs[k] = torch.empty(shape, dtype=torch.uint8, device=self.device)
         return t
 
 
 class YoloDetector(GpuPipelineElement):
     """uint8 RGB frames -> YOLOv8 detections (fixed-size rows + counts), on the HIP kernels."""
+    lane_safe = True          # one model workspace per lane
 
     def __init__(self, context):
         context.set_protocol("yolo_detector:0")
@@ -94,6 +97,7 @@ class YoloDetector(GpuPipelineElement):
         self._tuned = set()
 
     def _run(self, images):
+        self.model.ws_tag = f"lane{self.lane}." if self.lane else ""
         return self.model.detect(images)
 
     def process_frame(self, stream, images):
@@ -110,6 +114,7 @@ class YoloDetector(GpuPipelineElement):
 
 class DetectionsGather(GpuPipelineElement):
     """All-gather fixed-size detections over RCCL, copy to pinned host, emit a DeviceResult."""
+    lane_safe = True
 
     def __init__(self, context):
         context.set_protocol("detections_gather:0")
@@ -118,7 +123,7 @@ class DetectionsGather(GpuPipelineElement):
         self._bufs = {}
 
     def _buffers(self, shape, world):
-        key = (shape, world)
+        key = (shape, world, self.lane)
         b = self._bufs.get(key)
         if b is None:
             B, D_, six = shape

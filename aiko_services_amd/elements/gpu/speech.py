@@ -34,12 +34,15 @@ def _p(el, name, default):
 
 
 class AudioChunks(GpuPipelineElement):
+    lane_safe = True          # read-only synthetic pool; pinned upload ring
+
     def __init__(self, context):
         context.set_protocol("audio_chunks:0")
         super().__init__(context)
         self._pool = None
         self._cursor = 0
-        self._pinned = None
+        self._pinned: list = []
+        self._pin_slot = 0
 
     def _synthetic(self):
         if self._pool is None:
@@ -62,10 +65,18 @@ class AudioChunks(GpuPipelineElement):
             x = x[None]
         if x.device.type == "cuda":
             return x.float()
-        if self._pinned is None or self._pinned.shape != x.shape:
-            self._pinned = torch.empty(x.shape, dtype=torch.float32, pin_memory=True)
-        self._pinned.copy_(x)
-        return self._pinned.to(self.device, non_blocking=True)
+        if not self._pinned or self._pinned[0][0].shape != x.shape:
+            self._pinned = [[torch.empty(x.shape, dtype=torch.float32, pin_memory=True), None]
+                            for _ in range(4)]
+        slot = self._pinned[self._pin_slot]
+        self._pin_slot = (self._pin_slot + 1) % len(self._pinned)
+        if slot[1] is not None:
+            slot[1].synchronize()          # the H2D copy that last read this slot is done
+        slot[0].copy_(x)
+        out = slot[0].to(self.device, non_blocking=True)
+        slot[1] = torch.cuda.Event()
+        slot[1].record()
+        return out
 
     def process_frame(self, stream, audio_samples=None, **kwargs):
         audio = self._synthetic() if audio_samples is None else self._upload(audio_samples)
@@ -73,29 +84,48 @@ class AudioChunks(GpuPipelineElement):
 
 
 class AudioWindow(GpuPipelineElement):
+    """Per-stream sliding window over the last ``window`` seconds: frame k writes ring slot
+    k % R from slot (k-1) % R.  With L frame lanes, R = L + 1 and every update waits for the
+    previous frame's update (an event chain across the lane streams): slot k % R was last
+    read by frame k-L's window update and by the encoder of frame k-R, which ran on frame
+    k-1's lane before frame k-1's update — so the chain orders every reuse."""
+    lane_safe = True
+
     def __init__(self, context):
         context.set_protocol("audio_window:0")
         super().__init__(context)
         self.window = int(float(_p(self, "window", 30.0)) * RATE)
         self._ring = None
+        self._last = None
 
     def process_frame(self, stream, audio):
         B, n = audio.shape
         W = self.window
-        if self._ring is None or self._ring[0].shape[0] != B:
-            self._ring = [torch.zeros(B, W, dtype=torch.float32, device=self.device) for _ in range(2)]
+        lanes = getattr(self.pipeline, "_lanes_cfg", (1, None))[0] if self.pipeline is not None else 1
+        R = max(2, lanes + 1)
+        if self._ring is None or self._ring[0].shape[0] != B or len(self._ring) != R:
+            self._ring = [torch.zeros(B, W, dtype=torch.float32, device=self.device) for _ in range(R)]
             self._cur = 0
-        src, dst = self._ring[self._cur], self._ring[self._cur ^ 1]
+            self._last = None
+        src = self._ring[self._cur]
+        self._cur = (self._cur + 1) % R
+        dst = self._ring[self._cur]
+        if self._last is not None and self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).wait_event(self._last)
         if n >= W:
             dst.copy_(audio[:, n - W:])
         else:
             dst[:, :W - n].copy_(src[:, n:])
             dst[:, W - n:].copy_(audio)
-        self._cur ^= 1
+        if self.device.type == "cuda":
+            self._last = torch.cuda.Event()
+            self._last.record()
         return StreamEvent.OKAY, {"audio": dst}
 
 
 class WhisperEncoder(GpuPipelineElement):
+    lane_safe = True          # one model workspace per lane
+
     def __init__(self, context):
         context.set_protocol("whisper_encoder:0")
         super().__init__(context)
@@ -108,6 +138,7 @@ class WhisperEncoder(GpuPipelineElement):
         self._tuned = set()
 
     def _run(self, audio):
+        self.model.ws_tag = f"lane{self.lane}." if self.lane else ""
         return self.model.encode(audio)
 
     def process_frame(self, stream, audio):
@@ -124,23 +155,26 @@ class WhisperEncoder(GpuPipelineElement):
 
 
 class FeatureSink(GpuPipelineElement):
+    lane_safe = True          # device + pinned buffers per lane
+
     def __init__(self, context):
         context.set_protocol("feature_sink:0")
         super().__init__(context)
-        self._host = []
-        self._slot = 0
-        self._pooled = None
+        self._bufs: dict = {}
 
     def process_frame(self, stream, features, t_submit=None):
         B, T, d = features.shape
-        if self._pooled is None or self._pooled.shape != (B, d):
-            self._pooled = torch.empty(B, d, dtype=torch.float32, device=self.device)
+        b = self._bufs.get((B, d, self.lane))
+        if b is None:
             pin = self.device.type == "cuda"
-            self._host = [torch.empty(B, d, dtype=torch.float32, pin_memory=pin) for _ in range(8)]
-        torch.mean(features, dim=1, dtype=torch.float32, out=self._pooled)
-        h = self._host[self._slot]
-        self._slot = (self._slot + 1) % len(self._host)
-        h.copy_(self._pooled, non_blocking=True)
+            b = self._bufs[(B, d, self.lane)] = {
+                "pooled": torch.empty(B, d, dtype=torch.float32, device=self.device),
+                "host": [torch.empty(B, d, dtype=torch.float32, pin_memory=pin) for _ in range(8)],
+                "slot": 0}
+        torch.mean(features, dim=1, dtype=torch.float32, out=b["pooled"])
+        h = b["host"][b["slot"]]
+        b["slot"] = (b["slot"] + 1) % len(b["host"])
+        h.copy_(b["pooled"], non_blocking=True)
         ev = None
         if self.device.type == "cuda":
             ev = torch.cuda.Event()

@@ -92,6 +92,7 @@ class WhisperEncoder(WeightsMixin):
             self.blocks.append(blk)
         self.ln_post = ((1.0 + 0.1 * torch.randn(d, generator=g)).to(dev), small(d).to(dev))
         self._ws: dict = {}
+        self.ws_tag = ""             # workspace key prefix (one workspace per frame lane)
         self._pos_ready: set = set()
 
     # ---- weights ---------------------------------------------------------------------------------
@@ -112,7 +113,7 @@ class WhisperEncoder(WeightsMixin):
 
     # ---- workspace ------------------------------------------------------------------------------
     def _buf(self, key, shape, dtype=torch.bfloat16, zero=False):
-        k = (key, tuple(shape), dtype)
+        k = (self.ws_tag + key, tuple(shape), dtype)
         t = self._ws.get(k)
         if t is None:
             t = (torch.zeros if zero else torch.empty)(shape, dtype=dtype, device=self.device)
@@ -162,9 +163,9 @@ class WhisperEncoder(WeightsMixin):
         x = self._buf("x", (B * Tp, d), zero=True)
         M2 = B * Tp - 1
         pos = self._buf(f"pos{T}", (B * Tp, d), zero=True)
-        if (B, T) not in self._pos_ready:
+        if (self.ws_tag, B, T) not in self._pos_ready:
             pos.view(B, Tp, d)[:, :T] = self.pos[:T]
-            self._pos_ready.add((B, T))
+            self._pos_ready.add((self.ws_tag, B, T))
         C.conv2d(h1.view(1, B * rows1, 1, d), self.conv2, out=x[:M2].view(1, M2, 1, d),
                  residual=pos[:M2].view(1, M2, 1, d), residual_after_act=True)
         M = B * Tp
@@ -175,10 +176,10 @@ class WhisperEncoder(WeightsMixin):
         # fc1 -> fc2 hand-off in MX-fp8: the fc1 epilogue applies GELU and writes e4m3 + E8M0
         # block scales, fc2 feeds those scales straight to the scaled MFMA (no bf16 round trip,
         # no separate row-quantisation pass)
-        u8, usc = self._ws.get(("u_mx", M, 4 * d)) or (None, None)
+        u8, usc = self._ws.get((self.ws_tag + "u_mx", M, 4 * d)) or (None, None)
         if u8 is None:
             u8, usc = TR.mx_buffers(M, 4 * d, self.device)
-            self._ws[("u_mx", M, 4 * d)] = (u8, usc)
+            self._ws[(self.ws_tag + "u_mx", M, 4 * d)] = (u8, usc)
         for blk in self.blocks:
             TR.rownorm(x, *blk.ln1, q=q8, qs=s8)
             TR.linear_fp8(q8, s8, blk.qkv, out=qkv)

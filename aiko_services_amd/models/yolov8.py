@@ -143,6 +143,7 @@ class YOLOv8(WeightsMixin):
             cls.append(C.make_conv_spec(wcls, bcls, act=None, device=dev))
             self.heads.append(DetectLevel(box, cls, concat_cout(box[0], cls[0])))
         self._ws: dict = {}
+        self.ws_tag = ""             # workspace key prefix (one workspace per frame lane)
 
     def _c2f(self, g, cin, cout, n, shortcut):
         c = cout // 2
@@ -154,7 +155,7 @@ class YOLOv8(WeightsMixin):
 
     # ---- workspace ----------------------------------------------------------------------------
     def _buf(self, key, shape, dtype=torch.bfloat16):
-        k = (key, tuple(shape), dtype)
+        k = (self.ws_tag + key, tuple(shape), dtype)
         t = self._ws.get(k)
         if t is None:
             t = torch.empty(shape, dtype=dtype, device=self.device)

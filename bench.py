@@ -59,7 +59,7 @@ def definition(batch: int, graph: bool, height: int, width: int, lanes: int = 1)
 DETECT = "aiko_services_amd.elements.gpu.detect"
 
 
-def yolo_definition(batch: int, graph: bool, height: int, width: int, fanout: str) -> dict:
+def yolo_definition(batch: int, graph: bool, height: int, width: int, fanout: str, lanes: int = 1) -> dict:
     """BASELINE config 4: ingest rank decodes the node's frames, RCCL fan-out, YOLOv8-n +
     NMS kernels per GPU, RCCL all-gather of fixed-size detections."""
     def el(name, module, inputs, outputs, params):
@@ -68,7 +68,8 @@ def yolo_definition(batch: int, graph: bool, height: int, width: int, fanout: st
                 "parameters": params, "deploy": {"local": {"module": module}}}
     return {
         "version": 0, "name": "p_yolov8n_dp", "runtime": "python",
-        "graph": ["(SyntheticFrames FrameFanout YoloDetector DetectionsGather)"], "parameters": {},
+        "graph": ["(SyntheticFrames FrameFanout YoloDetector DetectionsGather)"],
+        "parameters": {"gpu_lanes": lanes},
         "elements": [
             el("SyntheticFrames", ELEMENTS, [], ["images", "t_submit"],
                {"batch": batch, "height": height, "width": width, "pool": 2, "global": True}),
@@ -84,7 +85,8 @@ SPEECH = "aiko_services_amd.elements.gpu.speech"
 WHISPER_METRIC = "30 s audio windows/sec (whole node) + p50 latency, Whisper encoder fp8 on streamed chunks"
 
 
-def whisper_definition(streams: int, graph: bool, size: str, chunk: float, window: float) -> dict:
+def whisper_definition(streams: int, graph: bool, size: str, chunk: float, window: float,
+                       lanes: int = 1) -> dict:
     """BASELINE config 5: streamed audio chunks -> per-stream sliding window on the GPU ->
     log-mel + Whisper encoder (fp8 linears) -> pooled features to the host."""
     def el(name, inputs, outputs, params):
@@ -93,7 +95,8 @@ def whisper_definition(streams: int, graph: bool, size: str, chunk: float, windo
                 "parameters": params, "deploy": {"local": {"module": SPEECH}}}
     return {
         "version": 0, "name": "p_whisper_encoder", "runtime": "python",
-        "graph": ["(AudioChunks AudioWindow WhisperEncoder FeatureSink)"], "parameters": {},
+        "graph": ["(AudioChunks AudioWindow WhisperEncoder FeatureSink)"],
+        "parameters": {"gpu_lanes": lanes},
         "elements": [
             el("AudioChunks", [], ["audio", "t_submit"], {"streams": streams, "chunk": chunk}),
             el("AudioWindow", ["audio"], ["audio"], {"window": window}),
@@ -130,7 +133,7 @@ def main(argv=None):
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture")
     ap.add_argument("--depth", type=int, default=2, help="batches in flight")
     ap.add_argument("--lanes", type=int, default=2,
-                    help="(resnet50) frame lanes: successive batches alternate over this many HIP "
+                    help="frame lanes: successive batches alternate over this many HIP "
                          "streams with private workspaces (gpu/lanes.py)")
     ap.add_argument("--model", choices=["resnet50", "yolov8n", "whisper-small", "whisper-tiny", "whisper-base"],
                     default="resnet50",
@@ -170,16 +173,16 @@ def main(argv=None):
     metric, unit = METRIC, "frames/s"
     if a.model.startswith("whisper"):
         size = a.model.split("-", 1)[1]
-        d = parse_pipeline_definition_dict(whisper_definition(a.batch, not a.no_graph, size, a.chunk, a.window))
+        d = parse_pipeline_definition_dict(whisper_definition(a.batch, not a.no_graph, size, a.chunk, a.window, a.lanes))
         result_key, model_cfg = "embedding", {"model": f"whisper-{size}-encoder", "weights": "fp8 e4m3 (per-channel)",
                                               "chunk_s": a.chunk, "window_s": a.window, "streams": a.batch,
-                                              "pipeline": d.graph[0]}
+                                              "pipeline": d.graph[0], "gpu_lanes": a.lanes}
         metric, unit = WHISPER_METRIC, "windows/s"
     elif a.model == "yolov8n":
-        d = parse_pipeline_definition_dict(yolo_definition(a.batch, not a.no_graph, a.height, a.width, a.fanout))
+        d = parse_pipeline_definition_dict(yolo_definition(a.batch, not a.no_graph, a.height, a.width, a.fanout, a.lanes))
         result_key, model_cfg = "detections", {"model": "yolov8n", "image_size": [640, 640],
                                                "frame_size": [a.height, a.width], "fanout": a.fanout,
-                                               "pipeline": d.graph[0]}
+                                               "pipeline": d.graph[0], "gpu_lanes": a.lanes}
     else:
         d = parse_pipeline_definition_dict(definition(a.batch, not a.no_graph, a.height, a.width, a.lanes))
         result_key, model_cfg = "topk", {"model": "resnet50", "image_size": [a.height, a.width],

@@ -119,3 +119,34 @@ def test_face_detector_example_pipeline(native):
     assert len(out["images"]) == 3 and out["images"][0].shape == (240, 320, 3)
     face = p.get_element("FaceDetector")
     assert face.model.nc == 1 and face.share["detections"] >= 0
+
+
+def _run_bench_pipeline(d, frames):
+    from aiko_services_amd.pipeline.definition import parse_pipeline_definition_dict
+    from aiko_services_amd.pipeline.engine import PipelineImpl
+    q = queue.Queue()
+    p = PipelineImpl.create_pipeline("<t>", parse_pipeline_definition_dict(d), None, None, "l", [], 0,
+                                     None, 60, queue_response=q)
+    outs = []
+    for i in range(frames):
+        p.process_frame({"stream_id": "l", "frame_id": i}, {})
+        info, out = q.get_nowait()
+        assert info["state"] == 0, out
+        outs.append(next(iter(out.values())))
+    return p, [{k: v.clone() for k, v in r.wait().items()} for r in outs]
+
+
+@pytest.mark.parametrize("lanes", [2, 3])
+def test_yolo_and_whisper_pipelines_lanes_match_single_lane(native, lanes):
+    """Frame lanes change only the schedule: YOLOv8n detections and the Whisper sliding-window
+    embeddings (a cross-frame state chained by events across lane streams) equal lanes=1."""
+    import bench
+    ref = _run_bench_pipeline(bench.yolo_definition(2, True, 240, 320, "scatter", 1), 5)[1]
+    p, got = _run_bench_pipeline(bench.yolo_definition(2, True, 240, 320, "scatter", lanes), 5)
+    assert p.share["gpu_lanes"] == lanes
+    for a, b in zip(ref, got):
+        assert torch.equal(a["count"], b["count"]) and torch.equal(a["det"], b["det"])
+    ref = _run_bench_pipeline(bench.whisper_definition(2, True, "tiny", 2.0, 6.0, 1), 6)[1]
+    p, got = _run_bench_pipeline(bench.whisper_definition(2, True, "tiny", 2.0, 6.0, lanes), 6)
+    for a, b in zip(ref, got):
+        assert torch.equal(a["pooled"], b["pooled"])
