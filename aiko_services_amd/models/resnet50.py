@@ -91,6 +91,7 @@ class ResNet50(WeightsMixin):
         self.fc = C.make_linear_spec(fc_w, fc_b, device=self.device)
         self._ws: dict = {}
         self.fuse_shortcut = True
+        self.fuse_stem_pool = True       # stem conv + ReLU + max-pool in one kernel
 
     # ---- workspace: every activation buffer allocated once per batch size ----------------
     def _buf(self, key: str, shape, dtype=torch.bfloat16) -> torch.Tensor:
@@ -118,9 +119,12 @@ class ResNet50(WeightsMixin):
         B = x.shape[0]
         S = self.image_size
         Ho, Wo = C.stem_out_hw(S, S)
-        x = C.conv2d(x, self.stem, out=self._buf(tag + "stem", (B, Ho, Wo, 64)), image_hw=(S, S))
         Hm, Wm = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
-        x = V.maxpool2d(x, 3, 2, 1, out=self._buf(tag + "pool", (B, Hm, Wm, 64)))
+        if self.fuse_stem_pool:
+            x = C.stem_pool(x, self.stem, (S, S), out=self._buf(tag + "pool", (B, Hm, Wm, 64)))
+        else:
+            x = C.conv2d(x, self.stem, out=self._buf(tag + "stem", (B, Ho, Wo, 64)), image_hw=(S, S))
+            x = V.maxpool2d(x, 3, 2, 1, out=self._buf(tag + "pool", (B, Hm, Wm, 64)))
         if after_block is not None and after_block[0] < 0:
             after_block[1]()
         for bi, blk in enumerate(self.blocks):

@@ -338,6 +338,23 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None
     return out
 
 
+def stem_pool(x: torch.Tensor, spec: ConvSpec, image_hw: tuple[int, int],
+              out: torch.Tensor | None = None) -> torch.Tensor:
+    """ResNet stem fused with its max-pool: ``maxpool3x3/s2/p1(relu(stem7x7/s2(x) + b))`` in ONE
+    kernel (``csrc/kernels/stem_pool.hip``) — the [B, H/2, W/2, 64] stem activation never
+    reaches HBM.  ``x`` is the zero-bordered preprocess buffer, ``spec`` a 7x7/s2 ReLU stem
+    with 64 output channels (``make_stem_spec``).  Bit-identical to ``conv2d`` + ``maxpool2d``."""
+    if spec.kind != "stem" or spec.stem_k != 7 or spec.stride != 2 or spec.cout != 64 \
+            or spec.act != ACT_RELU or spec.bias is None:
+        raise ValueError("stem_pool: needs a 7x7/s2 ReLU stem spec with 64 channels and a bias")
+    Ho, Wo = spec.out_hw(*image_hw)
+    Hm, Wm = (Ho - 1) // 2 + 1, (Wo - 1) // 2 + 1
+    if out is None:
+        out = torch.empty(x.shape[0], Hm, Wm, 64, dtype=torch.bfloat16, device=x.device)
+    torch.ops.aiko.stem_pool_out(x, spec.weight, spec.bias, out, Ho, Wo)
+    return out
+
+
 def linear(x: torch.Tensor, spec: ConvSpec, out: torch.Tensor | None = None,
            residual: torch.Tensor | None = None) -> torch.Tensor:
     """``[B, K] @ W^T + b`` on the same kernel (1x1 "image")."""

@@ -214,3 +214,28 @@ def test_batchnorm_standalone(native):
                                          gamma.to(DEV), beta.to(DEV), False, 0.0, 1e-5).relu()
     assert _rel_err(out[..., :32].permute(0, 3, 1, 2), ref) < 1e-2
     assert out[..., 32:].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("hw", [(224, 224), (160, 200)])
+def test_stem_pool_fused(native, hw):
+    """Fused stem + ReLU + max-pool kernel == conv2d stem + maxpool kernels (bit-exact), and
+    the fp32 torch reference of the same ops."""
+    import torch.nn.functional as F
+    from aiko_services_amd.ops import conv as C
+    from aiko_services_amd.ops import reference as R
+    from aiko_services_amd.ops import vision as V
+    g = torch.Generator().manual_seed(11)
+    B = 3
+    frames = torch.randint(0, 256, (B, hw[0], hw[1], 3), generator=g, dtype=torch.uint8)
+    w = torch.randn(64, 3, 7, 7, generator=g) / (3 * 49) ** 0.5
+    b = torch.randn(64, generator=g) * 0.1
+    spec = C.make_stem_spec(w, b, act="relu", device=DEV)
+    pre = V.preprocess_frames(frames.to(DEV), hw)
+    fused = C.stem_pool(pre, spec, hw)
+    unfused = V.maxpool2d(C.conv2d(pre, spec, image_hw=hw), 3, 2, 1)
+    torch.cuda.synchronize()
+    assert fused.shape == unfused.shape
+    assert torch.equal(fused, unfused)
+    xr = R.preprocess_ref(frames.to(DEV), hw)
+    ref = F.max_pool2d(R.conv_ref(xr.to(torch.bfloat16).float(), spec), 3, 2, 1)
+    assert _rel_err(fused.permute(0, 3, 1, 2), ref) < 1e-2
