@@ -56,7 +56,7 @@ int aiko_topk_nms(const void* boxes, const float* scores, const int* cls, int B,
                   hipStream_t stream);
 int aiko_avgpool(const void* x, void* y, int B, int HW, int C, hipStream_t stream);
 int aiko_stem_pool(const void* x, const void* w, const float* bias, void* y, int B, int Hp, int Wp,
-                   int Ho, int Wo, int Hm, int Wm, int ldy, hipStream_t stream);
+                   int Ho, int Wo, int Hm, int Wm, int ldy, int variant, hipStream_t stream);
 int aiko_softmax_topk(const void* logits, float* prob, int* index, int B, int N, int k,
                       hipStream_t stream);
 }
@@ -228,17 +228,19 @@ void maxpool_out(const at::Tensor& x, at::Tensor& y, int64_t k, int64_t s, int64
 }
 
 // Fused 7x7/s2 stem conv + bias + ReLU + 3x3/s2/p1 max-pool (stem_pool.hip).  x: the zero-bordered
-// [B, Hp, Wp, 4] preprocess buffer; w: [64, 256] packed stem weights; y: [B, Hm, Wm, 64] (slice ok).
+// [B, Hp, Wp, 4] preprocess buffer; w: [7, 64, 32] LDS image of the stem weights (16-byte chunks
+// XOR-swizzled by channel >> 2, built by ops.conv.stem_pool); y: [B, Hm, Wm, 64] (slice ok).
 void stem_pool_out(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, at::Tensor& y,
-                   int64_t Ho, int64_t Wo) {
+                   int64_t Ho, int64_t Wo, int64_t variant) {
   check_cuda(x, "x");
   check_cuda(w, "w");
   check_cuda(bias, "bias");
   check_cuda(y, "y");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(3) == 4 && x.is_contiguous(),
               "aiko.stem_pool_out: x must be a contiguous [B, Hp, Wp, 4] bf16 stem buffer");
-  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.dim() == 2 && w.size(0) == 64 && w.size(1) == 256 &&
-                  w.is_contiguous(), "aiko.stem_pool_out: w must be the packed [64, 256] 7x7 stem weight");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.dim() == 3 && w.size(0) == 7 && w.size(1) == 64 &&
+                  w.size(2) == 32 && w.is_contiguous(),
+              "aiko.stem_pool_out: w must be the [7, 64, 32] swizzled stem weight image (ops.conv.stem_pool)");
   TORCH_CHECK(bias.scalar_type() == at::kFloat && bias.numel() == 64 && bias.is_contiguous(),
               "aiko.stem_pool_out: bias must be fp32 [64]");
   const int64_t ldy = pixel_pitch(y, "stem_pool_out");
@@ -253,7 +255,7 @@ void stem_pool_out(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b
                   reinterpret_cast<uintptr_t>(bias.data_ptr()) % 16 == 0,
               "aiko.stem_pool_out: operands must be 16-byte aligned");
   check_launch(aiko_stem_pool(x.data_ptr(), w.data_ptr(), bias.data_ptr<float>(), y.data_ptr(), B, Hp, Wp,
-                              Ho, Wo, Hm, Wm, ldy, cur_stream()),
+                              Ho, Wo, Hm, Wm, ldy, (int)variant, cur_stream()),
                "stem_pool");
 }
 
@@ -589,7 +591,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("topk_nms_out(Tensor boxes, Tensor scores, Tensor cls, int max_cand, float[] params, Tensor(a!) det, Tensor(b!) count) -> ()");
   m.def("maxpool_out(Tensor x, Tensor(a!) y, int k, int s, int p) -> ()");
   m.def("avgpool_out(Tensor x, Tensor(a!) y) -> ()");
-  m.def("stem_pool_out(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, int Ho, int Wo) -> ()");
+  m.def("stem_pool_out(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, int Ho, int Wo, int variant=0) -> ()");
   m.def("gemm_fp8_out(Tensor a, Tensor? sa, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!)? y, int act, int bm, int bn, int variant=0, Tensor? zero=None, Tensor? amx=None, Tensor(b!)? yq=None, Tensor(c!)? ysc=None) -> ()");
   m.def("rownorm_quant_out(Tensor x, Tensor? gamma, Tensor? beta, float eps, Tensor(a!)? yb, Tensor(b!)? q, Tensor(c!)? qs) -> ()");
   m.def("attn_fwd_out(Tensor q, Tensor k, Tensor v, Tensor(a!) o, int B, int H, int T, int Tpad, float scale) -> ()");

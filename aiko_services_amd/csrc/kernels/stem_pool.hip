@@ -7,8 +7,10 @@
 // stem pixels (10 % halo recompute), and never writes the stem activation to HBM:
 //
 //  1. the input patch the region needs — 39 rows x 64 pixels x 4 channels of the zero-bordered
-//     preprocess buffer, 20 KB — is loaded into LDS once; the folded weights [7][64][32] (28 KB)
-//     too, 16-byte chunks XOR-swizzled by (channel >> 2) so fragment reads are conflict-free;
+//     preprocess buffer, 20 KB — is DMA'd into LDS (buffer_load ... lds, out-of-image chunks
+//     read as zero); the folded weights [7][64][32] (28 KB) too, from a host-prepared image
+//     whose 16-byte chunks are XOR-swizzled by (channel >> 2) & 2, which makes the A-fragment
+//     ds_read_b128 conflict-free for its lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, ...;
 //  2. MFMA v_mfma_f32_16x16x32_bf16 with channels as the A rows and stem pixels as the B
 //     columns: one K=32 step is exactly one filter row (8 pixels x 4 channels; pixel 7 and
 //     channel 3 carry zero weights), so a B fragment is 16 contiguous bytes of one patch row —
@@ -16,8 +18,10 @@
 //     Each of the 4 waves computes 128 stem pixels x 64 channels (8 x 4 accumulator tiles);
 //  3. epilogue: bias + ReLU, stem pixels outside the image forced to 0 (ReLU output >= 0, so 0
 //     is a valid -inf for the pool), 4 channels packed per 8-byte LDS write into the stem tile
-//     [512 px][64 ch] (aliasing the patch/weights), chunks XOR-swizzled by (pixel & 15);
-//  4. 3x3/s2 max over the LDS tile, 8 channels (16 B) per thread, coalesced 16-byte stores.
+//     [px][64 ch + 8 B pad] (aliasing the patch/weights; the 136-B pitch spreads 16 pixels'
+//     8-byte writes over all 32 write banks);
+//  4. 3x3/s2 max over the LDS tile, 8 channels (16 B) per thread as packed u16 max on the
+//     non-negative bf16 bit patterns, coalesced 16-byte stores.
 //
 // Rounding is identical to the unfused path: the stem value is rounded to bf16 before the max.
 #include "common.h"
@@ -26,30 +30,47 @@ namespace aiko {
 
 namespace {
 
-constexpr int kTPH = 8, kTPW = 14;                     // pooled tile
-constexpr int kSRH = 2 * kTPH + 1, kSRW = 2 * kTPW + 1;  // stem region 17 x 29
-constexpr int kNPix = kSRH * kSRW;                      // 493 stem pixels
+constexpr int kTPH = 8;                                 // pooled tile rows
+constexpr int kSRH = 2 * kTPH + 1;                      // stem region rows (17)
 constexpr int kPatchH = 2 * (kSRH - 1) + 7;             // 39 input rows
-constexpr int kPatchW = 2 * (kSRW - 1) + 8;             // 64 input pixels
-constexpr int kPatchRowB = kPatchW * 8;                 // 512 B per patch row
-constexpr int kPatchB = kPatchH * kPatchRowB;           // 19968 B
 constexpr int kWB = 7 * 64 * 64;                        // 28672 B of weights
-constexpr int kSB = 512 * 128;                          // stem tile, 128 B per pixel
-constexpr int kLdsB = (kPatchB + kWB) > kSB ? (kPatchB + kWB) : kSB;
-static_assert(kNPix <= 512, "4 waves x 128 pixels");
+constexpr int kSPitch = 136;                            // stem-tile pixel pitch: 64 ch + 8 B pad
+
+// pooled tile width TPW: 14 -> 17 x 29 stem region, 4 waves x 128 pixels, 64 KB LDS (2 WG/CU);
+//                         7 -> 17 x 15 stem region, 4 waves x 64 pixels, 39 KB LDS (4 WG/CU)
+template <int TPW>
+struct StemTile {
+  static constexpr int SRW = 2 * TPW + 1;
+  static constexpr int NPIX = kSRH * SRW;
+  static constexpr int NB = TPW == 14 ? 8 : 4;          // 16-pixel blocks per wave
+  static constexpr int PATCH_W = 2 * (SRW - 1) + 8;     // input pixels per patch row
+  static constexpr int ROW_B = PATCH_W * 8;
+  static constexpr int PATCH_CH = kPatchH * (PATCH_W / 2);              // 16-byte chunks
+  static constexpr int PATCH_B = (PATCH_CH + 255) / 256 * 256 * 16;    // whole DMA rounds
+  static constexpr int S_B = 4 * NB * 16 * kSPitch;     // stem tile, 136 B per pixel
+  static constexpr int LDS_B = (PATCH_B + kWB) > S_B ? (PATCH_B + kWB) : S_B;
+  static constexpr int WGS = TPW == 14 ? 2 : 4;
+  static_assert(NPIX <= 4 * NB * 16, "4 waves cover the stem region");
+};
+
+typedef __attribute__((ext_vector_type(2))) unsigned short u16x2;
 
 struct StemPoolParams {
   const bf16_t* x;      // [B, Hp, Wp, 4]
-  const bf16_t* w;      // [64, 256]  K = r * 32 + pixel * 4 + channel
+  const bf16_t* w;      // [7][64][4 x 16 B] pre-swizzled LDS image of the stem weights
   const float* bias;    // [64]
   bf16_t* y;            // [B, Hm, Wm, ldy]
   int B, Hp, Wp, Ho, Wo, Hm, Wm, ldy, tiles_h, tiles_w;
 };
 
-__global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemPoolParams p) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[kLdsB];
+template <int TPW>
+__global__ __launch_bounds__(256, StemTile<TPW>::WGS) void stem_pool_kernel(StemPoolParams p) {
+  using T = StemTile<TPW>;
+  constexpr int kTPW = TPW, kSRW = T::SRW, kNPix = T::NPIX, NB = T::NB;
+  constexpr int kPatchW = T::PATCH_W, kPatchRowB = T::ROW_B;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[T::LDS_B];
   unsigned char* patch = smem;
-  unsigned char* wl = smem + kPatchB;
+  unsigned char* wl = smem + T::PATCH_B;
   unsigned char* st = smem;                             // stem tile, after the MFMAs
 
   const int tid = threadIdx.x;
@@ -64,29 +85,45 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemPoolParams p) {
   const int sy0 = 2 * py0 - 1, sx0 = 2 * px0 - 1;      // stem region origin
   const int gy0 = 2 * sy0, gx0 = 2 * sx0;               // patch origin in the padded buffer
 
-  // ---- 1. patch + weights -> LDS ----
-  const bf16_t* ximg = p.x + (size_t)img * p.Hp * p.Wp * 4;
-  for (int i = tid; i < kPatchH * (kPatchW / 2); i += 256) {
-    const int r = i / (kPatchW / 2), c = i - r * (kPatchW / 2);
-    const int gy = gy0 + r, gx = gx0 + 2 * c;
-    u32x4 v = {0u, 0u, 0u, 0u};
-    if ((unsigned)gy < (unsigned)p.Hp && gx >= 0 && gx + 1 < p.Wp)
-      v = *reinterpret_cast<const u32x4*>(ximg + ((size_t)gy * p.Wp + gx) * 4);
-    *reinterpret_cast<u32x4*>(patch + r * kPatchRowB + c * 16) = v;
-  }
-  for (int i = tid; i < 7 * 64 * 4; i += 256) {
-    const int r = i >> 8, o = (i >> 2) & 63, q = i & 3;
-    const u32x4 v = *reinterpret_cast<const u32x4*>(p.w + o * 256 + r * 32 + q * 8);
-    *reinterpret_cast<u32x4*>(wl + ((r * 64 + o) * 4 + (q ^ ((o >> 2) & 3))) * 16) = v;
+  // ---- 1. patch + weights -> LDS by buffer DMA (no VGPR staging, no ds_write) ----
+  // patch chunk i (row i / (W/2), 2 pixels) lands at LDS byte 16 i: one wave instruction
+  // fills 64 consecutive chunks.  Chunks outside the image get an offset past num_records,
+  // which the hardware reads as zero (conv padding / region beyond the image); the rounds
+  // past the last chunk write zeros into the patch's own rounding slack.
+  {
+    const uint32_t img_bytes = (uint32_t)p.Hp * p.Wp * 8;
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(p.x + (size_t)img * p.Hp * p.Wp * 4), (short)0, (int)img_bytes, 0x00020000);
+    constexpr int CPR = kPatchW / 2;                     // chunks per patch row
+#pragma unroll
+    for (int k = 0; k < T::PATCH_B / 16 / 256; ++k) {
+      const int i = (k * 4 + wave) * 64 + lane;
+      const int r = i / CPR, c = i - r * CPR;
+      const int gy = gy0 + r, gx = gx0 + 2 * c;
+      const bool ok = i < T::PATCH_CH && (unsigned)gy < (unsigned)p.Hp && gx >= 0 && gx + 1 < p.Wp;
+      const uint32_t off = ok ? (uint32_t)(gy * p.Wp + gx) * 8 : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rx, reinterpret_cast<__attribute__((address_space(3))) void*>(
+                  reinterpret_cast<uintptr_t>(patch + (k * 4 + wave) * 1024)), 16, off, 0, 0, 0);
+    }
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(p.w), (short)0, kWB, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < kWB / 16 / 256; ++k)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rw, reinterpret_cast<__attribute__((address_space(3))) void*>(
+                  reinterpret_cast<uintptr_t>(wl + (k * 4 + wave) * 1024)), 16,
+          (uint32_t)(((k * 4 + wave) * 64 + lane) * 16), 0, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
 
   // ---- 2. MFMA: channels (A rows) x stem pixels (B columns), one filter row per K step ----
   const int fr = lane & 15, fq = lane >> 4;
-  int b_off[8];
+  int b_off[NB];
 #pragma unroll
-  for (int nb = 0; nb < 8; ++nb) {
-    int n = wave * 128 + nb * 16 + fr;
+  for (int nb = 0; nb < NB; ++nb) {
+    int n = wave * NB * 16 + nb * 16 + fr;
     if (n >= kNPix) n = 0;                               // dummy column, result discarded
     const int ly = n / kSRW, lx = n - ly * kSRW;
     b_off[nb] = 2 * ly * kPatchRowB + (2 * lx) * 8 + fq * 16;
@@ -95,13 +132,13 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemPoolParams p) {
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) {
     const int o = mb * 16 + fr;
-    a_off[mb] = (o * 4 + (fq ^ ((o >> 2) & 3))) * 16;
+    a_off[mb] = (o * 4 + (fq ^ ((o >> 2) & 2))) * 16;
   }
-  f32x4 acc[4][8];
+  f32x4 acc[4][NB];
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
-    for (int nb = 0; nb < 8; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll
   for (int r = 0; r < 7; ++r) {
@@ -110,7 +147,7 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemPoolParams p) {
     for (int mb = 0; mb < 4; ++mb)
       af[mb] = *reinterpret_cast<const bf16x8*>(wl + r * 64 * 64 + a_off[mb]);
 #pragma unroll
-    for (int nb = 0; nb < 8; ++nb) {
+    for (int nb = 0; nb < NB; ++nb) {
       const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(patch + r * kPatchRowB + b_off[nb]);
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb)
@@ -126,52 +163,58 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemPoolParams p) {
   __syncthreads();                                       // patch/weights dead: reuse as stem tile
 
   // ---- 3. bias + ReLU -> bf16 stem tile in LDS ----
+  // Tiles whose whole stem region lies inside the image (most of them) skip the per-pixel
+  // validity test (a workgroup-uniform branch).
+  const bool interior = sy0 >= 0 && sx0 >= 0 && sy0 + kSRH <= p.Ho && sx0 + kSRW <= p.Wo;
 #pragma unroll
-  for (int nb = 0; nb < 8; ++nb) {
-    const int n = wave * 128 + nb * 16 + fr;
+  for (int nb = 0; nb < NB; ++nb) {
+    const int n = wave * NB * 16 + nb * 16 + fr;
     if (n >= kNPix) continue;
-    const int ly = n / kSRW, lx = n - ly * kSRW;
-    const bool valid = (unsigned)(sy0 + ly) < (unsigned)p.Ho && (unsigned)(sx0 + lx) < (unsigned)p.Wo;
+    bool valid = true;
+    if (!interior) {
+      const int ly = n / kSRW, lx = n - ly * kSRW;
+      valid = (unsigned)(sy0 + ly) < (unsigned)p.Ho && (unsigned)(sx0 + lx) < (unsigned)p.Wo;
+    }
 #pragma unroll
     for (int mb = 0; mb < 4; ++mb) {
-      float v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = valid ? fmaxf(acc[mb][nb][e] + bias[mb][e], 0.f) : 0.f;
-      const int c = mb * 4 + fq;                         // 8-byte chunk (4 channels)
+      // acc + bias in packed fp32; max(., 0) gives +0 for non-positive sums (acc starts at +0,
+      // so the sum is never -0) — the pool below compares bit patterns
+      const f32x2 a01 = f32x2{acc[mb][nb][0], acc[mb][nb][1]} + f32x2{bias[mb][0], bias[mb][1]};
+      const f32x2 a23 = f32x2{acc[mb][nb][2], acc[mb][nb][3]} + f32x2{bias[mb][2], bias[mb][3]};
       uint2 o2;
-      o2.x = pack2(v[0], v[1]);
-      o2.y = pack2(v[2], v[3]);
-      *reinterpret_cast<uint2*>(st + n * 128 + ((c ^ (n & 15)) * 8)) = o2;
+      o2.x = valid ? pack2(fmaxf(a01[0], 0.f), fmaxf(a01[1], 0.f)) : 0u;
+      o2.y = valid ? pack2(fmaxf(a23[0], 0.f), fmaxf(a23[1], 0.f)) : 0u;
+      *reinterpret_cast<uint2*>(st + n * kSPitch + (mb * 4 + fq) * 8) = o2;
     }
   }
   __syncthreads();
 
   // ---- 4. 3x3/s2 max-pool from LDS, 8 channels per item ----
+  // Every value is a ReLU output (+0 or positive; the epilogue never produces -0), so the max
+  // of the bf16 bit patterns as unsigned 16-bit integers is the float max: v_pk_max_u16 on
+  // packed pairs, no unpacking.  The 9 reads are immediate offsets from one base address.
   for (int it = tid; it < kTPH * kTPW * 8; it += 256) {
     const int pp = it >> 3, g = it & 7;
     const int py = pp / kTPW, px = pp - py * kTPW;
     const int gy = py0 + py, gx = px0 + px;
     if (gy >= p.Hm || gx >= p.Wm) continue;
-    float m[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) m[e] = 0.f;
+    const unsigned char* base = st + ((2 * py) * kSRW + 2 * px) * kSPitch + g * 16;
+    u16x2 m[4] = {u16x2{0, 0}, u16x2{0, 0}, u16x2{0, 0}, u16x2{0, 0}};
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
       for (int dx = 0; dx < 3; ++dx) {
-        const int n = (2 * py + dy) * kSRW + 2 * px + dx;
-        const int s = n & 15;
-        u32x4 v = *reinterpret_cast<const u32x4*>(st + n * 128 + ((g ^ (s >> 1)) * 16));
-        if (s & 1) v = u32x4{v[2], v[3], v[0], v[1]};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          m[2 * e] = fmaxf(m[2 * e], __uint_as_float(v[e] << 16));
-          m[2 * e + 1] = fmaxf(m[2 * e + 1], __uint_as_float(v[e] & 0xffff0000u));
-        }
+        const unsigned char* q = base + (dy * kSRW + dx) * kSPitch;
+        const uint2 lo = *reinterpret_cast<const uint2*>(q);
+        const uint2 hi = *reinterpret_cast<const uint2*>(q + 8);
+        m[0] = __builtin_elementwise_max(m[0], __builtin_bit_cast(u16x2, lo.x));
+        m[1] = __builtin_elementwise_max(m[1], __builtin_bit_cast(u16x2, lo.y));
+        m[2] = __builtin_elementwise_max(m[2], __builtin_bit_cast(u16x2, hi.x));
+        m[3] = __builtin_elementwise_max(m[3], __builtin_bit_cast(u16x2, hi.y));
       }
     u32x4 o;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = pack2(m[2 * e], m[2 * e + 1]);
+    for (int e = 0; e < 4; ++e) o[e] = __builtin_bit_cast(uint32_t, m[e]);
     *reinterpret_cast<u32x4*>(p.y + ((size_t)(img * p.Hm + gy) * p.Wm + gx) * p.ldy + g * 8) = o;
   }
 }
@@ -183,9 +226,11 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemPoolParams p) {
 // x: zero-bordered stem input [B, Hp, Wp, 4] bf16 (image at (3, 3)); w: packed stem weights
 // [64, 256] (make_stem_spec: 7 filter rows x 8 pixels x 4 channels, K padded to 256); y: pooled
 // [B, Hm, Wm, >= 64] (pixel pitch ldy).  Host preconditions (binding): Cout 64, 7x7/s2 stem,
-// Hp >= 2 * Ho + 5, Wp >= 2 * Wo + 6, Hm/Wm = pool(Ho/Wo), 16-byte alignment.
+// Hp >= 2 * Ho + 5, Wp >= 2 * Wo + 6, Hm/Wm = pool(Ho/Wo), 16-byte alignment.  variant 0: 8x7
+// pooled tiles (4 WG/CU), 1: 8x14 (2 WG/CU, less halo recompute).
 extern "C" int aiko_stem_pool(const void* x, const void* w, const float* bias, void* y, int B, int Hp,
-                              int Wp, int Ho, int Wo, int Hm, int Wm, int ldy, hipStream_t stream) {
+                              int Wp, int Ho, int Wo, int Hm, int Wm, int ldy, int variant,
+                              hipStream_t stream) {
   using namespace aiko;
   StemPoolParams p;
   p.x = static_cast<const bf16_t*>(x);
@@ -193,10 +238,14 @@ extern "C" int aiko_stem_pool(const void* x, const void* w, const float* bias, v
   p.bias = bias;
   p.y = static_cast<bf16_t*>(y);
   p.B = B; p.Hp = Hp; p.Wp = Wp; p.Ho = Ho; p.Wo = Wo; p.Hm = Hm; p.Wm = Wm; p.ldy = ldy;
+  const int tpw = variant == 1 ? 14 : 7;
   p.tiles_h = (Hm + kTPH - 1) / kTPH;
-  p.tiles_w = (Wm + kTPW - 1) / kTPW;
+  p.tiles_w = (Wm + tpw - 1) / tpw;
   const long grid = (long)B * p.tiles_h * p.tiles_w;
   if (grid <= 0 || grid > 0x7fffffffL) return -1;
-  stem_pool_kernel<<<dim3((unsigned)grid), dim3(256), 0, stream>>>(p);
+  if (tpw == 14)
+    stem_pool_kernel<14><<<dim3((unsigned)grid), dim3(256), 0, stream>>>(p);
+  else
+    stem_pool_kernel<7><<<dim3((unsigned)grid), dim3(256), 0, stream>>>(p);
   return (int)hipGetLastError();
 }

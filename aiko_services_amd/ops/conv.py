@@ -338,8 +338,28 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None
     return out
 
 
+STEM_POOL_VARIANT = 0     # 0: 8x7 pooled tiles (4 workgroups/CU); 1: 8x14 (2 workgroups/CU)
+
+
+def stem_pool_weight(spec: ConvSpec) -> torch.Tensor:
+    """[7, 64, 32] LDS image of a packed 7x7 stem weight for the fused kernel: filter row r,
+    channel o, 16-byte chunk ``pos`` holds K columns ``r*32 + 8*(pos ^ ((o >> 2) & 2))`` (the
+    swizzle that makes the kernel's A-fragment reads bank-conflict free).  Cached on the spec,
+    rebuilt when the weight tensor changes."""
+    key = (spec.weight.data_ptr(), spec.weight._version)
+    cached = getattr(spec, "_stem_pool_w", None)
+    if cached is not None and cached[0] == key:
+        return cached[1]
+    w = spec.weight.view(64, 8, 4, 8)[:, :7].permute(1, 0, 2, 3)         # [r, o, q, j]
+    o = torch.arange(64, device=w.device)
+    q = torch.arange(4, device=w.device)[None, :] ^ ((o[:, None] >> 2) & 2)  # [o, pos]
+    img = torch.gather(w, 2, q[None, :, :, None].expand(7, 64, 4, 8)).reshape(7, 64, 32).contiguous()
+    spec._stem_pool_w = (key, img)
+    return img
+
+
 def stem_pool(x: torch.Tensor, spec: ConvSpec, image_hw: tuple[int, int],
-              out: torch.Tensor | None = None) -> torch.Tensor:
+              out: torch.Tensor | None = None, variant: int | None = None) -> torch.Tensor:
     """ResNet stem fused with its max-pool: ``maxpool3x3/s2/p1(relu(stem7x7/s2(x) + b))`` in ONE
     kernel (``csrc/kernels/stem_pool.hip``) — the [B, H/2, W/2, 64] stem activation never
     reaches HBM.  ``x`` is the zero-bordered preprocess buffer, ``spec`` a 7x7/s2 ReLU stem
@@ -351,7 +371,8 @@ def stem_pool(x: torch.Tensor, spec: ConvSpec, image_hw: tuple[int, int],
     Hm, Wm = (Ho - 1) // 2 + 1, (Wo - 1) // 2 + 1
     if out is None:
         out = torch.empty(x.shape[0], Hm, Wm, 64, dtype=torch.bfloat16, device=x.device)
-    torch.ops.aiko.stem_pool_out(x, spec.weight, spec.bias, out, Ho, Wo)
+    torch.ops.aiko.stem_pool_out(x, stem_pool_weight(spec), spec.bias, out, Ho, Wo,
+                                 STEM_POOL_VARIANT if variant is None else variant)
     return out
 
 

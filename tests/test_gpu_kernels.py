@@ -231,11 +231,12 @@ def test_stem_pool_fused(native, hw):
     b = torch.randn(64, generator=g) * 0.1
     spec = C.make_stem_spec(w, b, act="relu", device=DEV)
     pre = V.preprocess_frames(frames.to(DEV), hw)
-    fused = C.stem_pool(pre, spec, hw)
+    fused = C.stem_pool(pre, spec, hw, variant=0)
     unfused = V.maxpool2d(C.conv2d(pre, spec, image_hw=hw), 3, 2, 1)
+    wide = C.stem_pool(pre, spec, hw, variant=1)
     torch.cuda.synchronize()
     assert fused.shape == unfused.shape
-    assert torch.equal(fused, unfused)
+    assert torch.equal(fused, unfused) and torch.equal(wide, unfused)
     xr = R.preprocess_ref(frames.to(DEV), hw)
     ref = F.max_pool2d(R.conv_ref(xr.to(torch.bfloat16).float(), spec), 3, 2, 1)
     assert _rel_err(fused.permute(0, 3, 1, 2), ref) < 1e-2
