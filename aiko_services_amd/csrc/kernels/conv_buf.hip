@@ -44,22 +44,24 @@ __device__ __forceinline__ void vm_barrier() {
 
 }  // namespace
 
-// WGM x WGN waves per workgroup; ring slots as many as fit the workgroup's LDS share (up to 3)
-template <int BM, int BN, int NW>
+// WGM x WGN waves per workgroup; ring slots as many as fit the workgroup's LDS share (up to 3).
+// OCC > 0 forces that many workgroups per CU (high-occupancy variant 3: short-K GEMMs are
+// bound by one memory latency per tile, so more tiles in flight per CU beat a deeper ring).
+template <int BM, int BN, int NW, int OCC>
 constexpr int buf_wgs_per_cu() {
-  return NW == 8 ? 1 : ((BM == 64 && BN == 64) ? 3 : 2);
+  return OCC ? OCC : (NW == 8 ? 1 : ((BM == 64 && BN == 64) ? 3 : 2));
 }
-template <int BM, int BN, int NW>
+template <int BM, int BN, int NW, int OCC>
 constexpr int buf_slots() {
-  return (BM + BN) * 64 * 2 * 3 <= (160 * 1024) / buf_wgs_per_cu<BM, BN, NW>() ? 3 : 2;
+  return (BM + BN) * 64 * 2 * 3 <= (160 * 1024) / buf_wgs_per_cu<BM, BN, NW, OCC>() ? 3 : 2;
 }
 
-template <int BM, int BN, int WGM, int WGN>
-__global__ __launch_bounds__(64 * WGM * WGN, (buf_wgs_per_cu<BM, BN, WGM * WGN>())) void conv_buf_kernel(
+template <int BM, int BN, int WGM, int WGN, int OCC = 0>
+__global__ __launch_bounds__(64 * WGM * WGN, (buf_wgs_per_cu<BM, BN, WGM * WGN, OCC>())) void conv_buf_kernel(
     ConvParams p) {
   constexpr int NW = WGM * WGN, NT = 64 * NW;
   constexpr int BK = 64;
-  constexpr int NS = buf_slots<BM, BN, NW>();
+  constexpr int NS = buf_slots<BM, BN, NW, OCC>();
   constexpr int D = NS - 1;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int MI = WM / 16, NI = WN / 16;
@@ -71,7 +73,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (buf_wgs_per_cu<BM, BN, WGM * WGN>(
   constexpr int EPI_BYTES = BM * (BN + CPAD) * 4;
   constexpr int RING_BYTES = NS * STAGE_ELEMS * 2;
   constexpr int LDS_BYTES = EPI_BYTES > RING_BYTES ? EPI_BYTES : RING_BYTES;
-  static_assert(LDS_BYTES * buf_wgs_per_cu<BM, BN, NW>() <= 160 * 1024, "LDS budget");
+  static_assert(LDS_BYTES * buf_wgs_per_cu<BM, BN, NW, OCC>() <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
   bf16_t* ring = reinterpret_cast<bf16_t*>(smem);
 
@@ -325,7 +327,7 @@ extern "C" int aiko_conv_buf(const void* x, const void* w, const float* bias, co
                              void* y, int H, int W, int C, int Cc, int R, int S, int stride,
                              int pad, int Ho, int Wo, int M, int Cout, int K, int act, int ldy,
                              int ldr, int bm, int bn, const void* x2, int K1, int H2, int W2,
-                             int C2, int stride2, hipStream_t stream) {
+                             int C2, int stride2, int occ, hipStream_t stream) {
   using namespace aiko;
   if (Cc % 64 || R * S > 32 || (x2 && (K - K1) % 64)) return -1;
   ConvParams p;
@@ -340,7 +342,18 @@ extern "C" int aiko_conv_buf(const void* x, const void* w, const float* bias, co
   p.x2 = static_cast<const bf16_t*>(x2);
   p.K1 = x2 ? K1 : K; p.H2 = H2; p.W2 = W2; p.C2 = C2; p.stride2 = stride2;
   dim3 grid(((M + bm - 1) / bm) * ((Cout + bn - 1) / bn)), block(256);
-  if (bm == 128 && bn == 128) {
+  if (occ) {                               // variant 3: high occupancy, 2-slot rings
+    if (bm == 64 && bn == 64 && occ == 5)
+      conv_buf_kernel<64, 64, 2, 2, 5><<<grid, block, 0, stream>>>(p);
+    else if (bm == 64 && bn == 128 && occ == 3)
+      conv_buf_kernel<64, 128, 2, 2, 3><<<grid, block, 0, stream>>>(p);
+    else if (bm == 128 && bn == 64 && occ == 3)
+      conv_buf_kernel<128, 64, 2, 2, 3><<<grid, block, 0, stream>>>(p);
+    else if (bm == 64 && bn == 64 && occ == 4)
+      conv_buf_kernel<64, 64, 2, 2, 4><<<grid, block, 0, stream>>>(p);
+    else
+      return -1;
+  } else if (bm == 128 && bn == 128) {
     conv_buf_kernel<128, 128, 2, 2><<<grid, block, 0, stream>>>(p);
   } else if (bm == 128 && bn == 64) {
     conv_buf_kernel<128, 64, 2, 2><<<grid, block, 0, stream>>>(p);

@@ -23,6 +23,8 @@ LAYERS = {
     "b3.conv2": (128, 128, 3, 2, 56, False, 0),
     "b4.conv3": (128, 512, 1, 1, 28, True, 0),
     "b8.conv2": (256, 256, 3, 1, 14, False, 0),
+    "b8.conv3": (256, 1024, 1, 1, 14, True, 0),
+    "b14.conv3": (512, 2048, 1, 1, 7, True, 0),
     "b14.conv2": (512, 512, 3, 1, 7, False, 0),
     "b13.conv1": (1024, 512, 1, 1, 14, False, 0),
     "gemm4k": (4096, 4096, 1, 1, 16, False, 0),       # M = 256*16*16 = 65536: main-loop ceiling
@@ -64,6 +66,8 @@ def main():
         base = C.NARROW_TILES if cout <= 32 else C.TILES
         res[name] = {}
         cands = [tt + (0,) for tt in base] + ([tt + (1,) for tt in base] if cout > 32 else [])
+        if cout > 32 and C.buf_variant_ok(spec, x, x2):
+            cands += [tt + (2,) for tt in base + C.BUF_WIDE_TILES] + [tt + (3,) for tt in C.BUF_OCC_TILES]
         if a.tile:
             cands = [tuple(int(v) for v in a.tile.split(","))]
         for t in cands:
