@@ -229,6 +229,7 @@ def zero_page(device) -> torch.Tensor:
 
 BUF_WIDE_TILES = ((256, 128), (128, 256), (256, 64))   # 8-wave buffer-DMA kernels (one workgroup per CU)
 BUF_OCC_TILES = ((64, 64), (64, 128), (128, 64))       # variant 3: buffer-DMA at 5 / 3 / 3 workgroups per CU
+PERSIST_TILES = ((64, 128),)   # variant 4: persistent, one K-block ring across tiles (2 workgroups/CU)
 
 
 def buf_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = None) -> bool:
@@ -248,6 +249,7 @@ def _tune(key, M, cout, launch, buf_ok=False):
         cands = [t + (0,) for t in TILES] + [t + (1,) for t in TILES]
         if buf_ok:
             cands += [t + (2,) for t in TILES + BUF_WIDE_TILES] + [t + (3,) for t in BUF_OCC_TILES]
+            cands += [t + (4,) for t in PERSIST_TILES]
     best, best_t = None, None
     for t in cands:
         launch(t)  # warm

@@ -49,6 +49,17 @@ def _nhwc(x_nchw):
     (3, 14, 14, 256, 512, 1, 1, 0, None, False, (128, 256, 2)),
     (1, 9, 11, 128, 64, 3, 2, 1, "silu", False, (256, 128, 2)),
     (2, 30, 30, 64, 64, 3, 1, 1, "relu", True, (256, 64, 2)),
+    # high-occupancy buffer-DMA (variant 3)
+    (2, 28, 28, 128, 512, 1, 1, 0, "relu", True, (64, 128, 3)),
+    (1, 9, 11, 128, 64, 3, 1, 1, "silu", False, (64, 64, 3)),
+    # persistent: one K-block stream across each workgroup's tiles (variant 4); K = 64 / 128
+    # (1-2 blocks per tile, the ring spans several tiles), 3x3 taps, odd M tails
+    (2, 56, 56, 64, 256, 1, 1, 0, "relu", True, (64, 128, 4)),
+    (3, 14, 14, 256, 1024, 1, 1, 0, None, True, (64, 128, 4)),
+    (2, 28, 28, 128, 512, 1, 1, 0, "relu", True, (128, 128, 4)),
+    (1, 13, 9, 192, 72, 3, 2, 1, "gelu", True, (64, 64, 4)),
+    (2, 28, 28, 128, 128, 3, 1, 1, "relu", False, (64, 128, 4)),
+    (1, 7, 7, 512, 2048, 1, 1, 0, "relu", True, (128, 128, 4)),
 ])
 def test_conv_igemm_matches_torch(native, B, H, W, cin, cout, k, stride, pad, act, res, tile):
     from aiko_services_amd.ops import conv as C
@@ -168,7 +179,7 @@ def test_resnet50_matches_fp32_reference(native):
     assert (i[:, 0].long() == lg.argmax(1)).all()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("B,H,cin_main,cin_sc,cout,stride", [(2, 28, 64, 64, 256, 1), (2, 28, 128, 256, 512, 2),
                                                               (1, 14, 512, 1024, 2048, 2)])
 def test_fused_projection_shortcut(native, B, H, cin_main, cin_sc, cout, stride, variant):
