@@ -9,6 +9,7 @@ disabled; BASELINE's north star names ``aiko pipeline create``).
     aiko storage start|test_command|test_request
     aiko lifecycle manager N | client ID TOPIC
     aiko ec-test sc_test | ec_test [PID [SID [FILTER]]]   EC share / ServicesCache self tests
+                                       (also: aiko share ..., the reference's command name)
     aiko echo-bench                    BASELINE config 1 (two-process echo pipeline)
     aiko bench ...                     bench.py (ResNet-50 pipeline on MI355X)
     aiko build                         compile the HIP/C++ library for gfx950
@@ -39,7 +40,7 @@ def main(argv=None):
         from .storage import main as m
     elif cmd == "lifecycle":
         from ..control.lifecycle import main as m
-    elif cmd == "ec-test":
+    elif cmd in ("ec-test", "share"):
         from .ec_test import main as m
     elif cmd == "echo-bench":
         from .echo_bench import main as m

@@ -293,10 +293,15 @@ class Dashboard:
 def main(argv=None):
     ap = argparse.ArgumentParser(description="aiko dashboard")
     ap.add_argument("--history_limit", "-hl", type=int, default=HISTORY_LIMIT)
+    ap.add_argument("--plugin", "-p", action="append", default=[],
+                    help="module (or path/file.py) whose PLUGINS dict adds plugin pages (repeatable)")
     ap.add_argument("--snapshot", action="store_true", help="print services once and exit")
     ap.add_argument("--service", default=None, help="(snapshot) also print this service's variables")
     ap.add_argument("--timeout", type=float, default=5.0)
     a = ap.parse_args(argv)
+    for module in a.plugin:
+        from ..utils.misc import load_module
+        PLUGINS.update(getattr(load_module(module), "PLUGINS", {}))
     dash = Dashboard(a.history_limit)
     if not a.snapshot:
         dash.run_curses()

@@ -336,3 +336,40 @@ def test_ec_test_services(aiko_process):
     assert ("update", "log_level", "DEBUG") in producer.changes
     event.call_on_loop(consumer.ec_consumer.terminate)
     event.call_on_loop(lambda: aiko.aiko.connection.update_state(ConnectionState.TRANSPORT))
+
+
+def test_mailbox_stress_many_producers():
+    """mailboxes and the queue under concurrent producers — every item delivered
+    exactly once, per-producer FIFO order kept, priority mailbox never starved."""
+    eng = EventEngine()
+    producers, per = 8, 3000
+    got_in, got_ctl, got_q = [], [], []
+    eng.add_mailbox_handler(lambda n, item, t: got_ctl.append(item), "s/1/control")
+    eng.add_mailbox_handler(lambda n, item, t: got_in.append(item), "s/1/in")
+    eng.add_queue_handler(lambda item, typ: got_q.append(item), ["message"])
+    t = threading.Thread(target=eng.loop, kwargs={"loop_when_no_handlers": True}, daemon=True)
+    t.start()
+
+    def produce(p):
+        for i in range(per):
+            eng.mailbox_put("s/1/in", (p, i))
+            if i % 10 == 0:
+                eng.mailbox_put("s/1/control", (p, i))
+            if i % 7 == 0:
+                eng.queue_put((p, i), "message")
+    ths = [threading.Thread(target=produce, args=(p,)) for p in range(producers)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    deadline = time.time() + 20
+    while (len(got_in) < producers * per or len(got_ctl) < producers * per // 10) and time.time() < deadline:
+        time.sleep(0.01)
+    eng.terminate()
+    t.join(5)
+    assert len(got_in) == producers * per and len(set(got_in)) == producers * per
+    assert len(got_ctl) == producers * (per // 10)
+    assert len(got_q) == producers * len(range(0, per, 7))
+    for p in range(producers):
+        seq = [i for (q, i) in got_in if q == p]
+        assert seq == sorted(seq)                 # per-producer FIFO
