@@ -94,7 +94,9 @@ __global__ __launch_bounds__(64 * WGM * WGN, (buf_wgs_per_cu<BM, BN, WGM * WGN, 
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w);
   const __amdgpu_buffer_rsrc_t rx2 = make_rsrc(p.x2 ? p.x2 : p.x);
 
-  // per-piece geometry: byte offset of the tap-(0,0) pixel and a validity bit per tap
+  // per-piece geometry: byte offset of the tap-(0,0) pixel and the valid filter rows / columns
+  // (bit r of the low half, bit s of the high half: tap (r, s) reads inside the image iff both
+  // bits are set — two clamps per piece instead of a test per tap)
   int a_base[APT];
   uint32_t a_mask[APT], a2_off[APT];
 #pragma unroll
@@ -104,16 +106,17 @@ __global__ __launch_bounds__(64 * WGM * WGN, (buf_wgs_per_cu<BM, BN, WGM * WGN, 
     a_base[i] = 0;
     a2_off[i] = kBufOOB;
     if (m < p.M) {
-      const int img = m / HoWo;
+      const int img = fdiv(m, p.mHoWo, p.lHoWo);
       const int rem = m - img * HoWo;
-      const int oh = rem / p.Wo;
+      const int oh = fdiv(rem, p.mWo, p.lWo);
       const int ow = rem - oh * p.Wo;
       const int ih0 = oh * p.stride - p.pad, iw0 = ow * p.stride - p.pad;
       a_base[i] = (((img * p.H + ih0) * p.W + iw0) * p.C + lp * 8) * 2;
-      for (int t = 0; t < RS; ++t) {
-        const int r = t / p.S, s = t - r * p.S;
-        if ((unsigned)(ih0 + r) < (unsigned)p.H && (unsigned)(iw0 + s) < (unsigned)p.W) a_mask[i] |= 1u << t;
-      }
+      const int r_lo = max(0, -ih0), r_hi = min(p.R, p.H - ih0);
+      const int s_lo = max(0, -iw0), s_hi = min(p.S, p.W - iw0);
+      const uint32_t mr = r_hi > r_lo ? ((1u << r_hi) - 1u) & ~((1u << r_lo) - 1u) : 0u;
+      const uint32_t ms = s_hi > s_lo ? ((1u << s_hi) - 1u) & ~((1u << s_lo) - 1u) : 0u;
+      a_mask[i] = mr | (ms << 16);
       a2_off[i] = (uint32_t)((((img * p.H2 + oh * p.stride2) * p.W2 + ow * p.stride2) * p.C2 + lp * 8) * 2);
     }
   }
@@ -160,6 +163,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (buf_wgs_per_cu<BM, BN, WGM * WGN, 
 #pragma unroll
   for (int i = 0; i < APT; ++i) a_off[i] = kBufOOB;
   int iss_tap = 0, iss_c = 0;             // position of the next K block to issue
+  int iss_r = 0, iss_s = 0;               // its filter row / column
 
   auto issue = [&](int kb, auto slot_tag) {
     constexpr int SLOT = decltype(slot_tag)::value;
@@ -173,11 +177,12 @@ __global__ __launch_bounds__(64 * WGM * WGN, (buf_wgs_per_cu<BM, BN, WGM * WGN, 
     } else {
       if (iss_tap != cur_tap) {           // wave-uniform: new tap -> new per-lane offsets
         cur_tap = iss_tap;
-        const int r = iss_tap / p.S, s = iss_tap - r * p.S;
+        const int r = iss_r, s = iss_s;
         const int tap_off = ((r * p.W + s) * p.C) * 2;
+        const uint32_t bit = (1u << r) | (1u << (s + 16));
 #pragma unroll
         for (int i = 0; i < APT; ++i)
-          a_off[i] = (a_mask[i] >> iss_tap) & 1u ? (uint32_t)(a_base[i] + tap_off) : kBufOOB;
+          a_off[i] = (a_mask[i] & bit) == bit ? (uint32_t)(a_base[i] + tap_off) : kBufOOB;
       }
       const uint32_t soff = (uint32_t)(iss_c * 2);
 #pragma unroll
@@ -186,6 +191,10 @@ __global__ __launch_bounds__(64 * WGM * WGN, (buf_wgs_per_cu<BM, BN, WGM * WGN, 
       if (iss_c >= p.Cc) {
         iss_c = 0;
         ++iss_tap;
+        if (++iss_s == p.S) {
+          iss_s = 0;
+          ++iss_r;
+        }
       }
     }
     const uint32_t sb = (uint32_t)(k0 * 2);
@@ -285,16 +294,17 @@ __global__ __launch_bounds__(64 * WGM * WGN, (buf_wgs_per_cu<BM, BN, WGM * WGN, 
     if (m >= p.M || e_n >= p.Cout) continue;
     const f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + e_cc * 8);
     const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + e_cc * 8 + 4);
-    float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] += e_bias[e];
+    // packed fp32 pairs (v_pk_add_f32) for the bias and residual adds
+    f32x2 v2[4] = {f32x2{v0[0], v0[1]} + f32x2{e_bias[0], e_bias[1]},
+                   f32x2{v0[2], v0[3]} + f32x2{e_bias[2], e_bias[3]},
+                   f32x2{v1[0], v1[1]} + f32x2{e_bias[4], e_bias[5]},
+                   f32x2{v1[2], v1[3]} + f32x2{e_bias[6], e_bias[7]}};
     if (p.res && !post) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[2 * e] += __uint_as_float(e_res[i][e] << 16);
-        v[2 * e + 1] += __uint_as_float(e_res[i][e] & 0xffff0000u);
-      }
+      for (int e = 0; e < 4; ++e)
+        v2[e] += f32x2{__uint_as_float(e_res[i][e] << 16), __uint_as_float(e_res[i][e] & 0xffff0000u)};
     }
+    float v[8] = {v2[0][0], v2[0][1], v2[1][0], v2[1][1], v2[2][0], v2[2][1], v2[3][0], v2[3][1]};
     if (act == 1) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
@@ -329,7 +339,7 @@ extern "C" int aiko_conv_buf(const void* x, const void* w, const float* bias, co
                              int ldr, int bm, int bn, const void* x2, int K1, int H2, int W2,
                              int C2, int stride2, int occ, hipStream_t stream) {
   using namespace aiko;
-  if (Cc % 64 || R * S > 32 || (x2 && (K - K1) % 64)) return -1;
+  if (Cc % 64 || R * S > 32 || R > 16 || S > 16 || (x2 && (K - K1) % 64)) return -1;
   ConvParams p;
   p.x = static_cast<const bf16_t*>(x);
   p.w = static_cast<const bf16_t*>(w);
@@ -341,6 +351,7 @@ extern "C" int aiko_conv_buf(const void* x, const void* w, const float* bias, co
   p.act = act; p.ldy = ldy; p.ldr = ldr;
   p.x2 = static_cast<const bf16_t*>(x2);
   p.K1 = x2 ? K1 : K; p.H2 = H2; p.W2 = W2; p.C2 = C2; p.stride2 = stride2;
+  conv_params_finalize(p);
   dim3 grid(((M + bm - 1) / bm) * ((Cout + bn - 1) / bn)), block(256);
   if (occ) {                               // variant 3: high occupancy, 2-slot rings
     if (bm == 64 && bn == 64 && occ == 5)

@@ -22,6 +22,27 @@ struct ConvParams {
   // fuse a ResNet projection shortcut into the block's last conv (K-concatenation)
   const bf16_t* x2;
   int K1, H2, W2, C2, stride2;
+  // magic numbers for n / (Ho*Wo) and n / Wo without a VALU division loop (fdiv below)
+  uint32_t mHoWo, mWo;
+  int lHoWo, lWo;
 };
+
+// n / d for 0 <= n < 2^31 as (umulhi(n, m) + n) >> l with l = ceil(log2 d),
+// m = floor(2^32 (2^l - d) / d) + 1 (Hacker's Delight 10-9): 3 VALU instead of ~30.
+__host__ inline void fastdiv_init(int d, uint32_t* m, int* l) {
+  int k = 0;
+  while ((1LL << k) < d) ++k;
+  *l = k;
+  *m = (uint32_t)(((1ULL << 32) * ((1ULL << k) - (unsigned long long)d)) / (unsigned long long)d + 1ULL);
+}
+
+__device__ __forceinline__ int fdiv(int n, uint32_t m, int l) {
+  return (int)((__umulhi((uint32_t)n, m) + (uint32_t)n) >> l);
+}
+
+__host__ inline void conv_params_finalize(ConvParams& p) {
+  fastdiv_init(p.Ho * p.Wo, &p.mHoWo, &p.lHoWo);
+  fastdiv_init(p.Wo, &p.mWo, &p.lWo);
+}
 
 }  // namespace aiko

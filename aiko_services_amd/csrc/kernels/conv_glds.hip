@@ -278,6 +278,7 @@ extern "C" int aiko_conv_glds(const void* x, const void* w, const float* bias, c
   p.act = act; p.ldy = ldy; p.ldr = ldr;
   p.x2 = static_cast<const bf16_t*>(x2);
   p.K1 = x2 ? K1 : K; p.H2 = H2; p.W2 = W2; p.C2 = C2; p.stride2 = stride2;
+  conv_params_finalize(p);
   const bf16_t* z = static_cast<const bf16_t*>(zero);
   dim3 grid(((M + bm - 1) / bm) * ((Cout + bn - 1) / bn)), block(256);
   if (bm == 128 && bn == 128) {

@@ -318,6 +318,7 @@ extern "C" int aiko_conv_igemm(const void* x, const void* w, const float* bias, 
   p.act = act; p.ldy = ldy; p.ldr = ldr;
   p.x2 = static_cast<const bf16_t*>(x2);
   p.K1 = x2 ? K1 : K; p.H2 = H2; p.W2 = W2; p.C2 = C2; p.stride2 = stride2;
+  conv_params_finalize(p);
   const int ntm = (M + bm - 1) / bm;
   const int ntn = (Cout + bn - 1) / bn;
   dim3 grid(ntm * ntn), block(256);
