@@ -22,9 +22,9 @@ struct ConvParams {
   // fuse a ResNet projection shortcut into the block's last conv (K-concatenation)
   const bf16_t* x2;
   int K1, H2, W2, C2, stride2;
-  // magic numbers for n / (Ho*Wo) and n / Wo without a VALU division loop (fdiv below)
-  uint32_t mHoWo, mWo;
-  int lHoWo, lWo;
+  // magic numbers for n / (Ho*Wo), n / Wo, n / Cc, n / S without a VALU division loop (fdiv)
+  uint32_t mHoWo, mWo, mCc, mS;
+  int lHoWo, lWo, lCc, lS;
 };
 
 // n / d for 0 <= n < 2^31 as (umulhi(n, m) + n) >> l with l = ceil(log2 d),
@@ -43,6 +43,8 @@ __device__ __forceinline__ int fdiv(int n, uint32_t m, int l) {
 __host__ inline void conv_params_finalize(ConvParams& p) {
   fastdiv_init(p.Ho * p.Wo, &p.mHoWo, &p.lHoWo);
   fastdiv_init(p.Wo, &p.mWo, &p.lWo);
+  fastdiv_init(p.Cc, &p.mCc, &p.lCc);
+  fastdiv_init(p.S, &p.mS, &p.lS);
 }
 
 }  // namespace aiko

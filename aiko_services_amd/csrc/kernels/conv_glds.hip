@@ -77,9 +77,9 @@ __global__ __launch_bounds__(256, (glds_occupancy<BM, BN>())) void conv_glds_ker
   for (int i = 0; i < APT; ++i) {
     const int m = m0 + lrow + 32 * i;
     if (m < p.M) {
-      const int img = m / HoWo;
+      const int img = fdiv(m, p.mHoWo, p.lHoWo);
       const int rem = m - img * HoWo;
-      const int oh = rem / p.Wo;
+      const int oh = fdiv(rem, p.mWo, p.lWo);
       const int ow = rem - oh * p.Wo;
       a_ih[i] = oh * p.stride - p.pad;
       a_iw[i] = ow * p.stride - p.pad;
@@ -136,9 +136,9 @@ __global__ __launch_bounds__(256, (glds_occupancy<BM, BN>())) void conv_glds_ker
       }
     } else {
       const int koff = kb * BK + lp * 8;
-      const int tap = koff / p.Cc;
+      const int tap = fdiv(koff, p.mCc, p.lCc);
       const int c = koff - tap * p.Cc;
-      const int r = tap / p.S;
+      const int r = fdiv(tap, p.mS, p.lS);
       const int s = tap - r * p.S;
       const int tap_off = (r * p.W + s) * p.C + c;
 #pragma unroll

@@ -68,9 +68,9 @@ __global__ __launch_bounds__(256, (conv_occupancy<BM, BN>())) void conv_igemm_ke
   for (int i = 0; i < APT; ++i) {
     const int m = m0 + prow + 32 * i;
     if (m < p.M) {
-      const int img = m / HoWo;
+      const int img = fdiv(m, p.mHoWo, p.lHoWo);
       const int rem = m - img * HoWo;
-      const int oh = rem / p.Wo;
+      const int oh = fdiv(rem, p.mWo, p.lWo);
       const int ow = rem - oh * p.Wo;
       a_ih[i] = oh * p.stride - p.pad;
       a_iw[i] = ow * p.stride - p.pad;
@@ -87,9 +87,9 @@ __global__ __launch_bounds__(256, (conv_occupancy<BM, BN>())) void conv_igemm_ke
     for (int i = 0; i < APT; ++i) {
       const int m = m0 + prow + 32 * i;
       if (m < p.M) {
-        const int img = m / HoWo;
+        const int img = fdiv(m, p.mHoWo, p.lHoWo);
         const int rem = m - img * HoWo;
-        const int oh = rem / p.Wo;
+        const int oh = fdiv(rem, p.mWo, p.lWo);
         const int ow = rem - oh * p.Wo;
         a2_base[i] = ((img * p.H2 + oh * p.stride2) * p.W2 + ow * p.stride2) * p.C2;
       } else {
@@ -157,9 +157,9 @@ __global__ __launch_bounds__(256, (conv_occupancy<BM, BN>())) void conv_igemm_ke
       return;
     }
     const int koff = kb * BK + piece * 8;
-    const int tap = koff / p.Cc;  // K may be zero-padded past R*S*Cc: taps >= R*S meet zero weights
+    const int tap = fdiv(koff, p.mCc, p.lCc);  // K may be zero-padded past R*S*Cc: taps >= R*S meet zero weights
     const int c = koff - tap * p.Cc;
-    const int r = tap / p.S;
+    const int r = fdiv(tap, p.mS, p.lS);
     const int s = tap - r * p.S;
     const int tap_off = (r * p.W + s) * p.C + c;
 #pragma unroll

@@ -118,9 +118,9 @@ __global__ __launch_bounds__(256, OCC) void conv_persist_kernel(ConvParams p, in
       a2_off[i] = kPOOB;
       a_off[i] = kPOOB;
       if (m < p.M) {
-        const int img = m / HoWo;
+        const int img = fdiv(m, p.mHoWo, p.lHoWo);
         const int rem = m - img * HoWo;
-        const int oh = rem / p.Wo;
+        const int oh = fdiv(rem, p.mWo, p.lWo);
         const int ow = rem - oh * p.Wo;
         const int ih0 = oh * p.stride - p.pad, iw0 = ow * p.stride - p.pad;
         a_base[i] = (((img * p.H + ih0) * p.W + iw0) * p.C + lp * 8) * 2;
