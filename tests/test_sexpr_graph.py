@@ -114,3 +114,24 @@ def test_dashboard_plugin_pages():
     D.register_plugin("yolo", D.gpu_page)
     assert D.find_plugin(gpu) is D.gpu_page
     del D.PLUGINS["yolo"]
+
+
+def test_gstreamer_launch_descriptions_and_gating():
+    """elements/gstreamer: reference launch strings; without the Gst typelib the readers and
+    writers raise GStreamerError (no silent fallback)."""
+    import pytest
+    from aiko_services_amd.elements import gstreamer as G
+    assert G.file_reader_launch("a.mp4").startswith("filesrc location=a.mp4 ! qtdemux ! avdec_h264")
+    assert "appsink name=sink" in G.camera_reader_launch("/dev/video0")
+    assert "udpsink host=h port=5000" in G.stream_writer_launch("h", 5000)
+    assert "rtmpsink" in G.stream_writer_launch("h", 5000, "rtmp://x/y")
+    assert "framerate=25/1" in G.file_writer_launch("o_%02d.mp4", 640, 480, 25)
+    assert "rtph264depay" in G.stream_reader_launch("0.0.0.0", 6000)
+    try:
+        G.gst_initialise()
+        available = True
+    except G.GStreamerError:
+        available = False
+    if not available:
+        with pytest.raises(G.GStreamerError):
+            G.VideoFileReader("missing.mp4")
