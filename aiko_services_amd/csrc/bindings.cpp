@@ -63,6 +63,15 @@ int aiko_stem_pool(const void* x, const void* w, const float* bias, void* y, int
                    int Ho, int Wo, int Hm, int Wm, int ldy, int variant, hipStream_t stream);
 int aiko_softmax_topk(const void* logits, float* prob, int* index, int B, int N, int k,
                       hipStream_t stream);
+int aiko_embed_tokens(const int* ids, const int* pos, const void* tok, const void* pemb, void* x, int B,
+                      int d, int ldx, int vocab, int n_pos, hipStream_t stream);
+int aiko_attn_decode(const void* q, int ldq, void* k, void* v, int ldk, int ldv, int S, const int* pos,
+                     int T, const void* knew, const void* vnew, int ldnew, void* o, int ldo, int B,
+                     int H, float scale, float* work, long work_elems, hipStream_t stream);
+long aiko_attn_decode_work(int B, int H, int maxlen);
+int aiko_argmax_step(const void* logits, int ld, int V, int B, int* ids, int* pos, int* out_tokens,
+                     int max_len, const int* forced, int n_forced, int eot, int* done, unsigned* counter,
+                     hipStream_t stream);
 }
 
 namespace {
@@ -593,6 +602,106 @@ void logmel_out(const at::Tensor& audio, const at::Tensor& mel, int64_t n_fft, i
                "logmel");
 }
 
+// ---- decoder step ops (decode_ops.hip) ----------------------------------------------------------
+
+void check_i32(const at::Tensor& t, int64_t n, const char* what) {
+  check_cuda(t, what);
+  TORCH_CHECK(t.scalar_type() == at::kInt && t.is_contiguous() && t.numel() >= n, "aiko: ", what,
+              " must be contiguous int32 with >= ", n, " elements");
+}
+
+// x[b] = tok[ids[b]] + pemb[pos[0]]; tok bf16 [V, d], pemb bf16 [P, d], x bf16 [B, d]
+void embed_tokens_out(const at::Tensor& ids, const at::Tensor& pos, const at::Tensor& tok, const at::Tensor& pemb,
+                      at::Tensor& x) {
+  const int64_t B = x.size(0), d = x.size(1);
+  check_i32(ids, B, "ids");
+  check_i32(pos, 1, "pos");
+  for (const at::Tensor* t : {&tok, &pemb, (const at::Tensor*)&x}) {
+    check_cuda(*t, "embedding operand");
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->dim() == 2 && t->size(1) == d,
+                "aiko.embed_tokens_out: bf16 [*, d] tensors required");
+  }
+  TORCH_CHECK(tok.is_contiguous() && pemb.is_contiguous() && d % 8 == 0, "aiko.embed_tokens_out: contiguous tables, d % 8 == 0");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "aiko.embed_tokens_out: x alignment");
+  const int64_t ldx = row_pitch(x, d, "embed_tokens_out", "x");
+  check_launch(aiko_embed_tokens(ids.data_ptr<int>(), pos.data_ptr<int>(), tok.data_ptr(), pemb.data_ptr(), x.data_ptr(),
+                                 B, d, ldx, tok.size(0), pemb.size(0), cur_stream()),
+               "embed_tokens");
+}
+
+// One query row per sequence against K/V rows [B*S, >= H*64] (sequence b's key j at row b*S+j).
+// With ``pos`` (device int32 [1]) the step appends ``knew``/``vnew`` [B, >= H*64] at row pos of
+// every sequence and attends keys 0..pos; otherwise it attends keys 0..T-1.
+void attn_decode_out(const at::Tensor& q, at::Tensor& k, at::Tensor& v, at::Tensor& o, int64_t B, int64_t H,
+                     int64_t S, int64_t T, const c10::optional<at::Tensor>& pos,
+                     const c10::optional<at::Tensor>& knew, const c10::optional<at::Tensor>& vnew, double scale,
+                     at::Tensor& work) {
+  const bool app = pos.has_value() && pos->defined();
+  for (const at::Tensor* t : {&q, (const at::Tensor*)&k, (const at::Tensor*)&v, (const at::Tensor*)&o}) {
+    check_cuda(*t, "q/k/v/o");
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->dim() == 2, "aiko.attn_decode_out: bf16 2-D tensors required");
+    row_pitch(*t, H * 64, "attn_decode_out", "q/k/v/o");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "aiko.attn_decode_out: 16-byte alignment");
+  }
+  TORCH_CHECK(q.size(0) == B && o.size(0) == B, "aiko.attn_decode_out: q/o need B rows");
+  TORCH_CHECK(k.size(0) == B * S && v.size(0) == B * S, "aiko.attn_decode_out: k/v need B*S rows");
+  const void *kn = nullptr, *vn = nullptr;
+  int64_t ldnew = 0;
+  const int* pp = nullptr;
+  if (app) {
+    check_i32(*pos, 1, "pos");
+    pp = pos->data_ptr<int>();
+    TORCH_CHECK(knew.has_value() && knew->defined() && vnew.has_value() && vnew->defined(),
+                "aiko.attn_decode_out: append mode needs knew and vnew");
+    for (const at::Tensor* t : {&*knew, &*vnew}) {
+      check_cuda(*t, "knew/vnew");
+      TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->size(0) == B &&
+                      reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
+                  "aiko.attn_decode_out: knew/vnew bf16 [B, >= H*64], 16-byte aligned");
+      row_pitch(*t, H * 64, "attn_decode_out", "knew/vnew");
+    }
+    TORCH_CHECK(knew->stride(0) == vnew->stride(0), "aiko.attn_decode_out: knew/vnew must share a row pitch");
+    kn = knew->data_ptr();
+    vn = vnew->data_ptr();
+    ldnew = knew->stride(0);
+  } else {
+    TORCH_CHECK(T >= 1 && T <= S, "aiko.attn_decode_out: 1 <= T <= S");
+  }
+  check_cuda(work, "work");
+  TORCH_CHECK(work.scalar_type() == at::kFloat && work.is_contiguous(), "aiko.attn_decode_out: work fp32");
+  TORCH_CHECK(work.numel() >= aiko_attn_decode_work(B, H, app ? S : T), "aiko.attn_decode_out: work too small");
+  check_launch(aiko_attn_decode(q.data_ptr(), q.stride(0), k.data_ptr(), v.data_ptr(), k.stride(0), v.stride(0), S, pp,
+                                T, kn, vn, ldnew, o.data_ptr(), o.stride(0), B, H, (float)scale,
+                                work.data_ptr<float>(), work.numel(), cur_stream()),
+               "attn_decode");
+}
+
+int64_t attn_decode_work(int64_t B, int64_t H, int64_t maxlen) { return aiko_attn_decode_work(B, H, maxlen); }
+
+// greedy next token per sequence; advances pos[0] on the device (see decode_ops.hip)
+void argmax_step_out(const at::Tensor& logits, int64_t V, at::Tensor& ids, at::Tensor& pos, at::Tensor& out_tokens,
+                     const at::Tensor& forced, int64_t eot, at::Tensor& done, at::Tensor& counter) {
+  check_cuda(logits, "logits");
+  TORCH_CHECK(logits.scalar_type() == at::kBFloat16 && logits.dim() == 2 && logits.stride(1) == 1 &&
+                  reinterpret_cast<uintptr_t>(logits.data_ptr()) % 16 == 0,
+              "aiko.argmax_step_out: logits bf16 [B, >= V], 16-byte aligned rows");
+  const int64_t B = logits.size(0);
+  check_i32(ids, B, "ids");
+  check_i32(pos, 1, "pos");
+  check_i32(done, B, "done");
+  check_i32(counter, 1, "counter");
+  check_cuda(out_tokens, "out_tokens");
+  TORCH_CHECK(out_tokens.scalar_type() == at::kInt && out_tokens.dim() == 2 && out_tokens.size(0) == B &&
+                  out_tokens.is_contiguous(),
+              "aiko.argmax_step_out: out_tokens int32 [B, max_len]");
+  check_i32(forced, 1, "forced");
+  check_launch(aiko_argmax_step(logits.data_ptr(), logits.stride(0), V, B, ids.data_ptr<int>(), pos.data_ptr<int>(),
+                                out_tokens.data_ptr<int>(), out_tokens.size(1), forced.data_ptr<int>(), forced.numel(),
+                                eot, done.data_ptr<int>(), reinterpret_cast<unsigned*>(counter.data_ptr<int>()),
+                                cur_stream()),
+               "argmax_step");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(aiko, m) {
@@ -611,6 +720,9 @@ TORCH_LIBRARY(aiko, m) {
   m.def("attn_fwd_out(Tensor q, Tensor k, Tensor v, Tensor(a!) o, int B, int H, int T, int Tpad, float scale) -> ()");
   m.def("logmel_out(Tensor audio, Tensor mel, int n_fft, int hop, int F, Tensor(a!) work, Tensor(b!) gmax, Tensor(c!) dst, int rows, int pad) -> ()");
   m.def("softmax_topk_out(Tensor logits, Tensor(a!) prob, Tensor(b!) index, int k) -> ()");
+  m.def("embed_tokens_out(Tensor ids, Tensor pos, Tensor tok, Tensor pemb, Tensor(a!) x) -> ()");
+  m.def("attn_decode_out(Tensor q, Tensor(a!) k, Tensor(b!) v, Tensor(c!) o, int B, int H, int S, int T, Tensor? pos, Tensor? knew, Tensor? vnew, float scale, Tensor(d!) work) -> ()");
+  m.def("argmax_step_out(Tensor logits, int V, Tensor(a!) ids, Tensor(b!) pos, Tensor(c!) out_tokens, Tensor forced, int eot, Tensor(d!) done, Tensor(e!) counter) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
@@ -629,4 +741,7 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("rownorm_quant_out", &rownorm_quant_out);
   m.impl("attn_fwd_out", &attn_fwd_out);
   m.impl("logmel_out", &logmel_out);
+  m.impl("embed_tokens_out", &embed_tokens_out);
+  m.impl("attn_decode_out", &attn_decode_out);
+  m.impl("argmax_step_out", &argmax_step_out);
 }
