@@ -69,6 +69,9 @@ int aiko_attn_decode(const void* q, int ldq, void* k, void* v, int ldk, int ldv,
                      int T, const void* knew, const void* vnew, int ldnew, void* o, int ldo, int B,
                      int H, float scale, float* work, long work_elems, hipStream_t stream);
 long aiko_attn_decode_work(int B, int H, int maxlen);
+int aiko_dec_linear(const void* x, int ldx, const float* gamma, const float* beta, float eps, const void* w,
+                    const float* sw, const float* bias, const void* res, int ldr, void* y, int ldy, int M, int N,
+                    int K, int act, hipStream_t stream);
 int aiko_argmax_step(const void* logits, int ld, int V, int B, int* ids, int* pos, int* out_tokens,
                      int max_len, const int* forced, int n_forced, int eot, int* done, unsigned* counter,
                      hipStream_t stream);
@@ -676,7 +679,51 @@ void attn_decode_out(const at::Tensor& q, at::Tensor& k, at::Tensor& v, at::Tens
                "attn_decode");
 }
 
-int64_t attn_decode_work(int64_t B, int64_t H, int64_t maxlen) { return aiko_attn_decode_work(B, H, maxlen); }
+
+// y = act(LN?(x) quantised per row to e4m3 @ W^T * scales + bias) (+ res): the decoder's fused
+// skinny-M linear (x bf16 [M, K], K % 128 == 0, K <= 3072; W e4m3 [N, K])
+void dec_linear_out(const at::Tensor& x, const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta,
+                    double eps, const at::Tensor& w, const at::Tensor& sw, const c10::optional<at::Tensor>& bias,
+                    const c10::optional<at::Tensor>& res, at::Tensor& y, int64_t act) {
+  for (const at::Tensor* t : {&x, &w, &sw, (const at::Tensor*)&y}) check_cuda(*t, "dec_linear operand");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16, "aiko.dec_linear_out: bf16 x / y");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.element_size() == 1 && w.dim() == 2 && w.size(1) == K && w.is_contiguous(),
+              "aiko.dec_linear_out: w e4m3 [N, K] contiguous with K == x width");
+  TORCH_CHECK(K % 128 == 0 && K <= 3072, "aiko.dec_linear_out: K % 128 == 0 and K <= 3072");
+  TORCH_CHECK(sw.scalar_type() == at::kFloat && sw.numel() == N && sw.is_contiguous(), "aiko.dec_linear_out: sw fp32 [N]");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
+              "aiko.dec_linear_out: x / w 16-byte alignment");
+  const int64_t ldx = row_pitch(x, K, "dec_linear_out", "x");
+  TORCH_CHECK(y.size(0) == M, "aiko.dec_linear_out: y [M, N]");
+  const int64_t ldy = row_pitch(y, N, "dec_linear_out", "y");
+  const float *g = nullptr, *be = nullptr, *bp = nullptr;
+  if (gamma.has_value() && gamma->defined()) {
+    TORCH_CHECK(beta.has_value() && beta->defined(), "aiko.dec_linear_out: gamma needs beta");
+    for (const at::Tensor* t : {&*gamma, &*beta}) {
+      check_cuda(*t, "gamma/beta");
+      TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() == K && t->is_contiguous(), "aiko.dec_linear_out: gamma/beta fp32 [K]");
+    }
+    g = gamma->data_ptr<float>();
+    be = beta->data_ptr<float>();
+  }
+  if (bias.has_value() && bias->defined()) {
+    check_cuda(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == N && bias->is_contiguous(), "aiko.dec_linear_out: bias fp32 [N]");
+    bp = bias->data_ptr<float>();
+  }
+  const void* rp = nullptr;
+  int64_t ldr = 0;
+  if (res.has_value() && res->defined()) {
+    check_cuda(*res, "residual");
+    TORCH_CHECK(res->scalar_type() == at::kBFloat16 && res->size(0) == M, "aiko.dec_linear_out: residual bf16 [M, N]");
+    ldr = row_pitch(*res, N, "dec_linear_out", "residual");
+    rp = res->data_ptr();
+  }
+  check_launch(aiko_dec_linear(x.data_ptr(), ldx, g, be, (float)eps, w.data_ptr(), sw.data_ptr<float>(), bp, rp, ldr,
+                               y.data_ptr(), ldy, M, N, K, act, cur_stream()),
+               "dec_linear");
+}
 
 // greedy next token per sequence; advances pos[0] on the device (see decode_ops.hip)
 void argmax_step_out(const at::Tensor& logits, int64_t V, at::Tensor& ids, at::Tensor& pos, at::Tensor& out_tokens,
@@ -722,6 +769,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("softmax_topk_out(Tensor logits, Tensor(a!) prob, Tensor(b!) index, int k) -> ()");
   m.def("embed_tokens_out(Tensor ids, Tensor pos, Tensor tok, Tensor pemb, Tensor(a!) x) -> ()");
   m.def("attn_decode_out(Tensor q, Tensor(a!) k, Tensor(b!) v, Tensor(c!) o, int B, int H, int S, int T, Tensor? pos, Tensor? knew, Tensor? vnew, float scale, Tensor(d!) work) -> ()");
+  m.def("dec_linear_out(Tensor x, Tensor? gamma, Tensor? beta, float eps, Tensor w, Tensor sw, Tensor? bias, Tensor? res, Tensor(a!) y, int act) -> ()");
   m.def("argmax_step_out(Tensor logits, int V, Tensor(a!) ids, Tensor(b!) pos, Tensor(c!) out_tokens, Tensor forced, int eot, Tensor(d!) done, Tensor(e!) counter) -> ()");
 }
 
@@ -744,4 +792,5 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("embed_tokens_out", &embed_tokens_out);
   m.impl("attn_decode_out", &attn_decode_out);
   m.impl("argmax_step_out", &argmax_step_out);
+  m.impl("dec_linear_out", &dec_linear_out);
 }

@@ -11,8 +11,11 @@
   60-83``, as one device ring per stream: shift + append, no host copies);
 * ``WhisperEncoder`` — log-mel + Whisper encoder (fp8 linear layers) over the windows,
   optional hipGraph capture; emits encoder features [B, T, d] on the device;
-* ``FeatureSink``   — mean-pooled features to pinned host memory as a DeviceResult (a
-  stand-in consumer; decoding is not part of the encoder config).
+* ``FeatureSink``   — mean-pooled features to pinned host memory as a DeviceResult (the
+  encoder-only BASELINE config's consumer);
+* ``WhisperTranscribe`` — greedy text decoding of the features (``models/whisper_decoder.py``),
+  ``{"tokens", "text"}`` like the reference's ``PE_WhisperX`` output;
+* ``SpeechToText``  — ``PE_WhisperX`` in one element: audio -> encoder -> decoder -> text.
 """
 from __future__ import annotations
 
@@ -24,7 +27,7 @@ import torch
 from ...gpu.element import DeviceResult, GpuPipelineElement
 from ...pipeline.stream import StreamEvent
 
-__all__ = ["AudioChunks", "AudioWindow", "WhisperEncoder", "FeatureSink"]
+__all__ = ["AudioChunks", "AudioWindow", "WhisperEncoder", "WhisperTranscribe", "SpeechToText", "FeatureSink"]
 
 RATE = 16000
 
@@ -152,6 +155,111 @@ class WhisperEncoder(GpuPipelineElement):
                 self._run(audio)
             self._tuned.add(key)
         return StreamEvent.OKAY, {"features": self.run_maybe_captured(key, self._run, audio)}
+
+
+_SILENCE = ("", "you", "thank you.", "thanks for watching!")
+
+
+def _load_tokenizer(el):
+    """Optional ``tokenizer`` parameter: a Whisper ``tokenizer.json`` read with the
+    ``tokenizers`` library (no vocabulary ships offline; without it ids render as ``<id>``)."""
+    path, found = el.get_parameter("tokenizer")
+    if not found or not path:
+        return None
+    from tokenizers import Tokenizer
+    return Tokenizer.from_file(str(path))
+
+
+def _reply(text: str) -> str:
+    """The reference's post-filter (``speech_elements.py:240-255``): lower-case, strip a final
+    full stop, map Whisper's usual hallucinations on silence to ``<silence>``."""
+    t = text.strip().lower()
+    if t in _SILENCE:
+        return "<silence>"
+    return t.removesuffix(".")
+
+
+class WhisperTranscribe(GpuPipelineElement):
+    """Greedy Whisper decoding of encoder ``features`` [B, T, d] -> ``tokens`` (int32 [B, n] on
+    the host) and ``text`` (one string per stream, "<silence>" when empty).  Parameters:
+    ``size``, ``seed``, ``max_tokens`` (default 96), ``tokenizer`` (tokenizer.json path),
+    ``weights``, ``graph`` (hipGraph-replayed decode steps, default on), ``stop_early``
+    (default on: stop once every stream has emitted end-of-text, checked every 8 steps),
+    ``defer_text`` (default off: with it the tokens come back as a DeviceResult on pinned host
+    memory without a host synchronisation and ``text`` is not produced — for throughput runs
+    where the next frame's encoder should queue behind this frame's decoder)."""
+    lane_safe = True          # one decode state / graph per lane (ws_tag)
+
+    def __init__(self, context):
+        context.set_protocol("speech_to_text:0")
+        super().__init__(context)
+        from ...models.whisper_decoder import WhisperDecoder
+        from ...ops import require_native
+        require_native()
+        self.model = WhisperDecoder(size=str(_p(self, "size", "small")), seed=int(_p(self, "seed", 1)),
+                                    device=self.device)
+        self.load_model_weights(self.model)
+        self.tokenizer = _load_tokenizer(self)
+
+    def _decode(self, features, stop: bool):
+        self.model.ws_tag = f"lane{self.lane}." if self.lane else ""
+        return self.model.transcribe(features, max_new_tokens=int(_p(self, "max_tokens", 96)),
+                                     use_graph=self.use_graph, check_every=8 if stop else 0)
+
+    def transcribe(self, features):
+        from ...models.whisper_decoder import decode_text
+        stop = str(_p(self, "stop_early", True)).lower() in ("true", "1", "yes")
+        tokens = self._decode(features, stop).cpu()
+        texts = [_reply(t) for t in decode_text(tokens, self.tokenizer, eot=self.model.eot)]
+        return tokens, texts
+
+    def process_frame(self, stream, features, t_submit=None):
+        t0 = t_submit if isinstance(t_submit, float) else None
+        if str(_p(self, "defer_text", False)).lower() in ("true", "1", "yes"):
+            tok = self._decode(features, False)
+            key = (tuple(tok.shape), self.lane)
+            bufs = self.__dict__.setdefault("_pinned", {})
+            ring = bufs.get(key)
+            if ring is None:
+                ring = bufs[key] = [[torch.empty(tok.shape, dtype=tok.dtype, pin_memory=True), None]
+                                    for _ in range(4)]
+            slot = ring[0]
+            ring.append(ring.pop(0))
+            if slot[1] is not None:
+                slot[1].synchronize()          # this slot's previous copy has landed
+            slot[0].copy_(tok, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            slot[1] = ev
+            return StreamEvent.OKAY, {"transcript": DeviceResult({"tokens": slot[0]}, ev, t_submit=t0)}
+        tokens, texts = self.transcribe(features)
+        return StreamEvent.OKAY, {"tokens": tokens, "text": texts[0] if len(texts) == 1 else texts,
+                                  "transcript": DeviceResult({"tokens": tokens}, None, t_submit=t0)}
+
+
+class SpeechToText(WhisperTranscribe):
+    """The reference's ``PE_WhisperX`` shape in one element: ``audio`` (16 kHz samples, [N] or
+    [B, N], host or device) -> log-mel + encoder + greedy decoder -> ``{"text": ...}``."""
+
+    def __init__(self, context):
+        super().__init__(context)
+        from ...models.whisper import WhisperEncoder as Encoder
+        self.encoder = Encoder(size=str(_p(self, "size", "small")), seed=int(_p(self, "encoder_seed", 0)),
+                               device=self.device)
+        path, found = self.get_parameter("encoder_weights")
+        if found and path:
+            self.encoder.load(str(path))
+
+    def process_frame(self, stream, audio):
+        x = audio if isinstance(audio, torch.Tensor) else torch.as_tensor(np.asarray(audio, dtype=np.float32))
+        x = x.to(self.device, torch.float32)
+        if x.dim() == 1:
+            x = x[None]
+        n = x.shape[1] - x.shape[1] % 320                     # whole encoder frames (320 samples)
+        if n <= 0:
+            return StreamEvent.OKAY, {"text": "<silence>", "tokens": None}
+        tokens, texts = self.transcribe(self.encoder.encode(x[:, :n].contiguous()))
+        return StreamEvent.OKAY, {"tokens": tokens, "text": texts[0] if len(texts) == 1 else texts}
 
 
 class FeatureSink(GpuPipelineElement):

@@ -8,12 +8,13 @@ token per sequence per step, entirely on the device:
   prepare(features [B, T, d]):   per layer, cross-attention K|V = fp8 GEMM over the encoder
                                  rows (once per window)  -> kv_cross[l] bf16 [B*S, 2d]
   step():                        embed(ids, pos) -> x [B, d]
-                                 L x { LN + e4m3 -> QKV GEMM -> decode attention (appends K/V at
-                                       pos into kv_self[l], attends 0..pos) -> e4m3 -> out GEMM
-                                       (+res) -> LN + e4m3 -> cross-Q GEMM -> decode attention
-                                       over kv_cross[l] -> e4m3 -> cross-out GEMM (+res) ->
-                                       LN + e4m3 -> fc1 GEMM (GELU) -> e4m3 -> fc2 GEMM (+res) }
-                                 LN + e4m3 -> logits GEMM (tied embedding, fp8) -> argmax step
+                                 L x { [LN + e4m3 + QKV GEMM] -> decode attention (appends K/V
+                                       at pos into kv_self[l], attends 0..pos) -> [e4m3 + out
+                                       GEMM + res] -> [LN + e4m3 + cross-Q GEMM] -> decode
+                                       attention over kv_cross[l] -> [e4m3 + cross-out GEMM +
+                                       res] -> [LN + e4m3 + fc1 GEMM + GELU] -> [e4m3 + fc2
+                                       GEMM + res] }   ([...] = one dec_linear launch)
+                                 [LN + e4m3 + logits GEMM (tied embedding)] -> argmax step
                                  (forced prompt, sticky end-of-text, pos += 1 on the device)
 
 Every launch reads the step position from device memory, so ``step`` is captured once into a
@@ -45,7 +46,18 @@ _KC = 256                # keys per split of the decode-attention kernel (decode
 
 
 def attn_decode_work(B: int, H: int, maxlen: int) -> int:
+    """fp32 elements of the decode-attention workspace (per-split partials; an upper bound of
+    the kernel's own split choice)."""
     return B * H * (-(-maxlen // _KC)) * (64 + 2)
+
+
+def dec_linear(x, lin: TR.Fp8Linear, out, ln: tuple | None = None, residual=None, act: int = TR.ACT_NONE,
+               eps: float = 1e-5):
+    """Decoder linear for a few rows: LayerNorm (``ln`` = (gamma, beta)) and per-row e4m3
+    quantisation fused into the fp8 MFMA GEMM (``dec_linear_kernel``)."""
+    g, b = ln if ln is not None else (None, None)
+    torch.ops.aiko.dec_linear_out(x, g, b, float(eps), lin.weight, lin.scale, lin.bias, residual, out, act)
+    return out
 
 
 def attn_decode(q, k, v, out, B: int, H: int, S: int, T: int, scale: float, work,
@@ -117,6 +129,8 @@ class WhisperDecoder(WeightsMixin):
         self._ws: dict = {}
         self._graphs: dict = {}
         self._geom = None
+        self.ws_tag = ""             # workspace key prefix (one decode state per frame lane)
+        self.fused_linear = True     # dec_linear_kernel (LN/quantise fused) where K <= 3072
 
     def _make_logit_weight(self):
         """Logits use the token embedding (tied), quantised to e4m3 per vocabulary row; rows are
@@ -145,7 +159,7 @@ class WhisperDecoder(WeightsMixin):
 
     # ---- workspace ------------------------------------------------------------------------------
     def _buf(self, key, shape, dtype=torch.bfloat16, zero=False):
-        k = (key, tuple(shape), dtype)
+        k = (self.ws_tag + key, tuple(shape), dtype)
         t = self._ws.get(k)
         if t is None:
             t = (torch.zeros if zero else torch.empty)(shape, dtype=dtype, device=self.device)
@@ -215,27 +229,28 @@ class WhisperDecoder(WeightsMixin):
         work = self._buf("work", (attn_decode_work(B, H, max(n_ctx, T)),), torch.float32)
         scale = (d // H) ** -0.5
         qd = q8[:, :d]
+
+        def lin(src, layer, out, ln=None, residual=None, act=TR.ACT_NONE):
+            if self.fused_linear and src.shape[1] <= 3072:
+                return dec_linear(src, layer, out, ln, residual, act)
+            qs = q8[:, :src.shape[1]]
+            TR.rownorm(src, *(ln or (None, None)), q=qs, qs=s8)
+            return TR.linear_fp8(qs, s8, layer, out=out, residual=residual, act=act)
+
         torch.ops.aiko.embed_tokens_out(st["ids"], st["pos"], self.tok_emb, self.pos_emb, x)
         for i, blk in enumerate(self.blocks):
             kvs = self._buf(f"kv_self{i}", (B * n_ctx, 2 * d))
             kvc = self._buf(f"kv_cross{i}", (B * S, 2 * d))
-            TR.rownorm(x, *blk.ln1, q=qd, qs=s8)
-            TR.linear_fp8(qd, s8, blk.qkv, out=qkv)
+            lin(x, blk.qkv, qkv, ln=blk.ln1)
             attn_decode(qkv[:, :d], kvs[:, :d], kvs[:, d:], att, B, H, n_ctx, 0, scale, work,
                         pos=st["pos"], knew=qkv[:, d:2 * d], vnew=qkv[:, 2 * d:])
-            TR.rownorm(att, q=qd, qs=s8)
-            TR.linear_fp8(qd, s8, blk.out, out=x, residual=x)
-            TR.rownorm(x, *blk.lnx, q=qd, qs=s8)
-            TR.linear_fp8(qd, s8, blk.cq, out=cq)
+            lin(att, blk.out, x, residual=x)
+            lin(x, blk.cq, cq, ln=blk.lnx)
             attn_decode(cq, kvc[:, :d], kvc[:, d:], att, B, H, S, T, scale, work)
-            TR.rownorm(att, q=qd, qs=s8)
-            TR.linear_fp8(qd, s8, blk.cout, out=x, residual=x)
-            TR.rownorm(x, *blk.ln2, q=qd, qs=s8)
-            TR.linear_fp8(qd, s8, blk.fc1, act=TR.ACT_GELU, out=h)
-            TR.rownorm(h, q=q8, qs=s8)
-            TR.linear_fp8(q8, s8, blk.fc2, out=x, residual=x)
-        TR.rownorm(x, *self.ln_final, q=qd, qs=s8)
-        TR.linear_fp8(qd, s8, self.logits, out=logits)
+            lin(att, blk.cout, x, residual=x)
+            lin(x, blk.fc1, h, ln=blk.ln2, act=TR.ACT_GELU)
+            lin(h, blk.fc2, x, residual=x)
+        lin(x, self.logits, logits, ln=self.ln_final)
         torch.ops.aiko.argmax_step_out(logits, self.n_vocab, st["ids"], st["pos"], st["tokens"],
                                        st["forced"], self.eot, st["done"], st["counter"])
         return logits
@@ -244,11 +259,11 @@ class WhisperDecoder(WeightsMixin):
         if not use_graph or self.device.type != "cuda":
             self.step()
             return
-        key = self._geom
+        key = (self.ws_tag,) + self._geom
         g = self._graphs.get(key)
         if g is None:
             # warm-up (tile selection, workspace allocation) runs eagerly on a scratch state
-            st = self._state(key[0])
+            st = self._state(self._geom[0])
             saved = {k: v.clone() for k, v in st.items()}
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())

@@ -87,13 +87,27 @@ WHISPER_METRIC = "30 s audio windows/sec (whole node) + p50 latency, Whisper enc
 
 
 def whisper_definition(streams: int, graph: bool, size: str, chunk: float, window: float,
-                       lanes: int = 1) -> dict:
+                       lanes: int = 1, transcribe: int = 0) -> dict:
     """BASELINE config 5: streamed audio chunks -> per-stream sliding window on the GPU ->
     log-mel + Whisper encoder (fp8 linears) -> pooled features to the host."""
     def el(name, inputs, outputs, params):
         return {"name": name, "input": [{"name": n, "type": "tensor"} for n in inputs],
                 "output": [{"name": n, "type": "tensor"} for n in outputs],
                 "parameters": params, "deploy": {"local": {"module": SPEECH}}}
+    if transcribe:      # speech-to-text: greedy decoding of ``transcribe`` tokens per window
+        return {
+            "version": 0, "name": "p_whisper_asr", "runtime": "python",
+            "graph": ["(AudioChunks AudioWindow WhisperEncoder WhisperTranscribe)"],
+            "parameters": {"gpu_lanes": lanes},
+            "elements": [
+                el("AudioChunks", [], ["audio", "t_submit"], {"streams": streams, "chunk": chunk}),
+                el("AudioWindow", ["audio"], ["audio"], {"window": window}),
+                el("WhisperEncoder", ["audio"], ["features"], {"size": size, "graph": graph}),
+                el("WhisperTranscribe", ["features", "t_submit"], ["transcript", "text"],
+                   {"size": size, "graph": graph, "max_tokens": transcribe, "stop_early": False,
+                    "defer_text": True}),
+            ],
+        }
     return {
         "version": 0, "name": "p_whisper_encoder", "runtime": "python",
         "graph": ["(AudioChunks AudioWindow WhisperEncoder FeatureSink)"],
@@ -142,6 +156,8 @@ def main(argv=None):
                          "whisper-*: config 5 (--batch = concurrent audio streams)")
     ap.add_argument("--chunk", type=float, default=5.0, help="(whisper) seconds of audio per chunk")
     ap.add_argument("--window", type=float, default=30.0, help="(whisper) encoder window seconds")
+    ap.add_argument("--transcribe", type=int, default=0,
+                    help="(whisper) decode this many tokens per window (speech-to-text) instead of pooling features")
     ap.add_argument("--fanout", choices=["scatter", "broadcast"], default="scatter",
                     help="(yolov8n) RCCL fan-out of the ingest rank's frame batch")
     ap.add_argument("--parallel", choices=["dp", "pp"], default="dp",
@@ -174,10 +190,13 @@ def main(argv=None):
     metric, unit = METRIC, "frames/s"
     if a.model.startswith("whisper"):
         size = a.model.split("-", 1)[1]
-        d = parse_pipeline_definition_dict(whisper_definition(a.batch, not a.no_graph, size, a.chunk, a.window, a.lanes))
-        result_key, model_cfg = "embedding", {"model": f"whisper-{size}-encoder", "weights": "fp8 e4m3 (per-channel)",
-                                              "chunk_s": a.chunk, "window_s": a.window, "streams": a.batch,
-                                              "pipeline": d.graph[0], "gpu_lanes": a.lanes}
+        d = parse_pipeline_definition_dict(whisper_definition(a.batch, not a.no_graph, size, a.chunk, a.window,
+                                                              a.lanes, a.transcribe))
+        result_key = "transcript" if a.transcribe else "embedding"
+        model_cfg = {"model": f"whisper-{size}" + ("-asr" if a.transcribe else "-encoder"),
+                     "weights": "fp8 e4m3 (per-channel)", "decode_tokens": a.transcribe,
+                     "chunk_s": a.chunk, "window_s": a.window, "streams": a.batch,
+                     "pipeline": d.graph[0], "gpu_lanes": a.lanes}
         metric, unit = WHISPER_METRIC, "windows/s"
     elif a.model == "yolov8n":
         d = parse_pipeline_definition_dict(yolo_definition(a.batch, not a.no_graph, a.height, a.width, a.fanout, a.lanes))
@@ -254,6 +273,8 @@ def main(argv=None):
         }
         if a.model.startswith("whisper"):
             out["audio_seconds_per_s"] = round(ws * a.batch * a.chunk * a.steps / elapsed, 1)
+            if a.transcribe:
+                out["decoded_tokens_per_s"] = round(ws * a.batch * a.transcribe * a.steps / elapsed, 1)
         print(json.dumps(out), flush=True)
     D.barrier()
     D.destroy()

@@ -20,34 +20,39 @@ def _ref_attn(q, k, v, scale):
     return torch.einsum("bht,bthd->bhd", p, v).reshape(q.shape[0], -1)
 
 
-@pytest.mark.parametrize("T,S", [(33, 40), (600, 601), (1500, 1501)])
-def test_attn_decode_cross(native, T, S):
+@pytest.mark.parametrize("T,S,B", [(33, 40, 3), (600, 601, 3), (1500, 1501, 3), (1500, 1501, 16), (700, 701, 12)])
+def test_attn_decode_cross(native, T, S, B):
+    """Few sequences split the keys over workgroups (+ combine); B*H >= 128 streams all chunks
+    in one workgroup per (sequence, head)."""
     from aiko_services_amd.models.whisper_decoder import attn_decode, attn_decode_work
     g = torch.Generator().manual_seed(T)
-    B, H = 3, 6
+    H = 6 if B < 16 else 12
     d = H * 64
     q = torch.randn(B, d, generator=g).to(DEV, torch.bfloat16)
     kv = torch.randn(B * S, 2 * d, generator=g).to(DEV, torch.bfloat16)
     out = torch.empty(B, d, dtype=torch.bfloat16, device=DEV)
-    work = torch.empty(attn_decode_work(B, H, T), dtype=torch.float32, device=DEV)
+    work = torch.zeros(attn_decode_work(B, H, T), dtype=torch.float32, device=DEV)
     attn_decode(q, kv[:, :d], kv[:, d:], out, B, H, S, T, 0.125, work)
     kk = kv[:, :d].float().view(B, S, H, 64)[:, :T]
     vv = kv[:, d:].float().view(B, S, H, 64)[:, :T]
     ref = _ref_attn(q.float().view(B, H, 64), kk, vv, 0.125)
     assert _rel(out, ref) < 1e-2
+    out2 = torch.empty_like(out)
+    attn_decode(q, kv[:, :d], kv[:, d:], out2, B, H, S, T, 0.125, work)
+    assert torch.equal(out, out2)
 
 
-@pytest.mark.parametrize("p", [0, 5, 255, 256, 300])
-def test_attn_decode_append(native, p):
+@pytest.mark.parametrize("p,B", [(0, 2), (5, 2), (255, 2), (256, 2), (300, 2), (300, 16), (0, 16)])
+def test_attn_decode_append(native, p, B):
     from aiko_services_amd.models.whisper_decoder import attn_decode, attn_decode_work
     g = torch.Generator().manual_seed(100 + p)
-    B, H, S = 2, 4, 448
+    H, S = (4 if B < 16 else 12), 448
     d = H * 64
     cache = torch.randn(B * S, 2 * d, generator=g).to(DEV, torch.bfloat16)
     qkv = torch.randn(B, 3 * d, generator=g).to(DEV, torch.bfloat16)
     pos = torch.tensor([p], dtype=torch.int32, device=DEV)
     out = torch.empty(B, d, dtype=torch.bfloat16, device=DEV)
-    work = torch.empty(attn_decode_work(B, H, S), dtype=torch.float32, device=DEV)
+    work = torch.zeros(attn_decode_work(B, H, S), dtype=torch.float32, device=DEV)
     before = cache.clone()
     attn_decode(qkv[:, :d], cache[:, :d], cache[:, d:], out, B, H, S, 0, 0.125, work,
                 pos=pos, knew=qkv[:, d:2 * d], vnew=qkv[:, 2 * d:])
@@ -93,6 +98,45 @@ def test_embed_and_argmax_step(native):
     pos.fill_(0)
     torch.ops.aiko.argmax_step_out(logits, V, ids, pos, out_tokens, forced, eot, done, counter)
     assert ids.tolist() == [2, 2, 2, 2] and pos.item() == 1
+
+
+@pytest.mark.parametrize("M,K,N", [(16, 768, 2304), (5, 384, 51968), (37, 3072, 768), (16, 1280, 1280)])
+@pytest.mark.parametrize("ln", [False, True])
+def test_dec_linear_matches_unfused(native, M, K, N, ln):
+    """dec_linear (LN + e4m3 quantise fused into the skinny fp8 GEMM) equals rownorm +
+    linear_fp8 on the same inputs, and both track the fp32 reference."""
+    from aiko_services_amd.models.whisper_decoder import dec_linear
+    from aiko_services_amd.ops import transformer as TR
+    g = torch.Generator().manual_seed(M + K)
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    lin = TR.make_fp8_linear(torch.randn(N, K, generator=g) / K ** 0.5, 0.1 * torch.randn(N, generator=g), DEV)
+    res = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    gb = ((1 + 0.1 * torch.randn(K, generator=g)).to(DEV), (0.1 * torch.randn(K, generator=g)).to(DEV)) if ln else None
+    for act in (0, 3):
+        y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        dec_linear(x, lin, y, gb, residual=res, act=act)
+        q = torch.empty(M, K, dtype=torch.uint8, device=DEV)
+        s = torch.empty(M, dtype=torch.float32, device=DEV)
+        TR.rownorm(x, *(gb or (None, None)), q=q, qs=s)
+        y2 = TR.linear_fp8(q, s, lin, residual=res, act=act)
+        assert _rel(y, y2) < 2e-3
+        h = F.layer_norm(x.float(), (K,), *gb, 1e-5) if ln else x.float()
+        ref = h @ lin.ref_weight.T.to(DEV) + lin.bias
+        ref = (F.gelu(ref) if act == 3 else ref) + res.float()
+        assert _rel(y, ref) < 3e-2
+
+
+def test_decoder_fused_matches_unfused(native):
+    from aiko_services_amd.models.whisper_decoder import WhisperDecoder
+    feats = _features(3, 120, 384, seed=9)
+    dec = WhisperDecoder("tiny", device=DEV)
+    a = dec.transcribe(feats, max_new_tokens=10, use_graph=False, check_every=0).clone()
+    la = dec._buf("logits", (3, dec.logits.n)).clone()
+    dec.fused_linear = False
+    b = dec.transcribe(feats, max_new_tokens=10, use_graph=False, check_every=0).clone()
+    lb = dec._buf("logits", (3, dec.logits.n)).clone()
+    assert _rel(la, lb) < 1e-2
+    assert (a == b).float().mean().item() > 0.9
 
 
 def _features(B, T, d, seed=3):
@@ -146,3 +190,66 @@ def test_decoder_greedy_graph(native):
                 continue
             row = ref[b, t]
             assert row[nxt] >= row.max() - 0.25 * row.std(), (b, t)
+
+
+def _run(d, frames):
+    import queue
+    from aiko_services_amd.pipeline.definition import parse_pipeline_definition_dict
+    from aiko_services_amd.pipeline.engine import PipelineImpl
+    q = queue.Queue()
+    p = PipelineImpl.create_pipeline("<t>", parse_pipeline_definition_dict(d), None, None, "a", [], 0,
+                                     None, 60, queue_response=q)
+    outs = []
+    for i in range(frames):
+        p.process_frame({"stream_id": "a", "frame_id": i}, {})
+        info, out = q.get_nowait()
+        assert info["state"] == 0, out
+        outs.append(out)
+    return outs
+
+
+def test_asr_pipeline(native):
+    """(AudioChunks AudioWindow WhisperEncoder WhisperTranscribe): text per stream per frame."""
+    import bench
+    outs = _run(bench.whisper_definition(2, True, "tiny", 2.0, 6.0, 2, transcribe=8), 3)
+    for out in outs:
+        toks = out["transcript"].wait()["tokens"]
+        assert toks.shape == (2, 4 + 8) and toks.dtype == torch.int32
+        assert "text" not in out                                  # defer_text: tokens only
+    # synchronous mode yields the text outputs too, with the same tokens
+    d = bench.whisper_definition(2, True, "tiny", 2.0, 6.0, 1, transcribe=8)
+    d["elements"][-1]["parameters"].update(defer_text=False)
+    outs2 = _run(d, 3)
+    for a, b in zip(outs, outs2):
+        assert torch.equal(a["transcript"].wait()["tokens"], b["tokens"])
+        assert isinstance(b["text"], list) and len(b["text"]) == 2
+        assert all(t == "<silence>" or t.startswith("<") for t in b["text"])
+
+
+def test_speech_to_text_element(native):
+    """SpeechToText (PE_WhisperX shape): host audio in, text out; same tokens as encoder +
+    WhisperTranscribe on the same audio."""
+    import numpy as np
+    from aiko_services_amd.models.whisper import WhisperEncoder
+    from aiko_services_amd.models.whisper_decoder import WhisperDecoder
+    M = "aiko_services_amd.elements.gpu.speech"
+    audio = (0.3 * np.sin(np.arange(32000) * 0.05)).astype(np.float32)
+    d = {"version": 0, "name": "p_stt", "runtime": "python", "graph": ["(SpeechToText)"],
+         "elements": [{"name": "SpeechToText", "input": [{"name": "audio", "type": "tensor"}],
+                       "output": [{"name": "text", "type": "str"}],
+                       "parameters": {"size": "tiny", "max_tokens": 6},
+                       "deploy": {"local": {"module": M}}}]}
+    import queue
+    from aiko_services_amd.pipeline.definition import parse_pipeline_definition_dict
+    from aiko_services_amd.pipeline.engine import PipelineImpl
+    q = queue.Queue()
+    p = PipelineImpl.create_pipeline("<t>", parse_pipeline_definition_dict(d), None, None, "s", [], 0,
+                                     None, 60, queue_response=q)
+    p.process_frame({"stream_id": "s", "frame_id": 0}, {"audio": audio})
+    info, out = q.get_nowait()
+    assert info["state"] == 0, out
+    assert isinstance(out["text"], str)
+    enc = WhisperEncoder("tiny", seed=0, device=DEV)
+    dec = WhisperDecoder("tiny", seed=1, device=DEV)
+    ref = dec.transcribe(enc.encode(torch.from_numpy(audio)[None].to(DEV)), max_new_tokens=6).cpu()
+    assert torch.equal(out["tokens"], ref)
