@@ -13,6 +13,9 @@ from __future__ import annotations
 
 from abc import abstractmethod
 import argparse
+import time
+
+import numpy as np
 
 import aiko_services_amd as aiko
 from aiko_services_amd.runtime.actor import Actor
@@ -21,9 +24,13 @@ from aiko_services_amd.runtime.process import aiko as _aiko
 from aiko_services_amd.utils.configuration import get_namespace
 from aiko_services_amd.utils.sexpr import generate
 
-from .xgo_robot import XGORobot, decode_image, topic_video
+from aiko_services_amd.runtime import event
 
-__all__ = ["RobotControl", "RobotControlImpl"]
+from .xgo_robot import XGORobot, decode_image, encode_image, topic_video
+
+__all__ = ["RobotControl", "RobotControlImpl", "VideoTest", "VideoTestImpl"]
+
+SLEEP_PERIOD = 0.2          # seconds between published frames (EC-tunable ``sleep_period``)
 
 
 class RobotControl(Actor):
@@ -72,14 +79,70 @@ class RobotControlImpl(RobotControl):
         getattr(proxy, command)(*args)
 
 
+class VideoTest(Actor):
+    """Video source for testing the controller without a robot (reference
+    ``robot_control.py:302-355``): publishes ``zlib(np.save(image))`` frames on the video topic
+    every ``sleep_period`` seconds.  The reference reads camera 0 through OpenCV; without a
+    camera (no OpenCV in this image) frames are a synthetic moving gradient, 240 x 320 RGB, with
+    the per-frame time and rate in the share instead of drawn into the image."""
+    Interface.default("VideoTest", "aiko_services_amd.examples.xgo_robot.robot_control.VideoTestImpl")
+
+
+class VideoTestImpl(VideoTest):
+    def __init__(self, context, size=(240, 320)):
+        context.get_implementation("Actor").__init__(self, context)
+        self.size = (int(size[0]), int(size[1]))
+        self.share.update({"sleep_period": SLEEP_PERIOD, "source_file": __file__, "topic_video": topic_video(),
+                           "frames_published": 0, "fps": 0, "time_process_ms": 0.0})
+        self._frame_id = 0
+        self._last = None
+        self._period = None
+        self._schedule()
+
+    def _schedule(self):
+        try:
+            period = float(self.share["sleep_period"])
+        except (TypeError, ValueError):
+            period = SLEEP_PERIOD
+        period = max(period, 0.001)
+        if period != self._period:                 # live retune via (update sleep_period ...)
+            if self._period is not None:
+                event.remove_timer_handler(self._tick)
+            event.add_timer_handler(self._tick, period)
+            self._period = period
+
+    def frame(self) -> np.ndarray:
+        h, w = self.size
+        yy, xx = np.mgrid[0:h, 0:w]
+        k = self._frame_id
+        image = np.stack([(xx + 4 * k) % 256, (yy + 2 * k) % 256, np.full_like(xx, (16 * k) % 256)], axis=-1)
+        return image.astype(np.uint8)
+
+    def _tick(self):
+        t0 = time.time()
+        image = self.frame()
+        self.share["time_process_ms"] = round((time.time() - t0) * 1000, 1)
+        _aiko.message.publish(self.share["topic_video"], encode_image(image))
+        self._frame_id += 1
+        self.ec_producer.update("frames_published", self._frame_id)
+        if self._last is not None:
+            self.share["fps"] = int(1.0 / max(t0 - self._last, 1e-6))
+        self._last = t0
+        self._schedule()
+
+
 def main(argv=None):
-    ap = argparse.ArgumentParser(description="robot controller actor")
+    ap = argparse.ArgumentParser(description="robot controller actor (or --video_test: test video source)")
     ap.add_argument("--robot", default=None, help="robot actor /in topic")
     ap.add_argument("--detector", default=None, choices=[None, "yolo"])
+    ap.add_argument("--video_test", action="store_true", help="run the VideoTest source instead")
     a = ap.parse_args(argv)
-    args = aiko.actor_args("robot_control")
-    args.update(robot_topic=a.robot, detector=a.detector)
-    aiko.compose_instance(RobotControlImpl, args)
+    if a.video_test:
+        aiko.compose_instance(VideoTestImpl, aiko.actor_args("video_test"))
+    else:
+        args = aiko.actor_args("robot_control")
+        args.update(robot_topic=a.robot, detector=a.detector)
+        aiko.compose_instance(RobotControlImpl, args)
     aiko.process.run()
 
 

@@ -93,6 +93,59 @@ def find_plugin(details):
     return None
 
 
+class LogLevelPopupMenu:
+    """Log-level chooser for the selected service (reference ``dashboard.py:670-714``): a small
+    window listing the levels with the current one highlighted; up/down or a digit picks, enter
+    applies — the choice is published as ``(update log_level LEVEL)`` on the service's
+    ``/control`` topic, exactly like an edited variable."""
+
+    def __init__(self, dashboard, levels=None):
+        self.dashboard = dashboard
+        self.levels = list(levels or LOG_LEVELS)
+        current = str(dashboard.variables.get("log_level", "INFO")).upper()
+        self.index = self.levels.index(current) if current in self.levels else 0
+
+    def key(self, ch) -> str | None:
+        """Feed one key: returns the chosen level on enter/digit, "" on cancel, None to go on."""
+        if ch in (27, ord("q")):
+            return ""
+        if ord("1") <= ch < ord("1") + len(self.levels):
+            self.index = ch - ord("1")
+            return self.apply()
+        if ch in (258, ord("j")):                     # curses.KEY_DOWN
+            self.index = (self.index + 1) % len(self.levels)
+        elif ch in (259, ord("k")):                   # curses.KEY_UP
+            self.index = (self.index - 1) % len(self.levels)
+        elif ch in (10, 13):
+            return self.apply()
+        return None
+
+    def apply(self) -> str:
+        level = self.levels[self.index]
+        self.dashboard.edit_variable("log_level", level)
+        return level
+
+    def lines(self) -> list[str]:
+        return [f"{'>' if i == self.index else ' '} {i + 1} {lv}" for i, lv in enumerate(self.levels)]
+
+    def run(self, scr):
+        import curses
+        h, w = scr.getmaxyx()
+        bw, bh = 18, len(self.levels) + 2
+        win = curses.newwin(bh, bw, max(0, (h - bh) // 2), max(0, (w - bw) // 2))
+        win.keypad(True)
+        while True:
+            win.erase()
+            win.box()
+            win.addstr(0, 2, " log level ")
+            for i, line in enumerate(self.lines()):
+                win.addstr(1 + i, 1, line[: bw - 2], curses.A_REVERSE if i == self.index else 0)
+            win.refresh()
+            out = self.key(win.getch())
+            if out is not None:
+                return out
+
+
 class Dashboard:
     def __init__(self, history_limit=HISTORY_LIMIT):
         self.cache = services_cache_create_singleton(aiko.process, True, history_limit)
@@ -223,6 +276,9 @@ class Dashboard:
                 self.page = "plugin" if self.page != "plugin" else "services"
             elif ch == ord("L"):
                 self.status = f"log_level -> {self.cycle_log_level()}"
+            elif ch == ord("v"):
+                chosen = LogLevelPopupMenu(self).run(scr)
+                self.status = f"log_level -> {chosen}" if chosen else "log level unchanged"
             elif ch == ord("K"):
                 self.status = self.kill_selected()
             elif ch == ord("e") and self.focus == "variables":
@@ -285,7 +341,7 @@ class Dashboard:
                 import curses
                 attr = curses.A_REVERSE if (self.focus == "variables" and i == self.var_index) else 0
                 scr.addstr(top + 2 + i, 0, f"{k:40.40} {v}"[: w - 1], attr)
-        scr.addstr(h - 1, 0, (f"{self.status}  " + "q quit  arrows select  tab pane  e edit  L level  "
+        scr.addstr(h - 1, 0, (f"{self.status}  " + "q quit  arrows select  tab pane  e edit  v level menu  L next level  "
                               "l log  h history  p plugin  K kill")[: w - 1])
         scr.refresh()
 

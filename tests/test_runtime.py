@@ -305,6 +305,17 @@ def test_xgo_robot_simulated_video_and_control(aiko_process):
     assert robot.share["pose"][0] != 0 or robot.share["pose"][1] != 0
     control.robot("stop")
     event.call_on_loop(lambda: event.remove_timer_handler(robot._tick))
+    # VideoTest: the controller also consumes the test video source; live sleep_period retune
+    from aiko_services_amd.examples.xgo_robot.robot_control import VideoTestImpl
+    vt = event.call_on_loop(lambda: compose_instance(VideoTestImpl, actor_args("video_test")))
+    start = int(control.share["frames_received"])
+    event.call_on_loop(lambda: vt.ec_producer.update("sleep_period", 0.01))
+    deadline = time.time() + 5
+    while int(control.share["frames_received"]) < start + 5 and time.time() < deadline:
+        time.sleep(0.02)
+    assert int(control.share["frames_received"]) >= start + 5
+    assert control.last_image.shape == (240, 320, 3) and vt._period == 0.01
+    event.call_on_loop(lambda: event.remove_timer_handler(vt._tick))
 
 
 def test_ec_test_services(aiko_process):

@@ -116,6 +116,25 @@ def test_dashboard_plugin_pages():
     del D.PLUGINS["yolo"]
 
 
+def test_dashboard_log_level_popup():
+    """LogLevelPopupMenu: starts on the service's level, arrows/digits pick, enter publishes
+    (update log_level LEVEL) through the dashboard's edit path; escape cancels."""
+    from aiko_services_amd.tools import dashboard as D
+    sent = []
+
+    class Fake:
+        variables = {"log_level": "WARNING"}
+
+        def edit_variable(self, name, value):
+            sent.append((name, value))
+    menu = D.LogLevelPopupMenu(Fake())
+    assert menu.levels[menu.index] == "WARNING"
+    assert menu.key(258) is None and menu.key(10) == menu.levels[(menu.levels.index("WARNING") + 1) % len(menu.levels)]
+    assert sent[-1][0] == "log_level"
+    assert D.LogLevelPopupMenu(Fake()).key(ord("1")) == D.LOG_LEVELS[0]
+    assert D.LogLevelPopupMenu(Fake()).key(27) == "" and len(sent) == 2
+
+
 def test_gstreamer_launch_descriptions_and_gating():
     """elements/gstreamer: reference launch strings; without the Gst typelib the readers and
     writers raise GStreamerError (no silent fallback)."""
