@@ -16,6 +16,8 @@ statistics are random too and folded into the conv weights at construction.
 """
 from __future__ import annotations
 
+import os
+
 import math
 from dataclasses import dataclass
 
@@ -92,6 +94,9 @@ class ResNet50(WeightsMixin):
         self._ws: dict = {}
         self.fuse_shortcut = True
         self.fuse_stem_pool = True       # stem conv + ReLU + max-pool in one kernel
+        # Infinity-Cache blocking of the memory-bound early stages (see features_from_stem)
+        self.mall_chunk = int(os.environ.get("AIKO_RESNET_MALL_CHUNK", "0"))
+        self.mall_blocks = int(os.environ.get("AIKO_RESNET_MALL_BLOCKS", "3"))
 
     # ---- workspace: every activation buffer allocated once per batch size ----------------
     def _buf(self, key: str, shape, dtype=torch.bfloat16) -> torch.Tensor:
@@ -120,30 +125,55 @@ class ResNet50(WeightsMixin):
         S = self.image_size
         Ho, Wo = C.stem_out_hw(S, S)
         Hm, Wm = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
-        if self.fuse_stem_pool:
-            x = C.stem_pool(x, self.stem, (S, S), out=self._buf(tag + "pool", (B, Hm, Wm, 64)))
-        else:
-            x = C.conv2d(x, self.stem, out=self._buf(tag + "stem", (B, Ho, Wo, 64)), image_hw=(S, S))
-            x = V.maxpool2d(x, 3, 2, 1, out=self._buf(tag + "pool", (B, Hm, Wm, 64)))
-        if after_block is not None and after_block[0] < 0:
-            after_block[1]()
-        for bi, blk in enumerate(self.blocks):
-            H, W = x.shape[1], x.shape[2]
-            t1 = C.conv2d(x, blk.conv1, out=self._buf(tag + "t1", (B, H, W, blk.conv1.cout)))
-            Ho, Wo = blk.conv2.out_hw(H, W)
-            t2 = C.conv2d(t1, blk.conv2, out=self._buf(tag + "t2", (B, Ho, Wo, blk.conv2.cout)))
-            key = "xa" if bi % 2 == 0 else "xb"
-            out = self._buf(tag + key, (B, Ho, Wo, blk.conv3.cout))
-            if blk.fused is not None and self.fuse_shortcut:
-                x = C.conv2d(t2, blk.fused, x2=x, out=out)
-            elif blk.down is not None:
-                idn = C.conv2d(x, blk.down, out=self._buf(tag + "ds", (B, Ho, Wo, blk.down.cout)))
-                x = C.conv2d(t2, blk.conv3, residual=idn, out=out)
+        # Infinity-Cache blocking: the stem and the first ``mall_blocks`` bottlenecks run per
+        # sub-batch of ``mall_chunk`` frames (views of the full-batch buffers), so each block's
+        # input, intermediates and output stay within the 256 MiB die-level cache between
+        # producer and consumer instead of round-tripping HBM; later (compute-bound, small)
+        # stages run on the whole batch.
+        ch = self.mall_chunk if 0 < self.mall_chunk < B and B % self.mall_chunk == 0 else B
+        nb = self.mall_blocks if ch < B else 0
+        pool = self._buf(tag + "pool", (B, Hm, Wm, 64))
+        xs = []
+        for c0 in range(0, B, ch):
+            xc = x[c0:c0 + ch]
+            if self.fuse_stem_pool:
+                xc = C.stem_pool(xc, self.stem, (S, S), out=pool[c0:c0 + ch])
             else:
-                x = C.conv2d(t2, blk.conv3, residual=x, out=out)
+                st = self._buf(tag + "stem", (B, Ho, Wo, 64))[c0:c0 + ch]
+                xc = V.maxpool2d(C.conv2d(xc, self.stem, out=st, image_hw=(S, S)), 3, 2, 1, out=pool[c0:c0 + ch])
+            for bi in range(nb):
+                xc = self._block(bi, xc, tag, B, c0, ch)
+            xs.append(xc)
+        if len(xs) == 1:
+            x = xs[0]
+        elif nb == 0:
+            x = pool
+        else:                                      # the full-batch buffer the slices went to
+            x = self._buf(tag + ("xa" if (nb - 1) % 2 == 0 else "xb"), (B,) + tuple(xs[0].shape[1:]))
+        if after_block is not None and after_block[0] < nb:
+            after_block[1]()
+        for bi in range(nb, len(self.blocks)):
+            x = self._block(bi, x, tag, B, 0, B)
             if after_block is not None and after_block[0] == bi:
                 after_block[1]()
         return V.avgpool(x, out=self._buf(tag + "gap", (B, x.shape[3])))
+
+    def _block(self, bi: int, x: torch.Tensor, tag: str, B: int, c0: int, ch: int) -> torch.Tensor:
+        """Bottleneck ``bi`` on frames c0 .. c0+ch of the batch (slices of [B, ...] buffers)."""
+        blk = self.blocks[bi]
+        H, W = x.shape[1], x.shape[2]
+        sl = slice(c0, c0 + ch)
+        t1 = C.conv2d(x, blk.conv1, out=self._buf(tag + "t1", (B, H, W, blk.conv1.cout))[sl])
+        Ho, Wo = blk.conv2.out_hw(H, W)
+        t2 = C.conv2d(t1, blk.conv2, out=self._buf(tag + "t2", (B, Ho, Wo, blk.conv2.cout))[sl])
+        key = "xa" if bi % 2 == 0 else "xb"
+        out = self._buf(tag + key, (B, Ho, Wo, blk.conv3.cout))[sl]
+        if blk.fused is not None and self.fuse_shortcut:
+            return C.conv2d(t2, blk.fused, x2=x, out=out)
+        if blk.down is not None:
+            idn = C.conv2d(x, blk.down, out=self._buf(tag + "ds", (B, Ho, Wo, blk.down.cout))[sl])
+            return C.conv2d(t2, blk.conv3, residual=idn, out=out)
+        return C.conv2d(t2, blk.conv3, residual=x, out=out)
 
     def _lanes(self, n: int) -> list:
         lanes = getattr(self, "_lane_streams", None)

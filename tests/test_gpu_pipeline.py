@@ -150,3 +150,18 @@ def test_yolo_and_whisper_pipelines_lanes_match_single_lane(native, lanes):
     p, got = _run_bench_pipeline(bench.whisper_definition(2, True, "tiny", 2.0, 6.0, lanes), 6)
     for a, b in zip(ref, got):
         assert torch.equal(a["pooled"], b["pooled"])
+
+
+@pytest.mark.parametrize("chunk,blocks", [(32, 3), (16, 7)])
+def test_resnet50_mall_chunking_matches(native, chunk, blocks):
+    """Infinity-Cache blocking (stem + first bottlenecks per sub-batch) only reorders work:
+    logits equal the whole-batch forward."""
+    from aiko_services_amd.models.resnet50 import ResNet50
+    g = torch.Generator().manual_seed(4)
+    frames = torch.randint(0, 256, (64, 224, 224, 3), generator=g, dtype=torch.uint8).to("cuda")
+    m = ResNet50(device="cuda")
+    m.mall_chunk = 0
+    ref = m.logits(frames).clone()
+    m.mall_chunk, m.mall_blocks = chunk, blocks
+    got = m.logits(frames).clone()
+    assert torch.equal(got, ref) or ((got.float() - ref.float()).abs().max() < 1e-2 * ref.float().abs().max())
