@@ -34,6 +34,10 @@ int aiko_conv_glds(const void* x, const void* w, const float* bias, const void* 
 int aiko_preprocess(const void* in, void* out, int B, int Hin, int Win, int Ho, int Wo, int Hp,
                     int Wp, int pad_t, int pad_l, int Hc, int Wc, int off_t, int off_l, float fill,
                     const float* mean, const float* std, int bgr, hipStream_t stream);
+int aiko_stem_direct(const void* in, void* out, const void* w, const float* bias, int B, int Hin, int Win,
+                     int Ho, int Wo, int Hc, int Wc, int off_t, int off_l, float fill, const float* mean,
+                     const float* std, int bgr, int H1, int W1, int Cout, int ldo, int k, int stride, int pad,
+                     int act, hipStream_t stream);
 int aiko_maxpool(const void* x, void* y, int B, int H, int W, int C, int Ho, int Wo, int k,
                  int s, int p, int ldx, int ldy, hipStream_t stream);
 int aiko_resize_u8(const void* in, void* out, int B, int Hin, int Win, int Ho, int Wo, hipStream_t stream);
@@ -227,6 +231,46 @@ void preprocess_out(const at::Tensor& frames, at::Tensor& out, int64_t Ho, int64
                                  frames.size(2), Ho, Wo, out.size(1), out.size(2), pad_t, pad_l,
                                  Hc, Wc, off_t, off_l, (float)fill, m, s, bgr ? 1 : 0, cur_stream());
   check_launch(rc, "preprocess");
+}
+
+int64_t pixel_pitch(const at::Tensor& t, const char* op);
+
+// uint8 frames -> letterbox/normalise -> k x k stem conv (+bias, act) -> bf16 NHWC ``out``
+// [B, H1, W1, Cout]; w bf16 [Cout, 64] (k = tap * 4 + channel, zero padded); geom = [Ho, Wo, Hc, Wc, off_t, off_l, k, stride, pad, act]
+void stem_direct_out(const at::Tensor& frames, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                     at::Tensor& out, at::IntArrayRef geom, double fill, at::ArrayRef<double> mean,
+                     at::ArrayRef<double> std, bool bgr) {
+  check_cuda(frames, "frames");
+  check_cuda(w, "w");
+  check_cuda(out, "out");
+  TORCH_CHECK(frames.scalar_type() == at::kByte && frames.dim() == 4 && frames.size(3) == 3 && frames.is_contiguous(),
+              "aiko.stem_direct_out: frames must be uint8 [B, H, W, 3] contiguous");
+  TORCH_CHECK(geom.size() == 10, "aiko.stem_direct_out: geom = [Ho, Wo, Hc, Wc, off_t, off_l, k, stride, pad, act]");
+  const int64_t Ho = geom[0], Wo = geom[1], Hc = geom[2], Wc = geom[3], off_t = geom[4], off_l = geom[5];
+  const int64_t k = geom[6], stride = geom[7], pad = geom[8], act = geom[9];
+  TORCH_CHECK(off_t >= 0 && off_l >= 0 && off_t + Ho <= Hc && off_l + Wo <= Wc,
+              "aiko.stem_direct_out: image must lie inside the canvas");
+  const int64_t B = frames.size(0), Cout = out.size(3);
+  const int64_t H1 = (Hc + 2 * pad - k) / stride + 1, W1 = (Wc + 2 * pad - k) / stride + 1;
+  TORCH_CHECK(out.size(0) == B && out.size(1) == H1 && out.size(2) == W1, "aiko.stem_direct_out: out must be [B, ",
+              H1, ", ", W1, ", Cout]");
+  const int64_t ldo = pixel_pitch(out, "stem_direct_out");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 2 && w.size(0) == Cout &&
+                  w.size(1) == 64 && k * k * 4 <= 64 && Cout % 16 == 0,
+              "aiko.stem_direct_out: w bf16 [Cout, 64] contiguous (k <= 4, Cout % 16 == 0)");
+  const float* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    check_cuda(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == Cout && bias->is_contiguous(), "aiko.stem_direct_out: bias fp32 [Cout]");
+    bp = bias->data_ptr<float>();
+  }
+  TORCH_CHECK(mean.size() == 3 && std.size() == 3, "aiko.stem_direct_out: mean/std need 3 values");
+  float m[3] = {(float)mean[0], (float)mean[1], (float)mean[2]};
+  float s[3] = {(float)std[0], (float)std[1], (float)std[2]};
+  check_launch(aiko_stem_direct(frames.data_ptr(), out.data_ptr(), w.data_ptr(), bp, B, frames.size(1),
+                                frames.size(2), Ho, Wo, Hc, Wc, off_t, off_l, (float)fill, m, s, bgr ? 1 : 0, H1, W1,
+                                Cout, ldo, k, stride, pad, act, cur_stream()),
+               "stem_direct");
 }
 
 // NHWC bf16 tensor whose channels may be a slice of a wider buffer: returns the pixel pitch
@@ -759,6 +803,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("batchnorm_out(Tensor x, Tensor scale, Tensor shift, Tensor(a!) y, int act) -> ()");
   m.def("yolo_decode_out(Tensor[] feats, int[] strides, int nc, int reg_max, Tensor(a!) boxes, Tensor(b!) scores, Tensor(c!) cls) -> ()");
   m.def("topk_nms_out(Tensor boxes, Tensor scores, Tensor cls, int max_cand, float[] params, Tensor(a!) det, Tensor(b!) count) -> ()");
+  m.def("stem_direct_out(Tensor frames, Tensor w, Tensor? bias, Tensor(a!) out, int[] geom, float fill, float[] mean, float[] std, bool bgr) -> ()");
   m.def("maxpool_out(Tensor x, Tensor(a!) y, int k, int s, int p) -> ()");
   m.def("avgpool_out(Tensor x, Tensor(a!) y) -> ()");
   m.def("stem_pool_out(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, int Ho, int Wo, int variant=0) -> ()");
@@ -777,6 +822,7 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("conv_igemm_out", &conv_igemm_out);
   m.impl("preprocess_out", &preprocess_out);
   m.impl("maxpool_out", &maxpool_out);
+  m.impl("stem_direct_out", &stem_direct_out);
   m.impl("upsample2x_out", &upsample2x_out);
   m.impl("resize_u8_out", &resize_u8_out);
   m.impl("batchnorm_out", &batchnorm_out);

@@ -12,6 +12,44 @@ namespace aiko {
 // the canvas is the constant colour ``fill`` (letterbox bars, e.g. 114 for YOLO).  The 4th
 // channel is zero.  ResNet: canvas == image, YOLO: 640x640 canvas with an aspect-preserving
 // image.  One thread per padded output pixel (8-byte store): the buffer never needs a memset.
+// the canvas colour of one pixel (image bilinearly resized into the canvas, ``fill`` around it),
+// normalised; shared by the pre-processing kernel and the fused YOLO stem
+__device__ __forceinline__ void pre_pixel(const uint8_t* __restrict__ in, int b, int Hin, int Win, int Ho,
+                                          int Wo, int off_t, int off_l, int yc, int xc, float fill,
+                                          float m0, float m1, float m2, float is0, float is1, float is2,
+                                          int bgr, float& v0, float& v1, float& v2) {
+  const int yo = yc - off_t, xo = xc - off_l;
+  float c[3] = {fill, fill, fill};
+  if (yo >= 0 && yo < Ho && xo >= 0 && xo < Wo) {
+    if (Hin == Ho && Win == Wo) {
+      const uint8_t* px = in + (((long)b * Hin + yo) * Win + xo) * 3;
+      c[0] = px[0]; c[1] = px[1]; c[2] = px[2];
+    } else {
+      const float sy = fmaxf(((yo + 0.5f) * Hin) / Ho - 0.5f, 0.f);
+      const float sx = fmaxf(((xo + 0.5f) * Win) / Wo - 0.5f, 0.f);
+      int y0 = (int)sy, x0 = (int)sx;
+      y0 = min(y0, Hin - 1); x0 = min(x0, Win - 1);
+      const int y1 = min(y0 + 1, Hin - 1), x1 = min(x0 + 1, Win - 1);
+      const float fy = sy - y0, fx = sx - x0;
+      const uint8_t* base = in + (long)b * Hin * Win * 3;
+      const uint8_t* p00 = base + ((long)y0 * Win + x0) * 3;
+      const uint8_t* p01 = base + ((long)y0 * Win + x1) * 3;
+      const uint8_t* p10 = base + ((long)y1 * Win + x0) * 3;
+      const uint8_t* p11 = base + ((long)y1 * Win + x1) * 3;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const float top = p00[k] + (p01[k] - (float)p00[k]) * fx;
+        const float bot = p10[k] + (p11[k] - (float)p10[k]) * fx;
+        c[k] = top + (bot - top) * fy;
+      }
+    }
+    if (bgr) { const float t = c[0]; c[0] = c[2]; c[2] = t; }
+  }
+  v0 = (c[0] * (1.f / 255.f) - m0) * is0;
+  v1 = (c[1] * (1.f / 255.f) - m1) * is1;
+  v2 = (c[2] * (1.f / 255.f) - m2) * is2;
+}
+
 __global__ void preprocess_kernel(const uint8_t* __restrict__ in, bf16_t* __restrict__ out,
                                   int B, int Hin, int Win, int Ho, int Wo, int Hp, int Wp,
                                   int pad_t, int pad_l, int Hc, int Wc, int off_t, int off_l,
@@ -27,40 +65,94 @@ __global__ void preprocess_kernel(const uint8_t* __restrict__ in, bf16_t* __rest
     const int yc = yp - pad_t, xc = xp - pad_l;
     uint2 o = {0u, 0u};
     if (yc >= 0 && yc < Hc && xc >= 0 && xc < Wc) {
-      const int yo = yc - off_t, xo = xc - off_l;
-      float c[3] = {fill, fill, fill};
-      if (yo >= 0 && yo < Ho && xo >= 0 && xo < Wo) {
-        if (Hin == Ho && Win == Wo) {
-          const uint8_t* px = in + (((long)b * Hin + yo) * Win + xo) * 3;
-          c[0] = px[0]; c[1] = px[1]; c[2] = px[2];
-        } else {
-          const float sy = fmaxf(((yo + 0.5f) * Hin) / Ho - 0.5f, 0.f);
-          const float sx = fmaxf(((xo + 0.5f) * Win) / Wo - 0.5f, 0.f);
-          int y0 = (int)sy, x0 = (int)sx;
-          y0 = min(y0, Hin - 1); x0 = min(x0, Win - 1);
-          const int y1 = min(y0 + 1, Hin - 1), x1 = min(x0 + 1, Win - 1);
-          const float fy = sy - y0, fx = sx - x0;
-          const uint8_t* base = in + (long)b * Hin * Win * 3;
-          const uint8_t* p00 = base + ((long)y0 * Win + x0) * 3;
-          const uint8_t* p01 = base + ((long)y0 * Win + x1) * 3;
-          const uint8_t* p10 = base + ((long)y1 * Win + x0) * 3;
-          const uint8_t* p11 = base + ((long)y1 * Win + x1) * 3;
-#pragma unroll
-          for (int k = 0; k < 3; ++k) {
-            const float top = p00[k] + (p01[k] - (float)p00[k]) * fx;
-            const float bot = p10[k] + (p11[k] - (float)p10[k]) * fx;
-            c[k] = top + (bot - top) * fy;
-          }
-        }
-        if (bgr) { const float t = c[0]; c[0] = c[2]; c[2] = t; }
-      }
-      const float v0 = (c[0] * (1.f / 255.f) - m0) * is0;
-      const float v1 = (c[1] * (1.f / 255.f) - m1) * is1;
-      const float v2 = (c[2] * (1.f / 255.f) - m2) * is2;
+      float v0, v1, v2;
+      pre_pixel(in, b, Hin, Win, Ho, Wo, off_t, off_l, yc, xc, fill, m0, m1, m2, is0, is1, is2, bgr, v0, v1, v2);
       o.x = pack2(v0, v1);
       o.y = pack2(v2, 0.f);
     }
     *reinterpret_cast<uint2*>(out + idx * 4) = o;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused pre-processing + first conv (YOLOv8's 3x3/2 stem; k <= 4, any stride / pad): uint8
+// frames -> letterbox / normalise (pre_pixel, rounded to bf16 exactly like preprocess_kernel)
+// straight into an LDS tile [IH][IW][4 ch] -> implicit GEMM on v_mfma_f32_16x16x32_bf16 with
+// K = taps x 4 channels (<= 64, zero padded) -> bias + SiLU/ReLU -> bf16 NHWC.  The unfused
+// path paid a bf16 canvas round trip through HBM and a 27 -> 64 padded K over a pixel-run
+// layout; a VALU direct conv was LDS-bound on the weight reads.  Operand roles: A = weights
+// (lane row = output channel), B = pixel patches (lane column = pixel), so each lane ends with
+// 4 consecutive channels of one pixel: 8-byte stores, a wave writes 16 whole pixels.
+// Workgroup = 8 x 32 output pixels; wave w owns rows 2w, 2w+1 (4 tiles of 16 pixels).
+constexpr int kStemTH = 8, kStemTW = 32;
+__global__ __launch_bounds__(256) void stem_direct_kernel(
+    const uint8_t* __restrict__ in, bf16_t* __restrict__ out, const bf16_t* __restrict__ w,
+    const float* __restrict__ bias, int Hin, int Win, int Ho, int Wo, int Hc, int Wc, int off_t, int off_l,
+    float fill, float m0, float m1, float m2, float is0, float is1, float is2, int bgr, int H1, int W1,
+    int Cout, int ldo, int k, int stride, int pad, int act) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t stile[];   // [IH][IW] x (2 dwords = 4 bf16)
+  const int IH = (kStemTH - 1) * stride + k, IW = (kStemTW - 1) * stride + k;
+  const int tid = threadIdx.x, b = blockIdx.z, lane = tid & 63, wave = tid >> 6;
+  const int oy0 = blockIdx.y * kStemTH, ox0 = blockIdx.x * kStemTW;
+  for (int i = tid; i < IH * IW; i += 256) {
+    const int ty = i / IW, tx = i - ty * IW;
+    const int yc = oy0 * stride - pad + ty, xc = ox0 * stride - pad + tx;
+    uint2 o = {0u, 0u};                         // outside the canvas: the conv's zero padding
+    if (yc >= 0 && yc < Hc && xc >= 0 && xc < Wc) {
+      float v0, v1, v2;
+      pre_pixel(in, b, Hin, Win, Ho, Wo, off_t, off_l, yc, xc, fill, m0, m1, m2, is0, is1, is2, bgr, v0, v1, v2);
+      o.x = pack2(v0, v1);
+      o.y = pack2(v2, 0.f);
+    }
+    *reinterpret_cast<uint2*>(stile + 2 * i) = o;
+  }
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  const int taps = k * k;
+  // this lane's two taps per 32-K half: k-piece pc = fq + 4 kk covers taps 2 pc, 2 pc + 1
+  int toff[2][2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int t = 2 * (fq + 4 * kk) + h;
+      toff[kk][h] = t < taps ? (t / k) * IW + (t % k) : -1;
+    }
+  for (int n0 = 0; n0 < Cout; n0 += 16) {
+    bf16x8 wa[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+      wa[kk] = *reinterpret_cast<const bf16x8*>(w + (long)(n0 + fr) * 64 + 8 * (fq + 4 * kk));
+    float cb[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cb[e] = bias ? bias[n0 + 4 * fq + e] : 0.f;
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt) {
+      const int ly = 2 * wave + (pt >> 1), lx = 16 * (pt & 1) + fr;
+      const int base = (ly * stride) * IW + lx * stride;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        uint2 p0 = {0u, 0u}, p1 = {0u, 0u};
+        if (toff[kk][0] >= 0) p0 = *reinterpret_cast<const uint2*>(stile + 2 * (base + toff[kk][0]));
+        if (toff[kk][1] >= 0) p1 = *reinterpret_cast<const uint2*>(stile + 2 * (base + toff[kk][1]));
+        const u32x4 pv = {p0.x, p0.y, p1.x, p1.y};
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[kk], __builtin_bit_cast(bf16x8, pv), acc, 0, 0, 0);
+      }
+      const int oy = oy0 + ly, ox = ox0 + lx;
+      if (oy < H1 && ox < W1) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float a = acc[e] + cb[e];
+          if (act == 1) a = fmaxf(a, 0.f);
+          else if (act == 2) a = a / (1.f + __expf(-a));
+          v[e] = a;
+        }
+        *reinterpret_cast<uint2*>(out + (((long)b * H1 + oy) * W1 + ox) * ldo + n0 + 4 * fq) =
+            make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      }
+    }
   }
 }
 
@@ -293,6 +385,22 @@ extern "C" int aiko_preprocess(const void* in, void* out, int B, int Hin, int Wi
                      static_cast<const uint8_t*>(in), static_cast<aiko::bf16_t*>(out), B, Hin,
                      Win, Ho, Wo, Hp, Wp, pad_t, pad_l, Hc, Wc, off_t, off_l, fill, mean[0],
                      mean[1], mean[2], 1.f / std[0], 1.f / std[1], 1.f / std[2], bgr);
+  return (int)hipGetLastError();
+}
+
+extern "C" int aiko_stem_direct(const void* in, void* out, const void* w, const float* bias, int B, int Hin,
+                                int Win, int Ho, int Wo, int Hc, int Wc, int off_t, int off_l, float fill,
+                                const float* mean, const float* std, int bgr, int H1, int W1, int Cout, int ldo,
+                                int k, int stride, int pad, int act, hipStream_t stream) {
+  if (Cout % 16 || ldo % 4 || k < 1 || k > 4 || stride < 1 || B <= 0) return -1;
+  const int IH = (aiko::kStemTH - 1) * stride + k, IW = (aiko::kStemTW - 1) * stride + k;
+  const size_t lds = (size_t)IH * IW * 8;
+  if (lds > 64 * 1024) return -1;
+  dim3 grid((W1 + aiko::kStemTW - 1) / aiko::kStemTW, (H1 + aiko::kStemTH - 1) / aiko::kStemTH, B);
+  hipLaunchKernelGGL(aiko::stem_direct_kernel, grid, dim3(256), lds, stream, static_cast<const uint8_t*>(in),
+                     static_cast<aiko::bf16_t*>(out), static_cast<const aiko::bf16_t*>(w), bias, Hin, Win, Ho, Wo,
+                     Hc, Wc, off_t, off_l, fill, mean[0], mean[1], mean[2], 1.f / std[0], 1.f / std[1],
+                     1.f / std[2], bgr, H1, W1, Cout, ldo, k, stride, pad, act);
   return (int)hipGetLastError();
 }
 

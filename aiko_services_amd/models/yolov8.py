@@ -143,6 +143,8 @@ class YOLOv8(WeightsMixin):
             cls.append(C.make_conv_spec(wcls, bcls, act=None, device=dev))
             self.heads.append(DetectLevel(box, cls, concat_cout(box[0], cls[0])))
         self._ws: dict = {}
+        self.fused_stem = True            # stem_direct_kernel (letterbox + stem conv fused)
+        self._stem_w = None
         self.ws_tag = ""             # workspace key prefix (one workspace per frame lane)
 
     def _c2f(self, g, cin, cout, n, shortcut):
@@ -217,9 +219,31 @@ class YOLOv8(WeightsMixin):
                                    out=self._buf("input", (B, Hp, Wp, 4)), stem=(3, 2, 1),
                                    canvas=(S, S, top, left, 114.0))
 
-    def head_outputs(self, x: torch.Tensor):
-        """Stem buffer -> per-level head outputs [B, H/s, W/s, 64 + nc] for s = 8, 16, 32."""
-        B = x.shape[0]
+    def stem_from_frames(self, frames: torch.Tensor) -> torch.Tensor:
+        """uint8 [B, H, W, 3] -> the stem conv's output [B, S/2, S/2, c1] in ONE kernel
+        (``stem_direct_kernel``: letterbox + /255 into LDS, direct 3x3/2 conv, bias, SiLU) —
+        no bf16 canvas round trip through HBM, no 27 -> 64 K padding."""
+        B, H, W, _ = frames.shape
+        Ho, Wo, top, left, _ = self.letterbox((H, W))
+        S = self.image_size
+        h0, w0 = C.stem_out_hw(S, S, 3, 2, 1)
+        if self._stem_w is None:          # bf16 [Cout, 64]: k = (r * 3 + s) * 4 + c, from the packed stem
+            l0 = self.l0
+            cc = l0.Cc
+            wp = l0.weight[:, :3 * cc].reshape(l0.cout, 3, cc // 4, 4)[:, :, :3, :]   # [o][r][s][c4]
+            w = torch.zeros(l0.cout, 64, dtype=torch.bfloat16, device=l0.weight.device)
+            w[:, :36] = wp.reshape(l0.cout, 36)
+            self._stem_w = w.contiguous()
+        out = self._buf("a0", (B, h0, w0, self.ch[0]))
+        torch.ops.aiko.stem_direct_out(frames, self._stem_w, self.l0.bias, out,
+                                       [Ho, Wo, S, S, top, left, 3, 2, 1, 2], 114.0,
+                                       list(V.YOLO_MEAN), list(V.YOLO_STD), False)
+        return out
+
+    def head_outputs(self, x: torch.Tensor | None, a0: torch.Tensor | None = None):
+        """Stem buffer (or the stem output ``a0``) -> per-level head outputs
+        [B, H/s, W/s, 64 + nc] for s = 8, 16, 32."""
+        B = (x if a0 is None else a0).shape[0]
         S = self.image_size
         c1, c2, c3, c4, c5 = self.ch
         h0, w0 = C.stem_out_hw(S, S, 3, 2, 1)
@@ -228,7 +252,8 @@ class YOLOv8(WeightsMixin):
             h, w = s[-1]
             s.append(((h - 1) // 2 + 1, (w - 1) // 2 + 1))
         (H1, W1), (H2, W2), (H3, W3), (H4, W4), (H5, W5) = s
-        a0 = C.conv2d(x, self.l0, out=self._buf("a0", (B, H1, W1, c1)), image_hw=(S, S))
+        if a0 is None:
+            a0 = C.conv2d(x, self.l0, out=self._buf("a0", (B, H1, W1, c1)), image_hw=(S, S))
         a1 = C.conv2d(a0, self.l1, out=self._buf("a1", (B, H2, W2, c2)))
         a2 = self._run_c2f("l2", self.l2, a1, self._buf("a2", (B, H2, W2, c2)))
         a3 = C.conv2d(a2, self.l3, out=self._buf("a3", (B, H3, W3, c3)))
@@ -266,6 +291,8 @@ class YOLOv8(WeightsMixin):
 
     def detect(self, frames: torch.Tensor):
         H, W = frames.shape[1:3]
+        if self.fused_stem:
+            return self.postprocess(self.head_outputs(None, a0=self.stem_from_frames(frames)), (H, W))
         return self.postprocess(self.head_outputs(self.preprocess(frames)), (H, W))
 
     __call__ = detect
@@ -278,7 +305,9 @@ class YOLOv8(WeightsMixin):
         return {"scale": self.scale, "num_classes": self.nc, "image_size": self.image_size}
 
     def _weights_loaded(self):
-        """Re-derive each head level's fused box|cls first conv from the loaded layers."""
+        """Re-derive each head level's fused box|cls first conv (and the direct-stem weight)
+        from the loaded layers."""
+        self._stem_w = None
         for lvl in self.heads:
             a, b = lvl.box[0], lvl.cls[0]
             lvl.first.weight[:a.cout].copy_(a.weight)

@@ -111,6 +111,37 @@ def test_topk_nms_matches_reference(native, A, conf, max_cand, max_det):
         assert (det[b, n:, 5] == -1).all()
 
 
+@pytest.mark.parametrize("hw", [(480, 640), (360, 500), (720, 1280)])
+def test_stem_direct_matches_unfused(native, hw):
+    """stem_direct_kernel (letterbox + /255 in LDS, direct 3x3/2 conv, bias, SiLU) equals
+    preprocess + MFMA stem conv (resize and letterbox bars included)."""
+    from aiko_services_amd.models.yolov8 import YOLOv8
+    from aiko_services_amd.ops import conv as C
+    from aiko_services_amd.ops import reference as R
+    m = YOLOv8("n", device=DEV)
+    g = torch.Generator().manual_seed(hw[0])
+    frames = torch.randint(0, 256, (3,) + hw + (3,), generator=g, dtype=torch.uint8).to(DEV)
+    fused = m.stem_from_frames(frames).clone()
+    pre = m.preprocess(frames)
+    unfused = C.conv2d(pre, m.l0, image_hw=(640, 640))
+    assert fused.shape == unfused.shape == (3, 320, 320, 16)
+    assert _rel_err(fused.float(), unfused.float()) < 5e-3
+    canvas = pre[:, 1:641, 1:641, :3].permute(0, 3, 1, 2).float()
+    ref = R.conv_ref(canvas, m.l0)
+    assert _rel_err(fused.permute(0, 3, 1, 2), ref) < 1e-2
+
+
+def test_yolov8n_fused_stem_detect_matches(native):
+    from aiko_services_amd.models.yolov8 import YOLOv8
+    m = YOLOv8("n", device=DEV)
+    frames = torch.randint(0, 256, (2, 480, 640, 3), dtype=torch.uint8, device=DEV)
+    a = [o.clone() for o in m.head_outputs(None, a0=m.stem_from_frames(frames))]
+    b = m.head_outputs(m.preprocess(frames))
+    for x, y in zip(a, b):
+        cos = torch.nn.functional.cosine_similarity(x.float().flatten(), y.float().flatten(), dim=0).item()
+        assert cos > 0.999, cos
+
+
 def test_yolov8n_heads_match_reference(native):
     from aiko_services_amd.models.yolov8 import YOLOv8
     m = YOLOv8("n", device=DEV)
