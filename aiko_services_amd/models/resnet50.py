@@ -97,6 +97,8 @@ class ResNet50(WeightsMixin):
         # Infinity-Cache blocking of the memory-bound early stages (see features_from_stem)
         self.mall_chunk = int(os.environ.get("AIKO_RESNET_MALL_CHUNK", "0"))
         self.mall_blocks = int(os.environ.get("AIKO_RESNET_MALL_BLOCKS", "3"))
+        # conv_chain: identity block's 1x1 expansion + next block's 1x1 reduction in one launch
+        self.chain = os.environ.get("AIKO_RESNET_CHAIN", "1") != "0"
 
     # ---- workspace: every activation buffer allocated once per batch size ----------------
     def _buf(self, key: str, shape, dtype=torch.bfloat16) -> torch.Tensor:
@@ -141,8 +143,9 @@ class ResNet50(WeightsMixin):
             else:
                 st = self._buf(tag + "stem", (B, Ho, Wo, 64))[c0:c0 + ch]
                 xc = V.maxpool2d(C.conv2d(xc, self.stem, out=st, image_hw=(S, S)), 3, 2, 1, out=pool[c0:c0 + ch])
+            t1 = None
             for bi in range(nb):
-                xc = self._block(bi, xc, tag, B, c0, ch)
+                xc, t1 = self._block(bi, xc, tag, B, c0, ch, t1, chain=bi + 1 < nb)
             xs.append(xc)
         if len(xs) == 1:
             x = xs[0]
@@ -152,28 +155,40 @@ class ResNet50(WeightsMixin):
             x = self._buf(tag + ("xa" if (nb - 1) % 2 == 0 else "xb"), (B,) + tuple(xs[0].shape[1:]))
         if after_block is not None and after_block[0] < nb:
             after_block[1]()
+        t1 = None
         for bi in range(nb, len(self.blocks)):
-            x = self._block(bi, x, tag, B, 0, B)
+            x, t1 = self._block(bi, x, tag, B, 0, B, t1)
             if after_block is not None and after_block[0] == bi:
                 after_block[1]()
         return V.avgpool(x, out=self._buf(tag + "gap", (B, x.shape[3])))
 
-    def _block(self, bi: int, x: torch.Tensor, tag: str, B: int, c0: int, ch: int) -> torch.Tensor:
-        """Bottleneck ``bi`` on frames c0 .. c0+ch of the batch (slices of [B, ...] buffers)."""
+    def _block(self, bi: int, x: torch.Tensor, tag: str, B: int, c0: int, ch: int,
+               t1: torch.Tensor | None = None, chain: bool = True):
+        """Bottleneck ``bi`` on frames c0 .. c0+ch of the batch (slices of [B, ...] buffers).
+        ``t1``: this block's conv1 output when the previous block already produced it.
+        Returns (output, next block's conv1 output or None): an identity block whose expansion
+        conv3 feeds a 1x1 reduction runs both as one ``conv_chain`` launch."""
         blk = self.blocks[bi]
         H, W = x.shape[1], x.shape[2]
         sl = slice(c0, c0 + ch)
-        t1 = C.conv2d(x, blk.conv1, out=self._buf(tag + "t1", (B, H, W, blk.conv1.cout))[sl])
+        if t1 is None:
+            t1 = C.conv2d(x, blk.conv1, out=self._buf(tag + "t1", (B, H, W, blk.conv1.cout))[sl])
         Ho, Wo = blk.conv2.out_hw(H, W)
         t2 = C.conv2d(t1, blk.conv2, out=self._buf(tag + "t2", (B, Ho, Wo, blk.conv2.cout))[sl])
         key = "xa" if bi % 2 == 0 else "xb"
         out = self._buf(tag + key, (B, Ho, Wo, blk.conv3.cout))[sl]
         if blk.fused is not None and self.fuse_shortcut:
-            return C.conv2d(t2, blk.fused, x2=x, out=out)
+            return C.conv2d(t2, blk.fused, x2=x, out=out), None
         if blk.down is not None:
             idn = C.conv2d(x, blk.down, out=self._buf(tag + "ds", (B, Ho, Wo, blk.down.cout))[sl])
-            return C.conv2d(t2, blk.conv3, residual=idn, out=out)
-        return C.conv2d(t2, blk.conv3, residual=x, out=out)
+            return C.conv2d(t2, blk.conv3, residual=idn, out=out), None
+        nxt = self.blocks[bi + 1] if bi + 1 < len(self.blocks) else None
+        if (chain and self.chain and nxt is not None and C.chain_ok(blk.conv3, nxt.conv1)
+                and (ch * Ho * Wo) % 64 == 0 and x.is_contiguous()):
+            t1n = self._buf(tag + "t1", (B, Ho, Wo, nxt.conv1.cout))[sl]
+            C.conv_chain(t2, blk.conv3, x, out, nxt.conv1, t1n)
+            return out, t1n
+        return C.conv2d(t2, blk.conv3, residual=x, out=out), None
 
     def _lanes(self, n: int) -> list:
         lanes = getattr(self, "_lane_streams", None)

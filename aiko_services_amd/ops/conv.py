@@ -390,3 +390,33 @@ def linear(x: torch.Tensor, spec: ConvSpec, out: torch.Tensor | None = None,
             0 if residual is None else residual.stride(0), bm, bn, spec.K, 1, 1, 8, 1]
     torch.ops.aiko.conv_igemm_out(x, None, spec.weight, spec.bias, residual, out, geom)
     return out
+
+
+CHAIN_STAGE2 = False
+
+
+def chain_ok(spec3: ConvSpec, spec1: ConvSpec) -> bool:
+    """Can ``spec3`` (1x1 expansion, identity residual) and the next block's ``spec1`` (1x1
+    reduction) run as one ``conv_chain`` launch?"""
+    def one_by_one(s):
+        return s.kind == "conv" and s.R == 1 and s.S == 1 and s.stride == 1 and s.K1 is None and s.bias is not None
+    # (K1, N1) -> allowed N2.  The stage-2 shapes (128, 512) -> 128 | 256 are implemented and
+    # tested but spill at 512 threads (128-VGPR cap): 377 / 519 us against 151 / 200 us for
+    # the two unchained convs, so they are opt-in (CHAIN_STAGE2) until that is fixed.
+    shapes = {(64, 256): (64, 128)}
+    if CHAIN_STAGE2:
+        shapes[(128, 512)] = (128, 256)
+    k1, n1 = spec3.weight.shape[1], spec3.weight.shape[0]
+    return (one_by_one(spec3) and one_by_one(spec1) and spec3.cin == k1 and (k1, n1) in shapes
+            and spec1.cin == n1 and spec1.weight.shape[1] == n1 and spec1.cout in shapes[(k1, n1)]
+            and spec3.act == ACT_RELU and spec1.act == ACT_RELU)
+
+
+def conv_chain(x: torch.Tensor, spec3: ConvSpec, residual: torch.Tensor, out_y: torch.Tensor,
+               spec1: ConvSpec, out_z: torch.Tensor, grid: int = 0):
+    """``out_y = relu(conv1x1(x, spec3) + residual)``, ``out_z = relu(conv1x1(out_y, spec1))`` in
+    one kernel (``conv_chain.hip``): the 256-channel ``out_y`` is written once and never read
+    back.  All NHWC, contiguous."""
+    torch.ops.aiko.conv_chain_out(x, spec3.weight, spec3.bias, residual, out_y, spec1.weight, spec1.bias,
+                                  out_z, grid)
+    return out_y, out_z

@@ -165,3 +165,42 @@ def test_resnet50_mall_chunking_matches(native, chunk, blocks):
     m.mall_chunk, m.mall_blocks = chunk, blocks
     got = m.logits(frames).clone()
     assert torch.equal(got, ref) or ((got.float() - ref.float()).abs().max() < 1e-2 * ref.float().abs().max())
+
+
+@pytest.mark.parametrize("k1,n1,n2", [(64, 256, 64), (64, 256, 128), (128, 512, 128), (128, 512, 256)])
+def test_conv_chain_matches_two_convs(native, k1, n1, n2):
+    """conv_chain (1x1 expand + residual + ReLU -> 1x1 reduce + ReLU in one kernel) equals the two
+    separate igemm convs and the fp32 reference."""
+    from aiko_services_amd.ops import conv as C
+    g = torch.Generator().manual_seed(n2 + k1)
+    spec3 = C.make_conv_spec(torch.randn(n1, k1, 1, 1, generator=g) / k1 ** 0.5, 0.1 * torch.randn(n1, generator=g),
+                             act="relu", device="cuda")
+    spec1 = C.make_conv_spec(torch.randn(n2, n1, 1, 1, generator=g) / n1 ** 0.5, 0.1 * torch.randn(n2, generator=g),
+                             act="relu", device="cuda")
+    assert C.chain_ok(spec3, spec1) == (k1 == 64 or C.CHAIN_STAGE2)
+    B, H, W = 3, 28, 32                                      # M = 2688 = 42 tiles of 64
+    x = torch.randn(B, H, W, k1, generator=g).to("cuda", torch.bfloat16)
+    r = torch.randn(B, H, W, n1, generator=g).to("cuda", torch.bfloat16)
+    y = torch.empty(B, H, W, n1, dtype=torch.bfloat16, device="cuda")
+    z = torch.empty(B, H, W, n2, dtype=torch.bfloat16, device="cuda")
+    for grid in (0, 5):                                      # persistent loop over several tiles
+        C.conv_chain(x, spec3, r, y, spec1, z, grid=grid)
+        y2 = C.conv2d(x, spec3, residual=r)
+        z2 = C.conv2d(y2, spec1)
+        assert ((y.float() - y2.float()).abs() > 0.02 * (1 + y2.float().abs())).float().mean() < 1e-3
+        assert ((z.float() - z2.float()).abs().max() / z2.float().abs().max()) < 2e-2
+        yr = torch.relu(x.float() @ spec3.ref_weight[:, :, 0, 0].T.cuda() + spec3.ref_bias.cuda() + r.float())
+        assert ((y.float() - yr).norm() / yr.norm()).item() < 1e-2
+
+
+def test_resnet50_chain_matches_unchained(native):
+    from aiko_services_amd.models.resnet50 import ResNet50
+    g = torch.Generator().manual_seed(6)
+    frames = torch.randint(0, 256, (16, 224, 224, 3), generator=g, dtype=torch.uint8).to("cuda")
+    m = ResNet50(device="cuda")
+    m.chain = False
+    ref = m.logits(frames).float().clone()
+    m.chain = True
+    got = m.logits(frames).float()
+    cos = torch.nn.functional.cosine_similarity(got.flatten(), ref.flatten(), dim=0).item()
+    assert cos > 0.999, cos
