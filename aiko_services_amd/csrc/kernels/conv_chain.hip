@@ -77,6 +77,7 @@ __global__ __launch_bounds__(512, (N1 <= 256 ? 2 : 1)) void conv_chain_kernel(
         w1f[j][ks] = *reinterpret_cast<const bf16x8*>(W1 + (long)(N1 / 8 * wave + 16 * j + fr) * K1 + 32 * ks + 8 * fq);
   };
   if constexpr (W1_RESIDENT) load_w1();
+  (void)load_w1;
   float bias1[J1];
 #pragma unroll
   for (int j = 0; j < J1; ++j) bias1[j] = b1[N1 / 8 * wave + 16 * j + fr];
@@ -120,21 +121,38 @@ __global__ __launch_bounds__(512, (N1 <= 256 ? 2 : 1)) void conv_chain_kernel(
     if (next < ntiles) load_tile(next);        // in flight during this tile's compute
     // ---- 1. GEMM1: rows 16 i + (4 fq + e), cols N1/8 wave + 16 j + fr
     {
-      if constexpr (!W1_RESIDENT) load_w1();
       f32x4 acc[4][J1];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < J1; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (W1_RESIDENT) {
 #pragma unroll
-      for (int ks = 0; ks < KS1; ++ks)
+        for (int ks = 0; ks < KS1; ++ks)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const bf16x8 af = *reinterpret_cast<const bf16x8*>(As + sw_off(16 * i + fr, 4 * ks + fq, ARB, AMASK));
+          for (int i = 0; i < 4; ++i) {
+            const bf16x8 af = *reinterpret_cast<const bf16x8*>(As + sw_off(16 * i + fr, 4 * ks + fq, ARB, AMASK));
+#pragma unroll
+            for (int j = 0; j < J1; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, w1f[j][ks], acc[i][j], 0, 0, 0);
+          }
+      } else {
+        // one k-step of weight fragments live at a time (L2-resident weights), bounded registers
+#pragma unroll 1
+        for (int ks = 0; ks < KS1; ++ks) {
+          bf16x8 wk[J1];
 #pragma unroll
           for (int j = 0; j < J1; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, w1f[j][ks], acc[i][j], 0, 0, 0);
+            wk[j] = *reinterpret_cast<const bf16x8*>(W1 + (long)(N1 / 8 * wave + 16 * j + fr) * K1 + 32 * ks + 8 * fq);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const bf16x8 af = *reinterpret_cast<const bf16x8*>(As + sw_off(16 * i + fr, 4 * ks + fq, ARB, AMASK));
+#pragma unroll
+            for (int j = 0; j < J1; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wk[j], acc[i][j], 0, 0, 0);
+          }
         }
+      }
       // ---- 2. Y = relu(acc + b1 + R) in place of R
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -166,8 +184,7 @@ __global__ __launch_bounds__(512, (N1 <= 256 ? 2 : 1)) void conv_chain_kernel(
     for (int j = 0; j < J2; ++j)
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc2[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int k4 = 0; k4 < KS2; k4 += 4) {        // 4 k-steps of W2 fragments in flight
+    auto gemm2_step = [&](int k4) {        // 4 k-steps of W2 fragments in flight
       bf16x8 w2f[J2][4];
 #pragma unroll
       for (int j = 0; j < J2; ++j)
@@ -186,6 +203,13 @@ __global__ __launch_bounds__(512, (N1 <= 256 ? 2 : 1)) void conv_chain_kernel(
             acc2[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, w2f[j][u], acc2[j][i], 0, 0, 0);
         }
       }
+    };
+    if constexpr (N1 <= 256) {                   // stage 1: fully unrolled (no spills at 2 waves/SIMD)
+#pragma unroll
+      for (int k4 = 0; k4 < KS2; k4 += 4) gemm2_step(k4);
+    } else {                                     // stage 2: bounded live registers
+#pragma unroll 1
+      for (int k4 = 0; k4 < KS2; k4 += 4) gemm2_step(k4);
     }
     if constexpr (KH > 1) {
       if (kh == 1) {

@@ -392,7 +392,7 @@ def linear(x: torch.Tensor, spec: ConvSpec, out: torch.Tensor | None = None,
     return out
 
 
-CHAIN_STAGE2 = False
+CHAIN_STAGE2 = __import__("os").environ.get("AIKO_CHAIN_STAGE2", "0") == "1"
 
 
 def chain_ok(spec3: ConvSpec, spec1: ConvSpec) -> bool:
