@@ -39,7 +39,8 @@ int aiko_stem_direct(const void* in, void* out, const void* w, const float* bias
                      const float* std, int bgr, int H1, int W1, int Cout, int ldo, int k, int stride, int pad,
                      int act, hipStream_t stream);
 int aiko_conv_chain(const void* A, const void* W1, const float* b1, const void* R, void* Y, const void* W2,
-                    const float* b2, void* Z, int M, int K1, int N1, int N2, int grid, hipStream_t stream);
+                    const float* b2, void* Z, const void* A2, int M, int K1, int N1, int N2, int grid,
+                    hipStream_t stream);
 int aiko_maxpool(const void* x, void* y, int B, int H, int W, int C, int Ho, int Wo, int k,
                  int s, int p, int ldx, int ldy, hipStream_t stream);
 int aiko_resize_u8(const void* in, void* out, int B, int Hin, int Win, int Ho, int Wo, hipStream_t stream);
@@ -240,8 +241,13 @@ int64_t pixel_pitch(const at::Tensor& t, const char* op);
 // Chained 1x1 convs at a bottleneck boundary (conv_chain.hip):
 //   Y = relu(A W1^T + b1 + R) [M, N1],  Z = relu(Y W2^T + b2) [M, N2]
 //   (K1, N1, N2) in {(64, 256, 64), (64, 256, 128), (128, 512, 128), (128, 512, 256)}
-void conv_chain_out(const at::Tensor& A, const at::Tensor& W1, const at::Tensor& b1, const at::Tensor& R,
-                    at::Tensor& Y, const at::Tensor& W2, const at::Tensor& b2, at::Tensor& Z, int64_t grid) {
+void conv_chain_out(const at::Tensor& A, const at::Tensor& W1, const at::Tensor& b1, const c10::optional<at::Tensor>& R_opt,
+                    at::Tensor& Y, const at::Tensor& W2, const at::Tensor& b2, at::Tensor& Z, int64_t grid,
+                    const c10::optional<at::Tensor>& A2_opt) {
+  const bool dual = A2_opt.has_value() && A2_opt->defined();
+  TORCH_CHECK(dual != (R_opt.has_value() && R_opt->defined()),
+              "aiko.conv_chain_out: exactly one of R (identity residual) and A2 (fused projection shortcut)");
+  const at::Tensor& R = dual ? *A2_opt : *R_opt;   // (validated by the dual branch below when dual)
   for (const at::Tensor* t : {&A, &W1, &b1, &R, (const at::Tensor*)&Y, &W2, &b2, (const at::Tensor*)&Z}) {
     check_cuda(*t, "conv_chain operand");
     TORCH_CHECK(t->is_contiguous() && reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
@@ -252,18 +258,25 @@ void conv_chain_out(const at::Tensor& A, const at::Tensor& W1, const at::Tensor&
   TORCH_CHECK(b1.scalar_type() == at::kFloat && b2.scalar_type() == at::kFloat, "aiko.conv_chain_out: fp32 biases");
   TORCH_CHECK(W1.dim() == 2 && W2.dim() == 2, "aiko.conv_chain_out: W1 / W2 [Cout, K]");
   const int64_t N1 = W1.size(0), K1 = W1.size(1), N2 = W2.size(0);
-  const bool shape_ok = (K1 == 64 && N1 == 256 && (N2 == 64 || N2 == 128)) ||
-                        (K1 == 128 && N1 == 512 && (N2 == 128 || N2 == 256));
-  TORCH_CHECK(shape_ok, "aiko.conv_chain_out: unsupported (K1, N1, N2) = (", K1, ", ", N1, ", ", N2, ")");
-  const int64_t M = A.numel() / K1;
-  TORCH_CHECK(A.size(-1) == K1 && b1.numel() == N1 && W2.size(1) == N1 && b2.numel() == N2,
-              "aiko.conv_chain_out: A [.., K1], b1 [N1], W2 [N2, N1], b2 [N2]");
-  TORCH_CHECK(R.numel() == M * N1 && Y.numel() == M * N1 && R.size(-1) == N1 && Y.size(-1) == N1 &&
-                  Z.numel() == M * N2 && Z.size(-1) == N2,
-              "aiko.conv_chain_out: R / Y [M, N1], Z [M, N2]");
+  const bool shape_ok = dual ? (K1 == 128 && N1 == 256 && N2 == 64)
+                             : ((K1 == 64 && N1 == 256 && (N2 == 64 || N2 == 128)) ||
+                                (K1 == 128 && N1 == 512 && (N2 == 128 || N2 == 256)));
+  TORCH_CHECK(shape_ok, "aiko.conv_chain_out: unsupported (K1, N1, N2) = (", K1, ", ", N1, ", ", N2, ")", dual ? " dual" : "");
+  const int64_t ka = dual ? K1 / 2 : K1;           // width of each A source
+  const int64_t M = A.numel() / ka;
+  TORCH_CHECK(A.size(-1) == ka && b1.numel() == N1 && W2.size(1) == N1 && b2.numel() == N2,
+              "aiko.conv_chain_out: A [.., K1 (or K1/2 per source)], b1 [N1], W2 [N2, N1], b2 [N2]");
+  if (dual) {
+    TORCH_CHECK(R.numel() == M * ka && R.size(-1) == ka, "aiko.conv_chain_out: A2 [M, K1/2]");
+  } else {
+    TORCH_CHECK(R.numel() == M * N1 && R.size(-1) == N1, "aiko.conv_chain_out: R [M, N1]");
+  }
+  TORCH_CHECK(Y.numel() == M * N1 && Y.size(-1) == N1 && Z.numel() == M * N2 && Z.size(-1) == N2,
+              "aiko.conv_chain_out: Y [M, N1], Z [M, N2]");
   TORCH_CHECK(M % 64 == 0, "aiko.conv_chain_out: M must be a multiple of 64");
-  check_launch(aiko_conv_chain(A.data_ptr(), W1.data_ptr(), b1.data_ptr<float>(), R.data_ptr(), Y.data_ptr(),
-                               W2.data_ptr(), b2.data_ptr<float>(), Z.data_ptr(), M, K1, N1, N2, grid, cur_stream()),
+  check_launch(aiko_conv_chain(A.data_ptr(), W1.data_ptr(), b1.data_ptr<float>(), dual ? nullptr : R.data_ptr(),
+                               Y.data_ptr(), W2.data_ptr(), b2.data_ptr<float>(), Z.data_ptr(),
+                               dual ? R.data_ptr() : nullptr, M, K1, N1, N2, grid, cur_stream()),
                "conv_chain");
 }
 
@@ -836,7 +849,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("yolo_decode_out(Tensor[] feats, int[] strides, int nc, int reg_max, Tensor(a!) boxes, Tensor(b!) scores, Tensor(c!) cls) -> ()");
   m.def("topk_nms_out(Tensor boxes, Tensor scores, Tensor cls, int max_cand, float[] params, Tensor(a!) det, Tensor(b!) count) -> ()");
   m.def("stem_direct_out(Tensor frames, Tensor w, Tensor? bias, Tensor(a!) out, int[] geom, float fill, float[] mean, float[] std, bool bgr) -> ()");
-  m.def("conv_chain_out(Tensor A, Tensor W1, Tensor b1, Tensor R, Tensor(a!) Y, Tensor W2, Tensor b2, Tensor(b!) Z, int grid=0) -> ()");
+  m.def("conv_chain_out(Tensor A, Tensor W1, Tensor b1, Tensor? R, Tensor(a!) Y, Tensor W2, Tensor b2, Tensor(b!) Z, int grid=0, Tensor? A2=None) -> ()");
   m.def("maxpool_out(Tensor x, Tensor(a!) y, int k, int s, int p) -> ()");
   m.def("avgpool_out(Tensor x, Tensor(a!) y) -> ()");
   m.def("stem_pool_out(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, int Ho, int Wo, int variant=0) -> ()");

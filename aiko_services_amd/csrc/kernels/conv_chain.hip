@@ -39,9 +39,12 @@ __device__ __forceinline__ int sw_off(int row, int chunk, int rb, int mask) {
 
 // K1 -> N1 expansion (+ residual), then N1 -> N2 reduction; stage 1: (64, 256, 64 | 128),
 // stage 2: (128, 512, 128 | 256).
-template <int K1, int N1, int N2>
+// DUAL: the expansion is a block's first conv3 with its 1x1 projection shortcut fused by
+// K-concatenation (A = [t2 | x], K1 = 64 + 64, no residual term), as in ops.conv.fuse_shortcut.
+template <int K1, int N1, int N2, bool DUAL = false>
 __global__ __launch_bounds__(512, (N1 <= 256 ? 2 : 1)) void conv_chain_kernel(
-    const bf16_t* __restrict__ A, const bf16_t* __restrict__ W1, const float* __restrict__ b1,
+    const bf16_t* __restrict__ A, const bf16_t* __restrict__ A2, const bf16_t* __restrict__ W1,
+    const float* __restrict__ b1,
     const bf16_t* __restrict__ R, bf16_t* __restrict__ Y, const bf16_t* __restrict__ W2,
     const float* __restrict__ b2, bf16_t* __restrict__ Z, int M) {
   using namespace chain;
@@ -67,7 +70,7 @@ __global__ __launch_bounds__(512, (N1 <= 256 ? 2 : 1)) void conv_chain_kernel(
 
   // W1 fragments for this wave's N1/8 columns: kept in registers for the whole kernel when they
   // are few (stage 1: 16 VGPRs); stage 2's 64 would spill, so they are re-read from L2 per tile
-  constexpr bool W1_RESIDENT = J1 * KS1 <= 4;
+  constexpr bool W1_RESIDENT = J1 * KS1 <= 8;
   bf16x8 w1f[J1][KS1];
   auto load_w1 = [&]() {
 #pragma unroll
@@ -88,12 +91,18 @@ __global__ __launch_bounds__(512, (N1 <= 256 ? 2 : 1)) void conv_chain_kernel(
 #pragma unroll
     for (int i = 0; i < APT; ++i) {
       const int c = tid + NT * i;
-      ra[i] = *reinterpret_cast<const u32x4*>(A + (m0 + c / ACH) * K1 + (c % ACH) * 8);
+      if constexpr (DUAL) {                    // chunks 0..7 from t2, 8..15 from the block input
+        const int ch = c % ACH;
+        ra[i] = ch < ACH / 2 ? *reinterpret_cast<const u32x4*>(A + (m0 + c / ACH) * (K1 / 2) + ch * 8)
+                             : *reinterpret_cast<const u32x4*>(A2 + (m0 + c / ACH) * (K1 / 2) + (ch - ACH / 2) * 8);
+      } else {
+        ra[i] = *reinterpret_cast<const u32x4*>(A + (m0 + c / ACH) * K1 + (c % ACH) * 8);
+      }
     }
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
       const int c = tid + NT * i;
-      rr[i] = *reinterpret_cast<const u32x4*>(R + (m0 + c / YCH) * N1 + (c % YCH) * 8);
+      if constexpr (!DUAL) rr[i] = *reinterpret_cast<const u32x4*>(R + (m0 + c / YCH) * N1 + (c % YCH) * 8);
     }
   };
   auto store_tile_lds = [&]() {
@@ -105,7 +114,7 @@ __global__ __launch_bounds__(512, (N1 <= 256 ? 2 : 1)) void conv_chain_kernel(
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
       const int c = tid + NT * i;
-      *reinterpret_cast<u32x4*>(Ys + sw_off(c / YCH, c % YCH, YRB, YMASK)) = rr[i];
+      if constexpr (!DUAL) *reinterpret_cast<u32x4*>(Ys + sw_off(c / YCH, c % YCH, YRB, YMASK)) = rr[i];
     }
   };
 
@@ -163,7 +172,7 @@ __global__ __launch_bounds__(512, (N1 <= 256 ? 2 : 1)) void conv_chain_kernel(
           for (int e = 0; e < 4; ++e) {
             const int row = 16 * i + 4 * fq + e;
             bf16_t* p = reinterpret_cast<bf16_t*>(Ys + sw_off(row, col >> 3, YRB, YMASK)) + (col & 7);
-            *p = f2bf(fmaxf(acc[i][j][e] + bias1[j] + bf2f(*p), 0.f));
+            *p = f2bf(fmaxf(acc[i][j][e] + bias1[j] + (DUAL ? 0.f : bf2f(*p)), 0.f));
           }
         }
     }
@@ -247,7 +256,7 @@ __global__ __launch_bounds__(512, (N1 <= 256 ? 2 : 1)) void conv_chain_kernel(
 }  // namespace aiko
 
 extern "C" int aiko_conv_chain(const void* A, const void* W1, const float* b1, const void* R, void* Y,
-                               const void* W2, const float* b2, void* Z, int M, int K1, int N1, int N2,
+                               const void* W2, const float* b2, void* Z, const void* A2, int M, int K1, int N1, int N2,
                                int grid, hipStream_t stream) {
   using namespace aiko;
   if (M <= 0 || M % chain::BM) return -1;
@@ -262,8 +271,8 @@ extern "C" int aiko_conv_chain(const void* A, const void* W1, const float* b1, c
   auto w2 = static_cast<const bf16_t*>(W2);
   auto z = static_cast<bf16_t*>(Z);
 #define AIKO_CHAIN(k1, n1, n2)                                                                           \
-  if (K1 == k1 && N1 == n1 && N2 == n2) {                                                               \
-    hipLaunchKernelGGL((conv_chain_kernel<k1, n1, n2>), dim3(grid), dim3(chain::NT), 0, stream, a, w1, b1, r, y, \
+  if (!A2 && K1 == k1 && N1 == n1 && N2 == n2) {                                                               \
+    hipLaunchKernelGGL((conv_chain_kernel<k1, n1, n2>), dim3(grid), dim3(chain::NT), 0, stream, a, nullptr, w1, b1, r, y, \
                        w2, b2, z, M);                                                                   \
     return (int)hipGetLastError();                                                                      \
   }
@@ -271,6 +280,11 @@ extern "C" int aiko_conv_chain(const void* A, const void* W1, const float* b1, c
   AIKO_CHAIN(64, 256, 128)
   AIKO_CHAIN(128, 512, 128)
   AIKO_CHAIN(128, 512, 256)
+  if (A2 && K1 == 128 && N1 == 256 && N2 == 64) {
+    hipLaunchKernelGGL((conv_chain_kernel<128, 256, 64, true>), dim3(grid), dim3(chain::NT), 0, stream, a,
+                       static_cast<const bf16_t*>(A2), w1, b1, r, y, w2, b2, z, M);
+    return (int)hipGetLastError();
+  }
 #undef AIKO_CHAIN
   return -1;
 }

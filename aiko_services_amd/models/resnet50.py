@@ -177,12 +177,17 @@ class ResNet50(WeightsMixin):
         t2 = C.conv2d(t1, blk.conv2, out=self._buf(tag + "t2", (B, Ho, Wo, blk.conv2.cout))[sl])
         key = "xa" if bi % 2 == 0 else "xb"
         out = self._buf(tag + key, (B, Ho, Wo, blk.conv3.cout))[sl]
+        nxt = self.blocks[bi + 1] if bi + 1 < len(self.blocks) else None
         if blk.fused is not None and self.fuse_shortcut:
+            if (chain and self.chain and nxt is not None and C.chain_dual_ok(blk.fused, nxt.conv1)
+                    and (ch * Ho * Wo) % 64 == 0 and x.is_contiguous() and (H, W) == (Ho, Wo)):
+                t1n = self._buf(tag + "t1", (B, Ho, Wo, nxt.conv1.cout))[sl]
+                C.conv_chain(t2, blk.fused, None, out, nxt.conv1, t1n, x2=x)
+                return out, t1n
             return C.conv2d(t2, blk.fused, x2=x, out=out), None
         if blk.down is not None:
             idn = C.conv2d(x, blk.down, out=self._buf(tag + "ds", (B, Ho, Wo, blk.down.cout))[sl])
             return C.conv2d(t2, blk.conv3, residual=idn, out=out), None
-        nxt = self.blocks[bi + 1] if bi + 1 < len(self.blocks) else None
         if (chain and self.chain and nxt is not None and C.chain_ok(blk.conv3, nxt.conv1)
                 and (ch * Ho * Wo) % 64 == 0 and x.is_contiguous()):
             t1n = self._buf(tag + "t1", (B, Ho, Wo, nxt.conv1.cout))[sl]

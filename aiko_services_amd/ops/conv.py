@@ -412,11 +412,21 @@ def chain_ok(spec3: ConvSpec, spec1: ConvSpec) -> bool:
             and spec3.act == ACT_RELU and spec1.act == ACT_RELU)
 
 
-def conv_chain(x: torch.Tensor, spec3: ConvSpec, residual: torch.Tensor, out_y: torch.Tensor,
-               spec1: ConvSpec, out_z: torch.Tensor, grid: int = 0):
+def chain_dual_ok(fused: ConvSpec, spec1: ConvSpec) -> bool:
+    """A block's first conv3 with its fused 1x1 stride-1 projection shortcut (K = 64 + 64 -> 256)
+    followed by the next block's 1x1 reduction to 64 channels."""
+    return (fused.K1 == 64 and fused.stride2 == 1 and fused.weight.shape == (256, 128) and fused.R == 1
+            and fused.S == 1 and fused.stride == 1 and fused.bias is not None and fused.act == ACT_RELU
+            and spec1.kind == "conv" and spec1.R == 1 and spec1.S == 1 and spec1.stride == 1 and spec1.K1 is None
+            and spec1.weight.shape == (64, 256) and spec1.bias is not None and spec1.act == ACT_RELU)
+
+
+def conv_chain(x: torch.Tensor, spec3: ConvSpec, residual: torch.Tensor | None, out_y: torch.Tensor,
+               spec1: ConvSpec, out_z: torch.Tensor, grid: int = 0, x2: torch.Tensor | None = None):
     """``out_y = relu(conv1x1(x, spec3) + residual)``, ``out_z = relu(conv1x1(out_y, spec1))`` in
     one kernel (``conv_chain.hip``): the 256-channel ``out_y`` is written once and never read
-    back.  All NHWC, contiguous."""
+    back.  All NHWC, contiguous.  With ``x2`` (and no residual) ``spec3`` is a fused-shortcut
+    spec (:func:`chain_dual_ok`): ``out_y = relu([x | x2] . W^T + b)``."""
     torch.ops.aiko.conv_chain_out(x, spec3.weight, spec3.bias, residual, out_y, spec1.weight, spec1.bias,
-                                  out_z, grid)
+                                  out_z, grid, x2)
     return out_y, out_z

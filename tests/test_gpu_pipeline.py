@@ -193,6 +193,27 @@ def test_conv_chain_matches_two_convs(native, k1, n1, n2):
         assert ((y.float() - yr).norm() / yr.norm()).item() < 1e-2
 
 
+def test_conv_chain_dual_matches_fused_conv(native):
+    """Dual-source chain: [t2 | x] with the fused projection-shortcut weight (block 0 of stage 1)
+    -> next block's reduction; equals conv2d(x2=...) followed by the 1x1 conv."""
+    from aiko_services_amd.ops import conv as C
+    from aiko_services_amd.models.resnet50 import ResNet50
+    m = ResNet50(device="cuda")
+    fused, nxt = m.blocks[0].fused, m.blocks[1].conv1
+    assert C.chain_dual_ok(fused, nxt)
+    g = torch.Generator().manual_seed(3)
+    B, H, W = 2, 56, 56
+    t2 = torch.randn(B, H, W, 64, generator=g).to("cuda", torch.bfloat16)
+    x = torch.randn(B, H, W, 64, generator=g).to("cuda", torch.bfloat16)
+    y = torch.empty(B, H, W, 256, dtype=torch.bfloat16, device="cuda")
+    z = torch.empty(B, H, W, 64, dtype=torch.bfloat16, device="cuda")
+    C.conv_chain(t2, fused, None, y, nxt, z, x2=x)
+    y2 = C.conv2d(t2, fused, x2=x)
+    z2 = C.conv2d(y2, nxt)
+    assert ((y.float() - y2.float()).norm() / y2.float().norm()).item() < 5e-3
+    assert ((z.float() - z2.float()).norm() / z2.float().norm()).item() < 1e-2
+
+
 def test_resnet50_chain_matches_unchained(native):
     from aiko_services_amd.models.resnet50 import ResNet50
     g = torch.Generator().manual_seed(6)
