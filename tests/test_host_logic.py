@@ -1,0 +1,51 @@
+"""Host-side decision logic of the GPU paths (no GPU needed): which ResNet-50 block boundaries
+the chained 1x1 kernel takes, Whisper token -> text rendering and the reference's speech reply
+filter, the decode-attention workspace size."""
+import torch
+
+from aiko_services_amd.ops import conv as C
+
+
+def _resnet_specs():
+    """ResNet-50 bottleneck conv specs (CPU), as models/resnet50.py builds them."""
+    g = torch.Generator().manual_seed(0)
+
+    def conv(cout, cin, k, stride=1, act="relu"):
+        return C.make_conv_spec(torch.randn(cout, cin, k, k, generator=g), torch.randn(cout, generator=g),
+                                stride=stride, pad=k // 2, act=act)
+    return conv
+
+
+def test_chain_ok_shapes():
+    conv = _resnet_specs()
+    exp1, red1 = conv(256, 64, 1), conv(64, 256, 1)
+    assert C.chain_ok(exp1, red1)                                    # stage-1 identity boundary
+    assert C.chain_ok(exp1, conv(128, 256, 1))                       # stage-1 -> stage-2 entry
+    assert not C.chain_ok(exp1, conv(64, 256, 3))                    # 3x3 next conv
+    assert not C.chain_ok(conv(256, 64, 1, act="silu"), red1)        # non-ReLU epilogue
+    assert C.chain_ok(conv(512, 128, 1), conv(128, 512, 1)) == C.CHAIN_STAGE2
+    assert not C.chain_ok(conv(1024, 256, 1), conv(256, 1024, 1))    # stage 3: never
+
+
+def test_chain_dual_ok_requires_stride1_shortcut():
+    conv = _resnet_specs()
+    fused = C.fuse_shortcut(conv(256, 64, 1), conv(256, 64, 1))
+    assert C.chain_dual_ok(fused, conv(64, 256, 1))
+    assert not C.chain_dual_ok(fused, conv(128, 256, 1))
+    strided = C.fuse_shortcut(conv(512, 128, 1), conv(512, 256, 1, stride=2))
+    assert not C.chain_dual_ok(strided, conv(128, 512, 1))
+
+
+def test_whisper_text_rendering_and_reply_filter():
+    from aiko_services_amd.elements.gpu.speech import _reply
+    from aiko_services_amd.models.whisper_decoder import EOT, SOT_SEQUENCE, attn_decode_work, decode_text
+    rows = [list(SOT_SEQUENCE) + [10, 20, EOT, 30], list(SOT_SEQUENCE) + [EOT] * 3]
+    assert decode_text(rows) == ["<10> <20>", ""]
+
+    class Tok:
+        def decode(self, ids):
+            return " " + "".join(chr(97 + i % 26) for i in ids) + "."
+    assert decode_text(rows, Tok()) == ["kua.", "."]
+    assert _reply("") == "<silence>" and _reply("Thank you.") == "<silence>"
+    assert _reply(" Hello World. ") == "hello world"
+    assert attn_decode_work(16, 12, 1500) >= 16 * 12 * 66
