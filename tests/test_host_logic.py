@@ -45,7 +45,7 @@ def test_whisper_text_rendering_and_reply_filter():
     class Tok:
         def decode(self, ids):
             return " " + "".join(chr(97 + i % 26) for i in ids) + "."
-    assert decode_text(rows, Tok()) == ["kua.", "."]
+    assert decode_text(rows, Tok()) == ["ku.", "."]
     assert _reply("") == "<silence>" and _reply("Thank you.") == "<silence>"
     assert _reply(" Hello World. ") == "hello world"
     assert attn_decode_work(16, 12, 1500) >= 16 * 12 * 66
