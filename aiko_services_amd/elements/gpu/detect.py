@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import torch
 
-from ...gpu.element import DeviceResult, GpuPipelineElement
+from ...gpu.element import DeviceResult, GpuPipelineElement, HostRing
 from ...pipeline.stream import StreamEvent
 
 __all__ = ["FrameFanout", "YoloDetector", "DetectionsGather"]
@@ -131,10 +131,9 @@ class DetectionsGather(GpuPipelineElement):
             pin = dev.type == "cuda"
             b = {"all_det": torch.empty(world * B, D_, six, dtype=torch.float32, device=dev),
                  "all_count": torch.empty(world * B, dtype=torch.int32, device=dev),
-                 "host_det": [torch.empty(world * B, D_, six, dtype=torch.float32, pin_memory=pin)
-                              for _ in range(8)],
-                 "host_count": [torch.empty(world * B, dtype=torch.int32, pin_memory=pin) for _ in range(8)],
-                 "slot": 0}
+                 "host": HostRing(lambda: (
+                     torch.empty(world * B, D_, six, dtype=torch.float32, pin_memory=pin),
+                     torch.empty(world * B, dtype=torch.int32, pin_memory=pin)), 8)}
             self._bufs[key] = b
         return b
 
@@ -147,9 +146,7 @@ class DetectionsGather(GpuPipelineElement):
             D.all_gather_into(b["all_det"], detections)
             D.all_gather_into(b["all_count"], counts)
             det, cnt = b["all_det"], b["all_count"]
-        slot = b["slot"]
-        b["slot"] = (slot + 1) % len(b["host_det"])
-        hd, hc = b["host_det"][slot], b["host_count"][slot]
+        slot, (hd, hc) = b["host"].acquire()
         hd.copy_(det, non_blocking=True)
         hc.copy_(cnt, non_blocking=True)
         ev = None
@@ -158,4 +155,4 @@ class DetectionsGather(GpuPipelineElement):
             ev.record()
         result = DeviceResult({"det": hd, "count": hc}, ev,
                               t_submit=t_submit if isinstance(t_submit, (float, torch.Tensor)) else None)
-        return StreamEvent.OKAY, {"detections": result}
+        return StreamEvent.OKAY, {"detections": b["host"].bind(slot, result)}

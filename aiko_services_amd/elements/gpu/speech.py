@@ -24,7 +24,7 @@ import time
 import numpy as np
 import torch
 
-from ...gpu.element import DeviceResult, GpuPipelineElement
+from ...gpu.element import DeviceResult, GpuPipelineElement, HostRing
 from ...pipeline.stream import StreamEvent
 
 __all__ = ["AudioChunks", "AudioWindow", "WhisperEncoder", "WhisperTranscribe", "SpeechToText", "FeatureSink"]
@@ -277,15 +277,13 @@ class FeatureSink(GpuPipelineElement):
             pin = self.device.type == "cuda"
             b = self._bufs[(B, d, self.lane)] = {
                 "pooled": torch.empty(B, d, dtype=torch.float32, device=self.device),
-                "host": [torch.empty(B, d, dtype=torch.float32, pin_memory=pin) for _ in range(8)],
-                "slot": 0}
+                "host": HostRing(lambda: torch.empty(B, d, dtype=torch.float32, pin_memory=pin), 8)}
         torch.mean(features, dim=1, dtype=torch.float32, out=b["pooled"])
-        h = b["host"][b["slot"]]
-        b["slot"] = (b["slot"] + 1) % len(b["host"])
+        slot, h = b["host"].acquire()
         h.copy_(b["pooled"], non_blocking=True)
         ev = None
         if self.device.type == "cuda":
             ev = torch.cuda.Event()
             ev.record()
-        return StreamEvent.OKAY, {"embedding": DeviceResult({"pooled": h}, ev,
-                                                            t_submit=t_submit if isinstance(t_submit, float) else None)}
+        result = DeviceResult({"pooled": h}, ev, t_submit=t_submit if isinstance(t_submit, float) else None)
+        return StreamEvent.OKAY, {"embedding": b["host"].bind(slot, result)}

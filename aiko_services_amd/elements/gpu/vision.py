@@ -22,7 +22,7 @@ import time
 
 import torch
 
-from ...gpu.element import DeviceResult, GpuPipelineElement
+from ...gpu.element import DeviceResult, GpuPipelineElement, HostRing
 from ...pipeline.stream import StreamEvent
 
 __all__ = ["SyntheticFrames", "ImagePreprocess", "ResNet50Classifier", "ClassifierTopK"]
@@ -165,11 +165,9 @@ class ClassifierTopK(GpuPipelineElement):
                  "index": torch.empty(B, self.k, dtype=torch.int32, device=dev),
                  "all_prob": torch.empty(world * B, self.k, dtype=torch.float32, device=dev),
                  "all_index": torch.empty(world * B, self.k, dtype=torch.int32, device=dev),
-                 "host_prob": [torch.empty(world * B, self.k, dtype=torch.float32, pin_memory=True)
-                               for _ in range(8)],
-                 "host_index": [torch.empty(world * B, self.k, dtype=torch.int32, pin_memory=True)
-                                for _ in range(8)],
-                 "slot": 0}
+                 "host": HostRing(lambda: (
+                     torch.empty(world * B, self.k, dtype=torch.float32, pin_memory=dev.type == "cuda"),
+                     torch.empty(world * B, self.k, dtype=torch.int32, pin_memory=dev.type == "cuda")), 8)}
             self._bufs[key] = b
         return b
 
@@ -184,13 +182,13 @@ class ClassifierTopK(GpuPipelineElement):
             D.all_gather_into(b["all_prob"], prob)
             D.all_gather_into(b["all_index"], index)
             prob, index = b["all_prob"], b["all_index"]
-        slot = b["slot"]
-        b["slot"] = (slot + 1) % len(b["host_prob"])
-        hp, hi = b["host_prob"][slot], b["host_index"][slot]
+        slot, (hp, hi) = b["host"].acquire()
         hp.copy_(prob, non_blocking=True)
         hi.copy_(index, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
+        ev = None
+        if self.device.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
         result = DeviceResult({"top_prob": hp, "top_index": hi}, ev,
                               t_submit=t_submit if isinstance(t_submit, (float, torch.Tensor)) else None)
-        return StreamEvent.OKAY, {"topk": result}
+        return StreamEvent.OKAY, {"topk": b["host"].bind(slot, result)}

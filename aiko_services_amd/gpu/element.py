@@ -16,6 +16,7 @@ the pipeline synchronising the device per frame.
 from __future__ import annotations
 
 import time
+import weakref
 
 import torch
 
@@ -24,7 +25,7 @@ from ..pipeline.stream import StreamEvent
 from ..utils.configuration import get_gpu_configuration
 from .device import parse_device, require_gpu
 
-__all__ = ["GpuPipelineElement", "DeviceResult", "FramePool", "CapturedCall"]
+__all__ = ["GpuPipelineElement", "DeviceResult", "FramePool", "CapturedCall", "HostRing"]
 
 _DTYPE_CODES = {torch.uint8: 0, torch.int8: 1, torch.int16: 2, torch.int32: 3, torch.int64: 4,
                 torch.float16: 5, torch.float32: 6, torch.float64: 7, torch.bool: 11,
@@ -72,7 +73,7 @@ class FramePool:
 class DeviceResult:
     """Tensors produced asynchronously on the GPU plus the event that completes them."""
 
-    __slots__ = ("tensors", "event", "t_submit", "t_done", "meta")
+    __slots__ = ("tensors", "event", "t_submit", "t_done", "meta", "__weakref__")
 
     def __init__(self, tensors: dict, event: torch.cuda.Event | None, t_submit: float | None = None, meta=None):
         self.tensors = tensors
@@ -103,6 +104,55 @@ class DeviceResult:
     def __repr__(self):
         shapes = {k: tuple(v.shape) if hasattr(v, "shape") else v for k, v in self.tensors.items()}
         return f"DeviceResult({shapes}, ready={self.ready()})"
+
+
+class HostRing:
+    """Pinned host buffer sets handed out inside :class:`DeviceResult` objects.
+
+    A set is reused only once the DeviceResult that last carried it has been dropped by its
+    consumer (tracked with a weak reference) — a consumer holding many results in flight never
+    sees its data overwritten: the ring grows instead (up to ``max_sets``, then raises).  Before
+    a set is rewritten the current stream waits for the copy that last wrote it (its event), so
+    an abandoned result's late copy cannot land on top of the new one.
+    """
+
+    def __init__(self, factory, initial: int = 4, max_sets: int = 256):
+        self._factory = factory
+        self._sets = [factory() for _ in range(max(1, initial))]
+        self._holders = [None] * len(self._sets)       # weakref to the DeviceResult, or None
+        self._events = [None] * len(self._sets)
+        self._cursor = 0
+        self.max_sets = max_sets
+
+    def __len__(self):
+        return len(self._sets)
+
+    def acquire(self):
+        """(index, buffers) of a set no live DeviceResult refers to."""
+        n = len(self._sets)
+        for i in range(n):
+            idx = (self._cursor + i) % n
+            ref = self._holders[idx]
+            if ref is None or ref() is None:
+                break
+        else:
+            if n >= self.max_sets:
+                raise RuntimeError(f"HostRing: {n} results still held by consumers (max {self.max_sets}); "
+                                   "consume (drop) DeviceResults before requesting more")
+            self._sets.append(self._factory())
+            self._holders.append(None)
+            self._events.append(None)
+            idx = n
+        self._cursor = (idx + 1) % len(self._sets)
+        ev = self._events[idx]
+        if ev is not None:
+            torch.cuda.current_stream().wait_event(ev)
+        return idx, self._sets[idx]
+
+    def bind(self, idx: int, result: "DeviceResult") -> "DeviceResult":
+        self._holders[idx] = weakref.ref(result)
+        self._events[idx] = result.event
+        return result
 
 
 _STREAMS: dict = {}

@@ -227,13 +227,9 @@ class YOLOv8(WeightsMixin):
         Ho, Wo, top, left, _ = self.letterbox((H, W))
         S = self.image_size
         h0, w0 = C.stem_out_hw(S, S, 3, 2, 1)
-        if self._stem_w is None:          # bf16 [Cout, 64]: k = (r * 3 + s) * 4 + c, from the packed stem
-            l0 = self.l0
-            cc = l0.Cc
-            wp = l0.weight[:, :3 * cc].reshape(l0.cout, 3, cc // 4, 4)[:, :, :3, :]   # [o][r][s][c4]
-            w = torch.zeros(l0.cout, 64, dtype=torch.bfloat16, device=l0.weight.device)
-            w[:, :36] = wp.reshape(l0.cout, 36)
-            self._stem_w = w.contiguous()
+        if self._stem_w is None:
+            self._stem_w = torch.zeros(self.l0.cout, 64, dtype=torch.bfloat16, device=self.l0.weight.device)
+            self._derive_stem_w()
         out = self._buf("a0", (B, h0, w0, self.ch[0]))
         torch.ops.aiko.stem_direct_out(frames, self._stem_w, self.l0.bias, out,
                                        [Ho, Wo, S, S, top, left, 3, 2, 1, 2], 114.0,
@@ -304,10 +300,20 @@ class YOLOv8(WeightsMixin):
     def config(self) -> dict:
         return {"scale": self.scale, "num_classes": self.nc, "image_size": self.image_size}
 
+    def _derive_stem_w(self):
+        """bf16 [Cout, 64] direct-stem weight, k = (r * 3 + s) * 4 + c, from the packed stem —
+        written into the existing tensor so captured hipGraphs see reloaded weights."""
+        l0 = self.l0
+        cc = l0.Cc
+        wp = l0.weight[:, :3 * cc].reshape(l0.cout, 3, cc // 4, 4)[:, :, :3, :]   # [o][r][s][c4]
+        self._stem_w.zero_()
+        self._stem_w[:, :36] = wp.reshape(l0.cout, 36)
+
     def _weights_loaded(self):
         """Re-derive each head level's fused box|cls first conv (and the direct-stem weight)
-        from the loaded layers."""
-        self._stem_w = None
+        from the loaded layers, in place."""
+        if self._stem_w is not None:
+            self._derive_stem_w()
         for lvl in self.heads:
             a, b = lvl.box[0], lvl.cls[0]
             lvl.first.weight[:a.cout].copy_(a.weight)

@@ -347,8 +347,10 @@ STEM_POOL_VARIANT = 0     # 0: 8x7 pooled tiles (4 workgroups/CU); 1: 8x14 (2 wo
 def stem_pool_weight(spec: ConvSpec) -> torch.Tensor:
     """[7, 64, 32] LDS image of a packed 7x7 stem weight for the fused kernel: filter row r,
     channel o, 16-byte chunk ``pos`` holds K columns ``r*32 + 8*(pos ^ ((o >> 2) & 2))`` (the
-    swizzle that makes the kernel's A-fragment reads bank-conflict free).  Cached on the spec,
-    rebuilt when the weight tensor changes."""
+    swizzle that makes the kernel's A-fragment reads bank-conflict free).  Cached on the spec;
+    when the weight tensor changes (``load_state_dict`` copies in place, bumping ``_version``)
+    the image is re-derived INTO THE SAME TENSOR, so a hipGraph captured earlier replays the
+    new weights instead of a stale (or freed) image."""
     key = (spec.weight.data_ptr(), spec.weight._version)
     cached = getattr(spec, "_stem_pool_w", None)
     if cached is not None and cached[0] == key:
@@ -356,7 +358,12 @@ def stem_pool_weight(spec: ConvSpec) -> torch.Tensor:
     w = spec.weight.view(64, 8, 4, 8)[:, :7].permute(1, 0, 2, 3)         # [r, o, q, j]
     o = torch.arange(64, device=w.device)
     q = torch.arange(4, device=w.device)[None, :] ^ ((o[:, None] >> 2) & 2)  # [o, pos]
-    img = torch.gather(w, 2, q[None, :, :, None].expand(7, 64, 4, 8)).reshape(7, 64, 32).contiguous()
+    img = torch.gather(w, 2, q[None, :, :, None].expand(7, 64, 4, 8)).reshape(7, 64, 32)
+    if cached is not None:
+        cached[1].copy_(img)
+        img = cached[1]
+    else:
+        img = img.contiguous()
     spec._stem_pool_w = (key, img)
     return img
 

@@ -108,9 +108,14 @@ class StageLink:
     """One direction of a stage boundary: a ring of ``depth`` HBM slots (header + tensors)."""
 
     def __init__(self, peer: int, device, depth: int = 2):
+        if depth < 2:
+            # the receiver posts frame k+1's receive before frame k's compute is queued; with a
+            # single slot that receive would overwrite the inputs frame k is still reading
+            raise ValueError(f"StageLink depth must be >= 2 (got {depth}): one slot in use by the "
+                             "stage, one receiving the next frame")
         self.peer = peer
         self.device = torch.device(device)
-        self.depth = max(1, depth)
+        self.depth = depth
         self.signature = None           # [(name, dtype, shape)]
         self.slots = []                 # [(header, {name: tensor})]
         self.pending = [None] * self.depth

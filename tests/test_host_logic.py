@@ -49,3 +49,40 @@ def test_whisper_text_rendering_and_reply_filter():
     assert _reply("") == "<silence>" and _reply("Thank you.") == "<silence>"
     assert _reply(" Hello World. ") == "hello world"
     assert attn_decode_work(16, 12, 1500) >= 16 * 12 * 66
+
+
+def test_host_ring_never_reuses_a_held_result():
+    """pinned result rings must not overwrite buffers a consumer still holds."""
+    import gc
+    from aiko_services_amd.gpu.element import DeviceResult, HostRing
+    ring = HostRing(lambda: torch.zeros(4), initial=2, max_sets=6)
+    held = []
+    for k in range(5):                      # hold every result: the ring has to grow
+        idx, buf = ring.acquire()
+        buf.fill_(k)
+        held.append(ring.bind(idx, DeviceResult({"x": buf}, None)))
+    assert len(ring) == 5
+    assert [int(r.tensors["x"][0]) for r in held] == [0, 1, 2, 3, 4]
+    del held[:]
+    gc.collect()
+    for _ in range(10):                     # dropped results: sets are recycled, no growth
+        idx, buf = ring.acquire()
+        r = ring.bind(idx, DeviceResult({"x": buf}, None))
+        del r
+    assert len(ring) == 5
+    keep = []
+    for _ in range(6):
+        idx, buf = ring.acquire()
+        keep.append(ring.bind(idx, DeviceResult({"x": buf}, None)))
+    import pytest
+    with pytest.raises(RuntimeError):
+        ring.acquire()
+
+
+def test_stage_link_requires_two_slots():
+    """depth 1 would let the look-ahead receive overwrite the frame in use."""
+    import pytest
+    from aiko_services_amd.parallel.pipeline_parallel import StageLink
+    with pytest.raises(ValueError):
+        StageLink(1, "cpu", depth=1)
+    assert StageLink(1, "cpu", depth=2).depth == 2
