@@ -299,7 +299,11 @@ class ResNet50(WeightsMixin):
         return {"num_classes": self.num_classes, "image_size": self.image_size, "topk": self.topk}
 
     def _weights_loaded(self):
-        """Re-derive the K-concatenated conv3 + shortcut specs from the loaded layers."""
+        """Re-derive the K-concatenated conv3 + shortcut specs and the fused stem's LDS weight
+        image from the loaded layers, in place (a captured hipGraph never re-enters Python, so
+        the image must be refreshed here, not lazily at the next eager call)."""
+        if getattr(self.stem, "_stem_pool_w", None) is not None:
+            C.stem_pool_weight(self.stem)
         for b in self.blocks:
             if b.fused is None:
                 continue
