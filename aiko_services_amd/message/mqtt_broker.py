@@ -254,6 +254,10 @@ class Broker:
 
     def _route(self, topic: str, payload: bytes, qos: int, retain: bool):
         self.stats["published"] += 1
+        self.stats["max_payload"] = max(self.stats.get("max_payload", 0), len(payload))
+        tap = getattr(self, "on_publish", None)       # observability / tests: (topic, payload)
+        if tap is not None:
+            tap(topic, payload)
         if retain:
             if payload:
                 self.retained[topic] = (bytes(payload), qos)

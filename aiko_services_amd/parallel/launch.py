@@ -1,0 +1,170 @@
+"""Multi-GPU actor pipelines: one registered worker Pipeline process per rank of a Plan.
+
+``aiko_pipeline create DEFINITION`` with ``"parallel": {"mode": "pp", "gpus": N}`` (or
+``deploy.local.stage`` on the elements) lands here (reference entry point
+``/root/reference/src/aiko_services/main/pipeline.py:1444-1528``; multi-process orchestration
+in the reference is by hand, ``examples/pipeline/multitude/run_large.sh``):
+
+1. :func:`~aiko_services_amd.parallel.placement.make_plan` cuts the definition into stages,
+   replicas and ranks;
+2. :func:`spawn_workers` starts ranks 1..N-1 through the :class:`ProcessManager` — BEFORE this
+   process touches the GPU — each with ``LOCAL_RANK`` = its GPU, ``RANK`` / ``WORLD_SIZE``
+   and the plan file;
+3. every rank :func:`join` s: RCCL group bootstrap over the MQTT broker
+   (``parallel/rendezvous.py``) and the hop data plane's per-direction communicators
+   (``parallel/hop.py``);
+4. each worker creates its stage Pipeline, registered with tags ``rank=`` / ``stage=`` /
+   ``weight=`` and runs its event loop; rank 0 creates stage 0 (the pipeline the user asked
+   for), whose remote element discovers the stage-1 replicas through the registrar.
+
+Frames then flow as in the reference — ``process_frame`` to the remote, ``process_frame_
+response`` back — with the tensors on xGMI.  Workers exit when their parent process goes.
+"""
+from __future__ import annotations
+
+import atexit
+import os
+import sys
+import tempfile
+import threading
+import time
+
+from .placement import Plan
+
+__all__ = ["spawn_workers", "join", "create_rank_pipeline", "worker_main", "backend_for"]
+
+
+def backend_for() -> str:
+    b = os.environ.get("AIKO_HOP_BACKEND", "auto")
+    if b != "auto":
+        return b
+    import torch
+    return "nccl" if torch.cuda.is_available() else "gloo"
+
+
+def spawn_workers(plan: Plan, plan_path: str | None = None, env: dict | None = None):
+    """Start ranks 1..world-1 (``python -m aiko_services_amd.parallel.launch worker``)."""
+    from ..control.process_manager import ProcessManager
+    if plan_path is None:
+        fd, plan_path = tempfile.mkstemp(prefix="aiko_plan_", suffix=".json")
+        with os.fdopen(fd, "w") as f:
+            f.write(plan.to_json())
+    manager = ProcessManager()
+    base_env = dict(os.environ if env is None else env)
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    base_env["PYTHONPATH"] = root + os.pathsep + base_env.get("PYTHONPATH", "")
+    for spec in plan.ranks:
+        if spec.rank == 0:
+            continue
+        child = dict(base_env, LOCAL_RANK=str(spec.device), RANK=str(spec.rank),
+                     WORLD_SIZE=str(plan.world), AIKO_PARENT_PID=str(os.getpid()))
+        manager.create(f"rank{spec.rank}", sys.executable,
+                       ["-m", "aiko_services_amd.parallel.launch", "worker", plan_path, str(spec.rank)],
+                       env=child)
+    atexit.register(manager.terminate_all)
+    return manager, plan_path
+
+
+def join(plan: Plan, rank: int, timeout_s: float = 120.0):
+    """RCCL group over the MQTT broker + the hop data plane (collective: every rank calls)."""
+    from ..utils.configuration import get_mqtt_host
+    from . import hop
+    from .rendezvous import rendezvous_init
+    os.environ.setdefault("LOCAL_RANK", str(plan.ranks[rank].device))
+    _, host, port = get_mqtt_host()
+    backend = backend_for()
+    if plan.world > 1:
+        rendezvous_init(plan.group, rank, plan.world, host, port, backend=backend, timeout_s=timeout_s)
+    depth = int(os.environ.get("AIKO_HOP_DEPTH", "4"))
+    return hop.init_plane(plan.links, depth=depth)
+
+
+def create_rank_pipeline(plan: Plan, rank: int, stream_id=None, parameters=None, frame_id=0,
+                         frame_data=None, grace_time=60, queue_response=None, name=None,
+                         graph_path=None, stream_reset=False, definition_pathname="<parallel>"):
+    """This rank's stage Pipeline; on rank 0 also binds replicated / local stage members."""
+    from ..pipeline.definition import parse_pipeline_definition_dict
+    from ..pipeline.engine import PipelineImpl
+    spec = plan.ranks[rank]
+    definition = parse_pipeline_definition_dict(spec.definition)
+    pipeline = PipelineImpl.create_pipeline(definition_pathname, definition, name or spec.name, graph_path,
+                                            None, [], frame_id, None, grace_time,
+                                            queue_response=queue_response, tags=list(spec.tags))
+    if spec.stage + 1 < len(plan.stages):
+        remote = f"Stage{spec.stage + 1}"
+        local_def = None
+        weight = 0.0
+        if spec.stage == 0 and plan.local_share > 0:
+            nxt = next(r for r in plan.ranks if r.stage == 1)
+            local_def = parse_pipeline_definition_dict(nxt.definition)
+            weight = plan.local_share
+        expected = plan.replicas[spec.stage + 1] + (1 if local_def is not None else 0)
+        pipeline.set_remote_replicas(remote, expected, local_def, weight)
+
+    def start():
+        from ..runtime.actor import ActorTopic
+        if stream_id is not None:
+            if stream_reset:
+                pipeline._post_message(ActorTopic.IN, "destroy_stream", [stream_id])
+            pipeline._post_message(ActorTopic.IN, "create_stream",
+                                   [stream_id, None, dict(parameters or {}), grace_time, queue_response, None])
+        if frame_data is not None:
+            from ..utils.sexpr import parse
+            _, arguments = parse(f"(process_frame {frame_data})")
+            pipeline.create_frame({"stream_id": stream_id or "*", "frame_id": int(frame_id or 0),
+                                   "parameters": {}}, arguments[0])
+    start_when_ready(pipeline, start if rank == 0 else None)
+    return pipeline
+
+
+def start_when_ready(pipeline, then=None, timeout_s: float = 120.0):
+    """Helper thread: once this rank's stage is ready (its downstream stages discovered), join
+    the group-wide start barrier; rank 0 then creates the stream.  Every stage therefore
+    exists, end to end, before the first frame is generated."""
+    from . import hop
+
+    def run():
+        deadline = time.time() + timeout_s
+        while pipeline.share.get("lifecycle") != "ready" and time.time() < deadline:
+            time.sleep(0.02)
+        plane = hop.plane()
+        if plane is not None:
+            plane.barrier()
+        if then is not None:
+            then()
+    t = threading.Thread(target=run, daemon=True, name="aiko-parallel-start")
+    t.start()
+    return t
+
+
+def _watch_parent():
+    """Terminate this worker when the process that spawned it has gone."""
+    from ..runtime import event
+    from ..runtime.process import aiko
+    parent = int(os.environ.get("AIKO_PARENT_PID", "0") or 0)
+    if not parent:
+        return
+
+    def check():
+        try:
+            os.kill(parent, 0)
+        except OSError:
+            aiko.process.terminate(0)
+    event.add_timer_handler(check, 0.5)
+
+
+def worker_main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if len(argv) != 3 or argv[0] != "worker":
+        raise SystemExit("usage: python -m aiko_services_amd.parallel.launch worker PLAN.json RANK")
+    with open(argv[1]) as f:
+        plan = Plan.from_json(f.read())
+    rank = int(argv[2])
+    join(plan, rank)
+    pipeline = create_rank_pipeline(plan, rank)
+    _watch_parent()
+    pipeline.run(mqtt_connection_required=True)
+
+
+if __name__ == "__main__":
+    worker_main()

@@ -1,0 +1,258 @@
+"""Placement of one PipelineDefinition over the GPUs of a node: stages, replicas, ranks.
+
+The reference spreads a pipeline over processes by hand: each process runs its own definition
+and a parent reaches the next one through a ``remote`` element found by the registrar
+(``/root/reference/src/aiko_services/examples/pipeline/multitude/pipeline_small_a.json``,
+``run_large.sh``).  Here the same nested-remote topology is GENERATED from one definition
+annotated with ``"parallel": {"mode": "pp", "gpus": N}`` and/or ``deploy.local.stage``:
+
+* the element chain is cut into stages (explicit ``stage`` indices, or the planner below);
+* stage ``s`` runs as Pipeline ``{name}_s{s}`` (stage 0 keeps ``name``: it is the pipeline
+  ``aiko_pipeline create`` started) whose graph ends in a remote element standing for stage
+  ``s + 1`` — exactly the reference's chained remote pipelines, the response of the last stage
+  flowing back up the chain as ``process_frame_response``;
+* a stage may be REPLICATED on several GPUs (PP x DP): every replica registers under the same
+  service name with tags ``rank=r`` / ``weight=w`` and the upstream stage spreads frames over
+  them (``RemoteReplicas``, weighted round-robin).  ``local_share`` > 0 also runs a copy of
+  the LAST stage inside rank 0 (its GPU would otherwise only feed the others);
+* every process is one rank of one RCCL group; ``links`` lists the (src, dst) directions the
+  hop data plane needs (``parallel/hop.py``).
+
+``plan_stages`` is the balancer: from measured per-element GPU times (``frame.metrics
+["gpu_events"]`` of a 1-GPU run, or ``bench.py --profile-elements``) it picks the cut points,
+replica counts and rank-0 share that minimise the slowest rank's time per frame.
+"""
+from __future__ import annotations
+
+import copy
+import itertools
+import json
+import uuid
+from dataclasses import asdict, dataclass, field
+
+from ..pipeline.definition import parse_pipeline_definition_dict
+
+__all__ = ["Plan", "RankSpec", "plan_stages", "make_plan", "element_order", "predicted_times",
+           "stage_remote_name"]
+
+
+@dataclass
+class RankSpec:
+    rank: int
+    stage: int
+    name: str                  # Pipeline (service) name this rank registers
+    definition: dict           # PipelineDefinition (JSON dict) this rank runs
+    device: int                # local GPU index
+    weight: float = 1.0        # share of its stage's frames (replicas)
+    tags: list = field(default_factory=list)
+
+
+@dataclass
+class Plan:
+    group: str
+    world: int
+    mode: str
+    stages: list               # [[element names]]
+    replicas: list             # ranks per stage
+    local_share: float         # fraction of the last stage's frames run inside rank 0
+    ranks: list                # [RankSpec]
+    links: list                # [[src, dst]] hop directions (one RCCL communicator each)
+    predicted_ms: dict = field(default_factory=dict)
+
+    def to_json(self) -> str:
+        return json.dumps(asdict(self))
+
+    @classmethod
+    def from_json(cls, text: str) -> "Plan":
+        d = json.loads(text)
+        d["ranks"] = [RankSpec(**r) for r in d["ranks"]]
+        return cls(**d)
+
+
+def element_order(definition: dict):
+    from .pipeline_parallel import element_chain
+    return element_chain(parse_pipeline_definition_dict(definition))
+
+
+def stage_remote_name(base: str, stage: int) -> str:
+    return base if stage == 0 else f"{base}_s{stage}"
+
+
+# ---- balancer ---------------------------------------------------------------------------------
+
+def predicted_times(stages_ms, replicas, local_share=0.0):
+    """Per-rank ms per frame: stage s's time split over its replicas; rank 0 also runs
+    ``local_share`` of the last stage."""
+    per_rank = []
+    last = len(stages_ms) - 1
+    for s, (t, r) in enumerate(zip(stages_ms, replicas)):
+        if s == last and last > 0:
+            remote = (1.0 - local_share) * t
+            per_rank += [remote / r] * r
+        else:
+            per_rank += [t / r] * r
+    if last > 0:
+        per_rank[0] += local_share * stages_ms[last]
+    return per_rank
+
+
+def plan_stages(order, times_ms: dict, gpus: int, replicate: bool = True, local: bool = True,
+                boundary_ms: dict | None = None):
+    """Best (stages, replicas, local_share, per-rank ms) for ``gpus`` ranks.
+
+    ``order``: element names in execution order; ``times_ms``: measured GPU ms per frame of
+    each element on one GPU; ``boundary_ms[name]`` (optional): cost of shipping the swag after
+    element ``name`` to the next stage, added to the receiving stage.  Stage 0 has one rank
+    (the source); later stages may be replicated.  Exhaustive over cut points and replica
+    splits (chains are short: 2^(n-1) cuts x compositions of ``gpus``)."""
+    n = len(order)
+    boundary_ms = boundary_ms or {}
+    best = None
+    for cuts in itertools.product([0, 1], repeat=n - 1):
+        stages, cur = [], [order[0]]
+        for name, cut in zip(order[1:], cuts):
+            if cut:
+                stages.append(cur)
+                cur = []
+            cur.append(name)
+        stages.append(cur)
+        S = len(stages)
+        if S > gpus:
+            continue
+        t = []
+        for s, names in enumerate(stages):
+            ms = sum(float(times_ms.get(e, 0.0)) for e in names)
+            if s > 0:
+                ms += float(boundary_ms.get(stages[s - 1][-1], 0.0))
+            t.append(ms)
+        splits = [[1] * S]
+        if replicate and S > 1:
+            splits = [list(c) for c in _compositions(gpus, S) if c[0] == 1]
+        for reps in splits:
+            if sum(reps) > gpus:
+                continue
+            shares = [0.0]
+            if local and S == 2:              # rank 0 can host a copy of the (last) stage 1
+                shares = [i / 40 for i in range(0, 40)]
+            for share in shares:
+                per_rank = predicted_times(t, reps, share)
+                key = (round(max(per_rank), 6), len(per_rank), -share)
+                if best is None or key < best[0]:
+                    best = (key, stages, reps, share, per_rank)
+    _, stages, reps, share, per_rank = best
+    return stages, reps, share, per_rank
+
+
+def _compositions(total, parts):
+    """Positive integer tuples of length ``parts`` summing to at most ``total``."""
+    for k in range(parts, total + 1):
+        for cut in itertools.combinations(range(1, k), parts - 1):
+            edges = (0,) + cut + (k,)
+            yield tuple(edges[i + 1] - edges[i] for i in range(parts))
+
+
+# ---- plan construction -----------------------------------------------------------------------
+
+def _strip_stage(e: dict) -> dict:
+    e = copy.deepcopy(e)
+    local = e.get("deploy", {}).get("local")
+    if isinstance(local, dict):
+        local.pop("stage", None)
+    return e
+
+
+def _boundary(defn: dict, stages, s):
+    by = {e["name"]: e for e in defn["elements"]}
+    produced, consumed = set(), set()
+    for r, names in enumerate(stages):
+        for n in names:
+            if r <= s:
+                produced.update(o["name"] for o in by[n]["output"])
+            else:
+                consumed.update(i["name"] for i in by[n]["input"])
+    return sorted(produced & consumed)
+
+
+def make_plan(definition: dict, gpus: int | None = None, stages=None, replicas=None,
+              local_share: float = 0.0, times_ms: dict | None = None, group: str | None = None,
+              device_offset: int = 0) -> Plan:
+    """Plan for ``definition`` (a JSON dict).  Stages come from (in order) ``stages``, the
+    elements' ``deploy.local.stage``, the balancer (``times_ms``), or one element per stage."""
+    par = definition.get("parallel") or {}
+    mode = par.get("mode", "pp")
+    gpus = int(gpus or par.get("gpus", 1))
+    order = element_order(definition)
+    by = {e["name"]: e for e in definition["elements"]}
+    predicted = {}
+    if stages is None:
+        explicit = [by[n]["deploy"].get("local", {}).get("stage") for n in order]
+        if all(s is not None for s in explicit):
+            count = max(int(s) for s in explicit) + 1
+            stages = [[] for _ in range(count)]
+            for n, s in zip(order, explicit):
+                stages[int(s)].append(n)
+            stages = [s for s in stages if s]
+        elif times_ms:
+            stages, replicas, local_share, per_rank = plan_stages(order, times_ms, gpus)
+            predicted = {"per_rank_ms": [round(x, 4) for x in per_rank]}
+        else:
+            k = min(gpus, len(order))
+            sizes = [len(order) // k + (1 if i < len(order) % k else 0) for i in range(k)]
+            stages, at = [], 0
+            for size in sizes:
+                stages.append(order[at:at + size])
+                at += size
+    if replicas is None:
+        replicas = [1] * len(stages)
+        replicas[-1] += max(0, gpus - sum(replicas)) if par.get("replicate_last", False) else 0
+    if len(replicas) != len(stages) or replicas[0] != 1:
+        raise ValueError(f"replicas {replicas} must match stages {stages} and start with 1")
+    if sum(replicas) > max(gpus, 1):
+        raise ValueError(f"plan needs {sum(replicas)} GPUs, only {gpus} given")
+    base = definition["name"]
+    group = group or f"{base}-{uuid.uuid4().hex[:8]}"
+    rank_of_stage, r = [], 0
+    for reps in replicas:
+        rank_of_stage.append(list(range(r, r + reps)))
+        r += reps
+    world = r
+    last = len(stages) - 1
+    ranks = []
+    for s, names in enumerate(stages):
+        elements = [_strip_stage(by[n]) for n in names]
+        graph_names = list(names)
+        if s < last:
+            remote_name = f"Stage{s + 1}"
+            last_el = by[stages[-1][-1]]
+            elements.append({
+                "name": remote_name,
+                "input": [{"name": n, "type": "tensor"} for n in _boundary(definition, stages, s)],
+                "output": copy.deepcopy(last_el["output"]),
+                "deploy": {"remote": {"module": "aiko_services_amd.pipeline.engine",
+                                      "service_filter": {"name": stage_remote_name(base, s + 1)}}},
+            })
+            graph_names.append(remote_name)
+        d = {k: copy.deepcopy(v) for k, v in definition.items() if k not in ("elements", "graph", "parallel")}
+        d["name"] = stage_remote_name(base, s)
+        if s < last:                 # frame lanes need a fully local graph
+            d["parameters"] = dict(d.get("parameters") or {}, gpu_lanes=1)
+        d["graph"] = [f"({' '.join(graph_names)})"]
+        d["elements"] = elements
+        reps = replicas[s]
+        for i, rank in enumerate(rank_of_stage[s]):
+            w = 1.0
+            if s == last and last > 0:
+                w = (1.0 - local_share) / reps
+            ranks.append(RankSpec(rank=rank, stage=s, name=d["name"], definition=d,
+                                  device=device_offset + rank, weight=w,
+                                  tags=[f"rank={rank}", f"stage={s}", f"group={group}",
+                                        f"weight={w:.6g}"]))
+    links = []
+    for s in range(last):
+        for a in rank_of_stage[s]:
+            for b in rank_of_stage[s + 1]:
+                links += [[a, b], [b, a]]
+    if local_share > 0 and last != 1:
+        raise ValueError("local_share needs a two-stage plan (rank 0 hosts a copy of stage 1)")
+    return Plan(group=group, world=world, mode=mode, stages=stages, replicas=list(replicas),
+                local_share=float(local_share), ranks=ranks, links=links, predicted_ms=predicted)

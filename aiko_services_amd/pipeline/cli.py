@@ -21,6 +21,25 @@ import click
 from ..utils.configuration import get_pid
 
 
+def describe(value):
+    """Printable form of a response value: tensors (and DeviceResults, waited for) as dtype,
+    shape and a SHA-256 prefix of their bytes — bit-exact comparisons across runs."""
+    import hashlib
+    try:
+        import torch
+    except ImportError:                                   # pragma: no cover
+        torch = None
+    if hasattr(value, "wait") and hasattr(value, "tensors"):
+        return {k: describe(v) for k, v in value.wait().items()}
+    if torch is not None and isinstance(value, torch.Tensor):
+        t = value.detach().cpu().contiguous()
+        digest = hashlib.sha256(t.view(torch.uint8).numpy().tobytes() if t.numel() else b"").hexdigest()[:16]
+        return f"tensor({str(t.dtype).split('.')[-1]},{'x'.join(map(str, t.shape))},sha={digest})"
+    if isinstance(value, dict):
+        return {k: describe(v) for k, v in value.items()}
+    return value
+
+
 @click.group()
 def main():
     """Create and destroy Pipelines"""
@@ -84,7 +103,7 @@ def create(definition_pathname, graph_path, name, parameters, stream_id, stream_
                 info, data = q.get()
                 count += 1
                 if show_response:
-                    _LOGGER.info(f"Output: <{info['stream_id']}:{info['frame_id']}> {data}")
+                    _LOGGER.info(f"Output: <{info['stream_id']}:{info['frame_id']}> {describe(data)}")
                 if exit_after_frames and count >= exit_after_frames:
                     aiko.process.terminate()
                     return
@@ -92,6 +111,25 @@ def create(definition_pathname, graph_path, name, parameters, stream_id, stream_
         if stream_id is None and exit_after_frames:
             stream_id = "1"
 
+    par = definition.parallel or {}
+    staged = any(getattr(e.deploy, "stage", None) not in (None, 0) for e in definition.elements)
+    if (par.get("mode", "pp") != "none" and int(par.get("gpus", 1)) > 1) or staged:
+        # multi-GPU actor pipeline: one registered worker Pipeline per rank, hops over RCCL
+        import json
+        from ..parallel.launch import create_rank_pipeline, join, spawn_workers
+        from ..parallel.placement import make_plan
+        with open(definition_pathname) as f:
+            plan = make_plan(json.load(f))
+        _LOGGER.info(f"Parallel plan {plan.group}: stages {plan.stages} replicas {plan.replicas} "
+                     f"local_share {plan.local_share}")
+        spawn_workers(plan)
+        join(plan, 0)
+        pipeline = create_rank_pipeline(plan, 0, stream_id=stream_id, parameters=dict(parameters or {}),
+                                        frame_id=frame_id, frame_data=frame_data, grace_time=grace_time,
+                                        queue_response=response_queue, name=name, graph_path=graph_path,
+                                        stream_reset=stream_reset, definition_pathname=definition_pathname)
+        pipeline.run(mqtt_connection_required=True)
+        return
     pipeline = PipelineImpl.create_pipeline(definition_pathname, definition, name, graph_path, stream_id,
                                             parameters, frame_id, frame_data, grace_time,
                                             queue_response=response_queue, stream_reset=stream_reset)

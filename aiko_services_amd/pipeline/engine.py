@@ -36,7 +36,8 @@ from ..runtime.actor import Actor, ActorTopic
 from ..runtime.context import Interface, compose_instance, pipeline_args, pipeline_element_args
 from ..runtime.lease import Lease
 from ..runtime.process import aiko
-from ..runtime.service import ServiceFilter, ServiceProtocol
+from ..runtime.service import ServiceFilter, ServiceProtocol, ServiceTags
+from ..parallel import hop as _hop
 from ..utils import fault as _fault
 from ..utils import trace as _trace
 from ..utils.configuration import get_gpu_configuration
@@ -81,6 +82,8 @@ class PipelineGraph(Graph):
     @classmethod
     def get_element(cls, node):
         element = node.element
+        if isinstance(element, RemoteReplicas):
+            return element, node.name, False, "ready" if element.members else "absent"
         if type(element).__name__ == "ServiceRemoteProxy":
             return element, node.name, False, "ready"
         lifecycle = element.share["lifecycle"]
@@ -389,10 +392,11 @@ class PipelineImpl(Pipeline):
     @classmethod
     def create_pipeline(cls, definition_pathname, pipeline_definition, name, graph_path, stream_id,
                         parameters, frame_id, frame_data, grace_time, queue_response=None,
-                        stream_reset=False):
+                        stream_reset=False, tags=None):
         name = name or pipeline_definition.name
         init_args = pipeline_args(name, protocol=PROTOCOL_PIPELINE, definition=pipeline_definition,
-                                  definition_pathname=definition_pathname, graph_path=graph_path)
+                                  definition_pathname=definition_pathname, graph_path=graph_path,
+                                  tags=tags)
         pipeline = compose_instance(PipelineImpl, init_args)
         stream_dict = {"frame_id": int(frame_id or 0), "parameters": {}}
         parameters = dict(parameters or {})
@@ -471,27 +475,37 @@ class PipelineImpl(Pipeline):
         return graph
 
     def _pipeline_element_change_handler(self, command, service_details):
+        """Registrar add/remove of a service matching a remote element's filter.  Every
+        matching service becomes a member of the element's :class:`RemoteReplicas` (one for
+        the reference's single remote Pipeline; several when a stage is replicated).  A
+        ``rank=N`` tag marks a service reachable on the RCCL data plane (``parallel/hop.py``)."""
         if command not in ("add", "remove") or not service_details:
             return
         topic_path = f"{service_details[0]}/in"
         service_name = service_details[1]
         if service_name not in self.remote_pipelines:
             return
-        element_name, element_instance, element_topic_path = self.remote_pipelines[service_name]
+        element_name, element_instance, replicas = self.remote_pipelines[service_name]
         node = self.pipeline_graph.get_node(element_name)
-        definition = element_instance.definition
+        if replicas is None:
+            replicas = RemoteReplicas(element_instance.definition)
         if command == "add":
-            element_instance.set_remote_absent(False)
+            tags = ServiceTags.parse_tags(service_details[5] if len(service_details) > 5
+                                          and isinstance(service_details[5], list) else [])
             proxy = get_actor_mqtt(topic_path, PipelineRemote)
-            proxy.definition = definition
-            new_instance, new_tp = proxy, topic_path
-        elif topic_path == element_topic_path:
-            element_instance.set_remote_absent(True)
-            new_instance, new_tp = element_instance, None
-        else:
+            proxy.definition = element_instance.definition
+            rank = tags.get("rank")
+            proxy.hop_rank = int(rank) if rank not in (None, "") else None
+            replicas.add(topic_path, proxy, weight=float(tags.get("weight", 1) or 1))
+            element_instance.set_remote_absent(False)
+        elif not replicas.remove(topic_path):
             return
-        self.remote_pipelines[service_name] = (element_name, element_instance, new_tp)
-        node.element = new_instance
+        self.remote_pipelines[service_name] = (element_name, element_instance, replicas)
+        if replicas.members:
+            node.element = replicas
+        else:
+            element_instance.set_remote_absent(True)
+            node.element = element_instance
         self._update_lifecycle_state()
 
     # ---- streams -------------------------------------------------------------------------------
@@ -595,12 +609,31 @@ class PipelineImpl(Pipeline):
         stream = Stream()
         if not stream.update(stream_dict):
             self.logger.warning("Process frame: stream_dict must be a dictionary")
-            return None, None
+            return None, None, None
         if frame_data_in == [] or frame_data_in is None:
             frame_data_in = {}
         if not isinstance(frame_data_in, dict):
             self.logger.warning("Process frame: frame data must be a dictionary")
-            return None, None
+            return None, None, None
+        hop_handle = None
+        hop = _hop.plane()
+        if hop is not None and any(_hop.is_token(v) or isinstance(v, dict) for v in frame_data_in.values()):
+            # tensors of this message arrive over RCCL: always receive them (even if the frame is
+            # then rejected) so the link stays in order; forward hops land in FramePool slots
+            frame_data_in, hop_handle = hop.decode(frame_data_in, pooled=new_frame)
+        graph, stream = self._process_initialize_stream(stream, stream_dict, frame_data_in, new_frame)
+        if graph is None:
+            if hop_handle is not None:
+                hop.release([hop_handle])
+            return None, None, None
+        frame = stream.frames[stream.frame_id]
+        if hop_handle is not None:
+            frame.hop_handles.append(hop_handle)
+        if new_frame and stream_dict.get("hop_rank") is not None:
+            frame.hop_reply = int(stream_dict["hop_rank"])
+        return graph, stream, frame_data_in
+
+    def _process_initialize_stream(self, stream, stream_dict, frame_data_in, new_frame):
         stream_id = stream.stream_id
         if stream_id == DEFAULT_STREAM_ID and DEFAULT_STREAM_ID not in self.stream_leases:
             if not self.create_stream(DEFAULT_STREAM_ID, graph_path=stream.graph_path,
@@ -673,7 +706,7 @@ class PipelineImpl(Pipeline):
         return self._process_frame_body(stream_dict, frame_data_in, new_frame)
 
     def _process_frame_body(self, stream_dict, frame_data_in, new_frame):
-        graph, stream = self._process_initialize(stream_dict, frame_data_in, new_frame)
+        graph, stream, frame_data_in = self._process_initialize(stream_dict, frame_data_in, new_frame)
         if graph is None:
             return False
         frame_complete = True
@@ -696,6 +729,16 @@ class PipelineImpl(Pipeline):
                 header = (f'Error: Invoking Pipeline "{definition_pathname}": '
                           f'PipelineElement "{element_name}": process_frame()')
                 inputs = self._process_map_in(header, element, node.name, frame.swag)
+                target = None
+                if isinstance(element, RemoteReplicas) and self.share["lifecycle"] == "ready":
+                    target = element.pick()
+                    if isinstance(target, LocalStage):
+                        # this frame's share of a replicated stage runs in-process (no hop)
+                        stream_event, frame_data_out = target.run(stream.stream_id, frame_id, inputs)
+                        stream.state = self._process_stream_event(element_name, stream_event, frame_data_out)
+                        self._process_map_out(node.name, frame_data_out)
+                        frame.swag.update(frame_data_out)
+                        continue
                 if local:
                     start = time.time()
                     p_start = time.perf_counter() if tracer is not None else 0.0
@@ -743,7 +786,14 @@ class PipelineImpl(Pipeline):
                         frame_complete = False
                         frame_data_out = {}
                         frame.paused_pe_name = node.name
-                        element.process_frame({"stream_id": stream.stream_id, "frame_id": frame_id}, **inputs)
+                        target = target if target is not None else element
+                        stream_info = {"stream_id": stream.stream_id, "frame_id": frame_id}
+                        hop = _hop.plane()
+                        if hop is not None and getattr(target, "hop_rank", None) is not None:
+                            # metadata over MQTT, tensors over RCCL to the remote's rank
+                            stream_info["hop_rank"] = hop.rank
+                            inputs = hop.encode(target.hop_rank, inputs)
+                        target.process_frame(stream_info, **inputs)
                     break
             if frame_complete:
                 join = getattr(stream.frames.get(frame_id), "_hip_join", None)
@@ -764,12 +814,18 @@ class PipelineImpl(Pipeline):
                         frame_data_out = dict(frame.swag)
                     stream.queue_response.put((stream_info, frame_data_out))
                 elif stream.topic_response:
+                    hop = _hop.plane()
+                    reply = getattr(stream.frames.get(frame_id), "hop_reply", None)
+                    if hop is not None and reply is not None:
+                        frame_data_out = hop.encode(reply, frame_data_out)
                     get_actor_mqtt(stream.topic_response, Pipeline).process_frame_response(stream_info, frame_data_out)
                 else:
                     aiko.message.publish(self.topic_out, generate("process_frame", (stream_info, frame_data_out)))
         finally:
             if frame_complete:
-                stream.frames.pop(frame_id, None)
+                done = stream.frames.pop(frame_id, None)
+                if done is not None and done.hop_handles:
+                    _hop.plane().release(done.hop_handles)     # event-gated slot release
             self._disable_thread_local("process_frame")
             if stream.state == StreamState.DROP_FRAME:
                 stream.state = StreamState.RUN
@@ -852,8 +908,114 @@ class PipelineImpl(Pipeline):
     def get_element(self, name):
         return self.pipeline_graph.get_node(name).element
 
+    def set_remote_replicas(self, element_name, expected: int, local_definition=None, local_weight=0.0):
+        """Remote element ``element_name`` is a replicated stage: wait for ``expected`` members
+        (remote services + the local copy) before it is ready; with ``local_definition`` (a
+        PipelineDefinition) a copy of the stage runs in this process taking ``local_weight``
+        of the frames (``parallel/placement.py``)."""
+        for service_name, (name, instance, replicas) in list(self.remote_pipelines.items()):
+            if name != element_name:
+                continue
+            if replicas is None:
+                replicas = RemoteReplicas(instance.definition)
+            replicas.expected = int(expected)
+            if local_definition is not None and local_weight > 0:
+                child = PipelineImpl.create_pipeline("<local_stage>", local_definition,
+                                                     f"{local_definition.name}_local", None, None, [], 0,
+                                                     None, GRACE_TIME)
+                child.response_swag = getattr(self, "response_swag", False)
+                replicas.add("local", LocalStage(child), weight=local_weight)
+            self.remote_pipelines[service_name] = (name, instance, replicas)
+            if replicas.members:
+                self.pipeline_graph.get_node(name).element = replicas
+            self._update_lifecycle_state()
+            return replicas
+        raise KeyError(f"no remote element {element_name}")
+
 
 # ---- remote element placeholder --------------------------------------------------------------
+
+class RemoteReplicas:
+    """The discovered instances of one remote PipelineElement.
+
+    The reference binds a remote element to the single service its filter finds
+    (``/root/reference/src/aiko_services/main/pipeline.py:686-714``).  Here every matching
+    service is a member: streams are created / destroyed on all of them and each frame goes to
+    one, chosen by smooth weighted round-robin (service tag ``weight=w``, default 1) — a
+    replicated pipeline stage (PP x DP).  With one member this is exactly the reference hop.
+    """
+
+    def __init__(self, definition, expected: int = 1):
+        self.definition = definition
+        self.expected = expected        # members needed before the element counts as ready
+        self._members: "OrderedDict[str, list]" = OrderedDict()    # topic_path -> [proxy, weight, credit]
+
+    @property
+    def members(self):
+        return self._members if len(self._members) >= self.expected else {}
+
+    def add(self, topic_path, proxy, weight: float = 1.0):
+        self._members[topic_path] = [proxy, max(1e-6, float(weight)), 0.0]
+
+    def remove(self, topic_path) -> bool:
+        return self._members.pop(topic_path, None) is not None
+
+    def pick(self):
+        total = 0.0
+        best = None
+        for m in self._members.values():
+            m[2] += m[1]
+            total += m[1]
+            if best is None or m[2] > best[2]:
+                best = m
+        best[2] -= total
+        return best[0]
+
+    @property
+    def proxies(self):
+        return [m[0] for m in self._members.values()]
+
+    def create_stream(self, *args, **kwargs):
+        for p in self.proxies:
+            p.create_stream(*args, **kwargs)
+
+    def destroy_stream(self, *args, **kwargs):
+        for p in self.proxies:
+            p.destroy_stream(*args, **kwargs)
+
+    def __repr__(self):
+        return f"RemoteReplicas({list(self._members)})"
+
+
+class LocalStage:
+    """Member of a :class:`RemoteReplicas` that runs the replicated stage inside this process:
+    a child Pipeline built from the stage's definition, called synchronously (its graph must be
+    fully local).  Lets rank 0 take a share of the frames of the stage it feeds."""
+
+    def __init__(self, pipeline):
+        import queue as _queue
+        self.pipeline = pipeline
+        self.responses = _queue.Queue()
+        self.hop_rank = None
+
+    def create_stream(self, stream_id, graph_path=None, parameters=None, grace_time=GRACE_TIME,
+                      queue_response=None, topic_response=None):
+        self.pipeline.create_stream(stream_id, None, parameters, grace_time, queue_response=self.responses)
+
+    def destroy_stream(self, stream_id, graceful=False):
+        self.pipeline.destroy_stream(stream_id, graceful)
+
+    def run(self, stream_id, frame_id, inputs):
+        self.pipeline.process_frame({"stream_id": stream_id, "frame_id": frame_id}, dict(inputs))
+        try:
+            info, out = self.responses.get_nowait()
+        except Exception:
+            return StreamEvent.ERROR, {"diagnostic": "local stage replica produced no response"}
+        state = int(info.get("state", 0))
+        event_ = {StreamState.DROP_FRAME: StreamEvent.DROP_FRAME, StreamState.ERROR: StreamEvent.ERROR,
+                  StreamState.STOP: StreamEvent.STOP}.get(state, StreamEvent.OKAY)
+        return event_, dict(out)
+
 
 class PipelineRemote(PipelineElement):
 

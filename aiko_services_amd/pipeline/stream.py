@@ -57,6 +57,8 @@ class Frame:
     metrics: Dict[str, Any] = field(default_factory=dict)
     paused_pe_name: str = None     # remote element awaited (continuation point)
     swag: Dict[str, Any] = field(default_factory=dict)
+    hop_handles: list = field(default_factory=list)   # RCCL receive slots held by this frame
+    hop_reply: int = None          # rank to send the response tensors to (remote hop)
 
 
 @dataclass
