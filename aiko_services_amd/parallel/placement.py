@@ -132,8 +132,11 @@ def plan_stages(order, times_ms: dict, gpus: int, replicate: bool = True, local:
             if sum(reps) > gpus:
                 continue
             shares = [0.0]
-            if local and S == 2:              # rank 0 can host a copy of the (last) stage 1
-                shares = [i / 40 for i in range(0, 40)]
+            if local and S == 2 and t[1] > 0:
+                # rank 0 hosts a copy of stage 1 taking share s of its frames: balanced when
+                # t0 + s * t1 == (1 - s) * t1 / r1
+                r1 = reps[1]
+                shares.append(min(0.95, max(0.0, (t[1] - r1 * t[0]) / (t[1] * (1 + r1)))))
             for share in shares:
                 per_rank = predicted_times(t, reps, share)
                 key = (round(max(per_rank), 6), len(per_rank), -share)
@@ -181,6 +184,12 @@ def make_plan(definition: dict, gpus: int | None = None, stages=None, replicas=N
     par = definition.get("parallel") or {}
     mode = par.get("mode", "pp")
     gpus = int(gpus or par.get("gpus", 1))
+    if replicas is None and par.get("replicas") is not None:
+        replicas = [int(r) for r in par["replicas"]]
+    if not local_share and par.get("local_share") is not None:
+        local_share = float(par["local_share"])
+    if times_ms is None and par.get("times_ms"):
+        times_ms = {k: float(v) for k, v in par["times_ms"].items()}
     order = element_order(definition)
     by = {e["name"]: e for e in definition["elements"]}
     predicted = {}

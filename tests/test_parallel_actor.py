@@ -93,3 +93,41 @@ def test_plan_nested_stages():
     assert remote["deploy"]["remote"]["service_filter"]["name"] == "p_tensor_pp_s2"
     assert [i["name"] for i in remote["input"]] == ["t_submit", "x"]
     assert sorted(map(tuple, plan.links)) == [(0, 1), (1, 0), (1, 2), (2, 1)]
+
+
+def test_replicated_stage_matches_single_process(cluster):
+    """Stage 1 replicated on ranks 1 and 2 plus an in-process copy on rank 0 (PP x DP)."""
+    path = os.path.join(DEFS, "tensor_ppdp.json")
+    r, par = _create(cluster["env"], path, 8)
+    assert len(par) == 8, (r.returncode, r.stdout[-3000:], r.stderr[-3000:])
+    sent = {}
+    for topic, p in cluster["payloads"]:
+        if p.startswith(b"(process_frame ") and b"T@0/" in p:
+            sent[topic] = sent.get(topic, 0) + 1
+    assert len(sent) == 2, sent                       # both remote replicas got frames
+    with open(path) as f:
+        d = json.load(f)
+    d.pop("parallel")
+    for e in d["elements"]:
+        e["deploy"]["local"].pop("stage")
+    with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as f:
+        json.dump(d, f)
+    try:
+        _, single = _create(cluster["env"], f.name, 8)
+    finally:
+        os.unlink(f.name)
+    assert single == par
+
+
+def test_balancer_replicates_the_heavy_stage():
+    """Config 3 element times (1-GPU profile, ms per 256-frame batch): the planner replicates
+    ResNet-50 and gives rank 0 a share of it, so per-rank times are within 15 %."""
+    from aiko_services_amd.parallel.placement import plan_stages
+    order = ["SyntheticFrames", "ImagePreprocess", "ResNet50Classifier", "ClassifierTopK"]
+    times = {"SyntheticFrames": 0.01, "ImagePreprocess": 0.12, "ResNet50Classifier": 3.35,
+             "ClassifierTopK": 0.03}
+    for gpus in (2, 4, 8):
+        stages, reps, share, per_rank = plan_stages(order, times, gpus)
+        assert len(per_rank) == gpus, (stages, reps, share)
+        assert max(per_rank) <= 1.15 * min(per_rank), (gpus, stages, reps, share, per_rank)
+        assert max(per_rank) < sum(times.values()) / gpus * 1.1
