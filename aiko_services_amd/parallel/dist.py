@@ -82,14 +82,17 @@ def backend():
     return _backend
 
 
-def init(backend_name: str | None = None, timeout_s: float | None = None) -> bool:
-    """Initialise from the environment when WORLD_SIZE > 1; returns True if distributed."""
+def init(backend_name: str | None = None, timeout_s: float | None = None, force: bool = False) -> bool:
+    """Initialise from the environment when WORLD_SIZE > 1 (or ``force``: a world of one,
+    e.g. to exercise the RCCL code paths on a single GPU); returns True if distributed."""
     global _backend
     if is_initialized():
         return True
     ws = int(os.environ.get("WORLD_SIZE", "1"))
-    if ws <= 1:
+    if ws <= 1 and not force:
         return False
+    os.environ.setdefault("WORLD_SIZE", str(ws))
+    os.environ.setdefault("RANK", "0")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29500")
     from ..utils.configuration import get_gpu_configuration

@@ -160,12 +160,33 @@ class HopPlane:
         self.send_links: dict = {}
         self.recv_links: dict = {}
         self.links = [tuple(int(x) for x in l) for l in links]
+        self._loop: deque = deque()        # loopback link (src == dst): staged buffers in order
         for src, dst in self.links:
+            if src == dst:
+                if src == self.rank:
+                    self.send_links[dst] = _SendLink(dst, None, self.device, self.depth)
+                    self.recv_links[src] = _RecvLink(src, None, self.device, self.depth)
+                continue
             group = tdist.new_group(ranks=sorted({src, dst})) if D.is_initialized() else None
             if src == self.rank:
                 self.send_links[dst] = _SendLink(dst, group, self.device, self.depth)
             elif dst == self.rank:
                 self.recv_links[src] = _RecvLink(src, group, self.device, self.depth)
+        # Bring every link's communicator up now, in the same global order on every rank: RCCL
+        # creates a P2P communicator lazily at the first send/recv and blocks until the peer
+        # joins, but the peer only posts its receive once the frame's MQTT message arrives —
+        # which is published after the send.  A tiny exchange per link here breaks that cycle.
+        for src, dst in self.links:
+            if self.rank not in (src, dst) or src == dst or not D.is_initialized():
+                continue
+            link = self.send_links.get(dst) if src == self.rank else self.recv_links.get(src)
+            t = torch.zeros(1, dtype=torch.int64, device=self.device)
+            if src == self.rank:
+                tdist.isend(t, dst, group=link.group).wait()
+            else:
+                tdist.irecv(t, src, group=link.group).wait()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
         # host-side control group (gloo) for start-up barriers issued from helper threads
         self.control = tdist.new_group(backend="gloo") if D.is_initialized() else None
         self._releases: deque = deque()     # (event | None, pool, slot)
@@ -225,8 +246,12 @@ class HopPlane:
             container[key] = (f"{TOKEN}{self.rank}/{seq}/{idx}/{str(dt).split('.')[-1]}/"
                               + "x".join(str(int(s)) for s in shape))
         D._account("hop_send", total)
-        link.pending[slot] = tdist.isend(buf[:total], dst, group=link.group) if link.group is not None \
-            else None
+        if int(dst) == self.rank:               # loopback: the receiver copies from the stage
+            self._loop.append(buf)
+            link.pending[slot] = None
+        else:
+            link.pending[slot] = tdist.isend(buf[:total], dst, group=link.group) if link.group is not None \
+                else None
         self.counters["sent_msgs"] += 1
         self.counters["sent_bytes"] += total
         return out
@@ -282,7 +307,9 @@ class HopPlane:
         else:
             handle, buf = None, torch.empty(total, dtype=torch.uint8, device=self.device)
         D._account("hop_recv", total)
-        if link.group is not None:
+        if src == self.rank:
+            buf[:total].copy_(self._loop.popleft()[:total], non_blocking=True)
+        elif link.group is not None:
             tdist.irecv(buf[:total], src, group=link.group).wait()    # RCCL: the stream waits
         self.counters["recv_msgs"] += 1
         self.counters["recv_bytes"] += total

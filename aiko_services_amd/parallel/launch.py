@@ -81,8 +81,11 @@ def join(plan: Plan, rank: int, timeout_s: float = 120.0):
 
 def create_rank_pipeline(plan: Plan, rank: int, stream_id=None, parameters=None, frame_id=0,
                          frame_data=None, grace_time=60, queue_response=None, name=None,
-                         graph_path=None, stream_reset=False, definition_pathname="<parallel>"):
-    """This rank's stage Pipeline; on rank 0 also binds replicated / local stage members."""
+                         graph_path=None, stream_reset=False, definition_pathname="<parallel>",
+                         auto_start=True):
+    """This rank's stage Pipeline; on rank 0 also binds replicated / local stage members.
+    ``auto_start``: a helper thread waits until the stage is ready, joins the start barrier and
+    (rank 0) creates the stream — embedders that drive frames themselves pass False."""
     from ..pipeline.definition import parse_pipeline_definition_dict
     from ..pipeline.engine import PipelineImpl
     spec = plan.ranks[rank]
@@ -113,7 +116,8 @@ def create_rank_pipeline(plan: Plan, rank: int, stream_id=None, parameters=None,
             _, arguments = parse(f"(process_frame {frame_data})")
             pipeline.create_frame({"stream_id": stream_id or "*", "frame_id": int(frame_id or 0),
                                    "parameters": {}}, arguments[0])
-    start_when_ready(pipeline, start if rank == 0 else None)
+    if auto_start:
+        start_when_ready(pipeline, start if rank == 0 else None)
     return pipeline
 
 

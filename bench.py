@@ -121,10 +121,10 @@ def whisper_definition(streams: int, graph: bool, size: str, chunk: float, windo
     }
 
 
-def pp_definition(batch: int, graph: bool, height: int, width: int, world: int) -> dict:
-    """BASELINE config 3: decode -> resize/normalise -> ResNet-50 -> post-process, one stage per
-    GPU (``deploy.local.stage`` = i * world // 4, so fewer GPUs fold neighbouring stages)."""
-    d = definition(batch, graph, height, width)
+def pp_definition(batch: int, graph: bool, height: int, width: int, world: int, lanes: int = 1) -> dict:
+    """BASELINE config 3: decode -> resize/normalise -> ResNet-50 -> post-process, placed over
+    ``world`` GPUs by the balancer (``parallel/placement.py``)."""
+    d = definition(batch, graph, height, width, lanes)
     d["name"] = "p_resnet50_pp"
     d["graph"] = ["(SyntheticFrames ImagePreprocess ResNet50Classifier ClassifierTopK)"]
     pre = {"name": "ImagePreprocess", "input": [{"name": "images", "type": "tensor"}],
@@ -132,8 +132,7 @@ def pp_definition(batch: int, graph: bool, height: int, width: int, world: int) 
            "deploy": {"local": {"module": ELEMENTS}}}
     d["elements"].insert(1, pre)
     d["elements"][3]["parameters"]["gather"] = False
-    for i, e in enumerate(d["elements"]):
-        e["deploy"]["local"]["stage"] = i * world // 4
+    d["parallel"] = {"mode": "pp", "gpus": world}
     return d
 
 
@@ -162,7 +161,10 @@ def main(argv=None):
                     help="(yolov8n) RCCL fan-out of the ingest rank's frame batch")
     ap.add_argument("--parallel", choices=["dp", "pp"], default="dp",
                     help="dp: every GPU runs the whole pipeline (config 2/headline); "
-                         "pp: one pipeline stage per GPU over RCCL P2P (config 3)")
+                         "pp: config 3 as balanced multi-GPU actor pipelines (stages + replicas, "
+                         "MQTT metadata, RCCL P2P tensors)")
+    ap.add_argument("--element-times", default=None,
+                    help="(pp) JSON {element: ms per batch} for the stage balancer")
     a = ap.parse_args(argv)
     explicit_hw = "--height" in (argv or sys.argv)
     if (a.parallel == "pp" or a.model == "yolov8n") and not explicit_hw:
@@ -172,6 +174,8 @@ def main(argv=None):
     if a.model.startswith("whisper") and "--batch" not in (argv or sys.argv):
         a.batch = 16
 
+    procs = _control_plane(int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))) \
+        if a.parallel == "pp" else []
     from aiko_services_amd.parallel import dist as D
     D.init()
     ws, rank = D.world_size(), D.rank()
@@ -186,7 +190,7 @@ def main(argv=None):
     from aiko_services_amd.pipeline.engine import PipelineImpl
 
     if a.parallel == "pp":
-        return run_pp(a, device)
+        return run_pp(a, device, procs)
     metric, unit = METRIC, "frames/s"
     if a.model.startswith("whisper"):
         size = a.model.split("-", 1)[1]
@@ -280,75 +284,142 @@ def main(argv=None):
     D.destroy()
 
 
-def run_pp(a, device):
-    """Config 3: the stages of one pipeline spread over the GPUs; frames/s counted at the last
-    stage (each frame batch is processed once by the whole node)."""
+# per-element GPU ms per 256-frame batch on one MI355X (VGA frames), the balancer's default input
+# (override: --element-times '{"ResNet50Classifier": 3.3, ...}')
+PP_ELEMENT_MS = {"SyntheticFrames": 0.01, "ImagePreprocess": 0.12, "ResNet50Classifier": 3.35,
+                 "ClassifierTopK": 0.03}
+
+
+def _control_plane(ws, rank):
+    """Config 3 runs as actor pipelines: an MQTT broker and a registrar (subprocesses of rank 0,
+    started before anything touches the GPU) carry discovery and per-frame metadata."""
+    import subprocess
+    port = int(os.environ.get("MASTER_PORT", "29500")) + 7
+    os.environ.update({"AIKO_MQTT_HOST": "127.0.0.1", "AIKO_MQTT_PORT": str(port), "AIKO_MQTT_DISABLE": "0",
+                       "AIKO_NAMESPACE": f"bench{port}", "AIKO_REGISTRAR_SEARCH_TIMEOUT": "0.5",
+                       "AIKO_LOG_MQTT": "false"})
+    procs = []
+    if rank == 0:
+        procs.append(subprocess.Popen([sys.executable, "-m", "aiko_services_amd.message.mqtt_broker",
+                                       "--host", "127.0.0.1", "--port", str(port)],
+                                      stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL))
+        import socket
+        deadline = time.time() + 60
+        while True:                            # a fresh box's first python start can take a while
+            try:
+                socket.create_connection(("127.0.0.1", port), timeout=0.5).close()
+                break
+            except OSError:
+                if time.time() > deadline or procs[0].poll() is not None:
+                    raise RuntimeError(f"MQTT broker did not start on port {port}")
+                time.sleep(0.1)
+        procs.append(subprocess.Popen([sys.executable, "-m", "aiko_services_amd.tools.registrar"],
+                                      stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL))
+    return procs
+
+
+def run_pp(a, device, procs):
+    """Config 3 as multi-GPU ACTOR pipelines (the path ``aiko_pipeline create`` takes for a
+    ``parallel`` definition): the balancer cuts decode -> resize -> ResNet-50 -> post-process
+    into stages and replicas (``parallel/placement.py``), every rank runs its stage Pipeline
+    registered with the registrar, frames hop between ranks as ``process_frame`` metadata over
+    MQTT with the tensors on RCCL P2P (``parallel/hop.py``).  frames/s counted at rank 0 (each
+    frame batch is processed once by the whole node)."""
+    import threading
     from aiko_services_amd.parallel import dist as D
-    from aiko_services_amd.parallel.pipeline_parallel import PipelineParallelRunner
-    from aiko_services_amd.pipeline.definition import parse_pipeline_definition_dict
+    from aiko_services_amd.parallel import hop
+    from aiko_services_amd.parallel.launch import create_rank_pipeline
+    from aiko_services_amd.parallel.placement import make_plan
+    from aiko_services_amd.runtime.process import aiko
     ws, rank = D.world_size(), D.rank()
-    d = parse_pipeline_definition_dict(pp_definition(a.batch, not a.no_graph, a.height, a.width, ws))
-    D.barrier()
-    runner = PipelineParallelRunner(d, device=device, depth=2, stream_id="bench")
-    inflight: deque = deque()
+    times = dict(PP_ELEMENT_MS, **(json.loads(a.element_times) if a.element_times else {}))
+    d = pp_definition(a.batch, not a.no_graph, a.height, a.width, ws, a.lanes)
+    plan = make_plan(d, gpus=ws, times_ms=times, group=f"bench{os.environ.get('MASTER_PORT', '0')}")
+    plane = hop.init_plane(plan.links, device=device, depth=4)
+    responses: queue.Queue = queue.Queue()
+    pipeline = create_rank_pipeline(plan, rank, queue_response=responses if rank == 0 else None,
+                                    grace_time=3600, auto_start=False)
+    result = {}
+
+    def driver():
+        torch.cuda.set_device(device)
+        try:
+            result["out"] = _drive_pp(a, pipeline, plane, plan, responses, rank, ws)
+        except BaseException as exc:          # report, but still release the other ranks
+            result["error"] = repr(exc)
+        plane.barrier()                        # rank 0 finished timing: everyone stops
+        aiko.process.terminate(0)
+
+    threading.Thread(target=driver, daemon=True, name="bench-driver").start()
+    try:
+        aiko.process.run(mqtt_connection_required=True)    # event loop on the main thread
+    except SystemExit as exc:
+        if exc.code:
+            result.setdefault("error", f"event loop exit {exc.code} (MQTT broker unreachable?)")
+    if result.get("out") is not None:
+        print(json.dumps(result["out"]), flush=True)
+    for p in procs:
+        p.terminate()
+    if result.get("error") or (rank == 0 and result.get("out") is None):
+        print(f"rank {rank}: {result.get('error', 'no result')}", file=sys.stderr, flush=True)
+        os._exit(1)
+    os._exit(0)
+
+
+def _drive_pp(a, pipeline, plane, plan, responses, rank, ws):
+    deadline = time.time() + 120
+    while pipeline.share.get("lifecycle") != "ready":
+        if time.time() > deadline:
+            raise RuntimeError(f"rank {rank}: stage pipeline not ready (downstream not discovered)")
+        time.sleep(0.02)
+    plane.barrier()                            # every stage of the plan is up
+    if rank != 0:
+        return None
+    from aiko_services_amd.runtime.actor import ActorTopic
+    pipeline._post_message(ActorTopic.IN, "create_stream", ["bench", None, {}, 3600, responses, None])
+    while "bench" not in pipeline.stream_leases:
+        time.sleep(0.01)
+    depth = max(a.depth, 2 * ws)
+    state = {"frame_id": 0}
     latencies: list = []
 
-    def step(record):
-        r = runner.step({})
-        if r is None:
-            return
-        info, out = r
-        if info["state"] != 0:
-            raise RuntimeError(f"pipeline frame failed: {info} {out}")
-        inflight.append((out["topk"], record))
-        while len(inflight) > a.depth:
-            res, rec = inflight.popleft()
+    def run(n, record):
+        sent = done = 0
+        while done < n:
+            while sent < n and sent - done < depth:
+                pipeline.create_frame({"stream_id": "bench", "frame_id": state["frame_id"]}, {})
+                state["frame_id"] += 1
+                sent += 1
+            info, o = responses.get(timeout=120)
+            done += 1
+            if info["state"] != 0:
+                raise RuntimeError(f"pipeline frame failed: {info} {o}")
+            res = o["topk"]
             res.wait()
-            if rec:
+            if record:
                 latencies.append(res.latency)
-
-    def drain(record=True):
-        while inflight:
-            res, rec = inflight.popleft()
-            res.wait()
-            if rec and record:
-                latencies.append(res.latency)
-
-    for _ in range(a.warmup):
-        step(False)
-    drain(False)
-    torch.cuda.synchronize()
-    D.barrier()
+    run(max(a.warmup, 3 * ws), False)          # every replica tunes + captures its graphs
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step(True)
-    runner.finish()
-    drain()
-    torch.cuda.synchronize()
-    D.barrier()
+    run(a.steps, True)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed, statistics.median(latencies) if latencies else 0.0],
-                     dtype=torch.float64, device=device)
-    D.all_reduce_max(t)
-    elapsed, p50 = float(t[0]), float(t[1])
-    fps = a.batch * a.steps / elapsed
-    if rank == 0:
-        print(json.dumps({
-            "metric": METRIC, "value": round(fps, 1), "unit": "frames/s", "n_gpus": ws,
-            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
-            "data": f"synthetic (random uint8 {a.height}x{a.width} frames generated in HBM; random-init weights)",
-            "p50_latency_ms": round(p50 * 1e3, 3),
-            "config": {"model": "resnet50", "global_batch": a.batch, "seq_len": None,
-                       "image_size": [224, 224], "frame_size": [a.height, a.width],
-                       "per_gpu_batch": a.batch, "parallelism": f"pp{ws}", "hipgraph": not a.no_graph,
-                       "stages": runner.stages,
-                       "pipeline": "(SyntheticFrames ImagePreprocess ResNet50Classifier ClassifierTopK)"},
-        }), flush=True)
-    D.barrier()
-    D.destroy()
+    p50 = statistics.median(latencies) if latencies else 0.0
+    return {
+        "metric": METRIC, "value": round(a.batch * a.steps / elapsed, 1), "unit": "frames/s", "n_gpus": ws,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
+        "data": f"synthetic (random uint8 {a.height}x{a.width} frames generated in HBM; random-init weights)",
+        "p50_latency_ms": round(p50 * 1e3, 3),
+        "config": {"model": "resnet50", "global_batch": a.batch, "seq_len": None,
+                   "image_size": [224, 224], "frame_size": [a.height, a.width],
+                   "per_gpu_batch": a.batch, "parallelism": f"pp{ws}", "hipgraph": not a.no_graph,
+                   "stages": plan.stages, "replicas": plan.replicas, "local_share": round(plan.local_share, 4),
+                   "predicted_rank_ms": plan.predicted_ms.get("per_rank_ms"),
+                   "transport": "actor pipelines: MQTT metadata + RCCL P2P tensors",
+                   "hop": plane.stats(),
+                   "pipeline": "(SyntheticFrames ImagePreprocess ResNet50Classifier ClassifierTopK)"},
+    }
 
 
 if __name__ == "__main__":

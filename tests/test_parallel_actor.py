@@ -131,3 +131,21 @@ def test_balancer_replicates_the_heavy_stage():
         assert len(per_rank) == gpus, (stages, reps, share)
         assert max(per_rank) <= 1.15 * min(per_rank), (gpus, stages, reps, share, per_rank)
         assert max(per_rank) < sum(times.values()) / gpus * 1.1
+
+
+def test_hop_loopback_cpu():
+    """Hop encode/decode on a loopback link (no process group): tokens, packing, FramePool
+    slot, float and DeviceResult round trip."""
+    import torch
+    from aiko_services_amd.gpu.element import DeviceResult
+    from aiko_services_amd.parallel.hop import HopPlane
+    plane = HopPlane([(0, 0)], device="cpu", depth=2)
+    x = torch.randn(5, 7)
+    msg = plane.encode(0, {"x": x, "s": "keep", "t": 0.25,
+                           "r": DeviceResult({"a": torch.arange(3)}, None, t_submit=1.0)})
+    assert msg["s"] == "keep" and msg["t"] == "F@0.25" and msg["x"].startswith("T@0/0/0/float32/5x7")
+    got, handle = plane.decode(msg)
+    assert torch.equal(got["x"], x) and got["t"] == 0.25 and got["s"] == "keep"
+    assert torch.equal(got["r"].wait()["a"], torch.arange(3)) and got["r"].t_submit == 1.0
+    plane.release([handle])
+    assert plane.stats()["pool_free_from_0"] == 4
