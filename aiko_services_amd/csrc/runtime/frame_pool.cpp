@@ -15,6 +15,7 @@
 
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <vector>
 
@@ -30,8 +31,7 @@ class FramePool : public torch::CustomClassHolder {
       opts = opts.device(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(device_index)));
     }
     storage_ = at::empty({num_slots_ * slot_bytes_}, opts);
-    free_.reserve(num_slots_);
-    for (int64_t i = num_slots_ - 1; i >= 0; --i) free_.push_back(i);
+    for (int64_t i = 0; i < num_slots_; ++i) free_.push_back(i);   // FIFO: slots rotate
     in_use_.assign(num_slots_, 0);
   }
 
@@ -46,8 +46,8 @@ class FramePool : public torch::CustomClassHolder {
       return -1;
     }
     if (closed_ || free_.empty()) return -1;
-    const int64_t slot = free_.back();
-    free_.pop_back();
+    const int64_t slot = free_.front();
+    free_.pop_front();
     in_use_[slot] = 1;
     const int64_t used = num_slots_ - static_cast<int64_t>(free_.size());
     if (used > high_water_) high_water_ = used;
@@ -103,7 +103,7 @@ class FramePool : public torch::CustomClassHolder {
   at::Tensor storage_;
   std::mutex mu_;
   std::condition_variable cv_;
-  std::vector<int64_t> free_;
+  std::deque<int64_t> free_;
   std::vector<uint8_t> in_use_;
   bool closed_ = false;
   int64_t high_water_ = 0, acquired_ = 0, exhausted_ = 0;

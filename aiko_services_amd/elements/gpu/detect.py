@@ -68,11 +68,18 @@ class FrameFanout(GpuPipelineElement):
         return StreamEvent.OKAY, {"images": mine}
 
     def _buf(self, key, shape):
-        k = (key, shape, self.lane)
-        t = self._bufs.get(k)
-        if t is None:
-            t = self._bufs[k] = torch.empty(shape, dtype=torch.uint8, device=self.device)
-        return t
+        """Receive buffer of this frame: a slot of a per-shape HBM FramePool, held until the
+        frame completes (stable addresses: the detector's graphs capture on the slots)."""
+        from ...gpu.element import FramePool
+        k = (key, shape)
+        pool = self._bufs.get(k)
+        if pool is None:
+            n = shape[0] * shape[1] * shape[2] * shape[3]
+            pool = self._bufs[k] = FramePool(_int(self.get_parameter("pool", 4)[0], 4), n, device=self.device)
+            self.frame_pool = pool
+        slot = pool.acquire()
+        self.hold_for_frame(pool, slot)
+        return pool.view(slot, shape, torch.uint8)
 
 
 class YoloDetector(GpuPipelineElement):

@@ -36,13 +36,42 @@ def _int(v, d):
 
 
 class SyntheticFrames(GpuPipelineElement):
+    """The "decode" stage: frame batches written into slots of an HBM :class:`FramePool` (each
+    slot filled once with random pixels, like a hardware decoder writing device memory).  Every
+    frame holds its slot until the frame completes and the GPU is done with it; with all
+    ``pool`` slots in flight the next frame waits for the oldest (back-pressure on the device
+    queue) or — ``on_exhausted: drop`` — is dropped (DROP_FRAME).  Stable slot addresses let
+    the downstream hipGraphs be captured on the slots themselves (no input copy)."""
     lane_safe = True          # read-only frame pool
 
     def __init__(self, context):
         context.set_protocol("synthetic_frames:0")
         super().__init__(context)
-        self._pool = None
-        self._cursor = 0
+        self.frame_pool = None
+        self._shape = None
+        self.dropped = 0
+
+    def _ensure_pool(self, glob):
+        if self.frame_pool is not None:
+            return
+        from ...gpu.element import FramePool
+        B = _int(self.get_parameter("batch", 1)[0], 1)
+        if glob:
+            from ...parallel import dist as D
+            B *= D.world_size()
+        H = _int(self.get_parameter("height", 224)[0], 224)
+        W = _int(self.get_parameter("width", 224)[0], 224)
+        n = max(1, _int(self.get_parameter("pool", 2)[0], 2))
+        seed = _int(self.get_parameter("seed", 0)[0], 0)
+        self._shape = (B, H, W, 3)
+        self.frame_pool = FramePool(n, B * H * W * 3, device=self.device)
+        g = torch.Generator(device=self.device).manual_seed(seed)
+        slots = [self.frame_pool.acquire(0) for _ in range(n)]
+        for s in slots:
+            v = self.frame_pool.view(s, self._shape, torch.uint8)
+            v.copy_(torch.randint(0, 256, self._shape, dtype=torch.uint8, device=self.device, generator=g))
+        for s in slots:
+            self.frame_pool.release_after(s)
 
     def _frames(self):
         glob = str(self.get_parameter("global", False)[0]).lower() in ("true", "1", "yes")
@@ -52,21 +81,14 @@ class SyntheticFrames(GpuPipelineElement):
             from ...parallel import dist as D
             if D.rank() != _int(self.get_parameter("src", 0)[0], 0):
                 return None
-        if self._pool is None:
-            B = _int(self.get_parameter("batch", 1)[0], 1)
-            if glob:
-                from ...parallel import dist as D
-                B *= D.world_size()
-            H = _int(self.get_parameter("height", 224)[0], 224)
-            W = _int(self.get_parameter("width", 224)[0], 224)
-            n = _int(self.get_parameter("pool", 2)[0], 2)
-            seed = _int(self.get_parameter("seed", 0)[0], 0)
-            g = torch.Generator(device=self.device).manual_seed(seed)
-            self._pool = [torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=self.device,
-                                        generator=g) for _ in range(max(1, n))]
-        frames = self._pool[self._cursor % len(self._pool)]
-        self._cursor += 1
-        return frames
+        self._ensure_pool(glob)
+        drop = str(self.get_parameter("on_exhausted", "block")[0]).lower() == "drop"
+        timeout = self.get_parameter("acquire_timeout", None)[0]
+        slot = self.frame_pool.acquire(0.0 if drop else (float(timeout) if timeout is not None else None))
+        if slot < 0:
+            return False
+        self.hold_for_frame(self.frame_pool, slot)
+        return self.frame_pool.view(slot, self._shape, torch.uint8)
 
     def start_stream(self, stream, stream_id):
         limit, found = self.get_parameter("frames")
@@ -84,7 +106,12 @@ class SyntheticFrames(GpuPipelineElement):
         return StreamEvent.OKAY, {"t_submit": time.perf_counter()}
 
     def process_frame(self, stream, **kwargs):
-        return StreamEvent.OKAY, {"images": self._frames(), "t_submit": kwargs.get("t_submit", time.perf_counter())}
+        frames = self._frames()
+        if frames is False:
+            self.dropped += 1
+            self.share["frames_dropped"] = self.dropped
+            return StreamEvent.DROP_FRAME, {"diagnostic": "frame pool exhausted"}
+        return StreamEvent.OKAY, {"images": frames, "t_submit": kwargs.get("t_submit", time.perf_counter())}
 
 
 class ImagePreprocess(GpuPipelineElement):

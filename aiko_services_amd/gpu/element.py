@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import time
 import weakref
+from collections import deque
 
 import torch
 
@@ -33,20 +34,56 @@ _DTYPE_CODES = {torch.uint8: 0, torch.int8: 1, torch.int16: 2, torch.int32: 3, t
 
 
 class FramePool:
-    """Fixed-size HBM slots with blocking acquire (back-pressure) — native implementation."""
+    """Fixed-size HBM slots with blocking acquire (back-pressure) — native implementation.
+
+    ``release_after(slot)`` is the GPU-aware release: the slot returns to the pool once the
+    work queued so far on the current stream has finished (a HIP event, polled on the next
+    ``acquire``), so a frame's buffers are recycled only after its kernels stopped reading
+    them.  ``acquire(timeout)`` first retires completed releases, then — while releases are
+    still pending on the GPU — waits for the oldest one (back-pressure on the device queue)
+    before falling back to the native blocking wait; -1 on timeout."""
 
     def __init__(self, num_slots: int, slot_bytes: int, device=None):
         from ..ops import require_native
         require_native()
-        dev = parse_device(device) if device is not None else None
+        dev = parse_device(device) if device is not None and str(device) != "cpu" else None
+        self.device = dev if dev is not None else torch.device("cpu")
         self._pool = torch.classes.aiko.FramePool(int(num_slots), int(slot_bytes),
                                                   dev.index if dev is not None and dev.type == "cuda" else -1)
+        self._pending = deque()         # (event | None, slot)
+
+    def _reap(self, block: bool = False) -> None:
+        while self._pending:
+            ev, slot = self._pending[0]
+            if ev is not None and not ev.query():
+                if not block:
+                    return
+                ev.synchronize()
+                block = False
+            self._pending.popleft()
+            self._pool.release(int(slot))
 
     def acquire(self, timeout: float | None = None) -> int:
+        self._reap()
+        slot = self._pool.acquire(0)
+        if slot >= 0:
+            return slot
+        if self._pending:
+            self._reap(block=True)
+            slot = self._pool.acquire(0)
+            if slot >= 0:
+                return slot
         return self._pool.acquire(-1 if timeout is None else int(timeout * 1000))
 
     def release(self, slot: int) -> None:
         self._pool.release(int(slot))
+
+    def release_after(self, slot: int) -> None:
+        ev = None
+        if self.device.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+        self._pending.append((ev, int(slot)))
 
     def view(self, slot: int, shape, dtype=torch.uint8) -> torch.Tensor:
         return self._pool.view(int(slot), list(shape), _DTYPE_CODES[dtype])
@@ -168,10 +205,12 @@ def named_stream(name: str, device) -> "torch.cuda.Stream":
 
 
 class CapturedCall:
-    """hipGraph capture of ``fn(*static_inputs)`` for one input signature."""
+    """hipGraph capture of ``fn(*static_inputs)`` for one input signature.  ``static=True``
+    captures against the given input tensors themselves (stable FramePool slot addresses):
+    replays then read the producer's buffer directly, no input copy."""
 
-    def __init__(self, fn, example_inputs, warmup: int = 1):
-        self.static_inputs = [t.clone() for t in example_inputs]
+    def __init__(self, fn, example_inputs, warmup: int = 1, static: bool = False):
+        self.static_inputs = list(example_inputs) if static else [t.clone() for t in example_inputs]
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -186,6 +225,10 @@ class CapturedCall:
         for dst, src in zip(self.static_inputs, inputs):
             if dst.data_ptr() != src.data_ptr():
                 dst.copy_(src, non_blocking=True)
+        self.graph.replay()
+        return self.static_outputs
+
+    def graph_replay(self):
         self.graph.replay()
         return self.static_outputs
 
@@ -236,15 +279,41 @@ class GpuPipelineElement(PipelineElement):
         from .lanes import current_lane
         return current_lane()
 
+    # distinct input addresses per (key, lane) that get their own graph (frame-pool slots)
+    max_graphs_per_key = 16
+
     def run_maybe_captured(self, key, fn, *inputs):
+        """Replay a hipGraph of ``fn`` for this input signature and lane.  Inputs with stable
+        addresses (a FramePool's slots cycling) get one graph per slot address, captured on the
+        slot itself — no per-frame input copy; beyond ``max_graphs_per_key`` addresses the
+        element falls back to one graph with copied-in static inputs."""
         if not self.use_graph:
             return fn(*inputs)
-        key = (key, self.lane)
-        call = self._captured.get(key)
+        base = (key, self.lane)
+        addrs = tuple(t.data_ptr() for t in inputs)
+        seen = self._captured.setdefault(("addrs",) + base, set())
+        if addrs in seen or len(seen) < self.max_graphs_per_key:
+            k = base + (addrs,)
+            call = self._captured.get(k)
+            if call is None:
+                call = CapturedCall(fn, inputs, static=True)
+                self._captured[k] = call
+                seen.add(addrs)
+            return call.graph_replay()
+        call = self._captured.get(base)
         if call is None:
             call = CapturedCall(fn, inputs)
-            self._captured[key] = call
+            self._captured[base] = call
         return call(*inputs)
+
+    def hold_for_frame(self, pool: "FramePool", slot: int) -> None:
+        """Keep ``slot`` of ``pool`` until the frame being processed completes, then release it
+        once the GPU is done with the frame (``FramePool.release_after``)."""
+        frame = self.pipeline.current_frame() if self.pipeline is not None else None
+        if frame is None:
+            pool.release_after(slot)
+        else:
+            frame.on_complete.append(lambda: pool.release_after(slot))
 
     def stream_enter(self, frame):
         """Engine hook before process_frame: order this element after the producers of its

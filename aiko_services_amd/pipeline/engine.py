@@ -383,6 +383,13 @@ class PipelineImpl(Pipeline):
         assert stream, "thread_local.stream must be assigned"
         return stream, self.thread_local.frame_id
 
+    def current_frame(self):
+        """The Frame being processed on this thread (None outside ``process_frame``)."""
+        stream = getattr(self.thread_local, "stream", None)
+        if stream is None:
+            return None
+        return stream.frames.get(self.thread_local.frame_id)
+
     # ---- construction ----------------------------------------------------------------------------
     def create_frame(self, stream_dict, frame_data):
         if isinstance(stream_dict, Stream):
@@ -824,8 +831,11 @@ class PipelineImpl(Pipeline):
         finally:
             if frame_complete:
                 done = stream.frames.pop(frame_id, None)
-                if done is not None and done.hop_handles:
-                    _hop.plane().release(done.hop_handles)     # event-gated slot release
+                if done is not None:
+                    if done.hop_handles:
+                        _hop.plane().release(done.hop_handles)     # event-gated slot release
+                    for callback in done.on_complete:               # e.g. FramePool slots
+                        callback()
             self._disable_thread_local("process_frame")
             if stream.state == StreamState.DROP_FRAME:
                 stream.state = StreamState.RUN

@@ -59,6 +59,7 @@ class Frame:
     swag: Dict[str, Any] = field(default_factory=dict)
     hop_handles: list = field(default_factory=list)   # RCCL receive slots held by this frame
     hop_reply: int = None          # rank to send the response tensors to (remote hop)
+    on_complete: list = field(default_factory=list)   # callbacks when the frame completes
 
 
 @dataclass

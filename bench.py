@@ -49,7 +49,7 @@ def definition(batch: int, graph: bool, height: int, width: int, lanes: int = 1)
         "parameters": {"gpu_lanes": lanes},
         "elements": [
             el("SyntheticFrames", [], ["images", "t_submit"],
-               {"batch": batch, "height": height, "width": width, "pool": 4}),
+               {"batch": batch, "height": height, "width": width, "pool": 6}),
             el("ResNet50Classifier", ["images"], ["logits"], {"graph": graph}),
             el("ClassifierTopK", ["logits", "t_submit"], ["topk"], {"k": 5, "gather": True}),
         ],
@@ -72,7 +72,7 @@ def yolo_definition(batch: int, graph: bool, height: int, width: int, fanout: st
         "parameters": {"gpu_lanes": lanes},
         "elements": [
             el("SyntheticFrames", ELEMENTS, [], ["images", "t_submit"],
-               {"batch": batch, "height": height, "width": width, "pool": 2, "global": True}),
+               {"batch": batch, "height": height, "width": width, "pool": 4, "global": True}),
             el("FrameFanout", DETECT, ["images"], ["images"],
                {"mode": fanout, "batch": batch, "height": height, "width": width}),
             el("YoloDetector", DETECT, ["images"], ["detections", "counts"], {"graph": graph, "scale": "n"}),
