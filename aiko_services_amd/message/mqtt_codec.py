@@ -169,6 +169,8 @@ def topic_matches(filter_: str, topic: str) -> bool:
         return True
     f = filter_.split("/")
     t = topic.split("/")
+    if topic.startswith("$") and f[0] in ("+", "#"):
+        return False                   # 4.7.2: wildcards at the first level never match $-topics
     for i, level in enumerate(f):
         if level == "#":
             return i == len(f) - 1
