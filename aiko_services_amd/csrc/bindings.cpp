@@ -67,6 +67,7 @@ int aiko_topk_nms(const void* boxes, const float* scores, const int* cls, int B,
                   float pad_l, float pad_t, float img_w, float img_h, float* det, int* count,
                   void* workspace, hipStream_t stream);
 int aiko_avgpool(const void* x, void* y, int B, int HW, int C, hipStream_t stream);
+int aiko_mean_rows_f32(const void* x, float* y, int B, int T, int C, hipStream_t stream);
 int aiko_stem_pool(const void* x, const void* w, const float* bias, void* y, int B, int Hp, int Wp,
                    int Ho, int Wo, int Hm, int Wm, int ldy, int variant, hipStream_t stream);
 int aiko_softmax_topk(const void* logits, float* prob, int* index, int B, int N, int k,
@@ -480,6 +481,17 @@ void topk_nms_out(const at::Tensor& boxes, const at::Tensor& scores, const at::T
                "topk_nms");
 }
 
+void mean_rows_out(const at::Tensor& x, at::Tensor& y) {
+  check_cuda(x, "x");
+  check_cuda(y, "y");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 3 && x.is_contiguous() &&
+                  y.scalar_type() == at::kFloat && y.is_contiguous(),
+              "aiko.mean_rows_out: x bf16 [B, T, C] contiguous, y fp32 [B, C]");
+  const int64_t B = x.size(0), T = x.size(1), C = x.size(2);
+  TORCH_CHECK(C % 8 == 0 && y.numel() == B * C, "aiko.mean_rows_out: C % 8 == 0, y [B, C]");
+  check_launch(aiko_mean_rows_f32(x.data_ptr(), y.data_ptr<float>(), B, T, C, cur_stream()), "mean_rows");
+}
+
 void avgpool_out(const at::Tensor& x, at::Tensor& y) {
   check_cuda(x, "x");
   check_cuda(y, "y");
@@ -856,6 +868,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("conv_chain_out(Tensor A, Tensor W1, Tensor b1, Tensor? R, Tensor(a!) Y, Tensor W2, Tensor b2, Tensor(b!) Z, int grid=0, Tensor? A2=None) -> ()");
   m.def("maxpool_out(Tensor x, Tensor(a!) y, int k, int s, int p) -> ()");
   m.def("avgpool_out(Tensor x, Tensor(a!) y) -> ()");
+  m.def("mean_rows_out(Tensor x, Tensor(a!) y) -> ()");
   m.def("stem_pool_out(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, int Ho, int Wo, int variant=0) -> ()");
   m.def("gemm_fp8_out(Tensor a, Tensor? sa, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!)? y, int act, int bm, int bn, int variant=0, Tensor? zero=None, Tensor? amx=None, Tensor(b!)? yq=None, Tensor(c!)? ysc=None) -> ()");
   m.def("rownorm_quant_out(Tensor x, Tensor? gamma, Tensor? beta, float eps, Tensor(a!)? yb, Tensor(b!)? q, Tensor(c!)? qs) -> ()");
@@ -880,6 +893,7 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("yolo_decode_out", &yolo_decode_out);
   m.impl("topk_nms_out", &topk_nms_out);
   m.impl("avgpool_out", &avgpool_out);
+  m.impl("mean_rows_out", &mean_rows_out);
   m.impl("stem_pool_out", &stem_pool_out);
   m.impl("softmax_topk_out", &softmax_topk_out);
   m.impl("gemm_fp8_out", &gemm_fp8_out);

@@ -413,6 +413,69 @@ extern "C" int aiko_maxpool(const void* x, void* y, int B, int H, int W, int C, 
   return (int)hipGetLastError();
 }
 
+namespace aiko {
+// Mean over the rows of [B, T, C] bf16 -> [B, C] fp32 (Whisper feature pooling, long T): one
+// 256-thread block per (batch, 256 channels); 8 row phases x 32 lanes of 8 channels, each lane
+// keeping 4 row loads in flight, then an LDS reduction of the 8 phases.
+__global__ __launch_bounds__(256) void mean_rows_f32_kernel(const bf16_t* __restrict__ x,
+                                                            float* __restrict__ y, int T, int C) {
+  __shared__ float red[8][32][9];
+  const int cl = threadIdx.x & 31, ph = threadIdx.x >> 5;
+  const int C8 = C >> 3;
+  const int c8 = blockIdx.x * 32 + cl;
+  const int b = blockIdx.y;
+  float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c8 < C8) {
+    const bf16_t* src = x + (long)b * T * C + c8 * 8;
+    int i = ph;
+    for (; i + 24 < T; i += 32) {
+      u32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const u32x4*>(src + (long)(i + 8 * u) * C);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[2 * e] += __uint_as_float(v[u][e] << 16);
+          a[2 * e + 1] += __uint_as_float(v[u][e] & 0xffff0000u);
+        }
+    }
+    for (; i < T; i += 8) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(src + (long)i * C);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[2 * e] += __uint_as_float(v[e] << 16);
+        a[2 * e + 1] += __uint_as_float(v[e] & 0xffff0000u);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[ph][cl][e] = a[e];
+  __syncthreads();
+  if (ph == 0 && c8 < C8) {
+    const float inv = 1.f / T;
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) t += red[q][cl][e];
+      o[e] = t * inv;
+    }
+    float* dst = y + (long)b * C + c8 * 8;
+    *reinterpret_cast<f32x4*>(dst) = f32x4{o[0], o[1], o[2], o[3]};
+    *reinterpret_cast<f32x4*>(dst + 4) = f32x4{o[4], o[5], o[6], o[7]};
+  }
+}
+}  // namespace aiko
+
+extern "C" int aiko_mean_rows_f32(const void* x, float* y, int B, int T, int C, hipStream_t stream) {
+  if (C % 8 || T < 1) return -1;
+  dim3 grid((C / 8 + 31) / 32, B);
+  aiko::mean_rows_f32_kernel<<<grid, 256, 0, stream>>>(static_cast<const aiko::bf16_t*>(x), y, T, C);
+  return (int)hipGetLastError();
+}
+
 extern "C" int aiko_avgpool(const void* x, void* y, int B, int HW, int C, hipStream_t stream) {
   const long total = (long)B * (C / 8);
   hipLaunchKernelGGL(aiko::avgpool_kernel, dim3(grid_for(total, 256)), dim3(256), 0, stream,

@@ -278,7 +278,11 @@ class FeatureSink(GpuPipelineElement):
             b = self._bufs[(B, d, self.lane)] = {
                 "pooled": torch.empty(B, d, dtype=torch.float32, device=self.device),
                 "host": HostRing(lambda: torch.empty(B, d, dtype=torch.float32, pin_memory=pin), 8)}
-        torch.mean(features, dim=1, dtype=torch.float32, out=b["pooled"])
+        if self.device.type == "cuda":
+            from ...ops.vision import mean_rows
+            mean_rows(features.contiguous(), out=b["pooled"])      # HIP reduction kernel
+        else:
+            torch.mean(features, dim=1, dtype=torch.float32, out=b["pooled"])
         slot, h = b["host"].acquire()
         h.copy_(b["pooled"], non_blocking=True)
         ev = None

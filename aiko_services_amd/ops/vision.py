@@ -54,6 +54,14 @@ def maxpool2d(x: torch.Tensor, k: int = 3, s: int = 2, p: int = 1,
     return out
 
 
+def mean_rows(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """``x.mean(dim=1)`` of bf16 ``[B, T, C]`` in fp32 ``[B, C]`` (HIP kernel, long T)."""
+    if out is None:
+        out = torch.empty(x.shape[0], x.shape[2], dtype=torch.float32, device=x.device)
+    torch.ops.aiko.mean_rows_out(x, out)
+    return out
+
+
 def avgpool(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     B, H, W, C = x.shape
     if out is None:
