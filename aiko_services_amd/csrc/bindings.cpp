@@ -59,8 +59,9 @@ int aiko_rownorm_quant(const void* x, int ldx, const float* gamma, const float* 
                        void* yb, int ldyb, void* q, int ldq, float* qs, int M, int D, hipStream_t stream);
 int aiko_attn_fwd(const void* q, const void* k, const void* v, void* o, int ldq, int ldk, int ldv,
                   int ldo, int B, int H, int T, int Tpad, int dh, float scale, hipStream_t stream);
-int aiko_logmel(const float* audio, int B, int N, const float* mel, int n_mels, int n_fft, int hop,
-                int F, float* logmel, int* gmax, void* dst, int rows, int pad, int ld, hipStream_t stream);
+int aiko_logmel(const float* audio, int B, int N, const float* mel, int n_mels, const int* mel_range,
+                int n_fft, int hop, int F, float* logmel, int* gmax, void* dst, int rows, int pad, int ld,
+                hipStream_t stream);
 size_t aiko_topk_nms_workspace(int B);
 int aiko_topk_nms(const void* boxes, const float* scores, const int* cls, int B, int A,
                   int max_cand, int max_det, float conf, float iou, float max_wh, float gain,
@@ -690,21 +691,27 @@ void attn_fwd_out(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
 }
 
 // audio fp32 [B, N] -> bf16 log-mel rows [B*rows, n_mels] (frame t at row b*rows + pad + t)
-void logmel_out(const at::Tensor& audio, const at::Tensor& mel, int64_t n_fft, int64_t hop, int64_t F,
-                at::Tensor& work, at::Tensor& gmax, at::Tensor& dst, int64_t rows, int64_t pad) {
+void logmel_out(const at::Tensor& audio, const at::Tensor& mel, const at::Tensor& mel_range, int64_t n_fft,
+                int64_t hop, int64_t F, at::Tensor& work, at::Tensor& gmax, at::Tensor& dst, int64_t rows,
+                int64_t pad) {
   for (const at::Tensor* t : {&audio, &mel, (const at::Tensor*)&work, (const at::Tensor*)&gmax, (const at::Tensor*)&dst})
     check_cuda(*t, "logmel operand");
   TORCH_CHECK(audio.scalar_type() == at::kFloat && audio.dim() == 2 && audio.is_contiguous(), "aiko.logmel_out: audio fp32 [B, N]");
   const int64_t B = audio.size(0), N = audio.size(1), n_mels = mel.size(0);
   TORCH_CHECK(mel.scalar_type() == at::kFloat && mel.is_contiguous() && mel.size(1) == n_fft / 2 + 1,
               "aiko.logmel_out: mel filters fp32 [n_mels, n_fft/2+1]");
+  check_cuda(mel_range, "mel_range");
+  TORCH_CHECK(mel_range.scalar_type() == at::kInt && mel_range.is_contiguous() && mel_range.numel() == n_mels * 3 &&
+                  n_mels <= 128,
+              "aiko.logmel_out: mel_range int32 [n_mels, 3] (lo, len, offset), n_mels <= 128");
   TORCH_CHECK(N > n_fft / 2 && F >= 1 && (F - 1) * hop - n_fft / 2 < N, "aiko.logmel_out: bad frame count");
   TORCH_CHECK(work.scalar_type() == at::kFloat && work.numel() >= B * F * n_mels, "aiko.logmel_out: work fp32 [B*F*n_mels]");
   TORCH_CHECK(gmax.scalar_type() == at::kInt && gmax.numel() >= B, "aiko.logmel_out: gmax int32 [B]");
   TORCH_CHECK(dst.scalar_type() == at::kBFloat16 && dst.dim() == 2 && dst.size(1) == n_mels && dst.stride(1) == 1 &&
                   dst.size(0) == B * rows && rows >= F + pad,
               "aiko.logmel_out: dst bf16 [B*rows, n_mels]");
-  check_launch(aiko_logmel(audio.data_ptr<float>(), B, N, mel.data_ptr<float>(), n_mels, n_fft, hop, F,
+  check_launch(aiko_logmel(audio.data_ptr<float>(), B, N, mel.data_ptr<float>(), n_mels,
+                           mel_range.data_ptr<int>(), n_fft, hop, F,
                            work.data_ptr<float>(), gmax.data_ptr<int>(), dst.data_ptr(), rows, pad, dst.stride(0),
                            cur_stream()),
                "logmel");
@@ -873,7 +880,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("gemm_fp8_out(Tensor a, Tensor? sa, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!)? y, int act, int bm, int bn, int variant=0, Tensor? zero=None, Tensor? amx=None, Tensor(b!)? yq=None, Tensor(c!)? ysc=None) -> ()");
   m.def("rownorm_quant_out(Tensor x, Tensor? gamma, Tensor? beta, float eps, Tensor(a!)? yb, Tensor(b!)? q, Tensor(c!)? qs) -> ()");
   m.def("attn_fwd_out(Tensor q, Tensor k, Tensor v, Tensor(a!) o, int B, int H, int T, int Tpad, float scale) -> ()");
-  m.def("logmel_out(Tensor audio, Tensor mel, int n_fft, int hop, int F, Tensor(a!) work, Tensor(b!) gmax, Tensor(c!) dst, int rows, int pad) -> ()");
+  m.def("logmel_out(Tensor audio, Tensor mel, Tensor mel_range, int n_fft, int hop, int F, Tensor(a!) work, Tensor(b!) gmax, Tensor(c!) dst, int rows, int pad) -> ()");
   m.def("softmax_topk_out(Tensor logits, Tensor(a!) prob, Tensor(b!) index, int k) -> ()");
   m.def("embed_tokens_out(Tensor ids, Tensor pos, Tensor tok, Tensor pemb, Tensor(a!) x) -> ()");
   m.def("attn_decode_out(Tensor q, Tensor(a!) k, Tensor(b!) v, Tensor(c!) o, int B, int H, int S, int T, Tensor? pos, Tensor? knew, Tensor? vnew, float scale, Tensor(d!) work) -> ()");

@@ -4,10 +4,15 @@
 // hop 160, centred with reflect padding, periodic Hann window) are staged in LDS; the 201-bin
 // power spectrum is a direct DFT against an LDS twiddle table (0.26 MFLOP per frame: a few
 // microseconds for a 30 s clip, not worth an FFT's passes at this size); the mel filterbank
-// (80 x 201, in L2) maps it to mel energies; log10(max(e, 1e-10)) is written and the clip's
-// maximum is kept with an order-preserving integer atomicMax.
+// maps it to mel energies — sparse: each triangular filter covers a contiguous bin range
+// (host-computed lo / len / offset), whose weights (~400 nonzeros of 80 x 201) are staged in
+// LDS per workgroup (the dense 201-term dot per (frame, mel) from L2 took most of the former
+// 522 us per 16-clip batch); log10(max(e, 1e-10)) is written and the clip's maximum is kept
+// with an order-preserving integer atomicMax.
 // logmel_finalize_kernel: Whisper's dynamic-range clamp max(x, max - 8), (x + 4) / 4, written
 // as bf16 straight into the zero-bordered [rows][80] buffer the first conv reads.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace aiko {
@@ -24,19 +29,31 @@ __device__ __forceinline__ float float_from_key(int k) {
   return __int_as_float(k >= 0 ? k : k ^ 0x7fffffff);
 }
 
+constexpr int kMaxMels = 128;
+constexpr int kMaxMelNnz = 2048;
+
 __global__ __launch_bounds__(256) void logmel_kernel(const float* __restrict__ audio, int N,
                                                       const float* __restrict__ mel, int n_mels,
+                                                      const int* __restrict__ mel_range,
                                                       int n_fft, int hop, int F,
                                                       float* __restrict__ out, int* __restrict__ gmax) {
   __shared__ float tw_c[kMaxFFT], tw_s[kMaxFFT];
   __shared__ float frame[kFPB][kMaxFFT];
   __shared__ float power[kFPB][kMaxBins];
+  __shared__ float mw[kMaxMelNnz];
+  __shared__ int mr[kMaxMels][3];               // lo bin, length, offset into mw
   __shared__ float red[4];
   const int tid = threadIdx.x;
   const int b = blockIdx.y;
   const int f0 = blockIdx.x * kFPB;
   const int nbins = n_fft / 2 + 1;
   const float* x = audio + (long)b * N;
+  for (int i = tid; i < n_mels * 3; i += 256) mr[i / 3][i % 3] = mel_range[i];
+  __syncthreads();
+  for (int m = tid >> 4; m < n_mels; m += 16) {           // 16 lanes per filter row
+    const int lo = mr[m][0], len = mr[m][1], off = mr[m][2];
+    for (int j = tid & 15; j < len; j += 16) mw[off + j] = mel[(long)m * nbins + lo + j];
+  }
   for (int n = tid; n < n_fft; n += 256) {
     float s, c;
     sincosf(6.283185307179586f * n / n_fft, &s, &c);
@@ -82,9 +99,188 @@ __global__ __launch_bounds__(256) void logmel_kernel(const float* __restrict__ a
   for (int pr = tid; pr < kFPB * n_mels; pr += 256) {
     const int f = pr / n_mels, m = pr - f * n_mels;
     if (f0 + f >= F) continue;
-    const float* w = mel + (long)m * nbins;
+    const int lo = mr[m][0], len = mr[m][1], off = mr[m][2];
     float e = 0.f;
-    for (int k = 0; k < nbins; ++k) e += w[k] * power[f][k];
+    for (int j = 0; j < len; ++j) e += mw[off + j] * power[f][lo + j];
+    const float l = log10f(fmaxf(e, 1e-10f));
+    out[((long)b * F + f0 + f) * n_mels + m] = l;
+    mx = fmaxf(mx, l);
+  }
+  mx = wave_max(mx);
+  if ((tid & 63) == 0) red[tid >> 6] = mx;
+  __syncthreads();
+  if (tid == 0) {
+    const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    atomicMax(gmax + b, float_order_key(m));
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Whisper's n_fft = 400 as a real FFT: the 400 windowed samples of a frame are packed as 200
+// complex points z[n] = x[2n] + i x[2n+1], transformed by a mixed-radix (2 x 4 x 5 x 5)
+// Stockham FFT in LDS (each stage reads one buffer, writes the other in natural order), and
+// split into the 201 bins of the real transform: X[k] = E[k] + W400^k O[k] with
+// E = (Z[k] + conj Z[200-k]) / 2, O = -i (Z[k] - conj Z[200-k]) / 2.  ~10 kFLOP per frame
+// instead of the direct DFT's 160 kFLOP (measured 465 us per 16-clip batch with the DFT).
+constexpr int kHalf = 200;
+
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+template <int R>
+__device__ __forceinline__ void small_dft(float2 (&v)[R]) {
+  if constexpr (R == 2) {
+    const float2 a = v[0], b = v[1];
+    v[0] = make_float2(a.x + b.x, a.y + b.y);
+    v[1] = make_float2(a.x - b.x, a.y - b.y);
+  } else if constexpr (R == 4) {
+    const float2 t0 = make_float2(v[0].x + v[2].x, v[0].y + v[2].y);
+    const float2 t1 = make_float2(v[0].x - v[2].x, v[0].y - v[2].y);
+    const float2 t2 = make_float2(v[1].x + v[3].x, v[1].y + v[3].y);
+    const float2 d = make_float2(v[1].x - v[3].x, v[1].y - v[3].y);
+    const float2 t3 = make_float2(d.y, -d.x);                       // -i * d
+    v[0] = make_float2(t0.x + t2.x, t0.y + t2.y);
+    v[2] = make_float2(t0.x - t2.x, t0.y - t2.y);
+    v[1] = make_float2(t1.x + t3.x, t1.y + t3.y);
+    v[3] = make_float2(t1.x - t3.x, t1.y - t3.y);
+  } else {                                                          // R == 5, direct
+    const float c1 = 0.30901699437494745f, c2 = -0.8090169943749473f;
+    const float s1 = 0.9510565162951535f, s2 = 0.5877852522924732f;
+    const float2 w[5] = {make_float2(1.f, 0.f), make_float2(c1, -s1), make_float2(c2, -s2),
+                         make_float2(c2, s2), make_float2(c1, s1)};
+    float2 out[5];
+#pragma unroll
+    for (int u = 0; u < 5; ++u) {
+      float2 acc = v[0];
+#pragma unroll
+      for (int q = 1; q < 5; ++q) {
+        const float2 t = cmul(v[q], w[(u * q) % 5]);
+        acc.x += t.x;
+        acc.y += t.y;
+      }
+      out[u] = acc;
+    }
+#pragma unroll
+    for (int u = 0; u < 5; ++u) v[u] = out[u];
+  }
+}
+
+// one Stockham stage of radix R over kFPB frames: buffers [kFPB][kHalf]
+template <int R>
+__device__ __forceinline__ void fft_stage(const float2 (*in)[kHalf], float2 (*out)[kHalf], int Ns,
+                                          const float* tw_c, const float* tw_s) {
+  constexpr int M = kHalf / R;
+  for (int item = threadIdx.x; item < kFPB * M; item += 256) {
+    const int f = item / M, j = item - f * M;
+    const int jj = j % Ns;
+    const int step = jj * (kHalf / (Ns * R));                       // W200^(q * step)
+    float2 v[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      float2 a = in[f][j + q * M];
+      if (q) {
+        const int t = 2 * ((q * step) % kHalf);                     // W200^i = W400^(2i)
+        a = cmul(a, make_float2(tw_c[t], -tw_s[t]));
+      }
+      v[q] = a;
+    }
+    small_dft<R>(v);
+    const int dst = (j / Ns) * Ns * R + jj;
+#pragma unroll
+    for (int q = 0; q < R; ++q) out[f][dst + q * Ns] = v[q];
+  }
+  __syncthreads();
+}
+
+static_assert((kFPB - 1) * 160 + 400 <= kFPB * 201, "sample segment must fit the power buffer");
+__global__ __launch_bounds__(256) void logmel_fft400_kernel(const float* __restrict__ audio, int N,
+                                                             const float* __restrict__ mel, int n_mels,
+                                                             const int* __restrict__ mel_range, int hop,
+                                                             int F, float* __restrict__ out,
+                                                             int* __restrict__ gmax) {
+  constexpr int NFFT = 2 * kHalf, NB = kHalf + 1;
+  __shared__ float tw_c[NFFT], tw_s[NFFT];
+  __shared__ float2 buf0[kFPB][kHalf], buf1[kFPB][kHalf];
+  __shared__ float power[kFPB][NB];
+  __shared__ float mw[kMaxMelNnz];
+  __shared__ int mr[kMaxMels][3];
+  __shared__ float red[4];
+  const int tid = threadIdx.x;
+  const int b = blockIdx.y;
+  const int f0 = blockIdx.x * kFPB;
+  const float* x = audio + (long)b * N;
+  for (int n = tid; n < NFFT; n += 256) {
+    float sn, c;
+    sincosf(6.283185307179586f * n / NFFT, &sn, &c);
+    tw_c[n] = c;
+    tw_s[n] = sn;
+  }
+  for (int i = tid; i < n_mels * 3; i += 256) mr[i / 3][i % 3] = mel_range[i];
+  // the 16 overlapping frames span one contiguous sample segment: stage it in LDS with all of a
+  // thread's loads in flight at once (a load-per-sample loop pays one memory latency each),
+  // reflect padding at the clip ends; periodic Hann window as a table
+  float* seg = reinterpret_cast<float*>(&power[0][0]);             // power is not live yet
+  constexpr int kSegMax = kFPB * NB;                                  // 3216 floats >= 15*hop+400
+  const int seglen = (kFPB - 1) * hop + NFFT;
+  const int s0 = f0 * hop - NFFT / 2;
+  {
+    float v[13];
+#pragma unroll
+    for (int u = 0; u < 13; ++u) {
+      const int i = tid + u * 256;
+      int idx = s0 + i;
+      if (idx < 0) idx = -idx;
+      if (idx >= N) idx = 2 * (N - 1) - idx;
+      idx = idx < 0 ? 0 : (idx >= N ? N - 1 : idx);
+      v[u] = (i < seglen && i < kSegMax) ? x[idx] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 13; ++u) {
+      const int i = tid + u * 256;
+      if (i < seglen && i < kSegMax) seg[i] = v[u];
+    }
+  }
+  float* win = reinterpret_cast<float*>(&buf1[0][0]);                // buf1 is not live yet
+  for (int n = tid; n < NFFT; n += 256) win[n] = 0.5f - 0.5f * cospif(2.f * n / NFFT);
+  __syncthreads();
+  // windowed frames packed as complex pairs
+  for (int i = tid; i < kFPB * kHalf; i += 256) {
+    const int f = i / kHalf, n2 = i - f * kHalf;
+    float2 v = make_float2(0.f, 0.f);
+    if (f0 + f < F) {
+      const int o = f * hop + 2 * n2;
+      v = make_float2(seg[o] * win[2 * n2], seg[o + 1] * win[2 * n2 + 1]);
+    }
+    buf0[f][n2] = v;
+  }
+  __syncthreads();
+  for (int m = tid >> 4; m < n_mels; m += 16) {
+    const int lo = mr[m][0], len = mr[m][1], off = mr[m][2];
+    for (int j = tid & 15; j < len; j += 16) mw[off + j] = mel[(long)m * NB + lo + j];
+  }
+  fft_stage<2>(buf0, buf1, 1, tw_c, tw_s);
+  fft_stage<4>(buf1, buf0, 2, tw_c, tw_s);
+  fft_stage<5>(buf0, buf1, 8, tw_c, tw_s);
+  fft_stage<5>(buf1, buf0, 40, tw_c, tw_s);                          // Z in buf0, natural order
+  for (int i = tid; i < kFPB * NB; i += 256) {
+    const int f = i / NB, k = i - f * NB;
+    const float2 zk = buf0[f][k % kHalf];
+    const float2 zr = buf0[f][(kHalf - k) % kHalf];
+    const float2 ev = make_float2(0.5f * (zk.x + zr.x), 0.5f * (zk.y - zr.y));   // (Zk + conj Zr) / 2
+    const float2 od = make_float2(0.5f * (zk.y + zr.y), -0.5f * (zk.x - zr.x));  // -i (Zk - conj Zr) / 2
+    const float2 t = cmul(od, make_float2(tw_c[k], -tw_s[k]));
+    const float re = ev.x + t.x, im = ev.y + t.y;
+    power[f][k] = re * re + im * im;
+  }
+  __syncthreads();
+  float mx = -INFINITY;
+  for (int pr = tid; pr < kFPB * n_mels; pr += 256) {
+    const int f = pr / n_mels, m = pr - f * n_mels;
+    if (f0 + f >= F) continue;
+    const int lo = mr[m][0], len = mr[m][1], off = mr[m][2];
+    float e = 0.f;
+    for (int j = 0; j < len; ++j) e += mw[off + j] * power[f][lo + j];
     const float l = log10f(fmaxf(e, 1e-10f));
     out[((long)b * F + f0 + f) * n_mels + m] = l;
     mx = fmaxf(mx, l);
@@ -120,12 +316,16 @@ __global__ void logmel_finalize_kernel(const float* __restrict__ logmel, const i
 }  // namespace aiko
 
 extern "C" int aiko_logmel(const float* audio, int B, int N, const float* mel, int n_mels,
-                           int n_fft, int hop, int F, float* logmel, int* gmax, void* dst, int rows,
-                           int pad, int ld, hipStream_t stream) {
-  if (n_fft > aiko::kMaxFFT || n_fft % 2) return -1;
+                           const int* mel_range, int n_fft, int hop, int F, float* logmel, int* gmax,
+                           void* dst, int rows, int pad, int ld, hipStream_t stream) {
+  if (n_fft > aiko::kMaxFFT || n_fft % 2 || n_mels > aiko::kMaxMels) return -1;
   hipMemsetAsync(gmax, 0x80, sizeof(int) * B, stream);  // 0x80808080: below every key
   dim3 grid((F + aiko::kFPB - 1) / aiko::kFPB, B);
-  aiko::logmel_kernel<<<grid, 256, 0, stream>>>(audio, N, mel, n_mels, n_fft, hop, F, logmel, gmax);
+  static const bool use_dft = [] { const char* e = getenv("AIKO_LOGMEL_DFT"); return e && *e == '1'; }();
+  if (n_fft == 2 * aiko::kHalf && !use_dft && (aiko::kFPB - 1) * hop + n_fft <= aiko::kFPB * (aiko::kHalf + 1))
+    aiko::logmel_fft400_kernel<<<grid, 256, 0, stream>>>(audio, N, mel, n_mels, mel_range, hop, F, logmel, gmax);
+  else
+    aiko::logmel_kernel<<<grid, 256, 0, stream>>>(audio, N, mel, n_mels, mel_range, n_fft, hop, F, logmel, gmax);
   const long total = (long)B * rows * n_mels;
   long g = (total + 255) / 256;
   if (g > 4096) g = 4096;

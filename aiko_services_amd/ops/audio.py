@@ -43,6 +43,28 @@ def mel_filters(n_mels: int = 80, n_fft: int = N_FFT, sr: int = SAMPLE_RATE) -> 
     return (w * enorm[:, None]).float()
 
 
+_RANGES: dict = {}
+
+
+def mel_ranges(filters: torch.Tensor) -> torch.Tensor:
+    """int32 [n_mels, 3] = (first nonzero bin, run length, offset into the packed weights) of
+    each triangular filter — the log-mel kernel's sparse filterbank (cached per tensor)."""
+    key = (filters.data_ptr(), filters._version, tuple(filters.shape))
+    r = _RANGES.get(key)
+    if r is None:
+        rows, off = [], 0
+        for w in filters.detach().float().cpu():
+            nz = torch.nonzero(w != 0).flatten()
+            lo = int(nz[0]) if nz.numel() else 0
+            n = int(nz[-1]) - lo + 1 if nz.numel() else 0
+            rows.append((lo, n, off))
+            off += n
+        if off > 2048:
+            raise ValueError(f"mel filterbank has {off} nonzero span elements (kernel limit 2048)")
+        r = _RANGES[key] = torch.tensor(rows, dtype=torch.int32, device=filters.device)
+    return r
+
+
 def log_mel(audio: torch.Tensor, filters: torch.Tensor, out: torch.Tensor, rows: int, pad: int,
             work: torch.Tensor | None = None, gmax: torch.Tensor | None = None, frames: int | None = None):
     """fp32 audio [B, N] -> Whisper-normalised log-mel, bf16, frame t of clip b at row
@@ -54,7 +76,7 @@ def log_mel(audio: torch.Tensor, filters: torch.Tensor, out: torch.Tensor, rows:
         work = torch.empty(B * F * n_mels, dtype=torch.float32, device=audio.device)
     if gmax is None:
         gmax = torch.empty(B, dtype=torch.int32, device=audio.device)
-    torch.ops.aiko.logmel_out(audio, filters, N_FFT, HOP, F, work, gmax, out, rows, pad)
+    torch.ops.aiko.logmel_out(audio, filters, mel_ranges(filters), N_FFT, HOP, F, work, gmax, out, rows, pad)
     return out
 
 
