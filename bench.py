@@ -256,10 +256,12 @@ def main(argv=None):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
 
-    t = torch.tensor([elapsed, statistics.median(latencies) if latencies else 0.0],
+    lat = sorted(latencies)
+    p99_local = lat[min(len(lat) - 1, int(0.99 * len(lat)))] if lat else 0.0
+    t = torch.tensor([elapsed, statistics.median(latencies) if latencies else 0.0, p99_local],
                      dtype=torch.float64, device=device)
     D.all_reduce_max(t)
-    elapsed, p50 = float(t[0]), float(t[1])
+    elapsed, p50, p99 = float(t[0]), float(t[1]), float(t[2])
     frames = ws * a.batch * a.steps
     fps = frames / elapsed
     if rank == 0:
@@ -272,6 +274,7 @@ def main(argv=None):
                      if a.model.startswith("whisper") else
                      f"synthetic (random uint8 {a.height}x{a.width} frames generated in HBM; random-init weights)"),
             "p50_latency_ms": round(p50 * 1e3, 3),
+            "p99_latency_ms": round(p99 * 1e3, 3),
             "config": dict({"global_batch": ws * a.batch, "seq_len": None, "per_gpu_batch": a.batch,
                             "parallelism": f"dp{ws}", "hipgraph": not a.no_graph}, **model_cfg),
         }
