@@ -21,7 +21,7 @@ int aiko_conv_igemm(const void* x, const void* w, const float* bias, const void*
 int aiko_conv_buf(const void* x, const void* w, const float* bias, const void* res, void* y,
                   int H, int W, int C, int Cc, int R, int S, int stride, int pad, int Ho, int Wo,
                   int M, int Cout, int K, int act, int ldy, int ldr, int bm, int bn, const void* x2,
-                  int K1, int H2, int W2, int C2, int stride2, int occ, hipStream_t stream);
+                  int K1, int H2, int W2, int C2, int stride2, int occ, int mf32, hipStream_t stream);
 int aiko_conv_persist(const void* x, const void* w, const float* bias, const void* res, void* y,
                       int H, int W, int C, int Cc, int R, int S, int stride, int pad, int Ho, int Wo,
                       int M, int Cout, int K, int act, int ldy, int ldr, int bm, int bn, const void* x2,
@@ -183,7 +183,7 @@ void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, co
     rc = aiko_conv_persist(x.data_ptr(), w.data_ptr(), bptr, rptr, y.data_ptr(), H, W, C, Cc, R, S, stride,
                            pad, Ho, Wo, M, Cout, K, act, ldy, ldr, bm, bn, x2ptr, K1, H2, W2, C2, stride2,
                            cur_stream());
-  } else if (variant == 2 || variant == 3) {
+  } else if (variant == 2 || variant == 3 || variant == 5) {
     // buffer-LDS-DMA kernel: 64-channel K blocks inside one tap, byte offsets in 31 bits;
     // variant 3 = the same kernel at forced high occupancy (64x64: 5, 64x128 / 128x64: 3 WG/CU)
     TORCH_CHECK(Cc % 64 == 0 && R * S <= 32 && x_extent * 2 < (1LL << 31) - 64 && w.numel() * 2 < (1LL << 31),
@@ -191,7 +191,7 @@ void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, co
     TORCH_CHECK(!dual || avail_elems(*x2) * 2 < (1LL << 31) - 64, "aiko.conv_igemm_out: x2 too large for variant 2");
     rc = aiko_conv_buf(x.data_ptr(), w.data_ptr(), bptr, rptr, y.data_ptr(), H, W, C, Cc, R, S, stride,
                        pad, Ho, Wo, M, Cout, K, act, ldy, ldr, bm, bn, x2ptr, K1, H2, W2, C2, stride2,
-                       variant == 3 ? (bm == 64 && bn == 64 ? 5 : 3) : 0, cur_stream());
+                       variant == 3 ? (bm == 64 && bn == 64 ? 5 : 3) : 0, variant == 5 ? 1 : 0, cur_stream());
   } else if (variant == 1) {
     TORCH_CHECK(zero.has_value() && zero->defined() && zero->is_cuda() && zero->nbytes() >= 16 &&
                     reinterpret_cast<uintptr_t>(zero->data_ptr()) % 16 == 0,

@@ -56,7 +56,12 @@ constexpr int buf_slots() {
   return (BM + BN) * 64 * 2 * 3 <= (160 * 1024) / buf_wgs_per_cu<BM, BN, NW, OCC>() ? 3 : 2;
 }
 
-template <int BM, int BN, int WGM, int WGN, int OCC = 0>
+// MF: MFMA shape — 16 (v_mfma_f32_16x16x32_bf16) or 32 (v_mfma_f32_32x32x16_bf16).  The
+// 32x32x16 form does the same FLOPs in half the instructions, each holding the SIMD's vector
+// issue for 8 of its 32 cycles instead of 8 of 16: three times the free issue slots per MFMA for
+// the LDS-DMA pieces (60-185 issue cycles each beside MFMAs, MI355X_MICROARCH.md) and the
+// fragment reads — the issue budget, not the matrix pipe, bounds the long-K (3x3) convs.
+template <int BM, int BN, int WGM, int WGN, int OCC = 0, int MF = 16>
 __global__ __launch_bounds__(64 * WGM * WGN, (buf_wgs_per_cu<BM, BN, WGM * WGN, OCC>())) void conv_buf_kernel(
     ConvParams p) {
   constexpr int NW = WGM * WGN, NT = 64 * NW;
@@ -202,36 +207,74 @@ __global__ __launch_bounds__(64 * WGM * WGN, (buf_wgs_per_cu<BM, BN, WGM * WGN, 
     for (int i = 0; i < BPT; ++i) buf16(rw, b_off[i], sb, Bs + (i * RPI + wave * 8) * BK);
   };
 
-  f32x4 acc[MI][NI];
+  static_assert(MF == 16 || (WM % 32 == 0 && WN % 32 == 0), "32x32 MFMA needs 32-multiple wave tiles");
+  constexpr int MI2 = MF == 32 ? WM / 32 : 1, NI2 = MF == 32 ? WN / 32 : 1;
+  f32x4 acc[MF == 16 ? MI : 1][MF == 16 ? NI : 1];
+  f32x16 acc2[MI2][NI2];
+  if constexpr (MF == 16) {
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  } else {
+#pragma unroll
+    for (int i = 0; i < MI2; ++i)
+#pragma unroll
+      for (int j = 0; j < NI2; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc2[i][j][e] = 0.f;
+  }
 
   const int fr = lane & 15, fq = lane >> 4;
-  int a_rd[MI], b_rd[NI];                 // per-lane fragment offsets (elements) inside a stage
+  const int r32 = lane & 31, h32 = lane >> 5;
+  int a_rd[MF == 16 ? MI : MI2], b_rd[MF == 16 ? NI : NI2];   // per-lane fragment offsets (elements)
+  if constexpr (MF == 16) {
 #pragma unroll
-  for (int i = 0; i < MI; ++i) a_rd[i] = (wr * WM + i * 16 + fr) * BK;
+    for (int i = 0; i < MI; ++i) a_rd[i] = (wr * WM + i * 16 + fr) * BK;
 #pragma unroll
-  for (int j = 0; j < NI; ++j) b_rd[j] = BM * BK + (wc * WN + j * 16 + fr) * BK;
-  const int sw = fr & 7;                  // row & 7 of every fragment row (rows are 16-aligned + fr)
+    for (int j = 0; j < NI; ++j) b_rd[j] = BM * BK + (wc * WN + j * 16 + fr) * BK;
+  } else {
+#pragma unroll
+    for (int i = 0; i < MI2; ++i) a_rd[i] = (wr * WM + i * 32 + r32) * BK;
+#pragma unroll
+    for (int j = 0; j < NI2; ++j) b_rd[j] = BM * BK + (wc * WN + j * 32 + r32) * BK;
+  }
+  const int sw = (MF == 16 ? fr : r32) & 7;   // row & 7 of every fragment row (8-aligned bases)
 
   auto compute = [&](auto slot_tag) {
     constexpr int SLOT = decltype(slot_tag)::value;
     const bf16_t* St = ring + SLOT * STAGE_ELEMS;
+    if constexpr (MF == 16) {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[MI], bfr[NI];
-      const int pc = ((fq + 4 * kk) ^ sw) << 3;
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[MI], bfr[NI];
+        const int pc = ((fq + 4 * kk) ^ sw) << 3;
 #pragma unroll
-      for (int i = 0; i < MI; ++i) af[i] = *reinterpret_cast<const bf16x8*>(St + a_rd[i] + pc);
+        for (int i = 0; i < MI; ++i) af[i] = *reinterpret_cast<const bf16x8*>(St + a_rd[i] + pc);
 #pragma unroll
-      for (int j = 0; j < NI; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(St + b_rd[j] + pc);
+        for (int j = 0; j < NI; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(St + b_rd[j] + pc);
 #pragma unroll
-      for (int i = 0; i < MI; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < NI; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < NI; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+      // k-step ks covers K 16 ks .. 16 ks + 15: lane half h32 holds chunk 2 ks + h32 of its row
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        bf16x8 af[MI2], bfr[NI2];
+        const int pc = ((2 * ks + h32) ^ sw) << 3;
+#pragma unroll
+        for (int i = 0; i < MI2; ++i) af[i] = *reinterpret_cast<const bf16x8*>(St + a_rd[i] + pc);
+#pragma unroll
+        for (int j = 0; j < NI2; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(St + b_rd[j] + pc);
+#pragma unroll
+        for (int i = 0; i < MI2; ++i)
+#pragma unroll
+          for (int j = 0; j < NI2; ++j)
+            acc2[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc2[i][j], 0, 0, 0);
+      }
     }
   };
 
@@ -276,14 +319,27 @@ __global__ __launch_bounds__(64 * WGM * WGN, (buf_wgs_per_cu<BM, BN, WGM * WGN, 
   // ---- epilogue (as conv_glds) ----
   float* Cs = reinterpret_cast<float*>(smem);
   constexpr int LDC = BN + CPAD;
+  if constexpr (MF == 16) {
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int col = wc * WN + j * 16 + fr;
+      for (int j = 0; j < NI; ++j) {
+        const int col = wc * WN + j * 16 + fr;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) Cs[(wr * WM + i * 16 + fq * 4 + e) * LDC + col] = acc[i][j][e];
-    }
+        for (int e = 0; e < 4; ++e) Cs[(wr * WM + i * 16 + fq * 4 + e) * LDC + col] = acc[i][j][e];
+      }
+  } else {
+    // 32x32 C/D: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
+#pragma unroll
+    for (int i = 0; i < MI2; ++i)
+#pragma unroll
+      for (int j = 0; j < NI2; ++j) {
+        const int col = wc * WN + j * 32 + r32;
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+          Cs[(wr * WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h32) * LDC + col] = acc2[i][j][e];
+      }
+  }
   __syncthreads();
   const bool post = (p.act & 16) != 0;
   const int act = p.act & 15;
@@ -337,7 +393,7 @@ extern "C" int aiko_conv_buf(const void* x, const void* w, const float* bias, co
                              void* y, int H, int W, int C, int Cc, int R, int S, int stride,
                              int pad, int Ho, int Wo, int M, int Cout, int K, int act, int ldy,
                              int ldr, int bm, int bn, const void* x2, int K1, int H2, int W2,
-                             int C2, int stride2, int occ, hipStream_t stream) {
+                             int C2, int stride2, int occ, int mf32, hipStream_t stream) {
   using namespace aiko;
   if (Cc % 64 || R * S > 32 || R > 16 || S > 16 || (x2 && (K - K1) % 64)) return -1;
   ConvParams p;
@@ -362,6 +418,19 @@ extern "C" int aiko_conv_buf(const void* x, const void* w, const float* bias, co
       conv_buf_kernel<128, 64, 2, 2, 3><<<grid, block, 0, stream>>>(p);
     else if (bm == 64 && bn == 64 && occ == 4)
       conv_buf_kernel<64, 64, 2, 2, 4><<<grid, block, 0, stream>>>(p);
+    else
+      return -1;
+  } else if (mf32) {                       // variant 5: 32x32x16 MFMA
+    if (bm == 128 && bn == 128)
+      conv_buf_kernel<128, 128, 2, 2, 0, 32><<<grid, block, 0, stream>>>(p);
+    else if (bm == 128 && bn == 64)
+      conv_buf_kernel<128, 64, 2, 2, 0, 32><<<grid, block, 0, stream>>>(p);
+    else if (bm == 64 && bn == 128)
+      conv_buf_kernel<64, 128, 2, 2, 0, 32><<<grid, block, 0, stream>>>(p);
+    else if (bm == 256 && bn == 128)
+      conv_buf_kernel<256, 128, 4, 2, 0, 32><<<grid, 512, 0, stream>>>(p);
+    else if (bm == 128 && bn == 256)
+      conv_buf_kernel<128, 256, 2, 4, 0, 32><<<grid, 512, 0, stream>>>(p);
     else
       return -1;
   } else if (bm == 128 && bn == 128) {

@@ -230,6 +230,8 @@ def zero_page(device) -> torch.Tensor:
 BUF_WIDE_TILES = ((256, 128), (128, 256), (256, 64))   # 8-wave buffer-DMA kernels (one workgroup per CU)
 BUF_OCC_TILES = ((64, 64), (64, 128), (128, 64))       # variant 3: buffer-DMA at 5 / 3 / 3 workgroups per CU
 PERSIST_TILES = ((64, 128),)   # variant 4: persistent, one K-block ring across tiles (2 workgroups/CU)
+# variant 5: buffer-DMA kernel on v_mfma_f32_32x32x16_bf16 (3x the free issue slots per MFMA)
+MF32_TILES = ((128, 128), (128, 64), (64, 128), (256, 128), (128, 256))
 
 
 def buf_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = None) -> bool:
@@ -250,6 +252,7 @@ def _tune(key, M, cout, launch, buf_ok=False):
         if buf_ok:
             cands += [t + (2,) for t in TILES + BUF_WIDE_TILES] + [t + (3,) for t in BUF_OCC_TILES]
             cands += [t + (4,) for t in PERSIST_TILES]
+            cands += [t + (5,) for t in MF32_TILES]
     best, best_t = None, None
     for t in cands:
         launch(t)  # warm

@@ -69,6 +69,7 @@ def main():
         if cout > 32 and C.buf_variant_ok(spec, x, x2):
             cands += [tt + (2,) for tt in base + C.BUF_WIDE_TILES] + [tt + (3,) for tt in C.BUF_OCC_TILES]
             cands += [tt + (4,) for tt in C.PERSIST_TILES]
+            cands += [tt + (5,) for tt in C.MF32_TILES]
         if a.tile:
             cands = [tuple(int(v) for v in a.tile.split(","))]
         for t in cands:

@@ -49,6 +49,15 @@ def _nhwc(x_nchw):
     (3, 14, 14, 256, 512, 1, 1, 0, None, False, (128, 256, 2)),
     (1, 9, 11, 128, 64, 3, 2, 1, "silu", False, (256, 128, 2)),
     (2, 30, 30, 64, 64, 3, 1, 1, "relu", True, (256, 64, 2)),
+    # 32x32x16-MFMA buffer-DMA (variant 5): every tile shape, 1x1 / 3x3 / strided, residual
+    (2, 56, 56, 64, 256, 1, 1, 0, "relu", True, (128, 128, 5)),
+    (2, 56, 56, 64, 64, 3, 1, 1, "relu", False, (128, 64, 5)),
+    (2, 28, 28, 128, 128, 3, 2, 1, "relu", True, (64, 128, 5)),
+    (3, 14, 14, 256, 1024, 1, 1, 0, None, True, (64, 128, 5)),
+    (2, 28, 28, 128, 256, 3, 1, 1, "relu", True, (256, 128, 5)),
+    (3, 14, 14, 256, 512, 1, 1, 0, None, False, (128, 256, 5)),
+    (1, 9, 11, 128, 64, 3, 2, 1, "silu", False, (256, 128, 5)),
+    (2, 7, 7, 512, 512, 3, 1, 1, "relu", False, (128, 128, 5)),
     # high-occupancy buffer-DMA (variant 3)
     (2, 28, 28, 128, 512, 1, 1, 0, "relu", True, (64, 128, 3)),
     (1, 9, 11, 128, 64, 3, 1, 1, "silu", False, (64, 64, 3)),
