@@ -90,10 +90,15 @@ def create_rank_pipeline(plan: Plan, rank: int, stream_id=None, parameters=None,
     from ..pipeline.engine import PipelineImpl
     spec = plan.ranks[rank]
     definition = parse_pipeline_definition_dict(spec.definition)
+    if plan.mode == "dp" and rank != 0 and plan.stream:
+        # SPMD data parallelism: every rank runs the same stream (its collectives pair up)
+        stream_id = plan.stream.get("stream_id")
+        parameters = plan.stream.get("parameters") or {}
+        grace_time = int(plan.stream.get("grace_time", grace_time))
     pipeline = PipelineImpl.create_pipeline(definition_pathname, definition, name or spec.name, graph_path,
                                             None, [], frame_id, None, grace_time,
                                             queue_response=queue_response, tags=list(spec.tags))
-    if spec.stage + 1 < len(plan.stages):
+    if plan.mode != "dp" and spec.stage + 1 < len(plan.stages):
         remote = f"Stage{spec.stage + 1}"
         local_def = None
         weight = 0.0
@@ -117,7 +122,7 @@ def create_rank_pipeline(plan: Plan, rank: int, stream_id=None, parameters=None,
             pipeline.create_frame({"stream_id": stream_id or "*", "frame_id": int(frame_id or 0),
                                    "parameters": {}}, arguments[0])
     if auto_start:
-        start_when_ready(pipeline, start if rank == 0 else None)
+        start_when_ready(pipeline, start if rank == 0 or plan.mode == "dp" else None)
     return pipeline
 
 

@@ -58,6 +58,7 @@ class Plan:
     ranks: list                # [RankSpec]
     links: list                # [[src, dst]] hop directions (one RCCL communicator each)
     predicted_ms: dict = field(default_factory=dict)
+    stream: dict = field(default_factory=dict)   # dp: every rank creates this stream
 
     def to_json(self) -> str:
         return json.dumps(asdict(self))
@@ -176,6 +177,26 @@ def _boundary(defn: dict, stages, s):
     return sorted(produced & consumed)
 
 
+def _dp_plan(definition: dict, gpus: int, group: str | None) -> Plan:
+    """``mode: dp`` — SPMD data parallelism: every rank runs the WHOLE definition on its GPU
+    (registered as ``{name}_r{rank}``), every rank creates the same stream, and the elements'
+    collectives (FrameFanout scatter / broadcast, DetectionsGather / ClassifierTopK
+    all-gather) pair up frame by frame over RCCL — BASELINE config 4's topology
+    (``examples/yolo/yolo_dp8.json``)."""
+    base = definition["name"]
+    group = group or f"{base}-{uuid.uuid4().hex[:8]}"
+    d = {k: copy.deepcopy(v) for k, v in definition.items() if k != "parallel"}
+    d["elements"] = [_strip_stage(e) for e in definition["elements"]]
+    ranks = []
+    for r in range(gpus):
+        dr = copy.deepcopy(d)
+        dr["name"] = base if r == 0 else f"{base}_r{r}"
+        ranks.append(RankSpec(rank=r, stage=0, name=dr["name"], definition=dr, device=r,
+                              tags=[f"rank={r}", f"group={group}", "mode=dp"]))
+    return Plan(group=group, world=gpus, mode="dp", stages=[element_order(definition)], replicas=[gpus],
+                local_share=0.0, ranks=ranks, links=[])
+
+
 def make_plan(definition: dict, gpus: int | None = None, stages=None, replicas=None,
               local_share: float = 0.0, times_ms: dict | None = None, group: str | None = None,
               device_offset: int = 0) -> Plan:
@@ -184,6 +205,8 @@ def make_plan(definition: dict, gpus: int | None = None, stages=None, replicas=N
     par = definition.get("parallel") or {}
     mode = par.get("mode", "pp")
     gpus = int(gpus or par.get("gpus", 1))
+    if mode == "dp":
+        return _dp_plan(definition, gpus, group)
     if replicas is None and par.get("replicas") is not None:
         replicas = [int(r) for r in par["replicas"]]
     if not local_share and par.get("local_share") is not None:

@@ -120,6 +120,10 @@ def create(definition_pathname, graph_path, name, parameters, stream_id, stream_
         from ..parallel.placement import make_plan
         with open(definition_pathname) as f:
             plan = make_plan(json.load(f))
+        if plan.mode == "dp":
+            plan.stream = {"stream_id": stream_id or "1", "parameters": dict(parameters or {}),
+                           "grace_time": grace_time}
+            stream_id = stream_id or "1"
         _LOGGER.info(f"Parallel plan {plan.group}: stages {plan.stages} replicas {plan.replicas} "
                      f"local_share {plan.local_share}")
         spawn_workers(plan)

@@ -149,3 +149,12 @@ def test_hop_loopback_cpu():
     assert torch.equal(got["r"].wait()["a"], torch.arange(3)) and got["r"].t_submit == 1.0
     plane.release([handle])
     assert plane.stats()["pool_free_from_0"] == 4
+
+
+def test_dp_spmd_actor_pipeline(cluster):
+    """``parallel: {mode: dp, gpus: 2}`` through ``aiko_pipeline create``: both ranks run the
+    whole pipeline on the same stream; rank 0's results hold the all-gathered rows of both."""
+    r, out = _create(cluster["env"], os.path.join(DEFS, "tensor_dp2.json"), 4)
+    assert len(out) == 4, (r.returncode, r.stdout[-3000:], r.stderr[-3000:])
+    for v in out.values():
+        assert "float32,6x1x6" in v and "int32,6" in v, v      # world x batch rows gathered
