@@ -402,7 +402,9 @@ def linear(x: torch.Tensor, spec: ConvSpec, out: torch.Tensor | None = None,
     return out
 
 
-CHAIN_STAGE2 = __import__("os").environ.get("AIKO_CHAIN_STAGE2", "0") == "1"
+def _chain_stage2() -> bool:
+    """``AIKO_CHAIN_STAGE2=1`` admits the stage-2 chain shapes (read at call time)."""
+    return __import__("os").environ.get("AIKO_CHAIN_STAGE2", "0") == "1"
 
 
 def chain_ok(spec3: ConvSpec, spec1: ConvSpec) -> bool:
@@ -414,7 +416,7 @@ def chain_ok(spec3: ConvSpec, spec1: ConvSpec) -> bool:
     # tested but spill at 512 threads (128-VGPR cap): 377 / 519 us against 151 / 200 us for
     # the two unchained convs, so they are opt-in (CHAIN_STAGE2) until that is fixed.
     shapes = {(64, 256): (64, 128)}
-    if CHAIN_STAGE2:
+    if _chain_stage2():
         shapes[(128, 512)] = (128, 256)
     k1, n1 = spec3.weight.shape[1], spec3.weight.shape[0]
     return (one_by_one(spec3) and one_by_one(spec1) and spec3.cin == k1 and (k1, n1) in shapes
@@ -437,6 +439,10 @@ def conv_chain(x: torch.Tensor, spec3: ConvSpec, residual: torch.Tensor | None, 
     one kernel (``conv_chain.hip``): the 256-channel ``out_y`` is written once and never read
     back.  All NHWC, contiguous.  With ``x2`` (and no residual) ``spec3`` is a fused-shortcut
     spec (:func:`chain_dual_ok`): ``out_y = relu([x | x2] . W^T + b)``."""
+    ok = chain_dual_ok(spec3, spec1) if x2 is not None else chain_ok(spec3, spec1)
+    if not ok:
+        raise ValueError("conv_chain: shapes not eligible (chain_ok / chain_dual_ok); the stage-2 "
+                         "shapes need AIKO_CHAIN_STAGE2=1 (they spill registers and run slower)")
     torch.ops.aiko.conv_chain_out(x, spec3.weight, spec3.bias, residual, out_y, spec1.weight, spec1.bias,
                                   out_z, grid, x2)
     return out_y, out_z
