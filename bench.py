@@ -35,6 +35,7 @@ os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 import torch  # noqa: E402
 
 METRIC = "frames/sec (whole node) + p50 latency, ResNet-50 pipeline at 1/2/4/8 MI355X"
+SETUP_FRAMES = 12     # >= frame-pool slots x lanes distinct (slot, lane) graphs, see main()
 ELEMENTS = "aiko_services_amd.elements.gpu.vision"
 
 
@@ -241,6 +242,12 @@ def main(argv=None):
             if rec and record:
                 latencies.append(res.latency)
 
+    # setup (untimed, before the W warmup steps): the first frames tune the conv tiles and capture
+    # one hipGraph per frame-pool slot and lane (graphs read the slots in place, no input copy),
+    # so even a short warmup starts the timed region in steady state
+    for _ in range(SETUP_FRAMES):
+        step(False)
+    drain(False)
     for _ in range(a.warmup):
         step(False)
     drain(False)
@@ -276,7 +283,8 @@ def main(argv=None):
             "p50_latency_ms": round(p50 * 1e3, 3),
             "p99_latency_ms": round(p99 * 1e3, 3),
             "config": dict({"global_batch": ws * a.batch, "seq_len": None, "per_gpu_batch": a.batch,
-                            "parallelism": f"dp{ws}", "hipgraph": not a.no_graph}, **model_cfg),
+                            "parallelism": f"dp{ws}", "hipgraph": not a.no_graph,
+                            "setup_frames": SETUP_FRAMES}, **model_cfg),
         }
         if a.model.startswith("whisper"):
             out["audio_seconds_per_s"] = round(ws * a.batch * a.chunk * a.steps / elapsed, 1)
