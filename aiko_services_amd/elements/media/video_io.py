@@ -282,73 +282,4 @@ class VideoWriteFile(DataTarget):
         return StreamEvent.OKAY, {}
 
 
-class VideoReadWebcam(DataSource):
-    """Camera source with EC-tunable ``color``, ``flip``, ``path`` (needs OpenCV)."""
-
-    def __init__(self, context):
-        context.set_protocol("webcam:0")
-        context.get_implementation("PipelineElement").__init__(self, context)
-        self.path_current = None
-        self.stream_started = 0
-        self.video_capture = None
-        self.share["color"] = True
-        self.share["flip"] = "none"
-        self.share["frame_id"] = -1
-        self.share["path"] = "/dev/video0"
-        self.ec_producer.add_handler(self._ec_producer_change_handler)
-
-    def _ec_producer_change_handler(self, command, item_name, item_value):
-        if item_name == "color" and isinstance(item_value, str):
-            self.share["color"] = item_value.lower() == "true"
-        if item_name == "path":
-            if isinstance(item_value, str) and item_value.isdigit():
-                item_value = int(item_value)
-            if item_value != self.path_current and self.stream_started:
-                self._open_camera(item_value)
-
-    def _open_camera(self, path):
-        if self.video_capture is not None:
-            self.video_capture.release()
-            self.video_capture = None
-        cap = cv2.VideoCapture(path)
-        if cap.isOpened():
-            self.video_capture = cap
-            self.path_current = path
-            self.share["path"] = path
-        else:
-            self.logger.error(f"Open camera: {path} failed")
-
-    def start_stream(self, stream, stream_id):
-        if not _CV2:
-            return StreamEvent.ERROR, {"diagnostic": "VideoReadWebcam needs OpenCV (cv2), not installed"}
-        self.stream_started += 1
-        path, _ = self.get_parameter("path", "/dev/video0")
-        self._open_camera(path)
-        self.create_frames(stream, self.frame_generator, rate=None)
-        return StreamEvent.OKAY, {}
-
-    def frame_generator(self, stream, frame_id):
-        if self.video_capture is None or not self.video_capture.isOpened():
-            return StreamEvent.DROP_FRAME, {}
-        ok, bgr = self.video_capture.read()
-        if not ok:
-            return StreamEvent.DROP_FRAME, {}
-        if frame_id % 10 == 0:
-            self.ec_producer.update("frame_id", frame_id)
-        image = cv2.cvtColor(bgr, cv2.COLOR_BGR2RGB if self.share["color"] else cv2.COLOR_BGR2GRAY)
-        flip = self.share["flip"]
-        if flip in ("both", "horizontal"):
-            image = image[:, ::-1]
-        if flip in ("both", "vertical"):
-            image = image[::-1]
-        return StreamEvent.OKAY, {"images": [np.ascontiguousarray(image)]}
-
-    def process_frame(self, stream, images):
-        return StreamEvent.OKAY, {"images": images}
-
-    def stop_stream(self, stream, stream_id):
-        self.stream_started = max(0, self.stream_started - 1)
-        if self.stream_started == 0 and self.video_capture is not None:
-            self.video_capture.release()
-            self.video_capture = None
-        return StreamEvent.OKAY, {}
+from .webcam_io import VideoReadWebcam  # noqa: E402,F401  (kept importable from here)
