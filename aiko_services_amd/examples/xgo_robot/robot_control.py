@@ -26,7 +26,7 @@ from aiko_services_amd.utils.sexpr import generate
 
 from aiko_services_amd.runtime import event
 
-from .xgo_robot import XGORobot, decode_image, encode_image, topic_video
+from .xgo_robot import XGORobot, topic_video, video_frame, video_payload
 
 __all__ = ["RobotControl", "RobotControlImpl", "VideoTest", "VideoTestImpl"]
 
@@ -51,7 +51,9 @@ class RobotControlImpl(RobotControl):
         _aiko.process.add_message_handler(self._video_handler, topic_video(), binary=True)
 
     def _video_handler(self, _aiko_ctx, topic, payload):
-        image = decode_image(payload)
+        image = video_frame(payload)
+        if image is None:                 # frame-ring slot reused before we read it: dropped
+            return True
         self.last_image = image
         n = int(self.share["frames_received"]) + 1
         self.ec_producer.update("frames_received", n)
@@ -122,7 +124,7 @@ class VideoTestImpl(VideoTest):
         t0 = time.time()
         image = self.frame()
         self.share["time_process_ms"] = round((time.time() - t0) * 1000, 1)
-        _aiko.message.publish(self.share["topic_video"], encode_image(image))
+        _aiko.message.publish(self.share["topic_video"], video_payload(image))
         self._frame_id += 1
         self.ec_producer.update("frames_published", self._frame_id)
         if self._last is not None:

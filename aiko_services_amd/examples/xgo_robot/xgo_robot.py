@@ -17,6 +17,7 @@ from abc import abstractmethod
 import argparse
 from io import BytesIO
 import math
+import os
 import zlib
 
 import numpy as np
@@ -28,7 +29,8 @@ from aiko_services_amd.runtime.context import Interface
 from aiko_services_amd.runtime.process import aiko as _aiko
 from aiko_services_amd.utils.configuration import get_namespace
 
-__all__ = ["XGORobot", "XGORobotImpl", "encode_image", "decode_image", "topic_video", "ACTIONS"]
+__all__ = ["XGORobot", "XGORobotImpl", "encode_image", "decode_image", "video_payload", "video_frame",
+           "topic_video", "ACTIONS"]
 
 ACTIONS = {"lie_down": 1, "stand_up": 2, "crawl": 3, "turn_around": 4, "mark_time": 5, "squat": 6,
            "turn_roll": 7, "turn_pitch": 8, "turn_yaw": 9, "three_axis": 10, "pee": 11, "sit_down": 12,
@@ -51,6 +53,31 @@ def encode_image(image: np.ndarray) -> bytes:
 
 def decode_image(payload: bytes) -> np.ndarray:
     return np.load(BytesIO(zlib.decompress(payload)), allow_pickle=False)
+
+
+_RING = None
+
+
+def video_payload(image: np.ndarray):
+    """What to publish for one video frame: the reference's ``zlib(np.save(image))`` bytes, or
+    — with ``AIKO_FRAME_RING=1`` (publisher and subscribers on one node) — a slot token of a
+    shared-memory frame ring (``message/frame_ring.py``): the pixels never cross the broker."""
+    global _RING
+    if os.environ.get("AIKO_FRAME_RING", "0") in ("1", "true"):
+        if _RING is None:
+            from ...message.frame_ring import SharedFrameRing
+            _RING = SharedFrameRing(f"aiko_video_{os.getpid()}", slots=16,
+                                    slot_bytes=max(np.asarray(image).nbytes, 1 << 16), create=True)
+        return _RING.put(image)
+    return encode_image(image)
+
+
+def video_frame(payload):
+    """Inverse of :func:`video_payload` (None if a ring slot was overwritten before the read)."""
+    from ...message.frame_ring import SharedFrameRing, is_ring_token
+    if is_ring_token(payload):
+        return SharedFrameRing.get(payload)
+    return decode_image(payload)
 
 
 def _clip(name, value):
@@ -133,7 +160,7 @@ class XGORobotImpl(XGORobot):
         h, w = self.size
         image = self._rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
         image[:8, :8] = self._frame_id % 256                    # frame stamp for consumers
-        _aiko.message.publish(topic_video(), encode_image(image))
+        _aiko.message.publish(topic_video(), video_payload(image))
         self._frame_id += 1
         self.ec_producer.update("frames_published", self._frame_id)
 
