@@ -65,14 +65,8 @@ class FramePool:
 
     def acquire(self, timeout: float | None = None) -> int:
         self._reap()
-        slot = self._pool.acquire(0)
-        if slot >= 0:
-            return slot
-        if self._pending:
-            self._reap(block=True)
-            slot = self._pool.acquire(0)
-            if slot >= 0:
-                return slot
+        if self._pending and self._pool.free_count() == 0:
+            self._reap(block=True)          # wait for the GPU to finish the oldest holder
         return self._pool.acquire(-1 if timeout is None else int(timeout * 1000))
 
     def release(self, slot: int) -> None:

@@ -22,7 +22,8 @@ def test_resnet_pipeline_matches_direct_model(native):
             info, out = q.get_nowait()
             assert info["state"] == 0
             results.append(out["topk"])
-        frames = p.get_element("SyntheticFrames")._pool
+        src = p.get_element("SyntheticFrames")      # frames live in FIFO FramePool slots
+        frames = [src.frame_pool.view(s, src._shape, torch.uint8) for s in range(src.frame_pool.capacity)]
         model = ResNet50(seed=0, device="cuda")
         for i, r in enumerate(results):
             got = r.wait()
