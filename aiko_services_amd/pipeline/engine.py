@@ -331,6 +331,7 @@ class PipelineImpl(Pipeline):
         self.thread_local = threading.local()
         self.frames_completed = 0
         self._latencies: deque = deque(maxlen=1024)     # recent frame latencies (s) -> p50 / p99
+        self.gpu_event_log: deque = deque(maxlen=4096)  # (element, start, end) HIP events (AIKO_GPU_TIMING)
         self.pipeline_graph = self._create_pipeline_graph(context.definition)
         self.share["element_count"] = self.pipeline_graph.element_count
         self.share["streams"] = 0
@@ -362,6 +363,18 @@ class PipelineImpl(Pipeline):
         pick = lambda q: lat[min(len(lat) - 1, int(q * len(lat)))] * 1e3
         return {"frames": len(lat), "p50_ms": round(pick(0.50), 3), "p99_ms": round(pick(0.99), 3),
                 "max_ms": round(lat[-1] * 1e3, 3)}
+
+    def gpu_element_ms(self) -> dict:
+        """Mean GPU ms per frame of each local GPU element over the completed events in
+        ``gpu_event_log`` (``AIKO_GPU_TIMING=1``; also the placement balancer's input)."""
+        acc: dict = {}
+        for name, start, end in list(self.gpu_event_log):
+            if end is None or not end.query():
+                continue
+            a = acc.setdefault(name, [0.0, 0])
+            a[0] += start.elapsed_time(end)
+            a[1] += 1
+        return {name: round(t / n, 4) for name, (t, n) in acc.items() if n}
 
     def _add_node_properties(self, node_name, properties, predecessor_name):
         d = self.definition
@@ -773,6 +786,7 @@ class PipelineImpl(Pipeline):
                     metrics["time_pipeline"] = t - metrics["time_pipeline_start"]
                     if gpu_t is not None:
                         metrics.setdefault("gpu_events", {})[element.name] = gpu_t
+                        self.gpu_event_log.append((element.name, gpu_t, gpu_end))
                         if tracer is not None:
                             tracer.gpu_span(element_name, gpu_t, gpu_end,
                                             args={"frame_id": frame_id},

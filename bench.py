@@ -175,8 +175,10 @@ def main(argv=None):
     if a.model.startswith("whisper") and "--batch" not in (argv or sys.argv):
         a.batch = 16
 
-    procs = _control_plane(int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))) \
-        if a.parallel == "pp" else []
+    procs = []
+    if a.parallel == "pp":
+        os.environ.setdefault("AIKO_GPU_TIMING", "1")       # per-stage GPU ms (element events)
+        procs = _control_plane(int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")))
     from aiko_services_amd.parallel import dist as D
     D.init()
     ws, rank = D.world_size(), D.rank()
@@ -359,6 +361,27 @@ def run_pp(a, device, procs):
         except BaseException as exc:          # report, but still release the other ranks
             result["error"] = repr(exc)
         plane.barrier()                        # rank 0 finished timing: everyone stops
+        torch.cuda.synchronize()
+        # measured GPU ms per frame of this rank's stage (its elements' events; rank 0 includes
+        # its local copy of the replicated stage, weighted by the share of frames it ran)
+        mine = pipeline.gpu_element_ms()
+        for el in getattr(pipeline, "remote_pipelines", {}).values():
+            replicas = el[2]
+            for proxy in (replicas.proxies if replicas is not None else []):
+                child = getattr(proxy, "pipeline", None)
+                if child is not None:
+                    share = plan.local_share
+                    for k, v in child.gpu_element_ms().items():
+                        mine[f"local:{k}"] = round(v * share, 4)
+        if plane.control is not None:
+            import torch.distributed as tdist
+            gathered = [None] * ws
+            tdist.all_gather_object(gathered, mine, group=plane.control)
+        else:
+            gathered = [mine]
+        if result.get("out") is not None:
+            result["out"]["config"]["measured_rank_ms"] = [round(sum(g.values()), 4) for g in gathered]
+            result["out"]["config"]["measured_element_ms"] = gathered
         aiko.process.terminate(0)
 
     threading.Thread(target=driver, daemon=True, name="bench-driver").start()
