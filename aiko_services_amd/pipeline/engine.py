@@ -365,16 +365,15 @@ class PipelineImpl(Pipeline):
                 "max_ms": round(lat[-1] * 1e3, 3)}
 
     def gpu_element_ms(self) -> dict:
-        """Mean GPU ms per frame of each local GPU element over the completed events in
-        ``gpu_event_log`` (``AIKO_GPU_TIMING=1``; also the placement balancer's input)."""
+        """Median GPU ms per frame of each local GPU element over the completed events in
+        ``gpu_event_log`` (``AIKO_GPU_TIMING=1``; the placement balancer's input).  The median
+        keeps first-frame tuning / graph capture out of the figure."""
         acc: dict = {}
         for name, start, end in list(self.gpu_event_log):
             if end is None or not end.query():
                 continue
-            a = acc.setdefault(name, [0.0, 0])
-            a[0] += start.elapsed_time(end)
-            a[1] += 1
-        return {name: round(t / n, 4) for name, (t, n) in acc.items() if n}
+            acc.setdefault(name, []).append(start.elapsed_time(end))
+        return {name: round(sorted(v)[len(v) // 2], 4) for name, v in acc.items() if v}
 
     def _add_node_properties(self, node_name, properties, predecessor_name):
         d = self.definition
