@@ -36,7 +36,6 @@ tokens and are rebuilt (with a completion event) on the receiver.
 """
 from __future__ import annotations
 
-import threading
 from collections import deque
 
 import torch
@@ -125,18 +124,8 @@ class _RecvLink:
             # slots of a retired pool stay valid: their frames hold a reference to it
             pool = self.pool = FramePool(2 * self.depth, int(nbytes * 1.25) // _ALIGN * _ALIGN + _ALIGN,
                                          device=self.device if self.device.type == "cuda" else "cpu")
-        plane._reap()
-        try:
-            s = pool.acquire(timeout=0.0)
-        except RuntimeError:
-            s = -1
-        if s < 0:
-            plane._reap(block=True)
-            try:
-                s = pool.acquire(timeout=0.0)
-            except RuntimeError:
-                s = -1
-        if s < 0:                          # more frames in flight than slots: allocator buffer
+        s = pool.acquire(0.0)          # retires finished releases; waits on the GPU if all held
+        if s < 0:                      # more frames in flight than slots: allocator buffer
             plane.counters["pool_overflow"] += 1
             return None, torch.empty(nbytes, dtype=torch.uint8, device=self.device)
         return (pool, s), pool.view(s, (pool.slot_bytes,), torch.uint8)
@@ -189,8 +178,6 @@ class HopPlane:
             torch.cuda.synchronize(self.device)
         # host-side control group (gloo) for start-up barriers issued from helper threads
         self.control = tdist.new_group(backend="gloo") if D.is_initialized() else None
-        self._releases: deque = deque()     # (event | None, pool, slot)
-        self._lock = threading.Lock()
         self.counters = {"sent_msgs": 0, "sent_bytes": 0, "recv_msgs": 0, "recv_bytes": 0,
                          "pool_overflow": 0}
 
@@ -329,30 +316,12 @@ class HopPlane:
 
     # ---- slot release ------------------------------------------------------------------------
     def release(self, handles) -> None:
-        """Return receive slots once the work queued so far on the current stream is done."""
-        handles = [h for h in (handles or []) if h is not None]
-        if not handles:
-            return
-        ev = None
-        if self.device.type == "cuda":
-            ev = torch.cuda.Event()
-            ev.record()
-        with self._lock:
-            for pool, slot in handles:
-                self._releases.append((ev, pool, slot))
-        self._reap()
-
-    def _reap(self, block: bool = False):
-        with self._lock:
-            while self._releases:
-                ev, pool, slot = self._releases[0]
-                if ev is not None and not ev.query():
-                    if not block:
-                        break
-                    ev.synchronize()
-                    block = False            # one blocking wait frees at least one slot
-                self._releases.popleft()
-                pool.release(slot)
+        """Return receive slots once the work queued so far on the current stream is done
+        (``FramePool.release_after``: a HIP event gates the reuse)."""
+        for h in handles or []:
+            if h is not None:
+                pool, slot = h
+                pool.release_after(slot)
 
     def barrier(self):
         if self.control is not None:
@@ -368,9 +337,8 @@ class HopPlane:
     def close(self):
         for link in self.send_links.values():
             link.drain()
-        self._reap(block=True)
-        while self._releases:
-            self._reap(block=True)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
 
 
 _plane: HopPlane | None = None

@@ -62,6 +62,7 @@ def spawn_workers(plan: Plan, plan_path: str | None = None, env: dict | None = N
                        ["-m", "aiko_services_amd.parallel.launch", "worker", plan_path, str(spec.rank)],
                        env=child)
     atexit.register(manager.terminate_all)
+    atexit.register(lambda: os.path.exists(plan_path) and os.unlink(plan_path))
     return manager, plan_path
 
 

@@ -51,7 +51,6 @@ def main():
         assert torch.equal(res["p"].cpu(), hp) and torch.equal(res["i"], idx)
         plane.release([handle])
     torch.cuda.synchronize()
-    plane._reap()
     st = plane.stats()
     assert st["pool_overflow"] == 0 and st["recv_msgs"] == 6, st
     hop.shutdown_plane()
