@@ -236,6 +236,37 @@ class ResNet50(WeightsMixin):
             cur.wait_stream(s)
         return out
 
+    # ---- two-part forward (frame-lane phase gating, elements/gpu/vision.py) -----------------
+    SPLIT_BLOCK = 6          # end of stage 2: stem + stages 1-2 (memory-bound) | stages 3-4 (compute-bound)
+
+    def logits_part_a(self, frames: torch.Tensor, tag: str = "") -> torch.Tensor:
+        """uint8 frames -> activation after bottleneck ``SPLIT_BLOCK`` (a workspace buffer)."""
+        x = frames if frames.dtype != torch.uint8 else self.preprocess(frames, tag)
+        B = x.shape[0]
+        S = self.image_size
+        Ho, Wo = C.stem_out_hw(S, S)
+        Hm, Wm = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
+        pool = self._buf(tag + "pool", (B, Hm, Wm, 64))
+        if self.fuse_stem_pool:
+            x = C.stem_pool(x, self.stem, (S, S), out=pool)
+        else:
+            st = self._buf(tag + "stem", (B, Ho, Wo, 64))
+            x = V.maxpool2d(C.conv2d(x, self.stem, out=st, image_hw=(S, S)), 3, 2, 1, out=pool)
+        t1 = None
+        for bi in range(self.SPLIT_BLOCK + 1):
+            x, t1 = self._block(bi, x, tag, B, 0, B, t1, chain=bi < self.SPLIT_BLOCK)
+        assert t1 is None, "the split must not cut a chained block boundary"
+        return x
+
+    def logits_part_b(self, x: torch.Tensor, tag: str = "") -> torch.Tensor:
+        """Activation after bottleneck ``SPLIT_BLOCK`` -> logits."""
+        B = x.shape[0]
+        t1 = None
+        for bi in range(self.SPLIT_BLOCK + 1, len(self.blocks)):
+            x, t1 = self._block(bi, x, tag, B, 0, B, t1)
+        f = V.avgpool(x, out=self._buf(tag + "gap", (B, x.shape[3])))
+        return C.linear(f, self.fc, out=self._buf(tag + "logits", (B, self.num_classes)))
+
     def features(self, frames: torch.Tensor) -> torch.Tensor:
         """uint8 [B, H, W, 3] -> pooled features bf16 [B, 2048]."""
         return self.features_from_stem(self.preprocess(frames))

@@ -229,3 +229,25 @@ def test_resnet50_chain_matches_unchained(native):
     got = m.logits(frames).float()
     cos = torch.nn.functional.cosine_similarity(got.flatten(), ref.flatten(), dim=0).item()
     assert cos > 0.999, cos
+
+
+def test_phase_gated_lanes_match_ungated(native):
+    """Lane phase gating (two-part forward, stage 1-2 half waits for the previous frame's)
+    gives bit-identical results to the single-graph forward."""
+    import bench
+    from aiko_services_amd.pipeline.definition import parse_pipeline_definition_dict
+    from aiko_services_amd.pipeline.engine import PipelineImpl
+    outs = []
+    for gate in (False, True):
+        d = bench.definition(8, True, 224, 224, 2)
+        d["elements"][1]["parameters"]["phase_gate"] = gate
+        q = queue.Queue()
+        p = PipelineImpl.create_pipeline("<t>", parse_pipeline_definition_dict(d), None, None, "g", [], 0, None, 60,
+                                         queue_response=q)
+        res = []
+        for i in range(6):
+            p.process_frame({"stream_id": "g", "frame_id": i}, {})
+            res.append(q.get_nowait()[1]["topk"])
+        outs.append([r.wait()["top_index"].clone() for r in res])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
