@@ -4,7 +4,7 @@
 // top-k + NMS — three kernels.  Measured (rocprofv3, YOLOv8-n bench batch: B=64 x 8400 anchors,
 // random weights, 1024 candidates per image): the former single 1024-thread workgroup per
 // image took 246 us (IoU bitmask 130 us on 64 CUs, shuffle-bound greedy scan 86 us); now
-// nms_select 31 us + nms_mask 46 us + nms_greedy 37 us = 114 us:
+// nms_select 31 us + nms_mask 46 us + nms_greedy 26 us = 103 us:
 //   nms_select (one workgroup per image): phases 1-3, sorted candidates to a workspace;
 //   nms_mask   (B x 136 waves, balanced): phase 4 over the whole GPU, plus the transposed
 //              diagonal words;
@@ -421,6 +421,7 @@ __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, i
 constexpr int kGreedyThreads = 1024;
 __global__ __launch_bounds__(kGreedyThreads) void nms_greedy_kernel(NmsParams p, NmsWork ws) {
   __shared__ unsigned long long words[kMaskWords * kMaxCand];   // [w][i]
+  __shared__ unsigned long long lowd[kMaxCand];                  // row i's transposed diagonal word
   __shared__ int kept[kMaxCand];
   __shared__ int nk_sh;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -437,8 +438,11 @@ __global__ __launch_bounds__(kGreedyThreads) void nms_greedy_kernel(NmsParams p,
 #pragma unroll
     for (int w = 0; w < kMaskWords; ++w)
       tmp[w] = (w < W && tid < n) ? mk[(long)w * kMaxCand + tid] : 0ull;
+    const unsigned long long lw =
+        tid < n ? ws.low[((long)b * kMaskWords + (tid >> 6)) * kMaxCand + tid] : 0ull;
 #pragma unroll
     for (int w = 0; w < kMaskWords; ++w) words[w * kMaxCand + tid] = tmp[w];
+    lowd[tid] = lw;
   }
   __syncthreads();
   if (tid < 64) {
@@ -448,7 +452,7 @@ __global__ __launch_bounds__(kGreedyThreads) void nms_greedy_kernel(NmsParams p,
       unsigned long long cur = readlane64(removed, w);
       const int row = w * 64 + lane;
       // suppressors of this lane's candidate inside the word (rows k < row, transposed diagonal)
-      const unsigned long long low = row < n ? ws.low[((long)b * kMaskWords + w) * kMaxCand + row] : 0ull;
+      const unsigned long long low = row < n ? lowd[row] : 0ull;
       const int left = n - w * 64;
       const unsigned long long valid = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
       const unsigned long long alive = ~cur & valid;
@@ -478,13 +482,24 @@ __global__ __launch_bounds__(kGreedyThreads) void nms_greedy_kernel(NmsParams p,
         kept[nkept + __popcll(below)] = row;
       }
       nkept += __popcll(keep);
+      // OR the kept rows' words into the later words: 8 LDS reads in flight per round (a
+      // one-read-per-iteration loop exposes the LDS latency for every kept row)
       unsigned long long kk = keep;
       unsigned long long acc = 0ull;
       const bool mine = lane > w && lane < W;
+      const unsigned long long* wl = words + lane * kMaxCand + w * 64;
       while (kk) {
-        const int bb = __ffsll((long long)kk) - 1;
-        kk &= kk - 1ull;
-        if (mine) acc |= words[lane * kMaxCand + w * 64 + bb];
+        int bsel[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          bsel[u] = kk ? __ffsll((long long)kk) - 1 : -1;
+          kk &= kk - 1ull;
+        }
+        unsigned long long v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = (mine && bsel[u] >= 0) ? wl[bsel[u]] : 0ull;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc |= v[u];
       }
       removed |= acc;
     }
