@@ -215,9 +215,14 @@ __global__ __launch_bounds__(kNmsThreads) void nms_select_kernel(NmsParams p, Nm
   const float4* bx = p.boxes + (long)b * A;
   const int* cl = p.cls + (long)b * A;
 
-  if (tid == 0) sh[32] = 0;
+  if (tid == 0) {
+    sh[32] = 0;
+    sh[36] = 0;                      // max key
+    sh[37] = (int)0xffffffffu;       // min live key (as unsigned)
+  }
   __syncthreads();
   int cnt = 0;
+  unsigned kmax = 0u, kmin = 0xffffffffu;
   for (int i0 = 0; i0 < A; i0 += 8 * kNmsThreads) {     // 8 independent loads in flight
     float v[8];
 #pragma unroll
@@ -232,41 +237,66 @@ __global__ __launch_bounds__(kNmsThreads) void nms_select_kernel(NmsParams p, Nm
         const unsigned k = v[u] > p.conf ? __float_as_uint(v[u]) : 0u;
         keys[i] = k;
         cnt += k != 0u;
+        kmax = max(kmax, k);
+        if (k != 0u) kmin = min(kmin, k);
       }
     }
   }
-  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
-  if (lane == 0) atomicAdd(&sh[32], cnt);
+  for (int o = 32; o > 0; o >>= 1) {
+    cnt += __shfl_xor(cnt, o, 64);
+    kmax = max(kmax, (unsigned)__shfl_xor((int)kmax, o, 64));
+    kmin = min(kmin, (unsigned)__shfl_xor((int)kmin, o, 64));
+  }
+  if (lane == 0) {
+    atomicAdd(&sh[32], cnt);
+    atomicMax(reinterpret_cast<unsigned*>(&sh[36]), kmax);
+    atomicMin(reinterpret_cast<unsigned*>(&sh[37]), kmin);
+  }
   __syncthreads();
   const int total = sh[32];
   const int K = min(p.max_cand, total);
   if (tid == 0) ws.n[b] = K;
-  if (K == 0) return;
+  if (K == 0 || p.stop == 1) return;
 
-  // radix select of the K-th largest key
+  // radix select of the K-th largest key, on d = key - (min live key): only as many 8-bit digits
+  // as the live range needs (scores in (conf, 1) span ~24 bits -> 3 passes, not 4); skipped when
+  // every live key is a candidate.  T = threshold key, remaining = candidates equal to T.
+  const unsigned klo = (unsigned)sh[37];
+  const unsigned range = (unsigned)sh[36] - klo;
   unsigned prefix = 0u, pmask = 0u;
   int remaining = K;
-  for (int shift = 24; shift >= 0; shift -= 8) {
+  const int top_shift = total <= p.max_cand ? -8 : (range == 0u ? -8 : ((31 - __clz((int)range)) / 8) * 8);
+  for (int shift = top_shift; shift >= 0; shift -= 8) {
     if (tid < 256) hist[tid] = 0u;
     __syncthreads();
+    // scores cluster: most live keys of a wave share a bin; a wave accumulates same-bin ballots
+    // in a (wave-uniform) running count and issues one LDS atomic per bin change, not one per
+    // iteration on the same hot address
+    unsigned run_bin = 0u, run_cnt = 0u;
     for (int i0 = 0; i0 < A; i0 += kNmsThreads) {   // wave-uniform trip count (ballots below)
       const int i = i0 + tid;
       const unsigned k = i < A ? keys[i] : 0u;
-      const bool live = k != 0u && (k & pmask) == prefix;
-      const unsigned bin = (k >> shift) & 255u;
-      // scores cluster: most live keys of a wave share a bin -> one aggregated LDS atomic
+      const unsigned d = k - klo;
+      const bool live = k != 0u && (d & pmask) == prefix;
+      const unsigned bin = (d >> shift) & 255u;
       const unsigned long long lm = __ballot(live);
       if (lm) {
         const int leader = __ffsll((long long)lm) - 1;
         const unsigned lbin = __shfl(bin, leader, 64);
         const unsigned long long same = __ballot(live && bin == lbin);
         if (same == lm) {
-          if (lane == leader) atomicAdd(&hist[lbin], (unsigned)__popcll(lm));
+          if (lbin != run_bin) {
+            if (lane == 0 && run_cnt) atomicAdd(&hist[run_bin], run_cnt);
+            run_bin = lbin;
+            run_cnt = 0u;
+          }
+          run_cnt += (unsigned)__popcll(lm);
         } else if (live) {
           atomicAdd(&hist[bin], 1u);
         }
       }
     }
+    if (lane == 0 && run_cnt) atomicAdd(&hist[run_bin], run_cnt);
     __syncthreads();
     if (wave == 0) {
       const int s_l = hist[4 * lane] + hist[4 * lane + 1] + hist[4 * lane + 2] + hist[4 * lane + 3];
@@ -296,8 +326,12 @@ __global__ __launch_bounds__(kNmsThreads) void nms_select_kernel(NmsParams p, Nm
     remaining = sh[35];
     __syncthreads();
   }
-  const unsigned T = prefix;
+  // all live keys are candidates: threshold below every live key, none "equal"
+  const bool take_all = total <= p.max_cand;
+  const unsigned T = take_all ? 0u : (top_shift < 0 ? klo : klo + prefix);
+  if (take_all) remaining = 0;
   const int n_gt = K - remaining;
+  if (p.stop == 2) return;
 
   // deterministic compaction (contiguous chunks + block scan) and bitonic sort
   const int chunk = (A + kNmsThreads - 1) / kNmsThreads;
@@ -324,20 +358,43 @@ __global__ __launch_bounds__(kNmsThreads) void nms_select_kernel(NmsParams p, Nm
   while (NP < K) NP <<= 1;
   if (tid >= K && tid < NP) ckey[tid] = 0ull;
   __syncthreads();
-  for (int size = 2; size <= NP; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      const int i = tid, j = tid ^ stride;
-      if (i < NP && j > i) {
-        const unsigned long long a = ckey[i], c = ckey[j];
-        const bool desc = (i & size) == 0;
-        if (desc ? (a < c) : (a > c)) {
-          ckey[i] = c;
-          ckey[j] = a;
-        }
+  if (p.stop == 3) return;
+  // sort = per-wave bitonic sort of 64 keys in registers (21 shuffle passes, no barrier) + merge
+  // by rank: a key's final position is its place in its own wave's sorted list plus, for each of
+  // the other lists, the number of keys greater than it (7-step binary search of the LDS copy;
+  // the 15 searches are independent).  Keys are unique (index in the low word); padding keys
+  // are 0 and are not written.  Two barriers instead of the 55-pass block-wide network's 20.
+  {
+    unsigned long long v = tid < NP ? ckey[tid] : 0ull;
+    for (int size = 2; size <= 64; size <<= 1) {
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        const unsigned lo = __shfl_xor((unsigned)(v & 0xffffffffull), stride, 64);
+        const unsigned hi = __shfl_xor((unsigned)(v >> 32), stride, 64);
+        const unsigned long long c = ((unsigned long long)hi << 32) | lo;
+        const bool desc = size == 64 || (lane & size) == 0, lower = (lane & stride) == 0;
+        v = (desc == lower) ? (v > c ? v : c) : (v < c ? v : c);
       }
-      __syncthreads();
     }
+    __syncthreads();
+    ckey[tid] = v;                                   // [wave][64] sorted descending
+    __syncthreads();
+    int rank = lane;
+    const int nl = (NP + 63) >> 6;
+#pragma unroll 4
+    for (int l = 0; l < nl; ++l) {
+      if (l == wave) continue;
+      const unsigned long long* L = ckey + l * 64;
+      int pos = 0;
+#pragma unroll
+      for (int st = 32; st > 0; st >>= 1)
+        if (L[pos + st - 1] > v) pos += st;
+      rank += pos + (L[pos] > v ? 1 : 0);
+    }
+    __syncthreads();
+    if (v != 0ull) ckey[rank] = v;
+    __syncthreads();
   }
+  if (p.stop == 4) return;
   // sorted keys + class-offset boxes to the workspace
   for (int i = tid; i < K; i += kNmsThreads) {
     const unsigned long long ck = ckey[i];
@@ -347,6 +404,35 @@ __global__ __launch_bounds__(kNmsThreads) void nms_select_kernel(NmsParams p, Nm
     ws.ckey[(long)b * kMaxCand + i] = ck;
     ws.cbox[(long)b * kMaxCand + i] = make_float4(q.x + off, q.y + off, q.z + off, q.w + off);
   }
+}
+
+// IoU > thr bits of row box bi against the 64 column boxes in LDS (bit jj = column jj), one
+// fully unrolled pass: constant bit positions, broadcast LDS reads batched (FULL: all 64 columns
+// valid, no per-column guard).  A 4-compare overlap test on both axes (a superset of inter > 0)
+// gates the exact intersection + IEEE division, so the decisions are box_iou() > thr bit for
+// bit; most pairs (other classes sit max_wh apart) stop at the 4 compares.  The test is symmetric
+// bit for bit (fminf / fmaxf and the area sum commute), so the diagonal word's transposed half
+// comes out of the same pass.
+template <bool FULL>
+__device__ __forceinline__ unsigned long long mask_word(const float4* col, float4 bi, float area_i,
+                                                        int je, float thr) {
+  unsigned long long hit = 0ull;
+#pragma unroll
+  for (int jj = 0; jj < 64; ++jj) {
+    if (FULL || jj < je) {                                  // wave-uniform
+      const float4 bj = col[jj];
+      if (thr < 0.f || (bi.z > bj.x && bj.z > bi.x && bi.w > bj.y && bj.w > bi.y)) {
+        const float iw = fmaxf(0.f, fminf(bi.z, bj.z) - fmaxf(bi.x, bj.x));
+        const float ih = fmaxf(0.f, fminf(bi.w, bj.w) - fmaxf(bi.y, bj.y));
+        const float inter = iw * ih;
+        if (inter > 0.f || thr < 0.f) {
+          const float iou = inter / (area_i + (bj.z - bj.x) * (bj.w - bj.y) - inter);
+          if (iou > thr) hit |= 1ull << jj;
+        }
+      }
+    }
+  }
+  return hit;
 }
 
 // 2. IoU suppression bitmask over the whole GPU: one wave per (image, 64-row block rb, word
@@ -375,34 +461,13 @@ __global__ __launch_bounds__(64) void nms_mask_kernel(NmsParams p, NmsWork ws) {
   if (i >= n) return;
   const float area_i = (bi.z - bi.x) * (bi.w - bi.y);
   const int je = min(64, n - j0);
-  unsigned long long bits = 0ull, low = 0ull;
-  const int jb = w == rb ? lane + 1 : 0;
-  for (int jj = jb; jj < je; ++jj) {
-    const float4 bj = col[jj];
-    const float iw = fmaxf(0.f, fminf(bi.z, bj.z) - fmaxf(bi.x, bj.x));
-    const float ih = fmaxf(0.f, fminf(bi.w, bj.w) - fmaxf(bi.y, bj.y));
-    const float inter = iw * ih;
-    // disjoint pairs (most of them: other classes sit max_wh apart) have IoU 0 — skip the
-    // IEEE division; identical predicate to box_iou() > iou for iou >= 0
-    if (inter > 0.f || p.iou < 0.f) {
-      const float iou = inter / (area_i + (bj.z - bj.x) * (bj.w - bj.y) - inter);
-      if (iou > p.iou) bits |= 1ull << jj;
-    }
-  }
-  if (w == rb) {
-    for (int jj = 0; jj < lane; ++jj) {
-      const float4 bj = col[jj];
-      const float iw = fmaxf(0.f, fminf(bj.z, bi.z) - fmaxf(bj.x, bi.x));
-      const float ih = fmaxf(0.f, fminf(bj.w, bi.w) - fmaxf(bj.y, bi.y));
-      const float inter = iw * ih;
-      if (inter > 0.f || p.iou < 0.f) {
-        // same operand order as row j's own test above: bit-identical decisions
-        const float area_j = (bj.z - bj.x) * (bj.w - bj.y);
-        const float iou = inter / (area_j + area_i - inter);
-        if (iou > p.iou) low |= 1ull << jj;
-      }
-    }
-    ws.low[((long)b * kMaskWords + w) * kMaxCand + i] = low;
+  const bool diag = w == rb;
+  const unsigned long long hit = je == 64 ? mask_word<true>(col, bi, area_i, je, p.iou)
+                                          : mask_word<false>(col, bi, area_i, je, p.iou);
+  unsigned long long bits = hit;
+  if (diag) {
+    bits = lane == 63 ? 0ull : hit & (~0ull << (lane + 1));
+    ws.low[((long)b * kMaskWords + w) * kMaxCand + i] = hit & ((1ull << lane) - 1ull);
   }
   ws.mask[((long)b * kMaskWords + w) * kMaxCand + i] = bits;
 }
@@ -413,14 +478,17 @@ __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, i
   return ((unsigned long long)hi << 32) | lo;
 }
 
-// 3. greedy scan per image: the image's mask words are first staged into LDS by 256 threads
-//    (coalesced, 128 KB), then one wave scans: lane w holds the "removed" word w; inside a
-//    64-candidate word the suppression chain runs on scalars (v_readlane of the diagonal
-//    words), then the kept rows' words are OR-ed lane-parallel into the later words; stops at
-//    max_det.  Finally the kept boxes are mapped back from letterbox to frame coordinates.
+// 3. greedy scan per image.  The mask words at / right of the diagonal are staged into LDS
+//    (row stride padded by one word: the scan's lane-parallel reads hit distinct banks).  (A
+//    chunked variant — 256 rows at a time, next chunk loaded during the scan, stopping at
+//    max_det — measured slower: 26.7 -> 31.6 us.)  The scan: lane w holds the "removed" word w;
+//    inside a 64-candidate word the suppression chain is a ballot fixed point over the
+//    transposed diagonal words, then the kept rows' words are OR-ed lane-parallel into the later
+//    words.  Finally the kept boxes are mapped back from letterbox to frame coordinates.
 constexpr int kGreedyThreads = 1024;
+constexpr int kWordStride = kMaxCand + 1;   // padded: lane w's reads of words[w][row] hit distinct banks
 __global__ __launch_bounds__(kGreedyThreads) void nms_greedy_kernel(NmsParams p, NmsWork ws) {
-  __shared__ unsigned long long words[kMaskWords * kMaxCand];   // [w][i]
+  __shared__ unsigned long long words[kMaskWords * kWordStride];  // [w][i]
   __shared__ unsigned long long lowd[kMaxCand];                  // row i's transposed diagonal word
   __shared__ int kept[kMaxCand];
   __shared__ int nk_sh;
@@ -430,78 +498,82 @@ __global__ __launch_bounds__(kGreedyThreads) void nms_greedy_kernel(NmsParams p,
   const int W = (n + 63) >> 6;
   const unsigned long long* mk = ws.mask + (long)b * kMaxCand * kMaskWords;
   // staging: all 16 loads of a thread are issued before the first LDS store (a load -> store
-  // loop would pay one HBM/L2 latency per word); words left of the diagonal are copied too but
-  // never read by the scan
+  // loop would pay one HBM/L2 latency per word); only the words at / right of the diagonal
+  // (w >= row block), the only ones the scan reads
   {
     static_assert(kGreedyThreads == kMaxCand, "one thread per candidate row");
+    const int rb = tid >> 6;
     unsigned long long tmp[kMaskWords];
 #pragma unroll
     for (int w = 0; w < kMaskWords; ++w)
-      tmp[w] = (w < W && tid < n) ? mk[(long)w * kMaxCand + tid] : 0ull;
+      tmp[w] = (w >= rb && w < W && tid < n) ? mk[(long)w * kMaxCand + tid] : 0ull;
     const unsigned long long lw =
-        tid < n ? ws.low[((long)b * kMaskWords + (tid >> 6)) * kMaxCand + tid] : 0ull;
+        tid < n ? ws.low[((long)b * kMaskWords + rb) * kMaxCand + tid] : 0ull;
 #pragma unroll
-    for (int w = 0; w < kMaskWords; ++w) words[w * kMaxCand + tid] = tmp[w];
+    for (int w = 0; w < kMaskWords; ++w) words[w * kWordStride + tid] = tmp[w];
     lowd[tid] = lw;
   }
+  if (tid == 0) nk_sh = 0;
   __syncthreads();
   if (tid < 64) {
     unsigned long long removed = 0ull;
     int nkept = 0;
-    for (int w = 0; w < W && nkept < p.max_det; ++w) {
-      unsigned long long cur = readlane64(removed, w);
-      const int row = w * 64 + lane;
-      // suppressors of this lane's candidate inside the word (rows k < row, transposed diagonal)
-      const unsigned long long low = row < n ? lowd[row] : 0ull;
-      const int left = n - w * 64;
-      const unsigned long long valid = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
-      const unsigned long long alive = ~cur & valid;
-      const bool me_alive = (alive >> lane) & 1ull;
-      // greedy inside the word as a fixed point: kept = alive minus those with a kept
-      // suppressor.  Candidate c's status is final once all k < c are, so <= 64 rounds; the
-      // first repeat is the (unique) greedy solution.  One ballot per round, not one
-      // dependent step per candidate.
-      unsigned long long keep = alive;
-      for (int it = 0; it <= 64; ++it) {
-        const unsigned long long nk = __ballot(me_alive && !(low & keep));
-        if (nk == keep) break;
-        keep = nk;
-      }
-      const int room = p.max_det - nkept;
-      if (__popcll(keep) > room) {
-        unsigned long long trimmed = 0ull, kk = keep;
-        for (int r = 0; r < room; ++r) {
-          const unsigned long long low = kk & (~kk + 1ull);
-          trimmed |= low;
-          kk ^= low;
+    {
+      for (int w = 0; w < W && nkept < p.max_det; ++w) {
+        unsigned long long cur = readlane64(removed, w);
+        const int row = w * 64 + lane;
+        // suppressors of this lane's candidate inside the word (rows k < row, transposed diagonal)
+        const unsigned long long low = row < n ? lowd[row] : 0ull;
+        const int left = n - w * 64;
+        const unsigned long long valid = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
+        const unsigned long long alive = ~cur & valid;
+        const bool me_alive = (alive >> lane) & 1ull;
+        // greedy inside the word as a fixed point: kept = alive minus those with a kept
+        // suppressor.  Candidate c's status is final once all k < c are, so <= 64 rounds; the
+        // first repeat is the (unique) greedy solution.  One ballot per round, not one
+        // dependent step per candidate.
+        unsigned long long keep = alive;
+        for (int it = 0; it <= 64; ++it) {
+          const unsigned long long nk = __ballot(me_alive && !(low & keep));
+          if (nk == keep) break;
+          keep = nk;
         }
-        keep = trimmed;
-      }
-      if ((keep >> lane) & 1ull) {
-        const unsigned long long below = lane ? (keep & ((1ull << lane) - 1ull)) : 0ull;
-        kept[nkept + __popcll(below)] = row;
-      }
-      nkept += __popcll(keep);
-      // OR the kept rows' words into the later words: 8 LDS reads in flight per round (a
-      // one-read-per-iteration loop exposes the LDS latency for every kept row)
-      unsigned long long kk = keep;
-      unsigned long long acc = 0ull;
-      const bool mine = lane > w && lane < W;
-      const unsigned long long* wl = words + lane * kMaxCand + w * 64;
-      while (kk) {
-        int bsel[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          bsel[u] = kk ? __ffsll((long long)kk) - 1 : -1;
-          kk &= kk - 1ull;
+        const int room = p.max_det - nkept;
+        if (__popcll(keep) > room) {
+          unsigned long long trimmed = 0ull, kk = keep;
+          for (int r = 0; r < room; ++r) {
+            const unsigned long long lowb = kk & (~kk + 1ull);
+            trimmed |= lowb;
+            kk ^= lowb;
+          }
+          keep = trimmed;
         }
-        unsigned long long v[8];
+        if ((keep >> lane) & 1ull) {
+          const unsigned long long below = lane ? (keep & ((1ull << lane) - 1ull)) : 0ull;
+          kept[nkept + __popcll(below)] = row;
+        }
+        nkept += __popcll(keep);
+        // OR the kept rows' words into the later words: 8 LDS reads in flight per round (a
+        // one-read-per-iteration loop exposes the LDS latency for every kept row)
+        unsigned long long kk = keep;
+        unsigned long long acc = 0ull;
+        const bool mine = lane > w && lane < W;
+        const unsigned long long* wl = words + lane * kWordStride + w * 64;
+        while (kk) {
+          int bsel[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = (mine && bsel[u] >= 0) ? wl[bsel[u]] : 0ull;
+          for (int u = 0; u < 8; ++u) {
+            bsel[u] = kk ? __ffsll((long long)kk) - 1 : -1;
+            kk &= kk - 1ull;
+          }
+          unsigned long long v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) acc |= v[u];
+          for (int u = 0; u < 8; ++u) v[u] = (mine && bsel[u] >= 0) ? wl[bsel[u]] : 0ull;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) acc |= v[u];
+        }
+        removed |= acc;
       }
-      removed |= acc;
     }
     if (lane == 0) nk_sh = nkept;
   }
@@ -594,6 +666,7 @@ extern "C" int aiko_topk_nms(const void* boxes, const float* scores, const int* 
   p.det = det;
   p.count = count;
   p.stop = 99;
+  if (const char* e = getenv("AIKO_NMS_STOP")) p.stop = atoi(e);
   char* w = static_cast<char*>(workspace);
   aiko::NmsWork ws;
   ws.mask = reinterpret_cast<unsigned long long*>(w);
@@ -606,6 +679,7 @@ extern "C" int aiko_topk_nms(const void* boxes, const float* scores, const int* 
   w += ((size_t)B * 4 + 255) / 256 * 256;
   ws.low = reinterpret_cast<unsigned long long*>(w);
   aiko::nms_select_kernel<<<B, aiko::kNmsThreads, 0, stream>>>(p, ws);
+  if (p.stop < 99) return 0;
   aiko::nms_mask_kernel<<<B * aiko::kMaskPairs, 64, 0, stream>>>(p, ws);
   aiko::nms_greedy_kernel<<<B, aiko::kGreedyThreads, 0, stream>>>(p, ws);
   return (int)hipGetLastError();
