@@ -4,28 +4,31 @@
 // top-k + NMS — three kernels.  Measured (rocprofv3, YOLOv8-n bench batch: B=64 x 8400 anchors,
 // random weights, 1024 candidates per image): the former single 1024-thread workgroup per
 // image took 246 us (IoU bitmask 130 us on 64 CUs, shuffle-bound greedy scan 86 us); now
-// nms_select 31 us + nms_mask 46 us + nms_greedy 26 us = 103 us:
-//   nms_select (one workgroup per image): phases 1-3, sorted candidates to a workspace;
-//   nms_mask   (B x 136 waves, balanced): phase 4 over the whole GPU, plus the transposed
-//              diagonal words;
-//   nms_greedy (one workgroup per image): masks staged in LDS, phase 5 per 64-candidate word as
-//              a ballot fixed point instead of a 64-step dependent chain, phase 6.
-// Phases (of the original single-kernel design):
+// nms_select 24 us + nms_mask 31-32 us + nms_greedy 26 us = 83 us (scripts/nms_phases.py,
+// per-phase stops: scripts/nms_stop.sh):
+//   nms_select (one workgroup per image): keys (5 us), radix select (2 x 12-bit passes over
+//              key - min key, skipped when every live key is a candidate), compaction, sort
+//              (per-wave register bitonic + merge by rank), sorted candidates to a workspace;
+//   nms_mask   (B x 136 waves, balanced): the IoU bitmask over the whole GPU, 4-compare overlap
+//              gate before the exact IoU, plus the transposed diagonal words;
+//   nms_greedy (one workgroup per image): upper-triangle masks staged in LDS (padded rows), the
+//              scan per 64-candidate word as a ballot fixed point, output mapping.
+// Phases:
 //   1. scores above the confidence threshold -> 32-bit keys (float bits are monotone for
 //      positive floats) in LDS;
-//   2. radix select (4 x 8-bit passes, 256-bin LDS histograms, one wave resolves each pass
-//      with a suffix scan) finds the K-th largest key, K = min(max_candidates, #above conf);
+//   2. radix select finds the K-th largest key, K = min(max_candidates, #above conf);
 //   3. deterministic compaction (block-wide exclusive scan, ties -> lowest anchor index) and a
-//      bitonic sort of the <= 1024 candidates by (score desc, index asc);
-//   4. the IoU suppression bitmask (n x ceil(n/64) 64-bit words) is built in LDS by all 16
-//      waves — boxes are offset by class * max_wh so one pass is class-aware — overlaying the
-//      key array that is no longer needed;
+//      sort of the <= 1024 candidates by (score desc, index asc);
+//   4. the IoU suppression bitmask (n x ceil(n/64) 64-bit words) — boxes are offset by
+//      class * max_wh so one pass is class-aware;
 //   5. one wave scans the bitmask 64 candidates at a time: inside a word the suppression chain
-//      is resolved from the diagonal words with wave shuffles, then the kept rows' words are
-//      OR-ed into the later words lane-parallel; stops at max_det;
+//      is resolved from the diagonal words, then the kept rows' words are OR-ed into the later
+//      words lane-parallel; stops at max_det;
 //   6. kept boxes are mapped back from letterbox to frame coordinates, clipped, and written
 //      as fixed-size [max_det, 6] rows (x1, y1, x2, y2, score, class) + a count, so results can
 //      be all-gathered over RCCL without a size exchange.
+// AIKO_NMS_STOP=<phase> (profiling only) ends the kernels early: 1-4 inside nms_select (then
+// nothing else runs), 5 / 6 inside nms_greedy.
 #include "common.h"
 
 namespace aiko {
@@ -200,11 +203,12 @@ struct NmsWork {
 
 // 1. keys, radix select, deterministic compaction and bitonic sort — one 1024-thread
 //    workgroup per image, keys in LDS; writes the sorted candidates to the workspace.
+constexpr int kRadixBits = 12, kRadixBins = 1 << kRadixBits;   // 4096 bins = 4 per thread
 __global__ __launch_bounds__(kNmsThreads) void nms_select_kernel(NmsParams p, NmsWork ws) {
   constexpr int REGION0 = kMaxAnchors * 4;
   __shared__ __attribute__((aligned(16))) unsigned char region0[REGION0];
   __shared__ unsigned long long ckey[kMaxCand];
-  __shared__ unsigned hist[256];
+  __shared__ unsigned hist[kRadixBins];
   __shared__ int sh[40];
 
   unsigned* keys = reinterpret_cast<unsigned*>(region0);
@@ -223,15 +227,16 @@ __global__ __launch_bounds__(kNmsThreads) void nms_select_kernel(NmsParams p, Nm
   __syncthreads();
   int cnt = 0;
   unsigned kmax = 0u, kmin = 0xffffffffu;
-  for (int i0 = 0; i0 < A; i0 += 8 * kNmsThreads) {     // 8 independent loads in flight
-    float v[8];
+  // 16 independent loads in flight: one latency round covers A <= 16384 (YOLO VGA: 8400 / 6300)
+  for (int i0 = 0; i0 < A; i0 += 16 * kNmsThreads) {
+    float v[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 16; ++u) {
       const int i = i0 + u * kNmsThreads + tid;
       v[u] = i < A ? sc[i] : 0.f;
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 16; ++u) {
       const int i = i0 + u * kNmsThreads + tid;
       if (i < A) {
         const unsigned k = v[u] > p.conf ? __float_as_uint(v[u]) : 0u;
@@ -258,27 +263,28 @@ __global__ __launch_bounds__(kNmsThreads) void nms_select_kernel(NmsParams p, Nm
   if (tid == 0) ws.n[b] = K;
   if (K == 0 || p.stop == 1) return;
 
-  // radix select of the K-th largest key, on d = key - (min live key): only as many 8-bit digits
-  // as the live range needs (scores in (conf, 1) span ~24 bits -> 3 passes, not 4); skipped when
+  // radix select of the K-th largest key, on d = key - (min live key), 12-bit digits: only as
+  // many as the live range needs (scores in (conf, 1) span ~24 bits -> 2 passes); skipped when
   // every live key is a candidate.  T = threshold key, remaining = candidates equal to T.
   const unsigned klo = (unsigned)sh[37];
   const unsigned range = (unsigned)sh[36] - klo;
   unsigned prefix = 0u, pmask = 0u;
   int remaining = K;
-  const int top_shift = total <= p.max_cand ? -8 : (range == 0u ? -8 : ((31 - __clz((int)range)) / 8) * 8);
-  for (int shift = top_shift; shift >= 0; shift -= 8) {
-    if (tid < 256) hist[tid] = 0u;
+  const int nbits = range == 0u ? 0 : 32 - __clz((int)range);
+  int shift = (total <= p.max_cand || nbits == 0) ? -1 : max(0, nbits - kRadixBits);
+  while (shift >= 0) {
+#pragma unroll
+    for (int u = 0; u < kRadixBins / kNmsThreads; ++u) hist[u * kNmsThreads + tid] = 0u;
     __syncthreads();
-    // scores cluster: most live keys of a wave share a bin; a wave accumulates same-bin ballots
-    // in a (wave-uniform) running count and issues one LDS atomic per bin change, not one per
-    // iteration on the same hot address
+    // scores cluster: most live keys of a wave often share a bin; a wave accumulates same-bin
+    // ballots in a (wave-uniform) running count and issues one LDS atomic per bin change
     unsigned run_bin = 0u, run_cnt = 0u;
     for (int i0 = 0; i0 < A; i0 += kNmsThreads) {   // wave-uniform trip count (ballots below)
       const int i = i0 + tid;
       const unsigned k = i < A ? keys[i] : 0u;
       const unsigned d = k - klo;
       const bool live = k != 0u && (d & pmask) == prefix;
-      const unsigned bin = (d >> shift) & 255u;
+      const unsigned bin = (d >> shift) & (kRadixBins - 1u);
       const unsigned long long lm = __ballot(live);
       if (lm) {
         const int leader = __ffsll((long long)lm) - 1;
@@ -298,37 +304,34 @@ __global__ __launch_bounds__(kNmsThreads) void nms_select_kernel(NmsParams p, Nm
     }
     if (lane == 0 && run_cnt) atomicAdd(&hist[run_bin], run_cnt);
     __syncthreads();
-    if (wave == 0) {
-      const int s_l = hist[4 * lane] + hist[4 * lane + 1] + hist[4 * lane + 2] + hist[4 * lane + 3];
-      int suf = s_l;
+    // thread t owns bins 4095-4t .. 4092-4t (descending): an exclusive scan of the per-thread
+    // sums gives the count of keys in higher bins; the owner of the K-th key picks its bin
+    const int top = kRadixBins - 1 - 4 * tid;
+    const int h0 = hist[top], h1 = hist[top - 1], h2 = hist[top - 2], h3 = hist[top - 3];
+    const int above = block_exclusive_scan(h0 + h1 + h2 + h3, sh);
+    if (above < remaining && above + h0 + h1 + h2 + h3 >= remaining) {
+      const int hs[4] = {h0, h1, h2, h3};
+      int acc = above;
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_down(suf, o, 64);
-        if (lane + o < 64) suf += t;
-      }
-      const int above = suf - s_l;
-      if (above < remaining && suf >= remaining) {
-        int acc = above;
-        for (int j = 3; j >= 0; --j) {
-          const int h = hist[4 * lane + j];
-          acc += h;
-          if (acc >= remaining) {
-            sh[34] = 4 * lane + j;
-            sh[35] = remaining - (acc - h);
-            break;
-          }
+      for (int j = 0; j < 4; ++j) {
+        if (acc + hs[j] >= remaining) {
+          sh[34] = top - j;
+          sh[35] = remaining - acc;
+          break;
         }
+        acc += hs[j];
       }
     }
     __syncthreads();
     prefix |= (unsigned)sh[34] << shift;
-    pmask |= 255u << shift;
+    pmask |= (kRadixBins - 1u) << shift;
     remaining = sh[35];
     __syncthreads();
+    shift = shift == 0 ? -1 : max(0, shift - kRadixBits);
   }
   // all live keys are candidates: threshold below every live key, none "equal"
   const bool take_all = total <= p.max_cand;
-  const unsigned T = take_all ? 0u : (top_shift < 0 ? klo : klo + prefix);
+  const unsigned T = take_all ? 0u : klo + prefix;
   if (take_all) remaining = 0;
   const int n_gt = K - remaining;
   if (p.stop == 2) return;
@@ -407,26 +410,30 @@ __global__ __launch_bounds__(kNmsThreads) void nms_select_kernel(NmsParams p, Nm
 }
 
 // IoU > thr bits of row box bi against the 64 column boxes in LDS (bit jj = column jj), one
-// fully unrolled pass: constant bit positions, broadcast LDS reads batched (FULL: all 64 columns
-// valid, no per-column guard).  A 4-compare overlap test on both axes (a superset of inter > 0)
+// fully unrolled pass: constant bit positions, broadcast LDS reads (FULL: all 64 columns valid,
+// no per-column guard; NEG: negative threshold, every pair tested).  Measured alternatives, all
+// slower on the bench inputs (most candidate pairs overlap, so the exact IoU math is the work):
+// LDS reads issued 8 at a time 32.9 us, a division-free fma test with an exact 1-ulp fallback
+// 35 us, a branch-free overlap pass + scalar loop over overlapping columns 50 us, 4 items per
+// workgroup 33 us, partial unroll 33-38 us — against 30.7 us for this form.  A 4-compare overlap test on both axes (a superset of inter > 0)
 // gates the exact intersection + IEEE division, so the decisions are box_iou() > thr bit for
 // bit; most pairs (other classes sit max_wh apart) stop at the 4 compares.  The test is symmetric
 // bit for bit (fminf / fmaxf and the area sum commute), so the diagonal word's transposed half
 // comes out of the same pass.
-template <bool FULL>
+template <bool FULL, bool NEG>
 __device__ __forceinline__ unsigned long long mask_word(const float4* col, float4 bi, float area_i,
                                                         int je, float thr) {
   unsigned long long hit = 0ull;
 #pragma unroll
   for (int jj = 0; jj < 64; ++jj) {
     if (FULL || jj < je) {                                  // wave-uniform
-      const float4 bj = col[jj];
-      if (thr < 0.f || (bi.z > bj.x && bj.z > bi.x && bi.w > bj.y && bj.w > bi.y)) {
-        const float iw = fmaxf(0.f, fminf(bi.z, bj.z) - fmaxf(bi.x, bj.x));
-        const float ih = fmaxf(0.f, fminf(bi.w, bj.w) - fmaxf(bi.y, bj.y));
+      const float4 c = col[jj];
+      if (NEG || (bi.z > c.x && c.z > bi.x && bi.w > c.y && c.w > bi.y)) {
+        const float iw = fmaxf(0.f, fminf(bi.z, c.z) - fmaxf(bi.x, c.x));
+        const float ih = fmaxf(0.f, fminf(bi.w, c.w) - fmaxf(bi.y, c.y));
         const float inter = iw * ih;
-        if (inter > 0.f || thr < 0.f) {
-          const float iou = inter / (area_i + (bj.z - bj.x) * (bj.w - bj.y) - inter);
+        if (NEG || inter > 0.f) {
+          const float iou = inter / (area_i + (c.z - c.x) * (c.w - c.y) - inter);
           if (iou > thr) hit |= 1ull << jj;
         }
       }
@@ -440,10 +447,14 @@ __device__ __forceinline__ unsigned long long mask_word(const float4* col, float
 //    LDS and are read as broadcasts.  The diagonal word also yields its transposed half (bits
 //    k < i: the suppressors of row i inside the word) for the greedy kernel's fixed point.
 constexpr int kMaskPairs = kMaskWords * (kMaskWords + 1) / 2;   // 136 (rb, w) with w >= rb
-__global__ __launch_bounds__(64) void nms_mask_kernel(NmsParams p, NmsWork ws) {
-  __shared__ float4 col[64];
-  const int b = blockIdx.x / kMaskPairs;
-  int q = blockIdx.x - b * kMaskPairs, rb = 0;
+constexpr int kMaskWaves = 1;   // work items (waves) per workgroup
+static_assert(kMaskPairs % kMaskWaves == 0, "items of an image fill whole workgroups");
+__global__ __launch_bounds__(64 * kMaskWaves) void nms_mask_kernel(NmsParams p, NmsWork ws) {
+  __shared__ float4 cols[kMaskWaves][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int item = blockIdx.x * kMaskWaves + wave;
+  const int b = item / kMaskPairs;
+  int q = item - b * kMaskPairs, rb = 0;
   while (q >= kMaskWords - rb) {                 // (rb, w) from the triangle index
     q -= kMaskWords - rb;
     ++rb;
@@ -451,19 +462,22 @@ __global__ __launch_bounds__(64) void nms_mask_kernel(NmsParams p, NmsWork ws) {
   const int w = rb + q;
   const int n = ws.n[b];
   const int r0 = rb * 64, j0 = w * 64;
-  if (r0 >= n || j0 >= n) return;
-  const int lane = threadIdx.x;
+  const bool work = r0 < n && j0 < n;            // wave-uniform; no return before the barrier
+  float4* col = cols[wave];
   const float4* cb = ws.cbox + (long)b * kMaxCand;
-  if (j0 + lane < n) col[lane] = cb[j0 + lane];
+  if (work && j0 + lane < n) col[lane] = cb[j0 + lane];
   const int i = r0 + lane;
-  const float4 bi = i < n ? cb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 bi = work && i < n ? cb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
-  if (i >= n) return;
+  if (!work || i >= n) return;
   const float area_i = (bi.z - bi.x) * (bi.w - bi.y);
   const int je = min(64, n - j0);
   const bool diag = w == rb;
-  const unsigned long long hit = je == 64 ? mask_word<true>(col, bi, area_i, je, p.iou)
-                                          : mask_word<false>(col, bi, area_i, je, p.iou);
+  // (a negative threshold keeps every pair, disjoint ones included: the generic instantiation)
+  const unsigned long long hit =
+      p.iou < 0.f ? mask_word<false, true>(col, bi, area_i, je, p.iou)
+                  : (je == 64 ? mask_word<true, false>(col, bi, area_i, je, p.iou)
+                              : mask_word<false, false>(col, bi, area_i, je, p.iou));
   unsigned long long bits = hit;
   if (diag) {
     bits = lane == 63 ? 0ull : hit & (~0ull << (lane + 1));
@@ -515,6 +529,7 @@ __global__ __launch_bounds__(kGreedyThreads) void nms_greedy_kernel(NmsParams p,
   }
   if (tid == 0) nk_sh = 0;
   __syncthreads();
+  if (p.stop == 5) return;
   if (tid < 64) {
     unsigned long long removed = 0ull;
     int nkept = 0;
@@ -578,6 +593,7 @@ __global__ __launch_bounds__(kGreedyThreads) void nms_greedy_kernel(NmsParams p,
     if (lane == 0) nk_sh = nkept;
   }
   __syncthreads();
+  if (p.stop == 6) return;
   const int nk = nk_sh;
   const float4* bx = p.boxes + (long)b * p.A;
   const int* cl = p.cls + (long)b * p.A;
@@ -679,8 +695,8 @@ extern "C" int aiko_topk_nms(const void* boxes, const float* scores, const int* 
   w += ((size_t)B * 4 + 255) / 256 * 256;
   ws.low = reinterpret_cast<unsigned long long*>(w);
   aiko::nms_select_kernel<<<B, aiko::kNmsThreads, 0, stream>>>(p, ws);
-  if (p.stop < 99) return 0;
-  aiko::nms_mask_kernel<<<B * aiko::kMaskPairs, 64, 0, stream>>>(p, ws);
+  if (p.stop < 5) return 0;
+  aiko::nms_mask_kernel<<<B * aiko::kMaskPairs / aiko::kMaskWaves, 64 * aiko::kMaskWaves, 0, stream>>>(p, ws);
   aiko::nms_greedy_kernel<<<B, aiko::kGreedyThreads, 0, stream>>>(p, ws);
   return (int)hipGetLastError();
 }
