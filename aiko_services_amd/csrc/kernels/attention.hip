@@ -16,6 +16,10 @@
 //     accumulator registers (no LDS round trip): element j of lane group g of k-step s is key
 //     32s + 16(j>>2) + 4g + (j&3), and the V^T fragment is two transposed reads of rows
 //     32s + 4g .. +3 and 32s + 16 + 4g .. +3 — that same key order.
+// Measured and dropped (round 2): software-pipelining S^T of tile it+1 under the softmax of
+// tile it (FA3-style, one extra S block = +32 VGPRs): 201-224 VGPRs -> 2 waves / SIMD, 216-240
+// us against 186 us for this kernel at 124 VGPRs / 4 waves; forcing 3 waves spills.  Occupancy
+// (other waves' MFMAs under this wave's softmax) beats intra-wave overlap here.
 // Q stays in registers for the whole key loop.  Sequences are rows b*Tpad .. b*Tpad+T-1 of
 // q/k/v (any row pitch: q, k, v may be column slices of one fused QKV buffer).
 #include <cstdlib>
