@@ -1,9 +1,11 @@
 """Video elements (reference ``elements/media/video_io.py:96-308``, ``webcam_io.py:61-144``).
 
 OpenCV is optional (absent on the MI355X boxes).  Without it, video files are read/written
-with in-repo codecs for formats that need no external library: raw ``.y4m`` (YUV4MPEG2,
-4:2:0 / 4:4:4, converted to RGB with BT.601), ``.npy`` arrays ``[T, H, W, 3]`` uint8, and
-directories of images.  With OpenCV present any container it supports works too.
+with in-repo codecs: ``.avi`` (RIFF container, Motion-JPEG through Pillow or uncompressed DIB
+frames — ``avi.py``; what cameras and ``cv2.VideoWriter('MJPG')`` produce), animated ``.gif``
+(Pillow), raw ``.y4m`` (YUV4MPEG2, 4:2:0 / 4:4:4, converted to RGB with BT.601), ``.npy``
+arrays ``[T, H, W, 3]`` uint8, and directories of images.  With OpenCV present any other
+container it supports works too.
 ``VideoShow`` needs a display: without one it logs frame statistics instead.
 """
 from __future__ import annotations
@@ -14,6 +16,7 @@ import numpy as np
 
 from ...pipeline.engine import PipelineElement
 from ...pipeline.stream import StreamEvent
+from .avi import AviWriter, iter_avi
 from .common_io import DataSource, DataTarget, contains_all
 
 try:  # optional
@@ -114,7 +117,14 @@ def iter_video_frames(path):
                 yield np.asarray(Image.open(p).convert("RGB"))
         return
     suffix = path.suffix.lower()
-    if suffix == ".y4m":
+    if suffix == ".avi" and not _CV2:
+        yield from iter_avi(path)
+    elif suffix == ".gif":
+        from PIL import Image, ImageSequence
+        with Image.open(path) as im:
+            for fr in ImageSequence.Iterator(im):
+                yield np.asarray(fr.convert("RGB"))
+    elif suffix == ".y4m":
         yield from iter_y4m(path)
     elif suffix in (".npy", ".npz"):
         arr = np.load(path, allow_pickle=False)
@@ -134,7 +144,8 @@ def iter_video_frames(path):
         finally:
             cap.release()
     else:
-        raise ValueError(f"{path}: unsupported video format without OpenCV (use .y4m, .npy or a frame directory)")
+        raise ValueError(f"{path}: unsupported video format without OpenCV "
+                         f"(use .avi, .gif, .y4m, .npy or a frame directory)")
 
 
 # ---- elements -------------------------------------------------------------------------------
@@ -229,7 +240,8 @@ class VideoShow(PipelineElement):
 
 
 class VideoWriteFile(DataTarget):
-    """Writes ``.y4m`` (default) or ``.npy``; other suffixes need OpenCV."""
+    """Writes ``.avi`` (parameters ``codec``: ``MJPG`` (default) | ``raw``, ``quality``),
+    ``.gif``, ``.y4m`` or ``.npy``; other suffixes need OpenCV.  ``rate``: frames per second."""
 
     def __init__(self, context):
         context.set_protocol("video_write_file:0")
@@ -251,7 +263,7 @@ class VideoWriteFile(DataTarget):
         suffix = Path(path).suffix.lower()
         for image in images:
             arr = np.asarray(image).astype(np.uint8)
-            if suffix == ".npy":
+            if suffix in (".npy", ".gif"):
                 stream.variables["video_frames"].append(arr)
                 continue
             writer = stream.variables["video_writer"]
@@ -259,13 +271,17 @@ class VideoWriteFile(DataTarget):
                 rate, _ = self.get_parameter("rate", 30)
                 if suffix == ".y4m":
                     writer = Y4MWriter(path, arr.shape[1], arr.shape[0], float(rate))
+                elif suffix == ".avi" and not _CV2:
+                    codec, _ = self.get_parameter("codec", "MJPG")
+                    quality, _ = self.get_parameter("quality", 90)
+                    writer = AviWriter(path, arr.shape[1], arr.shape[0], float(rate), str(codec), int(quality))
                 elif _CV2:
                     writer = cv2.VideoWriter(path, cv2.VideoWriter_fourcc(*"mp4v"), float(rate),
                                              (arr.shape[1], arr.shape[0]))
                 else:
                     return StreamEvent.ERROR, {"diagnostic": f"{path}: unsupported format without OpenCV"}
                 stream.variables["video_writer"] = writer
-            if isinstance(writer, Y4MWriter):
+            if isinstance(writer, (Y4MWriter, AviWriter)):
                 writer.write(arr)
             else:
                 writer.write(cv2.cvtColor(arr, cv2.COLOR_RGB2BGR))
@@ -274,11 +290,17 @@ class VideoWriteFile(DataTarget):
     def stop_stream(self, stream, stream_id):
         path = stream.variables.get("video_path")
         frames = stream.variables.get("video_frames")
-        if path and frames and Path(path).suffix.lower() == ".npy":
+        suffix = Path(path).suffix.lower() if path else ""
+        if path and frames and suffix == ".npy":
             np.save(path, np.stack(frames))
+        elif path and frames and suffix == ".gif":
+            from PIL import Image
+            rate, _ = self.get_parameter("rate", 30)
+            ims = [Image.fromarray(f if f.ndim == 3 else np.repeat(f[..., None], 3, 2)) for f in frames]
+            ims[0].save(path, save_all=True, append_images=ims[1:], duration=int(round(1000 / float(rate))), loop=0)
         writer = stream.variables.get("video_writer")
         if writer is not None:
-            (writer.close if isinstance(writer, Y4MWriter) else writer.release)()
+            (writer.close if isinstance(writer, (Y4MWriter, AviWriter)) else writer.release)()
         return StreamEvent.OKAY, {}
 
 

@@ -202,6 +202,37 @@ def test_text_files_data_source_target(aiko_process, tmp_path):
     assert "f1" not in pipeline.stream_leases
 
 
+def test_video_files_avi_read_write(aiko_process, tmp_path):
+    """VideoReadFile -> VideoWriteFile through the in-repo AVI codec (no OpenCV): a raw-DIB
+    AVI is read frame by frame and written back bit-exact as a raw AVI."""
+    import numpy as np
+    from aiko_services_amd.elements.media import avi as A
+    M = "aiko_services_amd.elements.media.video_io"
+    rng = np.random.default_rng(5)
+    frames = [rng.integers(0, 256, (18, 26, 3), dtype=np.uint8) for _ in range(4)]
+    src = tmp_path / "in.avi"
+    A.write_avi(src, frames, fps=10, codec="raw")
+    out = tmp_path / "out.avi"
+    d = {
+        "version": 0, "name": "p_video_files", "runtime": "python",
+        "graph": ["(VideoReadFile VideoWriteFile)"],
+        "elements": [
+            {"name": "VideoReadFile", "parameters": {"data_sources": f"(file://{src})"},
+             "input": [{"name": "images", "type": "[image]"}], "output": [{"name": "images", "type": "[image]"}],
+             "deploy": {"local": {"module": M}}},
+            {"name": "VideoWriteFile", "parameters": {"data_targets": f"file://{out}", "codec": "raw", "rate": 10},
+             "input": [{"name": "images", "type": "[image]"}], "output": [],
+             "deploy": {"local": {"module": M}}}],
+    }
+    pipeline, q = _create(d, stream_id="v1")
+    assert len([q.get(timeout=10) for _ in range(4)]) == 4
+    deadline = time.time() + 5                      # STOP at end of file -> stop_stream closes the writer
+    while "v1" in pipeline.stream_leases and time.time() < deadline:
+        time.sleep(0.05)
+    back = A.read_avi(out)
+    assert back.shape == (4, 18, 26, 3) and all(np.array_equal(a, b) for a, b in zip(frames, back))
+
+
 def test_get_parameter_precedence(aiko_process):
     from aiko_services_amd.pipeline.engine import PipelineElementImpl
     pipeline, q = _create(DIAMOND, stream_id="pp", parameters={"PE_1.pe_1_inc": 7, "p_3": "stream"})
