@@ -537,3 +537,36 @@ def test_aruco_example_fallback_detector(aiko_process):
     assert ids == sorted([canon(0b1000_0110_0010_1101), canon(0b0001_0000_0111_0011)])
     assert len(ov["corners"]) == 2 and ov["corners"][0].shape == (1, 4, 2)
     assert (out["images"][0] != img).any()
+
+
+def test_aruco_original_dictionary_ids(aiko_process):
+    """aruco_tags DICT_ARUCO_ORIGINAL: the fallback decodes the original-ArUco ids (2 bits per
+    codeword row) in every rotation, with the marker's own top-left corner first; a grid whose
+    rows are not codewords is rejected."""
+    import numpy as np
+    from aiko_services_amd.examples.aruco_marker.aruco import decode_original, make_marker_original, original_bits
+    assert all(decode_original(original_bits(i)) == i for i in range(1024))
+    bad = original_bits(5).copy()
+    bad[2, 0] ^= 1                                          # row 2 no longer a codeword
+    assert decode_original(bad) is None
+    img = np.full((160, 240, 3), 255, np.uint8)
+    placed = {}
+    for n, (mid, k, y, x) in enumerate([(213, 0, 8, 8), (517, 1, 8, 120), (42, 2, 90, 8), (999, 3, 90, 120)]):
+        m = np.rot90(make_marker_original(mid, 6), k)       # k quarter turns counter-clockwise
+        img[y:y + m.shape[0], x:x + m.shape[1]] = m[..., None]
+        side = m.shape[0] - 12                              # marker without its quiet zone
+        tl = [(x + 6, y + 6), (x + 6, y + 6 + side), (x + 6 + side, y + 6 + side), (x + 6 + side, y + 6)][k]
+        placed[mid] = tl
+    M = "aiko_services_amd.examples.aruco_marker.aruco"
+    d = {"version": 0, "name": "p_aruco_orig", "runtime": "python", "graph": ["(ArucoMarkerDetector)"],
+         "elements": [{"name": "ArucoMarkerDetector", "parameters": {"aruco_tags": "DICT_ARUCO_ORIGINAL"},
+                       "input": [{"name": "images", "type": "[image]"}],
+                       "output": [{"name": "overlays", "type": "[overlay]"}], "deploy": {"local": {"module": M}}}]}
+    p, q = _create(d, name="p_aruco_orig", stream_id="52")
+    p.create_frame({"stream_id": "52", "frame_id": 0}, {"images": [img]})
+    info, out = q.get(timeout=5)
+    ov = out["overlays"][0]
+    got = {int(i): tuple(c.reshape(4, 2)[0]) for i, c in zip(ov["ids"].reshape(-1), ov["corners"])}
+    assert sorted(got) == sorted(placed)
+    for mid, tl in placed.items():
+        assert got[mid] == tl, (mid, got[mid], tl)
