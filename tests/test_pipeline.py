@@ -459,6 +459,74 @@ def test_speech_example_elements(aiko_process, tmp_path):
         server.shutdown()
 
 
+def test_llm_example_backends(aiko_process):
+    """examples/llm PE_LLM: Ollama /api/chat (default llm_type) and OpenAI chat-completions
+    against a local stub; the system prompt carries the robot vocabulary and the objects
+    published on {namespace}/detections within the last second; <silence> passes through; a
+    dead server ends the frame with an error; PE_COQUI_TTS passes text through."""
+    import http.server
+    import threading
+    from aiko_services_amd.examples.llm import elements_llm as L
+    seen = []
+
+    class Stub(http.server.BaseHTTPRequestHandler):
+        def do_POST(self):
+            body = json.loads(self.rfile.read(int(self.headers["Content-Length"])))
+            seen.append((self.path, body))
+            text = "(action " + body["messages"][1]["content"].split()[-1] + ")"
+            reply = ({"message": {"role": "assistant", "content": text}} if self.path == "/api/chat"
+                     else {"choices": [{"message": {"content": text}}]})
+            data = json.dumps(reply).encode()
+            self.send_response(200)
+            self.send_header("Content-Type", "application/json")
+            self.send_header("Content-Length", str(len(data)))
+            self.end_headers()
+            self.wfile.write(data)
+
+        def log_message(self, *a):
+            pass
+    server = http.server.HTTPServer(("127.0.0.1", 0), Stub)
+    threading.Thread(target=server.serve_forever, daemon=True).start()
+    M = "aiko_services_amd.examples.llm.elements_llm"
+
+    def el(name, params=None):
+        return {"name": name, "input": [{"name": "text", "type": "str"}], "output": [{"name": "text", "type": "str"}],
+                "parameters": params or {}, "deploy": {"local": {"module": M}}}
+    try:
+        base = f"http://127.0.0.1:{server.server_port}"
+        d = {"version": 0, "name": "p_llm_ollama", "runtime": "python", "graph": ["(PE_LLM PE_COQUI_TTS)"],
+             "elements": [el("PE_LLM", {"url": base}), el("PE_COQUI_TTS")]}
+        p, q = _create(d, name="p_llm_ollama", stream_id="61")
+        aiko_process.aiko.message.publish(L.topic_detections(), "(detections person ball)")
+        time.sleep(0.2)
+        p.create_frame({"stream_id": "61", "frame_id": 0}, {"text": "please sit"})
+        info, data = q.get(timeout=10)
+        assert info["state"] == 0 and data["text"] == "(action sit)"
+        path, body = seen[-1]
+        assert path == "/api/chat" and body["stream"] is False and body["model"] == L.LLM_MODEL_NAME
+        assert body["options"]["temperature"] == 0.0
+        assert "(action wag)" in body["messages"][0]["content"] and "person ball" in body["messages"][0]["content"]
+        n = len(seen)
+        p.create_frame({"stream_id": "61", "frame_id": 1}, {"text": "<silence>"})
+        info, data = q.get(timeout=10)
+        assert data["text"] == "<silence>" and len(seen) == n
+        d = {"version": 0, "name": "p_llm_openai", "runtime": "python", "graph": ["(PE_LLM)"],
+             "elements": [el("PE_LLM", {"llm_type": "openai", "url": base + "/v1", "model": "m"})]}
+        p, q = _create(d, name="p_llm_openai", stream_id="62")
+        p.create_frame({"stream_id": "62", "frame_id": 0}, {"text": "turn left"})
+        info, data = q.get(timeout=10)
+        assert data["text"] == "(action left)" and seen[-1][0] == "/v1/chat/completions"
+    finally:
+        server.shutdown()
+        server.server_close()
+    d = {"version": 0, "name": "p_llm_down", "runtime": "python", "graph": ["(PE_LLM)"],
+         "elements": [el("PE_LLM", {"url": base, "timeout": 2})]}
+    p, q = _create(d, name="p_llm_down", stream_id="63")
+    p.create_frame({"stream_id": "63", "frame_id": 0}, {"text": "sit"})
+    info, data = q.get(timeout=10)
+    assert info["state"] != 0
+
+
 def test_audio_spectrum_and_remote_elements(aiko_process):
     """Reference dead audio elements: FFT -> filter -> bands -> XY graph; array frames sent by
     PE_RemoteSend0 over a binary topic arrive as new frames of PE_RemoteReceive0's pipeline."""
