@@ -71,4 +71,45 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
+// erf for every GELU epilogue (fp8 GEMMs, convs, decoder linears — one definition so fused and
+// unfused paths agree): Abramowitz & Stegun 7.1.26, erf(|x|) = 1 - poly(t) e^{-x^2}, t = 1 / (1 +
+// p |x|) — max abs error 1.5e-7, far below the bf16 / e4m3 outputs' resolution.  One v_rcp +
+// 5 FMAs + one v_exp instead of OCML erff: the exact erff made the epilogue of the Whisper fc1
+// GEMM (73.8M GELUs) cost 81 us on top of the 98 us GEMM (scripts/op_bench.py gemm_fc1 /
+// fc1_gelu).
+// Every step is an explicit fmaf / mul so the scalar and the packed (two-lane) forms below
+// round identically whatever the compiler contracts elsewhere.
+__device__ __forceinline__ float gelu_erf(float x) {
+  const float z = x * 0.70710678118654752f;
+  const float az = fabsf(z);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, az, 1.f));
+  float poly = fmaf(1.061405429f, t, -1.453152027f);
+  poly = fmaf(poly, t, 1.421413741f);
+  poly = fmaf(poly, t, -0.284496736f);
+  poly = fmaf(poly, t, 0.254829592f);
+  const float e = __expf(-(az * az));
+  const float erf = copysignf(fmaf(-(poly * t), e, 1.f), z);
+  const float h = 0.5f * x;
+  return fmaf(h, erf, h);
+}
+
+// two GELUs per packed-fp32 VALU op (v_pk_fma_f32 / v_pk_mul_f32) for the polynomial and
+// scaling; only v_rcp / v_exp are per lane.  Bit-identical to gelu_erf (same op sequence).
+__device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
+  const f32x2 z = x * f32x2{0.70710678118654752f, 0.70710678118654752f};
+  const f32x2 az = {fabsf(z[0]), fabsf(z[1])};
+  const f32x2 d = __builtin_elementwise_fma(f32x2{0.3275911f, 0.3275911f}, az, f32x2{1.f, 1.f});
+  const f32x2 t = {__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+  f32x2 poly = __builtin_elementwise_fma(f32x2{1.061405429f, 1.061405429f}, t, f32x2{-1.453152027f, -1.453152027f});
+  poly = __builtin_elementwise_fma(poly, t, f32x2{1.421413741f, 1.421413741f});
+  poly = __builtin_elementwise_fma(poly, t, f32x2{-0.284496736f, -0.284496736f});
+  poly = __builtin_elementwise_fma(poly, t, f32x2{0.254829592f, 0.254829592f});
+  const f32x2 sq = az * az;
+  const f32x2 e = {__expf(-sq[0]), __expf(-sq[1])};
+  const f32x2 y = __builtin_elementwise_fma(-(poly * t), e, f32x2{1.f, 1.f});
+  const f32x2 erf = {copysignf(y[0], z[0]), copysignf(y[1], z[1])};
+  const f32x2 h = f32x2{0.5f, 0.5f} * x;
+  return __builtin_elementwise_fma(h, erf, h);
+}
+
 }  // namespace aiko

@@ -369,7 +369,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, (buf_wgs_per_cu<BM, BN, WGM * WGN, 
       for (int e = 0; e < 8; ++e) v[e] = v[e] / (1.f + __expf(-v[e]));
     } else if (act == 3) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
+      for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
     }
     if (p.res && post) {
 #pragma unroll

@@ -56,9 +56,7 @@ __device__ __forceinline__ int mx_exponent(float amax) {
   return e < -126 ? -126 : (e > 127 ? 127 : e);
 }
 
-__device__ __forceinline__ float gelu_erf(float x) {
-  return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
-}
+
 
 // Epilogue for a WGM x WGN grid of waves, each owning (BM / WGM) x (BN / WGN) of the tile: the
 // fp32 accumulators go through padded LDS so that every thread then owns whole 8-column chunks
@@ -133,7 +131,11 @@ __device__ __forceinline__ void fp8_epilogue(const Fp8GemmParams& p,
       for (int e = 0; e < 8; ++e) v[e] = v[e] / (1.f + __expf(-v[e]));
     } else if (p.act == 3) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+      for (int e = 0; e < 4; ++e) {
+        const f32x2 g = gelu_erf2(f32x2{v[2 * e], v[2 * e + 1]});
+        v[2 * e] = g[0];
+        v[2 * e + 1] = g[1];
+      }
     }
     if constexpr (MXO) {
       // MX block b = columns 32b .. 32b+31 of this 128-column tile row = chunks 4b .. 4b+3,

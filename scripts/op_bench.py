@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Run one op repeatedly at Whisper-small encoder shapes (for rocprofv3 --pmc / timing).
 
-    python scripts/op_bench.py attn|gemm_qkv|gemm_fc2 [--batch 16] [--iters 20]
+    python scripts/op_bench.py attn|gemm_qkv|gemm_fc1|gemm_fc2|gemm_out|fc1_gelu_mx [--batch 16] [--iters 20]
+fc1_gelu_mx is the encoder's fc1 as run: GELU + MX-fp8 output quantisation in the epilogue.
 """
 import argparse
 import os
@@ -30,14 +31,22 @@ def main():
         fn = lambda: TR.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], out, B, H, T, Tp, 0.125)  # noqa: E731
         flops = 4 * B * H * T * T * 64
     else:
-        K, N = {"gemm_qkv": (d, 3 * d), "gemm_fc1": (d, 4 * d), "gemm_fc2": (4 * d, d), "gemm_out": (d, d)}[a.op]
+        K, N = {"gemm_qkv": (d, 3 * d), "gemm_fc1": (d, 4 * d), "gemm_fc2": (4 * d, d), "gemm_out": (d, d),
+                "fc1_gelu_mx": (d, 4 * d), "fc1_gelu": (d, 4 * d), "fc1_mx": (d, 4 * d)}[a.op]
         x = torch.randn(M, K, device=dev)
         xq, xs = TR.quantize_rows_ref(x.cpu())
         xq, xs = xq.to(dev), xs.to(dev)
         lin = TR.make_fp8_linear(torch.randn(N, K) / K ** 0.5, torch.zeros(N), dev)
         out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
         tile = tuple(int(v) for v in a.tile.split(",")) if a.tile else None
-        fn = lambda: TR.linear_fp8(xq, xs, lin, out=out, tile=tile)  # noqa: E731
+        if a.op in ("fc1_gelu_mx", "fc1_mx"):
+            u8, usc = TR.mx_buffers(M, N, dev)
+            act = TR.ACT_GELU if a.op == "fc1_gelu_mx" else TR.ACT_NONE
+            fn = lambda: TR.linear_fp8(xq, xs, lin, act=act, out_mx=(u8, usc), tile=tile)  # noqa: E731
+        elif a.op == "fc1_gelu":
+            fn = lambda: TR.linear_fp8(xq, xs, lin, act=TR.ACT_GELU, out=out, tile=tile)  # noqa: E731
+        else:
+            fn = lambda: TR.linear_fp8(xq, xs, lin, out=out, tile=tile)  # noqa: E731
         flops = 2 * M * N * K
     for _ in range(3):
         fn()
