@@ -69,6 +69,7 @@ int aiko_topk_nms(const void* boxes, const float* scores, const int* cls, int B,
                   void* workspace, hipStream_t stream);
 int aiko_avgpool(const void* x, void* y, int B, int HW, int C, hipStream_t stream);
 int aiko_mean_rows_f32(const void* x, float* y, int B, int T, int C, hipStream_t stream);
+int aiko_window_shift(const float* src, const float* chunk, float* dst, int B, int W, int n, hipStream_t stream);
 int aiko_stem_pool(const void* x, const void* w, const float* bias, void* y, int B, int Hp, int Wp,
                    int Ho, int Wo, int Hm, int Wm, int ldy, int variant, hipStream_t stream);
 int aiko_softmax_topk(const void* logits, float* prob, int* index, int B, int N, int k,
@@ -493,6 +494,21 @@ void mean_rows_out(const at::Tensor& x, at::Tensor& y) {
   check_launch(aiko_mean_rows_f32(x.data_ptr(), y.data_ptr<float>(), B, T, C, cur_stream()), "mean_rows");
 }
 
+void window_shift_out(const at::Tensor& src, const at::Tensor& chunk, at::Tensor& dst) {
+  check_cuda(src, "src");
+  check_cuda(chunk, "chunk");
+  check_cuda(dst, "dst");
+  TORCH_CHECK(src.scalar_type() == at::kFloat && chunk.scalar_type() == at::kFloat && dst.scalar_type() == at::kFloat &&
+                  src.dim() == 2 && chunk.dim() == 2 && src.sizes() == dst.sizes() && src.is_contiguous() &&
+                  chunk.is_contiguous() && dst.is_contiguous() && chunk.size(0) == src.size(0),
+              "aiko.window_shift_out: fp32 contiguous src / dst [B, W], chunk [B, n]");
+  TORCH_CHECK(src.data_ptr() != dst.data_ptr(), "aiko.window_shift_out: dst must not alias src");
+  const int64_t B = src.size(0), W = src.size(1), n = chunk.size(1);
+  TORCH_CHECK(n <= W && W % 4 == 0 && n % 4 == 0, "aiko.window_shift_out: n <= W, both multiples of 4");
+  check_launch(aiko_window_shift(src.data_ptr<float>(), chunk.data_ptr<float>(), dst.data_ptr<float>(), B, W, n,
+                                 cur_stream()), "window_shift");
+}
+
 void avgpool_out(const at::Tensor& x, at::Tensor& y) {
   check_cuda(x, "x");
   check_cuda(y, "y");
@@ -876,6 +892,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("maxpool_out(Tensor x, Tensor(a!) y, int k, int s, int p) -> ()");
   m.def("avgpool_out(Tensor x, Tensor(a!) y) -> ()");
   m.def("mean_rows_out(Tensor x, Tensor(a!) y) -> ()");
+  m.def("window_shift_out(Tensor src, Tensor chunk, Tensor(a!) dst) -> ()");
   m.def("stem_pool_out(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, int Ho, int Wo, int variant=0) -> ()");
   m.def("gemm_fp8_out(Tensor a, Tensor? sa, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!)? y, int act, int bm, int bn, int variant=0, Tensor? zero=None, Tensor? amx=None, Tensor(b!)? yq=None, Tensor(c!)? ysc=None) -> ()");
   m.def("rownorm_quant_out(Tensor x, Tensor? gamma, Tensor? beta, float eps, Tensor(a!)? yb, Tensor(b!)? q, Tensor(c!)? qs) -> ()");
@@ -901,6 +918,7 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("topk_nms_out", &topk_nms_out);
   m.impl("avgpool_out", &avgpool_out);
   m.impl("mean_rows_out", &mean_rows_out);
+  m.impl("window_shift_out", &window_shift_out);
   m.impl("stem_pool_out", &stem_pool_out);
   m.impl("softmax_topk_out", &softmax_topk_out);
   m.impl("gemm_fp8_out", &gemm_fp8_out);

@@ -313,6 +313,24 @@ __global__ void logmel_finalize_kernel(const float* __restrict__ logmel, const i
   }
 }
 
+
+// Sliding audio window update, one pass: dst[b] = src[b][n:W] ++ chunk[b][0:n] (fp32, float4
+// lanes; W, n multiples of 4).  Replaces two strided device copies per step.
+__global__ __launch_bounds__(256) void window_shift_kernel(const float* __restrict__ src,
+                                                           const float* __restrict__ chunk,
+                                                           float* __restrict__ dst, int B, int W,
+                                                           int n) {
+  const int W4 = W >> 2, keep4 = (W - n) >> 2, n4 = n >> 2;
+  const long total = (long)B * W4;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(idx / W4), i = (int)(idx - (long)b * W4);
+    const f32x4 v = i < keep4 ? reinterpret_cast<const f32x4*>(src)[(long)b * W4 + i + n4]
+                              : reinterpret_cast<const f32x4*>(chunk)[(long)b * n4 + (i - keep4)];
+    reinterpret_cast<f32x4*>(dst)[idx] = v;
+  }
+}
+
 }  // namespace aiko
 
 extern "C" int aiko_logmel(const float* audio, int B, int N, const float* mel, int n_mels,
@@ -331,5 +349,15 @@ extern "C" int aiko_logmel(const float* audio, int B, int N, const float* mel, i
   if (g > 4096) g = 4096;
   aiko::logmel_finalize_kernel<<<(int)g, 256, 0, stream>>>(logmel, gmax, static_cast<aiko::bf16_t*>(dst),
                                                           B, F, n_mels, rows, pad, ld);
+  return (int)hipGetLastError();
+}
+
+extern "C" int aiko_window_shift(const float* src, const float* chunk, float* dst, int B, int W, int n,
+                                 hipStream_t stream) {
+  if (B <= 0 || n <= 0 || n > W || (W & 3) || (n & 3)) return -1;
+  const long total = (long)B * (W >> 2);
+  long g = (total + 255) / 256;
+  if (g > 256 * 16) g = 256 * 16;
+  aiko::window_shift_kernel<<<(int)g, 256, 0, stream>>>(src, chunk, dst, B, W, n);
   return (int)hipGetLastError();
 }

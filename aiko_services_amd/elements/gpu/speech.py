@@ -118,8 +118,8 @@ class AudioWindow(GpuPipelineElement):
         if n >= W:
             dst.copy_(audio[:, n - W:])
         else:
-            dst[:, :W - n].copy_(src[:, n:])
-            dst[:, W - n:].copy_(audio)
+            from ...ops.audio import window_shift
+            window_shift(src, audio.contiguous(), dst)     # one aiko:: kernel on the GPU
         if self.device.type == "cuda":
             self._last = torch.cuda.Event()
             self._last.record()

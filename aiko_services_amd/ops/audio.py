@@ -91,3 +91,15 @@ def log_mel_ref(audio: torch.Tensor, filters: torch.Tensor, frames: int | None =
     log_spec = torch.clamp(mel, min=1e-10).log10()
     log_spec = torch.maximum(log_spec, log_spec.amax(dim=(1, 2), keepdim=True) - 8.0)
     return (log_spec + 4.0) / 4.0
+
+
+def window_shift(src: torch.Tensor, chunk: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
+    """``dst[b] = concat(src[b, n:], chunk[b])`` — a sliding audio window advanced by one chunk
+    (fp32 [B, W] / [B, n]); one HIP kernel on the GPU, torch slicing on the CPU."""
+    n = chunk.shape[1]
+    if dst.is_cuda:
+        torch.ops.aiko.window_shift_out(src, chunk, dst)
+    else:
+        dst[:, :dst.shape[1] - n].copy_(src[:, n:])
+        dst[:, dst.shape[1] - n:].copy_(chunk)
+    return dst

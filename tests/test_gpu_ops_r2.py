@@ -13,3 +13,15 @@ def test_mean_rows_f32(native, B, T, C):
     got = mean_rows(x)
     torch.cuda.synchronize()
     assert torch.allclose(got, ref, atol=1e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("B,W,n", [(16, 480000, 80000), (3, 64, 4), (2, 1024, 1024)])
+def test_window_shift(native, B, W, n):
+    """window_shift_kernel: dst = src[:, n:] ++ chunk, exactly (a copy) — the AudioWindow update."""
+    from aiko_services_amd.ops.audio import window_shift
+    g = torch.Generator(device="cuda").manual_seed(B + W)
+    src = torch.randn(B, W, device="cuda", generator=g)
+    chunk = torch.randn(B, n, device="cuda", generator=g)
+    dst = torch.empty_like(src)
+    window_shift(src, chunk, dst)
+    assert torch.equal(dst, torch.cat([src[:, n:], chunk], 1))
