@@ -77,6 +77,13 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // 5 FMAs + one v_exp instead of OCML erff: the exact erff made the epilogue of the Whisper fc1
 // GEMM (73.8M GELUs) cost 81 us on top of the 98 us GEMM (scripts/op_bench.py gemm_fc1 /
 // fc1_gelu).
+// SiLU for every epilogue: x * rcp(1 + e^-x) — v_rcp_f32 (1 ulp) instead of the IEEE division
+// sequence (~10 VALU ops); the fused YOLO stem was VALU-issue bound (PMC: 819 VALU instructions
+// per wave, 16 SiLUs per lane).  Limits as the division: -inf side -> -0, +inf side -> x.
+__device__ __forceinline__ float silu(float x) {
+  return x * __builtin_amdgcn_rcpf(1.f + __expf(-x));
+}
+
 // Every step is an explicit fmaf / mul so the scalar and the packed (two-lane) forms below
 // round identically whatever the compiler contracts elsewhere.
 __device__ __forceinline__ float gelu_erf(float x) {

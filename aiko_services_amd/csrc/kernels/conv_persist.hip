@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256, OCC) void conv_persist_kernel(ConvParams p, in
           for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
         } else if (act == 2) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = v[e] / (1.f + __expf(-v[e]));
+          for (int e = 0; e < 8; ++e) v[e] = silu(v[e]);
         } else if (act == 3) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);

@@ -395,7 +395,7 @@ __global__ __launch_bounds__(256) void dec_linear_kernel(
         if (m >= M) continue;
         float val = acc[e] * sa[r] * cs + cb;
         if (act == 1) val = fmaxf(val, 0.f);
-        else if (act == 2) val = val / (1.f + __expf(-val));
+        else if (act == 2) val = silu(val);
         else if (act == 3) val = gelu_erf(val);
         y[(long)m * ldy + n] = f2bf(val + rv[e]);
       }

@@ -128,7 +128,7 @@ __device__ __forceinline__ void fp8_epilogue(const Fp8GemmParams& p,
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
     } else if (p.act == 2) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = v[e] / (1.f + __expf(-v[e]));
+      for (int e = 0; e < 8; ++e) v[e] = silu(v[e]);
     } else if (p.act == 3) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -672,7 +672,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_big_kernel(Fp8GemmParams p, c
           for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
         } else if (p.act == 2) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = v[e] / (1.f + __expf(-v[e]));
+          for (int e = 0; e < 8; ++e) v[e] = silu(v[e]);
         } else if (p.act == 3) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);

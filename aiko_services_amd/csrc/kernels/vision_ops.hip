@@ -12,6 +12,15 @@ namespace aiko {
 // the canvas is the constant colour ``fill`` (letterbox bars, e.g. 114 for YOLO).  The 4th
 // channel is zero.  ResNet: canvas == image, YOLO: 640x640 canvas with an aspect-preserving
 // image.  One thread per padded output pixel (8-byte store): the buffer never needs a memset.
+// (x / 255 - mean) / std — one definition, so the unfused pre-processing and the fused stem
+// round identically
+__device__ __forceinline__ void normalize3(const float c[3], float m0, float m1, float m2, float is0,
+                                           float is1, float is2, float& v0, float& v1, float& v2) {
+  v0 = (c[0] * (1.f / 255.f) - m0) * is0;
+  v1 = (c[1] * (1.f / 255.f) - m1) * is1;
+  v2 = (c[2] * (1.f / 255.f) - m2) * is2;
+}
+
 // the canvas colour of one pixel (image bilinearly resized into the canvas, ``fill`` around it),
 // normalised; shared by the pre-processing kernel and the fused YOLO stem
 __device__ __forceinline__ void pre_pixel(const uint8_t* __restrict__ in, int b, int Hin, int Win, int Ho,
@@ -45,9 +54,7 @@ __device__ __forceinline__ void pre_pixel(const uint8_t* __restrict__ in, int b,
     }
     if (bgr) { const float t = c[0]; c[0] = c[2]; c[2] = t; }
   }
-  v0 = (c[0] * (1.f / 255.f) - m0) * is0;
-  v1 = (c[1] * (1.f / 255.f) - m1) * is1;
-  v2 = (c[2] * (1.f / 255.f) - m2) * is2;
+  normalize3(c, m0, m1, m2, is0, is1, is2, v0, v1, v2);
 }
 
 __global__ void preprocess_kernel(const uint8_t* __restrict__ in, bf16_t* __restrict__ out,
@@ -94,13 +101,30 @@ __global__ __launch_bounds__(256) void stem_direct_kernel(
   const int IH = (kStemTH - 1) * stride + k, IW = (kStemTW - 1) * stride + k;
   const int tid = threadIdx.x, b = blockIdx.z, lane = tid & 63, wave = tid >> 6;
   const int oy0 = blockIdx.y * kStemTH, ox0 = blockIdx.x * kStemTW;
+  // the kernel is VALU-issue bound (PMC: ~820 VALU instructions per wave against 8 MFMAs), so
+  // the fill avoids the integer division by IW (exact float reciprocal: i < 2^16) and, at scale
+  // 1 (no resize, the camera-size case), pre_pixel's 64-bit per-pixel address arithmetic
+  const float inv_iw = 1.f / (float)IW;
+  const bool noresize = Hin == Ho && Win == Wo;
+  const uint8_t* img = in + (long)b * Hin * Win * 3;
   for (int i = tid; i < IH * IW; i += 256) {
-    const int ty = i / IW, tx = i - ty * IW;
+    const int ty = (int)(((float)i + 0.5f) * inv_iw), tx = i - ty * IW;
     const int yc = oy0 * stride - pad + ty, xc = ox0 * stride - pad + tx;
     uint2 o = {0u, 0u};                         // outside the canvas: the conv's zero padding
     if (yc >= 0 && yc < Hc && xc >= 0 && xc < Wc) {
       float v0, v1, v2;
-      pre_pixel(in, b, Hin, Win, Ho, Wo, off_t, off_l, yc, xc, fill, m0, m1, m2, is0, is1, is2, bgr, v0, v1, v2);
+      if (noresize) {
+        const int yo = yc - off_t, xo = xc - off_l;
+        float c[3] = {fill, fill, fill};
+        if ((unsigned)yo < (unsigned)Ho && (unsigned)xo < (unsigned)Wo) {
+          const uint8_t* px = img + (yo * Win + xo) * 3;
+          c[0] = px[0]; c[1] = px[1]; c[2] = px[2];
+          if (bgr) { const float t = c[0]; c[0] = c[2]; c[2] = t; }
+        }
+        normalize3(c, m0, m1, m2, is0, is1, is2, v0, v1, v2);
+      } else {
+        pre_pixel(in, b, Hin, Win, Ho, Wo, off_t, off_l, yc, xc, fill, m0, m1, m2, is0, is1, is2, bgr, v0, v1, v2);
+      }
       o.x = pack2(v0, v1);
       o.y = pack2(v2, 0.f);
     }
@@ -146,7 +170,7 @@ __global__ __launch_bounds__(256) void stem_direct_kernel(
         for (int e = 0; e < 4; ++e) {
           float a = acc[e] + cb[e];
           if (act == 1) a = fmaxf(a, 0.f);
-          else if (act == 2) a = a / (1.f + __expf(-a));
+          else if (act == 2) a = silu(a);
           v[e] = a;
         }
         *reinterpret_cast<uint2*>(out + (((long)b * H1 + oy) * W1 + ox) * ldo + n0 + 4 * fq) =
@@ -333,7 +357,7 @@ __global__ void batchnorm_kernel(const bf16_t* __restrict__ x, bf16_t* __restric
     for (int e = 0; e < 8; ++e) {
       float t = f[e] * scale[c8 * 8 + e] + shift[c8 * 8 + e];
       if (act == 1) t = fmaxf(t, 0.f);
-      else if (act == 2) t = t / (1.f + __expf(-t));
+      else if (act == 2) t = silu(t);
       f[e] = t;
     }
     u32x4 o;
