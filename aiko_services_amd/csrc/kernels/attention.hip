@@ -44,6 +44,17 @@ constexpr float kRescale = 8.f;   // lazy-rescale threshold (log2 units): P <= 2
 
 __device__ __forceinline__ bf16x8 as_bf16x8(u32x4 u) { return __builtin_bit_cast(bf16x8, u); }
 
+// max over lanes l, l^16, l^32, l^48 on the VALU: gfx950's v_permlane32_swap / v_permlane16_swap
+// with both operands = v return the two halves (rows) of the exchange, so max(result pair) is
+// the xor-32 (xor-16) reduction — no ds_bpermute LDS round trip (~100+ cycles each) on the
+// softmax's critical path
+__device__ __forceinline__ float max_xor16_32(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
 typedef __attribute__((ext_vector_type(4))) short v4i16;
 
 // byte offset of 16-bit column `col` (multiple of 4) of key row `row` in the V image
@@ -240,8 +251,7 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int j = 0; j < 4; ++j) mloc = fmaxf(mloc, s[kt][qt][j]);
-      mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
-      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+      mloc = max_xor16_32(mloc);
       if (mloc * c > m_run[qt] * c + kRescale || m_run[qt] == -INFINITY) {   // wave-uniform per column group
         const float m_new = fmaxf(m_run[qt], mloc);
         const float alpha = fast_exp2((m_run[qt] - m_new) * c);
