@@ -37,16 +37,35 @@ __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
 // which is what softmax wants
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// Wave-wide reductions without the LDS crossbar (each ds_bpermute is an LDS round trip on the
+// reduction's dependency chain): DPP quad_perm xor 1 / xor 2, DPP row_half_mirror / row_mirror
+// (lane i <-> 7 - i, 15 - i inside each 16-lane row: after the quad steps this pairs whole quads
+// and half-rows), then gfx950's v_permlane16_swap / v_permlane32_swap for the row pairs and the
+// wave halves.  Every step adds / maxes the same two operands in every lane, so all 64 lanes end
+// with the bit-identical result, like the xor butterfly this replaces.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+template <class Op>
+__device__ __forceinline__ float wave_reduce(float v, Op op) {
+  v = op(v, dpp_f32<0xB1>(v));     // quad_perm [1,0,3,2]
+  v = op(v, dpp_f32<0x4E>(v));     // quad_perm [2,3,0,1]
+  v = op(v, dpp_f32<0x141>(v));    // row_half_mirror
+  v = op(v, dpp_f32<0x140>(v));    // row_mirror
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = op(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return op(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  return wave_reduce(v, [](float x, float y) { return fmaxf(x, y); });
 }
 
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  return wave_reduce(v, [](float x, float y) { return x + y; });
 }
 
 // 16-byte LDS-DMA (global_load_lds_dwordx4) issued through inline asm: the LDS destination is
