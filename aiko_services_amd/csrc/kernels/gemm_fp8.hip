@@ -143,8 +143,8 @@ __device__ __forceinline__ void fp8_epilogue(const Fp8GemmParams& p,
       float amax = 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[e]));
-      amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
-      amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+      amax = fmaxf(amax, dpp_f32<0xB1>(amax));     // quad_perm: lanes ^1 (DPP, no LDS trip)
+      amax = fmaxf(amax, dpp_f32<0x4E>(amax));     // lanes ^2
       const int ex = mx_exponent(amax);
       const float inv = __uint_as_float((uint32_t)(127 - ex) << 23);
       unsigned w0 = 0u, w1 = 0u;
