@@ -184,7 +184,7 @@ void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, co
     rc = aiko_conv_persist(x.data_ptr(), w.data_ptr(), bptr, rptr, y.data_ptr(), H, W, C, Cc, R, S, stride,
                            pad, Ho, Wo, M, Cout, K, act, ldy, ldr, bm, bn, x2ptr, K1, H2, W2, C2, stride2,
                            cur_stream());
-  } else if (variant == 2 || variant == 3 || variant == 5) {
+  } else if (variant == 2 || variant == 3 || variant == 5 || variant == 6) {
     // buffer-LDS-DMA kernel: 64-channel K blocks inside one tap, byte offsets in 31 bits;
     // variant 3 = the same kernel at forced high occupancy (64x64: 5, 64x128 / 128x64: 3 WG/CU)
     TORCH_CHECK(Cc % 64 == 0 && R * S <= 32 && x_extent * 2 < (1LL << 31) - 64 && w.numel() * 2 < (1LL << 31),
@@ -192,7 +192,8 @@ void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, co
     TORCH_CHECK(!dual || avail_elems(*x2) * 2 < (1LL << 31) - 64, "aiko.conv_igemm_out: x2 too large for variant 2");
     rc = aiko_conv_buf(x.data_ptr(), w.data_ptr(), bptr, rptr, y.data_ptr(), H, W, C, Cc, R, S, stride,
                        pad, Ho, Wo, M, Cout, K, act, ldy, ldr, bm, bn, x2ptr, K1, H2, W2, C2, stride2,
-                       variant == 3 ? (bm == 64 && bn == 64 ? 5 : 3) : 0, variant == 5 ? 1 : 0, cur_stream());
+                       variant == 3 ? (bm == 64 && bn == 64 ? 5 : 3) : (variant == 6 ? 1 : 0), variant == 5 ? 1 : 0,
+                       cur_stream());
   } else if (variant == 1) {
     TORCH_CHECK(zero.has_value() && zero->defined() && zero->is_cuda() && zero->nbytes() >= 16 &&
                     reinterpret_cast<uintptr_t>(zero->data_ptr()) % 16 == 0,

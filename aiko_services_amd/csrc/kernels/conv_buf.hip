@@ -418,6 +418,13 @@ extern "C" int aiko_conv_buf(const void* x, const void* w, const float* bias, co
       conv_buf_kernel<128, 64, 2, 2, 3><<<grid, block, 0, stream>>>(p);
     else if (bm == 64 && bn == 64 && occ == 4)
       conv_buf_kernel<64, 64, 2, 2, 4><<<grid, block, 0, stream>>>(p);
+    // variant 6: 4 waves of 128 x 64 / 64 x 128 (one workgroup per CU, 3-slot ring in 144 KB):
+    // half the LDS fragment bytes per MFMA of the 8-wave 64 x 64 layout — the wide 3x3 tiles are
+    // bound by LDS read bandwidth, not by the matrix pipe
+    else if (bm == 256 && bn == 128 && occ == 1)
+      conv_buf_kernel<256, 128, 2, 2, 1><<<grid, block, 0, stream>>>(p);
+    else if (bm == 128 && bn == 256 && occ == 1)
+      conv_buf_kernel<128, 256, 2, 2, 1><<<grid, block, 0, stream>>>(p);
     else
       return -1;
   } else if (mf32) {                       // variant 5: 32x32x16 MFMA

@@ -232,6 +232,11 @@ BUF_OCC_TILES = ((64, 64), (64, 128), (128, 64))       # variant 3: buffer-DMA a
 PERSIST_TILES = ((64, 128),)   # variant 4: persistent, one K-block ring across tiles (2 workgroups/CU)
 # variant 5: buffer-DMA kernel on v_mfma_f32_32x32x16_bf16 (3x the free issue slots per MFMA)
 MF32_TILES = ((128, 128), (128, 64), (64, 128), (256, 128), (128, 256))
+# variant 6: 4 waves of 128 x 64 / 64 x 128 per workgroup, one workgroup per CU (fewer LDS
+# fragment bytes per MFMA than the 8-wave 64 x 64 layouts of BUF_WIDE_TILES).  Measured on the
+# ResNet-50 layers: never the tuner's pick — one wave per SIMD exposes the DMA / LDS latency
+# that the 8-wave layouts hide — kept as a candidate for other shapes
+WIDE4_TILES = ((256, 128), (128, 256))
 
 
 def buf_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = None) -> bool:
@@ -253,6 +258,7 @@ def _tune(key, M, cout, launch, buf_ok=False):
             cands += [t + (2,) for t in TILES + BUF_WIDE_TILES] + [t + (3,) for t in BUF_OCC_TILES]
             cands += [t + (4,) for t in PERSIST_TILES]
             cands += [t + (5,) for t in MF32_TILES]
+            cands += [t + (6,) for t in WIDE4_TILES]
     best, best_t = None, None
     for t in cands:
         launch(t)  # warm

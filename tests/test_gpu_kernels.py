@@ -58,6 +58,11 @@ def _nhwc(x_nchw):
     (3, 14, 14, 256, 512, 1, 1, 0, None, False, (128, 256, 5)),
     (1, 9, 11, 128, 64, 3, 2, 1, "silu", False, (256, 128, 5)),
     (2, 7, 7, 512, 512, 3, 1, 1, "relu", False, (128, 128, 5)),
+    # 4-wave wide tiles (variant 6): 128 x 64 / 64 x 128 per wave, one workgroup per CU
+    (2, 28, 28, 128, 256, 3, 1, 1, "relu", True, (256, 128, 6)),
+    (3, 14, 14, 256, 512, 1, 1, 0, None, False, (128, 256, 6)),
+    (1, 9, 11, 128, 256, 3, 2, 1, "silu", True, (128, 256, 6)),
+    (2, 7, 7, 512, 128, 3, 1, 1, "relu", False, (256, 128, 6)),
     # high-occupancy buffer-DMA (variant 3)
     (2, 28, 28, 128, 512, 1, 1, 0, "relu", True, (64, 128, 3)),
     (1, 9, 11, 128, 64, 3, 1, 1, "silu", False, (64, 64, 3)),
