@@ -70,6 +70,9 @@ int aiko_topk_nms(const void* boxes, const float* scores, const int* cls, int B,
 int aiko_avgpool(const void* x, void* y, int B, int HW, int C, hipStream_t stream);
 int aiko_mean_rows_f32(const void* x, float* y, int B, int T, int C, hipStream_t stream);
 int aiko_window_shift(const float* src, const float* chunk, float* dst, int B, int W, int n, hipStream_t stream);
+int aiko_conv_narrow(const void* x, const void* w, const float* bias, const void* res, void* y, int H, int W, int C,
+                     int Cc, int R, int S, int stride, int pad, int Ho, int Wo, int M, int Cout, int K, int act,
+                     int ldy, int ldr, hipStream_t stream);
 int aiko_stem_pool(const void* x, const void* w, const float* bias, void* y, int B, int Hp, int Wp,
                    int Ho, int Wo, int Hm, int Wm, int ldy, int variant, hipStream_t stream);
 int aiko_softmax_topk(const void* logits, float* prob, int* index, int B, int N, int k,
@@ -110,7 +113,9 @@ void check_launch(int rc, const char* what) {
 //         K1, H2, W2, C2, stride2 (the optional second source x2), [variant]]
 // variant 0: register-staged kernel (conv_igemm.hip); 1: LDS-DMA kernel (conv_glds.hip), which
 // needs ``zero`` (>= 16 B of zeros on the device) as the source of conv padding; 2: buffer
-// LDS-DMA kernel (conv_buf.hip, padding by out-of-range buffer reads).
+// LDS-DMA kernel (conv_buf.hip, padding by out-of-range buffer reads); 3 / 5 / 6: conv_buf at high
+// occupancy / on 32x32x16 MFMA / as 4-wave wide tiles; 4: persistent conv_buf; 7: direct 3x3 kernel
+// for narrow layers (conv_narrow.hip).
 void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, const at::Tensor& w,
                     const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& res,
                     at::Tensor& y, at::IntArrayRef geom, const c10::optional<at::Tensor>& zero) {
@@ -175,7 +180,14 @@ void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, co
     rptr = res->data_ptr();
   }
   int rc;
-  if (variant == 4) {
+  if (variant == 7) {
+    // direct 3x3 kernel for narrow layers (conv_narrow.hip): Cc, Cout in {16, 32}, pad 1, stride 1/2
+    TORCH_CHECK(!dual && R == 3 && S == 3 && pad == 1 && (stride == 1 || stride == 2) && (Cc == 16 || Cc == 32) &&
+                    (Cout == 16 || Cout == 32),
+                "aiko.conv_igemm_out: variant 7 needs a 3x3 / pad 1 / stride 1-2 conv with Cc, Cout in {16, 32}");
+    rc = aiko_conv_narrow(x.data_ptr(), w.data_ptr(), bptr, rptr, y.data_ptr(), H, W, C, Cc, R, S, stride, pad, Ho,
+                          Wo, M, Cout, K, act, ldy, ldr, cur_stream());
+  } else if (variant == 4) {
     // persistent buffer-LDS-DMA kernel: one K-block stream across each workgroup's run of tiles
     TORCH_CHECK(Cc % 64 == 0 && R * S <= 32 && K % 64 == 0 && x_extent * 2 < (1LL << 31) - 64 &&
                     w.numel() * 2 < (1LL << 31),

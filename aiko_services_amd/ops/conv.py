@@ -249,9 +249,18 @@ def buf_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = No
             and (x2 is None or nbytes(x2) < 2**31 - 64))
 
 
-def _tune(key, M, cout, launch, buf_ok=False):
+def narrow_variant_ok(spec: ConvSpec, x2: torch.Tensor | None = None) -> bool:
+    """Whether the direct narrow-layer kernel (variant 7, conv_narrow.hip) applies: a 3x3 / pad 1
+    / stride 1-2 conv with 16 or 32 input and output channels, no second source."""
+    return (spec.kind != "stem" and x2 is None and spec.K1 is None and spec.R == 3 and spec.S == 3
+            and spec.pad == 1 and spec.stride in (1, 2) and spec.Cc in (16, 32) and spec.cout in (16, 32))
+
+
+def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False):
     if cout <= 32:
         cands = [t + (0,) for t in NARROW_TILES]
+        if narrow_ok:
+            cands.append((8, 32, 7))         # variant 7: tile fixed by the kernel (8 x 32 pixels)
     else:
         cands = [t + (0,) for t in TILES] + [t + (1,) for t in TILES]
         if buf_ok:
@@ -343,7 +352,7 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None
         tile = _tile_cache.get(key)
         if tile is None:
             if _tuning:
-                tile = _tune(key, M, spec.cout, launch, buf_variant_ok(spec, x, x2))
+                tile = _tune(key, M, spec.cout, launch, buf_variant_ok(spec, x, x2), narrow_variant_ok(spec, x2))
             else:
                 tile = pick_tile(M, spec.cout)
     launch(tile)

@@ -63,6 +63,12 @@ def _nhwc(x_nchw):
     (3, 14, 14, 256, 512, 1, 1, 0, None, False, (128, 256, 6)),
     (1, 9, 11, 128, 256, 3, 2, 1, "silu", True, (128, 256, 6)),
     (2, 7, 7, 512, 128, 3, 1, 1, "relu", False, (256, 128, 6)),
+    # direct narrow 3x3 kernel (variant 7): Cc / Cout 16 or 32, stride 1 / 2, ragged tiles
+    (2, 40, 70, 16, 16, 3, 1, 1, "silu", True, (8, 32, 7)),
+    (1, 33, 65, 16, 32, 3, 2, 1, "silu", False, (8, 32, 7)),
+    (2, 17, 37, 32, 32, 3, 1, 1, "relu", True, (8, 32, 7)),
+    (1, 20, 64, 32, 16, 3, 2, 1, None, False, (8, 32, 7)),
+    (1, 9, 10, 16, 32, 3, 1, 1, "gelu", True, (8, 32, 7)),
     # high-occupancy buffer-DMA (variant 3)
     (2, 28, 28, 128, 512, 1, 1, 0, "relu", True, (64, 128, 3)),
     (1, 9, 11, 128, 64, 3, 1, 1, "silu", False, (64, 64, 3)),
@@ -111,6 +117,26 @@ def test_conv_writes_into_channel_slice(native):
     ref = R.conv_ref(xin.permute(0, 3, 1, 2).float(), spec)
     assert _rel_err(cat[..., 64:].permute(0, 3, 1, 2), ref) < 1e-2
     assert cat[..., :64].abs().max().item() == 0
+
+
+def test_conv_narrow_slices_post_residual(native):
+    """Variant 7 as YOLO's C2f bottleneck runs it: 16-channel input slice of a concat buffer,
+    output into another slice, residual (the input slice) added AFTER the SiLU."""
+    from aiko_services_amd.ops import conv as C
+    g = torch.Generator().manual_seed(11)
+    B, H, W = 2, 24, 40
+    cat = torch.randn(B, H, W, 48, generator=g).to(torch.bfloat16).to(DEV)
+    xin = cat[..., 16:32]
+    w = torch.randn(16, 16, 3, 3, generator=g) / 12
+    b = torch.randn(16, generator=g) * 0.1
+    spec = C.make_conv_spec(w, b, pad=1, act="silu", device=DEV)
+    out = torch.zeros(B, H, W, 64, dtype=torch.bfloat16, device=DEV)
+    C.conv2d(xin, spec, residual=xin, out=out[..., 32:48], tile=(8, 32, 7), residual_after_act=True)
+    ref_out = torch.zeros_like(out)
+    C.conv2d(xin, spec, residual=xin, out=ref_out[..., 32:48], tile=(128, 32, 0), residual_after_act=True)
+    torch.cuda.synchronize()
+    assert _rel_err(out[..., 32:48].float(), ref_out[..., 32:48].float()) < 1e-2
+    assert out[..., :32].abs().max().item() == 0 and out[..., 48:].abs().max().item() == 0
 
 
 def test_stem_and_preprocess(native):
