@@ -9,7 +9,7 @@
 //     is copied into LDS once, pixel-major with the channels contiguous — all of a thread's
 //     16-byte loads issued before the first LDS store — and every tap reads it from there;
 //   * v_mfma_f32_16x16x32_bf16 with the WEIGHTS as the A operand (lane row = output channel, held
-//     in registers for the whole tile) and pixels as B (lane column = pixel): a 32-wide K chunk
+//     in registers for the whole tile — in LDS for Cc 32) and pixels as B (lane column = pixel): a 32-wide K chunk
 //     is two taps x 16 channels (Cc 16) or one tap x 32 channels (Cc 32), so a B fragment is one
 //     16-byte LDS read at a per-lane tap offset computed once;
 //   * each lane ends with 4 consecutive output channels of one pixel: bias, residual (before or
@@ -41,7 +41,13 @@ __global__ __launch_bounds__(256) void conv_narrow_kernel(NarrowParams p) {
   constexpr int KT = 9 * CC;                    // real K
   constexpr int NKC = (KT + 31) / 32;           // 32-wide K chunks
   constexpr int NT = COUT / 16;                 // 16-channel output tiles
+  // Cc 32: the 9-chunk weight set would hold 72 VGPRs per lane for the whole tile; it is staged
+  // in LDS instead and read per K chunk (16-B reads, 16 lanes share a row).  Measured on the
+  // YOLOv8-n Cc-32 layers: on par with the igemm kernel (28-32 us), either may win per layer
+  constexpr bool WLDS = CC == 32;
+  constexpr int WELEMS = WLDS ? COUT * NKC * 32 : 8;
   __shared__ __attribute__((aligned(16))) bf16_t tile[IH * IW * CC];
+  __shared__ __attribute__((aligned(16))) bf16_t wlds[WELEMS];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int per_img = p.tiles_h * p.tiles_w;
@@ -75,14 +81,24 @@ __global__ __launch_bounds__(256) void conv_narrow_kernel(NarrowParams p) {
     }
   }
 
-  // ---- 2. weights (A operand) into registers while the halo lands ----
+  // ---- 2. weights (A operand): registers (Cc 16) or LDS (Cc 32) while the halo lands ----
   const int fr = lane & 15, fq = lane >> 4;
-  bf16x8 wa[NT][NKC];
+  bf16x8 wa[NT][WLDS ? 1 : NKC];
+  if constexpr (WLDS) {
+    // [n][NKC * 32] row-major copy of the used K range: (COUT * NKC * 4) 16-byte pieces
+    constexpr int WP = COUT * NKC * 4;
+    for (int i = tid; i < WP; i += 256) {
+      const int n = i / (NKC * 4), q = i - n * (NKC * 4);
+      *reinterpret_cast<u32x4*>(wlds + n * (NKC * 32) + q * 8) =
+          *reinterpret_cast<const u32x4*>(p.w + (long)n * p.K + q * 8);
+    }
+  } else {
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt)
+    for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-    for (int kc = 0; kc < NKC; ++kc)
-      wa[nt][kc] = *reinterpret_cast<const bf16x8*>(p.w + (long)(nt * 16 + fr) * p.K + kc * 32 + fq * 8);
+      for (int kc = 0; kc < (WLDS ? 1 : NKC); ++kc)
+        wa[nt][kc] = *reinterpret_cast<const bf16x8*>(p.w + (long)(nt * 16 + fr) * p.K + kc * 32 + fq * 8);
+  }
   // this lane's B-fragment offset (elements, relative to the pixel) for every K chunk; -1 = the
   // zero padding past the 9th tap
   int toff[NKC];
@@ -118,8 +134,15 @@ __global__ __launch_bounds__(256) void conv_narrow_kernel(NarrowParams p) {
         b = __builtin_bit_cast(bf16x8, u32x4{0u, 0u, 0u, 0u});
       }
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[nt][kc], b, acc[nt], 0, 0, 0);
+      for (int nt = 0; nt < NT; ++nt) {
+        bf16x8 a;
+        if constexpr (WLDS) {
+          a = *reinterpret_cast<const bf16x8*>(wlds + (nt * 16 + fr) * (NKC * 32) + kc * 32 + fq * 8);
+        } else {
+          a = wa[nt][kc];
+        }
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[nt], 0, 0, 0);
+      }
     }
     const int oy = oy0 + ly, ox = ox0 + lx;
     if (oy >= p.Ho || ox >= p.Wo) continue;
