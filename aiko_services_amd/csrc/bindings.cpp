@@ -182,9 +182,10 @@ void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, co
   int rc;
   if (variant == 7) {
     // direct 3x3 kernel for narrow layers (conv_narrow.hip): Cc, Cout in {16, 32}, pad 1, stride 1/2
-    TORCH_CHECK(!dual && R == 3 && S == 3 && pad == 1 && (stride == 1 || stride == 2) && (Cc == 16 || Cc == 32) &&
-                    (Cout == 16 || Cout == 32),
-                "aiko.conv_igemm_out: variant 7 needs a 3x3 / pad 1 / stride 1-2 conv with Cc, Cout in {16, 32}");
+    TORCH_CHECK(!dual && ((R == 3 && S == 3 && pad == 1 && (stride == 1 || stride == 2)) ||
+                          (R == 1 && S == 1 && pad == 0 && stride == 1)) &&
+                    (Cc == 16 || Cc == 32) && (Cout == 16 || Cout == 32),
+                "aiko.conv_igemm_out: variant 7 needs a 3x3 / pad 1 / stride 1-2 or 1x1 / stride 1 conv with Cc, Cout in {16, 32}");
     rc = aiko_conv_narrow(x.data_ptr(), w.data_ptr(), bptr, rptr, y.data_ptr(), H, W, C, Cc, R, S, stride, pad, Ho,
                           Wo, M, Cout, K, act, ldy, ldr, cur_stream());
   } else if (variant == 4) {

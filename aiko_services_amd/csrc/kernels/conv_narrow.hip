@@ -1,5 +1,6 @@
-// Direct 3x3 convolution for narrow layers: Cc (input channels) and Cout in {16, 32}, pad 1,
-// stride 1 or 2 — YOLOv8's 160x160 stage (the stride-2 16 -> 32 conv and the C2f bottlenecks).
+// Direct convolution for narrow layers: 3x3 / pad 1 (stride 1 or 2) and 1x1 (stride 1), Cc (input
+// channels) and Cout in {16, 32} — YOLOv8's 160x160 stage (the stride-2 16 -> 32 conv, the C2f
+// bottlenecks and the C2f 1x1 convs).
 //
 // The implicit-GEMM kernels spend these layers on address arithmetic: with K = 144 / 288 a tile
 // runs only 3-5 K blocks, so the per-row gather setup, per-piece tap decoding and the LDS-staged
@@ -32,13 +33,14 @@ struct NarrowParams {
 
 constexpr int kNTH = 8, kNTW = 32;   // output tile rows x cols: 4 waves x 4 blocks of 16 pixels
 
-template <int CC, int COUT, int ST>
+template <int CC, int COUT, int ST, int FR = 3>
 __global__ __launch_bounds__(256) void conv_narrow_kernel(NarrowParams p) {
-  constexpr int IH = (kNTH - 1) * ST + 3, IW = (kNTW - 1) * ST + 3;
+  constexpr int TAPS = FR * FR, PAD = FR / 2;   // 3x3 / pad 1 or 1x1 / pad 0
+  constexpr int IH = (kNTH - 1) * ST + FR, IW = (kNTW - 1) * ST + FR;
   constexpr int CH = CC / 8;                    // 16-byte chunks per pixel
   constexpr int NCHUNK = IH * IW * CH;
   constexpr int PER = (NCHUNK + 255) / 256;
-  constexpr int KT = 9 * CC;                    // real K
+  constexpr int KT = TAPS * CC;                 // real K
   constexpr int NKC = (KT + 31) / 32;           // 32-wide K chunks
   constexpr int NT = COUT / 16;                 // 16-channel output tiles
   // Cc 32: the 9-chunk weight set would hold 72 VGPRs per lane for the whole tile; it is staged
@@ -56,7 +58,7 @@ __global__ __launch_bounds__(256) void conv_narrow_kernel(NarrowParams p) {
   const int t = bid - img * per_img;
   const int ty = t / p.tiles_w, tx = t - ty * p.tiles_w;
   const int oy0 = ty * kNTH, ox0 = tx * kNTW;
-  const int iy0 = oy0 * ST - 1, ix0 = ox0 * ST - 1;          // pad 1
+  const int iy0 = oy0 * ST - PAD, ix0 = ox0 * ST - PAD;
   const bf16_t* xi = p.x + (long)img * p.H * p.W * p.C;
 
   // ---- 1. input halo -> LDS (zeros outside the image: the conv's padding) ----
@@ -100,13 +102,13 @@ __global__ __launch_bounds__(256) void conv_narrow_kernel(NarrowParams p) {
         wa[nt][kc] = *reinterpret_cast<const bf16x8*>(p.w + (long)(nt * 16 + fr) * p.K + kc * 32 + fq * 8);
   }
   // this lane's B-fragment offset (elements, relative to the pixel) for every K chunk; -1 = the
-  // zero padding past the 9th tap
+  // zero padding past the last tap
   int toff[NKC];
 #pragma unroll
   for (int kc = 0; kc < NKC; ++kc) {
     const int k0 = kc * 32 + fq * 8;
     const int tap = k0 / CC, c0 = k0 - tap * CC;
-    toff[kc] = tap < 9 ? ((tap / 3) * IW + (tap % 3)) * CC + c0 : -1;
+    toff[kc] = tap < TAPS ? ((tap / FR) * IW + (tap % FR)) * CC + c0 : -1;
   }
   float cb[NT][4];
 #pragma unroll
@@ -178,15 +180,17 @@ __global__ __launch_bounds__(256) void conv_narrow_kernel(NarrowParams p) {
 
 }  // namespace aiko
 
-// Same arguments as aiko_conv_igemm (bm / bn / second source unused).  Supported: R = S = 3,
-// pad 1, stride 1 / 2, Cc and Cout in {16, 32}, K = 9 Cc rounded up to 64; returns -1 otherwise.
+// Same arguments as aiko_conv_igemm (bm / bn / second source unused).  Supported: R = S = 3 with
+// pad 1 or R = S = 1 with pad 0, stride 1 / 2, Cc and Cout in {16, 32}, K = R S Cc rounded up to
+// 64; returns -1 otherwise.
 extern "C" int aiko_conv_narrow(const void* x, const void* w, const float* bias, const void* res,
                                 void* y, int H, int W, int C, int Cc, int R, int S, int stride,
                                 int pad, int Ho, int Wo, int M, int Cout, int K, int act, int ldy,
                                 int ldr, hipStream_t stream) {
   using namespace aiko;
-  if (R != 3 || S != 3 || pad != 1 || (stride != 1 && stride != 2) || (Cc != 16 && Cc != 32) ||
-      (Cout != 16 && Cout != 32) || K < 9 * Cc || K % 64 || C % 8 || ldy % 4 || ldr % 4 ||
+  const bool k3 = R == 3 && S == 3 && pad == 1, k1 = R == 1 && S == 1 && pad == 0;
+  if ((!k3 && !k1) || (stride != 1 && stride != 2) || (Cc != 16 && Cc != 32) ||
+      (Cout != 16 && Cout != 32) || K < R * S * Cc || K % 64 || C % 8 || ldy % 4 || ldr % 4 ||
       Ho <= 0 || Wo <= 0 || M % (Ho * Wo))
     return -1;
   NarrowParams p;
@@ -201,10 +205,11 @@ extern "C" int aiko_conv_narrow(const void* x, const void* w, const float* bias,
   const long grid = (long)(M / (Ho * Wo)) * p.tiles_h * p.tiles_w;
   if (grid <= 0 || grid > 0x7fffffffL) return -1;
   const dim3 g((unsigned)grid), b(256);
-#define AIKO_NARROW(CC, CO, ST) \
-  if (Cc == CC && Cout == CO && stride == ST) { conv_narrow_kernel<CC, CO, ST><<<g, b, 0, stream>>>(p); return (int)hipGetLastError(); }
-  AIKO_NARROW(16, 16, 1) AIKO_NARROW(16, 32, 1) AIKO_NARROW(32, 16, 1) AIKO_NARROW(32, 32, 1)
-  AIKO_NARROW(16, 16, 2) AIKO_NARROW(16, 32, 2) AIKO_NARROW(32, 16, 2) AIKO_NARROW(32, 32, 2)
+#define AIKO_NARROW(FR, CC, CO, ST) \
+  if (R == FR && Cc == CC && Cout == CO && stride == ST) { conv_narrow_kernel<CC, CO, ST, FR><<<g, b, 0, stream>>>(p); return (int)hipGetLastError(); }
+  AIKO_NARROW(3, 16, 16, 1) AIKO_NARROW(3, 16, 32, 1) AIKO_NARROW(3, 32, 16, 1) AIKO_NARROW(3, 32, 32, 1)
+  AIKO_NARROW(3, 16, 16, 2) AIKO_NARROW(3, 16, 32, 2) AIKO_NARROW(3, 32, 16, 2) AIKO_NARROW(3, 32, 32, 2)
+  AIKO_NARROW(1, 16, 16, 1) AIKO_NARROW(1, 16, 32, 1) AIKO_NARROW(1, 32, 16, 1) AIKO_NARROW(1, 32, 32, 1)
 #undef AIKO_NARROW
   return -1;
 }

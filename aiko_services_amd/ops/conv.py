@@ -251,9 +251,11 @@ def buf_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = No
 
 def narrow_variant_ok(spec: ConvSpec, x2: torch.Tensor | None = None) -> bool:
     """Whether the direct narrow-layer kernel (variant 7, conv_narrow.hip) applies: a 3x3 / pad 1
-    / stride 1-2 conv with 16 or 32 input and output channels, no second source."""
-    return (spec.kind != "stem" and x2 is None and spec.K1 is None and spec.R == 3 and spec.S == 3
-            and spec.pad == 1 and spec.stride in (1, 2) and spec.Cc in (16, 32) and spec.cout in (16, 32))
+    / stride 1-2 or 1x1 / stride 1 conv with 16 or 32 input and output channels, no second source."""
+    shape_ok = ((spec.R == 3 and spec.S == 3 and spec.pad == 1 and spec.stride in (1, 2))
+                or (spec.R == 1 and spec.S == 1 and spec.pad == 0 and spec.stride == 1))
+    return (spec.kind != "stem" and x2 is None and spec.K1 is None and shape_ok
+            and spec.Cc in (16, 32) and spec.cout in (16, 32))
 
 
 def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False):

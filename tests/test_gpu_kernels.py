@@ -69,6 +69,8 @@ def _nhwc(x_nchw):
     (2, 17, 37, 32, 32, 3, 1, 1, "relu", True, (8, 32, 7)),
     (1, 20, 64, 32, 16, 3, 2, 1, None, False, (8, 32, 7)),
     (1, 9, 10, 16, 32, 3, 1, 1, "gelu", True, (8, 32, 7)),
+    (2, 21, 45, 32, 32, 1, 1, 0, "silu", True, (8, 32, 7)),
+    (1, 16, 32, 16, 32, 1, 1, 0, None, False, (8, 32, 7)),
     # high-occupancy buffer-DMA (variant 3)
     (2, 28, 28, 128, 512, 1, 1, 0, "relu", True, (64, 128, 3)),
     (1, 9, 11, 128, 64, 3, 1, 1, "silu", False, (64, 64, 3)),
