@@ -68,7 +68,8 @@ int aiko_topk_nms(const void* boxes, const float* scores, const int* cls, int B,
                   float pad_l, float pad_t, float img_w, float img_h, float* det, int* count,
                   void* workspace, hipStream_t stream);
 int aiko_avgpool(const void* x, void* y, int B, int HW, int C, hipStream_t stream);
-int aiko_mean_rows_f32(const void* x, float* y, int B, int T, int C, hipStream_t stream);
+int aiko_mean_rows_f32(const void* x, float* y, int B, int T, int C, long ldb, hipStream_t stream);
+int aiko_zero_border_rows(void* x, int B, int rows, int C, hipStream_t stream);
 int aiko_window_shift(const float* src, const float* chunk, float* dst, int B, int W, int n, hipStream_t stream);
 int aiko_conv_narrow(const void* x, const void* w, const float* bias, const void* res, void* y, int H, int W, int C,
                      int Cc, int R, int S, int stride, int pad, int Ho, int Wo, int M, int Cout, int K, int act,
@@ -500,12 +501,28 @@ void topk_nms_out(const at::Tensor& boxes, const at::Tensor& scores, const at::T
 void mean_rows_out(const at::Tensor& x, at::Tensor& y) {
   check_cuda(x, "x");
   check_cuda(y, "y");
-  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 3 && x.is_contiguous() &&
+  // x may be a T-prefix view of a [B, Tp, C] buffer: rows contiguous, any batch pitch >= T*C
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 3 && x.stride(2) == 1 &&
+                  x.stride(1) == x.size(2) && x.stride(0) >= x.size(1) * x.size(2) &&
                   y.scalar_type() == at::kFloat && y.is_contiguous(),
-              "aiko.mean_rows_out: x bf16 [B, T, C] contiguous, y fp32 [B, C]");
+              "aiko.mean_rows_out: x bf16 [B, T, C] with contiguous rows, y fp32 [B, C]");
   const int64_t B = x.size(0), T = x.size(1), C = x.size(2);
   TORCH_CHECK(C % 8 == 0 && y.numel() == B * C, "aiko.mean_rows_out: C % 8 == 0, y [B, C]");
-  check_launch(aiko_mean_rows_f32(x.data_ptr(), y.data_ptr<float>(), B, T, C, cur_stream()), "mean_rows");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && x.stride(0) % 8 == 0,
+              "aiko.mean_rows_out: 16-byte aligned rows");
+  TORCH_CHECK(avail_elems(x) >= (B - 1) * x.stride(0) + T * C, "aiko.mean_rows_out: x storage too small");
+  check_launch(aiko_mean_rows_f32(x.data_ptr(), y.data_ptr<float>(), B, T, C, (long)x.stride(0), cur_stream()),
+               "mean_rows");
+}
+
+void zero_border_rows_(at::Tensor& x, int64_t rows) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.is_contiguous() && x.size(1) % 8 == 0 &&
+                  rows >= 2 && x.size(0) % rows == 0,
+              "aiko.zero_border_rows_: x bf16 [B*rows, C] contiguous, C % 8 == 0");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "aiko.zero_border_rows_: alignment");
+  check_launch(aiko_zero_border_rows(x.data_ptr(), x.size(0) / rows, rows, x.size(1), cur_stream()),
+               "zero_border_rows");
 }
 
 void window_shift_out(const at::Tensor& src, const at::Tensor& chunk, at::Tensor& dst) {
@@ -907,6 +924,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("avgpool_out(Tensor x, Tensor(a!) y) -> ()");
   m.def("mean_rows_out(Tensor x, Tensor(a!) y) -> ()");
   m.def("window_shift_out(Tensor src, Tensor chunk, Tensor(a!) dst) -> ()");
+  m.def("zero_border_rows_(Tensor(a!) x, int rows) -> ()");
   m.def("stem_pool_out(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, int Ho, int Wo, int variant=0) -> ()");
   m.def("gemm_fp8_out(Tensor a, Tensor? sa, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!)? y, int act, int bm, int bn, int variant=0, Tensor? zero=None, Tensor? amx=None, Tensor(b!)? yq=None, Tensor(c!)? ysc=None) -> ()");
   m.def("rownorm_quant_out(Tensor x, Tensor? gamma, Tensor? beta, float eps, Tensor(a!)? yb, Tensor(b!)? q, Tensor(c!)? qs) -> ()");
@@ -933,6 +951,7 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("avgpool_out", &avgpool_out);
   m.impl("mean_rows_out", &mean_rows_out);
   m.impl("window_shift_out", &window_shift_out);
+  m.impl("zero_border_rows_", &zero_border_rows_);
   m.impl("stem_pool_out", &stem_pool_out);
   m.impl("softmax_topk_out", &softmax_topk_out);
   m.impl("gemm_fp8_out", &gemm_fp8_out);

@@ -442,7 +442,8 @@ namespace aiko {
 // 256-thread block per (batch, 256 channels); 8 row phases x 32 lanes of 8 channels, each lane
 // keeping 4 row loads in flight, then an LDS reduction of the 8 phases.
 __global__ __launch_bounds__(256) void mean_rows_f32_kernel(const bf16_t* __restrict__ x,
-                                                            float* __restrict__ y, int T, int C) {
+                                                            float* __restrict__ y, int T, int C,
+                                                            long ldb) {
   __shared__ float red[8][32][9];
   const int cl = threadIdx.x & 31, ph = threadIdx.x >> 5;
   const int C8 = C >> 3;
@@ -450,7 +451,7 @@ __global__ __launch_bounds__(256) void mean_rows_f32_kernel(const bf16_t* __rest
   const int b = blockIdx.y;
   float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (c8 < C8) {
-    const bf16_t* src = x + (long)b * T * C + c8 * 8;
+    const bf16_t* src = x + (long)b * ldb + c8 * 8;      // ldb: batch pitch (rows may be a T-prefix)
     int i = ph;
     for (; i + 24 < T; i += 32) {
       u32x4 v[4];
@@ -491,12 +492,26 @@ __global__ __launch_bounds__(256) void mean_rows_f32_kernel(const bf16_t* __rest
     *reinterpret_cast<f32x4*>(dst + 4) = f32x4{o[4], o[5], o[6], o[7]};
   }
 }
+
+// Zero rows b*rows and b*rows + rows - 1 of a [B*rows, C] bf16 buffer (the per-clip zero border
+// rows of the Whisper conv stem; the conv over the concatenated clips writes across them)
+__global__ __launch_bounds__(256) void zero_border_rows_kernel(bf16_t* __restrict__ x, int B, int rows, int C) {
+  const int C8 = C >> 3;
+  const long total = (long)B * 2 * C8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % C8);
+    const long br = i / C8;
+    const int b = (int)(br >> 1), last = (int)(br & 1);
+    const long row = (long)b * rows + (last ? rows - 1 : 0);
+    *reinterpret_cast<u32x4*>(x + row * C + c8 * 8) = u32x4{0u, 0u, 0u, 0u};
+  }
+}
 }  // namespace aiko
 
-extern "C" int aiko_mean_rows_f32(const void* x, float* y, int B, int T, int C, hipStream_t stream) {
-  if (C % 8 || T < 1) return -1;
+extern "C" int aiko_mean_rows_f32(const void* x, float* y, int B, int T, int C, long ldb, hipStream_t stream) {
+  if (C % 8 || T < 1 || ldb < (long)T * C) return -1;
   dim3 grid((C / 8 + 31) / 32, B);
-  aiko::mean_rows_f32_kernel<<<grid, 256, 0, stream>>>(static_cast<const aiko::bf16_t*>(x), y, T, C);
+  aiko::mean_rows_f32_kernel<<<grid, 256, 0, stream>>>(static_cast<const aiko::bf16_t*>(x), y, T, C, ldb);
   return (int)hipGetLastError();
 }
 
@@ -521,5 +536,14 @@ extern "C" int aiko_softmax_topk(const void* logits, float* prob, int* index, in
   } else {
     return -1;
   }
+  return (int)hipGetLastError();
+}
+
+extern "C" int aiko_zero_border_rows(void* x, int B, int rows, int C, hipStream_t stream) {
+  if (C % 8 || rows < 2 || B < 1) return -1;
+  const long total = (long)B * 2 * (C / 8);
+  long g = (total + 255) / 256;
+  if (g > 4096) g = 4096;
+  aiko::zero_border_rows_kernel<<<(int)g, 256, 0, stream>>>(static_cast<aiko::bf16_t*>(x), B, rows, C);
   return (int)hipGetLastError();
 }

@@ -280,7 +280,7 @@ class FeatureSink(GpuPipelineElement):
                 "host": HostRing(lambda: torch.empty(B, d, dtype=torch.float32, pin_memory=pin), 8)}
         if self.device.type == "cuda":
             from ...ops.vision import mean_rows
-            mean_rows(features.contiguous(), out=b["pooled"])      # HIP reduction kernel
+            mean_rows(features, out=b["pooled"])     # HIP reduction kernel (reads the T-prefix view)
         else:
             torch.mean(features, dim=1, dtype=torch.float32, out=b["pooled"])
         slot, h = b["host"].acquire()

@@ -156,9 +156,12 @@ class WhisperEncoder(WeightsMixin):
         h1 = self._buf("h1", (B * rows1, d))
         M1 = B * rows1 - 2
         C.conv2d(mel.view(1, B * rows1, 1, N_MELS), self.conv1, out=h1[1:1 + M1].view(1, M1, 1, d))
-        h1v = h1.view(B, rows1, d)
-        h1v[:, 0].zero_()
-        h1v[:, rows1 - 1].zero_()
+        if h1.is_cuda:
+            torch.ops.aiko.zero_border_rows_(h1, rows1)     # per-clip zero border rows (one kernel)
+        else:
+            h1v = h1.view(B, rows1, d)
+            h1v[:, 0].zero_()
+            h1v[:, rows1 - 1].zero_()
         # conv2 (stride 2) + positional embedding -> residual stream x [B*Tp, d]
         x = self._buf("x", (B * Tp, d), zero=True)
         M2 = B * Tp - 1

@@ -55,7 +55,10 @@ def maxpool2d(x: torch.Tensor, k: int = 3, s: int = 2, p: int = 1,
 
 
 def mean_rows(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-    """``x.mean(dim=1)`` of bf16 ``[B, T, C]`` in fp32 ``[B, C]`` (HIP kernel, long T)."""
+    """``x.mean(dim=1)`` of bf16 ``[B, T, C]`` in fp32 ``[B, C]`` (HIP kernel, long T).  ``x`` may
+    be a T-prefix view of a longer buffer (contiguous rows, any batch pitch)."""
+    if x.stride(2) != 1 or x.stride(1) != x.shape[2]:
+        x = x.contiguous()
     if out is None:
         out = torch.empty(x.shape[0], x.shape[2], dtype=torch.float32, device=x.device)
     torch.ops.aiko.mean_rows_out(x, out)
