@@ -57,27 +57,33 @@ __device__ __forceinline__ void pre_pixel(const uint8_t* __restrict__ in, int b,
   normalize3(c, m0, m1, m2, is0, is1, is2, v0, v1, v2);
 }
 
-__global__ void preprocess_kernel(const uint8_t* __restrict__ in, bf16_t* __restrict__ out,
+// 2-D grid (x: pixels of one padded image, y: image): no 64-bit division of a flat index per
+// pixel (~100 VALU instructions each); the row is an exact float-reciprocal quotient with a
+// one-step integer fix-up.  Output bit-identical to the flat version (same pre_pixel).
+__global__ __launch_bounds__(256) void preprocess_kernel(const uint8_t* __restrict__ in, bf16_t* __restrict__ out,
                                   int B, int Hin, int Win, int Ho, int Wo, int Hp, int Wp,
                                   int pad_t, int pad_l, int Hc, int Wc, int off_t, int off_l,
                                   float fill, float m0, float m1, float m2,
                                   float is0, float is1, float is2, int bgr) {
-  const long total = (long)B * Hp * Wp;
-  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
-       idx += (long)gridDim.x * blockDim.x) {
-    const int b = idx / (Hp * Wp);
-    const int rem = idx - (long)b * Hp * Wp;
-    const int yp = rem / Wp;
+  const int b = blockIdx.y;
+  const int HW = Hp * Wp;
+  const float inv_wp = 1.f / (float)Wp;
+  const uint8_t* img = in + (long)b * Hin * Win * 3;
+  bf16_t* ob = out + (long)b * HW * 4;
+  for (int rem = blockIdx.x * blockDim.x + threadIdx.x; rem < HW; rem += gridDim.x * blockDim.x) {
+    int yp = (int)(((float)rem + 0.5f) * inv_wp);
+    if (yp * Wp > rem) --yp;
+    else if ((yp + 1) * Wp <= rem) ++yp;
     const int xp = rem - yp * Wp;
     const int yc = yp - pad_t, xc = xp - pad_l;
     uint2 o = {0u, 0u};
     if (yc >= 0 && yc < Hc && xc >= 0 && xc < Wc) {
       float v0, v1, v2;
-      pre_pixel(in, b, Hin, Win, Ho, Wo, off_t, off_l, yc, xc, fill, m0, m1, m2, is0, is1, is2, bgr, v0, v1, v2);
+      pre_pixel(img, 0, Hin, Win, Ho, Wo, off_t, off_l, yc, xc, fill, m0, m1, m2, is0, is1, is2, bgr, v0, v1, v2);
       o.x = pack2(v0, v1);
       o.y = pack2(v2, 0.f);
     }
-    *reinterpret_cast<uint2*>(out + idx * 4) = o;
+    *reinterpret_cast<uint2*>(ob + (long)rem * 4) = o;
   }
 }
 
@@ -404,8 +410,11 @@ extern "C" int aiko_preprocess(const void* in, void* out, int B, int Hin, int Wi
                                int Wo, int Hp, int Wp, int pad_t, int pad_l, int Hc, int Wc,
                                int off_t, int off_l, float fill, const float* mean,
                                const float* std, int bgr, hipStream_t stream) {
-  const long total = (long)B * Hp * Wp;
-  hipLaunchKernelGGL(aiko::preprocess_kernel, dim3(grid_for(total, 256)), dim3(256), 0, stream,
+  if (B <= 0 || B > 65535 || Hp <= 0 || Wp <= 0) return -1;
+  const long per_img = (long)Hp * Wp;
+  long gx = (per_img + 255) / 256;
+  if (gx > 1024) gx = 1024;
+  hipLaunchKernelGGL(aiko::preprocess_kernel, dim3((unsigned)gx, (unsigned)B), dim3(256), 0, stream,
                      static_cast<const uint8_t*>(in), static_cast<aiko::bf16_t*>(out), B, Hin,
                      Win, Ho, Wo, Hp, Wp, pad_t, pad_l, Hc, Wc, off_t, off_l, fill, mean[0],
                      mean[1], mean[2], 1.f / std[0], 1.f / std[1], 1.f / std[2], bgr);
