@@ -1,6 +1,6 @@
 """Host-side decision logic of the GPU paths (no GPU needed): which ResNet-50 block boundaries
 the chained 1x1 kernel takes, Whisper token -> text rendering and the reference's speech reply
-filter, the decode-attention workspace size."""
+filter, the decode-attention workspace size, narrow-kernel eligibility, the host window shift."""
 import torch
 
 from aiko_services_amd.ops import conv as C
@@ -86,3 +86,30 @@ def test_stage_link_requires_two_slots():
     with pytest.raises(ValueError):
         StageLink(1, "cpu", depth=1)
     assert StageLink(1, "cpu", depth=2).depth == 2
+
+
+def test_narrow_variant_eligibility():
+    """The direct narrow-layer kernel (tuner variant 7) is offered exactly for 3x3 / pad 1 /
+    stride 1-2 and 1x1 / stride 1 convs with 16 or 32 input and output channels."""
+    g = torch.Generator().manual_seed(1)
+
+    def conv(cout, cin, k, stride=1):
+        return C.make_conv_spec(torch.randn(cout, cin, k, k, generator=g), None, stride=stride, pad=k // 2, act="silu")
+    assert C.narrow_variant_ok(conv(16, 16, 3))
+    assert C.narrow_variant_ok(conv(32, 16, 3, stride=2))
+    assert C.narrow_variant_ok(conv(32, 32, 1))
+    assert not C.narrow_variant_ok(conv(32, 32, 1, stride=2))          # 1x1 only at stride 1
+    assert not C.narrow_variant_ok(conv(64, 32, 3))                    # Cout 64: buffer-DMA kernels
+    assert not C.narrow_variant_ok(conv(32, 48, 3))                    # Cc 48
+    assert not C.narrow_variant_ok(conv(32, 32, 5))                    # 5x5
+    assert not C.narrow_variant_ok(conv(16, 16, 3), x2=torch.zeros(1))  # second source
+
+
+def test_window_shift_cpu_path():
+    """ops.audio.window_shift on host tensors: the AudioWindow update dst = src[:, n:] ++ chunk."""
+    from aiko_services_amd.ops.audio import window_shift
+    src = torch.arange(2 * 12, dtype=torch.float32).view(2, 12)
+    chunk = -torch.arange(2 * 4, dtype=torch.float32).view(2, 4) - 1
+    dst = torch.empty_like(src)
+    window_shift(src, chunk, dst)
+    assert torch.equal(dst, torch.cat([src[:, 4:], chunk], 1))
