@@ -700,13 +700,48 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_big_kernel(Fp8GemmParams p, c
 //   z = gamma ? (x - mean) * rstd * gamma + beta : x
 //   yb (optional) = bf16(z);  q (optional) = e4m3(z / s), s = amax(|z|) / 448 per row.
 // Rows are read once with 16-byte loads and kept in registers (D <= 64 * 8 * MAXC).
-template <int MAXC>
+// sum / max over a row's lane group: the whole wave (HALF = 0) or a 32-lane half (HALF = 1:
+// DPP steps inside 16-lane rows, then v_permlane16_swap pairs rows 0-1 and 2-3 only)
+template <int HALF>
+__device__ __forceinline__ float group_sum(float v) {
+  if constexpr (HALF == 0) {
+    return wave_sum(v);
+  } else {
+    auto add = [](float x, float y) { return x + y; };
+    v = add(v, dpp_f32<0xB1>(v));
+    v = add(v, dpp_f32<0x4E>(v));
+    v = add(v, dpp_f32<0x141>(v));
+    v = add(v, dpp_f32<0x140>(v));
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return add(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  }
+}
+
+template <int HALF>
+__device__ __forceinline__ float group_max(float v) {
+  if constexpr (HALF == 0) {
+    return wave_max(v);
+  } else {
+    auto mx = [](float x, float y) { return fmaxf(x, y); };
+    v = mx(v, dpp_f32<0xB1>(v));
+    v = mx(v, dpp_f32<0x4E>(v));
+    v = mx(v, dpp_f32<0x141>(v));
+    v = mx(v, dpp_f32<0x140>(v));
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return mx(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  }
+}
+
+// HALF = 1: two rows per wave, 32 lanes each (D <= 768: 96 chunks = 32 lanes x 3, no idle lanes
+// in a second pass), reductions inside the 32-lane half
+template <int MAXC, int HALF = 0>
 __global__ __launch_bounds__(256) void rownorm_quant_kernel(
     const bf16_t* __restrict__ x, int ldx, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, bf16_t* __restrict__ yb, int ldyb,
     uint8_t* __restrict__ q, int ldq, float* __restrict__ qs, int M, int D) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  constexpr int G = 64 >> HALF;                  // lanes per row
+  const int lane = threadIdx.x & (G - 1);
+  const int row = blockIdx.x * (4 << HALF) + (threadIdx.x >> (6 - HALF));
   if (row >= M) return;
   const int nchunk = D >> 3;
   const bf16_t* src = x + (long)row * ldx;
@@ -714,7 +749,7 @@ __global__ __launch_bounds__(256) void rownorm_quant_kernel(
   float s = 0.f;
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
-    const int ch = lane + 64 * c;
+    const int ch = lane + G * c;
     if (ch < nchunk) {
       const u32x4 u = *reinterpret_cast<const u32x4*>(src + ch * 8);
 #pragma unroll
@@ -730,11 +765,11 @@ __global__ __launch_bounds__(256) void rownorm_quant_kernel(
     for (int e = 0; e < 8; ++e) s += v[c][e];
   }
   if (gamma) {
-    const float mean = wave_sum(s) / D;
+    const float mean = group_sum<HALF>(s) / D;
     float ss = 0.f;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
-      if (lane + 64 * c < nchunk) {
+      if (lane + G * c < nchunk) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float d = v[c][e] - mean;
@@ -742,10 +777,10 @@ __global__ __launch_bounds__(256) void rownorm_quant_kernel(
         }
       }
     }
-    const float rstd = rsqrtf(wave_sum(ss) / D + eps);
+    const float rstd = rsqrtf(group_sum<HALF>(ss) / D + eps);
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
-      const int ch = lane + 64 * c;
+      const int ch = lane + G * c;
       if (ch < nchunk) {
 #pragma unroll
         for (int e = 0; e < 8; ++e)
@@ -756,7 +791,7 @@ __global__ __launch_bounds__(256) void rownorm_quant_kernel(
   if (yb) {
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
-      const int ch = lane + 64 * c;
+      const int ch = lane + G * c;
       if (ch < nchunk) {
         u32x4 o;
 #pragma unroll
@@ -769,17 +804,17 @@ __global__ __launch_bounds__(256) void rownorm_quant_kernel(
     float amax = 0.f;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c)
-      if (lane + 64 * c < nchunk) {
+      if (lane + G * c < nchunk) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[c][e]));
       }
-    amax = wave_max(amax);
+    amax = group_max<HALF>(amax);
     const float scale = amax > 0.f ? amax / 448.f : 1.f;
     const float inv = 1.f / scale;
-    if (lane == 0) qs[row] = scale;
+    if (lane == 0) qs[row] = scale;        // lane = index inside the row's group
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
-      const int ch = lane + 64 * c;
+      const int ch = lane + G * c;
       if (ch < nchunk) {
         unsigned w0 = 0u, w1 = 0u;
         w0 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[c][0] * inv, -448.f), 448.f),
@@ -885,6 +920,11 @@ extern "C" int aiko_rownorm_quant(const void* x, int ldx, const float* gamma, co
   const bf16_t* xp = static_cast<const bf16_t*>(x);
   bf16_t* yp = static_cast<bf16_t*>(yb);
   uint8_t* qp = static_cast<uint8_t*>(q);
+  if (D <= 32 * 8 * 3) {               // 2 rows per wave, 32 lanes x <= 3 chunks each
+    rownorm_quant_kernel<3, 1><<<dim3((M + 7) / 8), block, 0, stream>>>(xp, ldx, gamma, beta, eps, yp, ldyb, qp, ldq,
+                                                                       qs, M, D);
+    return (int)hipGetLastError();
+  }
   if (D <= 64 * 8 * 2) {
     rownorm_quant_kernel<2><<<grid, block, 0, stream>>>(xp, ldx, gamma, beta, eps, yp, ldyb, qp, ldq, qs, M, D);
   } else if (D <= 64 * 8 * 6) {

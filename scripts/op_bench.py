@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run one op repeatedly at Whisper-small encoder shapes (for rocprofv3 --pmc / timing).
 
-    python scripts/op_bench.py attn|gemm_qkv|gemm_fc1|gemm_fc2|gemm_out|fc1_gelu_mx [--batch 16] [--iters 20]
+    python scripts/op_bench.py attn|rownorm|gemm_qkv|gemm_fc1|gemm_fc2|gemm_out|fc1_gelu_mx [--batch 16] [--iters 20]
 fc1_gelu_mx is the encoder's fc1 as run: GELU + MX-fp8 output quantisation in the epilogue.
 """
 import argparse
@@ -25,7 +25,15 @@ def main():
     dev = "cuda"
     B, T, Tp, H, d = a.batch, 1500, 1501, 12, 768
     M = B * Tp
-    if a.op == "attn":
+    if a.op == "rownorm":
+        x = torch.randn(M, d, device=dev).to(torch.bfloat16)
+        gamma = torch.rand(d, device=dev) + 0.5
+        beta = torch.randn(d, device=dev) * 0.1
+        q8 = torch.empty(M, d, dtype=torch.uint8, device=dev)
+        s8 = torch.empty(M, dtype=torch.float32, device=dev)
+        fn = lambda: TR.rownorm(x, gamma, beta, q=q8, qs=s8)  # noqa: E731
+        flops = 0
+    elif a.op == "attn":
         qkv = (torch.randn(M, 3 * d, device=dev) * 1.5).to(torch.bfloat16)
         out = torch.empty(M, d, dtype=torch.bfloat16, device=dev)
         fn = lambda: TR.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], out, B, H, T, Tp, 0.125)  # noqa: E731
@@ -57,7 +65,10 @@ def main():
     e1.record()
     e1.synchronize()
     us = e0.elapsed_time(e1) / a.iters * 1e3
-    print(f"{a.op}: {us:.1f} us  {flops / us / 1e6:.1f} TFLOP/s", flush=True)
+    if flops:
+        print(f"{a.op}: {us:.1f} us  {flops / us / 1e6:.1f} TFLOP/s", flush=True)
+    else:
+        print(f"{a.op}: {us:.1f} us", flush=True)
 
 
 if __name__ == "__main__":
