@@ -147,7 +147,7 @@ struct NmsParams {
   float gain, pad_l, pad_t, img_w, img_h;  // letterbox -> frame mapping
   float* det;   // [B, max_det, 6]
   int* count;   // [B]
-  int stop;     // unused (kept for layout)
+  int stop;     // profiling: end the kernels early at phase `stop` (99 = run everything)
 };
 
 __device__ __forceinline__ unsigned long long shfl64(unsigned long long v, int src) {
@@ -681,8 +681,11 @@ extern "C" int aiko_topk_nms(const void* boxes, const float* scores, const int* 
   p.gain = gain; p.pad_l = pad_l; p.pad_t = pad_t; p.img_w = img_w; p.img_h = img_h;
   p.det = det;
   p.count = count;
-  p.stop = 99;
-  if (const char* e = getenv("AIKO_NMS_STOP")) p.stop = atoi(e);
+  static const int stop = [] {                  // profiling hook (scripts/nms_stop.sh), read once
+    const char* e = getenv("AIKO_NMS_STOP");
+    return e ? atoi(e) : 99;
+  }();
+  p.stop = stop;
   char* w = static_cast<char*>(workspace);
   aiko::NmsWork ws;
   ws.mask = reinterpret_cast<unsigned long long*>(w);
