@@ -240,7 +240,22 @@ __global__ void avgpool_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict_
     const int b = idx / C8;
     float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const bf16_t* src = x + (long)b * HW * C + c8 * 8;
-    for (int i = 0; i < HW; ++i) {
+    // 7 rows' loads in flight per step (one wave per SIMD at ResNet's 256 x 2048 / 8 threads:
+    // a load -> add chain per row was latency-bound); same summation order as row by row
+    int i = 0;
+    for (; i + 7 <= HW; i += 7) {
+      u32x4 v[7];
+#pragma unroll
+      for (int u = 0; u < 7; ++u) v[u] = *reinterpret_cast<const u32x4*>(src + (long)(i + u) * C);
+#pragma unroll
+      for (int u = 0; u < 7; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[2 * e] += __uint_as_float(v[u][e] << 16);
+          a[2 * e + 1] += __uint_as_float(v[u][e] & 0xffff0000u);
+        }
+    }
+    for (; i < HW; ++i) {
       const u32x4 v = *reinterpret_cast<const u32x4*>(src + (long)i * C);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {

@@ -1,0 +1,13 @@
+import sys, os
+sys.path.insert(0, os.getcwd())
+import torch
+from aiko_services_amd.ops import vision as V, require_native
+require_native()
+x = torch.randn(256, 7, 7, 2048, device="cuda").to(torch.bfloat16)
+for _ in range(3): V.avgpool(x)
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for _ in range(20): y = V.avgpool(x)
+e1.record(); torch.cuda.synchronize()
+print(f"avgpool: {e0.elapsed_time(e1)/20*1e3:.1f} us  exact={torch.equal(y.float(), x.float().mean((1,2)).to(torch.bfloat16).float()) }")
