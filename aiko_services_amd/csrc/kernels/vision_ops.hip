@@ -298,27 +298,37 @@ __global__ void softmax_topk_kernel(const bf16_t* __restrict__ logits, float* __
   }
   s = wave_sum(s);
   const float inv = 1.f / s;
+  // Each round's arg-max is one unsigned wave max over 32-bit keys: the logit's bf16 bits mapped
+  // to an order-preserving code (high half; -0 folded onto +0) and 0xFFFF - column (low half), so
+  // ties go to the lower column exactly as the (value, index) compare did.  Logits come from bf16,
+  // so the key holds the value exactly; N <= 2048 fits the low half.  A taken column's key becomes
+  // the key of -INF at that column, i.e. what setting its value to -INF gave.
+  unsigned key[PER_LANE];
+#pragma unroll
+  for (int i = 0; i < PER_LANE; ++i) {
+    unsigned b = __float_as_uint(v[i]) >> 16;
+    if (b == 0x8000u) b = 0;
+    const unsigned ord = (b & 0x8000u) ? (~b & 0xFFFFu) : (b | 0x8000u);
+    key[i] = (ord << 16) | (0xFFFFu - (unsigned)(lane + 64 * i));
+  }
+  const auto umax = [](float x, float y) {
+    return __uint_as_float(max(__float_as_uint(x), __float_as_uint(y)));
+  };
   for (int t = 0; t < k; ++t) {
-    float best = -INFINITY;
-    int bi = 0x7fffffff;
+    unsigned best = 0;
 #pragma unroll
-    for (int i = 0; i < PER_LANE; ++i) {
-      const int c = lane + 64 * i;
-      if (v[i] > best || (v[i] == best && c < bi)) { best = v[i]; bi = c; }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ob = __shfl_xor(best, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-    }
+    for (int i = 0; i < PER_LANE; ++i) best = max(best, key[i]);
+    best = __float_as_uint(wave_reduce(__uint_as_float(best), umax));
+    const int bi = 0xFFFF - (int)(best & 0xFFFFu);
+    const unsigned ord = best >> 16;
+    const unsigned b = (ord & 0x8000u) ? (ord & 0x7FFFu) : (~ord & 0xFFFFu);
     if (lane == 0) {
-      prob[(long)row * k + t] = __expf(best - mx) * inv;
+      prob[(long)row * k + t] = __expf(__uint_as_float(b << 16) - mx) * inv;
       index[(long)row * k + t] = bi;
     }
 #pragma unroll
     for (int i = 0; i < PER_LANE; ++i)
-      if (lane + 64 * i == bi) v[i] = -INFINITY;
+      if (lane + 64 * i == bi) key[i] = (0x007Fu << 16) | (0xFFFFu - (unsigned)bi);
   }
 }
 

@@ -205,6 +205,23 @@ def test_pools_and_topk(native):
     assert torch.allclose(p, rp, rtol=1e-3, atol=1e-5)
 
 
+@pytest.mark.parametrize("N,k", [(10, 8), (1000, 5), (2000, 7)])
+def test_softmax_topk_exact_ties(native, N, k):
+    """Packed-key arg-max: ties (incl. -0 vs +0) go to the lower column, like a stable sort."""
+    from aiko_services_amd.ops import vision as V
+    g = torch.Generator().manual_seed(N)
+    lg = torch.randint(-4, 5, (19, N), generator=g).float()
+    lg[:, ::3] *= -0.0   # every third column becomes +0 or -0
+    lg = lg.to(torch.bfloat16)
+    p, i = V.softmax_topk(lg.to(DEV), k)
+    torch.cuda.synchronize()
+    order = torch.stack([torch.tensor(sorted(range(N), key=lambda c: (-float(r[c]), c)))
+                         for r in lg.float()])[:, :k]
+    assert torch.equal(i.cpu().long(), order)
+    rp = torch.softmax(lg.float(), -1).gather(1, order)
+    assert torch.allclose(p.cpu(), rp, rtol=1e-4, atol=1e-6)
+
+
 def test_resnet50_matches_fp32_reference(native):
     from aiko_services_amd.models.resnet50 import ResNet50
     m = ResNet50(seed=0, device=DEV)
