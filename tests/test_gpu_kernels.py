@@ -172,6 +172,29 @@ def test_preprocess_resize(native):
     assert _rel_err(pre[:, 3:227, 3:227, :3].permute(0, 3, 1, 2), ref) < 1e-2
 
 
+@pytest.mark.parametrize("H,W,bgr", [(224, 224, False), (36, 100, True)])
+def test_preprocess_rows_fast_path_exact(native, H, W, bgr):
+    """No-resize frames take preprocess_rows_kernel (dword loads, a wave per row); the same
+    frames at a 1-byte-offset base take the flat kernel.  Outputs must be bit-identical and the
+    zero border must be written over whatever the buffer held."""
+    from aiko_services_amd.ops import conv as C
+    from aiko_services_amd.ops import vision as V
+    g = torch.Generator().manual_seed(H + W)
+    B = 3
+    flat = torch.randint(0, 256, (B * H * W * 3 + 1,), generator=g, dtype=torch.uint8).to(DEV)
+    odd = flat[1:].view(B, H, W, 3)                 # base % 4 == 1 -> flat kernel
+    even = odd.clone()                              # aligned -> row kernel
+    Hp, Wp = C.stem_geometry(H, W)
+    outs = []
+    for fr in (odd, even):
+        out = torch.full((B, Hp, Wp, 4), 7.0, dtype=torch.bfloat16, device=DEV)
+        outs.append(V.preprocess_frames(fr, (H, W), bgr=bgr, out=out))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
+    assert outs[1][:, :3].abs().max().item() == 0 and outs[1][..., 3].abs().max().item() == 0
+    assert outs[1][:, :, :3].abs().max().item() == 0 and outs[1][:, :, 3 + W:].abs().max().item() == 0
+
+
 def test_linear_with_n_tail(native):
     from aiko_services_amd.ops import conv as C
     from aiko_services_amd.ops import reference as R
