@@ -206,18 +206,23 @@ class ClassifierTopK(GpuPipelineElement):
         self.gather = str(gather).lower() in ("true", "1", "yes")
         self._bufs = {}
 
+    @staticmethod
+    def _split(flat, rows, k):
+        """(prob fp32 [rows, k], index int32 [rows, k]) as contiguous views of one int32 buffer,
+        so the per-step device->host result copy is a single transfer."""
+        n = rows * k
+        return flat[:n].view(torch.float32).view(rows, k), flat[n:].view(rows, k)
+
     def _buffers(self, B, world):
         key = (B, world, self.lane)
         b = self._bufs.get(key)
         if b is None:
-            dev = self.device
-            b = {"prob": torch.empty(B, self.k, dtype=torch.float32, device=dev),
-                 "index": torch.empty(B, self.k, dtype=torch.int32, device=dev),
-                 "all_prob": torch.empty(world * B, self.k, dtype=torch.float32, device=dev),
-                 "all_index": torch.empty(world * B, self.k, dtype=torch.int32, device=dev),
-                 "host": HostRing(lambda: (
-                     torch.empty(world * B, self.k, dtype=torch.float32, pin_memory=dev.type == "cuda"),
-                     torch.empty(world * B, self.k, dtype=torch.int32, pin_memory=dev.type == "cuda")), 8)}
+            dev, k = self.device, self.k
+            pin = dev.type == "cuda"
+            b = {"dev": torch.empty(2 * B * k, dtype=torch.int32, device=dev),
+                 "all": torch.empty(2 * world * B * k, dtype=torch.int32, device=dev),
+                 "host": HostRing(lambda: torch.empty(2 * world * B * k, dtype=torch.int32,
+                                                      pin_memory=pin), 8)}
             self._bufs[key] = b
         return b
 
@@ -227,14 +232,17 @@ class ClassifierTopK(GpuPipelineElement):
         B = logits.shape[0]
         world = D.world_size() if self.gather else 1
         b = self._buffers(B, world)
-        prob, index = V.softmax_topk(logits, self.k, prob=b["prob"], index=b["index"])
+        prob, index = self._split(b["dev"], B, self.k)
+        V.softmax_topk(logits, self.k, prob=prob, index=index)
+        flat = b["dev"]
         if world > 1:
-            D.all_gather_into(b["all_prob"], prob)
-            D.all_gather_into(b["all_index"], index)
-            prob, index = b["all_prob"], b["all_index"]
-        slot, (hp, hi) = b["host"].acquire()
-        hp.copy_(prob, non_blocking=True)
-        hi.copy_(index, non_blocking=True)
+            all_prob, all_index = self._split(b["all"], world * B, self.k)
+            D.all_gather_into(all_prob, prob)
+            D.all_gather_into(all_index, index)
+            flat = b["all"]
+        slot, host = b["host"].acquire()
+        host.copy_(flat, non_blocking=True)
+        hp, hi = self._split(host, world * B, self.k)
         ev = None
         if self.device.type == "cuda":
             ev = torch.cuda.Event()
