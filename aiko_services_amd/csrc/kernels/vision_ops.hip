@@ -524,24 +524,28 @@ extern "C" int aiko_maxpool(const void* x, void* y, int B, int H, int W, int C, 
 
 namespace aiko {
 // Mean over the rows of [B, T, C] bf16 -> [B, C] fp32 (Whisper feature pooling, long T): one
-// 256-thread block per (batch, 256 channels); 8 row phases x 32 lanes of 8 channels, each lane
-// keeping 4 row loads in flight, then an LDS reduction of the 8 phases.
+// 256-thread block per (batch, CL x 8 channels); 256/CL row phases x CL lanes of 8 channels, each
+// lane keeping 4 row loads in flight, then an LDS reduction of the phases in a fixed order.
+// CL = 32 (512 B of each row per block) when B x C/256 blocks fill the chip; CL = 8 (one 128 B
+// line per row) otherwise -- Whisper-small's [16, 1500, 768] gets 192 blocks instead of 48.
+template <int CL>
 __global__ __launch_bounds__(256) void mean_rows_f32_kernel(const bf16_t* __restrict__ x,
                                                             float* __restrict__ y, int T, int C,
                                                             long ldb) {
-  __shared__ float red[8][32][9];
-  const int cl = threadIdx.x & 31, ph = threadIdx.x >> 5;
+  constexpr int PH = 256 / CL;
+  __shared__ float red[PH][CL][9];
+  const int cl = threadIdx.x % CL, ph = threadIdx.x / CL;
   const int C8 = C >> 3;
-  const int c8 = blockIdx.x * 32 + cl;
+  const int c8 = blockIdx.x * CL + cl;
   const int b = blockIdx.y;
   float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (c8 < C8) {
     const bf16_t* src = x + (long)b * ldb + c8 * 8;      // ldb: batch pitch (rows may be a T-prefix)
     int i = ph;
-    for (; i + 24 < T; i += 32) {
+    for (; i + 3 * PH < T; i += 4 * PH) {
       u32x4 v[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const u32x4*>(src + (long)(i + 8 * u) * C);
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const u32x4*>(src + (long)(i + PH * u) * C);
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -550,7 +554,7 @@ __global__ __launch_bounds__(256) void mean_rows_f32_kernel(const bf16_t* __rest
           a[2 * e + 1] += __uint_as_float(v[u][e] & 0xffff0000u);
         }
     }
-    for (; i < T; i += 8) {
+    for (; i < T; i += PH) {
       const u32x4 v = *reinterpret_cast<const u32x4*>(src + (long)i * C);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -569,7 +573,7 @@ __global__ __launch_bounds__(256) void mean_rows_f32_kernel(const bf16_t* __rest
     for (int e = 0; e < 8; ++e) {
       float t = 0.f;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) t += red[q][cl][e];
+      for (int q = 0; q < PH; ++q) t += red[q][cl][e];
       o[e] = t * inv;
     }
     float* dst = y + (long)b * C + c8 * 8;
@@ -595,8 +599,13 @@ __global__ __launch_bounds__(256) void zero_border_rows_kernel(bf16_t* __restric
 
 extern "C" int aiko_mean_rows_f32(const void* x, float* y, int B, int T, int C, long ldb, hipStream_t stream) {
   if (C % 8 || T < 1 || ldb < (long)T * C) return -1;
-  dim3 grid((C / 8 + 31) / 32, B);
-  aiko::mean_rows_f32_kernel<<<grid, 256, 0, stream>>>(static_cast<const aiko::bf16_t*>(x), y, T, C, ldb);
+  const aiko::bf16_t* xp = static_cast<const aiko::bf16_t*>(x);
+  const int C8 = C / 8;
+  if ((long)B * ((C8 + 31) / 32) < 256) {
+    aiko::mean_rows_f32_kernel<8><<<dim3((C8 + 7) / 8, B), 256, 0, stream>>>(xp, y, T, C, ldb);
+  } else {
+    aiko::mean_rows_f32_kernel<32><<<dim3((C8 + 31) / 32, B), 256, 0, stream>>>(xp, y, T, C, ldb);
+  }
   return (int)hipGetLastError();
 }
 

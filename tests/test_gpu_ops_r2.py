@@ -5,7 +5,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("B,T,C", [(16, 1500, 768), (3, 7, 64), (2, 33, 520)])
+@pytest.mark.parametrize("B,T,C", [(16, 1500, 768), (3, 7, 64), (2, 33, 520), (64, 41, 1032)])
 def test_mean_rows_f32(native, B, T, C):
     from aiko_services_amd.ops.vision import mean_rows
     x = torch.randn(B, T, C, device="cuda").to(torch.bfloat16)
