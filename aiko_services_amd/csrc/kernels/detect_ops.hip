@@ -66,6 +66,7 @@ constexpr int kRegMax = 16;   // DFL bins per box side (YOLOv8)
 struct DecodeParams {
   const bf16_t* feat[kMaxLevels];  // [B, H, W, ld] bf16: box logits [0, 4*reg_max), cls after
   int H[kMaxLevels], W[kMaxLevels], stride[kMaxLevels], ld[kMaxLevels], start[kMaxLevels];
+  int tstart[kMaxLevels];          // first 64-anchor tile of each level (tiled kernel)
   int nlev, B, A, nc, reg_max;
   float4* boxes;   // [B, A]
   float* scores;   // [B, A]
@@ -127,6 +128,97 @@ __global__ void yolo_decode_kernel(DecodeParams p) {
     const float ax = w + 0.5f, ay = h + 0.5f;
     p.boxes[idx] = make_float4((ax - dist[0]) * s, (ay - dist[1]) * s, (ax + dist[2]) * s,
                                (ay + dist[3]) * s);
+    p.scores[idx] = 1.f / (1.f + __expf(-best));
+    p.cls[idx] = bi;
+  }
+}
+
+// Coalesced variant: a 256-thread block takes 64 consecutive anchors of one level of one image
+// (blockIdx.y = image, blockIdx.x = tile; tiles never straddle levels), copies their rows
+// (contiguous [64, ld] in memory) into LDS with 16-byte loads, then a quad of lanes decodes each
+// anchor: lane j takes DFL side j and class chunks j, j+4, j+8 (8 classes each), combined with
+// quad DPP (max value, lowest index on ties).  The per-anchor thread version above reads 16 B at
+// a 288 B lane stride, touching 64 lines per load instruction.  Same per-side arithmetic in the
+// same order and an exact max, so the outputs are bit-identical to it.
+template <int Q>
+__device__ __forceinline__ int dpp_i32(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, Q, 0xF, 0xF, false);
+}
+
+__global__ __launch_bounds__(256) void yolo_decode_tiled_kernel(DecodeParams p) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t rows[];
+  const int CH = 4 * kRegMax + p.nc, CHP = CH + 8, NCH = CH >> 3;
+  const int b = blockIdx.y;
+  int l = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxLevels; ++i)
+    if (i < p.nlev && (int)blockIdx.x >= p.tstart[i]) l = i;
+  const int HW = p.H[l] * p.W[l];
+  const int r0 = ((int)blockIdx.x - p.tstart[l]) * 64;
+  const int n = min(64, HW - r0);
+  const bf16_t* src = p.feat[l] + ((long)b * HW + r0) * p.ld[l];
+  for (int i = threadIdx.x; i < n * NCH; i += 256) {
+    const int row = i / NCH, ch = i - row * NCH;
+    *reinterpret_cast<u32x4*>(rows + row * CHP + ch * 8) =
+        *reinterpret_cast<const u32x4*>(src + (long)row * p.ld[l] + ch * 8);
+  }
+  __syncthreads();
+  const int j = threadIdx.x & 3, ai = threadIdx.x >> 2;
+  const bool live = ai < n;
+  const bf16_t* f = rows + (live ? ai : 0) * CHP;
+  float v[kRegMax];
+#pragma unroll
+  for (int k = 0; k < kRegMax; k += 8) {
+    const u32x4 u = *reinterpret_cast<const u32x4*>(f + j * kRegMax + k);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[k + 2 * e] = __uint_as_float(u[e] << 16);
+      v[k + 2 * e + 1] = __uint_as_float(u[e] & 0xffff0000u);
+    }
+  }
+  float m = v[0];
+#pragma unroll
+  for (int k = 1; k < kRegMax; ++k) m = fmaxf(m, v[k]);
+  float se = 0.f, sk = 0.f;
+#pragma unroll
+  for (int k = 0; k < kRegMax; ++k) {
+    const float e = __expf(v[k] - m);
+    se += e;
+    sk += e * k;
+  }
+  const float dist = sk / se;
+  const bf16_t* c = f + 4 * kRegMax;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int k = 8 * j; k < p.nc; k += 32) {
+    const u32x4 u = *reinterpret_cast<const u32x4*>(c + k);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float v0 = __uint_as_float(u[e] << 16), v1 = __uint_as_float(u[e] & 0xffff0000u);
+      if (v0 > best) { best = v0; bi = k + 2 * e; }
+      if (v1 > best) { best = v1; bi = k + 2 * e + 1; }
+    }
+  }
+  {
+    const float ob = dpp_f32<0xB1>(best);
+    const int oi = dpp_i32<0xB1>(bi);
+    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+  }
+  {
+    const float ob = dpp_f32<0x4E>(best);
+    const int oi = dpp_i32<0x4E>(bi);
+    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+  }
+  if (bi == 0x7fffffff) bi = 0;       // no logit above -INF: class 0, as the sequential scan gives
+  const float d0 = dpp_f32<0x00>(dist), d1 = dpp_f32<0x55>(dist);
+  const float d2 = dpp_f32<0xAA>(dist), d3 = dpp_f32<0xFF>(dist);
+  if (live && j == 0) {
+    const int r = r0 + ai;
+    const int h = r / p.W[l], w = r - h * p.W[l];
+    const float s = (float)p.stride[l];
+    const float ax = w + 0.5f, ay = h + 0.5f;
+    const long idx = (long)b * p.A + p.start[l] + r;
+    p.boxes[idx] = make_float4((ax - d0) * s, (ay - d1) * s, (ax + d2) * s, (ay + d3) * s);
     p.scores[idx] = 1.f / (1.f + __expf(-best));
     p.cls[idx] = bi;
   }
@@ -643,8 +735,15 @@ extern "C" int aiko_yolo_decode(const void* const* feats, const int* H, const in
                                 hipStream_t stream) {
   if (nlev < 1 || nlev > aiko::kMaxLevels || reg_max != aiko::kRegMax || nc % 8) return -1;
   aiko::DecodeParams p;
-  int A = 0;
+  int A = 0, tiles = 0;
+  bool tiled = (4 * aiko::kRegMax + nc) * 2 * 64 + 16 * 64 <= 64 * 1024;
   for (int i = 0; i < aiko::kMaxLevels; ++i) {
+    p.tstart[i] = tiles;
+    if (i < nlev) {
+      tiles += (H[i] * W[i] + 63) / 64;
+      tiled = tiled && ld[i] % 8 == 0 && ld[i] >= 4 * aiko::kRegMax + nc &&
+              reinterpret_cast<uintptr_t>(feats[i]) % 16 == 0;
+    }
     p.feat[i] = i < nlev ? static_cast<const aiko::bf16_t*>(feats[i]) : nullptr;
     p.H[i] = i < nlev ? H[i] : 0;
     p.W[i] = i < nlev ? W[i] : 1;
@@ -657,6 +756,13 @@ extern "C" int aiko_yolo_decode(const void* const* feats, const int* H, const in
   p.boxes = static_cast<float4*>(boxes);
   p.scores = scores;
   p.cls = cls;
+  // AIKO_DECODE_FLAT=1 selects the per-anchor kernel (read per call: the exactness test flips it)
+  const char* flat = getenv("AIKO_DECODE_FLAT");
+  if (tiled && B <= 65535 && !(flat && flat[0] == '1')) {
+    const size_t lds = (size_t)64 * (4 * aiko::kRegMax + nc + 8) * sizeof(aiko::bf16_t);
+    aiko::yolo_decode_tiled_kernel<<<dim3(tiles, B), 256, lds, stream>>>(p);
+    return (int)hipGetLastError();
+  }
   aiko::yolo_decode_kernel<<<grid_for_d((long)B * A, 256), 256, 0, stream>>>(p);
   return (int)hipGetLastError();
 }

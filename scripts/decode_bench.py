@@ -1,0 +1,37 @@
+#!/usr/bin/env python3
+"""Time the YOLOv8 DFL decode at the bench's head shapes (B=64, 640x640: 80/40/20 levels, 144 ch):
+LDS-tiled kernel vs the per-anchor kernel (AIKO_DECODE_FLAT=1), same inputs, outputs compared."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+
+def timed(fn, n=20):
+    for _ in range(3):
+        out = fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        out = fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n * 1e3, out
+
+
+def main():
+    from aiko_services_amd.ops import detect as DT, require_native
+    require_native()
+    feats = [torch.randn(64, s, s, 144, device="cuda").to(torch.bfloat16) for s in (80, 40, 20)]
+    fn = lambda: DT.yolo_decode(feats, (8, 16, 32), 80)  # noqa: E731
+    t_tiled, a = timed(fn)
+    os.environ["AIKO_DECODE_FLAT"] = "1"
+    t_flat, b = timed(fn)
+    same = all(torch.equal(x, y) for x, y in zip(a, b))
+    print(f"yolo_decode B=64: tiled {t_tiled:.1f} us, per-anchor {t_flat:.1f} us, identical={same}")
+
+
+if __name__ == "__main__":
+    main()

@@ -80,6 +80,22 @@ def test_yolo_decode(native):
     assert (cls == rc).float().mean().item() > 0.999
 
 
+def test_yolo_decode_tiled_matches_per_anchor(native, monkeypatch):
+    """The LDS-tiled decode and the per-anchor kernel (AIKO_DECODE_FLAT=1) give bit-identical
+    boxes / scores / classes, incl. a partial last tile (5x5 = 25 anchors) and exact ties among
+    class logits."""
+    from aiko_services_amd.ops import detect as DT
+    g = torch.Generator().manual_seed(9)
+    feats = [(torch.randn(3, s, s, 144, generator=g) * 3).round().to(torch.bfloat16).to(DEV)
+             for s in (20, 10, 5)]
+    tiled = DT.yolo_decode(feats, (8, 16, 32), 80)
+    monkeypatch.setenv("AIKO_DECODE_FLAT", "1")
+    flat = DT.yolo_decode(feats, (8, 16, 32), 80)
+    torch.cuda.synchronize()
+    for a, b in zip(tiled, flat):
+        assert torch.equal(a, b)
+
+
 def _random_dets(B, A, g, n_centers=40):
     centers = torch.rand(B, n_centers, 2, generator=g) * 600
     pick = torch.randint(0, n_centers, (B, A), generator=g)
