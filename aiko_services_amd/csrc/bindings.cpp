@@ -70,6 +70,7 @@ int aiko_topk_nms(const void* boxes, const float* scores, const int* cls, int B,
 int aiko_avgpool(const void* x, void* y, int B, int HW, int C, hipStream_t stream);
 int aiko_mean_rows_f32(const void* x, float* y, int B, int T, int C, long ldb, hipStream_t stream);
 int aiko_zero_border_rows(void* x, int B, int rows, int C, hipStream_t stream);
+int aiko_sppf_pool(void* x, int B, int H, int W, int ld, int c, int k, hipStream_t stream);
 int aiko_window_shift(const float* src, const float* chunk, float* dst, int B, int W, int n, hipStream_t stream);
 int aiko_conv_narrow(const void* x, const void* w, const float* bias, const void* res, void* y, int H, int W, int C,
                      int Cc, int R, int S, int stride, int pad, int Ho, int Wo, int M, int Cout, int K, int act,
@@ -515,6 +516,16 @@ void mean_rows_out(const at::Tensor& x, at::Tensor& y) {
                "mean_rows");
 }
 
+// SPPF: slices 1..3 of the [B, H, W, >= 4c] concat buffer = chained k x k / 1 max pools of slice 0
+void sppf_pool_(at::Tensor& cat, int64_t c, int64_t k) {
+  check_cuda(cat, "cat");
+  const int64_t ld = pixel_pitch(cat, "sppf_pool_");
+  TORCH_CHECK(c % 8 == 0 && 4 * c <= cat.size(3) && k % 2 == 1 && cat.size(1) * cat.size(2) <= 2048,
+              "aiko.sppf_pool_: c % 8 == 0, 4c <= C, odd k, H*W <= 2048");
+  check_launch(aiko_sppf_pool(cat.data_ptr(), cat.size(0), cat.size(1), cat.size(2), (int)ld, (int)c, (int)k,
+                              cur_stream()), "sppf_pool");
+}
+
 void zero_border_rows_(at::Tensor& x, int64_t rows) {
   check_cuda(x, "x");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.is_contiguous() && x.size(1) % 8 == 0 &&
@@ -925,6 +936,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("mean_rows_out(Tensor x, Tensor(a!) y) -> ()");
   m.def("window_shift_out(Tensor src, Tensor chunk, Tensor(a!) dst) -> ()");
   m.def("zero_border_rows_(Tensor(a!) x, int rows) -> ()");
+  m.def("sppf_pool_(Tensor(a!) cat, int c, int k) -> ()");
   m.def("stem_pool_out(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, int Ho, int Wo, int variant=0) -> ()");
   m.def("gemm_fp8_out(Tensor a, Tensor? sa, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!)? y, int act, int bm, int bn, int variant=0, Tensor? zero=None, Tensor? amx=None, Tensor(b!)? yq=None, Tensor(c!)? ysc=None) -> ()");
   m.def("rownorm_quant_out(Tensor x, Tensor? gamma, Tensor? beta, float eps, Tensor(a!)? yb, Tensor(b!)? q, Tensor(c!)? qs) -> ()");
@@ -952,6 +964,7 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("mean_rows_out", &mean_rows_out);
   m.impl("window_shift_out", &window_shift_out);
   m.impl("zero_border_rows_", &zero_border_rows_);
+  m.impl("sppf_pool_", &sppf_pool_);
   m.impl("stem_pool_out", &stem_pool_out);
   m.impl("softmax_topk_out", &softmax_topk_out);
   m.impl("gemm_fp8_out", &gemm_fp8_out);

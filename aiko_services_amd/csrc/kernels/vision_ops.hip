@@ -232,6 +232,50 @@ __global__ __launch_bounds__(256) void stem_direct_kernel(
 // Max pool (k x k, stride s, pad p) NHWC bf16, C % 8 == 0: one thread per 8 channels of one
 // output pixel (16-byte loads/stores).  Padding never wins (-inf).  ``ldx`` / ``ldy`` are the
 // pixel pitches, so input and output may be channel slices of concat buffers (YOLO SPPF).
+// YOLOv8 SPPF's three chained k x k / stride-1 max pools in one kernel: slice 0 of the concat
+// buffer [B, H, W, ld] (channels [0, c)) -> slices 1, 2, 3.  One block per (image, 8 channels)
+// stages the H x W map in LDS and runs each pool as a row max then a column max (clipped
+// windows, so separable); max is exact, so the three slices are bit-identical to three
+// maxpool_kernel launches, without two round trips through HBM and two launches.
+__global__ __launch_bounds__(256) void sppf_pool_kernel(bf16_t* __restrict__ x, int H, int W, int ld,
+                                                        int c, int k) {
+  extern __shared__ __attribute__((aligned(16))) u32x4 tile[];   // [2][H*W]: map, row max
+  const int HW = H * W, r = k / 2;
+  const int c8 = blockIdx.x, b = blockIdx.y;
+  u32x4* cur = tile;
+  u32x4* rmax = tile + HW;
+  bf16_t* img = x + (long)b * HW * ld + c8 * 8;
+  for (int i = threadIdx.x; i < HW; i += 256) cur[i] = *reinterpret_cast<const u32x4*>(img + (long)i * ld);
+  __syncthreads();
+  const auto vmax = [](u32x4 a, u32x4 v) {
+    u32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float lo = fmaxf(__uint_as_float(a[e] << 16), __uint_as_float(v[e] << 16));
+      const float hi = fmaxf(__uint_as_float(a[e] & 0xffff0000u), __uint_as_float(v[e] & 0xffff0000u));
+      o[e] = (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xffff0000u);
+    }
+    return o;
+  };
+  for (int it = 1; it <= 3; ++it) {
+    for (int i = threadIdx.x; i < HW; i += 256) {
+      const int h = i / W, w = i - h * W;
+      u32x4 m = cur[i];
+      for (int d = max(-r, -w); d <= min(r, W - 1 - w); ++d) m = vmax(m, cur[h * W + w + d]);
+      rmax[i] = m;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < HW; i += 256) {
+      const int h = i / W, w = i - h * W;
+      u32x4 m = rmax[i];
+      for (int d = max(-r, -h); d <= min(r, H - 1 - h); ++d) m = vmax(m, rmax[(h + d) * W + w]);
+      cur[i] = m;
+      *reinterpret_cast<u32x4*>(img + (long)i * ld + it * c) = m;
+    }
+    __syncthreads();
+  }
+}
+
 __global__ void maxpool_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int B,
                                int H, int W, int C, int Ho, int Wo, int k, int s, int p,
                                int ldx, int ldy) {
@@ -630,6 +674,14 @@ extern "C" int aiko_softmax_topk(const void* logits, float* prob, int* index, in
   } else {
     return -1;
   }
+  return (int)hipGetLastError();
+}
+
+extern "C" int aiko_sppf_pool(void* x, int B, int H, int W, int ld, int c, int k, hipStream_t stream) {
+  if (B < 1 || B > 65535 || c % 8 || ld % 8 || 4 * c > ld || k < 1 || k % 2 == 0 || (long)H * W > 2048)
+    return -1;
+  const size_t lds = (size_t)2 * H * W * sizeof(aiko::u32x4);
+  aiko::sppf_pool_kernel<<<dim3(c / 8, B), 256, lds, stream>>>(static_cast<aiko::bf16_t*>(x), H, W, ld, c, k);
   return (int)hipGetLastError();
 }
 

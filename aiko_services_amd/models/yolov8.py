@@ -187,6 +187,9 @@ class YOLOv8(WeightsMixin):
         c = blk.cv1.cout
         cat = self._buf(f"{name}.cat", (B, H, W, 4 * c))
         C.conv2d(x, blk.cv1, out=cat[..., :c])
+        if cat.is_cuda and H * W <= 2048 and c % 8 == 0:
+            V.sppf_pool(cat, c, blk.k)          # the three chained pools in one kernel
+            return C.conv2d(cat, blk.cv2, out=out)
         for i in range(3):
             V.maxpool2d(cat[..., i * c:(i + 1) * c], blk.k, 1, blk.k // 2, out=cat[..., (i + 1) * c:(i + 2) * c])
         C.conv2d(cat, blk.cv2, out=out)

@@ -44,6 +44,13 @@ def letterbox_geometry(h: int, w: int, new_shape: int | tuple[int, int] = 640):
     return Ho, Wo, int(round(dh - 0.1)), int(round(dw - 0.1)), r
 
 
+def sppf_pool(cat: torch.Tensor, c: int, k: int = 5) -> torch.Tensor:
+    """YOLOv8 SPPF pools in one kernel: channels [i*c, (i+1)*c) of the [B, H, W, 4c] concat
+    buffer for i = 1, 2, 3 <- the k x k / stride-1 max pool of slice i-1 (GPU, H*W <= 2048)."""
+    torch.ops.aiko.sppf_pool_(cat, c, k)
+    return cat
+
+
 def maxpool2d(x: torch.Tensor, k: int = 3, s: int = 2, p: int = 1,
               out: torch.Tensor | None = None) -> torch.Tensor:
     B, H, W, C = x.shape

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Time the YOLOv8 DFL decode at the bench's head shapes (B=64, 640x640: 80/40/20 levels, 144 ch):
+"""Time the YOLOv8 DFL decode and the SPPF pools at the bench's head shapes (B=64, 640x640: 80/40/20 levels, 144 ch):
 LDS-tiled kernel vs the per-anchor kernel (AIKO_DECODE_FLAT=1), same inputs, outputs compared."""
 import os
 import sys
@@ -31,6 +31,18 @@ def main():
     t_flat, b = timed(fn)
     same = all(torch.equal(x, y) for x, y in zip(a, b))
     print(f"yolo_decode B=64: tiled {t_tiled:.1f} us, per-anchor {t_flat:.1f} us, identical={same}")
+    from aiko_services_amd.ops import vision as V
+    cat = torch.randn(64, 20, 20, 512, device="cuda").to(torch.bfloat16)
+    c = 128
+
+    def chained():
+        for i in range(3):
+            V.maxpool2d(cat[..., i * c:(i + 1) * c], 5, 1, 2, out=cat[..., (i + 1) * c:(i + 2) * c])
+    t_chain, _ = timed(chained)
+    ref = cat.clone()
+    t_fused, _ = timed(lambda: V.sppf_pool(cat, c, 5))
+    print(f"SPPF pools [64,20,20,4x128]: fused {t_fused:.1f} us, 3 chained maxpools {t_chain:.1f} us, "
+          f"identical={torch.equal(cat, ref)}")
 
 
 if __name__ == "__main__":

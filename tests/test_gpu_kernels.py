@@ -195,6 +195,20 @@ def test_preprocess_rows_fast_path_exact(native, H, W, bgr):
     assert outs[1][:, :, :3].abs().max().item() == 0 and outs[1][:, :, 3 + W:].abs().max().item() == 0
 
 
+@pytest.mark.parametrize("B,H,W,c", [(3, 20, 20, 128), (2, 7, 33, 16), (1, 40, 40, 64)])
+def test_sppf_pool_matches_chained_maxpools(native, B, H, W, c):
+    """sppf_pool_ (one kernel, LDS separable pools) == three chained maxpool_out launches, exactly."""
+    from aiko_services_amd.ops import vision as V
+    g = torch.Generator().manual_seed(H * W + c)
+    cat = (torch.randn(B, H, W, 4 * c, generator=g) * 4).round().to(torch.bfloat16).to(DEV)
+    ref = cat.clone()
+    for i in range(3):
+        V.maxpool2d(ref[..., i * c:(i + 1) * c], 5, 1, 2, out=ref[..., (i + 1) * c:(i + 2) * c])
+    V.sppf_pool(cat, c, 5)
+    torch.cuda.synchronize()
+    assert torch.equal(cat, ref)
+
+
 def test_linear_with_n_tail(native):
     from aiko_services_amd.ops import conv as C
     from aiko_services_amd.ops import reference as R
