@@ -43,6 +43,11 @@ def main():
     t_fused, _ = timed(lambda: V.sppf_pool(cat, c, 5))
     print(f"SPPF pools [64,20,20,4x128]: fused {t_fused:.1f} us, 3 chained maxpools {t_chain:.1f} us, "
           f"identical={torch.equal(cat, ref)}")
+    up_in = torch.randn(64, 40, 40, 128, device="cuda").to(torch.bfloat16)
+    up_out = torch.empty(64, 80, 80, 192, device="cuda", dtype=torch.bfloat16)
+    t_up, _ = timed(lambda: DT.upsample2x(up_in, out=up_out[..., :128]))
+    ok = torch.equal(up_out[..., :128], up_in.repeat_interleave(2, 1).repeat_interleave(2, 2))
+    print(f"upsample2x [64,40,40,128] -> slice of [64,80,80,192]: {t_up:.1f} us, exact={ok}")
 
 
 if __name__ == "__main__":
