@@ -313,6 +313,36 @@ __global__ void logmel_finalize_kernel(const float* __restrict__ logmel, const i
   }
 }
 
+// Same, 8 mels per thread (n_mels % 8 == 0, 16-byte aligned rows): two float4 loads, one 16-byte
+// store of 8 bf16 and 32-bit index math -- the scalar version does a 64-bit division and a 2-byte
+// store per element.  Identical per-element arithmetic and rounding.
+__global__ __launch_bounds__(256) void logmel_finalize8_kernel(const float* __restrict__ logmel,
+                                                               const int* __restrict__ gmax,
+                                                               bf16_t* __restrict__ dst, int B, int F,
+                                                               int n_mels, int rows, int pad, int ld) {
+  const int n8 = n_mels >> 3;
+  const int total = B * rows * n8;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int r = i / n8, m8 = i - r * n8;
+    const int b = r / rows, row = r - b * rows;
+    const int t = row - pad;
+    u32x4 o = {0u, 0u, 0u, 0u};
+    if (t >= 0 && t < F) {
+      const float mx = float_from_key(gmax[b]) - 8.f;
+      const f32x4* src = reinterpret_cast<const f32x4*>(logmel + ((long)b * F + t) * n_mels + m8 * 8);
+      const f32x4 u0 = src[0], u1 = src[1];
+      const float v[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const unsigned lo = f2bf((fmaxf(v[2 * e], mx) + 4.f) * 0.25f);
+        const unsigned hi = f2bf((fmaxf(v[2 * e + 1], mx) + 4.f) * 0.25f);
+        o[e] = lo | (hi << 16);
+      }
+    }
+    *reinterpret_cast<u32x4*>(dst + ((long)b * rows + row) * ld + m8 * 8) = o;
+  }
+}
+
 
 // Sliding audio window update, one pass: dst[b] = src[b][n:W] ++ chunk[b][0:n] (fp32, float4
 // lanes; W, n multiples of 4).  Replaces two strided device copies per step.
@@ -347,6 +377,13 @@ extern "C" int aiko_logmel(const float* audio, int B, int N, const float* mel, i
   const long total = (long)B * rows * n_mels;
   long g = (total + 255) / 256;
   if (g > 4096) g = 4096;
+  if (n_mels % 8 == 0 && ld % 8 == 0 && reinterpret_cast<uintptr_t>(dst) % 16 == 0 &&
+      reinterpret_cast<uintptr_t>(logmel) % 16 == 0 && total < (1L << 31)) {
+    const long g8 = (total / 8 + 255) / 256;
+    aiko::logmel_finalize8_kernel<<<(int)(g8 < 4096 ? g8 : 4096), 256, 0, stream>>>(
+        logmel, gmax, static_cast<aiko::bf16_t*>(dst), B, F, n_mels, rows, pad, ld);
+    return (int)hipGetLastError();
+  }
   aiko::logmel_finalize_kernel<<<(int)g, 256, 0, stream>>>(logmel, gmax, static_cast<aiko::bf16_t*>(dst),
                                                           B, F, n_mels, rows, pad, ld);
   return (int)hipGetLastError();
