@@ -22,6 +22,10 @@ int aiko_conv_buf(const void* x, const void* w, const float* bias, const void* r
                   int H, int W, int C, int Cc, int R, int S, int stride, int pad, int Ho, int Wo,
                   int M, int Cout, int K, int act, int ldy, int ldr, int bm, int bn, const void* x2,
                   int K1, int H2, int W2, int C2, int stride2, int occ, int mf32, hipStream_t stream);
+int aiko_conv_wide(const void* x, const void* w, const float* bias, const void* res, void* y,
+                   int H, int W, int C, int Cc, int R, int S, int stride, int pad, int Ho, int Wo,
+                   int M, int Cout, int K, int act, int ldy, int ldr, int bm, int bn, const void* x2,
+                   int K1, int H2, int W2, int C2, int stride2, int occ, hipStream_t stream);
 int aiko_conv_persist(const void* x, const void* w, const float* bias, const void* res, void* y,
                       int H, int W, int C, int Cc, int R, int S, int stride, int pad, int Ho, int Wo,
                       int M, int Cout, int K, int act, int ldy, int ldr, int bm, int bn, const void* x2,
@@ -117,7 +121,8 @@ void check_launch(int rc, const char* what) {
 // needs ``zero`` (>= 16 B of zeros on the device) as the source of conv padding; 2: buffer
 // LDS-DMA kernel (conv_buf.hip, padding by out-of-range buffer reads); 3 / 5 / 6: conv_buf at high
 // occupancy / on 32x32x16 MFMA / as 4-wave wide tiles; 4: persistent conv_buf; 7: direct 3x3 kernel
-// for narrow layers (conv_narrow.hip).
+// for narrow layers (conv_narrow.hip); 8: 8-wave wide tiles with a register-direct epilogue
+// (conv_wide.hip); 9: the same kernel at several workgroups per CU.
 void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, const at::Tensor& w,
                     const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& res,
                     at::Tensor& y, at::IntArrayRef geom, const c10::optional<at::Tensor>& zero) {
@@ -190,6 +195,16 @@ void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, co
                 "aiko.conv_igemm_out: variant 7 needs a 3x3 / pad 1 / stride 1-2 or 1x1 / stride 1 conv with Cc, Cout in {16, 32}");
     rc = aiko_conv_narrow(x.data_ptr(), w.data_ptr(), bptr, rptr, y.data_ptr(), H, W, C, Cc, R, S, stride, pad, Ho,
                           Wo, M, Cout, K, act, ldy, ldr, cur_stream());
+  } else if (variant == 8 || variant == 9) {
+    // 8-wave wide tiles, transposed product, register-direct epilogue (conv_wide.hip)
+    TORCH_CHECK(Cc % 64 == 0 && R * S <= 32 && x_extent * 2 < (1LL << 31) - 64 && w.numel() * 2 < (1LL << 31),
+                "aiko.conv_igemm_out: variant 8 needs Cc % 64 == 0, R*S <= 32 and operands < 2 GiB");
+    TORCH_CHECK(!dual || avail_elems(*x2) * 2 < (1LL << 31) - 64, "aiko.conv_igemm_out: x2 too large for variant 8");
+    TORCH_CHECK(ldy % 8 == 0 && (!rptr || (ldr % 8 == 0 && reinterpret_cast<uintptr_t>(rptr) % 16 == 0)),
+                "aiko.conv_igemm_out: variant 8 needs 16-B aligned rows");
+    rc = aiko_conv_wide(x.data_ptr(), w.data_ptr(), bptr, rptr, y.data_ptr(), H, W, C, Cc, R, S, stride,
+                        pad, Ho, Wo, M, Cout, K, act, ldy, ldr, bm, bn, x2ptr, K1, H2, W2, C2, stride2,
+                        variant == 9 ? 2 : 1, cur_stream());
   } else if (variant == 4) {
     // persistent buffer-LDS-DMA kernel: one K-block stream across each workgroup's run of tiles
     TORCH_CHECK(Cc % 64 == 0 && R * S <= 32 && K % 64 == 0 && x_extent * 2 < (1LL << 31) - 64 &&

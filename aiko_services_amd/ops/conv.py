@@ -237,6 +237,12 @@ MF32_TILES = ((128, 128), (128, 64), (64, 128), (256, 128), (128, 256))
 # ResNet-50 layers: never the tuner's pick — one wave per SIMD exposes the DMA / LDS latency
 # that the 8-wave layouts hide — kept as a candidate for other shapes
 WIDE4_TILES = ((256, 128), (128, 256))
+# variant 8 (conv_wide.hip): 8 waves, transposed product (weights on the MFMA A side) so each
+# lane ends with 8 consecutive output channels of one pixel and the epilogue goes straight from
+# registers to memory (no LDS round trip) — tiles up to 256 x 256
+WIDE8_TILES = ((256, 256), (256, 128), (128, 256), (256, 64), (128, 128))
+# variant 9: the same kernel at 2-3 workgroups per CU (short-K, bandwidth-bound layers)
+WIDE_OCC_TILES = ((128, 128), (256, 64), (128, 64), (64, 128), (64, 64))
 
 
 def buf_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = None) -> bool:
@@ -270,6 +276,7 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False):
             cands += [t + (4,) for t in PERSIST_TILES]
             cands += [t + (5,) for t in MF32_TILES]
             cands += [t + (6,) for t in WIDE4_TILES]
+            cands += [t + (8,) for t in WIDE8_TILES] + [t + (9,) for t in WIDE_OCC_TILES]
     best, best_t = None, None
     for t in cands:
         launch(t)  # warm
