@@ -436,10 +436,10 @@ def chain_ok(spec3: ConvSpec, spec1: ConvSpec) -> bool:
     reduction) run as one ``conv_chain`` launch?"""
     def one_by_one(s):
         return s.kind == "conv" and s.R == 1 and s.S == 1 and s.stride == 1 and s.K1 is None and s.bias is not None
-    # (K1, N1) -> allowed N2.  The stage-2 shapes (128, 512) -> 128 | 256 are implemented and
-    # tested but spill at 512 threads (128-VGPR cap): 377 / 519 us against 151 / 200 us for
-    # the two unchained convs, so they are opt-in (CHAIN_STAGE2) until that is fixed.
-    shapes = {(64, 256): (64, 128)}
+    # (K1, N1) -> allowed N2.  Stage 2 -> 128 runs on conv_chain2.hip (both weight matrices
+    # resident in registers); stage 2 -> 256 (the stage-3 entry reduction) is still the
+    # register-staged kernel, which spills there (519 us against 200 us unchained): opt-in.
+    shapes = {(64, 256): (64, 128), (128, 512): (128,)}
     if _chain_stage2():
         shapes[(128, 512)] = (128, 256)
     k1, n1 = spec3.weight.shape[1], spec3.weight.shape[0]

@@ -174,14 +174,14 @@ def test_conv_chain_matches_two_convs(native, k1, n1, n2, monkeypatch):
     separate igemm convs and the fp32 reference.  The stage-2 shapes are opt-in (read at call
     time); without the opt-in conv_chain refuses them."""
     from aiko_services_amd.ops import conv as C
-    if k1 == 128:
+    if k1 == 128 and n2 == 256:
         monkeypatch.setenv("AIKO_CHAIN_STAGE2", "1")
     g = torch.Generator().manual_seed(n2 + k1)
     spec3 = C.make_conv_spec(torch.randn(n1, k1, 1, 1, generator=g) / k1 ** 0.5, 0.1 * torch.randn(n1, generator=g),
                              act="relu", device="cuda")
     spec1 = C.make_conv_spec(torch.randn(n2, n1, 1, 1, generator=g) / n1 ** 0.5, 0.1 * torch.randn(n2, generator=g),
                              act="relu", device="cuda")
-    assert C.chain_ok(spec3, spec1) == (k1 == 64 or C._chain_stage2())
+    assert C.chain_ok(spec3, spec1) == (k1 == 64 or n2 == 128 or C._chain_stage2())
     B, H, W = 3, 28, 32                                      # M = 2688 = 42 tiles of 64
     x = torch.randn(B, H, W, k1, generator=g).to("cuda", torch.bfloat16)
     r = torch.randn(B, H, W, n1, generator=g).to("cuda", torch.bfloat16)
