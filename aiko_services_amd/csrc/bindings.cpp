@@ -42,6 +42,8 @@ int aiko_stem_direct(const void* in, void* out, const void* w, const float* bias
                      int Ho, int Wo, int Hc, int Wc, int off_t, int off_l, float fill, const float* mean,
                      const float* std, int bgr, int H1, int W1, int Cout, int ldo, int k, int stride, int pad,
                      int act, hipStream_t stream);
+int aiko_conv3x3_patch(const void* x, const void* wimg, const float* bias, void* y, int B, int H, int W, int ldy,
+                       int act, int grid, hipStream_t stream);
 int aiko_conv_chain(const void* A, const void* W1, const float* b1, const void* R, void* Y, const void* W2,
                     const float* b2, void* Z, const void* A2, int M, int K1, int N1, int N2, int grid,
                     hipStream_t stream);
@@ -272,6 +274,38 @@ void preprocess_out(const at::Tensor& frames, at::Tensor& out, int64_t Ho, int64
 }
 
 int64_t pixel_pitch(const at::Tensor& t, const char* op);
+
+// 3x3 / stride 1 / pad 1 conv, 64 -> 64 channels, with an LDS-resident input patch (conv_patch.hip).
+// x [B, H, W, 64] contiguous; wimg the [9, 2, 4, 64, 8] fragment image (ops.conv.patch_weight);
+// y [B, H, W, >= 64] NHWC with unit channel stride (a channel slice of a wider buffer is fine).
+void conv3x3_patch_out(const at::Tensor& x, const at::Tensor& wimg, const c10::optional<at::Tensor>& bias,
+                       at::Tensor& y, int64_t act, int64_t grid) {
+  check_cuda(x, "x");
+  check_cuda(wimg, "wimg");
+  check_cuda(y, "y");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && wimg.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16,
+              "aiko.conv3x3_patch_out: bf16 tensors");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) == 64 && x.is_contiguous(), "aiko.conv3x3_patch_out: x must be [B, H, W, 64] contiguous");
+  TORCH_CHECK(wimg.is_contiguous() && wimg.numel() == 9 * 64 * 64, "aiko.conv3x3_patch_out: wimg must be the 36864-element image");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2);
+  TORCH_CHECK(W + 8 <= 64, "aiko.conv3x3_patch_out: W <= 56");
+  TORCH_CHECK(y.dim() == 4 && y.size(0) == B && y.size(1) == H && y.size(2) == W && y.size(3) == 64 && y.stride(3) == 1 &&
+                  y.stride(2) % 8 == 0 && y.stride(1) == W * y.stride(2) && y.stride(0) == H * W * y.stride(2) &&
+                  reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0,
+              "aiko.conv3x3_patch_out: y must be [B, H, W, 64] NHWC (16-B aligned pixel pitch)");
+  TORCH_CHECK(x.numel() * 2 < (1LL << 31) - 64 && avail_elems(y) * 2 < (1LL << 31) - 64,
+              "aiko.conv3x3_patch_out: tensors too large for 32-bit offsets");
+  TORCH_CHECK(act == 0 || act == 1 || act == 2, "aiko.conv3x3_patch_out: act none / relu / silu");
+  const float* bptr = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    check_cuda(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == 64, "aiko.conv3x3_patch_out: bias fp32 [64]");
+    bptr = bias->data_ptr<float>();
+  }
+  check_launch(aiko_conv3x3_patch(x.data_ptr(), wimg.data_ptr(), bptr, y.data_ptr(), (int)B, (int)H, (int)W,
+                                  (int)y.stride(2), (int)act, (int)grid, cur_stream()),
+               "conv3x3_patch");
+}
 
 // Chained 1x1 convs at a bottleneck boundary (conv_chain.hip):
 //   Y = relu(A W1^T + b1 + R) [M, N1],  Z = relu(Y W2^T + b2) [M, N2]
@@ -945,6 +979,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("yolo_decode_out(Tensor[] feats, int[] strides, int nc, int reg_max, Tensor(a!) boxes, Tensor(b!) scores, Tensor(c!) cls) -> ()");
   m.def("topk_nms_out(Tensor boxes, Tensor scores, Tensor cls, int max_cand, float[] params, Tensor(a!) det, Tensor(b!) count) -> ()");
   m.def("stem_direct_out(Tensor frames, Tensor w, Tensor? bias, Tensor(a!) out, int[] geom, float fill, float[] mean, float[] std, bool bgr) -> ()");
+  m.def("conv3x3_patch_out(Tensor x, Tensor wimg, Tensor? bias, Tensor(a!) y, int act, int grid=0) -> ()");
   m.def("conv_chain_out(Tensor A, Tensor W1, Tensor b1, Tensor? R, Tensor(a!) Y, Tensor W2, Tensor b2, Tensor(b!) Z, int grid=0, Tensor? A2=None) -> ()");
   m.def("maxpool_out(Tensor x, Tensor(a!) y, int k, int s, int p) -> ()");
   m.def("avgpool_out(Tensor x, Tensor(a!) y) -> ()");
@@ -969,6 +1004,7 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("preprocess_out", &preprocess_out);
   m.impl("maxpool_out", &maxpool_out);
   m.impl("conv_chain_out", &conv_chain_out);
+  m.impl("conv3x3_patch_out", &conv3x3_patch_out);
   m.impl("stem_direct_out", &stem_direct_out);
   m.impl("upsample2x_out", &upsample2x_out);
   m.impl("resize_u8_out", &resize_u8_out);

@@ -255,6 +255,37 @@ def buf_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = No
             and (x2 is None or nbytes(x2) < 2**31 - 64))
 
 
+def patch_variant_ok(spec: ConvSpec, x: torch.Tensor, residual=None, x2=None, out=None) -> bool:
+    """Whether the LDS-resident-patch 3x3 kernel (variant 10, conv_patch.hip) applies: a 3x3 /
+    stride 1 / pad 1 conv 64 -> 64 channels on a contiguous [B, H, W, 64] input (W = 56 or 24:
+    the kernel's patch pitch is a compile-time constant), no residual,
+    no second source, activation none / ReLU / SiLU."""
+    return (spec.kind == "conv" and spec.R == 3 and spec.S == 3 and spec.stride == 1 and spec.pad == 1
+            and spec.Cc == 64 and spec.cout == 64 and spec.K == 576 and spec.K1 is None
+            and residual is None and x2 is None and spec.act in (ACT_NONE, ACT_RELU, ACT_SILU)
+            and x.dim() == 4 and x.shape[3] == 64 and x.is_contiguous() and x.shape[2] in (56, 24)
+            and (out is None or (out.stride(3) == 1 and out.stride(2) % 8 == 0)))
+
+
+def patch_weight(spec: ConvSpec) -> torch.Tensor:
+    """[9, 2, 4, 64, 8] MFMA fragment image of a 3x3 64 -> 64 weight for conv_patch.hip: (tap,
+    32-channel half, 16-output-channel block, lane = 16 (k chunk) + output row, 8 channels).  Cached
+    on the spec and re-derived in place when the weight changes (as stem_pool_weight)."""
+    key = (spec.weight.data_ptr(), spec.weight._version)
+    cached = getattr(spec, "_patch_w", None)
+    if cached is not None and cached[0] == key:
+        return cached[1]
+    w = spec.weight.view(4, 16, 9, 2, 4, 8)                  # [nb, fr, tap, half, fq, e]
+    img = w.permute(2, 3, 0, 4, 1, 5).reshape(9, 2, 4, 64, 8)
+    if cached is not None:
+        cached[1].copy_(img)
+        img = cached[1]
+    else:
+        img = img.contiguous()
+    spec._patch_w = (key, img)
+    return img
+
+
 def narrow_variant_ok(spec: ConvSpec, x2: torch.Tensor | None = None) -> bool:
     """Whether the direct narrow-layer kernel (variant 7, conv_narrow.hip) applies: a 3x3 / pad 1
     / stride 1-2 or 1x1 / stride 1 conv with 16 or 32 input and output channels, no second source."""
@@ -264,7 +295,7 @@ def narrow_variant_ok(spec: ConvSpec, x2: torch.Tensor | None = None) -> bool:
             and spec.Cc in (16, 32) and spec.cout in (16, 32))
 
 
-def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False):
+def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False):
     if cout <= 32:
         cands = [t + (0,) for t in NARROW_TILES]
         if narrow_ok:
@@ -277,6 +308,8 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False):
             cands += [t + (5,) for t in MF32_TILES]
             cands += [t + (6,) for t in WIDE4_TILES]
             cands += [t + (8,) for t in WIDE8_TILES] + [t + (9,) for t in WIDE_OCC_TILES]
+        if patch_ok:
+            cands.append((8, 64, 10))        # variant 10: tile fixed by the kernel (8 rows x W)
     best, best_t = None, None
     for t in cands:
         launch(t)  # warm
@@ -353,6 +386,11 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None
         # t = (BM, BN) or (BM, BN, variant): variant 1 = LDS-DMA kernel (needs the zero page),
         # 2 = buffer-LDS-DMA kernel
         v = t[2] if len(t) > 2 else 0
+        if v == 10:
+            if not patch_variant_ok(spec, x, residual, x2, out):
+                raise ValueError("conv2d: variant 10 needs a 3x3/s1/p1 64->64 conv on a contiguous W<=56 input")
+            torch.ops.aiko.conv3x3_patch_out(x, patch_weight(spec), spec.bias, out, spec.act, 0)
+            return
         torch.ops.aiko.conv_igemm_out(x, x2, spec.weight, spec.bias, residual, out,
                                       head + [t[0], t[1]] + src2 + [v], zero_page(x.device) if v == 1 else None)
 
@@ -361,7 +399,8 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None
         tile = _tile_cache.get(key)
         if tile is None:
             if _tuning:
-                tile = _tune(key, M, spec.cout, launch, buf_variant_ok(spec, x, x2), narrow_variant_ok(spec, x2))
+                tile = _tune(key, M, spec.cout, launch, buf_variant_ok(spec, x, x2), narrow_variant_ok(spec, x2),
+                             patch_variant_ok(spec, x, residual, x2, out) and not residual_after_act)
             else:
                 tile = pick_tile(M, spec.cout)
     launch(tile)

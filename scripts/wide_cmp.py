@@ -19,7 +19,7 @@ def main():
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--variants", default="8,9")
+    ap.add_argument("--variants", default="8,9,10")
     a = ap.parse_args()
     new_v = {int(v) for v in a.variants.split(",")}
     from aiko_services_amd.ops import conv as C
@@ -73,6 +73,8 @@ def main():
         cands += [t + (4,) for t in C.PERSIST_TILES] + [t + (5,) for t in C.MF32_TILES]
         cands += [t + (6,) for t in C.WIDE4_TILES] + [t + (8,) for t in C.WIDE8_TILES]
         cands += [t + (9,) for t in C.WIDE_OCC_TILES]
+        if C.patch_variant_ok(spec, x, kw.get("residual"), x2, out):
+            cands.append((8, 64, 10))
         res = {}
         for t in cands:
             def fn(t=t):

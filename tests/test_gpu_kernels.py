@@ -121,6 +121,30 @@ def test_conv_igemm_matches_torch(native, B, H, W, cin, cout, k, stride, pad, ac
     assert err < 1e-2, err
 
 
+@pytest.mark.parametrize("B,H,W,act", [(2, 56, 56, "relu"), (3, 13, 24, "silu"), (1, 30, 24, None),
+                                          (2, 17, 56, "relu"), (1, 8, 56, "relu"), (3, 1, 24, "relu")])
+def test_conv3x3_patch_matches_torch(native, B, H, W, act):
+    """Variant 10 (LDS-resident input patch, conv_patch.hip): partial row tiles, narrow images,
+    every activation, output into a channel slice of a wider buffer."""
+    from aiko_services_amd.ops import conv as C
+    from aiko_services_amd.ops import reference as R
+    g = torch.Generator().manual_seed(B * 100 + H)
+    w = torch.randn(64, 64, 3, 3, generator=g) / 24
+    b = torch.randn(64, generator=g) * 0.1
+    spec = C.make_conv_spec(w, b, stride=1, pad=1, act=act, device=DEV)
+    x = torch.randn(B, 64, H, W, generator=g).to(torch.bfloat16)
+    xd = _nhwc(x).to(DEV)
+    assert C.patch_variant_ok(spec, xd)
+    y = C.conv2d(xd, spec, tile=(8, 64, 10))
+    cat = torch.zeros(B, H, W, 96, dtype=torch.bfloat16, device=DEV)
+    C.conv2d(xd, spec, out=cat[..., 16:80], tile=(8, 64, 10))
+    torch.cuda.synchronize()
+    ref = R.conv_ref(x.float().to(DEV), spec)
+    assert _rel_err(y.permute(0, 3, 1, 2), ref) < 1e-2
+    assert torch.equal(cat[..., 16:80], y)
+    assert cat[..., :16].abs().max().item() == 0 and cat[..., 80:].abs().max().item() == 0
+
+
 def test_conv_writes_into_channel_slice(native):
     """Output into a slice of a concat buffer and input from a channel slice (pitch != Cc)."""
     from aiko_services_amd.ops import conv as C
