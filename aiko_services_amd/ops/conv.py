@@ -192,6 +192,7 @@ TILES = ((128, 128), (128, 64), (64, 128), (64, 64))
 NARROW_TILES = ((128, 32), (256, 32), (64, 64), (128, 64))   # Cout <= 32 (YOLO stems / heads)
 _tile_cache: dict = {}          # geometry key -> (bm, bn), filled by autotune()
 _tuning = False
+_TUNE_VERBOSE = __import__("os").environ.get("AIKO_TUNE_VERBOSE", "0") == "1"
 
 
 class autotune:
@@ -213,6 +214,25 @@ class autotune:
 
 def tile_cache() -> dict:
     return dict(_tile_cache)
+
+
+def save_tile_cache(path: str) -> None:
+    """Write the tuner's per-geometry choices as JSON (profiling runs replay them without
+    re-tuning, so a kernel trace holds only the steady-state launches)."""
+    import json
+    rows = [[list(k), list(v)] for k, v in _tile_cache.items()]
+    with open(path, "w") as f:
+        json.dump(rows, f)
+
+
+def load_tile_cache(path: str) -> int:
+    """Merge a :func:`save_tile_cache` file into the tuner's cache; returns the entry count."""
+    import json
+    with open(path) as f:
+        rows = json.load(f)
+    for k, v in rows:
+        _tile_cache[tuple(k)] = tuple(v)
+    return len(rows)
 
 
 _ZERO: dict = {}
@@ -310,17 +330,21 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False):
             cands += [t + (8,) for t in WIDE8_TILES] + [t + (9,) for t in WIDE_OCC_TILES]
         if patch_ok:
             cands.append((8, 64, 10))        # variant 10: tile fixed by the kernel (8 rows x W)
+    # each candidate: 2 warm launches, then the median of 5 individually timed ones (a 3-launch
+    # sum was noisy enough to rank a 56 us kernel behind an 80 us one on a fresh box)
     best, best_t = None, None
     for t in cands:
-        launch(t)  # warm
-        start = torch.cuda.Event(enable_timing=True)
-        end = torch.cuda.Event(enable_timing=True)
-        start.record()
-        for _ in range(3):
+        launch(t)
+        launch(t)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
+        for e0, e1 in evs:
+            e0.record()
             launch(t)
-        end.record()
-        end.synchronize()
-        ms = start.elapsed_time(end)
+            e1.record()
+        evs[-1][1].synchronize()
+        ms = sorted(e0.elapsed_time(e1) for e0, e1 in evs)[2]
+        if _TUNE_VERBOSE:
+            print(f"[tune] M={M} N={cout} {t}: {ms * 1e3:.1f} us", flush=True)
         if best_t is None or ms < best_t:
             best, best_t = t, ms
     _tile_cache[key] = best
