@@ -40,7 +40,9 @@ class SyntheticFrames(GpuPipelineElement):
     slot filled once with random pixels, like a hardware decoder writing device memory).  Every
     frame holds its slot until the frame completes and the GPU is done with it; with all
     ``pool`` slots in flight the next frame waits for the oldest (back-pressure on the device
-    queue) or — ``on_exhausted: drop`` — is dropped (DROP_FRAME).  Stable slot addresses let
+    queue, at most ``acquire_timeout`` s) or — ``on_exhausted: drop`` — is dropped (DROP_FRAME).
+    The pool size is also the pipeline's credit window for generated frames
+    (``PipelineImpl.limit_frames``).  Stable slot addresses let
     the downstream hipGraphs be captured on the slots themselves (no input copy)."""
     lane_safe = True          # read-only frame pool
 
@@ -56,6 +58,11 @@ class SyntheticFrames(GpuPipelineElement):
             return
         from ...gpu.element import FramePool
         B = _int(self.get_parameter("batch", 1)[0], 1)
+        if self.pipeline is not None and hasattr(self.pipeline, "limit_frames"):
+            # generated frames in flight never exceed the slots (the generator thread waits
+            # for a credit): the actor thread's acquire below then never waits for a slot that
+            # only a later message on the same thread could free
+            self.pipeline.limit_frames(self.name, max(1, _int(self.get_parameter("pool", 2)[0], 2)))
         if glob:
             from ...parallel import dist as D
             B *= D.world_size()
@@ -83,8 +90,10 @@ class SyntheticFrames(GpuPipelineElement):
                 return None
         self._ensure_pool(glob)
         drop = str(self.get_parameter("on_exhausted", "block")[0]).lower() == "drop"
-        timeout = self.get_parameter("acquire_timeout", None)[0]
-        slot = self.frame_pool.acquire(0.0 if drop else (float(timeout) if timeout is not None else None))
+        # "block" waits for the GPU to finish the oldest frame, bounded: frames pushed in past the
+        # credit window (direct process_frame calls) are dropped rather than wedging the actor
+        timeout = self.get_parameter("acquire_timeout", 30.0)[0]
+        slot = self.frame_pool.acquire(0.0 if drop else float(timeout))
         if slot < 0:
             return False
         self.hold_for_frame(self.frame_pool, slot)

@@ -330,6 +330,9 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False):
             cands += [t + (8,) for t in WIDE8_TILES] + [t + (9,) for t in WIDE_OCC_TILES]
         if patch_ok:
             cands.append((8, 64, 10))        # variant 10: tile fixed by the kernel (8 rows x W)
+    skip = {int(v) for v in __import__("os").environ.get("AIKO_CONV_SKIP", "").split(",") if v.strip()}
+    if skip:                                   # A/B runs: exclude variants from the tuner
+        cands = [t for t in cands if (t[2] if len(t) > 2 else 0) not in skip] or cands
     # each candidate: 2 warm launches, then the median of 5 individually timed ones (a 3-launch
     # sum was noisy enough to rank a 56 us kernel behind an 80 us one on a fresh box)
     best, best_t = None, None
@@ -502,7 +505,9 @@ def chain_ok(spec3: ConvSpec, spec1: ConvSpec) -> bool:
     # (K1, N1) -> allowed N2.  Stage 2 -> 128 runs on conv_chain2.hip (both weight matrices
     # resident in registers); stage 2 -> 256 (the stage-3 entry reduction) is still the
     # register-staged kernel, which spills there (519 us against 200 us unchained): opt-in.
-    shapes = {(64, 256): (64, 128), (128, 512): (128,)}
+    shapes = {(64, 256): (64, 128)}
+    if __import__("os").environ.get("AIKO_CHAIN2", "1") != "0":
+        shapes[(128, 512)] = (128,)
     if _chain_stage2():
         shapes[(128, 512)] = (128, 256)
     k1, n1 = spec3.weight.shape[1], spec3.weight.shape[0]

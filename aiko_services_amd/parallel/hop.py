@@ -7,7 +7,7 @@ and continues the parent graph when ``process_frame_response`` comes back
 is split in two planes:
 
 * control plane (unchanged, MQTT): ``(process_frame (stream_id: s frame_id: f hop_rank: r)
-  (images: T@0/17/0/uint8/256x480x640x3 ...))`` — every tensor replaced by a short token
+  (images: T@0/17/0/uint8/256x224x224x3 ...))`` — every tensor replaced by a short token
   naming the sending rank, the per-link message number, the tensor's index in the message and
   its dtype / shape;
 * data plane (RCCL point-to-point over xGMI): the sender packs all tensors of the message into
@@ -23,12 +23,21 @@ travels back.  P2P ops within one direction match in issue order, and the contro
 one direction arrive in publish order (one MQTT connection per process), so no tags are
 needed; the per-link message number is checked on receipt.
 
-Send staging buffers form a ring of ``depth`` per link; a buffer is reused only after the
-transfer that last read it completed (the current stream waits on it: no host block on RCCL).
-Forward receive slots come from a capacity-``2 * depth`` FramePool per link and are released
-when the frame completes — gated by a HIP event recorded at completion, so a slot is never
-rewritten while kernels of that frame may still read it.  Pool exhaustion (more frames in
-flight than slots) falls back to an allocator buffer and is counted in ``stats()``.
+Credits (back-pressure).  A link has ``depth`` staging slots.  A FORWARD hop (``encode(...,
+key=frame)``) holds its slot until the frame's response comes back (``ack(key)``): the slot is
+the link's credit, so a sender can never have more frames in flight toward a peer than the
+peer's receive pool holds (``depth`` slots, the receiver's FramePool) — the engine only picks a
+replica with :meth:`credit` left and queues the frame otherwise.  The held slot is also the
+RETRANSMIT buffer: when the peer dies the same bytes are re-sent to a survivor (:meth:`resend`)
+or materialised locally (:meth:`held_values`), whatever the producing element has since written
+into its own buffers.  Responses (``key=None``) use the slots as a ring: a slot is reused once
+its previous transfer completed (the current stream waits on it: no host block on RCCL).
+
+Failure.  :meth:`mark_dead` (registrar ``remove`` / last will of the peer's process, or a
+transport error) retires every link to and from that rank: pending transfers are dropped, never
+waited on (an RCCL send to a dead rank never completes and a ``wait()`` on it would stall this
+GPU's stream), the per-link communicators are aborted, their staging buffers are not reused, and
+any later use raises :class:`StageFailure`.
 
 Python floats (``t_submit`` stamps) travel as ``F@<repr>`` tokens so they keep their type;
 :class:`~aiko_services_amd.gpu.element.DeviceResult` values travel as a nested dict of tensor
@@ -43,7 +52,8 @@ import torch.distributed as tdist
 
 from . import dist as D
 
-__all__ = ["HopPlane", "init_plane", "plane", "shutdown_plane", "is_token", "TOKEN", "FLOAT_TOKEN"]
+__all__ = ["HopPlane", "StageFailure", "NoCredit", "init_plane", "plane", "shutdown_plane", "is_token",
+           "needs_decode", "TOKEN", "FLOAT_TOKEN"]
 
 TOKEN = "T@"
 FLOAT_TOKEN = "F@"
@@ -54,8 +64,35 @@ _DTYPES = {str(dt).split(".")[-1]: dt for dt in
             torch.float32, torch.float64, torch.bfloat16, torch.bool)}
 
 
+class StageFailure(RuntimeError):
+    """A peer rank of the hop plane is gone (registrar removal, last will or transport error)."""
+
+    def __init__(self, peer: int, cause=None):
+        super().__init__(f"hop: stage rank {peer} failed" + (f": {cause}" if cause else ""))
+        self.peer = peer
+
+
+class NoCredit(RuntimeError):
+    """Every staging slot toward the peer holds an unacknowledged frame."""
+
+
 def is_token(v) -> bool:
     return isinstance(v, str) and (v.startswith(TOKEN) or v.startswith(FLOAT_TOKEN))
+
+
+def needs_decode(stream_dict, values) -> bool:
+    """Whether a ``process_frame`` / ``process_frame_response`` message went through
+    :meth:`HopPlane.encode`: the stream dict names a hop rank (forward hops), or a value is a
+    tensor / float token or an encoded DeviceResult (responses).  Plain nested-dict swag values
+    of reference pipelines never enter the token scanner."""
+    if isinstance(stream_dict, dict) and stream_dict.get("hop_rank") is not None:
+        return True
+    if not isinstance(values, dict):
+        return False
+    for v in values.values():
+        if is_token(v) or (isinstance(v, dict) and RESULT_KEY in v):
+            return True
+    return False
 
 
 def _nbytes(dtype, shape) -> int:
@@ -79,55 +116,114 @@ def _view(buf: torch.Tensor, off: int, dtype, shape) -> torch.Tensor:
     return buf[off:off + n].view(dtype).view(shape)
 
 
+def _parse(tok: str):
+    src, seq, idx, dt, shape = tok[len(TOKEN):].split("/")
+    dims = tuple(int(s) for s in shape.split("x")) if shape else ()
+    return int(src), int(seq), int(idx), _DTYPES[dt], dims
+
+
+def _retoken(values: dict, seq: int) -> dict:
+    """The token dict of a message with its per-link sequence number replaced."""
+    out = {}
+    for k, v in values.items():
+        if isinstance(v, str) and v.startswith(TOKEN):
+            f = v[len(TOKEN):].split("/")
+            f[1] = str(seq)
+            out[k] = TOKEN + "/".join(f)
+        elif isinstance(v, dict):
+            out[k] = _retoken(v, seq)
+        else:
+            out[k] = v
+    return out
+
+
 class _SendLink:
-    """This rank -> ``peer``: process group + ring of staging buffers."""
+    """This rank -> ``peer``: process group + ``depth`` staging slots (credits)."""
 
     def __init__(self, peer, group, device, depth):
         self.peer, self.group, self.device = peer, group, device
         self.bufs = [None] * depth
-        self.pending = [None] * depth
+        self.work = [None] * depth          # last transfer that read the slot's buffer
+        self.holder = [None] * depth        # frame key holding the slot until its ack
         self.cursor = 0
         self.seq = 0
+        self.dead = False
 
-    def stage(self, nbytes):
-        slot = self.cursor
-        self.cursor = (slot + 1) % len(self.bufs)
-        w = self.pending[slot]
+    def credit(self) -> int:
+        return 0 if self.dead else sum(h is None for h in self.holder)
+
+    def take(self, nbytes, key):
+        if self.dead:
+            raise StageFailure(self.peer)
+        n = len(self.bufs)
+        for step in range(n):
+            slot = (self.cursor + step) % n
+            if self.holder[slot] is None:
+                break
+        else:
+            raise NoCredit(f"hop: no credit toward rank {self.peer} ({n} frames unacknowledged)")
+        self.cursor = (slot + 1) % n
+        w = self.work[slot]
         if w is not None:
-            w.wait()                       # RCCL: stream-ordered; gloo: host waits (CPU tests)
-            self.pending[slot] = None
+            w.wait()                         # RCCL: stream-ordered; gloo: host waits (CPU tests)
+            self.work[slot] = None
         buf = self.bufs[slot]
         if buf is None or buf.numel() < nbytes:
             buf = self.bufs[slot] = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        self.holder[slot] = key
         return slot, buf
 
+    def release(self, slot, reuse=True):
+        self.holder[slot] = None
+        if not reuse:                        # a transfer that may never finish still owns it
+            self.work[slot] = None
+            self.bufs[slot] = None
+
+    def retire(self):
+        """Dead peer: forget every pending transfer (never wait on them) and every buffer."""
+        self.dead = True
+        keys = [k for k in self.holder if k is not None]
+        n = len(self.bufs)
+        self.bufs, self.work, self.holder = [None] * n, [None] * n, [None] * n
+        return keys
+
     def drain(self):
-        for i, w in enumerate(self.pending):
+        if self.dead:
+            return
+        for i, w in enumerate(self.work):
             if w is not None:
                 w.wait()
-                self.pending[i] = None
+                self.work[i] = None
 
 
 class _RecvLink:
-    """``peer`` -> this rank: process group + FramePool of receive slots."""
+    """``peer`` -> this rank: process group + FramePool of receive slots (the sender's credits)."""
 
     def __init__(self, peer, group, device, depth):
         self.peer, self.group, self.device, self.depth = peer, group, device, depth
         self.pool = None
         self.seq = 0
+        self.dead = False
 
-    def slot(self, nbytes, plane):
+    def slot(self, nbytes, plane, timeout_s: float = 30.0):
         pool = self.pool
         if pool is None or pool.slot_bytes < nbytes:
             from ..gpu.element import FramePool
-            # slots sized for the largest message so far (x1.25 headroom for small changes);
-            # slots of a retired pool stay valid: their frames hold a reference to it
+            # capacity 2 x depth >= the sender's credits; sized for the largest message so far
+            # (x1.25 headroom for small changes); slots of a retired pool stay valid: their frames
+            # hold a reference to it
             pool = self.pool = FramePool(2 * self.depth, int(nbytes * 1.25) // _ALIGN * _ALIGN + _ALIGN,
                                          device=self.device if self.device.type == "cuda" else "cpu")
-        s = pool.acquire(0.0)          # retires finished releases; waits on the GPU if all held
-        if s < 0:                      # more frames in flight than slots: allocator buffer
-            plane.counters["pool_overflow"] += 1
-            return None, torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        s = pool.acquire(0.0)            # retires finished releases; waits on the GPU if all held
+        if s < 0:
+            # only a sender exceeding its credits gets here: wait for a slot (bounded), never
+            # fall back to the allocator
+            plane.counters["pool_waits"] += 1
+            s = pool.acquire(timeout_s)
+            if s < 0:
+                plane.counters["pool_overflow"] += 1
+                raise RuntimeError(f"hop: receive pool from rank {self.peer} exhausted for {timeout_s}s "
+                                   "(sender exceeded its credits)")
         return (pool, s), pool.view(s, (pool.slot_bytes,), torch.uint8)
 
 
@@ -136,6 +232,7 @@ class HopPlane:
 
     ``links``: [(src, dst), ...] in the same order on every rank (each becomes one process
     group; every rank must call this constructor, it is collective over the default group).
+    ``depth``: staging slots = credits per forward link = half the receive pool.
     """
 
     def __init__(self, links, device=None, depth: int = 4):
@@ -149,7 +246,10 @@ class HopPlane:
         self.send_links: dict = {}
         self.recv_links: dict = {}
         self.links = [tuple(int(x) for x in l) for l in links]
+        self.dead: set = set()
+        self._held: dict = {}              # frame key -> [dst, slot, total, specs, template]
         self._loop: deque = deque()        # loopback link (src == dst): staged buffers in order
+        self._groups: dict = {}            # (src, dst) -> process group
         for src, dst in self.links:
             if src == dst:
                 if src == self.rank:
@@ -157,6 +257,7 @@ class HopPlane:
                     self.recv_links[src] = _RecvLink(src, None, self.device, self.depth)
                 continue
             group = tdist.new_group(ranks=sorted({src, dst})) if D.is_initialized() else None
+            self._groups[(src, dst)] = group
             if src == self.rank:
                 self.send_links[dst] = _SendLink(dst, group, self.device, self.depth)
             elif dst == self.rank:
@@ -179,15 +280,77 @@ class HopPlane:
         # host-side control group (gloo) for start-up barriers issued from helper threads
         self.control = tdist.new_group(backend="gloo") if D.is_initialized() else None
         self.counters = {"sent_msgs": 0, "sent_bytes": 0, "recv_msgs": 0, "recv_bytes": 0,
-                         "pool_overflow": 0}
+                         "pool_overflow": 0, "pool_waits": 0, "resent": 0, "dead_peers": 0}
+
+    # ---- credits / failure ------------------------------------------------------------------
+    def credit(self, dst: int) -> int:
+        """Frames that may still be sent toward ``dst`` before one is acknowledged."""
+        link = self.send_links.get(int(dst))
+        return 0 if link is None else link.credit()
+
+    def is_dead(self, rank: int) -> bool:
+        return int(rank) in self.dead
+
+    def ack(self, key) -> None:
+        """The response of forward frame ``key`` arrived: its staging slot is a credit again."""
+        rec = self._held.pop(key, None)
+        if rec is None:
+            return
+        link = self.send_links.get(rec[0])
+        if link is not None and not link.dead:
+            link.release(rec[1])
+
+    def drop(self, key) -> None:
+        """Abandon forward frame ``key`` (ERROR / timeout): its slot is not reused while its
+        transfer might still be reading it."""
+        rec = self._held.pop(key, None)
+        if rec is None:
+            return
+        link = self.send_links.get(rec[0])
+        if link is not None and not link.dead:
+            link.release(rec[1], reuse=False)
+
+    def mark_dead(self, rank: int) -> list:
+        """Retire every link to / from ``rank``; returns the keys of the forward frames it held
+        (for :meth:`resend` / :meth:`held_values`, which keep working: the buffers are kept)."""
+        rank = int(rank)
+        if rank in self.dead or rank == self.rank:
+            return []
+        self.dead.add(rank)
+        self.counters["dead_peers"] += 1
+        keys = []
+        link = self.send_links.get(rank)
+        if link is not None:
+            for key, rec in self._held.items():
+                if rec[0] == rank:
+                    rec[1] = None           # no slot any more: the record alone owns the buffer
+                    keys.append(key)
+            link.retire()
+        rlink = self.recv_links.get(rank)
+        if rlink is not None:
+            rlink.dead = True
+        if D.backend() == "nccl":
+            for (src, dst), group in self._groups.items():
+                if rank in (src, dst) and group is not None:
+                    try:                    # stop RCCL's proxy waiting on the dead peer
+                        from torch.distributed.distributed_c10d import _abort_process_group
+                        _abort_process_group(group)
+                    except Exception:       # noqa: BLE001 — best effort
+                        pass
+        return keys
 
     # ---- encode (sender) -------------------------------------------------------------------
-    def encode(self, dst: int, values: dict) -> dict:
+    def encode(self, dst: int, values: dict, key=None) -> dict:
         """``values`` with every tensor / DeviceResult / float replaced by tokens; the tensors
-        are packed and sent to ``dst``.  Non-tensor values pass through unchanged."""
+        are packed and sent to ``dst``.  ``key`` (forward hops): hold the staging slot until
+        :meth:`ack` (raises :class:`NoCredit` when none is free).  Non-tensor values pass
+        through unchanged."""
         from ..gpu.element import DeviceResult
-        link = self.send_links.get(int(dst))
+        dst = int(dst)
+        link = self.send_links.get(dst)
         if link is None:
+            if dst in self.dead:
+                raise StageFailure(dst)
             raise RuntimeError(f"hop: no send link {self.rank} -> {dst} in this plan")
         tensors = []
 
@@ -219,41 +382,95 @@ class HopPlane:
                     slots.append((out, k, len(tensors) - 1))
         if not tensors:
             return out
-        seq = link.seq
-        link.seq += 1
         specs = [(t.dtype, tuple(t.shape)) for t in tensors]
         offs, total = _layout(specs)
-        slot, buf = link.stage(total)
+        slot, buf = link.take(total, key if key is not None else ())
+        seq = link.seq
+        link.seq += 1
         for t, off, (dt, shape) in zip(tensors, offs, specs):
             dstv = _view(buf, off, dt, shape)
             dstv.copy_(t if t.device == buf.device else t.to(buf.device, non_blocking=True),
                        non_blocking=True)
-        for container, key, idx in slots:
+        for container, ckey, idx in slots:
             dt, shape = specs[idx]
-            container[key] = (f"{TOKEN}{self.rank}/{seq}/{idx}/{str(dt).split('.')[-1]}/"
-                              + "x".join(str(int(s)) for s in shape))
-        D._account("hop_send", total)
-        if int(dst) == self.rank:               # loopback: the receiver copies from the stage
-            self._loop.append(buf)
-            link.pending[slot] = None
+            container[ckey] = (f"{TOKEN}{self.rank}/{seq}/{idx}/{str(dt).split('.')[-1]}/"
+                               + "x".join(str(int(s)) for s in shape))
+        self._post(link, slot, buf, total, dst)
+        if key is not None:
+            self._held[key] = [dst, slot, total, specs, out, buf]
         else:
-            link.pending[slot] = tdist.isend(buf[:total], dst, group=link.group) if link.group is not None \
+            link.holder[slot] = None                 # ring slot: free once its transfer is done
+        return out
+
+    def _post(self, link, slot, buf, total, dst):
+        D._account("hop_send", total)
+        if dst == self.rank:                         # loopback: the receiver copies from the stage
+            self._loop.append(buf)
+            link.work[slot] = None
+        else:
+            link.work[slot] = tdist.isend(buf[:total], dst, group=link.group) if link.group is not None \
                 else None
         self.counters["sent_msgs"] += 1
         self.counters["sent_bytes"] += total
+
+    def resend(self, key, dst: int) -> dict:
+        """Send held forward frame ``key`` (its original bytes) to ``dst`` instead; returns the
+        message's new token dict.  The frame then holds a credit of ``dst``'s link."""
+        rec = self._held.get(key)
+        if rec is None:
+            raise KeyError(f"hop: no held frame {key}")
+        dst = int(dst)
+        link = self.send_links.get(dst)
+        if link is None:
+            raise StageFailure(dst) if dst in self.dead else RuntimeError(f"hop: no send link to {dst}")
+        old_dst, old_slot, total, specs, template, buf = rec
+        old = self.send_links.get(old_dst)
+        if old is not None and not old.dead and old_slot is not None:
+            old.release(old_slot, reuse=False)        # the buffer moves with the frame
+        slot, _ = link.take(0, key)
+        link.bufs[slot] = buf
+        seq = link.seq
+        link.seq += 1
+        self._post(link, slot, buf, total, dst)
+        out = _retoken(template, seq)
+        self._held[key] = [dst, slot, total, specs, out, buf]
+        self.counters["resent"] += 1
+        return out
+
+    def held_values(self, key) -> dict:
+        """The held forward frame ``key`` as tensors (views of its staging buffer), e.g. to run
+        it on a local replica after its remote peer died.  The frame keeps its record until
+        :meth:`ack` / :meth:`drop`."""
+        rec = self._held[key]
+        _dst, _slot, total, specs, template, buf = rec
+        offs, _ = _layout(specs)
+        return self._materialize(template, buf, offs)
+
+    def _materialize(self, template, buf, offs):
+        from ..gpu.element import DeviceResult
+        out = {}
+        for k, v in template.items():
+            if isinstance(v, str) and v.startswith(TOKEN):
+                _src, _seq, idx, dt, shape = _parse(v)
+                out[k] = _view(buf, offs[idx], dt, shape)
+            elif isinstance(v, str) and v.startswith(FLOAT_TOKEN):
+                out[k] = float(v[len(FLOAT_TOKEN):])
+            elif isinstance(v, dict) and RESULT_KEY in v:
+                sub = self._materialize({kk: vv for kk, vv in v.items() if kk != RESULT_KEY}, buf, offs)
+                t_submit = sub.pop("_t_submit", None)
+                out[k] = DeviceResult(sub, None, t_submit=t_submit)
+            else:
+                out[k] = v
         return out
 
     # ---- decode (receiver) -----------------------------------------------------------------
-    @staticmethod
-    def _parse(tok: str):
-        src, seq, idx, dt, shape = tok[len(TOKEN):].split("/")
-        dims = tuple(int(s) for s in shape.split("x")) if shape else ()
-        return int(src), int(seq), int(idx), _DTYPES[dt], dims
+    _parse = staticmethod(_parse)
 
     def decode(self, values: dict, pooled: bool = True):
         """Inverse of :meth:`encode`: posts the receive of the message's tensors and returns
         ``(values, handle)``; ``handle`` (or None) must be given to :meth:`release` once the
-        frame no longer needs the tensors (forward hops, ``pooled=True``)."""
+        frame no longer needs the tensors (forward hops, ``pooled=True``).  Raises
+        :class:`StageFailure` for a message of a dead peer or a failed transfer."""
         from ..gpu.element import DeviceResult
         found = []                   # (container, key, src, seq, idx, dtype, shape)
         out = {}
@@ -262,7 +479,7 @@ class HopPlane:
             for k, v in container_in.items():
                 if isinstance(v, str) and v.startswith(TOKEN):
                     container_out[k] = None
-                    found.append((container_out, k) + self._parse(v))
+                    found.append((container_out, k) + _parse(v))
                 elif isinstance(v, str) and v.startswith(FLOAT_TOKEN):
                     container_out[k] = float(v[len(FLOAT_TOKEN):])
                 elif isinstance(v, dict) and v.get(RESULT_KEY) is not None:
@@ -280,6 +497,8 @@ class HopPlane:
         if len(srcs) != 1 or len(seqs) != 1:
             raise RuntimeError(f"hop: one message must come from one send (got {srcs} / {seqs})")
         src, seq = srcs.pop(), seqs.pop()
+        if src in self.dead:
+            raise StageFailure(src, "message of a retired peer")
         link = self.recv_links.get(src)
         if link is None:
             raise RuntimeError(f"hop: no receive link {src} -> {self.rank} in this plan")
@@ -297,12 +516,17 @@ class HopPlane:
         if src == self.rank:
             buf[:total].copy_(self._loop.popleft()[:total], non_blocking=True)
         elif link.group is not None:
-            tdist.irecv(buf[:total], src, group=link.group).wait()    # RCCL: the stream waits
+            try:
+                tdist.irecv(buf[:total], src, group=link.group).wait()    # RCCL: the stream waits
+            except RuntimeError as exc:
+                if handle is not None:
+                    self.release([handle])
+                raise StageFailure(src, exc) from exc
         self.counters["recv_msgs"] += 1
         self.counters["recv_bytes"] += total
         for f, off in zip(found, offs):
-            container, key = f[0], f[1]
-            container[key] = _view(buf, off, f[5], f[6])
+            container, ckey = f[0], f[1]
+            container[ckey] = _view(buf, off, f[5], f[6])
         # rebuild DeviceResults: completion event after the receive on this stream
         for k, v in list(out.items()):
             if isinstance(v, dict) and isinstance(values.get(k), dict) and RESULT_KEY in values[k]:
@@ -329,9 +553,14 @@ class HopPlane:
 
     def stats(self) -> dict:
         s = dict(self.counters)
+        s["held_frames"] = len(self._held)
+        for dst, link in self.send_links.items():
+            s[f"credit_to_{dst}"] = link.credit()
         for src, link in self.recv_links.items():
             if link.pool is not None:
                 s[f"pool_free_from_{src}"] = link.pool.free_count()
+        if self.dead:
+            s["dead"] = sorted(self.dead)
         return s
 
     def close(self):

@@ -219,6 +219,14 @@ class PipelineElementImpl(PipelineElement):
                         frame_data = [frame_data]
                     if isinstance(frame_data, list):
                         for fd in frame_data:
+                            # credit window: block THIS thread (never the actor's) while the
+                            # pipeline has its limit of generated frames in flight
+                            if not pipeline.admit_frame(stream.stream_id, frame_id):
+                                stream.state = StreamState.ERROR
+                                self.logger.error(f"frame generator: no frame completed for "
+                                                  f"{pipeline.admission_timeout:g}s (window "
+                                                  f"{pipeline.frame_window()}): stopping")
+                                break
                             self.create_frame(stream, fd, frame_id)
                             frame_id += 1
                     else:
@@ -332,6 +340,17 @@ class PipelineImpl(Pipeline):
         self.frames_completed = 0
         self._latencies: deque = deque(maxlen=1024)     # recent frame latencies (s) -> p50 / p99
         self.gpu_event_log: deque = deque(maxlen=4096)  # (element, start, end) HIP events (AIKO_GPU_TIMING)
+        # remote hops: frames in flight per (stream_id, frame_id), frames waiting for a credit,
+        # generator admission window (see dispatch / admit_frame below)
+        self._inflight: dict = {}
+        self._pending_hops: deque = deque()
+        self._admit_cv = threading.Condition()
+        self._admitted: set = set()
+        self._window_limits: dict = {}
+        self._hop_watch = False
+        self.hops_failed = 0
+        self.hops_redispatched = 0
+        self.frames_dropped = 0
         self.pipeline_graph = self._create_pipeline_graph(context.definition)
         self.share["element_count"] = self.pipeline_graph.element_count
         self.share["streams"] = 0
@@ -517,7 +536,11 @@ class PipelineImpl(Pipeline):
             proxy.hop_rank = int(rank) if rank not in (None, "") else None
             replicas.add(topic_path, proxy, weight=float(tags.get("weight", 1) or 1))
             element_instance.set_remote_absent(False)
-        elif not replicas.remove(topic_path):
+        else:
+            if topic_path not in replicas._members:
+                return
+            self.remote_pipelines[service_name] = (element_name, element_instance, replicas)
+            self._replica_lost(service_name, topic_path)
             return
         self.remote_pipelines[service_name] = (element_name, element_instance, replicas)
         if replicas.members:
@@ -577,6 +600,15 @@ class PipelineImpl(Pipeline):
         stream_id = str(stream_id)
         if isinstance(graceful, str):
             graceful = graceful.lower() == "true"
+        lease = self.stream_leases.get(stream_id)
+        if graceful and lease is not None and lease.stream.frames:
+            # drain first, THEN tell the remote elements: the reference
+            # (/root/reference/src/aiko_services/main/pipeline.py:804-809) destroys the remote
+            # stream before its own frames — some still to be forwarded — have drained, so a
+            # downstream stage can drop the tail of a stream ("stream not found")
+            self._post_message(ActorTopic.IN, "destroy_stream", [stream_id, graceful, use_thread_local],
+                               delay=0.05 if self._inflight or self._pending_hops else 1.0)
+            return False
         if self.share["lifecycle"] == "ready":
             for node in self.pipeline_graph.get_path(self.share["graph_path"]):
                 element, _, local, _ = PipelineGraph.get_element(node)
@@ -636,10 +668,20 @@ class PipelineImpl(Pipeline):
             return None, None, None
         hop_handle = None
         hop = _hop.plane()
-        if hop is not None and any(_hop.is_token(v) or isinstance(v, dict) for v in frame_data_in.values()):
+        if not new_frame:
+            # the response of a remote hop: its credit (and held retransmit slot) is free again
+            self._remote_done((stream.stream_id, stream.frame_id))
+        if hop is not None and _hop.needs_decode(stream_dict, frame_data_in):
             # tensors of this message arrive over RCCL: always receive them (even if the frame is
             # then rejected) so the link stays in order; forward hops land in FramePool slots
-            frame_data_in, hop_handle = hop.decode(frame_data_in, pooled=new_frame)
+            try:
+                frame_data_in, hop_handle = hop.decode(frame_data_in, pooled=new_frame)
+            except _hop.StageFailure as exc:
+                self.logger.error(f"Process frame <{stream.stream_id}:{stream.frame_id}>: {exc}")
+                self._replica_lost_rank(exc.peer)
+                if not new_frame:
+                    self._fail_frame((stream.stream_id, stream.frame_id), str(exc))
+                return None, None, None
         graph, stream = self._process_initialize_stream(stream, stream_dict, frame_data_in, new_frame)
         if graph is None:
             if hop_handle is not None:
@@ -750,7 +792,7 @@ class PipelineImpl(Pipeline):
                 inputs = self._process_map_in(header, element, node.name, frame.swag)
                 target = None
                 if isinstance(element, RemoteReplicas) and self.share["lifecycle"] == "ready":
-                    target = element.pick()
+                    target = element.pick(self._has_credit)
                     if isinstance(target, LocalStage):
                         # this frame's share of a replicated stage runs in-process (no hop)
                         stream_event, frame_data_out = target.run(stream.stream_id, frame_id, inputs)
@@ -806,14 +848,13 @@ class PipelineImpl(Pipeline):
                         frame_complete = False
                         frame_data_out = {}
                         frame.paused_pe_name = node.name
-                        target = target if target is not None else element
-                        stream_info = {"stream_id": stream.stream_id, "frame_id": frame_id}
-                        hop = _hop.plane()
-                        if hop is not None and getattr(target, "hop_rank", None) is not None:
-                            # metadata over MQTT, tensors over RCCL to the remote's rank
-                            stream_info["hop_rank"] = hop.rank
-                            inputs = hop.encode(target.hop_rank, inputs)
-                        target.process_frame(stream_info, **inputs)
+                        if not isinstance(element, RemoteReplicas):
+                            target = element
+                        if target is None:
+                            # no replica has a credit left: the frame waits (bounded queue)
+                            self._queue_hop(element, node.name, stream.stream_id, frame_id, inputs)
+                        else:
+                            self._dispatch(element, target, node.name, stream.stream_id, frame_id, inputs)
                     break
             if frame_complete:
                 join = getattr(stream.frames.get(frame_id), "_hip_join", None)
@@ -843,12 +884,7 @@ class PipelineImpl(Pipeline):
                     aiko.message.publish(self.topic_out, generate("process_frame", (stream_info, frame_data_out)))
         finally:
             if frame_complete:
-                done = stream.frames.pop(frame_id, None)
-                if done is not None:
-                    if done.hop_handles:
-                        _hop.plane().release(done.hop_handles)     # event-gated slot release
-                    for callback in done.on_complete:               # e.g. FramePool slots
-                        callback()
+                self._release_frame(stream, frame_id)
             self._disable_thread_local("process_frame")
             if stream.state == StreamState.DROP_FRAME:
                 stream.state = StreamState.RUN
@@ -906,6 +942,271 @@ class PipelineImpl(Pipeline):
                 self.destroy_stream(current_stream_id(), use_thread_local=False)
             return StreamState.ERROR
         return StreamState.RUN
+
+    def _release_frame(self, stream, frame_id):
+        """A frame leaves the pipeline (completed, dropped or failed): its hop receive slots and
+        FramePool slots go back (event-gated) and its admission credit is returned."""
+        done = stream.frames.pop(frame_id, None)
+        if done is not None:
+            if done.hop_handles:
+                _hop.plane().release(done.hop_handles)     # event-gated slot release
+            for callback in done.on_complete:               # e.g. FramePool slots
+                callback()
+        self._admit_release((stream.stream_id, frame_id))
+
+    # ---- admission window (credits for generated frames) -----------------------------------------
+    @property
+    def admission_timeout(self) -> float:
+        v, found = self.get_parameter("admission_timeout")
+        try:
+            return float(v) if found else 120.0
+        except (TypeError, ValueError):
+            return 120.0
+
+    def limit_frames(self, owner: str, n: int) -> None:
+        """An element caps the frames the pipeline may have in flight (e.g. SyntheticFrames:
+        its FramePool slots, each held by a frame until it completes)."""
+        with self._admit_cv:
+            self._window_limits[owner] = max(1, int(n))
+            self._admit_cv.notify_all()
+
+    def frame_window(self) -> int:
+        """Generated frames allowed in flight (0 = unlimited): the ``frame_window`` parameter,
+        else the smallest element limit, else — with remote elements — twice the hop credits."""
+        v, found = self.get_parameter("frame_window")
+        if found:
+            try:
+                return max(0, int(v))
+            except (TypeError, ValueError):
+                pass
+        if self._window_limits:
+            return min(self._window_limits.values())
+        if self.remote_pipelines:
+            hop = _hop.plane()
+            return 2 * (hop.depth if hop is not None else 4) * max(1, self._remote_member_count())
+        return 0
+
+    def _remote_member_count(self) -> int:
+        return sum(len(r._members) for _, _, r in self.remote_pipelines.values() if r is not None)
+
+    def admit_frame(self, stream_id, frame_id, timeout: float | None = None) -> bool:
+        """Block the CALLING thread (a frame generator, a bench driver — never the actor) until
+        the pipeline has fewer than :meth:`frame_window` admitted frames in flight; the frame
+        ``(stream_id, frame_id)`` is then counted until it leaves the pipeline.  False on timeout."""
+        key = (str(stream_id), frame_id)
+        deadline = time.monotonic() + (self.admission_timeout if timeout is None else timeout)
+        with self._admit_cv:
+            while True:
+                window = self.frame_window()
+                if window <= 0 or len(self._admitted) < window:
+                    self._admitted.add(key)
+                    return True
+                left = deadline - time.monotonic()
+                if left <= 0:
+                    return False
+                self._admit_cv.wait(min(left, 0.5))
+
+    def _admit_release(self, key):
+        key = (str(key[0]), key[1])
+        with self._admit_cv:
+            if key in self._admitted:
+                self._admitted.discard(key)
+                self._admit_cv.notify_all()
+
+    # ---- remote hops: credits, dispatch, failure ------------------------------------------------
+    def _param_float(self, name, default):
+        v, found = self.get_parameter(name)
+        try:
+            return float(v) if found else default
+        except (TypeError, ValueError):
+            return default
+
+    def _has_credit(self, proxy) -> bool:
+        if isinstance(proxy, LocalStage):
+            return True
+        rank = getattr(proxy, "hop_rank", None)
+        hop = _hop.plane()
+        if hop is not None and rank is not None:
+            return hop.credit(rank) > 0
+        window = int(self._param_float("remote_window", 0))
+        if window <= 0:
+            return True
+        return sum(1 for f in self._inflight.values() if f["target"] is proxy) < window
+
+    def _dispatch(self, element, target, node_name, stream_id, frame_id, inputs, held=False):
+        """Send frame ``(stream_id, frame_id)`` (paused at ``node_name``) to ``target``: metadata
+        over MQTT, tensors over RCCL holding one of the target link's credits until the response
+        (``held``: the frame's bytes are already staged — a re-dispatch).  A LocalStage target runs
+        in-process and resumes the frame through ``process_frame_response``."""
+        key = (stream_id, frame_id)
+        if isinstance(target, LocalStage):
+            hop = _hop.plane()
+            values = hop.held_values(key) if held and hop is not None else inputs
+            event_, out = target.run(stream_id, frame_id, values)
+            if held and hop is not None:
+                hop.drop(key)
+            info = {"stream_id": stream_id, "frame_id": frame_id}
+            if event_ == StreamEvent.ERROR:
+                self._fail_frame(key, out.get("diagnostic", "local replica error") if isinstance(out, dict) else "")
+                return
+            self._post_message(ActorTopic.IN, "process_frame_response", [info, out],
+                               target_function=self.process_frame_response)
+            return
+        stream_info = {"stream_id": stream_id, "frame_id": frame_id}
+        hop = _hop.plane()
+        rank = getattr(target, "hop_rank", None)
+        out = inputs
+        if hop is not None and rank is not None:
+            # metadata over MQTT, tensors over RCCL to the remote's rank
+            stream_info["hop_rank"] = hop.rank
+            try:
+                out = hop.resend(key, rank) if held else hop.encode(rank, inputs, key=key)
+            except _hop.StageFailure as exc:
+                self._replica_lost_rank(exc.peer)
+                if not held:
+                    self._queue_hop(element, node_name, stream_id, frame_id, inputs)
+                return
+        self._inflight[key] = {"element": element, "target": target, "node": node_name, "rank": rank,
+                               "inputs": inputs if rank is None else None, "t": time.monotonic()}
+        self._watch_hops()
+        target.process_frame(stream_info, **out)
+
+    def _queue_hop(self, element, node_name, stream_id, frame_id, inputs, held=False):
+        limit = int(self._param_float("remote_pending", 256))
+        if len(self._pending_hops) >= limit:
+            self.frames_dropped += 1
+            self.logger.warning(f"remote {node_name}: {limit} frames already wait for a credit: dropping "
+                                f"<{stream_id}:{frame_id}>")
+            if held:
+                hop = _hop.plane()
+                if hop is not None:
+                    hop.drop((stream_id, frame_id))
+            lease = self.stream_leases.get(str(stream_id))
+            if lease is not None:
+                self._release_frame(lease.stream, frame_id)
+            return
+        self._pending_hops.append({"element": element, "node": node_name, "stream_id": stream_id,
+                                   "frame_id": frame_id, "inputs": inputs, "held": held,
+                                   "t": time.monotonic()})
+        self._watch_hops()
+
+    def _drain_pending(self):
+        """Dispatch waiting frames while their remote element has a member with a credit."""
+        kept = deque()
+        while self._pending_hops:
+            p = self._pending_hops.popleft()
+            lease = self.stream_leases.get(str(p["stream_id"]))
+            if lease is None or p["frame_id"] not in lease.stream.frames:
+                if p["held"] and _hop.plane() is not None:
+                    _hop.plane().drop((p["stream_id"], p["frame_id"]))
+                continue
+            element = self.pipeline_graph.get_node(p["node"]).element
+            target = element.pick(self._has_credit) if isinstance(element, RemoteReplicas) else None
+            if target is None:
+                kept.append(p)
+                continue
+            self._dispatch(element, target, p["node"], p["stream_id"], p["frame_id"], p["inputs"], held=p["held"])
+        self._pending_hops = kept
+
+    def _remote_done(self, key):
+        f = self._inflight.pop(key, None)
+        if f is None:
+            return
+        hop = _hop.plane()
+        if hop is not None and f["rank"] is not None:
+            hop.ack(key)
+        if self._pending_hops:
+            self._drain_pending()
+
+    def _fail_frame(self, key, diagnostic):
+        """A frame that cannot complete (its replica died with no survivor to take it, or its
+        hop timed out): StreamEvent.ERROR for its stream, as the reference does for a remote
+        that errors (``/root/reference/src/aiko_services/main/pipeline.py:1229-1263``)."""
+        self.hops_failed += 1
+        hop = _hop.plane()
+        if hop is not None:
+            hop.drop(key)
+        self._inflight.pop(key, None)
+        lease = self.stream_leases.get(str(key[0]))
+        if lease is None:
+            return
+        stream = lease.stream
+        self._release_frame(stream, key[1])
+        self.logger.error(f"Frame <{key[0]}:{key[1]}>: {diagnostic}")
+        if stream.state != StreamState.ERROR:
+            stream.state = StreamState.ERROR
+            if stream.queue_response is not None:
+                stream.queue_response.put(({"stream_id": key[0], "frame_id": key[1], "state": StreamState.ERROR},
+                                           {"diagnostic": diagnostic}))
+            self.destroy_stream(str(key[0]), use_thread_local=False)
+
+    def _replica_lost_rank(self, rank):
+        """A hop peer failed (transport error): drop it from every remote element."""
+        for service_name, (name, instance, replicas) in list(self.remote_pipelines.items()):
+            if replicas is None:
+                continue
+            for topic, m in list(replicas._members.items()):
+                if getattr(m[0], "hop_rank", None) == rank:
+                    self._replica_lost(service_name, topic)
+
+    def _replica_lost(self, service_name, topic_path):
+        """Member ``topic_path`` of a remote element is gone (registrar remove / last will, or
+        a transport error): retire its RCCL links (no wait on its pending transfers can reach a
+        live stream), then re-dispatch every frame it held to a survivor — its staged bytes are
+        re-sent, not recomputed — or queue it for a credit; the element drops to absent (and the
+        pipeline's lifecycle to waiting) when no member is left.  Reference: the remote swap to
+        the absent proxy, ``/root/reference/src/aiko_services/main/pipeline.py:975-1006``."""
+        element_name, element_instance, replicas = self.remote_pipelines[service_name]
+        member = replicas._members.get(topic_path) if replicas is not None else None
+        if member is None:
+            return
+        proxy = member[0]
+        replicas.remove(topic_path)
+        rank = getattr(proxy, "hop_rank", None)
+        hop = _hop.plane()
+        if hop is not None and rank is not None:
+            hop.mark_dead(rank)
+        node = self.pipeline_graph.get_node(element_name)
+        if replicas.members:
+            node.element = replicas
+        else:
+            element_instance.set_remote_absent(True)
+            node.element = element_instance
+        self._update_lifecycle_state()
+        lost = [(k, f) for k, f in self._inflight.items() if f["target"] is proxy]
+        for key, f in lost:
+            self._inflight.pop(key, None)
+            held = f["rank"] is not None
+            self.hops_redispatched += 1
+            self._queue_hop(f["element"], f["node"], key[0], key[1], f["inputs"], held=held)
+        if lost:
+            self.logger.warning(f"remote {element_name}: member {topic_path} lost with {len(lost)} frames "
+                                f"in flight: re-dispatching")
+        self._drain_pending()
+
+    def _watch_hops(self):
+        if not self._hop_watch:
+            self._hop_watch = True
+            event.add_timer_handler(self._hop_timer, 0.5)
+
+    def _hop_timer(self):
+        """Hop timeout (``hop_timeout`` s, default 60): a frame whose remote response or credit
+        never comes ends with StreamEvent.ERROR instead of holding its stream forever."""
+        timeout = self._param_float("hop_timeout", 60.0)
+        now = time.monotonic()
+        for key, f in list(self._inflight.items()):
+            if now - f["t"] > timeout:
+                self._fail_frame(key, f"remote hop to {f['node']} timed out after {timeout:g}s")
+        if self._pending_hops:
+            self._drain_pending()
+            for p in list(self._pending_hops):
+                if now - p["t"] > timeout:
+                    self._pending_hops.remove(p)
+                    self._fail_frame((p["stream_id"], p["frame_id"]),
+                                     f"no replica of {p['node']} had a credit for {timeout:g}s")
+        if not self._inflight and not self._pending_hops:
+            self._hop_watch = False
+            event.remove_timer_handler(self._hop_timer)
 
     # ---- parameters ------------------------------------------------------------------------------
     def set_parameter(self, stream_id, name, value):
@@ -983,14 +1284,20 @@ class RemoteReplicas:
     def remove(self, topic_path) -> bool:
         return self._members.pop(topic_path, None) is not None
 
-    def pick(self):
+    def pick(self, available=None):
+        """Smooth weighted round-robin over the members ``available(proxy)`` accepts (those
+        with a credit left); None when there is none."""
         total = 0.0
         best = None
         for m in self._members.values():
+            if available is not None and not available(m[0]):
+                continue
             m[2] += m[1]
             total += m[1]
             if best is None or m[2] > best[2]:
                 best = m
+        if best is None:
+            return None
         best[2] -= total
         return best[0]
 

@@ -133,6 +133,8 @@ def pp_definition(batch: int, graph: bool, height: int, width: int, world: int, 
            "deploy": {"local": {"module": ELEMENTS}}}
     d["elements"].insert(1, pre)
     d["elements"][3]["parameters"]["gather"] = False
+    # the frame pool is the pipeline's credit window: two batches in flight per rank
+    d["elements"][0]["parameters"]["pool"] = max(6, 2 * world + 2)
     d["parallel"] = {"mode": "pp", "gpus": world}
     return d
 
@@ -421,6 +423,9 @@ def _drive_pp(a, pipeline, plane, plan, responses, rank, ws):
         sent = done = 0
         while done < n:
             while sent < n and sent - done < depth:
+                # the pipeline's credit window (SyntheticFrames' pool) bounds frames in flight
+                if not pipeline.admit_frame("bench", state["frame_id"], timeout=0 if sent > done else 120):
+                    break
                 pipeline.create_frame({"stream_id": "bench", "frame_id": state["frame_id"]}, {})
                 state["frame_id"] += 1
                 sent += 1
