@@ -77,7 +77,12 @@ def join(plan: Plan, rank: int, timeout_s: float = 120.0):
     if plan.world > 1:
         rendezvous_init(plan.group, rank, plan.world, host, port, backend=backend, timeout_s=timeout_s)
     depth = int(os.environ.get("AIKO_HOP_DEPTH", "4"))
-    return hop.init_plane(plan.links, depth=depth)
+    plane = hop.init_plane(plan.links, depth=depth)
+
+    def report():
+        print(f"hop rank {rank} stats: {plane.stats()}", file=sys.stderr, flush=True)
+    atexit.register(report)
+    return plane
 
 
 def create_rank_pipeline(plan: Plan, rank: int, stream_id=None, parameters=None, frame_id=0,

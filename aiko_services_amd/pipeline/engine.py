@@ -647,6 +647,10 @@ class PipelineImpl(Pipeline):
         if lease is not None:
             lease.terminate()
             lease.stream.state = StreamState.STOP if lease.stream.state != StreamState.ERROR else StreamState.ERROR
+        hop = _hop.plane()
+        if hop is not None:
+            self.logger.info(f"Stream {stream_id} destroyed: hop {hop.stats()} redispatched "
+                             f"{self.hops_redispatched} failed {self.hops_failed} dropped {self.frames_dropped}")
         return True
 
     # ---- frames ----------------------------------------------------------------------------------
@@ -668,20 +672,20 @@ class PipelineImpl(Pipeline):
             return None, None, None
         hop_handle = None
         hop = _hop.plane()
-        if not new_frame:
-            # the response of a remote hop: its credit (and held retransmit slot) is free again
-            self._remote_done((stream.stream_id, stream.frame_id))
         if hop is not None and _hop.needs_decode(stream_dict, frame_data_in):
             # tensors of this message arrive over RCCL: always receive them (even if the frame is
             # then rejected) so the link stays in order; forward hops land in FramePool slots
             try:
                 frame_data_in, hop_handle = hop.decode(frame_data_in, pooled=new_frame)
             except _hop.StageFailure as exc:
+                # the sender died mid-transfer: a response is re-dispatched (the frame is still
+                # held, in flight toward that member) with every other frame the member held
                 self.logger.error(f"Process frame <{stream.stream_id}:{stream.frame_id}>: {exc}")
                 self._replica_lost_rank(exc.peer)
-                if not new_frame:
-                    self._fail_frame((stream.stream_id, stream.frame_id), str(exc))
                 return None, None, None
+        if not new_frame:
+            # the response of a remote hop: its credit (and held retransmit slot) is free again
+            self._remote_done((stream.stream_id, stream.frame_id))
         graph, stream = self._process_initialize_stream(stream, stream_dict, frame_data_in, new_frame)
         if graph is None:
             if hop_handle is not None:
@@ -1162,6 +1166,8 @@ class PipelineImpl(Pipeline):
             return
         proxy = member[0]
         replicas.remove(topic_path)
+        # degraded but serving: the survivors are the stage now (``expected`` only gates start-up)
+        replicas.expected = min(replicas.expected, len(replicas._members))
         rank = getattr(proxy, "hop_rank", None)
         hop = _hop.plane()
         if hop is not None and rank is not None:

@@ -10,7 +10,10 @@ separated list:
                              (exercises the StreamEvent.ERROR -> destroy_stream path);
 * ``delay=ELEMENT@SECONDS``  sleep before ELEMENT's ``process_frame`` (slow-stage / lease tests);
 * ``kill=N``                 this process exits (``os._exit(KILL_EXIT_CODE)``) once N frames have
-                             completed — a dead pipeline-parallel rank or worker.
+                             completed — a dead pipeline-parallel rank or worker;
+* ``kill=N@rankR``           the same, only in the process whose ``RANK`` is R (one AIKO_FAULTS
+                             for a whole multi-GPU launch: the other ranks ignore it).  The Nth
+                             frame dies after its compute, before its response is sent.
 
 The hot path pays one ``is None`` check per element when no fault is configured.
 """
@@ -92,6 +95,9 @@ def parse(spec: str, seed: int = 0) -> FaultPlan:
         elif kind == "delay":
             plan.delays[what] = float(where)
         elif kind == "kill":
+            if where and where.startswith("rank"):
+                if os.environ.get("RANK", "0") != where[4:]:
+                    continue
             plan.kill_after_frames = int(what)
         else:
             raise ValueError(f"AIKO_FAULTS: unknown fault '{kind}' in '{item}'")

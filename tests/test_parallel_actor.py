@@ -159,3 +159,70 @@ def test_dp_spmd_actor_pipeline(cluster):
     assert len(out) == 4, (r.returncode, r.stdout[-3000:], r.stderr[-3000:])
     for v in out.values():
         assert "float32,6x1x6" in v and "int32,6" in v, v      # world x batch rows gathered
+
+
+def _variant(path, **params):
+    """A temp copy of a definition with overridden pipeline parameters; returns (file, dict)."""
+    with open(path) as f:
+        d = json.load(f)
+    d["parameters"].update(params)
+    f = tempfile.NamedTemporaryFile("w", suffix=".json", delete=False)
+    json.dump(d, f)
+    f.close()
+    return f.name, d
+
+
+def _single(cluster, d, frames):
+    d = json.loads(json.dumps(d))
+    d.pop("parallel")
+    for e in d["elements"]:
+        e["deploy"]["local"].pop("stage", None)
+    with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as f:
+        json.dump(d, f)
+    try:
+        _, single = _create(cluster["env"], f.name, frames)
+    finally:
+        os.unlink(f.name)
+    return single
+
+
+def test_replica_death_redispatches_held_frames(cluster):
+    """Rank 2 (one replica of stage 1 in tensor_ppdp.json) dies after computing its 2nd frame,
+    before it answers.  Rank 0 learns it from the registrar (the dead process's last will),
+    retires the RCCL/gloo links to it, re-sends every frame it held (their staged bytes) to the
+    surviving replica / the local share, and every frame completes with the single-process
+    values in bounded time — the reference's remote-absent swap
+    (/root/reference/src/aiko_services/main/pipeline.py:975-1006) made frame-safe."""
+    path, d = _variant(os.path.join(DEFS, "tensor_ppdp.json"), frames=16, hop_timeout=30)
+    env = dict(cluster["env"], AIKO_FAULTS="kill=2@rank2", AIKO_LOG_LEVEL="INFO")
+    try:
+        t0 = time.time()
+        r, par = _create(env, path, 16, timeout=150)
+        elapsed = time.time() - t0
+    finally:
+        os.unlink(path)
+    text = r.stdout + r.stderr
+    assert len(par) == 16, (r.returncode, text[-4000:])
+    assert elapsed < 120
+    assert "lost with" in text, text[-3000:]                # rank 2 held frames when it died
+    rank0 = re.search(r"hop rank 0 stats: (\{.*\})", text)
+    assert rank0 and "'dead': [2]" in rank0.group(1), text[-3000:]
+    assert _single(cluster, d, 16) == par
+
+
+def test_credit_window_backpressure(cluster):
+    """A frame generator with ``rate`` unset pushes 40 frames through a 3-stage pipeline whose
+    links have 2 credits each: the generator waits for credits (frame_window) and the hop
+    queue, no receive pool ever overflows or waits, and no frame is lost."""
+    path, d = _variant(os.path.join(DEFS, "tensor_pp3.json"), frames=40)
+    env = dict(cluster["env"], AIKO_HOP_DEPTH="2", AIKO_LOG_LEVEL="INFO")
+    try:
+        r, par = _create(env, path, 40, timeout=150)
+    finally:
+        os.unlink(path)
+    text = r.stdout + r.stderr
+    assert len(par) == 40, (r.returncode, text[-4000:])
+    overflow = [int(v) for v in re.findall(r"'pool_overflow': (\d+)", text)]
+    waits = [int(v) for v in re.findall(r"'pool_waits': (\d+)", text)]
+    assert overflow and max(overflow) == 0 and max(waits) == 0, text[-3000:]
+    assert not re.search(r"dropped [1-9]", text)
