@@ -32,7 +32,7 @@ from dataclasses import asdict, dataclass, field
 
 from ..pipeline.definition import parse_pipeline_definition_dict
 
-__all__ = ["Plan", "RankSpec", "plan_stages", "make_plan", "element_order", "predicted_times",
+__all__ = ["Plan", "RankSpec", "plan_stages", "make_plan", "element_chain", "element_order", "predicted_times",
            "stage_remote_name"]
 
 
@@ -70,8 +70,22 @@ class Plan:
         return cls(**d)
 
 
+def element_chain(definition) -> list:
+    """Element names of a parsed PipelineDefinition in the engine's execution order for its
+    (single) graph path.  Elements exchange data through the frame's swag, so any execution
+    order can be cut into stages."""
+    from collections import OrderedDict
+    from ..utils.graph import Graph, Node
+    heads, successors = Graph.traverse(definition.graph)
+    if len(heads) != 1:
+        raise ValueError("pipeline parallelism needs exactly one graph path")
+    graph = Graph(heads)
+    for name, succ in successors.items():
+        graph.add(Node(name, None, OrderedDict(succ)))
+    return [node.name for node in graph.get_path()]
+
+
 def element_order(definition: dict):
-    from .pipeline_parallel import element_chain
     return element_chain(parse_pipeline_definition_dict(definition))
 
 

@@ -80,13 +80,25 @@ def test_host_ring_never_reuses_a_held_result():
         ring.acquire()
 
 
-def test_stage_link_requires_two_slots():
-    """depth 1 would let the look-ahead receive overwrite the frame in use."""
+def test_hop_credits_hold_until_ack():
+    """Forward hops hold a staging slot (a credit) until the response's ack; with every slot
+    held the link refuses (NoCredit) instead of reusing a buffer a retransmit may need; a dead
+    peer has no credit and keeps its held frames for re-dispatch."""
     import pytest
-    from aiko_services_amd.parallel.pipeline_parallel import StageLink
-    with pytest.raises(ValueError):
-        StageLink(1, "cpu", depth=1)
-    assert StageLink(1, "cpu", depth=2).depth == 2
+    from aiko_services_amd.parallel.hop import HopPlane, NoCredit
+    plane = HopPlane([(0, 0)], device="cpu", depth=2)
+    x = torch.arange(6.0)
+    plane.encode(0, {"x": x}, key=("s", 0))
+    plane.encode(0, {"x": x + 1}, key=("s", 1))
+    assert plane.credit(0) == 0
+    with pytest.raises(NoCredit):
+        plane.encode(0, {"x": x}, key=("s", 2))
+    assert torch.equal(plane.held_values(("s", 1))["x"], x + 1)     # the retransmit buffer
+    plane.ack(("s", 0))
+    assert plane.credit(0) == 1
+    plane.encode(0, {"x": x + 2}, key=("s", 2))
+    assert torch.equal(plane.held_values(("s", 1))["x"], x + 1)     # held slot never reused
+    assert plane.stats()["held_frames"] == 2
 
 
 def test_narrow_variant_eligibility():
