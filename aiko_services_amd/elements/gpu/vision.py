@@ -25,7 +25,7 @@ import torch
 from ...gpu.element import DeviceResult, GpuPipelineElement, HostRing
 from ...pipeline.stream import StreamEvent
 
-__all__ = ["SyntheticFrames", "ImagePreprocess", "ResNet50Classifier", "ClassifierTopK"]
+__all__ = ["SyntheticFrames", "FrameResize", "ImagePreprocess", "ResNet50Classifier", "ClassifierTopK"]
 
 
 def _int(v, d):
@@ -121,6 +121,31 @@ class SyntheticFrames(GpuPipelineElement):
             self.share["frames_dropped"] = self.dropped
             return StreamEvent.DROP_FRAME, {"diagnostic": "frame pool exhausted"}
         return StreamEvent.OKAY, {"images": frames, "t_submit": kwargs.get("t_submit", time.perf_counter())}
+
+
+class FrameResize(GpuPipelineElement):
+    """The "resize" stage of config 3: bilinear uint8 -> uint8 resize of a frame batch to
+    ``image_size`` (square) on the GPU.  Placed before a stage cut it makes the boundary the
+    small uint8 frame (150 KB per 224² frame) instead of the normalised bf16 stem buffer
+    (427 KB): ResNet50Classifier accepts uint8 frames and pre-processes them itself."""
+    lane_safe = True
+
+    def __init__(self, context):
+        context.set_protocol("frame_resize:0")
+        super().__init__(context)
+        self.size = _int(self.get_parameter("image_size", 224)[0], 224)
+        self._out = {}
+
+    def process_frame(self, stream, images):
+        from ...ops import vision as V
+        B = images.shape[0]
+        if images.shape[1] == self.size and images.shape[2] == self.size:
+            return StreamEvent.OKAY, {"images": images}
+        out = self._out.get((B, self.lane))
+        if out is None:
+            out = self._out[(B, self.lane)] = torch.empty(B, self.size, self.size, 3, dtype=torch.uint8,
+                                                          device=self.device)
+        return StreamEvent.OKAY, {"images": V.resize_u8(images, (self.size, self.size), out=out)}
 
 
 class ImagePreprocess(GpuPipelineElement):
@@ -249,6 +274,18 @@ class ClassifierTopK(GpuPipelineElement):
             D.all_gather_into(all_prob, prob)
             D.all_gather_into(all_index, index)
             flat = b["all"]
+        frame = self.pipeline.current_frame() if self.pipeline is not None else None
+        if getattr(frame, "hop_reply", None) is not None:
+            # this stage answers a remote hop: the result goes back as DEVICE tensors (the hop
+            # packs them on this stream); the requester decides whether it needs them on the host
+            hp, hi = self._split(flat, world * B, self.k)
+            ev = None
+            if self.device.type == "cuda":
+                ev = torch.cuda.Event()
+                ev.record()
+            return StreamEvent.OKAY, {"topk": DeviceResult(
+                {"top_prob": hp, "top_index": hi}, ev,
+                t_submit=t_submit if isinstance(t_submit, (float, torch.Tensor)) else None)}
         slot, host = b["host"].acquire()
         host.copy_(flat, non_blocking=True)
         hp, hi = self._split(host, world * B, self.k)

@@ -20,7 +20,7 @@ from __future__ import annotations
 
 import threading
 
-__all__ = ["current_lane", "lane_scope", "lane_stream"]
+__all__ = ["current_lane", "in_lane", "lane_scope", "lane_stream"]
 
 _tls = threading.local()
 _STREAMS: dict = {}
@@ -29,6 +29,12 @@ _STREAMS: dict = {}
 def current_lane() -> int:
     """Lane index of the frame being processed on this thread (0 outside lanes)."""
     return getattr(_tls, "lane", 0)
+
+
+def in_lane() -> bool:
+    """Whether this thread is inside a :class:`lane_scope` (a nested pipeline — e.g. rank 0's
+    local share of a replicated stage — then keeps the enclosing frame's lane)."""
+    return getattr(_tls, "depth", 0) > 0
 
 
 def lane_stream(device, lane: int):
@@ -59,9 +65,11 @@ class lane_scope:
         self._ctx.__enter__()
         self._prev = current_lane()
         _tls.lane = self.lane
+        _tls.depth = getattr(_tls, "depth", 0) + 1
         return self
 
     def __exit__(self, *exc):
         _tls.lane = self._prev
+        _tls.depth -= 1
         self._ctx.__exit__(*exc)
         return False

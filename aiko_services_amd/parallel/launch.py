@@ -109,8 +109,8 @@ def create_rank_pipeline(plan: Plan, rank: int, stream_id=None, parameters=None,
         local_def = None
         weight = 0.0
         if spec.stage == 0 and plan.local_share > 0:
-            nxt = next(r for r in plan.ranks if r.stage == 1)
-            local_def = parse_pipeline_definition_dict(nxt.definition)
+            nxt = plan.stage_defs[1] if plan.stage_defs else next(r for r in plan.ranks if r.stage == 1).definition
+            local_def = parse_pipeline_definition_dict(nxt)
             weight = plan.local_share
         expected = plan.replicas[spec.stage + 1] + (1 if local_def is not None else 0)
         pipeline.set_remote_replicas(remote, expected, local_def, weight)

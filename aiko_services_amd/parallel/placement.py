@@ -33,6 +33,7 @@ from dataclasses import asdict, dataclass, field
 from ..pipeline.definition import parse_pipeline_definition_dict
 
 __all__ = ["Plan", "RankSpec", "plan_stages", "make_plan", "element_chain", "element_order", "predicted_times",
+           "boundary_ms_from_bytes",
            "stage_remote_name"]
 
 
@@ -59,6 +60,7 @@ class Plan:
     links: list                # [[src, dst]] hop directions (one RCCL communicator each)
     predicted_ms: dict = field(default_factory=dict)
     stream: dict = field(default_factory=dict)   # dp: every rank creates this stream
+    stage_defs: list = field(default_factory=list)   # PipelineDefinition (JSON) of every stage
 
     def to_json(self) -> str:
         return json.dumps(asdict(self))
@@ -211,11 +213,18 @@ def _dp_plan(definition: dict, gpus: int, group: str | None) -> Plan:
                 local_share=0.0, ranks=ranks, links=[])
 
 
+def boundary_ms_from_bytes(boundary_bytes: dict, link_gbps: float) -> dict:
+    """Transfer cost of each element's output over one xGMI link: ``bytes / link rate`` (ms
+    per frame batch) — the balancer's ``boundary_ms``."""
+    return {k: float(v) / (float(link_gbps) * 1e9) * 1e3 for k, v in boundary_bytes.items()}
+
+
 def make_plan(definition: dict, gpus: int | None = None, stages=None, replicas=None,
               local_share: float = 0.0, times_ms: dict | None = None, group: str | None = None,
-              device_offset: int = 0) -> Plan:
+              device_offset: int = 0, boundary_ms: dict | None = None) -> Plan:
     """Plan for ``definition`` (a JSON dict).  Stages come from (in order) ``stages``, the
-    elements' ``deploy.local.stage``, the balancer (``times_ms``), or one element per stage."""
+    elements' ``deploy.local.stage``, the balancer (``times_ms`` and ``boundary_ms``: per
+    element, the cost of shipping its output to the next stage), or one element per stage."""
     par = definition.get("parallel") or {}
     mode = par.get("mode", "pp")
     gpus = int(gpus or par.get("gpus", 1))
@@ -227,6 +236,8 @@ def make_plan(definition: dict, gpus: int | None = None, stages=None, replicas=N
         local_share = float(par["local_share"])
     if times_ms is None and par.get("times_ms"):
         times_ms = {k: float(v) for k, v in par["times_ms"].items()}
+    if boundary_ms is None and par.get("boundary_ms"):
+        boundary_ms = {k: float(v) for k, v in par["boundary_ms"].items()}
     order = element_order(definition)
     by = {e["name"]: e for e in definition["elements"]}
     predicted = {}
@@ -239,8 +250,11 @@ def make_plan(definition: dict, gpus: int | None = None, stages=None, replicas=N
                 stages[int(s)].append(n)
             stages = [s for s in stages if s]
         elif times_ms:
-            stages, replicas, local_share, per_rank = plan_stages(order, times_ms, gpus)
+            stages, replicas, local_share, per_rank = plan_stages(order, times_ms, gpus,
+                                                                  boundary_ms=boundary_ms)
             predicted = {"per_rank_ms": [round(x, 4) for x in per_rank]}
+            if boundary_ms:
+                predicted["boundary_ms"] = {s[-1]: round(boundary_ms.get(s[-1], 0.0), 4) for s in stages[:-1]}
         else:
             k = min(gpus, len(order))
             sizes = [len(order) // k + (1 if i < len(order) % k else 0) for i in range(k)]
@@ -250,6 +264,8 @@ def make_plan(definition: dict, gpus: int | None = None, stages=None, replicas=N
                 at += size
     if replicas is None:
         replicas = [1] * len(stages)
+    if any(r < 0 for r in replicas) or (replicas[-1] == 0 and not local_share):
+        raise ValueError(f"replicas {replicas}: a stage needs a rank or (the last) a local share")
         replicas[-1] += max(0, gpus - sum(replicas)) if par.get("replicate_last", False) else 0
     if len(replicas) != len(stages) or replicas[0] != 1:
         raise ValueError(f"replicas {replicas} must match stages {stages} and start with 1")
@@ -264,6 +280,7 @@ def make_plan(definition: dict, gpus: int | None = None, stages=None, replicas=N
     world = r
     last = len(stages) - 1
     ranks = []
+    stage_defs = []
     for s, names in enumerate(stages):
         elements = [_strip_stage(by[n]) for n in names]
         graph_names = list(names)
@@ -280,10 +297,13 @@ def make_plan(definition: dict, gpus: int | None = None, stages=None, replicas=N
             graph_names.append(remote_name)
         d = {k: copy.deepcopy(v) for k, v in definition.items() if k not in ("elements", "graph", "parallel")}
         d["name"] = stage_remote_name(base, s)
-        if s < last:                 # frame lanes need a fully local graph
-            d["parameters"] = dict(d.get("parameters") or {}, gpu_lanes=1)
+        # every stage keeps the definition's gpu_lanes: a stage ending in a remote element runs
+        # its local prefix on the frame's lane and resumes the response on it (engine Frame.lane);
+        # rank 0's local share of the last stage runs in the enclosing frame's lane, so the
+        # balancer's element times (measured with lanes) hold on every rank
         d["graph"] = [f"({' '.join(graph_names)})"]
         d["elements"] = elements
+        stage_defs.append(d)
         reps = replicas[s]
         for i, rank in enumerate(rank_of_stage[s]):
             w = 1.0
@@ -301,4 +321,5 @@ def make_plan(definition: dict, gpus: int | None = None, stages=None, replicas=N
     if local_share > 0 and last != 1:
         raise ValueError("local_share needs a two-stage plan (rank 0 hosts a copy of stage 1)")
     return Plan(group=group, world=world, mode=mode, stages=stages, replicas=list(replicas),
-                local_share=float(local_share), ranks=ranks, links=links, predicted_ms=predicted)
+                local_share=float(local_share), ranks=ranks, links=links, predicted_ms=predicted,
+                stage_defs=stage_defs)

@@ -692,6 +692,8 @@ class PipelineImpl(Pipeline):
                 hop.release([hop_handle])
             return None, None, None
         frame = stream.frames[stream.frame_id]
+        if new_frame:
+            frame.lane = getattr(self, "_frame_lane", None) if self._frame_lanes()[0] > 1 else None
         if hop_handle is not None:
             frame.hop_handles.append(hop_handle)
         if new_frame and stream_dict.get("hop_rank") is not None:
@@ -748,7 +750,9 @@ class PipelineImpl(Pipeline):
             for node in self.pipeline_graph:
                 element, name, local, _ = PipelineGraph.get_element(node)
                 if not local:
-                    raise ValueError(f"gpu_lanes > 1 needs a fully local pipeline ({name} is remote)")
+                    # a remote element ends the local part of the frame; its response resumes the
+                    # frame on the lane it started on (Frame.lane)
+                    continue
                 if hasattr(element, "device") and hasattr(element, "run_maybe_captured"):
                     if not getattr(element, "lane_safe", False):
                         raise ValueError(f"gpu_lanes > 1: GPU element {name} is not lane-safe")
@@ -763,9 +767,25 @@ class PipelineImpl(Pipeline):
     def _process_frame_common(self, stream_dict, frame_data_in, new_frame):
         lanes, device = self._frame_lanes()
         if lanes > 1:
-            from ..gpu.lanes import lane_scope
-            lane = self._lane_next
-            self._lane_next = (lane + 1) % lanes
+            from ..gpu.lanes import in_lane, lane_scope
+            if in_lane():
+                # nested pipeline (rank 0's local share of a replicated stage): the frame keeps
+                # the lane of the enclosing frame
+                return self._process_frame_body(stream_dict, frame_data_in, new_frame)
+            lane = None
+            if not new_frame:
+                # a remote hop's response resumes the frame on the lane it started on
+                lease = self.stream_leases.get(str(stream_dict.get("stream_id"))) \
+                    if isinstance(stream_dict, dict) else None
+                try:
+                    frame = lease.stream.frames.get(int(stream_dict.get("frame_id"))) if lease else None
+                except (TypeError, ValueError):
+                    frame = None
+                lane = getattr(frame, "lane", None)
+            if lane is None:
+                lane = self._lane_next
+                self._lane_next = (lane + 1) % lanes
+            self._frame_lane = lane
             with lane_scope(lane, device):
                 return self._process_frame_body(stream_dict, frame_data_in, new_frame)
         return self._process_frame_body(stream_dict, frame_data_in, new_frame)

@@ -60,6 +60,7 @@ class Frame:
     hop_handles: list = field(default_factory=list)   # RCCL receive slots held by this frame
     hop_reply: int = None          # rank to send the response tensors to (remote hop)
     on_complete: list = field(default_factory=list)   # callbacks when the frame completes
+    lane: int = None               # frame lane (gpu_lanes > 1): a hop's response resumes on it
 
 
 @dataclass

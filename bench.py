@@ -127,8 +127,10 @@ def pp_definition(batch: int, graph: bool, height: int, width: int, world: int, 
     ``world`` GPUs by the balancer (``parallel/placement.py``)."""
     d = definition(batch, graph, height, width, lanes)
     d["name"] = "p_resnet50_pp"
-    d["graph"] = ["(SyntheticFrames ImagePreprocess ResNet50Classifier ClassifierTopK)"]
-    pre = {"name": "ImagePreprocess", "input": [{"name": "images", "type": "tensor"}],
+    d["graph"] = ["(SyntheticFrames FrameResize ResNet50Classifier ClassifierTopK)"]
+    # resize stays uint8 (224x224x3): cut after it, the stage boundary is 150 KB per frame; the
+    # ResNet stage normalises into its stem buffer itself
+    pre = {"name": "FrameResize", "input": [{"name": "images", "type": "tensor"}],
            "output": [{"name": "images", "type": "tensor"}], "parameters": {"image_size": 224},
            "deploy": {"local": {"module": ELEMENTS}}}
     d["elements"].insert(1, pre)
@@ -162,6 +164,8 @@ def main(argv=None):
                     help="(whisper) decode this many tokens per window (speech-to-text) instead of pooling features")
     ap.add_argument("--fanout", choices=["scatter", "broadcast"], default="scatter",
                     help="(yolov8n) RCCL fan-out of the ingest rank's frame batch")
+    ap.add_argument("--link-gbps", type=float, default=50.0,
+                    help="(pp) xGMI point-to-point rate the balancer prices stage boundaries at")
     ap.add_argument("--parallel", choices=["dp", "pp"], default="dp",
                     help="dp: every GPU runs the whole pipeline (config 2/headline); "
                          "pp: config 3 as balanced multi-GPU actor pipelines (stages + replicas, "
@@ -301,8 +305,14 @@ def main(argv=None):
 
 # per-element GPU ms per 256-frame batch on one MI355X (VGA frames), the balancer's default input
 # (override: --element-times '{"ResNet50Classifier": 3.3, ...}')
-PP_ELEMENT_MS = {"SyntheticFrames": 0.01, "ImagePreprocess": 0.12, "ResNet50Classifier": 3.35,
+PP_ELEMENT_MS = {"SyntheticFrames": 0.01, "FrameResize": 0.06, "ResNet50Classifier": 3.0,
                  "ClassifierTopK": 0.03}
+
+
+def pp_boundary_bytes(batch: int, height: int, width: int) -> dict:
+    """Bytes each element hands to the next per frame batch (the hop payload if cut there)."""
+    return {"SyntheticFrames": batch * height * width * 3, "FrameResize": batch * 224 * 224 * 3,
+            "ResNet50Classifier": batch * 1000 * 2, "ClassifierTopK": batch * 5 * 8}
 
 
 def _control_plane(ws, rank):
@@ -349,7 +359,16 @@ def run_pp(a, device, procs):
     ws, rank = D.world_size(), D.rank()
     times = dict(PP_ELEMENT_MS, **(json.loads(a.element_times) if a.element_times else {}))
     d = pp_definition(a.batch, not a.no_graph, a.height, a.width, ws, a.lanes)
-    plan = make_plan(d, gpus=ws, times_ms=times, group=f"bench{os.environ.get('MASTER_PORT', '0')}")
+    from aiko_services_amd.parallel.placement import boundary_ms_from_bytes
+    boundary = boundary_ms_from_bytes(pp_boundary_bytes(a.batch, a.height, a.width), a.link_gbps)
+    if ws == 1:
+        # one GPU: the two-stage actor topology with the ResNet stage as rank 0's local share
+        # (exercises the hop-free LocalStage path, frame lanes across the stage boundary)
+        plan = make_plan(d, gpus=1, stages=[["SyntheticFrames", "FrameResize"], ["ResNet50Classifier", "ClassifierTopK"]],
+                         replicas=[1, 0], local_share=1.0, group=f"bench{os.environ.get('MASTER_PORT', '0')}")
+    else:
+        plan = make_plan(d, gpus=ws, times_ms=times, group=f"bench{os.environ.get('MASTER_PORT', '0')}",
+                         boundary_ms=boundary)
     plane = hop.init_plane(plan.links, device=device, depth=4)
     responses: queue.Queue = queue.Queue()
     pipeline = create_rank_pipeline(plan, rank, queue_response=responses if rank == 0 else None,
@@ -457,7 +476,10 @@ def _drive_pp(a, pipeline, plane, plan, responses, rank, ws):
                    "predicted_rank_ms": plan.predicted_ms.get("per_rank_ms"),
                    "transport": "actor pipelines: MQTT metadata + RCCL P2P tensors",
                    "hop": plane.stats(),
-                   "pipeline": "(SyntheticFrames ImagePreprocess ResNet50Classifier ClassifierTopK)"},
+                   "hop_bytes_per_frame": round(plane.counters["sent_bytes"] / max(1, plane.counters["sent_msgs"])
+                                                / a.batch),
+                   "boundary_ms": plan.predicted_ms.get("boundary_ms"),
+                   "pipeline": "(SyntheticFrames FrameResize ResNet50Classifier ClassifierTopK)"},
     }
 
 

@@ -226,3 +226,22 @@ def test_credit_window_backpressure(cluster):
     waits = [int(v) for v in re.findall(r"'pool_waits': (\d+)", text)]
     assert overflow and max(overflow) == 0 and max(waits) == 0, text[-3000:]
     assert not re.search(r"dropped [1-9]", text)
+
+
+def test_balancer_prices_stage_boundaries():
+    """Config 3 with transfer costs (bytes / xGMI rate): the cut goes after the uint8 resize
+    (38.5 MB per 256-frame batch) rather than after decode (236 MB of VGA frames); make the
+    resize output the expensive one instead and the cut moves before it."""
+    import bench
+    from aiko_services_amd.parallel.placement import boundary_ms_from_bytes, plan_stages
+    order = ["SyntheticFrames", "FrameResize", "ResNet50Classifier", "ClassifierTopK"]
+    times = dict(bench.PP_ELEMENT_MS)
+    real = boundary_ms_from_bytes(bench.pp_boundary_bytes(256, 480, 640), 50.0)
+    assert 0.7 < real["FrameResize"] < 0.8 and real["SyntheticFrames"] > 4.0
+    for gpus in (2, 4, 8):
+        stages, reps, share, per_rank = plan_stages(order, times, gpus, boundary_ms=real)
+        assert stages[0] == ["SyntheticFrames", "FrameResize"], (gpus, stages)
+        assert max(per_rank) <= 1.2 * min(per_rank), (gpus, per_rank)
+    flipped = dict(real, SyntheticFrames=0.01, FrameResize=5.0)
+    stages, _, _, _ = plan_stages(order, times, 4, boundary_ms=flipped)
+    assert stages[0] == ["SyntheticFrames"], stages
