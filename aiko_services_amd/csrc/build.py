@@ -71,7 +71,37 @@ def _compile(src: Path, flags, headers) -> Path:
     return obj
 
 
+def build_host_modules(force: bool = False, verbose: bool = True) -> list:
+    """CPython extension modules of the control plane (``csrc/host/*.c`` ->
+    ``aiko_services_amd/_<name>.so``): plain C against the Python C API, no torch, no HIP, so
+    CPU-only processes (brokers, registrars, CPU tests) load them too."""
+    BUILD.mkdir(exist_ok=True)
+    py_inc = sysconfig.get_paths()["include"]
+    cc = os.environ.get("CC") or shutil.which("gcc") or shutil.which("cc") or "cc"
+    flags = ["-O2", "-shared", "-fPIC", "-Wall", "-Werror", "-I", py_inc]
+    out = []
+    for src in sorted((CSRC / "host").glob("*.c")):
+        so = PKG / f"_{src.stem}.so"
+        key = _hash([src], flags)
+        stamp = BUILD / f"host_{src.stem}.stamp"
+        if so.exists() and stamp.exists() and stamp.read_text() == key and not force:
+            out.append(so)
+            continue
+        tmp = so.with_suffix(".tmp.so")
+        cmd = [cc, *flags, str(src), "-o", str(tmp)]
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
+        tmp.replace(so)
+        stamp.write_text(key)
+        if verbose:
+            print(f"[aiko build] built {so}")
+        out.append(so)
+    return out
+
+
 def build(force: bool = False, debug: bool = False, jobs: int | None = None, verbose: bool = True) -> Path:
+    build_host_modules(force=force, verbose=verbose)
     BUILD.mkdir(exist_ok=True)
     kernels, runtime, binding = sources()
     tinc, tlib = _torch_paths()

@@ -62,6 +62,7 @@ _ALIGN = 256
 _DTYPES = {str(dt).split(".")[-1]: dt for dt in
            (torch.uint8, torch.int8, torch.int16, torch.int32, torch.int64, torch.float16,
             torch.float32, torch.float64, torch.bfloat16, torch.bool)}
+_DTYPE_NAMES = {dt: name for name, dt in _DTYPES.items()}
 
 
 class StageFailure(RuntimeError):
@@ -96,7 +97,7 @@ def needs_decode(stream_dict, values) -> bool:
 
 
 def _nbytes(dtype, shape) -> int:
-    n = torch.empty((), dtype=dtype).element_size()
+    n = dtype.itemsize
     for d in shape:
         n *= int(d)
     return n
@@ -114,6 +115,29 @@ def _layout(specs):
 def _view(buf: torch.Tensor, off: int, dtype, shape) -> torch.Tensor:
     n = _nbytes(dtype, shape)
     return buf[off:off + n].view(dtype).view(shape)
+
+
+def _views(buf: torch.Tensor, offs, specs) -> list:
+    """Typed views of ``specs`` [(dtype, shape)] at byte offsets ``offs`` of the uint8 buffer:
+    one ``view(dtype)`` per distinct dtype + one ``as_strided`` per tensor (the offsets are
+    256-byte aligned), instead of slice + two views per tensor."""
+    typed = {}
+    out = []
+    nbytes = buf.numel()
+    for off, (dt, shape) in zip(offs, specs):
+        size = dt.itemsize
+        if nbytes % size:
+            out.append(_view(buf, off, dt, shape))
+            continue
+        base = typed.get(dt)
+        if base is None:
+            base = typed[dt] = buf.view(dt)
+        stride, acc = [], 1
+        for d in reversed(shape):
+            stride.append(acc)
+            acc *= d
+        out.append(base.as_strided(shape, tuple(reversed(stride)), base.storage_offset() + off // size))
+    return out
 
 
 def _parse(tok: str):
@@ -140,17 +164,19 @@ def _retoken(values: dict, seq: int) -> dict:
 class _SendLink:
     """This rank -> ``peer``: process group + ``depth`` staging slots (credits)."""
 
-    def __init__(self, peer, group, device, depth):
+    def __init__(self, peer, group, device, depth, grank=0):
         self.peer, self.group, self.device = peer, group, device
+        self.grank = grank                  # the peer's rank within the link's 2-rank group
         self.bufs = [None] * depth
         self.work = [None] * depth          # last transfer that read the slot's buffer
         self.holder = [None] * depth        # frame key holding the slot until its ack
+        self.free = depth                   # slots with no holder (the link's credits)
         self.cursor = 0
         self.seq = 0
         self.dead = False
 
     def credit(self) -> int:
-        return 0 if self.dead else sum(h is None for h in self.holder)
+        return 0 if self.dead else self.free
 
     def take(self, nbytes, key):
         if self.dead:
@@ -171,9 +197,12 @@ class _SendLink:
         if buf is None or buf.numel() < nbytes:
             buf = self.bufs[slot] = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
         self.holder[slot] = key
+        self.free -= 1
         return slot, buf
 
     def release(self, slot, reuse=True):
+        if self.holder[slot] is not None:
+            self.free += 1
         self.holder[slot] = None
         if not reuse:                        # a transfer that may never finish still owns it
             self.work[slot] = None
@@ -185,6 +214,7 @@ class _SendLink:
         keys = [k for k in self.holder if k is not None]
         n = len(self.bufs)
         self.bufs, self.work, self.holder = [None] * n, [None] * n, [None] * n
+        self.free = 0
         return keys
 
     def drain(self):
@@ -199,8 +229,9 @@ class _SendLink:
 class _RecvLink:
     """``peer`` -> this rank: process group + FramePool of receive slots (the sender's credits)."""
 
-    def __init__(self, peer, group, device, depth):
+    def __init__(self, peer, group, device, depth, grank=0):
         self.peer, self.group, self.device, self.depth = peer, group, device, depth
+        self.grank = grank
         self.pool = None
         self.seq = 0
         self.dead = False
@@ -227,6 +258,14 @@ class _RecvLink:
         return (pool, s), pool.view(s, (pool.slot_bytes,), torch.uint8)
 
 
+class _SharedSlot:
+    """A receive slot shared by the members of a group message: free after the last release."""
+    __slots__ = ("pool", "slot", "count")
+
+    def __init__(self, pool, slot, count):
+        self.pool, self.slot, self.count = pool, slot, count
+
+
 class HopPlane:
     """Per-process RCCL data plane of the remote hops (see module docstring).
 
@@ -247,21 +286,25 @@ class HopPlane:
         self.recv_links: dict = {}
         self.links = [tuple(int(x) for x in l) for l in links]
         self.dead: set = set()
-        self._held: dict = {}              # frame key -> [dst, slot, total, specs, template]
+        self._held: dict = {}              # frame / group key -> record (see _encode_many)
         self._loop: deque = deque()        # loopback link (src == dst): staged buffers in order
         self._groups: dict = {}            # (src, dst) -> process group
+        self._waits = None                 # finish_later queue (host transfers), thread on first use
+        self._member_of: dict = {}         # frame key -> group key (encode_group)
+        self._group_seq = 0
         for src, dst in self.links:
             if src == dst:
                 if src == self.rank:
                     self.send_links[dst] = _SendLink(dst, None, self.device, self.depth)
                     self.recv_links[src] = _RecvLink(src, None, self.device, self.depth)
                 continue
-            group = tdist.new_group(ranks=sorted({src, dst})) if D.is_initialized() else None
+            members = sorted({src, dst})
+            group = tdist.new_group(ranks=members) if D.is_initialized() else None
             self._groups[(src, dst)] = group
             if src == self.rank:
-                self.send_links[dst] = _SendLink(dst, group, self.device, self.depth)
+                self.send_links[dst] = _SendLink(dst, group, self.device, self.depth, members.index(dst))
             elif dst == self.rank:
-                self.recv_links[src] = _RecvLink(src, group, self.device, self.depth)
+                self.recv_links[src] = _RecvLink(src, group, self.device, self.depth, members.index(src))
         # Bring every link's communicator up now, in the same global order on every rank: RCCL
         # creates a P2P communicator lazily at the first send/recv and blocks until the peer
         # joins, but the peer only posts its receive once the frame's MQTT message arrives —
@@ -291,24 +334,41 @@ class HopPlane:
     def is_dead(self, rank: int) -> bool:
         return int(rank) in self.dead
 
-    def ack(self, key) -> None:
-        """The response of forward frame ``key`` arrived: its staging slot is a credit again."""
-        rec = self._held.pop(key, None)
-        if rec is None:
-            return
-        link = self.send_links.get(rec[0])
-        if link is not None and not link.dead:
-            link.release(rec[1])
+    def grouped(self, key) -> bool:
+        """Whether held forward frame ``key`` travelled in a group message (:meth:`encode_group`)."""
+        return key in self._member_of
+
+    def ack(self, key) -> bool:
+        """The response of forward frame ``key`` arrived: its staging slot is a credit again
+        (a group's slot once every member is acknowledged or dropped).  True if a credit
+        returned."""
+        return self._settle(key, reuse=True)
 
     def drop(self, key) -> None:
         """Abandon forward frame ``key`` (ERROR / timeout): its slot is not reused while its
         transfer might still be reading it."""
+        self._settle(key, reuse=False)
+
+    def _settle(self, key, reuse):
+        gk = self._member_of.pop(key, None)
+        if gk is not None:
+            rec = self._held.get(gk)
+            if rec is None:
+                return False
+            members = rec[6]
+            members.pop(key, None)
+            rec[7] = rec[7] and reuse
+            if members:
+                return False
+            key, reuse = gk, rec[7]
         rec = self._held.pop(key, None)
         if rec is None:
-            return
+            return False
         link = self.send_links.get(rec[0])
-        if link is not None and not link.dead:
-            link.release(rec[1], reuse=False)
+        if link is not None and not link.dead and rec[1] is not None:
+            link.release(rec[1], reuse=reuse)
+            return True
+        return False
 
     def mark_dead(self, rank: int) -> list:
         """Retire every link to / from ``rank``; returns the keys of the forward frames it held
@@ -324,7 +384,7 @@ class HopPlane:
             for key, rec in self._held.items():
                 if rec[0] == rank:
                     rec[1] = None           # no slot any more: the record alone owns the buffer
-                    keys.append(key)
+                    keys.extend(rec[6] if rec[6] is not None else (key,))
             link.retire()
         rlink = self.recv_links.get(rank)
         if rlink is not None:
@@ -345,6 +405,26 @@ class HopPlane:
         are packed and sent to ``dst``.  ``key`` (forward hops): hold the staging slot until
         :meth:`ack` (raises :class:`NoCredit` when none is free).  Non-tensor values pass
         through unchanged."""
+        return self._encode_many(dst, [values], key)[0]
+
+    def encode_group(self, dst: int, values_list, keys=None) -> list:
+        """Several messages (frames) toward ``dst`` in ONE transfer: one staging slot, one
+        send, one per-link sequence number; returns one token dict per message.  ``keys``
+        (forward hops, one per frame): the slot is ONE credit, held until every member is
+        acknowledged or dropped — control-plane cost per frame falls with the group size."""
+        if keys is None:
+            return self._encode_many(dst, values_list, None)
+        gk = ("group", self._group_seq)
+        self._group_seq += 1
+        outs = self._encode_many(dst, values_list, gk)
+        rec = self._held.get(gk)
+        if rec is not None:
+            rec[6] = {k: i for i, k in enumerate(keys)}
+            for k in keys:
+                self._member_of[k] = gk
+        return outs
+
+    def _encode_many(self, dst, values_list, key):
         from ..gpu.element import DeviceResult
         dst = int(dst)
         link = self.send_links.get(dst)
@@ -362,45 +442,48 @@ class HopPlane:
                 return FLOAT_TOKEN + repr(v)
             return v
 
-        out, slots = {}, []
-        for k, v in values.items():
-            if isinstance(v, DeviceResult):
-                d = {RESULT_KEY: "1"}
-                t = v.t_submit
-                if isinstance(t, torch.Tensor):
-                    t = int(t.reshape(-1)[0]) * 1e-9
-                if isinstance(t, float):
-                    d["_t_submit"] = FLOAT_TOKEN + repr(t)
-                for name, tv in v.tensors.items():
-                    d[name] = tok(tv)
-                    if d[name] is None:
-                        slots.append((d, name, len(tensors) - 1))
-                out[k] = d
-            else:
-                out[k] = tok(v)
-                if out[k] is None:
-                    slots.append((out, k, len(tensors) - 1))
+        outs, slots = [], []
+        for values in values_list:
+            out = {}
+            for k, v in values.items():
+                if isinstance(v, DeviceResult):
+                    d = {RESULT_KEY: "1"}
+                    t = v.t_submit
+                    if isinstance(t, torch.Tensor):
+                        t = int(t.reshape(-1)[0]) * 1e-9
+                    if isinstance(t, float):
+                        d["_t_submit"] = FLOAT_TOKEN + repr(t)
+                    for name, tv in v.tensors.items():
+                        d[name] = tok(tv)
+                        if d[name] is None:
+                            slots.append((d, name, len(tensors) - 1))
+                    out[k] = d
+                else:
+                    out[k] = tok(v)
+                    if out[k] is None:
+                        slots.append((out, k, len(tensors) - 1))
+            outs.append(out)
         if not tensors:
-            return out
+            return outs
         specs = [(t.dtype, tuple(t.shape)) for t in tensors]
         offs, total = _layout(specs)
         slot, buf = link.take(total, key if key is not None else ())
         seq = link.seq
         link.seq += 1
-        for t, off, (dt, shape) in zip(tensors, offs, specs):
-            dstv = _view(buf, off, dt, shape)
+        for t, dstv in zip(tensors, _views(buf, offs, specs)):
             dstv.copy_(t if t.device == buf.device else t.to(buf.device, non_blocking=True),
                        non_blocking=True)
         for container, ckey, idx in slots:
             dt, shape = specs[idx]
-            container[ckey] = (f"{TOKEN}{self.rank}/{seq}/{idx}/{str(dt).split('.')[-1]}/"
-                               + "x".join(str(int(s)) for s in shape))
+            container[ckey] = (f"{TOKEN}{self.rank}/{seq}/{idx}/{_DTYPE_NAMES[dt]}/"
+                               + "x".join(map(str, shape)))
         self._post(link, slot, buf, total, dst)
         if key is not None:
-            self._held[key] = [dst, slot, total, specs, out, buf]
+            # [dst, slot, total, specs, templates, buf, members (groups), slot reusable]
+            self._held[key] = [dst, slot, total, specs, outs, buf, None, True]
         else:
-            link.holder[slot] = None                 # ring slot: free once its transfer is done
-        return out
+            link.release(slot)                       # ring slot: free once its transfer is done
+        return outs
 
     def _post(self, link, slot, buf, total, dst):
         D._account("hop_send", total)
@@ -408,7 +491,8 @@ class HopPlane:
             self._loop.append(buf)
             link.work[slot] = None
         else:
-            link.work[slot] = tdist.isend(buf[:total], dst, group=link.group) if link.group is not None \
+            # the link's process group directly: tdist.isend re-validates group and rank per call
+            link.work[slot] = link.group.send([buf[:total]], link.grank, 0) if link.group is not None \
                 else None
         self.counters["sent_msgs"] += 1
         self.counters["sent_bytes"] += total
@@ -419,11 +503,13 @@ class HopPlane:
         rec = self._held.get(key)
         if rec is None:
             raise KeyError(f"hop: no held frame {key}")
+        if rec[6] is not None:
+            raise ValueError("hop: a group's frames are re-sent one by one (held_values + encode)")
         dst = int(dst)
         link = self.send_links.get(dst)
         if link is None:
             raise StageFailure(dst) if dst in self.dead else RuntimeError(f"hop: no send link to {dst}")
-        old_dst, old_slot, total, specs, template, buf = rec
+        old_dst, old_slot, total, specs, templates, buf = rec[:6]
         old = self.send_links.get(old_dst)
         if old is not None and not old.dead and old_slot is not None:
             old.release(old_slot, reuse=False)        # the buffer moves with the frame
@@ -432,8 +518,8 @@ class HopPlane:
         seq = link.seq
         link.seq += 1
         self._post(link, slot, buf, total, dst)
-        out = _retoken(template, seq)
-        self._held[key] = [dst, slot, total, specs, out, buf]
+        out = _retoken(templates[0], seq)
+        self._held[key] = [dst, slot, total, specs, [out], buf, None, True]
         self.counters["resent"] += 1
         return out
 
@@ -441,10 +527,16 @@ class HopPlane:
         """The held forward frame ``key`` as tensors (views of its staging buffer), e.g. to run
         it on a local replica after its remote peer died.  The frame keeps its record until
         :meth:`ack` / :meth:`drop`."""
-        rec = self._held[key]
-        _dst, _slot, total, specs, template, buf = rec
+        index = 0
+        gk = self._member_of.get(key)
+        if gk is not None:
+            rec = self._held[gk]
+            index = rec[6][key]
+        else:
+            rec = self._held[key]
+        _dst, _slot, total, specs, templates, buf = rec[:6]
         offs, _ = _layout(specs)
-        return self._materialize(template, buf, offs)
+        return self._materialize(templates[index], buf, offs)
 
     def _materialize(self, template, buf, offs):
         from ..gpu.element import DeviceResult
@@ -466,14 +558,98 @@ class HopPlane:
     # ---- decode (receiver) -----------------------------------------------------------------
     _parse = staticmethod(_parse)
 
+    @property
+    def host_transfers(self) -> bool:
+        """Whether a receive blocks the host until its bytes arrived (gloo, CPU tensors) rather
+        than only ordering the current HIP stream after it (RCCL)."""
+        return self.device.type != "cuda"
+
     def decode(self, values: dict, pooled: bool = True):
         """Inverse of :meth:`encode`: posts the receive of the message's tensors and returns
         ``(values, handle)``; ``handle`` (or None) must be given to :meth:`release` once the
         frame no longer needs the tensors (forward hops, ``pooled=True``).  Raises
         :class:`StageFailure` for a message of a dead peer or a failed transfer."""
+        out, handle, work = self.decode_async(values, pooled)
+        if work is not None:
+            self.finish(work, handle)
+        return out, handle
+
+    def finish(self, work, handle) -> None:
+        """Wait for a receive posted by :meth:`decode_async` (RCCL: the current stream waits,
+        the host does not; gloo: the host blocks), then complete the message's DeviceResults
+        (their event follows the receive).  A transfer error releases the slot and raises
+        :class:`StageFailure`."""
+        try:
+            work[0].wait()
+        except RuntimeError as exc:
+            self.complete(work, handle, exc)
+        self.complete(work, handle, None)
+
+    def complete(self, work, handle, error) -> None:
+        """Second half of :meth:`finish` once the wait is over (on the actor's thread)."""
+        _w, src, results = work
+        if error is not None:
+            if handle is not None:
+                self.release([handle] * (handle.count if isinstance(handle, _SharedSlot) else 1))
+            raise StageFailure(src, error) from error
+        self._results(results)
+
+    def finish_later(self, work, callback) -> None:
+        """Host-blocking transfers (gloo): wait for ``work`` on the plane's waiter thread, then
+        call ``callback(error)`` (None, or the transport's exception) from that thread; the
+        callback hands over to the actor, which calls :meth:`complete`.  The actor keeps
+        dispatching while the bytes of several messages are in flight at once."""
+        q = self._waits
+        if q is None:
+            import queue
+            import threading
+            q = self._waits = queue.SimpleQueue()
+
+            def waiter():
+                while True:
+                    item = q.get()
+                    if item is None:
+                        return
+                    w, cb = item
+                    try:
+                        w[0].wait()
+                        err = None
+                    except RuntimeError as exc:
+                        err = exc
+                    cb(err)
+
+            threading.Thread(target=waiter, name="hop-waiter", daemon=True).start()
+        q.put((work, callback))
+
+    def _results(self, results):
         from ..gpu.element import DeviceResult
+        for out, result_keys in results:
+            for k in result_keys:
+                v = out[k]
+                t_submit = v.pop("_t_submit", None)
+                ev = None
+                if self.device.type == "cuda":
+                    ev = torch.cuda.Event()
+                    ev.record()
+                out[k] = DeviceResult(v, ev, t_submit=t_submit)
+
+    def decode_async(self, values: dict, pooled: bool = True):
+        """:meth:`decode` without waiting for the bytes: ``(values, handle, work)``, ``work``
+        (None when nothing is in flight) goes to :meth:`finish` before the values are read.
+        Receives are still POSTED in message order here, so a link stays in order however the
+        waits are scheduled."""
+        outs, handle, work = self._decode_many([values], pooled)
+        return outs[0], handle, work
+
+    def decode_group_async(self, values_list, pooled: bool = True):
+        """:meth:`decode_async` of an :meth:`encode_group` message: ``(values_list, handle,
+        work)``; ``handle`` is shared by the members (give it to :meth:`release` once per
+        member: the slot returns after the last)."""
+        return self._decode_many(values_list, pooled)
+
+    def _decode_many(self, values_list, pooled):
         found = []                   # (container, key, src, seq, idx, dtype, shape)
-        out = {}
+        outs = []
 
         def scan(container_in, container_out):
             for k, v in container_in.items():
@@ -489,9 +665,12 @@ class HopPlane:
                 else:
                     container_out[k] = v
 
-        scan(values, out)
+        for values in values_list:
+            out = {}
+            scan(values, out)
+            outs.append(out)
         if not found:
-            return out, None
+            return outs, None, None
         srcs = {f[2] for f in found}
         seqs = {f[3] for f in found}
         if len(srcs) != 1 or len(seqs) != 1:
@@ -510,42 +689,47 @@ class HopPlane:
         offs, total = _layout(specs)
         if pooled:
             handle, buf = link.slot(total, self)
+            if len(values_list) > 1:
+                handle = _SharedSlot(handle[0], handle[1], len(values_list))
         else:
             handle, buf = None, torch.empty(total, dtype=torch.uint8, device=self.device)
         D._account("hop_recv", total)
+        work = None
         if src == self.rank:
             buf[:total].copy_(self._loop.popleft()[:total], non_blocking=True)
         elif link.group is not None:
             try:
-                tdist.irecv(buf[:total], src, group=link.group).wait()    # RCCL: the stream waits
+                work = link.group.recv([buf[:total]], link.grank, 0)
             except RuntimeError as exc:
                 if handle is not None:
                     self.release([handle])
                 raise StageFailure(src, exc) from exc
         self.counters["recv_msgs"] += 1
         self.counters["recv_bytes"] += total
-        for f, off in zip(found, offs):
-            container, ckey = f[0], f[1]
-            container[ckey] = _view(buf, off, f[5], f[6])
-        # rebuild DeviceResults: completion event after the receive on this stream
-        for k, v in list(out.items()):
-            if isinstance(v, dict) and isinstance(values.get(k), dict) and RESULT_KEY in values[k]:
-                t_submit = v.pop("_t_submit", None)
-                ev = None
-                if self.device.type == "cuda":
-                    ev = torch.cuda.Event()
-                    ev.record()
-                out[k] = DeviceResult(v, ev, t_submit=t_submit)
-        return out, handle
+        for f, v in zip(found, _views(buf, offs, specs)):
+            f[0][f[1]] = v
+        # DeviceResults are rebuilt once the receive is ordered (their completion event follows it)
+        results = [(out, [k for k, v in values.items() if isinstance(v, dict) and RESULT_KEY in v])
+                   for out, values in zip(outs, values_list)]
+        if work is None:
+            self._results(results)
+            return outs, handle, None
+        return outs, handle, (work, src, results)
 
     # ---- slot release ------------------------------------------------------------------------
     def release(self, handles) -> None:
         """Return receive slots once the work queued so far on the current stream is done
         (``FramePool.release_after``: a HIP event gates the reuse)."""
         for h in handles or []:
-            if h is not None:
-                pool, slot = h
-                pool.release_after(slot)
+            if h is None:
+                continue
+            if isinstance(h, _SharedSlot):
+                h.count -= 1
+                if h.count > 0:
+                    continue
+                h = (h.pool, h.slot)
+            pool, slot = h
+            pool.release_after(slot)
 
     def barrier(self):
         if self.control is not None:
@@ -553,7 +737,7 @@ class HopPlane:
 
     def stats(self) -> dict:
         s = dict(self.counters)
-        s["held_frames"] = len(self._held)
+        s["held_frames"] = sum(1 if rec[6] is None else len(rec[6]) for rec in self._held.values())
         for dst, link in self.send_links.items():
             s[f"credit_to_{dst}"] = link.credit()
         for src, link in self.recv_links.items():
@@ -564,6 +748,8 @@ class HopPlane:
         return s
 
     def close(self):
+        if self._waits is not None:
+            self._waits.put(None)
         for link in self.send_links.values():
             link.drain()
         if self.device.type == "cuda":

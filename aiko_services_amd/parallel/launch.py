@@ -168,6 +168,38 @@ def _watch_parent():
     event.add_timer_handler(check, 0.5)
 
 
+def _sample_main_thread(path, period=0.005):
+    """Statistical profiler of the event-loop thread (cProfile does not see time spent in C
+    without a Python frame change): every ``period`` s record the innermost 6 frames."""
+    import collections
+    import traceback
+    main_id = threading.main_thread().ident
+    counts = collections.Counter()
+    clock = time.pthread_getcpuclockid(main_id)
+    start = (time.perf_counter(), time.clock_gettime(clock), os.times())
+
+    def run():
+        while True:
+            time.sleep(period)
+            frame = sys._current_frames().get(main_id)
+            if frame is not None:
+                stack = traceback.extract_stack(frame)[-6:]
+                counts[" <- ".join(f"{os.path.basename(f.filename)}:{f.lineno}:{f.name}"
+                                   for f in reversed(stack))] += 1
+
+    def dump():
+        with open(path, "w") as f:
+            wall = time.perf_counter() - start[0]
+            t = os.times()
+            f.write(f"wall {wall:.2f}s main-thread cpu {time.clock_gettime(clock) - start[1]:.2f}s "
+                    f"process user {t.user - start[2].user:.2f}s sys {t.system - start[2].system:.2f}s\n")
+            total = sum(counts.values()) or 1
+            for stack, n in counts.most_common(40):
+                f.write(f"{100.0 * n / total:5.1f}% {stack}\n")
+    threading.Thread(target=run, daemon=True).start()
+    atexit.register(dump)
+
+
 def worker_main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
     if len(argv) != 3 or argv[0] != "worker":
@@ -178,6 +210,20 @@ def worker_main(argv=None):
     join(plan, rank)
     pipeline = create_rank_pipeline(plan, rank)
     _watch_parent()
+    if os.environ.get("AIKO_WORKER_SAMPLE"):             # sampled main-thread stacks -> DIR/worker_R.txt
+        _sample_main_thread(os.path.join(os.environ["AIKO_WORKER_SAMPLE"], f"worker_{rank}.txt"))
+    prof_dir = os.environ.get("AIKO_WORKER_PROFILE")      # cProfile of each worker's event loop
+    if not prof_dir:
+        pipeline.run(mqtt_connection_required=True)
+        return
+    import cProfile
+    prof = cProfile.Profile()
+
+    def dump():
+        prof.disable()
+        prof.dump_stats(os.path.join(prof_dir, f"worker_{rank}.prof"))
+    atexit.register(dump)
+    prof.enable()
     pipeline.run(mqtt_connection_required=True)
 
 

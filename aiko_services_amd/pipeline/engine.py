@@ -60,6 +60,7 @@ PROTOCOL_ELEMENT = f"{ServiceProtocol.AIKO}/{ACTOR_TYPE_ELEMENT}:{_VERSION}"
 GRACE_TIME = 60
 STATUS_UPDATE_PERIOD = 3.0
 _GPU_TIMING = get_gpu_configuration().timing
+_UNDECODED = object()          # _process_initialize: the message's hop tensors still to receive
 
 _LOGGER = aiko.logger(__name__)
 
@@ -319,6 +320,14 @@ class Pipeline(PipelineElement):
         pass
 
     @abstractmethod
+    def process_frames(self, stream_dicts, frame_datas):
+        """Several frames in one message (a remote hop group, see ``parallel/hop.py``)."""
+
+    @abstractmethod
+    def process_frame_responses(self, stream_dicts, frame_datas):
+        """The responses of several frames in one message."""
+
+    @abstractmethod
     def set_parameter(self, stream_id, name, value):
         pass
 
@@ -343,7 +352,7 @@ class PipelineImpl(Pipeline):
         # remote hops: frames in flight per (stream_id, frame_id), frames waiting for a credit,
         # generator admission window (see dispatch / admit_frame below)
         self._inflight: dict = {}
-        self._pending_hops: deque = deque()
+        self._pending_hops: dict = {}      # remote node name -> FIFO of frames waiting for a credit
         self._admit_cv = threading.Condition()
         self._admitted: set = set()
         self._window_limits: dict = {}
@@ -351,6 +360,9 @@ class PipelineImpl(Pipeline):
         self.hops_failed = 0
         self.hops_redispatched = 0
         self.frames_dropped = 0
+        self.hop_groups = 0                # group messages sent (hop_batch > 1)
+        self._draining = False
+        self._response_batch = None        # replica: responses of a group message, sent as one
         self.pipeline_graph = self._create_pipeline_graph(context.definition)
         self.share["element_count"] = self.pipeline_graph.element_count
         self.share["streams"] = 0
@@ -607,7 +619,7 @@ class PipelineImpl(Pipeline):
             # stream before its own frames — some still to be forwarded — have drained, so a
             # downstream stage can drop the tail of a stream ("stream not found")
             self._post_message(ActorTopic.IN, "destroy_stream", [stream_id, graceful, use_thread_local],
-                               delay=0.05 if self._inflight or self._pending_hops else 1.0)
+                               delay=0.05 if self._inflight or self._pending_total() else 1.0)
             return False
         if self.share["lifecycle"] == "ready":
             for node in self.pipeline_graph.get_path(self.share["graph_path"]):
@@ -660,7 +672,94 @@ class PipelineImpl(Pipeline):
     def process_frame_response(self, stream_dict, frame_data):
         return self._process_frame_common(stream_dict, frame_data, False)
 
-    def _process_initialize(self, stream_dict, frame_data_in, new_frame):
+    # ---- hop groups: several frames per control message + transfer -----------------------------
+    def process_frames(self, stream_dicts, frame_datas):
+        return self._process_group(stream_dicts, frame_datas, True)
+
+    def process_frame_responses(self, stream_dicts, frame_datas):
+        return self._process_group(stream_dicts, frame_datas, False)
+
+    def _process_group(self, stream_dicts, frame_datas, new_frame):
+        """A group message (``hop_batch`` > 1 at the sender): ONE receive for every member's
+        tensors, then each member runs as its own frame.  A replica answers the members that
+        complete here with ONE ``process_frame_responses`` per reply rank."""
+        if not isinstance(stream_dicts, list) or not isinstance(frame_datas, list) \
+                or len(stream_dicts) != len(frame_datas):
+            self.logger.warning("Process frames: stream dicts and frame data must be lists of one length")
+            return False
+        frame_datas = [d if isinstance(d, dict) else {} for d in frame_datas]
+        hop = _hop.plane()
+        if hop is None:
+            for sd, fd in zip(stream_dicts, frame_datas):
+                self._process_frame_common(sd, fd, new_frame)
+            return True
+        try:
+            outs, handle, work = hop.decode_group_async(frame_datas, pooled=new_frame)
+            if work is not None:
+                if hop.host_transfers:
+                    hop.finish_later(work, lambda error: self._post_message(
+                        ActorTopic.IN, "hop_group_arrived", [stream_dicts, outs, handle, work, new_frame, error],
+                        target_function=self._hop_group_arrived))
+                    return True
+                hop.finish(work, handle)
+        except _hop.StageFailure as exc:
+            self.logger.error(f"Process frames: {exc}")
+            self._replica_lost_rank(exc.peer)
+            return False
+        return self._group_continue(stream_dicts, outs, handle, new_frame)
+
+    def _hop_group_arrived(self, stream_dicts, outs, handle, work, new_frame, error):
+        try:
+            _hop.plane().complete(work, handle, error)
+        except _hop.StageFailure as exc:
+            self.logger.error(f"Process frames: {exc}")
+            self._replica_lost_rank(exc.peer)
+            return False
+        return self._group_continue(stream_dicts, outs, handle, new_frame)
+
+    def _group_continue(self, stream_dicts, outs, handle, new_frame):
+        outer = self._response_batch
+        batch = self._response_batch = [] if outer is None else outer
+        try:
+            for sd, values in zip(stream_dicts, outs):
+                self._process_frame_common(sd, values, new_frame, decoded=handle)
+        finally:
+            if batch is not outer:
+                self._response_batch = outer
+                self._flush_responses(batch)
+        return True
+
+    def _flush_responses(self, batch):
+        """Send the responses collected while a group ran: one message + one transfer per
+        (response topic, reply rank), then release their frames (after the staging copies, so
+        no receive slot is reused under them)."""
+        hop = _hop.plane()
+        groups: dict = {}
+        for topic, reply, info, data, stream, frame_id in batch:
+            groups.setdefault((topic, reply), []).append((info, data))
+        try:
+            for (topic, reply), items in groups.items():
+                proxy = get_actor_mqtt(topic, Pipeline)
+                if len(items) == 1:
+                    proxy.process_frame_response(items[0][0], hop.encode(reply, items[0][1]))
+                else:
+                    outs = hop.encode_group(reply, [data for _, data in items])
+                    proxy.process_frame_responses([info for info, _ in items], outs)
+        finally:
+            for *_, stream, frame_id in batch:
+                self._release_frame(stream, frame_id)
+
+    def _hop_arrived(self, stream_dict, values, handle, work, new_frame, error):
+        """The bytes of a host-transfer hop message (gloo) arrived: resume its frame."""
+        try:
+            _hop.plane().complete(work, handle, error)
+        except _hop.StageFailure as exc:
+            self.logger.error(f"Process frame <{stream_dict.get('stream_id')}:{stream_dict.get('frame_id')}>: {exc}")
+            self._replica_lost_rank(exc.peer)
+            return False
+        return self._process_frame_common(stream_dict, values, new_frame, decoded=handle)
+
+    def _process_initialize(self, stream_dict, frame_data_in, new_frame, decoded=_UNDECODED):
         stream = Stream()
         if not stream.update(stream_dict):
             self.logger.warning("Process frame: stream_dict must be a dictionary")
@@ -672,11 +771,25 @@ class PipelineImpl(Pipeline):
             return None, None, None
         hop_handle = None
         hop = _hop.plane()
-        if hop is not None and _hop.needs_decode(stream_dict, frame_data_in):
+        if decoded is not _UNDECODED:
+            hop_handle = decoded                 # resumed by _hop_arrived: the bytes are in
+        elif hop is not None and _hop.needs_decode(stream_dict, frame_data_in):
             # tensors of this message arrive over RCCL: always receive them (even if the frame is
             # then rejected) so the link stays in order; forward hops land in FramePool slots
             try:
-                frame_data_in, hop_handle = hop.decode(frame_data_in, pooled=new_frame)
+                if hop.host_transfers:
+                    # gloo: the receive blocks the host until the bytes are in — wait on the
+                    # plane's waiter thread and resume the frame from the mailbox, so the
+                    # receives of several messages overlap (they are still POSTED in order)
+                    values, handle, work = hop.decode_async(frame_data_in, pooled=new_frame)
+                    if work is not None:
+                        hop.finish_later(work, lambda error: self._post_message(
+                            ActorTopic.IN, "hop_arrived", [stream_dict, values, handle, work, new_frame, error],
+                            target_function=self._hop_arrived))
+                        return None, None, None
+                    frame_data_in, hop_handle = values, handle
+                else:
+                    frame_data_in, hop_handle = hop.decode(frame_data_in, pooled=new_frame)
             except _hop.StageFailure as exc:
                 # the sender died mid-transfer: a response is re-dispatched (the frame is still
                 # held, in flight toward that member) with every other frame the member held
@@ -764,14 +877,14 @@ class PipelineImpl(Pipeline):
         self.share["gpu_lanes"] = lanes
         return self._lanes_cfg
 
-    def _process_frame_common(self, stream_dict, frame_data_in, new_frame):
+    def _process_frame_common(self, stream_dict, frame_data_in, new_frame, decoded=_UNDECODED):
         lanes, device = self._frame_lanes()
         if lanes > 1:
             from ..gpu.lanes import in_lane, lane_scope
             if in_lane():
                 # nested pipeline (rank 0's local share of a replicated stage): the frame keeps
                 # the lane of the enclosing frame
-                return self._process_frame_body(stream_dict, frame_data_in, new_frame)
+                return self._process_frame_body(stream_dict, frame_data_in, new_frame, decoded)
             lane = None
             if not new_frame:
                 # a remote hop's response resumes the frame on the lane it started on
@@ -787,11 +900,11 @@ class PipelineImpl(Pipeline):
                 self._lane_next = (lane + 1) % lanes
             self._frame_lane = lane
             with lane_scope(lane, device):
-                return self._process_frame_body(stream_dict, frame_data_in, new_frame)
-        return self._process_frame_body(stream_dict, frame_data_in, new_frame)
+                return self._process_frame_body(stream_dict, frame_data_in, new_frame, decoded)
+        return self._process_frame_body(stream_dict, frame_data_in, new_frame, decoded)
 
-    def _process_frame_body(self, stream_dict, frame_data_in, new_frame):
-        graph, stream, frame_data_in = self._process_initialize(stream_dict, frame_data_in, new_frame)
+    def _process_frame_body(self, stream_dict, frame_data_in, new_frame, decoded=_UNDECODED):
+        graph, stream, frame_data_in = self._process_initialize(stream_dict, frame_data_in, new_frame, decoded)
         if graph is None:
             return False
         frame_complete = True
@@ -901,9 +1014,16 @@ class PipelineImpl(Pipeline):
                 elif stream.topic_response:
                     hop = _hop.plane()
                     reply = getattr(stream.frames.get(frame_id), "hop_reply", None)
-                    if hop is not None and reply is not None:
-                        frame_data_out = hop.encode(reply, frame_data_out)
-                    get_actor_mqtt(stream.topic_response, Pipeline).process_frame_response(stream_info, frame_data_out)
+                    if hop is not None and reply is not None and self._response_batch is not None:
+                        # member of a group message: answered with the group, released after
+                        self._response_batch.append((stream.topic_response, reply, stream_info, frame_data_out,
+                                                     stream, frame_id))
+                        frame_complete = False
+                    else:
+                        if hop is not None and reply is not None:
+                            frame_data_out = hop.encode(reply, frame_data_out)
+                        get_actor_mqtt(stream.topic_response, Pipeline).process_frame_response(stream_info,
+                                                                                               frame_data_out)
                 else:
                     aiko.message.publish(self.topic_out, generate("process_frame", (stream_info, frame_data_out)))
         finally:
@@ -1007,7 +1127,7 @@ class PipelineImpl(Pipeline):
             return min(self._window_limits.values())
         if self.remote_pipelines:
             hop = _hop.plane()
-            return 2 * (hop.depth if hop is not None else 4) * max(1, self._remote_member_count())
+            return 2 * (hop.depth if hop is not None else 4) * self.hop_batch * max(1, self._remote_member_count())
         return 0
 
     def _remote_member_count(self) -> int:
@@ -1097,7 +1217,7 @@ class PipelineImpl(Pipeline):
 
     def _queue_hop(self, element, node_name, stream_id, frame_id, inputs, held=False):
         limit = int(self._param_float("remote_pending", 256))
-        if len(self._pending_hops) >= limit:
+        if self._pending_total() >= limit:
             self.frames_dropped += 1
             self.logger.warning(f"remote {node_name}: {limit} frames already wait for a credit: dropping "
                                 f"<{stream_id}:{frame_id}>")
@@ -1109,37 +1229,95 @@ class PipelineImpl(Pipeline):
             if lease is not None:
                 self._release_frame(lease.stream, frame_id)
             return
-        self._pending_hops.append({"element": element, "node": node_name, "stream_id": stream_id,
+        self._pending_hops.setdefault(node_name, deque()).append({
+                                   "element": element, "node": node_name, "stream_id": stream_id,
                                    "frame_id": frame_id, "inputs": inputs, "held": held,
                                    "t": time.monotonic()})
         self._watch_hops()
 
+    @property
+    def hop_batch(self) -> int:
+        """Frames per remote-hop message (pipeline parameter ``hop_batch``, default 1 = the
+        reference's one message per frame).  Frames waiting for a credit leave in groups of up
+        to this many: one control message, one transfer, ONE credit per group."""
+        return max(1, int(self._param_float("hop_batch", 1)))
+
+    def _pending_alive(self, p) -> bool:
+        lease = self.stream_leases.get(str(p["stream_id"]))
+        if lease is None or p["frame_id"] not in lease.stream.frames:
+            if p["held"] and _hop.plane() is not None:
+                _hop.plane().drop((p["stream_id"], p["frame_id"]))
+            return False
+        return True
+
     def _drain_pending(self):
-        """Dispatch waiting frames while their remote element has a member with a credit."""
-        kept = deque()
-        while self._pending_hops:
-            p = self._pending_hops.popleft()
-            lease = self.stream_leases.get(str(p["stream_id"]))
-            if lease is None or p["frame_id"] not in lease.stream.frames:
-                if p["held"] and _hop.plane() is not None:
-                    _hop.plane().drop((p["stream_id"], p["frame_id"]))
-                continue
-            element = self.pipeline_graph.get_node(p["node"]).element
-            target = element.pick(self._has_credit) if isinstance(element, RemoteReplicas) else None
-            if target is None:
-                kept.append(p)
-                continue
-            self._dispatch(element, target, p["node"], p["stream_id"], p["frame_id"], p["inputs"], held=p["held"])
-        self._pending_hops = kept
+        """Dispatch waiting frames while their remote element has a member with a credit
+        (grouped up to :attr:`hop_batch` frames per message)."""
+        if self._draining:
+            return                       # re-entered (a replica lost mid-dispatch): the outer pass continues
+        self._draining = True
+        try:
+            k = self.hop_batch
+            for node_name, fifo in list(self._pending_hops.items()):
+                while fifo:
+                    p = fifo[0]
+                    if not self._pending_alive(p):
+                        fifo.popleft()
+                        continue
+                    element = self.pipeline_graph.get_node(node_name).element
+                    target = element.pick(self._has_credit) if isinstance(element, RemoteReplicas) else None
+                    if target is None:
+                        break                # no member credit left: the FIFO waits
+                    fifo.popleft()
+                    group = [p]
+                    if k > 1 and not p["held"] and getattr(target, "hop_rank", None) is not None:
+                        while fifo and len(group) < k and not fifo[0]["held"]:
+                            q = fifo.popleft()
+                            if self._pending_alive(q):
+                                group.append(q)
+                    if len(group) == 1:
+                        self._dispatch(element, target, node_name, p["stream_id"], p["frame_id"], p["inputs"],
+                                       held=p["held"])
+                    else:
+                        self._dispatch_group(element, target, node_name, group)
+                if not fifo and self._pending_hops.get(node_name) is fifo:
+                    del self._pending_hops[node_name]
+        finally:
+            self._draining = False
+
+    def _pending_total(self) -> int:
+        return sum(len(f) for f in self._pending_hops.values())
+
+    def _dispatch_group(self, element, target, node_name, group):
+        """Frames ``group`` (pending entries of one remote node) to ``target`` as ONE
+        ``process_frames`` message whose tensors travel in ONE transfer holding ONE credit."""
+        hop = _hop.plane()
+        rank = target.hop_rank
+        keys = [(g["stream_id"], g["frame_id"]) for g in group]
+        try:
+            outs = hop.encode_group(rank, [g["inputs"] for g in group], keys)
+        except _hop.StageFailure as exc:
+            self._replica_lost_rank(exc.peer)
+            for g in group:
+                self._queue_hop(element, node_name, g["stream_id"], g["frame_id"], g["inputs"])
+            return
+        now = time.monotonic()
+        for key in keys:
+            self._inflight[key] = {"element": element, "target": target, "node": node_name, "rank": rank,
+                                   "inputs": None, "t": now}
+        self.hop_groups += 1
+        self._watch_hops()
+        target.process_frames([{"stream_id": s, "frame_id": f, "hop_rank": hop.rank} for s, f in keys], outs)
 
     def _remote_done(self, key):
         f = self._inflight.pop(key, None)
         if f is None:
             return
         hop = _hop.plane()
+        freed = True
         if hop is not None and f["rank"] is not None:
-            hop.ack(key)
-        if self._pending_hops:
+            freed = hop.ack(key)         # a group's credit returns with its last member
+        if freed and self._pending_hops:
             self._drain_pending()
 
     def _fail_frame(self, key, diagnostic):
@@ -1203,8 +1381,14 @@ class PipelineImpl(Pipeline):
         for key, f in lost:
             self._inflight.pop(key, None)
             held = f["rank"] is not None
+            inputs = f["inputs"]
+            if held and hop is not None and hop.grouped(key):
+                # a group member: re-sent on its own from views of the group's staging buffer
+                inputs = hop.held_values(key)
+                hop.ack(key)
+                held = False
             self.hops_redispatched += 1
-            self._queue_hop(f["element"], f["node"], key[0], key[1], f["inputs"], held=held)
+            self._queue_hop(f["element"], f["node"], key[0], key[1], inputs, held=held)
         if lost:
             self.logger.warning(f"remote {element_name}: member {topic_path} lost with {len(lost)} frames "
                                 f"in flight: re-dispatching")
@@ -1225,11 +1409,14 @@ class PipelineImpl(Pipeline):
                 self._fail_frame(key, f"remote hop to {f['node']} timed out after {timeout:g}s")
         if self._pending_hops:
             self._drain_pending()
-            for p in list(self._pending_hops):
-                if now - p["t"] > timeout:
-                    self._pending_hops.remove(p)
-                    self._fail_frame((p["stream_id"], p["frame_id"]),
-                                     f"no replica of {p['node']} had a credit for {timeout:g}s")
+            for fifo in list(self._pending_hops.values()):
+                for p in list(fifo):
+                    if now - p["t"] > timeout:
+                        fifo.remove(p)
+                        self._fail_frame((p["stream_id"], p["frame_id"]),
+                                         f"no replica of {p['node']} had a credit for {timeout:g}s")
+            for node_name in [n for n, f in self._pending_hops.items() if not f]:
+                del self._pending_hops[node_name]
         if not self._inflight and not self._pending_hops:
             self._hop_watch = False
             event.remove_timer_handler(self._hop_timer)
@@ -1405,6 +1592,12 @@ class PipelineRemote(PipelineElement):
 
     def process_frame_response(self, stream, frame_data):
         pass
+
+    def process_frames(self, stream_dicts, frame_datas):
+        """A hop group (see ``PipelineImpl.process_frames``)."""
+        if self.absent:
+            self.log_error("process_frames")
+        return not self.absent
 
     def set_remote_absent(self, absent):
         self.absent = absent

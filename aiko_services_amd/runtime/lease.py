@@ -24,6 +24,7 @@ class Lease:
         self.automatic_extend = automatic_extend
         self.expired = False
         self.terminated = False
+        self._deadline = event.engine.clock() + lease_time
         event.add_timer_handler(self._lease_expired_timer, lease_time)
         if automatic_extend:
             event.add_timer_handler(self.extend, lease_time * LEASE_EXTEND_TIME_FACTOR)
@@ -31,15 +32,22 @@ class Lease:
     def extend(self, lease_time=None):
         if self.terminated:
             return
-        if lease_time:
+        if lease_time and lease_time != self.lease_time:
             self.lease_time = lease_time
-        event.remove_timer_handler(self._lease_expired_timer)
-        event.add_timer_handler(self._lease_expired_timer, self.lease_time)
+            event.remove_timer_handler(self._lease_expired_timer)
+            event.add_timer_handler(self._lease_expired_timer, self.lease_time)
+        # lazy: only the deadline moves (a stream lease is extended by every frame); the timer
+        # re-arms itself for the rest when it fires early
+        self._deadline = event.engine.clock() + self.lease_time
         if self.lease_extend_handler:
             self.lease_extend_handler(self.lease_time, self.lease_uuid)
 
     def _lease_expired_timer(self):
         event.remove_timer_handler(self._lease_expired_timer)
+        left = self._deadline - event.engine.clock()
+        if left > 1e-3 and not self.terminated:
+            event.add_timer_handler(self._lease_expired_timer, left)
+            return
         if self.automatic_extend:
             event.remove_timer_handler(self.extend)
         self.expired = True

@@ -1,0 +1,203 @@
+"""Control-plane ceiling of the multi-GPU actor pipelines (hop metadata rate at rank 0).
+
+Config 3 at 8 GPUs moves one frame BATCH per hop: rank 0 publishes ``process_frame`` (tensor
+tokens) to a replica, the replica answers ``process_frame_response``, both through the in-repo
+MQTT broker, while the tensors cross on the data plane.  At ~86k frames/s per GPU and 256
+frames per batch the node needs ~2.7k such pairs per second through rank 0's event loop.  This
+bench measures the sustained rate of that loop with the data plane doing nothing heavy: gloo,
+tiny tensors, a 2-stage plan ``TensorFrames | (TensorAffine TensorStats) x R`` with R replicas
+(default 7 = the 8-GPU shape), rank 0 admitting frames through the pipeline's credit window.
+Reference analog: the multitude chain (``/root/reference/src/aiko_services/examples/pipeline/
+multitude/run_large.sh``, ≤ 50 frames/s there).
+
+    python -m aiko_services_amd.tools.hop_bench [--replicas 7] [--seconds 10] [--width 16]
+
+Prints one JSON line: pairs/s at rank 0, p50 / p99 frame latency, hop stats.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import queue
+import socket
+import statistics
+import subprocess
+import sys
+import threading
+import time
+import uuid
+
+ELEMENTS = "aiko_services_amd.examples.pipeline.tensor_elements"
+
+
+def definition(replicas: int, batch: int, width: int, hop_batch: int = 1) -> dict:
+    def el(name, inputs, outputs, stage, params=None):
+        return {"name": name, "input": [{"name": n, "type": "tensor"} for n in inputs],
+                "output": [{"name": n, "type": "tensor"} for n in outputs], "parameters": params or {},
+                "deploy": {"local": {"module": ELEMENTS, "stage": stage}}}
+    return {"version": 0, "name": "p_hop_bench", "runtime": "python",
+            "graph": ["(TensorFrames TensorAffine TensorStats)"],
+            "parameters": {"device": "cpu", "batch": batch, "width": width, "hop_batch": hop_batch},
+            "parallel": {"mode": "pp", "gpus": 1 + replicas, "replicas": [1, replicas]},
+            "elements": [el("TensorFrames", [], ["x", "t_submit"], 0),
+                         el("TensorAffine", ["x"], ["x"], 1, {"scale": "2.0", "shift": "0.5"}),
+                         el("TensorStats", ["x", "t_submit"], ["stats"], 1)]}
+
+
+def _port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--replicas", type=int, default=7)
+    ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--warmup", type=float, default=2.0)
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--width", type=int, default=16)
+    ap.add_argument("--hop-batch", type=int, default=1, help="frames per hop message (pipeline hop_batch)")
+    a = ap.parse_args(argv)
+    if os.environ.get("AIKO_HOP_BENCH_RANK0") == "1":
+        return _rank0(a)
+    # the control-plane environment must exist before aiko_services_amd is imported (the process
+    # singleton reads it at import): set it here, run rank 0 as a child process
+    port = _port()
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env = dict(os.environ)
+    env.update({"AIKO_MQTT_HOST": "127.0.0.1", "AIKO_MQTT_PORT": str(port), "AIKO_MQTT_DISABLE": "0",
+                "AIKO_NAMESPACE": f"hb{uuid.uuid4().hex[:6]}", "AIKO_REGISTRAR_SEARCH_TIMEOUT": "0.3",
+                "AIKO_LOG_MQTT": "false", "AIKO_LOG_LEVEL": os.environ.get("AIKO_LOG_LEVEL", "WARNING"),
+                "AIKO_HOP_BACKEND": "gloo", "OMP_NUM_THREADS": "1", "AIKO_HOP_BENCH_RANK0": "1",
+                "PYTHONPATH": root + os.pathsep + os.environ.get("PYTHONPATH", "")})
+    procs = [subprocess.Popen([sys.executable, "-m", "aiko_services_amd.message.mqtt_broker", "--host", "127.0.0.1",
+                               "--port", str(port)], env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)]
+    deadline = time.time() + 30
+    while True:
+        try:
+            socket.create_connection(("127.0.0.1", port), timeout=0.5).close()
+            break
+        except OSError:
+            if time.time() > deadline:
+                raise SystemExit("broker did not start")
+            time.sleep(0.05)
+    procs.append(subprocess.Popen([sys.executable, "-m", "aiko_services_amd.tools.registrar"], env=env,
+                                  stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL))
+    time.sleep(0.5)
+    import tempfile
+    fd, out_path = tempfile.mkstemp(prefix="hop_bench_", suffix=".json")
+    os.close(fd)
+    env["AIKO_HOP_BENCH_OUT"] = out_path
+    try:
+        # no pipes: the workers rank 0 spawns inherit its stdio, and a pipe would stay open
+        # until the last of them has exited
+        r = subprocess.run([sys.executable, "-m", "aiko_services_amd.tools.hop_bench", *(argv or sys.argv[1:])],
+                           env=env, cwd=root, stdout=subprocess.DEVNULL,
+                           timeout=float(os.environ.get("AIKO_HOP_BENCH_TIMEOUT", "300")))
+        with open(out_path) as f:
+            text = f.read().strip()
+    finally:
+        for p in procs:
+            p.terminate()
+        os.unlink(out_path)
+    if r.returncode != 0 or not text:
+        raise SystemExit(r.returncode or 1)
+    print(text, flush=True)
+
+
+def _rank0(a):
+    if os.environ.get("AIKO_HOP_BENCH_DEBUG"):
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["AIKO_HOP_BENCH_DEBUG"]), exit=False)
+    from ..parallel.launch import _sample_main_thread, create_rank_pipeline, join, spawn_workers
+    if os.environ.get("AIKO_WORKER_SAMPLE"):
+        _sample_main_thread(os.path.join(os.environ["AIKO_WORKER_SAMPLE"], "worker_0.txt"))
+    from ..parallel.placement import make_plan
+    from ..runtime.actor import ActorTopic
+    from ..runtime.process import aiko
+    plan = make_plan(definition(a.replicas, a.batch, a.width, a.hop_batch))
+    spawn_workers(plan)
+    plane = join(plan, 0)
+    q: queue.Queue = queue.Queue()
+    pipeline = create_rank_pipeline(plan, 0, queue_response=q, grace_time=3600, auto_start=False)
+    result = {}
+
+    def driver():
+        try:
+            t_end = time.time() + 120
+            while pipeline.share.get("lifecycle") != "ready":
+                if time.time() > t_end:
+                    raise RuntimeError("replicas not discovered")
+                time.sleep(0.02)
+            plane.barrier()
+            pipeline._post_message(ActorTopic.IN, "create_stream", ["hb", None, {}, 3600, q, None])
+            while "hb" not in pipeline.stream_leases:
+                time.sleep(0.01)
+            fid, done, lat = 0, 0, []
+            t0 = time.perf_counter()
+            t_meas = t0 + a.warmup
+            t_stop = t_meas + a.seconds
+            counted = 0
+            while True:
+                now = time.perf_counter()
+                if now >= t_stop:
+                    break
+                for _ in range(64):
+                    if not pipeline.admit_frame("hb", fid, timeout=0):
+                        break
+                    pipeline.create_frame({"stream_id": "hb", "frame_id": fid}, {"t_submit": time.perf_counter()})
+                    fid += 1
+                try:
+                    info, out = q.get(timeout=1.0)
+                except queue.Empty:
+                    continue
+                done += 1
+                if info.get("state", 0) != 0:
+                    raise RuntimeError(f"frame failed: {info} {out}")
+                if time.perf_counter() >= t_meas:
+                    counted += 1
+                    st = out.get("stats")
+                    if st is not None and getattr(st, "t_submit", None):
+                        lat.append(time.perf_counter() - float(st.t_submit))
+            elapsed = a.seconds
+            result["out"] = {
+                "metric": "hop pairs/s at rank 0 (process_frame + process_frame_response, MQTT metadata + gloo tensors)",
+                "value": round(counted / elapsed, 1), "unit": "frames/s", "replicas": a.replicas,
+                "hop_batch": a.hop_batch, "hop_messages_per_s": round(
+                    counted / elapsed / max(1.0, (done / max(1, pipeline.hop_groups)) if a.hop_batch > 1 else 1.0), 1),
+                "window": pipeline.frame_window(), "frames_completed": done,
+                "p50_latency_ms": round(statistics.median(lat) * 1e3, 3) if lat else None,
+                "p99_latency_ms": round(sorted(lat)[int(0.99 * (len(lat) - 1))] * 1e3, 3) if lat else None,
+                "hop": plane.stats(), "cpus": os.cpu_count()}
+        except BaseException as exc:           # report and stop the loop
+            result["error"] = repr(exc)
+        aiko.process.terminate(0)
+
+    threading.Thread(target=driver, daemon=True).start()
+    prof = None
+    if os.environ.get("AIKO_HOP_BENCH_PROFILE"):
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
+    try:
+        aiko.process.run(mqtt_connection_required=True)
+    except SystemExit:
+        pass
+    if prof is not None:
+        prof.disable()
+        prof.dump_stats(os.environ["AIKO_HOP_BENCH_PROFILE"])
+    if "out" in result:
+        with open(os.environ["AIKO_HOP_BENCH_OUT"], "w") as f:
+            f.write(json.dumps(result["out"]))
+        if os.environ.get("AIKO_WORKER_SAMPLE"):
+            import atexit
+            atexit._run_exitfuncs()
+        os._exit(0)
+    print(f"hop_bench: {result.get('error')}", file=sys.stderr, flush=True)
+    os._exit(1)
+
+
+if __name__ == "__main__":
+    main()

@@ -12,11 +12,23 @@ Wire-compatible with the reference codec (``main/utilities/parser.py:85-227``):
 
 The implementation is a single-pass index scanner (no per-character regex, no recursion
 on sub-strings), which matters because every actor message and every ``process_frame``
-metadata record passes through it.
+metadata record passes through it.  The native module ``aiko_services_amd/_sexpr.so``
+(``csrc/host/sexpr.c``, built by ``csrc/build.py``) implements the same scanner, dict
+conversion and generator in C and is used when present (``AIKO_SEXPR_NATIVE=0`` forces the
+Python code below, which stays the reference: ``tests/test_sexpr_native.py`` fuzzes one
+against the other).
 """
 from __future__ import annotations
 
+import os
 from typing import Any
+
+try:
+    from .. import _sexpr as _native          # csrc/host/sexpr.c
+except ImportError:                           # not built (source checkout before build())
+    _native = None
+if os.environ.get("AIKO_SEXPR_NATIVE", "1") == "0":
+    _native = None
 
 __all__ = ["generate", "parse", "parse_float", "parse_int", "parse_number",
            "generate_s_expression", "parse_list_to_dict"]
@@ -73,6 +85,12 @@ def _gen(expr, parts: list) -> None:
 
 
 def generate_s_expression(expression) -> str:
+    if _native is not None:
+        return _native.generate(expression)
+    return _generate_py(expression)
+
+
+def _generate_py(expression) -> str:
     parts: list = []
     _gen(expression, parts)
     return "".join(parts)
@@ -168,7 +186,7 @@ def parse(payload, dictionaries_flag: bool = True):
     """``"(cmd a (b c) k: v)"`` -> ``("cmd", ["a", ["b", "c"], ...])``."""
     if isinstance(payload, (bytes, bytearray)):
         payload = payload.decode("utf-8")
-    result = _Scanner(payload).parse_list()
+    result = _native.scan(payload) if _native is not None else _Scanner(payload).parse_list()
     car, cdr = "", []
     if result:
         head = result[0]
@@ -183,6 +201,12 @@ def parse(payload, dictionaries_flag: bool = True):
 
 
 def parse_list_to_dict(tree: Any):
+    if _native is not None:
+        return _native.to_dict(tree)
+    return _to_dict_py(tree)
+
+
+def _to_dict_py(tree: Any):
     if isinstance(tree, list) and tree:
         car = tree[0]
         if isinstance(car, str) and car.endswith(":"):
@@ -198,9 +222,9 @@ def parse_list_to_dict(tree: Any):
                 if key and not key.endswith(":"):
                     raise ValueError(f'Error parsing S-Expression dictionary starting at keyword "{key}", '
                                      'keyword must end with ":" character')
-                out[key[:-1]] = parse_list_to_dict(tree[i + 1])
+                out[key[:-1]] = _to_dict_py(tree[i + 1])
             return out
-        return [parse_list_to_dict(e) for e in tree]
+        return [_to_dict_py(e) for e in tree]
     return tree
 
 

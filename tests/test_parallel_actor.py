@@ -161,11 +161,13 @@ def test_dp_spmd_actor_pipeline(cluster):
         assert "float32,6x1x6" in v and "int32,6" in v, v      # world x batch rows gathered
 
 
-def _variant(path, **params):
-    """A temp copy of a definition with overridden pipeline parameters; returns (file, dict)."""
+def _variant(path, parallel=None, **params):
+    """A temp copy of a definition with overridden pipeline parameters (and ``parallel``
+    block entries); returns (file, dict)."""
     with open(path) as f:
         d = json.load(f)
     d["parameters"].update(params)
+    d["parallel"].update(parallel or {})
     f = tempfile.NamedTemporaryFile("w", suffix=".json", delete=False)
     json.dump(d, f)
     f.close()
@@ -186,14 +188,18 @@ def _single(cluster, d, frames):
     return single
 
 
-def test_replica_death_redispatches_held_frames(cluster):
+@pytest.mark.parametrize("hop_batch", [1, 4])
+def test_replica_death_redispatches_held_frames(cluster, hop_batch):
     """Rank 2 (one replica of stage 1 in tensor_ppdp.json) dies after computing its 2nd frame,
     before it answers.  Rank 0 learns it from the registrar (the dead process's last will),
     retires the RCCL/gloo links to it, re-sends every frame it held (their staged bytes) to the
     surviving replica / the local share, and every frame completes with the single-process
     values in bounded time — the reference's remote-absent swap
-    (/root/reference/src/aiko_services/main/pipeline.py:975-1006) made frame-safe."""
-    path, d = _variant(os.path.join(DEFS, "tensor_ppdp.json"), frames=16, hop_timeout=30)
+    (/root/reference/src/aiko_services/main/pipeline.py:975-1006) made frame-safe.  With
+    ``hop_batch`` 4 the dead replica held GROUP messages: their members are re-sent one by one."""
+    # with groups: no local share on rank 0, so frames queue for credits and leave in groups
+    path, d = _variant(os.path.join(DEFS, "tensor_ppdp.json"), frames=16, hop_timeout=30, hop_batch=hop_batch,
+                       parallel={"local_share": 0.0} if hop_batch > 1 else None)
     env = dict(cluster["env"], AIKO_FAULTS="kill=2@rank2", AIKO_LOG_LEVEL="INFO")
     try:
         t0 = time.time()
@@ -207,6 +213,8 @@ def test_replica_death_redispatches_held_frames(cluster):
     assert "lost with" in text, text[-3000:]                # rank 2 held frames when it died
     rank0 = re.search(r"hop rank 0 stats: (\{.*\})", text)
     assert rank0 and "'dead': [2]" in rank0.group(1), text[-3000:]
+    if hop_batch > 1:
+        assert any(p.startswith(b"(process_frames ") for _, p in cluster["payloads"])
     assert _single(cluster, d, 16) == par
 
 
@@ -245,3 +253,51 @@ def test_balancer_prices_stage_boundaries():
     flipped = dict(real, SyntheticFrames=0.01, FrameResize=5.0)
     stages, _, _, _ = plan_stages(order, times, 4, boundary_ms=flipped)
     assert stages[0] == ["SyntheticFrames"], stages
+
+
+def test_hop_groups_match_single_process(cluster):
+    """``hop_batch`` 4 with 2 credits per link on the 3-stage chain: frames waiting for a
+    credit leave in groups (ONE process_frames message + ONE transfer + ONE credit each), the
+    middle stage forwards groups on and answers with ONE process_frame_responses, and every
+    output matches the single-process run."""
+    path, d = _variant(os.path.join(DEFS, "tensor_pp3.json"), frames=32, hop_batch=4)
+    env = dict(cluster["env"], AIKO_HOP_DEPTH="2", AIKO_LOG_LEVEL="INFO")
+    try:
+        r, par = _create(env, path, 32, timeout=150)
+    finally:
+        os.unlink(path)
+    text = r.stdout + r.stderr
+    assert len(par) == 32, (r.returncode, text[-4000:])
+    groups = [p for _, p in cluster["payloads"] if p.startswith(b"(process_frames ")]
+    replies = [p for _, p in cluster["payloads"] if p.startswith(b"(process_frame_responses ")]
+    assert groups and replies, "no group messages were sent"
+    overflow = [int(v) for v in re.findall(r"'pool_overflow': (\d+)", text)]
+    assert overflow and max(overflow) == 0, text[-3000:]
+    assert _single(cluster, d, 32) == par
+
+
+def test_hop_group_loopback_credit_and_shared_slot():
+    """encode_group / decode_group_async on a loopback link: one sequence number and one
+    transfer for the group, ONE credit held until the LAST member is acknowledged, the receive
+    slot shared by the members and free after the last release, members re-materialised from
+    the held staging buffer (what a dead replica's group members are re-sent from)."""
+    import torch
+    from aiko_services_amd.parallel.hop import HopPlane
+    plane = HopPlane([(0, 0)], device="cpu", depth=2)
+    keys = [("s", i) for i in range(3)]
+    vals = [{"x": torch.full((2, 3), float(i)), "t": 0.5 * i} for i in range(3)]
+    msgs = plane.encode_group(0, vals, keys)
+    assert [m["x"].split("/")[1:3] for m in msgs] == [["0", "0"], ["0", "1"], ["0", "2"]]
+    assert plane.credit(0) == 1 and plane.grouped(keys[1])
+    assert torch.equal(plane.held_values(keys[2])["x"], vals[2]["x"])
+    outs, handle, work = plane.decode_group_async(msgs, pooled=True)
+    assert work is None and [float(o["x"][0, 0]) for o in outs] == [0.0, 1.0, 2.0]
+    assert [o["t"] for o in outs] == [0.0, 0.5, 1.0]
+    assert plane.ack(keys[0]) is False and plane.ack(keys[1]) is False and plane.credit(0) == 1
+    assert plane.ack(keys[2]) is True and plane.credit(0) == 2
+    pool = handle.pool
+    free0 = pool.free_count()
+    plane.release([handle, handle])
+    assert handle.count == 1 and pool.free_count() == free0
+    plane.release([handle])
+    assert handle.count == 0 and plane.stats()["held_frames"] == 0
