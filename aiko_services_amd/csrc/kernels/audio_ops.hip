@@ -377,7 +377,8 @@ extern "C" int aiko_logmel(const float* audio, int B, int N, const float* mel, i
   const long total = (long)B * rows * n_mels;
   long g = (total + 255) / 256;
   if (g > 4096) g = 4096;
-  if (n_mels % 8 == 0 && ld % 8 == 0 && reinterpret_cast<uintptr_t>(dst) % 16 == 0 &&
+  const char* scalar = getenv("AIKO_LOGMEL_SCALAR");     // exactness tests: force the scalar path
+  if (!(scalar && *scalar == '1') && n_mels % 8 == 0 && ld % 8 == 0 && reinterpret_cast<uintptr_t>(dst) % 16 == 0 &&
       reinterpret_cast<uintptr_t>(logmel) % 16 == 0 && total < (1L << 31)) {
     const long g8 = (total / 8 + 255) / 256;
     aiko::logmel_finalize8_kernel<<<(int)(g8 < 4096 ? g8 : 4096), 256, 0, stream>>>(

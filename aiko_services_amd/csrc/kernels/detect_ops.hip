@@ -37,22 +37,24 @@ namespace aiko {
 // Nearest 2x upsample, NHWC bf16 (C % 8 == 0), x / y may be channel slices (pixel pitches
 // ldx / ldy): one thread per 8 channels of an input pixel, one 16-B load -> four 16-B stores.
 // 2-D grid (y: image row b*H + h) so a thread only divides its in-row index by C/8 (32-bit);
-// the flat grid-stride version spent four 64-bit div/mods per 16 bytes.
+// the flat grid-stride version spent four 64-bit div/mods per 16 bytes.  More than 65535 rows
+// (B*H) stride over grid y.
 __global__ __launch_bounds__(256) void upsample2x_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
-                                                         int H, int W, int C, int ldx, int ldy) {
+                                                         int BH, int H, int W, int C, int ldx, int ldy) {
   const int C8 = C >> 3;
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= W * C8) return;
   const int w = i / C8, c8 = i - w * C8;
-  const int bh = blockIdx.y;
-  const int b = bh / H, h = bh - b * H;
   const int Wo = 2 * W;
-  const u32x4 v = *reinterpret_cast<const u32x4*>(x + ((long)bh * W + w) * ldx + c8 * 8);
-  bf16_t* o = y + (((long)b * 2 * H + 2 * h) * Wo + 2 * w) * ldy + c8 * 8;
-  *reinterpret_cast<u32x4*>(o) = v;
-  *reinterpret_cast<u32x4*>(o + ldy) = v;
-  *reinterpret_cast<u32x4*>(o + (long)Wo * ldy) = v;
-  *reinterpret_cast<u32x4*>(o + (long)Wo * ldy + ldy) = v;
+  for (int bh = blockIdx.y; bh < BH; bh += gridDim.y) {
+    const int b = bh / H, h = bh - b * H;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(x + ((long)bh * W + w) * ldx + c8 * 8);
+    bf16_t* o = y + (((long)b * 2 * H + 2 * h) * Wo + 2 * w) * ldy + c8 * 8;
+    *reinterpret_cast<u32x4*>(o) = v;
+    *reinterpret_cast<u32x4*>(o + ldy) = v;
+    *reinterpret_cast<u32x4*>(o + (long)Wo * ldy) = v;
+    *reinterpret_cast<u32x4*>(o + (long)Wo * ldy + ldy) = v;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -720,10 +722,12 @@ static inline int grid_for_d(long total, int block) {
 
 extern "C" int aiko_upsample2x(const void* x, void* y, int B, int H, int W, int C, int ldx,
                                int ldy, hipStream_t stream) {
-  if ((long)B * H > 65535 || (long)W * (C / 8) > (1L << 30)) return -1;
+  if ((long)B * H > (1L << 31) - 1 || (long)W * (C / 8) > (1L << 30)) return -1;
   const int gx = (W * (C / 8) + 255) / 256;
-  aiko::upsample2x_kernel<<<dim3(gx, B * H), 256, 0, stream>>>(
-      static_cast<const aiko::bf16_t*>(x), static_cast<aiko::bf16_t*>(y), H, W, C, ldx, ldy);
+  const int BH = B * H;
+  const int gy = BH < 65535 ? BH : 65535;
+  aiko::upsample2x_kernel<<<dim3(gx, gy), 256, 0, stream>>>(
+      static_cast<const aiko::bf16_t*>(x), static_cast<aiko::bf16_t*>(y), BH, H, W, C, ldx, ldy);
   return (int)hipGetLastError();
 }
 

@@ -28,6 +28,11 @@ from .device import parse_device, require_gpu
 
 __all__ = ["GpuPipelineElement", "DeviceResult", "FramePool", "CapturedCall", "HostRing"]
 
+# Device addresses known to be reused frame after frame: FramePool slot bases and the static
+# outputs of captured graphs.  run_maybe_captured captures a per-address graph at once for
+# inputs at these addresses; any other address must recur before it gets one.
+_STABLE_PTRS: set = set()
+
 _DTYPE_CODES = {torch.uint8: 0, torch.int8: 1, torch.int16: 2, torch.int32: 3, torch.int64: 4,
                 torch.float16: 5, torch.float32: 6, torch.float64: 7, torch.bool: 11,
                 torch.bfloat16: 15}
@@ -51,6 +56,8 @@ class FramePool:
         self._pool = torch.classes.aiko.FramePool(int(num_slots), int(slot_bytes),
                                                   dev.index if dev is not None and dev.type == "cuda" else -1)
         self._pending = deque()         # (event | None, slot)
+        self._slot_ptrs = [self.view(s, (1,)).data_ptr() for s in range(self.capacity)]
+        _STABLE_PTRS.update(self._slot_ptrs)
 
     def _reap(self, block: bool = False) -> None:
         while self._pending:
@@ -83,6 +90,7 @@ class FramePool:
         return self._pool.view(int(slot), list(shape), _DTYPE_CODES[dtype])
 
     def close(self):
+        _STABLE_PTRS.difference_update(self._slot_ptrs)
         self._pool.close()
 
     @property
@@ -214,6 +222,14 @@ class CapturedCall:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.static_outputs = fn(*self.static_inputs)
+        outs = self.static_outputs if isinstance(self.static_outputs, (tuple, list)) else (self.static_outputs,)
+        self._out_ptrs = [t.data_ptr() for t in outs if isinstance(t, torch.Tensor)]
+        _STABLE_PTRS.update(self._out_ptrs)
+
+    def drop(self):
+        """Forget this graph (LRU eviction): its static outputs stop counting as stable."""
+        _STABLE_PTRS.difference_update(self._out_ptrs)
+        self.graph = None
 
     def __call__(self, *inputs):
         for dst, src in zip(self.static_inputs, inputs):
@@ -273,32 +289,54 @@ class GpuPipelineElement(PipelineElement):
         from .lanes import current_lane
         return current_lane()
 
-    # distinct input addresses per (key, lane) that get their own graph (frame-pool slots)
+    # per-address graphs kept per (key, lane) — least recently used evicted beyond this
     max_graphs_per_key = 16
+    # addresses remembered (LRU) while waiting to recur
+    max_seen_addresses = 64
 
     def run_maybe_captured(self, key, fn, *inputs):
-        """Replay a hipGraph of ``fn`` for this input signature and lane.  Inputs with stable
-        addresses (a FramePool's slots cycling) get one graph per slot address, captured on the
-        slot itself — no per-frame input copy; beyond ``max_graphs_per_key`` addresses the
-        element falls back to one graph with copied-in static inputs."""
+        """Replay a hipGraph of ``fn`` for this input signature and lane.  Inputs at stable
+        addresses (FramePool slots cycling, static outputs of an upstream captured graph) get
+        one graph per address, captured on the buffer itself — no per-frame input copy.  Any
+        other address gets its own graph only once it recurs (a transient buffer never pays a
+        capture); until then, and for addresses that never recur, one graph with copied-in
+        static inputs runs.  Per-address graphs are kept LRU, ``max_graphs_per_key`` per key."""
         if not self.use_graph:
             return fn(*inputs)
         base = (key, self.lane)
         addrs = tuple(t.data_ptr() for t in inputs)
-        seen = self._captured.setdefault(("addrs",) + base, set())
-        if addrs in seen or len(seen) < self.max_graphs_per_key:
-            k = base + (addrs,)
-            call = self._captured.get(k)
-            if call is None:
-                call = CapturedCall(fn, inputs, static=True)
-                self._captured[k] = call
-                seen.add(addrs)
+        graphs = self._captured.get(("graphs",) + base)
+        if graphs is None:
+            from collections import OrderedDict
+            graphs = self._captured[("graphs",) + base] = OrderedDict()
+            self._captured[("seen",) + base] = OrderedDict()
+        call = graphs.get(addrs)
+        if call is not None:
+            graphs.move_to_end(addrs)
             return call.graph_replay()
+        seen = self._captured[("seen",) + base]
+        if all(a in _STABLE_PTRS for a in addrs) or addrs in seen:
+            seen.pop(addrs, None)
+            call = graphs[addrs] = CapturedCall(fn, inputs, static=True)
+            if len(graphs) > self.max_graphs_per_key:
+                self._retire_graph(graphs.popitem(last=False)[1])
+            return call.graph_replay()
+        seen[addrs] = True
+        if len(seen) > self.max_seen_addresses:
+            seen.popitem(last=False)
         call = self._captured.get(base)
         if call is None:
             call = CapturedCall(fn, inputs)
             self._captured[base] = call
         return call(*inputs)
+
+    def _retire_graph(self, call: "CapturedCall") -> None:
+        """An evicted graph is destroyed only once the GPU is past its last replay."""
+        ev = torch.cuda.Event()
+        ev.record()
+        graveyard = self._captured.setdefault(("retired",), [])
+        graveyard[:] = [(e, c) for e, c in graveyard if not e.query() or c.drop()]
+        graveyard.append((ev, call))
 
     def hold_for_frame(self, pool: "FramePool", slot: int) -> None:
         """Keep ``slot`` of ``pool`` until the frame being processed completes, then release it

@@ -487,8 +487,10 @@ class HopPlane:
 
     def _post(self, link, slot, buf, total, dst):
         D._account("hop_send", total)
-        if dst == self.rank:                         # loopback: the receiver copies from the stage
-            self._loop.append(buf)
+        if dst == self.rank:
+            # loopback: the message's own copy of its bytes — the staging slot may be reused
+            # (ring / ack) before the receiver decodes, so the queue must not alias it
+            self._loop.append(buf[:total].clone())
             link.work[slot] = None
         else:
             # the link's process group directly: tdist.isend re-validates group and rank per call

@@ -51,3 +51,21 @@ def test_robot_video_payload_modes(monkeypatch):
     assert np.array_equal(X.video_frame(payload), img)
     X._RING.close()
     X._RING = None
+
+
+def test_restarted_writer_is_reattached():
+    """A writer that restarts recreates its ring under the same name (new generation): a reader
+    that cached the old mapping re-attaches instead of serving the old run's slots."""
+    name = f"aiko_t_{uuid.uuid4().hex[:8]}"
+    ring = SharedFrameRing(name, slots=2, slot_bytes=1024, create=True)
+    old = ring.put(np.full(4, 1, np.int32))
+    assert SharedFrameRing.get(old).tolist() == [1] * 4          # reader caches the mapping
+    ring.close()
+    ring = SharedFrameRing(name, slots=2, slot_bytes=1024, create=True)
+    try:
+        new = ring.put(np.full(4, 2, np.int32))                  # same slot / seq as ``old``
+        assert new.split("/")[2:] == old.split("/")[2:] and new != old
+        assert SharedFrameRing.get(new).tolist() == [2] * 4
+        assert SharedFrameRing.get(old) is None                  # the old run's frame is gone
+    finally:
+        ring.close()

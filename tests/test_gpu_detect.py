@@ -22,6 +22,15 @@ def test_upsample2x_into_slice(native):
     assert big[..., :48].abs().max().item() == 0
 
 
+def test_upsample2x_more_rows_than_grid_y(native):
+    """B*H = 81920 image rows > 65535: the kernel strides over grid y."""
+    from aiko_services_amd.ops import detect as DT
+    x = torch.randn(2048, 40, 4, 8, device=DEV).to(torch.bfloat16)
+    out = DT.upsample2x(x)
+    ref = x.repeat_interleave(2, dim=1).repeat_interleave(2, dim=2)
+    assert torch.equal(out, ref)
+
+
 def test_maxpool_slices(native):
     from aiko_services_amd.ops import vision as V
     cat = torch.randn(3, 20, 20, 128, device=DEV).to(torch.bfloat16)

@@ -96,6 +96,30 @@ def test_log_mel(native):
     assert (got[:, 1:-1].float().transpose(1, 2) - ref).abs().max().item() < 2e-2
 
 
+@pytest.mark.parametrize("pad,ld", [(1, 80), (3, 88), (2, 96)])
+def test_log_mel_finalize8_matches_scalar(native, monkeypatch, pad, ld):
+    """The 8-mels-per-thread finalize kernel is bit-identical to the scalar one, with conv
+    padding rows (pad > 0, tail rows) and a padded row pitch."""
+    from aiko_services_amd.ops import audio as AU
+    g = torch.Generator().manual_seed(5)
+    B, N = 3, 16000 * 2
+    audio = (0.2 * torch.randn(B, N, generator=g)).float().to(DEV)
+    filters = AU.mel_filters().to(DEV)
+    F_ = N // AU.HOP
+    rows = F_ + pad + 2
+    outs = []
+    for scalar in ("0", "1"):
+        monkeypatch.setenv("AIKO_LOGMEL_SCALAR", scalar)
+        big = torch.full((B * rows, ld), 9.0, dtype=torch.bfloat16, device=DEV)
+        AU.log_mel(audio, filters, big[:, :80], rows, pad, frames=F_)
+        outs.append(big)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
+    got = outs[0].view(B, rows, ld)
+    assert (got[:, :pad, :80] == 0).all() and (got[:, pad + F_:, :80] == 0).all()
+    assert (got[..., 80:] == 9.0).all()                 # the pitch padding is never written
+
+
 def test_whisper_tiny_matches_reference(native):
     from aiko_services_amd.models.whisper import WhisperEncoder
     enc = WhisperEncoder("tiny", device=DEV)
