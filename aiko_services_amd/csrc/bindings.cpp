@@ -704,7 +704,8 @@ void gemm_fp8_out(const at::Tensor& a, const c10::optional<at::Tensor>& sa_opt, 
   } else {
     TORCH_CHECK(yp != nullptr, "aiko.gemm_fp8_out: y (or yq) required");
   }
-  TORCH_CHECK(!(mx_in || mx_out) || (variant == 1 && bn == 128), "aiko.gemm_fp8_out: MX paths need variant 1 and BN 128");
+  TORCH_CHECK(!(mx_in || mx_out) || (variant == 1 && bn == 128) || (variant == 3 && bm == 256 && bn == 256 && N % 256 == 0),
+              "aiko.gemm_fp8_out: MX paths need variant 1 with BN 128, or variant 3 (256 x 256, N % 256 == 0)");
   const float* bp = nullptr;
   if (bias.has_value() && bias->defined()) {
     check_cuda(*bias, "bias");

@@ -67,7 +67,16 @@ __device__ __forceinline__ int v_off(int row, int col) {
 // after the barrier that retires tile it-1 — two LDS slots, plain loads + ds_write_b128
 // (a handful of issue cycles) instead of one LDS-DMA per piece (60-185 issue cycles each beside
 // MFMAs, MI355X_MICROARCH.md).  REG = 0: the LDS-DMA ring (4 slots, counted vmcnt).
-template <int NW, int VPRE, int REG = 0>
+// SM = 1: softmax with the per-score VALU work cut to v_exp + cvt (the kernel is VALU-issue
+// bound beside its MFMAs, 6.2 VALU per MFMA in round 2):
+//   * Q is pre-scaled by scale*log2(e) once (bf16), so scores come out of the MFMA in log2 units;
+//   * the S accumulators start at -m_run (the running max): S' = Q K^T - m needs no subtraction
+//     and feeds v_exp_f32 directly; the tile max (v_max3 tree + 2 permlane swaps) only decides
+//     the lazy rescale (grow by > kRescale) — the rare rescale path shifts this tile's scores;
+//   * the row sums come out of the MFMA pipe: one extra 16x16x32 MFMA per P fragment with an
+//     all-ones A operand (rowsum(P) in every row of the result, no fp32 add chain and no
+//     end-of-kernel reduction), summing the same bf16 P that enters O.
+template <int NW, int VPRE, int REG = 0, int SM = 0>
 __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p) {
   constexpr int NT = 64 * NW;
   constexpr int QB = 32 * NW;
@@ -97,8 +106,18 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
     const int q = q0 + qt * 16 + fr;
     const int qc = q < p.T ? q : p.T - 1;     // rows past T: clamped, never written
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-      qf[qt][ks] = as_bf16x8(*reinterpret_cast<const u32x4*>(p.q + (seq0 + qc) * p.ldq + hc + ks * 32 + 8 * g));
+    for (int ks = 0; ks < 2; ++ks) {
+      const u32x4 raw = *reinterpret_cast<const u32x4*>(p.q + (seq0 + qc) * p.ldq + hc + ks * 32 + 8 * g);
+      if constexpr (SM == 1) {
+        u32x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          w[e] = pack2(__uint_as_float(raw[e] << 16) * p.scale_log2, __uint_as_float(raw[e] & 0xffff0000u) * p.scale_log2);
+        qf[qt][ks] = as_bf16x8(w);
+      } else {
+        qf[qt][ks] = as_bf16x8(raw);
+      }
+    }
   }
   // consume Q here, before the first (asm, compiler-invisible) DMA: the compiler's own vmcnt
   // for these loads would otherwise land inside the key loop and count the DMAs too
@@ -153,7 +172,9 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
   for (int d = 0; d < 4; ++d)
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) o[d][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
+  float m_run[2] = {SM ? 0.f : -INFINITY, SM ? 0.f : -INFINITY}, l_run[2] = {0.f, 0.f};
+  f32x4 lsum[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};   // SM = 1 row sums
+  const bf16x8 ones = as_bf16x8(u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
 
   // transposed-read lane geometry: lane 4q'+p' of its 16-lane group addresses row q', cols 4p'
   const int trq = fr >> 2, trp = fr & 3;
@@ -216,7 +237,10 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) s[kt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int qt = 0; qt < 2; ++qt) {
+        const float init = SM ? -m_run[qt] : 0.f;
+        s[kt][qt] = f32x4{init, init, init, init};
+      }
       const int row = kt * 16 + fr;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
@@ -237,6 +261,49 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
     // bounded by 2^kRescale and the stale max is exact for the final normalisation)
     const float c = p.scale_log2;
     bf16x8 pf[2][2];
+    if constexpr (SM == 1) {
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        if constexpr (MASK) {
+#pragma unroll
+          for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (t0 + kt * 16 + 4 * g + j >= p.T) s[kt][qt][j] = -INFINITY;
+        }
+        // tile max relative to m_run: a v_max3 tree
+        float m01 = fmaxf(s[0][qt][0], fmaxf(s[0][qt][1], s[0][qt][2]));
+        float m23 = fmaxf(s[0][qt][3], fmaxf(s[1][qt][0], s[1][qt][1]));
+        float m45 = fmaxf(s[1][qt][2], fmaxf(s[1][qt][3], s[2][qt][0]));
+        float m67 = fmaxf(s[2][qt][1], fmaxf(s[2][qt][2], s[2][qt][3]));
+        float m89 = fmaxf(s[3][qt][0], fmaxf(s[3][qt][1], s[3][qt][2]));
+        float mloc = fmaxf(s[3][qt][3], fmaxf(m01, m23));
+        mloc = fmaxf(mloc, fmaxf(m45, m67));
+        mloc = max_xor16_32(fmaxf(mloc, m89));
+        if (it == 0 || mloc > kRescale) {
+          // first tile: m_run = the tile max; later: raise it (lazy, > kRescale) — shift this
+          // tile's scores to the new max and rescale what O / l hold
+          if (it != 0) {
+            const float alpha = fast_exp2(-mloc);
+            lsum[qt] *= alpha;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) o[d][qt] *= alpha;
+          }
+          m_run[qt] += mloc;
+#pragma unroll
+          for (int kt = 0; kt < 4; ++kt) s[kt][qt] -= mloc;
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          u32x4 u;
+          u[0] = pack2(fast_exp2(s[2 * ks][qt][0]), fast_exp2(s[2 * ks][qt][1]));
+          u[1] = pack2(fast_exp2(s[2 * ks][qt][2]), fast_exp2(s[2 * ks][qt][3]));
+          u[2] = pack2(fast_exp2(s[2 * ks + 1][qt][0]), fast_exp2(s[2 * ks + 1][qt][1]));
+          u[3] = pack2(fast_exp2(s[2 * ks + 1][qt][2]), fast_exp2(s[2 * ks + 1][qt][3]));
+          pf[qt][ks] = as_bf16x8(u);
+        }
+      }
+    } else {
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       float mloc = -INFINITY;
@@ -285,6 +352,7 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
         pf[qt][ks] = as_bf16x8(u);
       }
     }
+    }
 
     // O^T += V^T P^T (fragments read above / here)
 #pragma unroll
@@ -296,6 +364,13 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
         for (int qt = 0; qt < 2; ++qt)
           o[d][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vfr[d][ks], pf[qt][ks], o[d][qt], 0, 0, 0);
     }
+    if constexpr (SM == 1) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+          lsum[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qt][ks], lsum[qt], 0, 0, 0);
+    }
 
     slot = slot == NS - 1 ? 0 : slot + 1;
   };
@@ -306,9 +381,14 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
   // normalise and write O[q][dh]: lane holds dh = d*16 + 4g + j for its query
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
-    float l = l_run[qt];
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
+    float l;
+    if constexpr (SM == 1) {
+      l = lsum[qt][0];                 // every row of the ones-MFMA result is the row sum
+    } else {
+      l = l_run[qt];
+      l += __shfl_xor(l, 16, 64);
+      l += __shfl_xor(l, 32, 64);
+    }
     const float inv = 1.f / l;
     const int q = q0 + qt * 16 + fr;
     if (q >= p.T) continue;
@@ -341,26 +421,33 @@ extern "C" int aiko_attn_fwd(const void* q, const void* k, const void* v, void* 
     const char* v = getenv("AIKO_ATTN_VARIANT");
     return v ? atoi(v) : 0;
   }();
-  auto launch = [&](auto nw_tag, auto vpre_tag, auto reg_tag) {
+  auto launch = [&](auto nw_tag, auto vpre_tag, auto reg_tag, auto sm_tag) {
     constexpr int NW = decltype(nw_tag)::value, VPRE = decltype(vpre_tag)::value;
-    constexpr int REG = decltype(reg_tag)::value;
+    constexpr int REG = decltype(reg_tag)::value, SM = decltype(sm_tag)::value;
     dim3 grid((T + 32 * NW - 1) / (32 * NW), H, B), block(64 * NW);
-    aiko::attn_fwd_kernel<NW, VPRE, REG><<<grid, block, 0, stream>>>(p);
+    aiko::attn_fwd_kernel<NW, VPRE, REG, SM><<<grid, block, 0, stream>>>(p);
   };
   using R0 = std::integral_constant<int, 0>;
   using R1 = std::integral_constant<int, 1>;
   using I8 = std::integral_constant<int, 8>;
   using I4 = std::integral_constant<int, 4>;
+  using V0 = std::integral_constant<int, 0>;
+  using V2 = std::integral_constant<int, 2>;
   switch (variant) {
-    case 1: launch(I8{}, std::integral_constant<int, 2>{}, R0{}); break;
-    case 2: launch(I8{}, std::integral_constant<int, 4>{}, R0{}); break;
-    case 3: launch(I4{}, std::integral_constant<int, 0>{}, R0{}); break;
-    case 4: launch(I4{}, std::integral_constant<int, 2>{}, R0{}); break;
-    case 5: launch(I8{}, std::integral_constant<int, 0>{}, R1{}); break;
-    case 6: launch(I8{}, std::integral_constant<int, 2>{}, R1{}); break;
-    case 7: launch(I4{}, std::integral_constant<int, 0>{}, R1{}); break;
-    case 8: launch(I4{}, std::integral_constant<int, 2>{}, R1{}); break;
-    default: launch(I8{}, std::integral_constant<int, 0>{}, R0{}); break;
+    case 1: launch(I8{}, V2{}, R0{}, R0{}); break;
+    case 2: launch(I8{}, std::integral_constant<int, 4>{}, R0{}, R0{}); break;
+    case 3: launch(I4{}, V0{}, R0{}, R0{}); break;
+    case 4: launch(I4{}, V2{}, R0{}, R0{}); break;
+    case 5: launch(I8{}, V0{}, R1{}, R0{}); break;
+    case 6: launch(I8{}, V2{}, R1{}, R0{}); break;
+    case 7: launch(I4{}, V0{}, R1{}, R0{}); break;
+    case 8: launch(I4{}, V2{}, R1{}, R0{}); break;
+    case 10: launch(I8{}, V0{}, R0{}, R0{}); break;        // round-2 softmax
+    case 11: launch(I8{}, V2{}, R0{}, R1{}); break;
+    case 12: launch(I8{}, V0{}, R1{}, R1{}); break;
+    case 13: launch(I4{}, V0{}, R0{}, R1{}); break;
+    case 14: launch(I4{}, V2{}, R1{}, R1{}); break;
+    default: launch(I8{}, V0{}, R0{}, R1{}); break;
   }
   return (int)hipGetLastError();
 }

@@ -84,7 +84,7 @@ __device__ __forceinline__ void fp8_epilogue(const Fp8GemmParams& p,
   static_assert(CHUNKS % NT == 0, "whole chunks per thread");
   const int e_cc = tid % CPR, e_row0 = tid / CPR;
   const int e_n = n0 + e_cc * 8;
-  static_assert(!MXO || BN == 128, "MX output needs whole 128-column K chunks per tile");
+  static_assert(!MXO || BN % 128 == 0, "MX output needs whole 128-column K chunks per tile");
   if (e_n >= p.N) return;
   float cs[8], cb[8];
   {
@@ -159,7 +159,7 @@ __device__ __forceinline__ void fp8_epilogue(const Fp8GemmParams& p,
       if (live) {
         *reinterpret_cast<uint2*>(p.yq + (long)m * p.ldq + e_n) = make_uint2(w0, w1);
         if ((e_cc & 3) == 0)
-          p.ysc[((long)(n0 >> 7) * p.ysr + m) * 4 + (e_cc >> 2)] = (uint8_t)(ex + 127);
+          p.ysc[((long)(e_n >> 7) * p.ysr + m) * 4 + ((e_n >> 5) & 3)] = (uint8_t)(ex + 127);
       }
       continue;
     }
@@ -176,6 +176,64 @@ __device__ __forceinline__ void fp8_epilogue(const Fp8GemmParams& p,
     for (int e = 0; e < 4; ++e) o[e] = pack2(v[2 * e], v[2 * e + 1]);
     *reinterpret_cast<u32x4*>(p.y + (long)m * p.ldy + e_n) = o;
   }
+}
+
+// One output row-chunk of 8 columns (shared by the epilogues below): scales, bias, activation,
+// then MX-fp8 quantisation (every lane takes part in the DPP block reduction; ``live`` gates
+// the stores) or residual add + bf16 store.
+template <bool MXO>
+__device__ __forceinline__ void fp8_store_chunk(const Fp8GemmParams& p, float (&v)[8], int m, int e_n, int e_cc,
+                                                bool live) {
+  if (p.act == 1) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+  } else if (p.act == 2) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = silu(v[e]);
+  } else if (p.act == 3) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const f32x2 g = gelu_erf2(f32x2{v[2 * e], v[2 * e + 1]});
+      v[2 * e] = g[0];
+      v[2 * e + 1] = g[1];
+    }
+  }
+  if constexpr (MXO) {
+    float amax = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[e]));
+    amax = fmaxf(amax, dpp_f32<0xB1>(amax));
+    amax = fmaxf(amax, dpp_f32<0x4E>(amax));
+    const int ex = mx_exponent(amax);
+    const float inv = __uint_as_float((uint32_t)(127 - ex) << 23);
+    unsigned w0 = 0u, w1 = 0u;
+    w0 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[0] * inv, -448.f), 448.f),
+                                         fminf(fmaxf(v[1] * inv, -448.f), 448.f), w0, false);
+    w0 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[2] * inv, -448.f), 448.f),
+                                         fminf(fmaxf(v[3] * inv, -448.f), 448.f), w0, true);
+    w1 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[4] * inv, -448.f), 448.f),
+                                         fminf(fmaxf(v[5] * inv, -448.f), 448.f), w1, false);
+    w1 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[6] * inv, -448.f), 448.f),
+                                         fminf(fmaxf(v[7] * inv, -448.f), 448.f), w1, true);
+    if (live) {
+      *reinterpret_cast<uint2*>(p.yq + (long)m * p.ldq + e_n) = make_uint2(w0, w1);
+      if ((e_cc & 3) == 0) p.ysc[((long)(e_n >> 7) * p.ysr + m) * 4 + ((e_n >> 5) & 3)] = (uint8_t)(ex + 127);
+    }
+    return;
+  }
+  if (!live) return;
+  if (p.res) {
+    const u32x4 r = *reinterpret_cast<const u32x4*>(p.res + (long)m * p.ldr + e_n);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[2 * e] += __uint_as_float(r[e] << 16);
+      v[2 * e + 1] += __uint_as_float(r[e] & 0xffff0000u);
+    }
+  }
+  u32x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = pack2(v[2 * e], v[2 * e + 1]);
+  *reinterpret_cast<u32x4*>(p.y + (long)m * p.ldy + e_n) = o;
 }
 
 template <int BM, int BN>
@@ -530,13 +588,15 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_w8_kernel(Fp8GemmParams p, co
 // LDS; 128 x 64 reads 0.75 KB per MFMA.  Double-buffered 64 KB stages (LDS-DMA, counted vmcnt +
 // raw barrier), 1024 MFMA cycles per wave per stage to cover the next stage's flight.  The fp32
 // epilogue is staged through LDS in two 128-row halves.
+template <bool MXA = false, bool MXO = false>
 __global__ __launch_bounds__(512, 1) void gemm_fp8_big_kernel(Fp8GemmParams p, const uint8_t* zero) {
   constexpr int BM = 256, BN = 256, BK = 128, NS = 2;
   constexpr int WGN = 4;
   constexpr int WM = 128, WN = 64, MI = WM / 16, NI = WN / 16;
   constexpr int APT = BM / 64, BPT = BN / 64;   // DMA instructions per thread per stage
   constexpr int PER = APT + BPT;
-  constexpr int STAGE_BYTES = (BM + BN) * BK;  // 64 KB
+  constexpr int TILE_BYTES = (BM + BN) * BK;   // 64 KB
+  constexpr int STAGE_BYTES = TILE_BYTES + (MXA ? BM * 4 : 0);   // + the MX scale tile of A
   constexpr int CPAD = 4, LDC = BN + CPAD;
   constexpr int EPI_BYTES = 128 * LDC * 4;     // one 128-row half
   constexpr int RING_BYTES = NS * STAGE_BYTES;
@@ -573,6 +633,12 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_big_kernel(Fp8GemmParams p, c
     for (int i = 0; i < APT; ++i) glds16_u8(a_src[i] ? a_src[i] + k0 : zero, As + (i * 64 + wave * 8) * BK);
 #pragma unroll
     for (int i = 0; i < BPT; ++i) glds16_u8(b_src[i] ? b_src[i] + k0 : zero, Bs + (i * 64 + wave * 8) * BK);
+    if constexpr (MXA) {   // scale rows m0 .. m0+255 (4 B each): wave w takes 32 rows with 8 lanes
+      // (the scale tensor holds M rounded up to 128 rows: a 32-row group past it reads zeros)
+      const int r0 = m0 + wave * 32;
+      const uint8_t* src = r0 < p.mxr ? p.amx + ((long)kb * p.mxr + r0) * 4 + lane * 16 : zero;
+      if (lane < 8) glds16_u8(src, As + TILE_BYTES + wave * 128);
+    }
   };
 
   f32x4 acc[MI][NI];
@@ -604,10 +670,16 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_big_kernel(Fp8GemmParams p, c
       const u32x4 lo = *reinterpret_cast<const u32x4*>(As + i * 16 * BK + off_lo);
       const u32x4 hi = *reinterpret_cast<const u32x4*>(As + i * 16 * BK + off_hi);
       const i32x8 af = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      int asc = 127;                   // E8M0 scale of this lane's A block (byte fg of its row's word)
+      if constexpr (MXA) {
+        const uint32_t w4 = *reinterpret_cast<const uint32_t*>(smem + slot * STAGE_BYTES + TILE_BYTES +
+                                                               (wr * WM + i * 16 + fr) * 4);
+        asc = (int)(w4 >> (8 * fg));
+      }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int j = 0; j < NI; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bfr[j], acc[i][j], 0, 0, 0, 127, 0, 127);
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bfr[j], acc[i][j], 0, 0, 0, asc, 0, 127);
       __builtin_amdgcn_s_setprio(0);
     }
   }
@@ -657,8 +729,9 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_big_kernel(Fp8GemmParams p, c
       for (int i = 0; i < CPT; ++i) {
         const int row = e_row0 + E_ROWS * i;
         const int m = m0 + half * 128 + row;
-        if (m >= p.M) continue;
-        const float rs = p.sa[m];
+        const bool live = m < p.M;
+        if (!MXO && !live) continue;     // (MX output: every lane joins the block reduction)
+        const float rs = p.sa && live ? p.sa[m] : 1.f;
         const f32x4 c0 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + e_cc * 8);
         const f32x4 c1 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + e_cc * 8 + 4);
         float v[8];
@@ -667,28 +740,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_big_kernel(Fp8GemmParams p, c
           v[e] = c0[e] * rs * cs[e] + cb[e];
           v[e + 4] = c1[e] * rs * cs[e + 4] + cb[e + 4];
         }
-        if (p.act == 1) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-        } else if (p.act == 2) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = silu(v[e]);
-        } else if (p.act == 3) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
-        }
-        if (p.res) {
-          const u32x4 r = *reinterpret_cast<const u32x4*>(p.res + (long)m * p.ldr + e_n);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            v[2 * e] += __uint_as_float(r[e] << 16);
-            v[2 * e + 1] += __uint_as_float(r[e] & 0xffff0000u);
-          }
-        }
-        u32x4 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = pack2(v[2 * e], v[2 * e + 1]);
-        *reinterpret_cast<u32x4*>(p.y + (long)m * p.ldy + e_n) = o;
+        fp8_store_chunk<MXO>(p, v, m, e_n, e_cc, live);
       }
     }
     __syncthreads();
@@ -846,7 +898,7 @@ extern "C" int aiko_gemm_fp8(const void* a, const void* b, const float* sa, cons
   p.ysc = static_cast<uint8_t*>(ysc);
   p.ldq = ldq;
   p.ysr = ysr;
-  if ((amx || yq) && variant != 1) return -1;   // MX paths: LDS-DMA kernel only
+  if ((amx || yq) && variant != 1 && variant != 3) return -1;   // MX paths: LDS-DMA kernels
   p.a = static_cast<const uint8_t*>(a);
   p.b = static_cast<const uint8_t*>(b);
   p.sa = sa; p.sb = sb; p.bias = bias;
@@ -857,7 +909,11 @@ extern "C" int aiko_gemm_fp8(const void* a, const void* b, const float* sa, cons
   if (variant == 3) {
     const uint8_t* z = static_cast<const uint8_t*>(zero);
     if (!z || bm != 256 || bn != 256) return -1;
-    gemm_fp8_big_kernel<<<grid, 512, 0, stream>>>(p, z);
+    if ((amx || yq) && (N % 256 || K % 128)) return -1;
+    if (amx && yq) gemm_fp8_big_kernel<true, true><<<grid, 512, 0, stream>>>(p, z);
+    else if (amx) gemm_fp8_big_kernel<true, false><<<grid, 512, 0, stream>>>(p, z);
+    else if (yq) gemm_fp8_big_kernel<false, true><<<grid, 512, 0, stream>>>(p, z);
+    else gemm_fp8_big_kernel<false, false><<<grid, 512, 0, stream>>>(p, z);
     return (int)hipGetLastError();
   }
   if (variant == 2) {

@@ -229,6 +229,107 @@ __global__ __launch_bounds__(256) void stem_direct_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
+// The same stem for the camera-size case (no resize, mean 0, one std for the three channels —
+// YOLO's /255 — 3x3/2 pad 1, 16 output channels, 4-pixel aligned image columns): VALU work per
+// wave cut ~4x against stem_direct_kernel, which is VALU-issue bound (PMC: ~820 VALU per wave):
+//   * the tile holds RAW pixel values (0..255, exact in bf16) and 1/std is applied to the fp32
+//     accumulator in the epilogue FMA that adds the bias — no per-pixel normalisation;
+//   * it is filled 4 pixels per thread (three dword loads, v_cvt_f32_ubyte*, cvt_pk) into a
+//     tile whose rows start 3 pixels early, so a group of 4 lands on 2 aligned ds_write_b128 —
+//     no per-pixel index division, bounds test or byte load;
+//   * letterbox bars / conv padding are decided per group (aligned groups never straddle).
+constexpr int kSfTH = 8, kSfTW = 32;
+constexpr int kSfIH = 2 * kSfTH + 1;            // 17 input rows
+constexpr int kSfG = kSfTW / 2 + 1;             // 17 groups of 4 pixels per input row
+constexpr int kSfIW = 4 * kSfG;                 // 68 tile columns (tile col = input x - (2 ox0 - 1) + 3)
+__global__ __launch_bounds__(256) void stem_fast_kernel(
+    const uint8_t* __restrict__ in, bf16_t* __restrict__ out, const bf16_t* __restrict__ w,
+    const float* __restrict__ bias, int Hin, int Win, int Hc, int Wc, int off_t, int off_l, float fill_raw,
+    float inv_std, int bgr, int H1, int W1, int ldo, int act) {
+  __shared__ __attribute__((aligned(16))) uint32_t stile[kSfIH * kSfIW * 2];   // [17][68] x 4 bf16
+  const int tid = threadIdx.x, b = blockIdx.z, lane = tid & 63, wave = tid >> 6;
+  const int oy0 = blockIdx.y * kSfTH, ox0 = blockIdx.x * kSfTW;
+  const int g0 = (2 * ox0 - 4) >> 2;            // first group: canvas x 2 ox0 - 4 .. 2 ox0 - 1
+  const uint8_t* img = in + (long)b * Hin * Win * 3;
+  const uint32_t f2 = pack2(fill_raw, fill_raw), fb = f2 & 0xffffu;
+  for (int task = tid; task < kSfIH * kSfG; task += 256) {
+    const int ty = task / kSfG, gi = task - ty * kSfG;
+    const int yc = 2 * oy0 - 1 + ty, xc = 4 * (g0 + gi);
+    u32x4 lo = {0u, 0u, 0u, 0u}, hi = {0u, 0u, 0u, 0u};    // outside the canvas: zero padding
+    if (yc >= 0 && yc < Hc && xc >= 0 && xc < Wc) {
+      const int yo = yc - off_t, xo = xc - off_l;
+      if ((unsigned)yo < (unsigned)Hin && (unsigned)xo < (unsigned)Win) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(img + ((long)yo * Win + xo) * 3);
+        const uint32_t w0 = src[0], w1 = src[1], w2 = src[2];
+        // bytes: p0 = w0[0..2], p1 = w0[3] w1[0..1], p2 = w1[2..3] w2[0], p3 = w2[1..3]
+        float c[12];
+        const uint32_t wd[3] = {w0, w1, w2};
+#pragma unroll
+        for (int j = 0; j < 12; ++j) c[j] = (float)((wd[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+        if (bgr) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) { const float t = c[3 * q]; c[3 * q] = c[3 * q + 2]; c[3 * q + 2] = t; }
+        }
+        lo = u32x4{pack2(c[0], c[1]), pack2(c[2], 0.f), pack2(c[3], c[4]), pack2(c[5], 0.f)};
+        hi = u32x4{pack2(c[6], c[7]), pack2(c[8], 0.f), pack2(c[9], c[10]), pack2(c[11], 0.f)};
+      } else {                                   // letterbox bar (raw fill value)
+        lo = u32x4{f2, fb, f2, fb};
+        hi = lo;
+      }
+    }
+    uint32_t* dst = stile + 2 * (ty * kSfIW + 4 * gi);
+    *reinterpret_cast<u32x4*>(dst) = lo;
+    *reinterpret_cast<u32x4*>(dst + 4) = hi;
+  }
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  // this lane's two taps per 32-K half (k-piece pc = fq + 4 kk covers taps 2 pc, 2 pc + 1);
+  // tile offset of tap (dy, dx) for output (ly, lx): (2 ly + dy) row, 2 lx + dx + 2 col (the
+  // output's first input column 2 ox0 - 1 sits at tile col 3)
+  int toff[2][2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int t = 2 * (fq + 4 * kk) + h;
+      toff[kk][h] = t < 9 ? (t / 3) * kSfIW + (t % 3) + 3 : -1;
+    }
+  bf16x8 wa[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) wa[kk] = *reinterpret_cast<const bf16x8*>(w + (long)fr * 64 + 8 * (fq + 4 * kk));
+  float cb[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) cb[e] = bias ? bias[4 * fq + e] : 0.f;
+#pragma unroll
+  for (int pt = 0; pt < 4; ++pt) {
+    const int ly = 2 * wave + (pt >> 1), lx = 16 * (pt & 1) + fr;
+    const int base = 2 * ly * kSfIW + 2 * lx;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      uint2 p0 = {0u, 0u}, p1 = {0u, 0u};
+      if (toff[kk][0] >= 0) p0 = *reinterpret_cast<const uint2*>(stile + 2 * (base + toff[kk][0]));
+      if (toff[kk][1] >= 0) p1 = *reinterpret_cast<const uint2*>(stile + 2 * (base + toff[kk][1]));
+      const u32x4 pv = {p0.x, p0.y, p1.x, p1.y};
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[kk], __builtin_bit_cast(bf16x8, pv), acc, 0, 0, 0);
+    }
+    const int oy = oy0 + ly, ox = ox0 + lx;
+    if (oy < H1 && ox < W1) {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float a = fmaf(acc[e], inv_std, cb[e]);
+        if (act == 1) a = fmaxf(a, 0.f);
+        else if (act == 2) a = silu(a);
+        v[e] = a;
+      }
+      *reinterpret_cast<uint2*>(out + (((long)b * H1 + oy) * W1 + ox) * ldo + 4 * fq) =
+          make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Max pool (k x k, stride s, pad p) NHWC bf16, C % 8 == 0: one thread per 8 channels of one
 // output pixel (16-byte loads/stores).  Padding never wins (-inf).  ``ldx`` / ``ldy`` are the
 // pixel pitches, so input and output may be channel slices of concat buffers (YOLO SPPF).
@@ -546,6 +647,16 @@ extern "C" int aiko_stem_direct(const void* in, void* out, const void* w, const 
                                 const float* mean, const float* std, int bgr, int H1, int W1, int Cout, int ldo,
                                 int k, int stride, int pad, int act, hipStream_t stream) {
   if (Cout % 16 || ldo % 4 || k < 1 || k > 4 || stride < 1 || B <= 0) return -1;
+  static const bool fast_ok = [] { const char* e = getenv("AIKO_STEM_FAST"); return !(e && *e == '0'); }();
+  if (fast_ok && k == 3 && stride == 2 && pad == 1 && Cout == 16 && Ho == Hin && Wo == Win && Win % 4 == 0 &&
+      off_l % 4 == 0 && Wc % 4 == 0 && mean[0] == 0.f && mean[1] == 0.f && mean[2] == 0.f &&
+      std[0] == std[1] && std[1] == std[2] && std[0] > 0.f) {
+    dim3 grid((W1 + aiko::kSfTW - 1) / aiko::kSfTW, (H1 + aiko::kSfTH - 1) / aiko::kSfTH, B);
+    hipLaunchKernelGGL(aiko::stem_fast_kernel, grid, dim3(256), 0, stream, static_cast<const uint8_t*>(in),
+                       static_cast<aiko::bf16_t*>(out), static_cast<const aiko::bf16_t*>(w), bias, Hin, Win, Hc,
+                       Wc, off_t, off_l, fill, 1.f / std[0], bgr, H1, W1, ldo, act);
+    return (int)hipGetLastError();
+  }
   const int IH = (aiko::kStemTH - 1) * stride + k, IW = (aiko::kStemTW - 1) * stride + k;
   const size_t lds = (size_t)IH * IW * 8;
   if (lds > 64 * 1024) return -1;

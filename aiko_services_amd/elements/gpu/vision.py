@@ -22,7 +22,7 @@ import time
 
 import torch
 
-from ...gpu.element import DeviceResult, GpuPipelineElement, HostRing
+from ...gpu.element import DeviceResult, FramePool, GpuPipelineElement, HostRing
 from ...pipeline.stream import StreamEvent
 
 __all__ = ["SyntheticFrames", "FrameResize", "ImagePreprocess", "ResNet50Classifier", "ClassifierTopK"]
@@ -134,17 +134,32 @@ class FrameResize(GpuPipelineElement):
         context.set_protocol("frame_resize:0")
         super().__init__(context)
         self.size = _int(self.get_parameter("image_size", 224)[0], 224)
+        # ``pool: N`` — resize into N FramePool slots, each held by its frame until the frame
+        # completes: before a stage cut the hop then sends the slot itself (no staging copy,
+        # ``parallel/hop.py`` mark_frame_held); 0 = one buffer per lane, reused every frame
+        self.pool_slots = _int(self.get_parameter("pool", 0)[0], 0)
         self._out = {}
+        self._pools = {}
 
     def process_frame(self, stream, images):
         from ...ops import vision as V
         B = images.shape[0]
         if images.shape[1] == self.size and images.shape[2] == self.size:
             return StreamEvent.OKAY, {"images": images}
+        shape = (B, self.size, self.size, 3)
+        if self.pool_slots > 0:
+            pool = self._pools.get(B)
+            if pool is None:
+                pool = self._pools[B] = FramePool(self.pool_slots, B * self.size * self.size * 3, device=self.device)
+            slot = pool.acquire(30.0)
+            if slot >= 0:
+                out = pool.view(slot, shape, torch.uint8)
+                self.hold_for_frame(pool, slot)
+                from ...parallel.hop import mark_frame_held
+                return StreamEvent.OKAY, {"images": mark_frame_held(V.resize_u8(images, shape[1:3], out=out))}
         out = self._out.get((B, self.lane))
         if out is None:
-            out = self._out[(B, self.lane)] = torch.empty(B, self.size, self.size, 3, dtype=torch.uint8,
-                                                          device=self.device)
+            out = self._out[(B, self.lane)] = torch.empty(shape, dtype=torch.uint8, device=self.device)
         return StreamEvent.OKAY, {"images": V.resize_u8(images, (self.size, self.size), out=out)}
 
 

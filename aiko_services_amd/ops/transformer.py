@@ -12,6 +12,8 @@ Quantisation scheme (inference):
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass, field
 
 import torch
@@ -156,21 +158,31 @@ FP8_TILES = ((128, 128), (128, 64), (64, 128), (64, 64))
 def _tune_fp8(key, launch, mx=False):
     """Pick (BM, BN, variant) by measurement, like ``ops.conv.autotune`` (shares its switch)."""
     best, best_t = None, None
-    if mx:                               # MX-fp8 in/out: LDS-DMA kernel, whole 128-wide K chunks
+    if mx:                               # MX-fp8 in/out: LDS-DMA kernels, whole 128-wide K chunks
         cands = [(128, 128, 1), (64, 128, 1)]
     else:
         cands = [tt + (v,) for tt in FP8_TILES for v in (0, 1)]
         if key[1] % 128 == 0:
             cands.append((256, 128, 2))  # 8-wave LDS-DMA kernel (one workgroup per CU)
+    if key[1] % 256 == 0:
+        cands.append((256, 256, 3))      # 256 x 256 tile, 8 waves of 128 x 64 (MX in / out too)
+    skip = {s.strip() for s in os.environ.get("AIKO_FP8_SKIP", "").split(",") if s.strip()}
+    cands = [t for t in cands if ",".join(map(str, t)) not in skip] or cands
     for t in cands:
-        launch(t)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(3):
+        try:
             launch(t)
-        e1.record()
-        e1.synchronize()
-        ms = e0.elapsed_time(e1)
+            launch(t)
+        except RuntimeError:
+            continue
+        times = []
+        for _ in range(5):               # median of individually timed launches
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            launch(t)
+            e1.record()
+            e1.synchronize()
+            times.append(e0.elapsed_time(e1))
+        ms = sorted(times)[2]
         if best_t is None or ms < best_t:
             best, best_t = t, ms
     _tile_cache[key] = best

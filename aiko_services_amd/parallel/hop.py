@@ -45,6 +45,7 @@ tokens and are rebuilt (with a completion event) on the receiver.
 """
 from __future__ import annotations
 
+import weakref
 from collections import deque
 
 import torch
@@ -53,7 +54,7 @@ import torch.distributed as tdist
 from . import dist as D
 
 __all__ = ["HopPlane", "StageFailure", "NoCredit", "init_plane", "plane", "shutdown_plane", "is_token",
-           "needs_decode", "TOKEN", "FLOAT_TOKEN"]
+           "needs_decode", "mark_frame_held", "TOKEN", "FLOAT_TOKEN"]
 
 TOKEN = "T@"
 FLOAT_TOKEN = "F@"
@@ -104,12 +105,34 @@ def _nbytes(dtype, shape) -> int:
 
 
 def _layout(specs):
-    """Byte offsets of ``specs`` [(dtype, shape)] packed with 256-byte alignment; total size."""
+    """Byte offsets of ``specs`` [(dtype, shape)] packed with 256-byte alignment; total size.
+    A one-tensor message is exactly that tensor's bytes (it may be sent from the producer's
+    own buffer, see :func:`mark_frame_held`)."""
+    if len(specs) == 1:
+        return [0], max(_nbytes(*specs[0]), 1)
     offs, at = [], 0
     for dt, shape in specs:
         offs.append(at)
         at += (_nbytes(dt, shape) + _ALIGN - 1) // _ALIGN * _ALIGN
     return offs, max(at, _ALIGN)
+
+
+# Tensors whose storage their frame holds until it completes (a FramePool slot released by the
+# frame's on_complete): a forward hop of such a tensor, alone in its message, is sent straight
+# from it — no staging copy — since the frame (and so the buffer) outlives the hop's credit.
+_FRAME_HELD: dict = {}
+
+
+def mark_frame_held(t: torch.Tensor) -> torch.Tensor:
+    """Declare that ``t``'s storage stays untouched until the current frame completes."""
+    key = id(t)
+    _FRAME_HELD[key] = weakref.ref(t, lambda _r, k=key: _FRAME_HELD.pop(k, None))
+    return t
+
+
+def _frame_held(t) -> bool:
+    r = _FRAME_HELD.get(id(t))
+    return r is not None and r() is t
 
 
 def _view(buf: torch.Tensor, off: int, dtype, shape) -> torch.Tensor:
@@ -178,7 +201,7 @@ class _SendLink:
     def credit(self) -> int:
         return 0 if self.dead else self.free
 
-    def take(self, nbytes, key):
+    def take(self, nbytes, key, staging=True):
         if self.dead:
             raise StageFailure(self.peer)
         n = len(self.bufs)
@@ -194,7 +217,7 @@ class _SendLink:
             w.wait()                         # RCCL: stream-ordered; gloo: host waits (CPU tests)
             self.work[slot] = None
         buf = self.bufs[slot]
-        if buf is None or buf.numel() < nbytes:
+        if staging and (buf is None or buf.numel() < nbytes):
             buf = self.bufs[slot] = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
         self.holder[slot] = key
         self.free -= 1
@@ -323,7 +346,7 @@ class HopPlane:
         # host-side control group (gloo) for start-up barriers issued from helper threads
         self.control = tdist.new_group(backend="gloo") if D.is_initialized() else None
         self.counters = {"sent_msgs": 0, "sent_bytes": 0, "recv_msgs": 0, "recv_bytes": 0,
-                         "pool_overflow": 0, "pool_waits": 0, "resent": 0, "dead_peers": 0}
+                         "pool_overflow": 0, "pool_waits": 0, "resent": 0, "dead_peers": 0, "zero_copy": 0}
 
     # ---- credits / failure ------------------------------------------------------------------
     def credit(self, dst: int) -> int:
@@ -467,12 +490,21 @@ class HopPlane:
             return outs
         specs = [(t.dtype, tuple(t.shape)) for t in tensors]
         offs, total = _layout(specs)
-        slot, buf = link.take(total, key if key is not None else ())
+        t0 = tensors[0]
+        # zero copy: a forward hop whose only tensor is frame-held on this device goes out of
+        # the producer's buffer (its credit still bounds the frames in flight)
+        direct = (key is not None and len(tensors) == 1 and t0.device == self.device and t0.is_contiguous()
+                  and dst != self.rank and _frame_held(t0))
+        slot, buf = link.take(total, key if key is not None else (), staging=not direct)
         seq = link.seq
         link.seq += 1
-        for t, dstv in zip(tensors, _views(buf, offs, specs)):
-            dstv.copy_(t if t.device == buf.device else t.to(buf.device, non_blocking=True),
-                       non_blocking=True)
+        if direct:
+            buf = t0.reshape(-1).view(torch.uint8)
+            self.counters["zero_copy"] += 1
+        else:
+            for t, dstv in zip(tensors, _views(buf, offs, specs)):
+                dstv.copy_(t if t.device == buf.device else t.to(buf.device, non_blocking=True),
+                           non_blocking=True)
         for container, ckey, idx in slots:
             dt, shape = specs[idx]
             container[ckey] = (f"{TOKEN}{self.rank}/{seq}/{idx}/{_DTYPE_NAMES[dt]}/"
@@ -515,8 +547,9 @@ class HopPlane:
         old = self.send_links.get(old_dst)
         if old is not None and not old.dead and old_slot is not None:
             old.release(old_slot, reuse=False)        # the buffer moves with the frame
-        slot, _ = link.take(0, key)
-        link.bufs[slot] = buf
+        # the record keeps the bytes (a staging buffer, or the producer's frame-held buffer);
+        # the new link's slot is only the credit — it must never alias them
+        slot, _ = link.take(0, key, staging=False)
         seq = link.seq
         link.seq += 1
         self._post(link, slot, buf, total, dst)

@@ -130,8 +130,10 @@ def pp_definition(batch: int, graph: bool, height: int, width: int, world: int, 
     d["graph"] = ["(SyntheticFrames FrameResize ResNet50Classifier ClassifierTopK)"]
     # resize stays uint8 (224x224x3): cut after it, the stage boundary is 150 KB per frame; the
     # ResNet stage normalises into its stem buffer itself
+    # FrameResize writes into frame-held pool slots: the hop sends them without a staging copy
     pre = {"name": "FrameResize", "input": [{"name": "images", "type": "tensor"}],
-           "output": [{"name": "images", "type": "tensor"}], "parameters": {"image_size": 224},
+           "output": [{"name": "images", "type": "tensor"}],
+           "parameters": {"image_size": 224, "pool": max(6, 2 * world + 2)},
            "deploy": {"local": {"module": ELEMENTS}}}
     d["elements"].insert(1, pre)
     d["elements"][3]["parameters"]["gather"] = False

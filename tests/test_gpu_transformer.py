@@ -79,6 +79,38 @@ def test_flash_attention(native, B, T, Tpad, H):
     assert out.view(B, Tpad, d)[:, T:].abs().max().item() == 0
 
 
+@pytest.mark.parametrize("case", ["growing", "negative", "spiky"])
+def test_flash_attention_rescale_paths(native, case):
+    """Data that drives the online softmax's rare branches (guide rule: bounded random data
+    never takes them): per-query maxima that keep growing across key tiles (lazy rescale fires
+    mid-sequence), scores far below zero everywhere (first-tile max, no underflow to l = 0),
+    and isolated huge scores late in the sequence."""
+    from aiko_services_amd.ops import transformer as TR
+    g = torch.Generator().manual_seed(11)
+    B, H, T, Tpad = 2, 3, 700, 704
+    d = H * 64
+    q = torch.randn(B, Tpad, H, 64, generator=g)
+    k = torch.randn(B, Tpad, H, 64, generator=g)
+    v = torch.randn(B, Tpad, H, 64, generator=g)
+    if case == "growing":
+        k = k * torch.linspace(0.2, 6.0, Tpad).view(1, Tpad, 1, 1)      # later keys score higher
+        q = q * 2
+    elif case == "negative":
+        q = q.abs() * 4 + 4
+        k = -(k.abs() * 4 + 4)                                          # every score << 0
+    else:
+        k[:, 650] = q[:, :, :, :].mean(dim=1) * 40                     # one dominant late key
+    qkv = torch.cat([q, k, v], dim=2).reshape(B * Tpad, 3 * d).to(DEV, torch.bfloat16)   # [q | k | v] heads
+    out = torch.zeros(B * Tpad, d, dtype=torch.bfloat16, device=DEV)
+    TR.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], out, B, H, T, Tpad, 0.125)
+    x = qkv.float().view(B, Tpad, 3, H, 64)[:, :T]
+    qq, kk, vv = (x[:, :, i].transpose(1, 2) for i in range(3))
+    ref = F.scaled_dot_product_attention(qq, kk, vv, scale=0.125).transpose(1, 2).reshape(B, T, d)
+    got = out.view(B, Tpad, d)[:, :T].float()
+    assert torch.isfinite(got).all()
+    assert _rel(got, ref) < 2e-2, _rel(got, ref)
+
+
 def test_log_mel(native):
     from aiko_services_amd.ops import audio as AU
     g = torch.Generator().manual_seed(3)
@@ -142,25 +174,26 @@ def test_whisper_small_30s(native):
     assert torch.isfinite(y.float()).all()
 
 
-@pytest.mark.parametrize("bm", [128, 64])
-def test_gemm_fp8_mx_in_and_out(native, bm):
+@pytest.mark.parametrize("tile", [(128, 128, 1), (64, 128, 1), (256, 256, 3)])
+def test_gemm_fp8_mx_in_and_out(native, tile):
     """MX-fp8 activations: E8M0 block scales straight into the scaled MFMA (A side), and an
-    epilogue that quantises GELU(out) to MX-fp8 (fc1 -> fc2 without a bf16 round trip)."""
+    epilogue that quantises GELU(out) to MX-fp8 (fc1 -> fc2 without a bf16 round trip); the
+    128-wide LDS-DMA tiles and the 256 x 256 8-wave tile."""
     from aiko_services_amd.ops import transformer as TR
     g = torch.Generator().manual_seed(5)
-    M, N, K = 300, 384, 512
+    M, N, K = 300, 512, 512
     lin = TR.make_fp8_linear(torch.randn(N, K, generator=g) / 20, torch.randn(N, generator=g) * 0.1, DEV)
     # A side: MX-quantised input with a wide dynamic range across blocks
     x = torch.randn(M, K, generator=g) * torch.exp2(torch.randint(-6, 6, (M, K // 32), generator=g).float()
                                                     ).repeat_interleave(32, dim=1)
     q, sc = TR.mx_quantize_ref(x)
-    y = TR.linear_fp8(q.to(DEV), None, lin, x_mx=sc.to(DEV), tile=(bm, 128, 1))
+    y = TR.linear_fp8(q.to(DEV), None, lin, x_mx=sc.to(DEV), tile=tile)
     ref = TR.mx_dequant(q, sc).to(DEV) @ lin.ref_weight.T.to(DEV) + lin.bias
     assert _rel(y, ref) < 5e-3
     # output side: GELU then MX quantisation in the epilogue
     xq, xs = TR.quantize_rows_ref(torch.randn(M, K, generator=g))
     oq, osc = TR.mx_buffers(M, N, DEV)
-    TR.linear_fp8(xq.to(DEV), xs.to(DEV), lin, act=TR.ACT_GELU, out_mx=(oq, osc), tile=(bm, 128, 1))
+    TR.linear_fp8(xq.to(DEV), xs.to(DEV), lin, act=TR.ACT_GELU, out_mx=(oq, osc), tile=tile)
     full = F.gelu((xq.view(torch.float8_e4m3fn).float() * xs[:, None]).to(DEV) @ lin.ref_weight.T.to(DEV) + lin.bias)
     rq, rsc = TR.mx_quantize_ref(full.cpu())
     got = TR.mx_dequant(oq.cpu(), osc.cpu())
