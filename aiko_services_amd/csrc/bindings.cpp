@@ -81,6 +81,8 @@ int aiko_window_shift(const float* src, const float* chunk, float* dst, int B, i
 int aiko_conv_narrow(const void* x, const void* w, const float* bias, const void* res, void* y, int H, int W, int C,
                      int Cc, int R, int S, int stride, int pad, int Ho, int Wo, int M, int Cout, int K, int act,
                      int ldy, int ldr, hipStream_t stream);
+int aiko_stem_pool_u8(const void* frames, const void* w, const float* bias, void* y, int B, int Hi, int Wi,
+                      int Ho, int Wo, int Hm, int Wm, int ldy, const float* mean255, int variant, hipStream_t stream);
 int aiko_stem_pool(const void* x, const void* w, const float* bias, void* y, int B, int Hp, int Wp,
                    int Ho, int Wo, int Hm, int Wm, int ldy, int variant, hipStream_t stream);
 int aiko_softmax_topk(const void* logits, float* prob, int* index, int B, int N, int k,
@@ -441,6 +443,40 @@ void stem_pool_out(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b
   check_launch(aiko_stem_pool(x.data_ptr(), w.data_ptr(), bias.data_ptr<float>(), y.data_ptr(), B, Hp, Wp,
                               Ho, Wo, Hm, Wm, ldy, (int)variant, cur_stream()),
                "stem_pool");
+}
+
+// The same fused stem fed with uint8 frames [B, Hi, Wi, 3] (Wi % 4 == 0) — no pre-processing
+// kernel, no bf16 stem buffer: w is the weight image scaled by 1 / (255 std_c)
+// (ops.conv.stem_pool_u8), mean255 the per-channel 255 * mean subtracted in the kernel.
+void stem_pool_u8_out(const at::Tensor& frames, const at::Tensor& w, const at::Tensor& bias, at::Tensor& y,
+                      at::ArrayRef<double> mean255, int64_t variant) {
+  check_cuda(frames, "frames");
+  check_cuda(w, "w");
+  check_cuda(bias, "bias");
+  check_cuda(y, "y");
+  TORCH_CHECK(frames.scalar_type() == at::kByte && frames.dim() == 4 && frames.size(3) == 3 && frames.is_contiguous() &&
+                  frames.size(2) % 4 == 0,
+              "aiko.stem_pool_u8_out: frames must be contiguous uint8 [B, H, W, 3] with W % 4 == 0");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.dim() == 3 && w.size(0) == 7 && w.size(1) == 64 &&
+                  w.size(2) == 32 && w.is_contiguous(),
+              "aiko.stem_pool_u8_out: w must be the [7, 64, 32] swizzled stem weight image");
+  TORCH_CHECK(bias.scalar_type() == at::kFloat && bias.numel() == 64 && bias.is_contiguous(),
+              "aiko.stem_pool_u8_out: bias must be fp32 [64]");
+  TORCH_CHECK(mean255.size() == 3, "aiko.stem_pool_u8_out: mean255 has 3 values");
+  const int64_t B = frames.size(0), Hi = frames.size(1), Wi = frames.size(2);
+  const int64_t Ho = (Hi + 6 - 7) / 2 + 1, Wo = (Wi + 6 - 7) / 2 + 1;
+  const int64_t Hm = (Ho + 2 - 3) / 2 + 1, Wm = (Wo + 2 - 3) / 2 + 1;
+  const int64_t ldy = pixel_pitch(y, "stem_pool_u8_out");
+  TORCH_CHECK(y.size(0) == B && y.size(1) == Hm && y.size(2) == Wm && y.size(3) == 64,
+              "aiko.stem_pool_u8_out: y must be [B, ", Hm, ", ", Wm, ", 64]");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(frames.data_ptr()) % 4 == 0 &&
+                  reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(bias.data_ptr()) % 16 == 0,
+              "aiko.stem_pool_u8_out: frames 4-byte, w / bias 16-byte aligned");
+  const float m[3] = {(float)mean255[0], (float)mean255[1], (float)mean255[2]};
+  check_launch(aiko_stem_pool_u8(frames.data_ptr(), w.data_ptr(), bias.data_ptr<float>(), y.data_ptr(), B, Hi, Wi,
+                                 Ho, Wo, Hm, Wm, ldy, m, (int)variant, cur_stream()),
+               "stem_pool_u8");
 }
 
 void resize_u8_out(const at::Tensor& x, at::Tensor& y) {
@@ -989,6 +1025,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("zero_border_rows_(Tensor(a!) x, int rows) -> ()");
   m.def("sppf_pool_(Tensor(a!) cat, int c, int k) -> ()");
   m.def("stem_pool_out(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, int Ho, int Wo, int variant=0) -> ()");
+  m.def("stem_pool_u8_out(Tensor frames, Tensor w, Tensor bias, Tensor(a!) y, float[] mean255, int variant=0) -> ()");
   m.def("gemm_fp8_out(Tensor a, Tensor? sa, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!)? y, int act, int bm, int bn, int variant=0, Tensor? zero=None, Tensor? amx=None, Tensor(b!)? yq=None, Tensor(c!)? ysc=None) -> ()");
   m.def("rownorm_quant_out(Tensor x, Tensor? gamma, Tensor? beta, float eps, Tensor(a!)? yb, Tensor(b!)? q, Tensor(c!)? qs) -> ()");
   m.def("attn_fwd_out(Tensor q, Tensor k, Tensor v, Tensor(a!) o, int B, int H, int T, int Tpad, float scale) -> ()");
@@ -1018,6 +1055,7 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("zero_border_rows_", &zero_border_rows_);
   m.impl("sppf_pool_", &sppf_pool_);
   m.impl("stem_pool_out", &stem_pool_out);
+  m.impl("stem_pool_u8_out", &stem_pool_u8_out);
   m.impl("softmax_topk_out", &softmax_topk_out);
   m.impl("gemm_fp8_out", &gemm_fp8_out);
   m.impl("rownorm_quant_out", &rownorm_quant_out);

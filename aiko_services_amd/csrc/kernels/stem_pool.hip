@@ -61,9 +61,14 @@ struct StemPoolParams {
   const float* bias;    // [64]
   bf16_t* y;            // [B, Hm, Wm, ldy]
   int B, Hp, Wp, Ho, Wo, Hm, Wm, ldy, tiles_h, tiles_w;
+  // U8 variant: raw frames [B, Hi, Wi, 3] (the stem's image, no resize); the patch holds
+  // c - 255 mean_c (bf16) and the weight image is pre-scaled by 1 / (255 std_c)
+  const uint8_t* xu8;
+  int Hi, Wi;
+  float m0, m1, m2;
 };
 
-template <int TPW>
+template <int TPW, bool U8 = false>
 __global__ __launch_bounds__(256, StemTile<TPW>::WGS) void stem_pool_kernel(StemPoolParams p) {
   using T = StemTile<TPW>;
   constexpr int kTPW = TPW, kSRW = T::SRW, kNPix = T::NPIX, NB = T::NB;
@@ -85,7 +90,49 @@ __global__ __launch_bounds__(256, StemTile<TPW>::WGS) void stem_pool_kernel(Stem
   const int sy0 = 2 * py0 - 1, sx0 = 2 * px0 - 1;      // stem region origin
   const int gy0 = 2 * sy0, gx0 = 2 * sx0;               // patch origin in the padded buffer
 
-  // ---- 1. patch + weights -> LDS by buffer DMA (no VGPR staging, no ds_write) ----
+  // ---- 1. patch + weights -> LDS ----
+  if constexpr (U8) {
+    // U8: the patch straight from the uint8 frame — no bf16 stem buffer in HBM, no separate
+    // pre-processing kernel.  Patch pixel (r, j) is image pixel (gy0 - 3 + r, gx0 - 3 + j)
+    // (the padded buffer's border is 3); 4-pixel groups aligned in the image (three dword
+    // loads), each pixel written as one 8-byte [c0 - m0, c1 - m1, c2 - m2, 0] entry; outside
+    // the image: 0 (= the normalised conv padding).  The weights still come by DMA.
+    const int xa = ((gx0 - 3) >> 2) << 2;                // floor to a 4-pixel boundary
+    constexpr int G = kPatchW / 4 + 1;                   // groups per patch row
+    const uint8_t* im = p.xu8 + (size_t)img * p.Hi * p.Wi * 3;
+    for (int task = tid; task < kPatchH * G; task += 256) {
+      const int r = task / G, gi = task - r * G;
+      const int y = gy0 - 3 + r, x = xa + 4 * gi;
+      float c[12];
+#pragma unroll
+      for (int e = 0; e < 12; ++e) c[e] = 0.f;
+      const bool in = (unsigned)y < (unsigned)p.Hi && x >= 0 && x + 3 < p.Wi;
+      if (in) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(im + ((size_t)y * p.Wi + x) * 3);
+        const uint32_t wd[3] = {src[0], src[1], src[2]};
+#pragma unroll
+        for (int e = 0; e < 12; ++e) c[e] = (float)((wd[e >> 2] >> (8 * (e & 3))) & 0xFFu);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = x + q - (gx0 - 3);
+        if ((unsigned)j >= (unsigned)kPatchW) continue;
+        uint2 o = {0u, 0u};
+        if (in) o = make_uint2(pack2(c[3 * q] - p.m0, c[3 * q + 1] - p.m1), pack2(c[3 * q + 2] - p.m2, 0.f));
+        *reinterpret_cast<uint2*>(patch + r * kPatchRowB + j * 8) = o;
+      }
+    }
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(p.w), (short)0, kWB, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < kWB / 16 / 256; ++k)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rw, reinterpret_cast<__attribute__((address_space(3))) void*>(
+                  reinterpret_cast<uintptr_t>(wl + (k * 4 + wave) * 1024)), 16,
+          (uint32_t)(((k * 4 + wave) * 64 + lane) * 16), 0, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else
+  // buffer DMA (no VGPR staging, no ds_write)
   // patch chunk i (row i / (W/2), 2 pixels) lands at LDS byte 16 i: one wave instruction
   // fills 64 consecutive chunks.  Chunks outside the image get an offset past num_records,
   // which the hardware reads as zero (conv padding / region beyond the image); the rounds
@@ -233,6 +280,9 @@ extern "C" int aiko_stem_pool(const void* x, const void* w, const float* bias, v
                               hipStream_t stream) {
   using namespace aiko;
   StemPoolParams p;
+  p.xu8 = nullptr;
+  p.Hi = p.Wi = 0;
+  p.m0 = p.m1 = p.m2 = 0.f;
   p.x = static_cast<const bf16_t*>(x);
   p.w = static_cast<const bf16_t*>(w);
   p.bias = bias;
@@ -247,5 +297,33 @@ extern "C" int aiko_stem_pool(const void* x, const void* w, const float* bias, v
     stem_pool_kernel<14><<<dim3((unsigned)grid), dim3(256), 0, stream>>>(p);
   else
     stem_pool_kernel<7><<<dim3((unsigned)grid), dim3(256), 0, stream>>>(p);
+  return (int)hipGetLastError();
+}
+
+// uint8 frames [B, Hi, Wi, 3] (Wi % 4 == 0) straight into the fused stem + pool: ``w`` is the
+// weight image pre-scaled by 1 / (255 std_c), ``mean255`` the per-channel 255 * mean.
+extern "C" int aiko_stem_pool_u8(const void* frames, const void* w, const float* bias, void* y, int B, int Hi,
+                                 int Wi, int Ho, int Wo, int Hm, int Wm, int ldy, const float* mean255,
+                                 int variant, hipStream_t stream) {
+  using namespace aiko;
+  if (Wi % 4 || B <= 0) return -1;
+  StemPoolParams p;
+  p.x = nullptr;
+  p.xu8 = static_cast<const uint8_t*>(frames);
+  p.Hi = Hi; p.Wi = Wi;
+  p.m0 = mean255[0]; p.m1 = mean255[1]; p.m2 = mean255[2];
+  p.w = static_cast<const bf16_t*>(w);
+  p.bias = bias;
+  p.y = static_cast<bf16_t*>(y);
+  p.B = B; p.Hp = Hi + 6; p.Wp = Wi + 6; p.Ho = Ho; p.Wo = Wo; p.Hm = Hm; p.Wm = Wm; p.ldy = ldy;
+  const int tpw = variant == 1 ? 14 : 7;
+  p.tiles_h = (Hm + kTPH - 1) / kTPH;
+  p.tiles_w = (Wm + tpw - 1) / tpw;
+  const long grid = (long)B * p.tiles_h * p.tiles_w;
+  if (grid <= 0 || grid > 0x7fffffffL) return -1;
+  if (tpw == 14)
+    stem_pool_kernel<14, true><<<dim3((unsigned)grid), dim3(256), 0, stream>>>(p);
+  else
+    stem_pool_kernel<7, true><<<dim3((unsigned)grid), dim3(256), 0, stream>>>(p);
   return (int)hipGetLastError();
 }

@@ -232,8 +232,8 @@ __global__ __launch_bounds__(256) void stem_direct_kernel(
 // The same stem for the camera-size case (no resize, mean 0, one std for the three channels —
 // YOLO's /255 — 3x3/2 pad 1, 16 output channels, 4-pixel aligned image columns): VALU work per
 // wave cut ~4x against stem_direct_kernel, which is VALU-issue bound (PMC: ~820 VALU per wave):
-//   * the tile holds RAW pixel values (0..255, exact in bf16) and 1/std is applied to the fp32
-//     accumulator in the epilogue FMA that adds the bias — no per-pixel normalisation;
+//   * the tile holds RAW pixel values (0..255, exact in bf16) and 1/(255 std) is applied to the
+//     fp32 accumulator in the epilogue FMA that adds the bias — no per-pixel normalisation;
 //   * it is filled 4 pixels per thread (three dword loads, v_cvt_f32_ubyte*, cvt_pk) into a
 //     tile whose rows start 3 pixels early, so a group of 4 lands on 2 aligned ds_write_b128 —
 //     no per-pixel index division, bounds test or byte load;
@@ -654,7 +654,7 @@ extern "C" int aiko_stem_direct(const void* in, void* out, const void* w, const 
     dim3 grid((W1 + aiko::kSfTW - 1) / aiko::kSfTW, (H1 + aiko::kSfTH - 1) / aiko::kSfTH, B);
     hipLaunchKernelGGL(aiko::stem_fast_kernel, grid, dim3(256), 0, stream, static_cast<const uint8_t*>(in),
                        static_cast<aiko::bf16_t*>(out), static_cast<const aiko::bf16_t*>(w), bias, Hin, Win, Hc,
-                       Wc, off_t, off_l, fill, 1.f / std[0], bgr, H1, W1, ldo, act);
+                       Wc, off_t, off_l, fill, 1.f / (255.f * std[0]), bgr, H1, W1, ldo, act);
     return (int)hipGetLastError();
   }
   const int IH = (aiko::kStemTH - 1) * stride + k, IW = (aiko::kStemTW - 1) * stride + k;

@@ -206,10 +206,8 @@ class ResNet50Classifier(GpuPipelineElement):
     def _run(self, images):
         tag = f"lane{self.lane}." if self.lane else ""
         if images.dtype == torch.uint8:
-            x = self.model.preprocess(images, tag)
-        else:
-            x = images
-        return self.model.logits_from_stem(x, tag)
+            return self.model.logits(images, tag)       # uint8 fused stem when the size fits
+        return self.model.logits_from_stem(images, tag)
 
     def _run_a(self, images):
         return self.model.logits_part_a(images, f"lane{self.lane}." if self.lane else "")

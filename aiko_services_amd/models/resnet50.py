@@ -99,6 +99,9 @@ class ResNet50(WeightsMixin):
         self.mall_blocks = int(os.environ.get("AIKO_RESNET_MALL_BLOCKS", "3"))
         # conv_chain: identity block's 1x1 expansion + next block's 1x1 reduction in one launch
         self.chain = os.environ.get("AIKO_RESNET_CHAIN", "1") != "0"
+        # uint8 frames of the model's own size go straight into the fused stem (it normalises
+        # while filling its LDS patch): no pre-processing kernel, no bf16 stem buffer
+        self.stem_u8 = os.environ.get("AIKO_STEM_U8", "1") != "0"
 
     # ---- workspace: every activation buffer allocated once per batch size ----------------
     def _buf(self, key: str, shape, dtype=torch.bfloat16) -> torch.Tensor:
@@ -120,9 +123,39 @@ class ResNet50(WeightsMixin):
         Hp, Wp = C.stem_geometry(S, S)
         return V.preprocess_frames(frames, (S, S), out=self._buf(tag + "pre", (B, Hp, Wp, 4)))
 
-    def features_from_stem(self, x: torch.Tensor, tag: str = "", after_block=None) -> torch.Tensor:
+    def _stem_u8_ok(self, frames: torch.Tensor) -> bool:
+        S = self.image_size
+        return (self.stem_u8 and self.fuse_stem_pool and frames.dtype == torch.uint8 and frames.dim() == 4
+                and frames.shape[1] == S and frames.shape[2] == S and S % 4 == 0 and frames.is_contiguous()
+                and not (0 < self.mall_chunk < frames.shape[0]))
+
+    def features_from_frames(self, frames: torch.Tensor, tag: str = "", after_block=None) -> torch.Tensor:
+        """uint8 frames -> pooled features: through the uint8 fused stem when the frames have
+        the model's size, else pre-processing + :meth:`features_from_stem`."""
+        if not self._stem_u8_ok(frames):
+            return self.features_from_stem(self.preprocess(frames, tag), tag, after_block=after_block)
+        B = frames.shape[0]
+        Ho, Wo = C.stem_out_hw(self.image_size, self.image_size)
+        Hm, Wm = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
+        pool = C.stem_pool_u8(frames, self.stem, V.IMAGENET_MEAN, V.IMAGENET_STD,
+                              out=self._buf(tag + "pool", (B, Hm, Wm, 64)))
+        return self.features_from_stem(None, tag, after_block=after_block, pooled=pool)
+
+    def features_from_stem(self, x: torch.Tensor | None, tag: str = "", after_block=None,
+                           pooled: torch.Tensor | None = None) -> torch.Tensor:
         """Stem buffer -> pooled features bf16 [B, 2048].  ``after_block`` = (index, fn): call
-        ``fn()`` once bottleneck ``index`` is enqueued (-1: after the max-pool)."""
+        ``fn()`` once bottleneck ``index`` is enqueued (-1: after the max-pool).  ``pooled``: the
+        stem + max-pool output already computed (``x`` unused)."""
+        if pooled is not None:
+            B = pooled.shape[0]
+            if after_block is not None and after_block[0] < 0:
+                after_block[1]()
+            x, t1 = pooled, None
+            for bi in range(len(self.blocks)):
+                x, t1 = self._block(bi, x, tag, B, 0, B, t1)
+                if after_block is not None and after_block[0] == bi:
+                    after_block[1]()
+            return V.avgpool(x, out=self._buf(tag + "gap", (B, x.shape[3])))
         B = x.shape[0]
         S = self.image_size
         Ho, Wo = C.stem_out_hw(S, S)
@@ -224,13 +257,12 @@ class ResNet50(WeightsMixin):
             with torch.cuda.stream(s):
                 xi = x[i * step:(i + 1) * step]
                 tag = f"l{i}."
-                if frames:
-                    xi = self.preprocess(xi, tag)
                 hook = None
                 if stagger is not None and i + 1 < lanes:
                     gate = torch.cuda.Event()
                     hook = (stagger, lambda ev=gate, st=s: ev.record(st))
-                f = self.features_from_stem(xi, tag, after_block=hook)
+                f = self.features_from_frames(xi, tag, after_block=hook) if frames \
+                    else self.features_from_stem(xi, tag, after_block=hook)
                 C.linear(f, self.fc, out=out[i * step:(i + 1) * step])
         for s in self._lanes(lanes):
             cur.wait_stream(s)
@@ -241,13 +273,16 @@ class ResNet50(WeightsMixin):
 
     def logits_part_a(self, frames: torch.Tensor, tag: str = "") -> torch.Tensor:
         """uint8 frames -> activation after bottleneck ``SPLIT_BLOCK`` (a workspace buffer)."""
-        x = frames if frames.dtype != torch.uint8 else self.preprocess(frames, tag)
-        B = x.shape[0]
+        B = frames.shape[0]
         S = self.image_size
         Ho, Wo = C.stem_out_hw(S, S)
         Hm, Wm = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
         pool = self._buf(tag + "pool", (B, Hm, Wm, 64))
-        if self.fuse_stem_pool:
+        u8 = self._stem_u8_ok(frames)
+        x = frames if frames.dtype != torch.uint8 or u8 else self.preprocess(frames, tag)
+        if u8:
+            x = C.stem_pool_u8(frames, self.stem, V.IMAGENET_MEAN, V.IMAGENET_STD, out=pool)
+        elif self.fuse_stem_pool:
             x = C.stem_pool(x, self.stem, (S, S), out=pool)
         else:
             st = self._buf(tag + "stem", (B, Ho, Wo, 64))
@@ -269,7 +304,7 @@ class ResNet50(WeightsMixin):
 
     def features(self, frames: torch.Tensor) -> torch.Tensor:
         """uint8 [B, H, W, 3] -> pooled features bf16 [B, 2048]."""
-        return self.features_from_stem(self.preprocess(frames))
+        return self.features_from_frames(frames)
 
     def logits_from_stem(self, x: torch.Tensor, tag: str = "") -> torch.Tensor:
         f = self.features_from_stem(x, tag)
@@ -282,7 +317,7 @@ class ResNet50(WeightsMixin):
                               index=self._buf("index", (B, self.topk), torch.int32))
 
     def logits(self, frames: torch.Tensor, tag: str = "") -> torch.Tensor:
-        f = self.features_from_stem(self.preprocess(frames, tag), tag)
+        f = self.features_from_frames(frames, tag)
         return C.linear(f, self.fc, out=self._buf(tag + "logits", (f.shape[0], self.num_classes)))
 
     def forward(self, frames: torch.Tensor):

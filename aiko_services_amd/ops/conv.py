@@ -479,6 +479,46 @@ def stem_pool(x: torch.Tensor, spec: ConvSpec, image_hw: tuple[int, int],
     return out
 
 
+def stem_pool_u8_weight(spec: ConvSpec, std) -> torch.Tensor:
+    """The fused stem's weight image (:func:`stem_pool_weight`) with input channel c scaled by
+    1 / (255 std_c): the uint8 variant feeds ``pixel - 255 mean_c`` instead of the normalised
+    value.  Cached and re-derived in place like the unscaled image."""
+    key = (spec.weight.data_ptr(), spec.weight._version, tuple(float(v) for v in std))
+    cached = getattr(spec, "_stem_pool_u8_w", None)
+    if cached is not None and cached[0] == key:
+        return cached[1]
+    base = stem_pool_weight(spec).float().view(7, 64, 4, 8)               # [r, o, chunk, 2 px x 4 ch]
+    scale = torch.tensor([1.0 / (255.0 * float(v)) for v in std] + [0.0], device=base.device)
+    img = (base.view(7, 64, 4, 2, 4) * scale).to(torch.bfloat16).view(7, 64, 32)
+    if cached is not None:
+        cached[1].copy_(img)
+        img = cached[1]
+    else:
+        img = img.contiguous()
+    spec._stem_pool_u8_w = (key, img)
+    return img
+
+
+def stem_pool_u8(frames: torch.Tensor, spec: ConvSpec, mean, std, out: torch.Tensor | None = None,
+                 variant: int | None = None) -> torch.Tensor:
+    """:func:`stem_pool` fed with uint8 frames ``[B, H, W, 3]`` (the stem's own image size,
+    ``W % 4 == 0``): the kernel normalises while it fills its LDS patch — no pre-processing
+    kernel and no bf16 stem buffer round trip through HBM.  ``mean`` / ``std`` as for
+    :func:`ops.vision.preprocess_frames` (fractions of 255)."""
+    if spec.kind != "stem" or spec.stem_k != 7 or spec.stride != 2 or spec.cout != 64 \
+            or spec.act != ACT_RELU or spec.bias is None:
+        raise ValueError("stem_pool_u8: needs a 7x7/s2 ReLU stem spec with 64 channels and a bias")
+    B, H, W, _ = frames.shape
+    Ho, Wo = spec.out_hw(H, W)
+    Hm, Wm = (Ho - 1) // 2 + 1, (Wo - 1) // 2 + 1
+    if out is None:
+        out = torch.empty(B, Hm, Wm, 64, dtype=torch.bfloat16, device=frames.device)
+    torch.ops.aiko.stem_pool_u8_out(frames, stem_pool_u8_weight(spec, std), spec.bias, out,
+                                    [255.0 * float(m) for m in mean],
+                                    STEM_POOL_VARIANT if variant is None else variant)
+    return out
+
+
 def linear(x: torch.Tensor, spec: ConvSpec, out: torch.Tensor | None = None,
            residual: torch.Tensor | None = None) -> torch.Tensor:
     """``[B, K] @ W^T + b`` on the same kernel (1x1 "image")."""

@@ -365,7 +365,7 @@ def test_batchnorm_standalone(native):
     assert out[..., 32:].abs().max().item() == 0
 
 
-@pytest.mark.parametrize("hw", [(224, 224), (160, 200)])
+@pytest.mark.parametrize("hw", [(224, 224), (160, 200), (96, 132)])
 def test_stem_pool_fused(native, hw):
     """Fused stem + ReLU + max-pool kernel == conv2d stem + maxpool kernels (bit-exact), and
     the fp32 torch reference of the same ops."""
@@ -389,3 +389,12 @@ def test_stem_pool_fused(native, hw):
     xr = R.preprocess_ref(frames.to(DEV), hw)
     ref = F.max_pool2d(R.conv_ref(xr.to(torch.bfloat16).float(), spec), 3, 2, 1)
     assert _rel_err(fused.permute(0, 3, 1, 2), ref) < 1e-2
+    # uint8 frames straight into the fused stem (normalised in the kernel's patch fill): the
+    # same values within bf16 rounding of the input / scaled weights, both tile widths
+    if hw[1] % 4 == 0:
+        for variant in (0, 1):
+            u8 = C.stem_pool_u8(frames.to(DEV), spec, V.IMAGENET_MEAN, V.IMAGENET_STD, variant=variant)
+            torch.cuda.synchronize()
+            assert u8.shape == fused.shape
+            assert _rel_err(u8.permute(0, 3, 1, 2), ref) < 1e-2
+            assert _rel_err(u8.float(), fused.float()) < 1e-2
