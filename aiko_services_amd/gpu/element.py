@@ -32,6 +32,8 @@ __all__ = ["GpuPipelineElement", "DeviceResult", "FramePool", "CapturedCall", "H
 # outputs of captured graphs.  run_maybe_captured captures a per-address graph at once for
 # inputs at these addresses; any other address must recur before it gets one.
 _STABLE_PTRS: set = set()
+# AIKO_GRAPH_ADMIT=0: every new address gets its own graph at once (round-2 behaviour, A/B)
+_ADMIT_ALL = __import__("os").environ.get("AIKO_GRAPH_ADMIT", "1") == "0"
 
 _DTYPE_CODES = {torch.uint8: 0, torch.int8: 1, torch.int16: 2, torch.int32: 3, torch.int64: 4,
                 torch.float16: 5, torch.float32: 6, torch.float64: 7, torch.bool: 11,
@@ -295,12 +297,13 @@ class GpuPipelineElement(PipelineElement):
     max_seen_addresses = 64
 
     def run_maybe_captured(self, key, fn, *inputs):
-        """Replay a hipGraph of ``fn`` for this input signature and lane.  Inputs at stable
-        addresses (FramePool slots cycling, static outputs of an upstream captured graph) get
-        one graph per address, captured on the buffer itself — no per-frame input copy.  Any
-        other address gets its own graph only once it recurs (a transient buffer never pays a
-        capture); until then, and for addresses that never recur, one graph with copied-in
-        static inputs runs.  Per-address graphs are kept LRU, ``max_graphs_per_key`` per key."""
+        """Replay a hipGraph of ``fn`` for this input signature and lane, captured on the input
+        buffers themselves (one graph per input address — FramePool slots and element rings
+        cycle through a few — no per-frame input copy).  Per-address graphs are kept LRU,
+        ``max_graphs_per_key`` per key; once that many exist, a NEW address gets its own graph
+        only if it is known stable (a FramePool slot, an upstream graph's static output) or it
+        recurs — a stream of transient buffers runs one graph with copied-in static inputs
+        instead of paying a capture each."""
         if not self.use_graph:
             return fn(*inputs)
         base = (key, self.lane)
@@ -315,7 +318,8 @@ class GpuPipelineElement(PipelineElement):
             graphs.move_to_end(addrs)
             return call.graph_replay()
         seen = self._captured[("seen",) + base]
-        if all(a in _STABLE_PTRS for a in addrs) or addrs in seen:
+        if (_ADMIT_ALL or len(graphs) < self.max_graphs_per_key or addrs in seen
+                or all(a in _STABLE_PTRS for a in addrs)):
             seen.pop(addrs, None)
             call = graphs[addrs] = CapturedCall(fn, inputs, static=True)
             if len(graphs) > self.max_graphs_per_key:

@@ -258,31 +258,38 @@ def test_run_maybe_captured_admission(native):
     static outputs of captured graphs): transient buffers run the copy-in graph and never pay a
     capture; per-address graphs are kept LRU."""
     from aiko_services_amd.gpu.element import FramePool, GpuPipelineElement
-    el = object.__new__(GpuPipelineElement)
-    el.use_graph, el._captured = True, {}
+
+    class _El:                      # the graph-cache state of an element, without a pipeline
+        use_graph, lane = True, 0
+        max_graphs_per_key = GpuPipelineElement.max_graphs_per_key
+        max_seen_addresses = GpuPipelineElement.max_seen_addresses
+        run_maybe_captured = GpuPipelineElement.run_maybe_captured
+        _retire_graph = GpuPipelineElement._retire_graph
+    el = _El()
+    el._captured = {}
+    el.max_graphs_per_key = 2
 
     def fn(x):
         return x * 2 + 1
-    for i in range(5):                                  # transient inputs
-        x = torch.full((256,), float(i), device="cuda")
+    keep = [torch.full((256,), float(i), device="cuda") for i in range(2)]
+    for x in keep:                                      # warm phase: graphs at first sight
         assert torch.equal(el.run_maybe_captured("k", fn, x), x * 2 + 1)
     graphs = el._captured[("graphs", "k", 0)]
-    assert len(graphs) == 0
+    assert len(graphs) == 2
+    transient = [torch.full((256,), 10.0 + i, device="cuda") for i in range(4)]   # distinct addresses
+    for x in transient:                                 # cache full: transient inputs, no capture
+        assert torch.equal(el.run_maybe_captured("k", fn, x), x * 2 + 1)
+    assert list(graphs) == [(t.data_ptr(),) for t in keep]
     x = torch.zeros(256, device="cuda")                 # a recurring address: graph on 2nd visit
     for v in (3.0, 4.0, 5.0):
         x.fill_(v)
         assert torch.equal(el.run_maybe_captured("k", fn, x), x * 2 + 1)
-    assert list(graphs) == [(x.data_ptr(),)]
+    assert list(graphs) == [(keep[1].data_ptr(),), (x.data_ptr(),)]     # LRU dropped the oldest
     pool = FramePool(2, 1024, device="cuda:0")         # a pool slot: captured at first sight
     slot = pool.view(pool.acquire(0.1), (256,), torch.float32)
     slot.fill_(7.0)
     assert torch.equal(el.run_maybe_captured("k", fn, slot), slot * 2 + 1)
-    assert len(graphs) == 2
-    el.max_graphs_per_key = 2                           # LRU: the oldest graph goes
-    y = torch.ones(256, device="cuda")
-    for _ in range(2):
-        assert torch.equal(el.run_maybe_captured("k", fn, y), y * 2 + 1)
-    assert list(graphs) == [(slot.data_ptr(),), (y.data_ptr(),)]
+    assert list(graphs) == [(x.data_ptr(),), (slot.data_ptr(),)]
     slot.fill_(-1.0)
     assert torch.equal(el.run_maybe_captured("k", fn, slot), slot * 2 + 1)
     torch.cuda.synchronize()
