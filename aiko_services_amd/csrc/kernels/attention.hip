@@ -57,6 +57,18 @@ __device__ __forceinline__ float max_xor16_32(float v) {
 
 typedef __attribute__((ext_vector_type(4))) short v4i16;
 
+// target builtins behind __device__ helpers (the host pass of a __global__ template must not
+// see them directly, or the kernel's host stub is silently dropped)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t attn_rsrc(const void* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void attn_dma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, void* lds) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(
+      r, reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(lds)), 16, voff,
+      soff, 0, 0);
+}
+
 // byte offset of 16-bit column `col` (multiple of 4) of key row `row` in the V image
 __device__ __forceinline__ int v_off(int row, int col) {
   return row * (kDH * 2) + (((col >> 4) ^ ((row >> 1) & 3)) << 5) + ((col & 15) << 1);
@@ -127,20 +139,32 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
     for (int ks = 0; ks < 2; ++ks) asm volatile("" : "+v"(qf[qt][ks]));
 
   // K / V tiles by LDS-DMA (lane-linear destination, swizzle on the SOURCE): instruction i of
-  // wave w fills rows (NT/8)*i + 8w .. +7; lane l -> row (l >> 3), physical 16-B slot (l & 7)
+  // wave w fills rows (NT/8)*i + 8w .. +7; lane l -> row (l >> 3), physical 16-B slot (l & 7).
+  // buffer_load ... lds against a per-sequence descriptor: the per-lane 32-bit offsets are
+  // tile-invariant and the tile's key offset rides in the scalar soffset, so issuing a tile
+  // costs no VALU (the 64-bit address math was ~35 VALU per tile); keys past T fall outside
+  // num_records and read as zeros (masked in the last tile, and p = 0 x V = 0).
   const int drow = wave * 8 + (lane >> 3);
   const int ps = lane & 7;
   const int k_lp = ps ^ (lane >> 3);                                   // K: piece ^ (row & 7)
+  const __amdgpu_buffer_rsrc_t rk = attn_rsrc(p.k + seq0 * p.ldk, p.T * p.ldk * 2);
+  const __amdgpu_buffer_rsrc_t rv = attn_rsrc(p.v + seq0 * p.ldv, p.T * p.ldv * 2);
+  uint32_t k_off[PPT], v_off_b[PPT];
+#pragma unroll
+  for (int i = 0; i < PPT; ++i) {
+    const int row = drow + (NT / 8) * i;
+    const int v_lp = ((((ps >> 1) ^ ((row >> 1) & 3))) << 1) | (ps & 1);
+    k_off[i] = (uint32_t)(row * p.ldk + hc + k_lp * 8) * 2u;
+    v_off_b[i] = (uint32_t)(row * p.ldv + hc + v_lp * 8) * 2u;
+  }
   auto issue = [&](int t0, int slot) {
     bf16_t* Ks = smem + slot * 2 * TILE;
     bf16_t* Vs = Ks + TILE;
+    const uint32_t sk = (uint32_t)(t0 * p.ldk) * 2u, sv = (uint32_t)(t0 * p.ldv) * 2u;
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
-      const int row = drow + (NT / 8) * i;
-      const int key = min(t0 + row, p.T - 1);   // keys past T: finite row T-1, masked later
-      const int v_lp = ((((ps >> 1) ^ ((row >> 1) & 3))) << 1) | (ps & 1);
-      glds16_asm(p.k + (seq0 + key) * p.ldk + hc + k_lp * 8, Ks + ((NT / 8) * i + wave * 8) * kDH);
-      glds16_asm(p.v + (seq0 + key) * p.ldv + hc + v_lp * 8, Vs + ((NT / 8) * i + wave * 8) * kDH);
+      attn_dma16(rk, k_off[i], sk, Ks + ((NT / 8) * i + wave * 8) * kDH);
+      attn_dma16(rv, v_off_b[i], sv, Vs + ((NT / 8) * i + wave * 8) * kDH);
     }
   };
 
