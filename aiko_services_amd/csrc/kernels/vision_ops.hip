@@ -1,5 +1,7 @@
 // Memory-bound vision kernels for gfx950: frame pre-processing, pooling, classifier head.
 // All NHWC, bf16 activations, 16-byte vectorised where the layout allows (Guideline 13).
+#include <type_traits>
+
 #include "common.h"
 
 namespace aiko {
@@ -242,10 +244,11 @@ constexpr int kSfTH = 8, kSfTW = 32;
 constexpr int kSfIH = 2 * kSfTH + 1;            // 17 input rows
 constexpr int kSfG = kSfTW / 2 + 1;             // 17 groups of 4 pixels per input row
 constexpr int kSfIW = 4 * kSfG;                 // 68 tile columns (tile col = input x - (2 ox0 - 1) + 3)
+template <int ACT, bool BGR>
 __global__ __launch_bounds__(256) void stem_fast_kernel(
     const uint8_t* __restrict__ in, bf16_t* __restrict__ out, const bf16_t* __restrict__ w,
     const float* __restrict__ bias, int Hin, int Win, int Hc, int Wc, int off_t, int off_l, float fill_raw,
-    float inv_std, int bgr, int H1, int W1, int ldo, int act) {
+    float inv_std, int H1, int W1, int ldo) {
   __shared__ __attribute__((aligned(16))) uint32_t stile[kSfIH * kSfIW * 2];   // [17][68] x 4 bf16
   const int tid = threadIdx.x, b = blockIdx.z, lane = tid & 63, wave = tid >> 6;
   const int oy0 = blockIdx.y * kSfTH, ox0 = blockIdx.x * kSfTW;
@@ -266,7 +269,7 @@ __global__ __launch_bounds__(256) void stem_fast_kernel(
         const uint32_t wd[3] = {w0, w1, w2};
 #pragma unroll
         for (int j = 0; j < 12; ++j) c[j] = (float)((wd[j >> 2] >> (8 * (j & 3))) & 0xFFu);
-        if (bgr) {
+        if constexpr (BGR) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) { const float t = c[3 * q]; c[3 * q] = c[3 * q + 2]; c[3 * q + 2] = t; }
         }
@@ -300,10 +303,15 @@ __global__ __launch_bounds__(256) void stem_fast_kernel(
   float cb[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) cb[e] = bias ? bias[4 * fq + e] : 0.f;
+  // this lane's output pixel (2 wave, fr) of the tile, 32-bit element offsets from the image
+  const bf16_t* obase = out + (size_t)b * H1 * W1 * ldo;
+  const int orow = oy0 + 2 * wave, ocol = ox0 + fr;
+  const uint32_t o0 = (uint32_t)((orow * W1 + ocol) * ldo + 4 * fq);
+  const int lbase = 4 * wave * kSfIW + 2 * fr;              // tile pixel of output (2 wave, fr)
 #pragma unroll
   for (int pt = 0; pt < 4; ++pt) {
-    const int ly = 2 * wave + (pt >> 1), lx = 16 * (pt & 1) + fr;
-    const int base = 2 * ly * kSfIW + 2 * lx;
+    const int dy = pt >> 1, dx = 16 * (pt & 1);
+    const int base = lbase + 2 * dy * kSfIW + 2 * dx;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -313,17 +321,16 @@ __global__ __launch_bounds__(256) void stem_fast_kernel(
       const u32x4 pv = {p0.x, p0.y, p1.x, p1.y};
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[kk], __builtin_bit_cast(bf16x8, pv), acc, 0, 0, 0);
     }
-    const int oy = oy0 + ly, ox = ox0 + lx;
-    if (oy < H1 && ox < W1) {
+    if (orow + dy < H1 && ocol + dx < W1) {
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float a = fmaf(acc[e], inv_std, cb[e]);
-        if (act == 1) a = fmaxf(a, 0.f);
-        else if (act == 2) a = silu(a);
+        if constexpr (ACT == 1) a = fmaxf(a, 0.f);
+        else if constexpr (ACT == 2) a = silu(a);
         v[e] = a;
       }
-      *reinterpret_cast<uint2*>(out + (((long)b * H1 + oy) * W1 + ox) * ldo + 4 * fq) =
+      *reinterpret_cast<uint2*>(const_cast<bf16_t*>(obase) + o0 + (uint32_t)((dy * W1 + dx) * ldo)) =
           make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
     }
   }
@@ -652,9 +659,18 @@ extern "C" int aiko_stem_direct(const void* in, void* out, const void* w, const 
       off_l % 4 == 0 && Wc % 4 == 0 && mean[0] == 0.f && mean[1] == 0.f && mean[2] == 0.f &&
       std[0] == std[1] && std[1] == std[2] && std[0] > 0.f) {
     dim3 grid((W1 + aiko::kSfTW - 1) / aiko::kSfTW, (H1 + aiko::kSfTH - 1) / aiko::kSfTH, B);
-    hipLaunchKernelGGL(aiko::stem_fast_kernel, grid, dim3(256), 0, stream, static_cast<const uint8_t*>(in),
-                       static_cast<aiko::bf16_t*>(out), static_cast<const aiko::bf16_t*>(w), bias, Hin, Win, Hc,
-                       Wc, off_t, off_l, fill, 1.f / (255.f * std[0]), bgr, H1, W1, ldo, act);
+    auto go = [&](auto act_tag, auto bgr_tag) {
+      constexpr int A = decltype(act_tag)::value;
+      constexpr bool G = decltype(bgr_tag)::value;
+      aiko::stem_fast_kernel<A, G><<<grid, 256, 0, stream>>>(
+          static_cast<const uint8_t*>(in), static_cast<aiko::bf16_t*>(out), static_cast<const aiko::bf16_t*>(w),
+          bias, Hin, Win, Hc, Wc, off_t, off_l, fill, 1.f / (255.f * std[0]), H1, W1, ldo);
+    };
+    using F = std::false_type;
+    using T = std::true_type;
+    if (act == 2) bgr ? go(std::integral_constant<int, 2>{}, T{}) : go(std::integral_constant<int, 2>{}, F{});
+    else if (act == 1) bgr ? go(std::integral_constant<int, 1>{}, T{}) : go(std::integral_constant<int, 1>{}, F{});
+    else bgr ? go(std::integral_constant<int, 0>{}, T{}) : go(std::integral_constant<int, 0>{}, F{});
     return (int)hipGetLastError();
   }
   const int IH = (aiko::kStemTH - 1) * stride + k, IW = (aiko::kStemTW - 1) * stride + k;
