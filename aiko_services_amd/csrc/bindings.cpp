@@ -64,7 +64,8 @@ int aiko_gemm_fp8(const void* a, const void* b, const float* sa, const float* sb
 int aiko_rownorm_quant(const void* x, int ldx, const float* gamma, const float* beta, float eps,
                        void* yb, int ldyb, void* q, int ldq, float* qs, int M, int D, hipStream_t stream);
 int aiko_attn_fwd(const void* q, const void* k, const void* v, void* o, int ldq, int ldk, int ldv,
-                  int ldo, int B, int H, int T, int Tpad, int dh, float scale, hipStream_t stream);
+                  int ldo, int B, int H, int T, int Tpad, int dh, float scale, void* work, long work_bytes,
+                  hipStream_t stream);
 int aiko_logmel(const float* audio, int B, int N, const float* mel, int n_mels, const int* mel_range,
                 int n_fft, int hop, int F, float* logmel, int* gmax, void* dst, int rows, int pad, int ld,
                 hipStream_t stream);
@@ -821,7 +822,8 @@ void rownorm_quant_out(const at::Tensor& x, const c10::optional<at::Tensor>& gam
 
 // q/k/v/o: [B*Tpad, >= H*64] row-major (column slices of a fused QKV buffer allowed)
 void attn_fwd_out(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& o,
-                  int64_t B, int64_t H, int64_t T, int64_t Tpad, double scale) {
+                  int64_t B, int64_t H, int64_t T, int64_t Tpad, double scale,
+                  const c10::optional<at::Tensor>& work) {
   for (const at::Tensor* t : {&q, &k, &v, (const at::Tensor*)&o}) {
     check_cuda(*t, "q/k/v/o");
     TORCH_CHECK(t->scalar_type() == at::kBFloat16, "aiko.attn_fwd_out: bf16 tensors required");
@@ -829,8 +831,17 @@ void attn_fwd_out(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
     row_pitch(*t, H * 64, "attn_fwd_out", "q/k/v/o");
   }
   TORCH_CHECK(T >= 1 && T <= Tpad, "aiko.attn_fwd_out: 1 <= T <= Tpad");
+  void* wp = nullptr;
+  long wb = 0;
+  if (work.has_value() && work->defined()) {
+    check_cuda(*work, "work");
+    TORCH_CHECK(work->is_contiguous() && reinterpret_cast<uintptr_t>(work->data_ptr()) % 256 == 0,
+                "aiko.attn_fwd_out: work must be a contiguous, 256-byte aligned (zero-initialised) buffer");
+    wp = work->data_ptr();
+    wb = (long)(work->numel() * work->element_size());
+  }
   check_launch(aiko_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), q.stride(0), k.stride(0),
-                             v.stride(0), o.stride(0), B, H, T, Tpad, 64, (float)scale, cur_stream()),
+                             v.stride(0), o.stride(0), B, H, T, Tpad, 64, (float)scale, wp, wb, cur_stream()),
                "attn_fwd");
 }
 
@@ -1028,7 +1039,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("stem_pool_u8_out(Tensor frames, Tensor w, Tensor bias, Tensor(a!) y, float[] mean255, int variant=0) -> ()");
   m.def("gemm_fp8_out(Tensor a, Tensor? sa, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!)? y, int act, int bm, int bn, int variant=0, Tensor? zero=None, Tensor? amx=None, Tensor(b!)? yq=None, Tensor(c!)? ysc=None) -> ()");
   m.def("rownorm_quant_out(Tensor x, Tensor? gamma, Tensor? beta, float eps, Tensor(a!)? yb, Tensor(b!)? q, Tensor(c!)? qs) -> ()");
-  m.def("attn_fwd_out(Tensor q, Tensor k, Tensor v, Tensor(a!) o, int B, int H, int T, int Tpad, float scale) -> ()");
+  m.def("attn_fwd_out(Tensor q, Tensor k, Tensor v, Tensor(a!) o, int B, int H, int T, int Tpad, float scale, Tensor(b!)? work=None) -> ()");
   m.def("logmel_out(Tensor audio, Tensor mel, Tensor mel_range, int n_fft, int hop, int F, Tensor(a!) work, Tensor(b!) gmax, Tensor(c!) dst, int rows, int pad) -> ()");
   m.def("softmax_topk_out(Tensor logits, Tensor(a!) prob, Tensor(b!) index, int k) -> ()");
   m.def("embed_tokens_out(Tensor ids, Tensor pos, Tensor tok, Tensor pemb, Tensor(a!) x) -> ()");

@@ -37,6 +37,11 @@ struct AttnParams {
   int ldq, ldk, ldv, ldo;
   int T, Tpad, H;
   float scale_log2;     // softmax scale * log2(e)
+  // split-KV tail (split_s > 0; SM = 1 kernels): 1-D grid, per XCD `split_full` whole items
+  // then `split_r` items cut into split_s key ranges; see aiko_attn_fwd
+  int nqb, split_s, split_full, split_r, split_fence;
+  float* part;          // [pieces][QB][64] fp32 partial O, then [pieces][QB] (m, l) pairs
+  int* cnt;             // [8 * split_r] arrival counters, zero between launches
 };
 
 constexpr int kKB = 64, kDH = 64;
@@ -101,11 +106,31 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, g = lane >> 4;
+  const int ntiles = (p.T + kKB - 1) / kKB;
   // XCD-aware mapping: the query blocks of one (sequence, head) share its K/V stream, so they
   // are placed on one XCD (one L2) instead of round-robin over all eight
-  const int nqb = gridDim.x;
-  const int lin = xcd_remap(blockIdx.x + nqb * (blockIdx.y + gridDim.y * blockIdx.z),
-                            nqb * gridDim.y * gridDim.z);
+  const int nqb = p.nqb;
+  int lin, piece = -1, su = 0, tb = 0, te = ntiles;
+  if (p.split_s == 0) {
+    lin = xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
+                    gridDim.x * gridDim.y * gridDim.z);
+  } else {
+    // split-KV tail: workgroup b runs on XCD b % 8 as that XCD's (b / 8)-th dispatch; each XCD
+    // owns a contiguous range of items, the last split_r of them cut into split_s key ranges
+    // that fill the final round's slots instead of leaving them idle
+    const int xcd = blockIdx.x & 7, idx = blockIdx.x >> 3;
+    const int n = p.split_full + p.split_r;
+    if (idx < p.split_full) {
+      lin = xcd * n + idx;
+    } else {
+      const int j = idx - p.split_full;
+      lin = xcd * n + p.split_full + j / p.split_s;
+      piece = j % p.split_s;
+      su = xcd * p.split_r + j / p.split_s;
+      tb = piece * ntiles / p.split_s;
+      te = (piece + 1) * ntiles / p.split_s;
+    }
+  }
   const int qblk = lin % nqb, h = (lin / nqb) % p.H, b = lin / (nqb * p.H);
   const long seq0 = (long)b * p.Tpad;
   const int q0 = qblk * QB + wave * 32;
@@ -203,15 +228,14 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
   // transposed-read lane geometry: lane 4q'+p' of its 16-lane group addresses row q', cols 4p'
   const int trq = fr >> 2, trp = fr & 3;
 
-  const int ntiles = (p.T + kKB - 1) / kKB;
   if constexpr (REG) {
-    load_regs(0);
+    load_regs(tb * kKB);
     write_regs(0);
-    if (1 < ntiles) load_regs(kKB);              // tile 1 in flight in VGPRs
+    if (tb + 1 < te) load_regs((tb + 1) * kKB);  // tile tb+1 in flight in VGPRs
   } else {
 #pragma unroll
     for (int j = 0; j < NS - 1; ++j)
-      if (j < ntiles) issue(j * kKB, j);
+      if (tb + j < te) issue((tb + j) * kKB, j);
   }
   int slot = 0;
   // one key tile; MASK only for the ragged last tile (keeps the compare/select chain out of the
@@ -223,20 +247,20 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
       // tile it is in LDS (written last iteration) and every wave is done with tile it-1, whose
       // slot now takes tile it+1 from the VGPRs; then tile it+2's loads go out under compute
       __syncthreads();
-      if (it + 1 < ntiles) {
+      if (it + 1 < te) {
         write_regs(slot ^ 1);
-        if (it + 2 < ntiles) load_regs(t0 + 2 * kKB);
+        if (it + 2 < te) load_regs(t0 + 2 * kKB);
       }
     } else {
       // retire tile it (this wave's DMAs; the younger tiles stay in flight), then barrier
-      if (it + 2 < ntiles) {
+      if (it + 2 < te) {
         asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(2 * PER) : "memory");
-      } else if (it + 1 < ntiles) {
+      } else if (it + 1 < te) {
         asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(PER) : "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       }
-      if (it + NS - 1 < ntiles) issue(t0 + (NS - 1) * kKB, slot == 0 ? NS - 1 : slot - 1);
+      if (it + NS - 1 < te) issue(t0 + (NS - 1) * kKB, slot == 0 ? NS - 1 : slot - 1);
     }
     const bf16_t* Kc = smem + slot * 2 * TILE;
     const bf16_t* Vc = Kc + TILE;
@@ -304,10 +328,10 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
         float mloc = fmaxf(s[3][qt][3], fmaxf(m01, m23));
         mloc = fmaxf(mloc, fmaxf(m45, m67));
         mloc = max_xor16_32(fmaxf(mloc, m89));
-        if (it == 0 || mloc > kRescale) {
+        if (it == tb || mloc > kRescale) {
           // first tile: m_run = the tile max; later: raise it (lazy, > kRescale) — shift this
           // tile's scores to the new max and rescale what O / l hold
-          if (it != 0) {
+          if (it != tb) {
             const float alpha = fast_exp2(-mloc);
             lsum[qt] *= alpha;
 #pragma unroll
@@ -399,8 +423,65 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
     slot = slot == NS - 1 ? 0 : slot + 1;
   };
   const int nfull = p.T / kKB;               // tiles with every key < T
-  for (int it = 0; it < nfull; ++it) tile(it, std::false_type{});
-  if (nfull < ntiles) tile(nfull, std::true_type{});
+  const int tfull = te < nfull ? te : nfull;
+  for (int it = tb; it < tfull; ++it) tile(it, std::false_type{});
+  if (nfull < te) tile(nfull, std::true_type{});
+
+  if constexpr (SM == 1) {
+    if (piece >= 0) {
+      // a key-range piece: publish (m, l, unnormalised O) for its rows; the last of the
+      // split_s pieces to arrive merges them: O = sum_i 2^(m_i - M) O_i / sum_i 2^(m_i - M) l_i
+      const int pieces = 8 * p.split_r * p.split_s;
+      float* po = p.part + (size_t)(su * p.split_s + piece) * QB * kDH;
+      float* pml = p.part + (size_t)pieces * QB * kDH + (size_t)(su * p.split_s + piece) * QB * 2;
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        const int lr = wave * 32 + qt * 16 + fr;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) *reinterpret_cast<f32x4*>(po + lr * kDH + d * 16 + 4 * g) = o[d][qt];
+        if (g == 0) *reinterpret_cast<f32x2*>(pml + lr * 2) = f32x2{m_run[qt], lsum[qt][0]};
+      }
+      __shared__ int last;
+      if (p.split_fence) {
+        __threadfence();
+      } else {
+        // the pieces of one item run on one XCD (see the mapping above), so its L2 is the point
+        // of coherence: the stores only have to be complete at L2 before the arrival count
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+      if (tid == 0) {
+        const int old = atomicAdd(p.cnt + su, 1);
+        last = old == p.split_s - 1;
+        if (last) p.cnt[su] = 0;                 // re-armed for the next launch
+      }
+      __syncthreads();
+      if (!last) return;
+      if (p.split_fence) __threadfence();
+      const float* po0 = p.part + (size_t)su * p.split_s * QB * kDH;
+      const float* pml0 = p.part + (size_t)pieces * QB * kDH + (size_t)su * p.split_s * QB * 2;
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        const int lr = wave * 32 + qt * 16 + fr;
+        float mx = -INFINITY;
+        for (int i = 0; i < p.split_s; ++i) mx = fmaxf(mx, pml0[(size_t)i * QB * 2 + lr * 2]);
+        float l = 0.f;
+        f32x4 acc[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
+                        f32x4{0.f, 0.f, 0.f, 0.f}};
+        for (int i = 0; i < p.split_s; ++i) {
+          const f32x2 ml = *reinterpret_cast<const f32x2*>(pml0 + (size_t)i * QB * 2 + lr * 2);
+          const float w = fast_exp2(ml[0] - mx);
+          l += w * ml[1];
+#pragma unroll
+          for (int d = 0; d < 4; ++d)
+            acc[d] += w * *reinterpret_cast<const f32x4*>(po0 + (size_t)i * QB * kDH + lr * kDH + d * 16 + 4 * g);
+        }
+#pragma unroll
+        for (int d = 0; d < 4; ++d) o[d][qt] = acc[d];
+        lsum[qt] = f32x4{l, l, l, l};
+      }
+    }
+  }
 
   // normalise and write O[q][dh]: lane holds dh = d*16 + 4g + j for its query
 #pragma unroll
@@ -429,9 +510,14 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
 
 }  // namespace aiko
 
+// work / work_bytes: optional zero-initialised workspace (fp32 partials + arrival counters) for
+// the split-KV tail: when the (query block, head, sequence) items leave a partial last round on
+// each XCD (Whisper-small: 1,152 items = 2.25 rounds of 512 slots), that round's items are cut
+// into key ranges so it runs at full occupancy.  Without a workspace (or for the round-2 softmax
+// variants) the grid is the plain one.
 extern "C" int aiko_attn_fwd(const void* q, const void* k, const void* v, void* o, int ldq, int ldk,
                              int ldv, int ldo, int B, int H, int T, int Tpad, int dh, float scale,
-                             hipStream_t stream) {
+                             void* work, long work_bytes, hipStream_t stream) {
   if (dh != aiko::kDH || T < 1 || Tpad < T) return -1;
   aiko::AttnParams p;
   p.q = static_cast<const aiko::bf16_t*>(q);
@@ -441,14 +527,58 @@ extern "C" int aiko_attn_fwd(const void* q, const void* k, const void* v, void* 
   p.ldq = ldq; p.ldk = ldk; p.ldv = ldv; p.ldo = ldo;
   p.T = T; p.Tpad = Tpad; p.H = H;
   p.scale_log2 = scale * 1.4426950408889634f;
+  p.split_s = p.split_full = p.split_r = 0;
+  p.part = nullptr;
+  p.cnt = nullptr;
   static const int variant = [] {
     const char* v = getenv("AIKO_ATTN_VARIANT");
     return v ? atoi(v) : 0;
   }();
+  // pieces per split item; 0 = no split.  Measured on MI355X at Whisper-small shapes (median of
+  // 7 x 50 launches, scripts/attn_split_ab.sh): unsplit 135.1-135.4 us, s=2 133.2-134.4, s=4
+  // 147.5-148.3, s=8 134.1-135.4, and the 1-D mapping alone (s=1) 139.7-140.4 — the final-round
+  // model (whole slots idle) does not hold on the hardware, so the split stays opt-in
+  const char* split_env = getenv("AIKO_ATTN_SPLIT_S");   // read per call (tests flip it)
+  const int force_s = split_env ? atoi(split_env) : 0;
+  static const int fence = [] {
+    const char* v = getenv("AIKO_ATTN_SPLIT_FENCE");
+    return v ? atoi(v) : 0;
+  }();
+  p.split_fence = fence;
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    return n;
+  }();
   auto launch = [&](auto nw_tag, auto vpre_tag, auto reg_tag, auto sm_tag) {
     constexpr int NW = decltype(nw_tag)::value, VPRE = decltype(vpre_tag)::value;
     constexpr int REG = decltype(reg_tag)::value, SM = decltype(sm_tag)::value;
-    dim3 grid((T + 32 * NW - 1) / (32 * NW), H, B), block(64 * NW);
+    constexpr int QB = 32 * NW;
+    p.nqb = (T + QB - 1) / QB;
+    const long items = (long)p.nqb * H * B;
+    const int ntiles = (T + aiko::kKB - 1) / aiko::kKB;
+    if (SM == 1 && work && force_s > 0 && cus >= 8 && items % 8 == 0) {
+      const long n = items / 8;
+      const int slots = (16 / NW) * (cus / 8);          // resident workgroups per XCD
+      const int r = (int)(n % slots);
+      if (r > 0 && 2 * r <= slots) {
+        const int sp = force_s < ntiles ? force_s : ntiles;
+        const long cnt_b = ((8L * r * 4 + 255) / 256) * 256;
+        const long need = cnt_b + 8L * r * sp * QB * (aiko::kDH + 2) * 4;
+        if (sp >= 1 && need <= work_bytes) {
+          p.split_s = sp;
+          p.split_r = r;
+          p.split_full = (int)(n - r);
+          p.cnt = static_cast<int*>(work);
+          p.part = reinterpret_cast<float*>(static_cast<char*>(work) + cnt_b);
+          dim3 grid((unsigned)(8 * (p.split_full + (long)r * sp))), block(64 * NW);
+          aiko::attn_fwd_kernel<NW, VPRE, REG, SM><<<grid, block, 0, stream>>>(p);
+          return;
+        }
+      }
+    }
+    dim3 grid(p.nqb, H, B), block(64 * NW);
     aiko::attn_fwd_kernel<NW, VPRE, REG, SM><<<grid, block, 0, stream>>>(p);
   };
   using R0 = std::integral_constant<int, 0>;

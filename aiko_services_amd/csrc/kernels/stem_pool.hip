@@ -266,6 +266,218 @@ __global__ __launch_bounds__(256, StemTile<TPW>::WGS) void stem_pool_kernel(Stem
   }
 }
 
+
+// ---- strip variant (uint8 frames): one workgroup walks a 7-wide column of pooled tiles ----
+//
+// The tile kernel above re-loads the 28 KB weight image into LDS for every 8 x 7 pooled tile,
+// re-reads the A fragments from LDS for every wave, recomputes a one-row stem halo per tile and
+// pools from a full 17 x 15 stem tile (9 LDS reads per output).  By LDS traffic it is bound
+// well before its MFMAs (~370 KB of LDS reads/writes per 448 MFMAs).  Here:
+//  * a workgroup owns one strip — all Hm/8 pooled tiles of 7 columns of one image — and keeps
+//    the A fragments (7 filter rows x 4 channel blocks, 112 VGPRs) in registers for the whole
+//    strip: weights are read once per strip, from L2, never through LDS;
+//  * each tile computes exactly the 16 new stem rows 2 py0 .. 2 py0 + 15 (one 16-column stem row
+//    per MFMA column block, wave w rows 4w .. 4w + 3); the pool's upper halo row is the previous
+//    tile's last stem row, still in the other half of the double-buffered pool tile (zeros above
+//    the image: ReLU outputs are >= 0, so 0 is a valid -inf for the max);
+//  * the horizontal 3-wide / stride-2 max runs in registers: stem column fr sits in lane fr of a
+//    16-lane DPP row, so max(v[fr-1], v[fr], v[fr+1]) is two row_shr / row_shl moves; only the
+//    7 odd lanes store, into a 16-row x 7-pixel tile (pixel pitch 144 B: the 7 pixels' 8-byte
+//    writes land in disjoint bank octets), and the vertical max reads 3 rows per output;
+//  * the next tile's uint8 patch is loaded into registers before this tile's MFMAs and written
+//    to the other patch buffer after the epilogue: one global-load latency per tile is hidden.
+// Bit-identical to the tile kernel (same patch values, same MFMA order per accumulator).
+constexpr int kSpRows = 16;                              // stem rows per tile
+constexpr int kSpCols = 16;                              // stem columns per strip (15 used)
+constexpr int kSpPW = 2 * (kSpCols - 1) + 8;             // 38 patch pixels per row
+constexpr int kSpPH = 2 * (kSpRows - 1) + 7;             // 37 patch rows
+constexpr int kSpRowB = kSpPW * 8;                       // 304 B
+constexpr int kSpPatchB = kSpPH * kSpRowB;               // 11248 B
+constexpr int kSpHpPitch = 144;                          // pool-tile pixel pitch
+constexpr int kSpHpRowB = 7 * kSpHpPitch;                // 1008 B
+constexpr int kSpHpB = kSpRows * kSpHpRowB;              // 16128 B
+constexpr int kSpGroups = kSpPW / 4 + 2;                 // 4-pixel groups per patch row (11)
+constexpr int kSpTasks = kSpPH * kSpGroups;              // 407
+constexpr int kSpTaskIt = (kSpTasks + 255) / 256;        // 2
+
+__device__ __forceinline__ uint32_t sp_dpp_shr1(uint32_t v) {       // lane i <- lane i - 1 (16-lane rows)
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t sp_dpp_shl1(uint32_t v) {       // lane i <- lane i + 1
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x101, 0xF, 0xF, true);
+}
+
+// (a helper, not __builtin_elementwise_max on u32x4 subscripts inside a loop: hipcc folded that
+// form to element 0 broadcast into all four dwords)
+__device__ __forceinline__ uint32_t sp_max3_u16x2(uint32_t a, uint32_t b, uint32_t c) {
+  const u16x2 m = __builtin_elementwise_max(__builtin_elementwise_max(__builtin_bit_cast(u16x2, a),
+                                                                      __builtin_bit_cast(u16x2, b)),
+                                            __builtin_bit_cast(u16x2, c));
+  return __builtin_bit_cast(uint32_t, m);
+}
+
+__global__ __launch_bounds__(256, 2) void stem_pool_strip_kernel(StemPoolParams p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * kSpPatchB + 2 * kSpHpB];
+  __shared__ __attribute__((aligned(16))) float bias_l[64];
+  unsigned char* patch0 = smem;
+  unsigned char* hp0 = smem + 2 * kSpPatchB;
+  if (threadIdx.x < 16)
+    *reinterpret_cast<f32x4*>(bias_l + 4 * threadIdx.x) = *reinterpret_cast<const f32x4*>(p.bias + 4 * threadIdx.x);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int strips = p.tiles_w;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int img = bid / strips;
+  const int sj = bid - img * strips;
+  const int px0 = sj * 7;                                // first pooled column
+  const int sx0 = 2 * px0 - 1;                           // first stem column
+  const int ix0 = 2 * sx0 - 3;                           // patch column 0 in the image
+  const int xa = ix0 >= 0 ? (ix0 & ~3) : -((3 - ix0) & ~3);   // floor to a 4-pixel boundary
+  const uint8_t* im = p.xu8 + (size_t)img * p.Hi * p.Wi * 3;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // ---- A fragments: the whole weight image in registers for the strip ----
+  bf16x8 af[7][4];
+#pragma unroll
+  for (int r = 0; r < 7; ++r)
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      const int o = mb * 16 + fr;
+      af[r][mb] = *reinterpret_cast<const bf16x8*>(
+          reinterpret_cast<const unsigned char*>(p.w) + r * 64 * 64 + (o * 4 + (fq ^ ((o >> 2) & 2))) * 16);
+    }
+
+  // ---- uint8 patch fill: load (registers) then store (LDS, normalised bf16) ----
+  uint32_t pre[kSpTaskIt][3];
+  auto load_patch = [&](int py0) {
+    const int iy0 = 4 * py0 - 3;                          // image row of patch row 0
+#pragma unroll
+    for (int k = 0; k < kSpTaskIt; ++k) {
+      const int task = tid + k * 256;
+      const int r = task / kSpGroups, gi = task - r * kSpGroups;
+      const int y = iy0 + r, x = xa + 4 * gi;
+      pre[k][0] = pre[k][1] = pre[k][2] = 0u;
+      if (task < kSpTasks && (unsigned)y < (unsigned)p.Hi && x >= 0 && x + 3 < p.Wi) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(im + ((size_t)y * p.Wi + x) * 3);
+        pre[k][0] = __builtin_nontemporal_load(src);
+        pre[k][1] = __builtin_nontemporal_load(src + 1);
+        pre[k][2] = __builtin_nontemporal_load(src + 2);
+      }
+    }
+  };
+  auto store_patch = [&](unsigned char* patch, int py0) {
+    const int iy0 = 4 * py0 - 3;
+#pragma unroll
+    for (int k = 0; k < kSpTaskIt; ++k) {
+      const int task = tid + k * 256;
+      if (task >= kSpTasks) continue;
+      const int r = task / kSpGroups, gi = task - r * kSpGroups;
+      const int y = iy0 + r, x = xa + 4 * gi;
+      const bool in = (unsigned)y < (unsigned)p.Hi && x >= 0 && x + 3 < p.Wi;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = x + q - ix0;
+        if ((unsigned)j >= (unsigned)kSpPW) continue;
+        uint2 o = {0u, 0u};
+        if (in) {
+          const int e = 3 * q;
+          const float c0 = (float)((pre[k][e >> 2] >> (8 * (e & 3))) & 0xFFu);
+          const float c1 = (float)((pre[k][(e + 1) >> 2] >> (8 * ((e + 1) & 3))) & 0xFFu);
+          const float c2 = (float)((pre[k][(e + 2) >> 2] >> (8 * ((e + 2) & 3))) & 0xFFu);
+          o = make_uint2(pack2(c0 - p.m0, c1 - p.m1), pack2(c2 - p.m2, 0.f));
+        }
+        *reinterpret_cast<uint2*>(patch + r * kSpRowB + j * 8) = o;
+      }
+    }
+  };
+
+  int b_off[4];
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) b_off[nb] = 2 * (wave * 4 + nb) * kSpRowB + 16 * fr + 16 * fq;
+  const bool col_ok = (unsigned)(sx0 + fr) < (unsigned)p.Wo;
+  const bool store_lane = (fr & 1) && fr < 15;
+  const int hp_lane = ((fr - 1) >> 1) * kSpHpPitch + fq * 8;
+
+  load_patch(0);
+  store_patch(patch0, 0);
+  __syncthreads();
+
+  for (int t = 0; t < p.tiles_h; ++t) {
+    const int py0 = t * 8;
+    const int sy0 = 2 * py0;
+    unsigned char* patch = patch0 + (t & 1) * kSpPatchB;
+    unsigned char* hp = hp0 + (t & 1) * kSpHpB;
+    const unsigned char* hprev = hp0 + ((t + 1) & 1) * kSpHpB;
+    const bool more = t + 1 < p.tiles_h;
+    if (more) load_patch(py0 + 8);
+
+    // two stem rows (column blocks) at a time: 32 accumulator VGPRs beside the 112 of A
+    // fragments (with all four rows live the compiler re-loaded the weights every tile)
+#pragma unroll
+    for (int np = 0; np < 2; ++np) {
+      f32x4 acc[4][2];
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) acc[mb][0] = acc[mb][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 7; ++r)
+#pragma unroll
+        for (int nj = 0; nj < 2; ++nj) {
+          const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(patch + r * kSpRowB + b_off[2 * np + nj]);
+#pragma unroll
+          for (int mb = 0; mb < 4; ++mb)
+            acc[mb][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[r][mb], bfr, acc[mb][nj], 0, 0, 0);
+        }
+      if (np == 0) __syncthreads();                      // pool(t - 1) is done with hp / hprev
+
+      // ---- epilogue: bias + ReLU (v_med3 against 0 and a per-lane ceiling: 0 for stem pixels
+      // outside the image, so they act as the pool's -inf), bf16 pack, then the 3-wide
+      // horizontal max on the packed bit patterns (values >= 0): two row_shr / row_shl DPP
+      // moves and two v_pk_max_u16 per dword; the 7 odd lanes store ----
+#pragma unroll
+      for (int nj = 0; nj < 2; ++nj) {
+        const int row = wave * 4 + 2 * np + nj;
+        const float hi = (col_ok && sy0 + row < p.Ho) ? __builtin_inff() : 0.f;
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+          const f32x4 bias = *reinterpret_cast<const f32x4*>(bias_l + mb * 16 + fq * 4);
+          const f32x2 s01 = f32x2{acc[mb][nj][0], acc[mb][nj][1]} + f32x2{bias[0], bias[1]};
+          const f32x2 s23 = f32x2{acc[mb][nj][2], acc[mb][nj][3]} + f32x2{bias[2], bias[3]};
+          const uint32_t w01 = pack2(__builtin_amdgcn_fmed3f(s01[0], 0.f, hi), __builtin_amdgcn_fmed3f(s01[1], 0.f, hi));
+          const uint32_t w23 = pack2(__builtin_amdgcn_fmed3f(s23[0], 0.f, hi), __builtin_amdgcn_fmed3f(s23[1], 0.f, hi));
+          const uint32_t h01 = sp_max3_u16x2(w01, sp_dpp_shr1(w01), sp_dpp_shl1(w01));
+          const uint32_t h23 = sp_max3_u16x2(w23, sp_dpp_shr1(w23), sp_dpp_shl1(w23));
+          if (store_lane)
+            *reinterpret_cast<uint2*>(hp + row * kSpHpRowB + hp_lane + mb * 32) = make_uint2(h01, h23);
+        }
+      }
+    }
+    if (more) store_patch(patch0 + ((t + 1) & 1) * kSpPatchB, py0 + 8);
+    __syncthreads();
+
+    // ---- vertical 3 / stride-2 max: pooled row i = stem rows 2i - 1 (previous tile's 15 for
+    // i = 0, zeros above the image), 2i, 2i + 1; packed u16 max of the bf16 bit patterns ----
+    for (int it = tid; it < 8 * 7 * 8; it += 256) {
+      const int pp = it >> 3, g = it & 7;
+      const int i = pp / 7, jx = pp - i * 7;
+      const int gy = py0 + i, gx = px0 + jx;
+      if (gy >= p.Hm || gx >= p.Wm) continue;
+      const int off = jx * kSpHpPitch + g * 16;
+      const u32x4 a = *reinterpret_cast<const u32x4*>(hp + (2 * i) * kSpHpRowB + off);
+      const u32x4 b = *reinterpret_cast<const u32x4*>(hp + (2 * i + 1) * kSpHpRowB + off);
+      u32x4 c = u32x4{0u, 0u, 0u, 0u};
+      if (i > 0)
+        c = *reinterpret_cast<const u32x4*>(hp + (2 * i - 1) * kSpHpRowB + off);
+      else if (t > 0)
+        c = *reinterpret_cast<const u32x4*>(hprev + 15 * kSpHpRowB + off);
+      const u32x4 o = u32x4{sp_max3_u16x2(a.x, b.x, c.x), sp_max3_u16x2(a.y, b.y, c.y),
+                            sp_max3_u16x2(a.z, b.z, c.z), sp_max3_u16x2(a.w, b.w, c.w)};
+      *reinterpret_cast<u32x4*>(p.y + ((size_t)(img * p.Hm + gy) * p.Wm + gx) * p.ldy + g * 8) = o;
+    }
+  }
+}
+
 }  // namespace
 
 }  // namespace aiko
@@ -316,6 +528,16 @@ extern "C" int aiko_stem_pool_u8(const void* frames, const void* w, const float*
   p.bias = bias;
   p.y = static_cast<bf16_t*>(y);
   p.B = B; p.Hp = Hi + 6; p.Wp = Wi + 6; p.Ho = Ho; p.Wo = Wo; p.Hm = Hm; p.Wm = Wm; p.ldy = ldy;
+  if (variant == 2) {
+    // strip kernel: stem rows 2 py0 .. 2 py0 + 15 of every pooled tile must exist in the stem
+    // geometry the pool expects (Ho = 2 Hm or 2 Hm - 1; stem rows past Ho read as zeros)
+    p.tiles_h = (Hm + 7) / 8;
+    p.tiles_w = (Wm + 6) / 7;
+    const long grid = (long)B * p.tiles_w;
+    if (grid <= 0 || grid > 0x7fffffffL) return -1;
+    stem_pool_strip_kernel<<<dim3((unsigned)grid), dim3(256), 0, stream>>>(p);
+    return (int)hipGetLastError();
+  }
   const int tpw = variant == 1 ? 14 : 7;
   p.tiles_h = (Hm + kTPH - 1) / kTPH;
   p.tiles_w = (Wm + tpw - 1) / tpw;

@@ -126,26 +126,22 @@ class ResNet50(WeightsMixin):
     def _stem_u8_ok(self, frames: torch.Tensor) -> bool:
         S = self.image_size
         return (self.stem_u8 and self.fuse_stem_pool and frames.dtype == torch.uint8 and frames.dim() == 4
-                and frames.shape[1] == S and frames.shape[2] == S and S % 4 == 0 and frames.is_contiguous()
-                and not (0 < self.mall_chunk < frames.shape[0]))
+                and frames.shape[1] == S and frames.shape[2] == S and S % 4 == 0 and frames.is_contiguous())
 
     def features_from_frames(self, frames: torch.Tensor, tag: str = "", after_block=None) -> torch.Tensor:
         """uint8 frames -> pooled features: through the uint8 fused stem when the frames have
         the model's size, else pre-processing + :meth:`features_from_stem`."""
         if not self._stem_u8_ok(frames):
             return self.features_from_stem(self.preprocess(frames, tag), tag, after_block=after_block)
-        B = frames.shape[0]
-        Ho, Wo = C.stem_out_hw(self.image_size, self.image_size)
-        Hm, Wm = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
-        pool = C.stem_pool_u8(frames, self.stem, V.IMAGENET_MEAN, V.IMAGENET_STD,
-                              out=self._buf(tag + "pool", (B, Hm, Wm, 64)))
-        return self.features_from_stem(None, tag, after_block=after_block, pooled=pool)
+        return self.features_from_stem(None, tag, after_block=after_block, frames=frames)
 
     def features_from_stem(self, x: torch.Tensor | None, tag: str = "", after_block=None,
-                           pooled: torch.Tensor | None = None) -> torch.Tensor:
+                           pooled: torch.Tensor | None = None,
+                           frames: torch.Tensor | None = None) -> torch.Tensor:
         """Stem buffer -> pooled features bf16 [B, 2048].  ``after_block`` = (index, fn): call
         ``fn()`` once bottleneck ``index`` is enqueued (-1: after the max-pool).  ``pooled``: the
-        stem + max-pool output already computed (``x`` unused)."""
+        stem + max-pool output already computed (``x`` unused); ``frames``: uint8 frames of the
+        model's size for the uint8 fused stem (``x`` unused)."""
         if pooled is not None:
             B = pooled.shape[0]
             if after_block is not None and after_block[0] < 0:
@@ -156,7 +152,7 @@ class ResNet50(WeightsMixin):
                 if after_block is not None and after_block[0] == bi:
                     after_block[1]()
             return V.avgpool(x, out=self._buf(tag + "gap", (B, x.shape[3])))
-        B = x.shape[0]
+        B = (frames if frames is not None else x).shape[0]
         S = self.image_size
         Ho, Wo = C.stem_out_hw(S, S)
         Hm, Wm = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
@@ -170,10 +166,13 @@ class ResNet50(WeightsMixin):
         pool = self._buf(tag + "pool", (B, Hm, Wm, 64))
         xs = []
         for c0 in range(0, B, ch):
-            xc = x[c0:c0 + ch]
-            if self.fuse_stem_pool:
-                xc = C.stem_pool(xc, self.stem, (S, S), out=pool[c0:c0 + ch])
+            if frames is not None:
+                xc = C.stem_pool_u8(frames[c0:c0 + ch], self.stem, V.IMAGENET_MEAN, V.IMAGENET_STD,
+                                    out=pool[c0:c0 + ch])
+            elif self.fuse_stem_pool:
+                xc = C.stem_pool(x[c0:c0 + ch], self.stem, (S, S), out=pool[c0:c0 + ch])
             else:
+                xc = x[c0:c0 + ch]
                 st = self._buf(tag + "stem", (B, Ho, Wo, 64))[c0:c0 + ch]
                 xc = V.maxpool2d(C.conv2d(xc, self.stem, out=st, image_hw=(S, S)), 3, 2, 1, out=pool[c0:c0 + ch])
             t1 = None

@@ -176,6 +176,7 @@ class WhisperEncoder(WeightsMixin):
         s8 = self._buf("s8", (M,), torch.float32)
         qkv = self._buf("qkv", (M, 3 * d))
         att = self._buf("att", (M, d), zero=True)
+        aws = self._buf("attn_ws", (TR.ATTN_WORKSPACE_BYTES // 4,), torch.float32, zero=True)
         # fc1 -> fc2 hand-off in MX-fp8: the fc1 epilogue applies GELU and writes e4m3 + E8M0
         # block scales, fc2 feeds those scales straight to the scaled MFMA (no bf16 round trip,
         # no separate row-quantisation pass)
@@ -186,7 +187,7 @@ class WhisperEncoder(WeightsMixin):
         for blk in self.blocks:
             TR.rownorm(x, *blk.ln1, q=q8, qs=s8)
             TR.linear_fp8(q8, s8, blk.qkv, out=qkv)
-            TR.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], att, B, H, T, Tp, (d // H) ** -0.5)
+            TR.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], att, B, H, T, Tp, (d // H) ** -0.5, work=aws)
             TR.rownorm(att, q=q8, qs=s8)
             TR.linear_fp8(q8, s8, blk.out, out=x, residual=x)
             TR.rownorm(x, *blk.ln2, q=q8, qs=s8)

@@ -435,6 +435,9 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None
 
 
 STEM_POOL_VARIANT = 0     # 0: 8x7 pooled tiles (4 workgroups/CU); 1: 8x14 (2 workgroups/CU)
+# uint8 stem: 2 = the strip kernel (weights in registers for a 7-column strip of pooled tiles,
+# horizontal max in DPP lanes): 126.6 us vs 136.1 us for the tile kernel at B=256 on MI355X
+STEM_POOL_U8_VARIANT = int(__import__("os").environ.get("AIKO_STEM_U8_VARIANT", "2"))
 
 
 def stem_pool_weight(spec: ConvSpec) -> torch.Tensor:
@@ -515,7 +518,7 @@ def stem_pool_u8(frames: torch.Tensor, spec: ConvSpec, mean, std, out: torch.Ten
         out = torch.empty(B, Hm, Wm, 64, dtype=torch.bfloat16, device=frames.device)
     torch.ops.aiko.stem_pool_u8_out(frames, stem_pool_u8_weight(spec, std), spec.bias, out,
                                     [255.0 * float(m) for m in mean],
-                                    STEM_POOL_VARIANT if variant is None else variant)
+                                    STEM_POOL_U8_VARIANT if variant is None else variant)
     return out
 
 

@@ -197,8 +197,20 @@ def rownorm(x: torch.Tensor, gamma=None, beta=None, eps: float = 1e-5, out: torc
     return out, q, qs
 
 
-def attention(q, k, v, out, batch: int, heads: int, T: int, Tpad: int, scale: float):
+ATTN_WORKSPACE_BYTES = 40 << 20     # split-KV tail partials: <= 8 x 64 pieces x 256 rows x 66 fp32
+
+
+def attention_workspace(device) -> torch.Tensor:
+    """Zero-initialised scratch for :func:`attention`'s split-KV tail (fp32 partial outputs and
+    per-item arrival counters, which the kernel re-arms): one per concurrently running stream."""
+    return torch.zeros(ATTN_WORKSPACE_BYTES // 4, dtype=torch.float32, device=device)
+
+
+def attention(q, k, v, out, batch: int, heads: int, T: int, Tpad: int, scale: float,
+              work: torch.Tensor | None = None):
     """Non-causal multi-head attention (head dim 64) over sequences of ``T`` tokens stored
-    every ``Tpad`` rows; q/k/v may be column slices of one fused QKV buffer."""
-    torch.ops.aiko.attn_fwd_out(q, k, v, out, batch, heads, T, Tpad, float(scale))
+    every ``Tpad`` rows; q/k/v may be column slices of one fused QKV buffer.  ``work``
+    (:func:`attention_workspace`, private to the calling stream) lets the kernel cut the items
+    of a partial last round into key ranges merged in-kernel."""
+    torch.ops.aiko.attn_fwd_out(q, k, v, out, batch, heads, T, Tpad, float(scale), work)
     return out

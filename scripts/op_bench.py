@@ -17,6 +17,7 @@ def main():
     ap.add_argument("op")
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--tile", default=None)
     a = ap.parse_args()
     from aiko_services_amd.ops import require_native
@@ -36,7 +37,8 @@ def main():
     elif a.op == "attn":
         qkv = (torch.randn(M, 3 * d, device=dev) * 1.5).to(torch.bfloat16)
         out = torch.empty(M, d, dtype=torch.bfloat16, device=dev)
-        fn = lambda: TR.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], out, B, H, T, Tp, 0.125)  # noqa: E731
+        ws = TR.attention_workspace(dev) if os.environ.get("AIKO_ATTN_WS", "1") != "0" else None
+        fn = lambda: TR.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], out, B, H, T, Tp, 0.125, work=ws)  # noqa: E731
         flops = 4 * B * H * T * T * 64
     else:
         K, N = {"gemm_qkv": (d, 3 * d), "gemm_fc1": (d, 4 * d), "gemm_fc2": (4 * d, d), "gemm_out": (d, d),
@@ -59,12 +61,15 @@ def main():
     for _ in range(3):
         fn()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(a.iters):
-        fn()
-    e1.record()
-    e1.synchronize()
-    us = e0.elapsed_time(e1) / a.iters * 1e3
+    runs = []
+    for _ in range(a.reps):                     # median of `reps` back-to-back runs of `iters`
+        e0.record()
+        for _ in range(a.iters):
+            fn()
+        e1.record()
+        e1.synchronize()
+        runs.append(e0.elapsed_time(e1) / a.iters * 1e3)
+    us = sorted(runs)[len(runs) // 2]
     if flops:
         print(f"{a.op}: {us:.1f} us  {flops / us / 1e6:.1f} TFLOP/s", flush=True)
     else:

@@ -26,10 +26,17 @@ def main():
     from aiko_services_amd.ops import vision as V
     require_native()
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+    only = sys.argv[2] if len(sys.argv) > 2 else ""      # e.g. "u8v2": time just that variant
     spec = C.make_stem_spec(torch.randn(64, 3, 7, 7) / 12, torch.randn(64) * 0.1, act="relu", device="cuda")
     frames = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, device="cuda")
-    pre = V.preprocess_frames(frames)
     out = torch.empty(B, 56, 56, 64, dtype=torch.bfloat16, device="cuda")
+    if only.startswith("u8v"):
+        from aiko_services_amd.ops.vision import IMAGENET_MEAN, IMAGENET_STD
+        v = int(only[3:])
+        t = timed(lambda: C.stem_pool_u8(frames, spec, IMAGENET_MEAN, IMAGENET_STD, out=out, variant=v), iters=20)
+        print(f"stem_pool_u8 variant {v} {t:8.1f} us")
+        return
+    pre = V.preprocess_frames(frames)
     stem = torch.empty(B, 112, 112, 64, dtype=torch.bfloat16, device="cuda")
     ref = V.maxpool2d(C.conv2d(pre, spec, image_hw=(224, 224), out=stem), 3, 2, 1)
     with C.autotune():
@@ -42,6 +49,12 @@ def main():
         ok = torch.equal(out, ref)
         t = timed(lambda: C.stem_pool(pre, spec, (224, 224), out=out, variant=v))
         print(f"stem_pool variant {v} {t:8.1f} us  exact={ok}")
+    from aiko_services_amd.ops.vision import IMAGENET_MEAN, IMAGENET_STD
+    outs = {}
+    for v in (0, 1, 2):
+        outs[v] = C.stem_pool_u8(frames, spec, IMAGENET_MEAN, IMAGENET_STD, variant=v).clone()
+        t = timed(lambda: C.stem_pool_u8(frames, spec, IMAGENET_MEAN, IMAGENET_STD, out=out, variant=v))
+        print(f"stem_pool_u8 variant {v} {t:8.1f} us  same_as_v0={torch.equal(outs[v], outs[0])}")
 
 
 
@@ -62,7 +75,7 @@ def debug_phases():
 
 
 if __name__ == "__main__":
-    if len(sys.argv) > 2 and sys.argv[2] == "phases":
+    if len(sys.argv) > 2 and sys.argv[2] == "phases":  # noqa: SIM114
         debug_phases()
     else:
         main()

@@ -111,6 +111,42 @@ def test_flash_attention_rescale_paths(native, case):
     assert _rel(got, ref) < 2e-2, _rel(got, ref)
 
 
+@pytest.mark.parametrize("B,H,T,Tpad,scale_k", [(1, 8, 256, 256, 1.0), (16, 12, 1500, 1504, 1.0), (2, 4, 1000, 1024, 6.0)])
+@pytest.mark.parametrize("pieces", [2, 4])
+def test_flash_attention_split_tail(native, B, H, T, Tpad, scale_k, pieces, monkeypatch):
+    """Split-KV tail (``work`` given): the items of a partial last round per XCD run as key-range
+    pieces merged in-kernel by the last arriver.  Same result as the unsplit grid (within bf16
+    rounding of the merge order) and the fp32 reference; the arrival counters re-arm, so
+    repeated launches agree; keys scaled up (scale_k) so pieces see very different maxima."""
+    from aiko_services_amd.ops import transformer as TR
+    monkeypatch.setenv("AIKO_ATTN_SPLIT_S", str(pieces))       # opt-in (attention.hip)
+    g = torch.Generator().manual_seed(T + B)
+    d = H * 64
+    qkv = torch.randn(B * Tpad, 3 * d, generator=g) * 1.5
+    qkv.view(B, Tpad, 3, H, 64)[:, :, 1] *= torch.linspace(0.3, scale_k, Tpad).view(1, Tpad, 1, 1)
+    qkv = qkv.to(DEV, torch.bfloat16)
+    plain = torch.zeros(B * Tpad, d, dtype=torch.bfloat16, device=DEV)
+    TR.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], plain, B, H, T, Tpad, 0.125)   # no workspace
+    ws = TR.attention_workspace(DEV)
+    outs = []
+    for _ in range(3):
+        o = torch.zeros(B * Tpad, d, dtype=torch.bfloat16, device=DEV)
+        TR.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, B, H, T, Tpad, 0.125, work=ws)
+        outs.append(o)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    cnt = ws[:8].view(torch.int32)                          # the first 8 x r counters (r >= 1)
+    assert cnt.abs().max().item() == 0                       # counters re-armed
+    x = qkv.float().view(B, Tpad, 3, H, 64)[:, :T]
+    q, k, v = (x[:, :, i].transpose(1, 2) for i in range(3))
+    ref = F.scaled_dot_product_attention(q, k, v, scale=0.125).transpose(1, 2).reshape(B, T, d)
+    got = outs[0].view(B, Tpad, d)[:, :T]
+    assert _rel(got, ref) < 1e-2
+    assert _rel(got, plain.view(B, Tpad, d)[:, :T].float()) < 1e-2
+    if Tpad > T:
+        assert outs[0].view(B, Tpad, d)[:, T:].abs().max().item() == 0
+
+
 def test_log_mel(native):
     from aiko_services_amd.ops import audio as AU
     g = torch.Generator().manual_seed(3)
