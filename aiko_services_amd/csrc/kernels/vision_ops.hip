@@ -244,7 +244,7 @@ constexpr int kSfTH = 8, kSfTW = 32;
 constexpr int kSfIH = 2 * kSfTH + 1;            // 17 input rows
 constexpr int kSfG = kSfTW / 2 + 1;             // 17 groups of 4 pixels per input row
 constexpr int kSfIW = 4 * kSfG;                 // 68 tile columns (tile col = input x - (2 ox0 - 1) + 3)
-template <int ACT, bool BGR>
+template <int ACT, bool BGR, bool WIDE>
 __global__ __launch_bounds__(256) void stem_fast_kernel(
     const uint8_t* __restrict__ in, bf16_t* __restrict__ out, const bf16_t* __restrict__ w,
     const float* __restrict__ bias, int Hin, int Win, int Hc, int Wc, int off_t, int off_l, float fill_raw,
@@ -308,20 +308,56 @@ __global__ __launch_bounds__(256) void stem_fast_kernel(
   const int orow = oy0 + 2 * wave, ocol = ox0 + fr;
   const uint32_t o0 = (uint32_t)((orow * W1 + ocol) * ldo + 4 * fq);
   const int lbase = 4 * wave * kSfIW + 2 * fr;              // tile pixel of output (2 wave, fr)
+  if constexpr (!WIDE) {
 #pragma unroll
-  for (int pt = 0; pt < 4; ++pt) {
-    const int dy = pt >> 1, dx = 16 * (pt & 1);
-    const int base = lbase + 2 * dy * kSfIW + 2 * dx;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int pt = 0; pt < 4; ++pt) {
+      const int dy = pt >> 1, dx = 16 * (pt & 1);
+      const int base = lbase + 2 * dy * kSfIW + 2 * dx;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      uint2 p0 = {0u, 0u}, p1 = {0u, 0u};
-      if (toff[kk][0] >= 0) p0 = *reinterpret_cast<const uint2*>(stile + 2 * (base + toff[kk][0]));
-      if (toff[kk][1] >= 0) p1 = *reinterpret_cast<const uint2*>(stile + 2 * (base + toff[kk][1]));
-      const u32x4 pv = {p0.x, p0.y, p1.x, p1.y};
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[kk], __builtin_bit_cast(bf16x8, pv), acc, 0, 0, 0);
+      for (int kk = 0; kk < 2; ++kk) {
+        uint2 p0 = {0u, 0u}, p1 = {0u, 0u};
+        if (toff[kk][0] >= 0) p0 = *reinterpret_cast<const uint2*>(stile + 2 * (base + toff[kk][0]));
+        if (toff[kk][1] >= 0) p1 = *reinterpret_cast<const uint2*>(stile + 2 * (base + toff[kk][1]));
+        const u32x4 pv = {p0.x, p0.y, p1.x, p1.y};
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[kk], __builtin_bit_cast(bf16x8, pv), acc, 0, 0, 0);
+      }
+      if (orow + dy < H1 && ocol + dx < W1) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float a = fmaf(acc[e], inv_std, cb[e]);
+          if constexpr (ACT == 1) a = fmaxf(a, 0.f);
+          else if constexpr (ACT == 2) a = silu(a);
+          v[e] = a;
+        }
+        *reinterpret_cast<uint2*>(const_cast<bf16_t*>(obase) + o0 + (uint32_t)((dy * W1 + dx) * ldo)) =
+            make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      }
     }
-    if (orow + dy < H1 && ocol + dx < W1) {
+    return;
+  }
+  // the two 16-pixel halves (dx = 0, 16) of one output row form a pair: after the epilogue a
+  // v_permlane16_swap per packed dword gives 16-lane row 0 channels 0-7 of the left half, row 1
+  // channels 0-7 of the right half, rows 2 / 3 channels 8-15 of each — one 16-B store per lane
+  // per pair instead of two 8-B stores (the kernel's tail is store-issue bound)
+  const int half = fq & 1;                                   // 0: left half, 1: right half
+  const uint32_t o_sw = (uint32_t)(half * 16 * ldo + 8 * (fq >> 1)) - 4 * fq;   // vs o0's 4 fq
+#pragma unroll
+  for (int dy = 0; dy < 2; ++dy) {
+    uint32_t u[2][2];
+#pragma unroll
+    for (int hx = 0; hx < 2; ++hx) {
+      const int base = lbase + 2 * dy * kSfIW + 2 * (16 * hx);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        uint2 p0 = {0u, 0u}, p1 = {0u, 0u};
+        if (toff[kk][0] >= 0) p0 = *reinterpret_cast<const uint2*>(stile + 2 * (base + toff[kk][0]));
+        if (toff[kk][1] >= 0) p1 = *reinterpret_cast<const uint2*>(stile + 2 * (base + toff[kk][1]));
+        const u32x4 pv = {p0.x, p0.y, p1.x, p1.y};
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[kk], __builtin_bit_cast(bf16x8, pv), acc, 0, 0, 0);
+      }
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -330,9 +366,18 @@ __global__ __launch_bounds__(256) void stem_fast_kernel(
         else if constexpr (ACT == 2) a = silu(a);
         v[e] = a;
       }
-      *reinterpret_cast<uint2*>(const_cast<bf16_t*>(obase) + o0 + (uint32_t)((dy * W1 + dx) * ldo)) =
-          make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      u[hx][0] = pack2(v[0], v[1]);
+      u[hx][1] = pack2(v[2], v[3]);
     }
+    u32x4 o;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const auto sw = __builtin_amdgcn_permlane16_swap(u[0][j], u[1][j], false, false);
+      o[j] = sw[0];
+      o[2 + j] = sw[1];
+    }
+    if (orow + dy < H1 && ocol + 16 * half < W1)
+      *reinterpret_cast<u32x4*>(const_cast<bf16_t*>(obase) + o0 + o_sw + (uint32_t)(dy * W1 * ldo)) = o;
   }
 }
 
@@ -656,13 +701,16 @@ extern "C" int aiko_stem_direct(const void* in, void* out, const void* w, const 
   if (Cout % 16 || ldo % 4 || k < 1 || k > 4 || stride < 1 || B <= 0) return -1;
   static const bool fast_ok = [] { const char* e = getenv("AIKO_STEM_FAST"); return !(e && *e == '0'); }();
   if (fast_ok && k == 3 && stride == 2 && pad == 1 && Cout == 16 && Ho == Hin && Wo == Win && Win % 4 == 0 &&
+      ldo % 8 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
       off_l % 4 == 0 && Wc % 4 == 0 && mean[0] == 0.f && mean[1] == 0.f && mean[2] == 0.f &&
       std[0] == std[1] && std[1] == std[2] && std[0] > 0.f) {
     dim3 grid((W1 + aiko::kSfTW - 1) / aiko::kSfTW, (H1 + aiko::kSfTH - 1) / aiko::kSfTH, B);
+    static const bool wide = [] { const char* e = getenv("AIKO_STEM_FAST_WIDE"); return !(e && *e == '0'); }();
     auto go = [&](auto act_tag, auto bgr_tag) {
       constexpr int A = decltype(act_tag)::value;
       constexpr bool G = decltype(bgr_tag)::value;
-      aiko::stem_fast_kernel<A, G><<<grid, 256, 0, stream>>>(
+      auto kern = wide ? aiko::stem_fast_kernel<A, G, true> : aiko::stem_fast_kernel<A, G, false>;
+      kern<<<grid, 256, 0, stream>>>(
           static_cast<const uint8_t*>(in), static_cast<aiko::bf16_t*>(out), static_cast<const aiko::bf16_t*>(w),
           bias, Hin, Win, Hc, Wc, off_t, off_l, fill, 1.f / (255.f * std[0]), H1, W1, ldo);
     };
