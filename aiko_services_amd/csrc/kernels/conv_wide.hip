@@ -51,16 +51,22 @@ __device__ __forceinline__ void wide_vm_barrier() {
 // before the K loop.  The 4-wave / multi-workgroup shapes are for the short-K, bandwidth-bound
 // layers: there a second resident workgroup's loads and stores cover one tile's prologue and
 // epilogue, which a lone 8-wave workgroup leaves exposed.
-template <int BM, int BN, int WGM, int WGN, int NS, bool RES_PF, int OCC>
+// BK = 32 (tuner variant 11): half-depth K blocks in a 4-slot ring, so a 256 x 256 tile keeps
+// three blocks in flight across every barrier (the 64-deep ring fits only two slots there and
+// retires each block with one block of MFMA work to cover its DMA); 64-B rows swizzled by
+// (row >> 1) & 3.
+template <int BM, int BN, int WGM, int WGN, int NS, bool RES_PF, int OCC, int BK = 64>
 __global__ __launch_bounds__(64 * WGM * WGN, OCC) void conv_wide_kernel(ConvParams p) {
   constexpr int NW = WGM * WGN;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
-  constexpr int BK = 64;
+  static_assert(BK == 64 || BK == 32, "64- or 32-deep K blocks");
+  constexpr int PPR = BK / 8;                    // 16-B pieces per tile row
   constexpr int D = NS - 1;                      // K blocks in flight ahead of the one computed
   constexpr int WM = BM / WGM, WN = BN / WGN;    // pixels / channels per wave
   constexpr int MI = WM / 16, NI = WN / 16;
   static_assert(NI % 2 == 0 && MI >= 1, "wave tile: whole 16-pixel blocks, channel blocks in pairs");
-  constexpr int RPI = 8 * NW;                    // tile rows filled per DMA instruction
+  constexpr int RPW = 64 / PPR;                  // tile rows per wave DMA instruction
+  constexpr int RPI = RPW * NW;                  // tile rows filled per DMA instruction
   static_assert(BM % RPI == 0 && BN % RPI == 0, "tile rows in whole DMA pieces");
   constexpr int APT = BM / RPI, BPT = BN / RPI;
   constexpr int PER = APT + BPT;                 // DMA instructions per K block per thread
@@ -77,8 +83,9 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCC) void conv_wide_kernel(ConvPara
   const int tile_n = bid % ntn, tile_m = bid / ntn;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
 
-  const int lrow = wave * 8 + (lane >> 3);
-  const int lp = (lane & 7) ^ (lane >> 3);
+  const int lrow = wave * RPW + lane / PPR;
+  // source-side swizzle: physical piece (lane % PPR) of the row holds logical piece lp
+  const int lp = BK == 64 ? ((lane & 7) ^ (lane >> 3)) : ((lane & 3) ^ ((lrow >> 1) & 3));
   const int HoWo = p.Ho * p.Wo;
   const __amdgpu_buffer_rsrc_t rx = wide_rsrc(p.x);
   const __amdgpu_buffer_rsrc_t rw = wide_rsrc(p.w);
@@ -166,11 +173,11 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCC) void conv_wide_kernel(ConvPara
     const int k0 = kb * BK;
     const uint32_t sb = (uint32_t)(k0 * 2);
 #pragma unroll
-    for (int i = 0; i < BPT; ++i) wide_dma16(rw, b_off[i], sb, Ws + (i * RPI + wave * 8) * BK);
+    for (int i = 0; i < BPT; ++i) wide_dma16(rw, b_off[i], sb, Ws + (i * RPI + wave * RPW) * BK);
     if (k0 >= K1) {
       const uint32_t soff = (uint32_t)((k0 - K1) * 2);
 #pragma unroll
-      for (int i = 0; i < APT; ++i) wide_dma16(rx2, a2_off[i], soff, Xs + (i * RPI + wave * 8) * BK);
+      for (int i = 0; i < APT; ++i) wide_dma16(rx2, a2_off[i], soff, Xs + (i * RPI + wave * RPW) * BK);
     } else {
       if (iss_tap != cur_tap) {
         cur_tap = iss_tap;
@@ -182,7 +189,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCC) void conv_wide_kernel(ConvPara
       }
       const uint32_t soff = (uint32_t)(iss_c * 2);
 #pragma unroll
-      for (int i = 0; i < APT; ++i) wide_dma16(rx, a_off[i], soff, Xs + (i * RPI + wave * 8) * BK);
+      for (int i = 0; i < APT; ++i) wide_dma16(rx, a_off[i], soff, Xs + (i * RPI + wave * RPW) * BK);
       iss_c += BK;
       if (iss_c >= p.Cc) {
         iss_c = 0;
@@ -202,7 +209,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCC) void conv_wide_kernel(ConvPara
     for (int i = 0; i < MI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // fragment row offsets (elements): weight rows (A operand) and pixel rows (B operand)
-  const int sw = fr & 7;
+  const int sw = BK == 64 ? (fr & 7) : ((fr >> 1) & 3);
   int w_rd[NI], x_rd[MI];
 #pragma unroll
   for (int j = 0; j < NI; ++j) w_rd[j] = BM * BK + (wc * WN + j * 16 + fr) * BK;
@@ -213,7 +220,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCC) void conv_wide_kernel(ConvPara
     constexpr int SLOT = decltype(slot_tag)::value;
     const bf16_t* St = ring + SLOT * STAGE_ELEMS;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < BK / 32; ++kk) {
       const int pc = ((fq + 4 * kk) ^ sw) << 3;
       bf16x8 wf[NI], xf[MI];
 #pragma unroll
@@ -233,8 +240,12 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCC) void conv_wide_kernel(ConvPara
     constexpr int SLOT = decltype(slot_tag)::value;
     constexpr int PREV = SLOT == 0 ? NS - 1 : SLOT - 1;
     // block kb must have landed; D - 1 younger blocks may stay in flight
-    if constexpr (D >= 2) {
-      if (kb + 1 < nkb) wide_vm_barrier<PER * (D - 1)>();
+    if constexpr (D >= 3) {
+      if (kb + 2 < nkb) wide_vm_barrier<PER * 2>();
+      else if (kb + 1 < nkb) wide_vm_barrier<PER>();
+      else wide_vm_barrier<0>();
+    } else if constexpr (D == 2) {
+      if (kb + 1 < nkb) wide_vm_barrier<PER>();
       else wide_vm_barrier<0>();
     } else {
       wide_vm_barrier<0>();
@@ -246,8 +257,22 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCC) void conv_wide_kernel(ConvPara
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1>;
   using S2 = std::integral_constant<int, 2>;
+  using S3 = std::integral_constant<int, 3>;
   issue(0, S0{});
-  if constexpr (NS == 3) {
+  if constexpr (NS == 4) {
+    if (1 < nkb) issue(1, S1{});
+    if (2 < nkb) issue(2, S2{});
+    int kb = 0;
+    for (; kb + 4 <= nkb; kb += 4) {
+      step(kb, S0{});
+      step(kb + 1, S1{});
+      step(kb + 2, S2{});
+      step(kb + 3, S3{});
+    }
+    if (kb < nkb) step(kb, S0{});
+    if (kb + 1 < nkb) step(kb + 1, S1{});
+    if (kb + 2 < nkb) step(kb + 2, S2{});
+  } else if constexpr (NS == 3) {
     if (1 < nkb) issue(1, S1{});
     int kb = 0;
     for (; kb + 3 <= nkb; kb += 3) {
@@ -359,6 +384,15 @@ extern "C" int aiko_conv_wide(const void* x, const void* w, const float* bias, c
       conv_wide_kernel<256, 64, 4, 2, 3, true, 1><<<grid, 512, 0, stream>>>(p);
     else if (bm == 128 && bn == 128)
       conv_wide_kernel<128, 128, 2, 4, 3, true, 1><<<grid, 512, 0, stream>>>(p);
+    else
+      return -1;
+  } else if (occ == 11) {             // 8 waves, 32-deep K blocks in a 4-slot ring
+    if (bm == 256 && bn == 256)
+      conv_wide_kernel<256, 256, 2, 4, 4, false, 1, 32><<<grid, 512, 0, stream>>>(p);
+    else if (bm == 256 && bn == 128)
+      conv_wide_kernel<256, 128, 4, 2, 4, true, 1, 32><<<grid, 512, 0, stream>>>(p);
+    else if (bm == 128 && bn == 256)
+      conv_wide_kernel<128, 256, 2, 4, 4, true, 1, 32><<<grid, 512, 0, stream>>>(p);
     else
       return -1;
   } else {                            // several workgroups per CU

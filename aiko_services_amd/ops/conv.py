@@ -263,6 +263,11 @@ WIDE4_TILES = ((256, 128), (128, 256))
 WIDE8_TILES = ((256, 256), (256, 128), (128, 256), (256, 64), (128, 128))
 # variant 9: the same kernel at 2-3 workgroups per CU (short-K, bandwidth-bound layers)
 WIDE_OCC_TILES = ((128, 128), (256, 64), (128, 64), (64, 128), (64, 64))
+# variant 11: the same kernel with 32-deep K blocks in a 4-slot ring (three blocks in flight
+# across each barrier instead of one for the 256-wide tiles) — the long-K compute-bound layers.
+# Measured on the ResNet-50 layers (MI355X, round 3): never the tuner's pick against variant 8,
+# i.e. the 2-slot 64-deep ring is not what limits those tiles; kept as a candidate
+WIDE_DEEP_TILES = ((256, 256), (256, 128), (128, 256))
 
 
 def buf_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = None) -> bool:
@@ -328,6 +333,7 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False):
             cands += [t + (5,) for t in MF32_TILES]
             cands += [t + (6,) for t in WIDE4_TILES]
             cands += [t + (8,) for t in WIDE8_TILES] + [t + (9,) for t in WIDE_OCC_TILES]
+            cands += [t + (11,) for t in WIDE_DEEP_TILES]
         if patch_ok:
             cands.append((8, 64, 10))        # variant 10: tile fixed by the kernel (8 rows x W)
     skip = {int(v) for v in __import__("os").environ.get("AIKO_CONV_SKIP", "").split(",") if v.strip()}

@@ -100,6 +100,14 @@ def _nhwc(x_nchw):
     (3, 14, 14, 256, 1024, 1, 1, 0, None, True, (128, 64, 9)),
     (1, 13, 9, 192, 72, 3, 2, 1, "gelu", True, (64, 128, 9)),
     (2, 30, 30, 64, 64, 3, 1, 1, "relu", True, (64, 64, 9)),
+    # variant 11: 32-deep K blocks in a 4-slot ring — ring tails (K/32 = 2, 4, 54, 144 blocks),
+    # 3x3 / strided / 1x1, M and N tails, residual prefetched or not
+    (2, 28, 28, 128, 256, 3, 1, 1, "relu", True, (256, 256, 11)),
+    (3, 14, 14, 64, 1024, 1, 1, 0, None, True, (256, 256, 11)),
+    (1, 13, 9, 192, 72, 3, 2, 1, "gelu", True, (256, 128, 11)),
+    (2, 7, 7, 512, 512, 3, 1, 1, "relu", False, (128, 256, 11)),
+    (1, 9, 11, 128, 200, 3, 1, 1, "silu", True, (256, 128, 11)),
+    (2, 30, 30, 64, 64, 3, 1, 1, "relu", True, (128, 256, 11)),
 ])
 def test_conv_igemm_matches_torch(native, B, H, W, cin, cout, k, stride, pad, act, res, tile):
     from aiko_services_amd.ops import conv as C
@@ -317,7 +325,7 @@ def test_resnet50_matches_fp32_reference(native):
     assert (i[:, 0].long() == lg.argmax(1)).all()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 8])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 8, 11])
 @pytest.mark.parametrize("B,H,cin_main,cin_sc,cout,stride", [(2, 28, 64, 64, 256, 1), (2, 28, 128, 256, 512, 2),
                                                               (1, 14, 512, 1024, 2048, 2)])
 def test_fused_projection_shortcut(native, B, H, cin_main, cin_sc, cout, stride, variant):
@@ -334,7 +342,7 @@ def test_fused_projection_shortcut(native, B, H, cin_main, cin_sc, cout, stride,
     fused = C.fuse_shortcut(main, down)
     t = torch.randn(B, Ho, Ho, cin_main, generator=g).to(torch.bfloat16).to(DEV)
     x = torch.randn(B, H, H, cin_sc, generator=g).to(torch.bfloat16).to(DEV)
-    y = C.conv2d(t, fused, x2=x, tile=(256, 128, 8) if variant == 8 else (64, 128, variant))
+    y = C.conv2d(t, fused, x2=x, tile=(256, 128, variant) if variant in (8, 11) else (64, 128, variant))
     torch.cuda.synchronize()
     idn = R.conv_ref(x.permute(0, 3, 1, 2).float(), down)
     ref = R.conv_ref(t.permute(0, 3, 1, 2).float(), main, idn)
