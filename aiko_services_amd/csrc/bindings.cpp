@@ -63,6 +63,8 @@ int aiko_gemm_fp8(const void* a, const void* b, const float* sa, const float* sb
                   hipStream_t stream);
 int aiko_rownorm_quant(const void* x, int ldx, const float* gamma, const float* beta, float eps,
                        void* yb, int ldyb, void* q, int ldq, float* qs, int M, int D, hipStream_t stream);
+int aiko_linear_splitk(const void* x, const void* w, const float* bias, float* part, void* y, int M, int N, int K,
+                       int ldx, int ldw, int ldy, int S, hipStream_t stream);
 int aiko_attn_fwd(const void* q, const void* k, const void* v, void* o, int ldq, int ldk, int ldv,
                   int ldo, int B, int H, int T, int Tpad, int dh, float scale, void* work, long work_bytes,
                   hipStream_t stream);
@@ -820,6 +822,36 @@ void rownorm_quant_out(const at::Tensor& x, const c10::optional<at::Tensor>& gam
                "rownorm_quant");
 }
 
+// Split-K linear (linear_splitk.hip): x [M, >= K] bf16, w [N, >= K] bf16 (row pitch w.stride(0)),
+// bias fp32 [N] or None, part fp32 with >= S*M*N elements, y [M, >= N] bf16.
+void linear_splitk_out(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                       at::Tensor& part, at::Tensor& y, int64_t K, int64_t S) {
+  for (const at::Tensor* t : {&x, &w, (const at::Tensor*)&part, (const at::Tensor*)&y}) check_cuda(*t, "x/w/part/y");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16,
+              "aiko.linear_splitk_out: x, w, y must be bf16");
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous(), "aiko.linear_splitk_out: part must be contiguous fp32");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2 && x.stride(1) == 1 && w.stride(1) == 1 && y.stride(1) == 1,
+              "aiko.linear_splitk_out: row-major 2-D operands");
+  const int64_t M = x.size(0), N = w.size(0);
+  TORCH_CHECK(y.size(0) == M && y.size(1) == N && x.size(1) >= K && w.size(1) >= K, "aiko.linear_splitk_out: shapes");
+  TORCH_CHECK(S >= 1 && K % (32 * S) == 0 && N % 4 == 0, "aiko.linear_splitk_out: K % (32 S) == 0 and N % 4 == 0");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && y.stride(0) % 4 == 0 &&
+                  reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(y.data_ptr()) % 8 == 0 && reinterpret_cast<uintptr_t>(part.data_ptr()) % 16 == 0,
+              "aiko.linear_splitk_out: 16-B aligned operand rows");
+  TORCH_CHECK(part.numel() >= S * M * N, "aiko.linear_splitk_out: part too small");
+  const float* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    check_cuda(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == N && bias->is_contiguous(),
+                "aiko.linear_splitk_out: bias must be fp32 [N]");
+    bp = bias->data_ptr<float>();
+  }
+  check_launch(aiko_linear_splitk(x.data_ptr(), w.data_ptr(), bp, part.data_ptr<float>(), y.data_ptr(), (int)M, (int)N,
+                                  (int)K, (int)x.stride(0), (int)w.stride(0), (int)y.stride(0), (int)S, cur_stream()),
+               "linear_splitk");
+}
+
 // q/k/v/o: [B*Tpad, >= H*64] row-major (column slices of a fused QKV buffer allowed)
 void attn_fwd_out(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& o,
                   int64_t B, int64_t H, int64_t T, int64_t Tpad, double scale,
@@ -1039,6 +1071,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("stem_pool_u8_out(Tensor frames, Tensor w, Tensor bias, Tensor(a!) y, float[] mean255, int variant=0) -> ()");
   m.def("gemm_fp8_out(Tensor a, Tensor? sa, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!)? y, int act, int bm, int bn, int variant=0, Tensor? zero=None, Tensor? amx=None, Tensor(b!)? yq=None, Tensor(c!)? ysc=None) -> ()");
   m.def("rownorm_quant_out(Tensor x, Tensor? gamma, Tensor? beta, float eps, Tensor(a!)? yb, Tensor(b!)? q, Tensor(c!)? qs) -> ()");
+  m.def("linear_splitk_out(Tensor x, Tensor w, Tensor? bias, Tensor(a!) part, Tensor(b!) y, int K, int S) -> ()");
   m.def("attn_fwd_out(Tensor q, Tensor k, Tensor v, Tensor(a!) o, int B, int H, int T, int Tpad, float scale, Tensor(b!)? work=None) -> ()");
   m.def("logmel_out(Tensor audio, Tensor mel, Tensor mel_range, int n_fft, int hop, int F, Tensor(a!) work, Tensor(b!) gmax, Tensor(c!) dst, int rows, int pad) -> ()");
   m.def("softmax_topk_out(Tensor logits, Tensor(a!) prob, Tensor(b!) index, int k) -> ()");
@@ -1071,6 +1104,7 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("gemm_fp8_out", &gemm_fp8_out);
   m.impl("rownorm_quant_out", &rownorm_quant_out);
   m.impl("attn_fwd_out", &attn_fwd_out);
+  m.impl("linear_splitk_out", &linear_splitk_out);
   m.impl("logmel_out", &logmel_out);
   m.impl("embed_tokens_out", &embed_tokens_out);
   m.impl("attn_decode_out", &attn_decode_out);

@@ -705,7 +705,10 @@ extern "C" int aiko_stem_direct(const void* in, void* out, const void* w, const 
       off_l % 4 == 0 && Wc % 4 == 0 && mean[0] == 0.f && mean[1] == 0.f && mean[2] == 0.f &&
       std[0] == std[1] && std[1] == std[2] && std[0] > 0.f) {
     dim3 grid((W1 + aiko::kSfTW - 1) / aiko::kSfTW, (H1 + aiko::kSfTH - 1) / aiko::kSfTH, B);
-    static const bool wide = [] { const char* e = getenv("AIKO_STEM_FAST_WIDE"); return !(e && *e == '0'); }();
+    // 16-B stores through v_permlane16_swap pairs: measured no faster on MI355X (69.2-69.8 us
+    // narrow vs 70.4-74.2 us wide at B=64, same box), so opt-in
+    const char* wide_env = getenv("AIKO_STEM_FAST_WIDE");    // read per call (tests flip it)
+    const bool wide = wide_env && *wide_env == '1';
     auto go = [&](auto act_tag, auto bgr_tag) {
       constexpr int A = decltype(act_tag)::value;
       constexpr bool G = decltype(bgr_tag)::value;

@@ -115,6 +115,10 @@ class ResNet50(WeightsMixin):
     def release_workspace(self) -> None:
         self._ws.clear()
 
+    def _fc_work(self, tag: str, B: int) -> torch.Tensor:
+        """fp32 partials of the split-K classifier (ops.conv.linear), one buffer per tag (lane)."""
+        return self._buf(tag + "fc_part", (C.LINEAR_SPLITK * B * self.num_classes,), torch.float32)
+
     # ---- forward ------------------------------------------------------------------------
     def preprocess(self, frames: torch.Tensor, tag: str = "") -> torch.Tensor:
         """uint8 [B, H, W, 3] (any H, W) -> zero-bordered bf16 stem buffer [B, Hp, Wp, 4]."""
@@ -262,7 +266,7 @@ class ResNet50(WeightsMixin):
                     hook = (stagger, lambda ev=gate, st=s: ev.record(st))
                 f = self.features_from_frames(xi, tag, after_block=hook) if frames \
                     else self.features_from_stem(xi, tag, after_block=hook)
-                C.linear(f, self.fc, out=out[i * step:(i + 1) * step])
+                C.linear(f, self.fc, out=out[i * step:(i + 1) * step], work=self._fc_work(tag, f.shape[0]))
         for s in self._lanes(lanes):
             cur.wait_stream(s)
         return out
@@ -299,7 +303,7 @@ class ResNet50(WeightsMixin):
         for bi in range(self.SPLIT_BLOCK + 1, len(self.blocks)):
             x, t1 = self._block(bi, x, tag, B, 0, B, t1)
         f = V.avgpool(x, out=self._buf(tag + "gap", (B, x.shape[3])))
-        return C.linear(f, self.fc, out=self._buf(tag + "logits", (B, self.num_classes)))
+        return C.linear(f, self.fc, out=self._buf(tag + "logits", (B, self.num_classes)), work=self._fc_work(tag, B))
 
     def features(self, frames: torch.Tensor) -> torch.Tensor:
         """uint8 [B, H, W, 3] -> pooled features bf16 [B, 2048]."""
@@ -307,7 +311,8 @@ class ResNet50(WeightsMixin):
 
     def logits_from_stem(self, x: torch.Tensor, tag: str = "") -> torch.Tensor:
         f = self.features_from_stem(x, tag)
-        return C.linear(f, self.fc, out=self._buf(tag + "logits", (f.shape[0], self.num_classes)))
+        return C.linear(f, self.fc, out=self._buf(tag + "logits", (f.shape[0], self.num_classes)),
+                        work=self._fc_work(tag, f.shape[0]))
 
     def topk_from_logits(self, lg: torch.Tensor):
         B = lg.shape[0]
@@ -317,7 +322,8 @@ class ResNet50(WeightsMixin):
 
     def logits(self, frames: torch.Tensor, tag: str = "") -> torch.Tensor:
         f = self.features_from_frames(frames, tag)
-        return C.linear(f, self.fc, out=self._buf(tag + "logits", (f.shape[0], self.num_classes)))
+        return C.linear(f, self.fc, out=self._buf(tag + "logits", (f.shape[0], self.num_classes)),
+                        work=self._fc_work(tag, f.shape[0]))
 
     def forward(self, frames: torch.Tensor):
         lg = self.logits(frames)

@@ -528,12 +528,31 @@ def stem_pool_u8(frames: torch.Tensor, spec: ConvSpec, mean, std, out: torch.Ten
     return out
 
 
+LINEAR_SPLITK = 4     # K slices of the split-K linear (linear_splitk.hip)
+_LINEAR_SPLITK_ON = __import__("os").environ.get("AIKO_FC_SPLITK", "1") != "0"
+
+
+def linear_splitk_ok(x: torch.Tensor, spec: ConvSpec, residual=None) -> bool:
+    """Whether the split-K kernel applies: no activation / residual, K a multiple of 32 S, a
+    short M (the tile grid over M x N alone would not fill the chip) and N % 4 == 0."""
+    return (residual is None and spec.act == ACT_NONE and spec.K % (32 * LINEAR_SPLITK) == 0
+            and spec.cout % 4 == 0 and x.shape[0] <= 2048 and spec.K >= 1024 and x.stride(1) == 1
+            and x.stride(0) % 8 == 0)
+
+
 def linear(x: torch.Tensor, spec: ConvSpec, out: torch.Tensor | None = None,
-           residual: torch.Tensor | None = None) -> torch.Tensor:
-    """``[B, K] @ W^T + b`` on the same kernel (1x1 "image")."""
+           residual: torch.Tensor | None = None, work: torch.Tensor | None = None) -> torch.Tensor:
+    """``[B, K] @ W^T + b`` on the same kernel (1x1 "image").  With ``work`` (fp32, >= S*B*N
+    elements, private to the calling stream) a short-M / long-K layer runs split-K
+    (linear_splitk.hip: S x more workgroups, deterministic two-kernel reduction)."""
     B, K = x.shape
     if out is None:
         out = torch.empty(B, spec.cout, dtype=torch.bfloat16, device=x.device)
+    if (work is not None and _LINEAR_SPLITK_ON and linear_splitk_ok(x, spec, residual)
+            and work.numel() >= LINEAR_SPLITK * B * spec.cout):
+        torch.ops.aiko.linear_splitk_out(x, spec.weight.view(spec.cout, -1), spec.bias, work, out, spec.K,
+                                         LINEAR_SPLITK)
+        return out
     bm, bn = pick_tile(B, spec.cout)
     geom = [1, 1, x.stride(0), spec.Cc, 1, 1, 1, 0, 1, 1, B, spec.act, out.stride(0),
             0 if residual is None else residual.stride(0), bm, bn, spec.K, 1, 1, 8, 1]

@@ -33,6 +33,8 @@ def main():
     print("weight", tuple(spec.weight.shape), "K", spec.K)
     print(f"igemm linear: {timeit(lambda: C.linear(f, spec, out=out)):.1f} us")
     print(f"addmm (hipBLASLt): {timeit(lambda: torch.addmm(bb, f, w.t(), out=out)):.1f} us")
+    work = torch.empty(C.LINEAR_SPLITK * 256 * 1000, device="cuda")
+    print(f"split-K linear (S={C.LINEAR_SPLITK}): {timeit(lambda: C.linear(f, spec, out=out, work=work)):.1f} us")
     ref = f.float() @ w.float().t() + spec.bias
     C.linear(f, spec, out=out)
     e1 = (out.float() - ref).abs().max().item()

@@ -156,6 +156,21 @@ def test_stem_direct_matches_unfused(native, hw):
     assert _rel_err(fused.permute(0, 3, 1, 2), ref) < 1e-2
 
 
+def test_fast_stem_wide_stores_identical(native, monkeypatch):
+    """The fast stem's opt-in 16-B store path (v_permlane16_swap of the two half-row tiles)
+    writes exactly the bytes of the 8-B store path, letterbox bars and ragged edges included."""
+    from aiko_services_amd.models.yolov8 import YOLOv8
+    m = YOLOv8("n", device=DEV)
+    g = torch.Generator().manual_seed(7)
+    frames = torch.randint(0, 256, (2, 480, 640, 3), generator=g, dtype=torch.uint8).to(DEV)
+    monkeypatch.setenv("AIKO_STEM_FAST_WIDE", "0")
+    narrow = m.stem_from_frames(frames).clone()
+    monkeypatch.setenv("AIKO_STEM_FAST_WIDE", "1")
+    wide = m.stem_from_frames(frames).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(wide, narrow)
+
+
 def test_yolov8n_fused_stem_detect_matches(native):
     from aiko_services_amd.models.yolov8 import YOLOv8
     m = YOLOv8("n", device=DEV)

@@ -273,6 +273,29 @@ def test_linear_with_n_tail(native):
         assert _rel_err(y, R.linear_ref(x.float(), spec)) < 1e-2
 
 
+@pytest.mark.parametrize("B,N,K", [(256, 1000, 2048), (37, 1000, 2048), (1, 64, 1024), (300, 520, 4096)])
+def test_linear_splitk(native, B, N, K):
+    """Split-K classifier path (linear_splitk.hip: S K-slices of 32 x 32 one-wave tiles, fp32
+    partials summed in a fixed order + bias): matches the igemm linear and the fp32 reference,
+    M / N tails included, and repeats bit-identically (no atomics)."""
+    from aiko_services_amd.ops import conv as C
+    from aiko_services_amd.ops import reference as R
+    g = torch.Generator().manual_seed(B + N)
+    w = torch.randn(N, K, generator=g) * 0.02
+    b = torch.randn(N, generator=g)
+    spec = C.make_linear_spec(w, b, device=DEV)
+    x = torch.randn(B, K, generator=g).to(torch.bfloat16).to(DEV)
+    assert C.linear_splitk_ok(x, spec)
+    work = torch.full((C.LINEAR_SPLITK * B * N,), float("nan"), device=DEV)
+    y1 = C.linear(x, spec, work=work).clone()
+    y2 = C.linear(x, spec, work=work).clone()
+    base = C.linear(x, spec)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+    assert _rel_err(y1, R.linear_ref(x.float(), spec)) < 1e-2
+    assert _rel_err(y1.float(), base.float()) < 1e-2
+
+
 def test_pools_and_topk(native):
     from aiko_services_amd.ops import vision as V
     g = torch.Generator().manual_seed(11)
