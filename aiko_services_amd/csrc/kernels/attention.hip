@@ -40,6 +40,7 @@ struct AttnParams {
   // split-KV tail (split_s > 0; SM = 1 kernels): 1-D grid, per XCD `split_full` whole items
   // then `split_r` items cut into split_s key ranges; see aiko_attn_fwd
   int nqb, split_s, split_full, split_r, split_fence;
+  int prio;             // 1: waves NW/2 .. NW-1 run at s_setprio 1 (static young-half priority)
   float* part;          // [pieces][QB][64] fp32 partial O, then [pieces][QB] (m, l) pairs
   int* cnt;             // [8 * split_r] arrival counters, zero between launches
 };
@@ -67,6 +68,8 @@ typedef __attribute__((ext_vector_type(4))) short v4i16;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t attn_rsrc(const void* base, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
 }
+
+__device__ __forceinline__ void attn_setprio1() { __builtin_amdgcn_s_setprio(1); }
 
 __device__ __forceinline__ void attn_dma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, void* lds) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -132,6 +135,9 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
     }
   }
   const int qblk = lin % nqb, h = (lin / nqb) % p.H, b = lin / (nqb * p.H);
+  // static priority for the second-dispatched half of the workgroup (MI355X_MICROARCH.md, two
+  // waves per SIMD, item 4): it loses every VALU arbitration by age otherwise
+  if (p.prio && wave >= NW / 2) attn_setprio1();
   const long seq0 = (long)b * p.Tpad;
   const int q0 = qblk * QB + wave * 32;
   const int hc = h * kDH;
@@ -545,6 +551,8 @@ extern "C" int aiko_attn_fwd(const void* q, const void* k, const void* v, void* 
     return v ? atoi(v) : 0;
   }();
   p.split_fence = fence;
+  const char* prio_env = getenv("AIKO_ATTN_PRIO");       // read per call (A/B runs flip it)
+  p.prio = prio_env ? atoi(prio_env) : 0;
   static const int cus = [] {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
