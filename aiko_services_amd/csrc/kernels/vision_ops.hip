@@ -240,18 +240,21 @@ __global__ __launch_bounds__(256) void stem_direct_kernel(
 //     tile whose rows start 3 pixels early, so a group of 4 lands on 2 aligned ds_write_b128 —
 //     no per-pixel index division, bounds test or byte load;
 //   * letterbox bars / conv padding are decided per group (aligned groups never straddle).
-constexpr int kSfTH = 8, kSfTW = 32;
-constexpr int kSfIH = 2 * kSfTH + 1;            // 17 input rows
+constexpr int kSfTH = 8, kSfTW = 32;             // default tile: 8 x 32 outputs (TH template: 8 or 16)
 constexpr int kSfG = kSfTW / 2 + 1;             // 17 groups of 4 pixels per input row
 constexpr int kSfIW = 4 * kSfG;                 // 68 tile columns (tile col = input x - (2 ox0 - 1) + 3)
-template <int ACT, bool BGR, bool WIDE>
+template <int ACT, bool BGR, bool WIDE, int TH = 8>
 __global__ __launch_bounds__(256) void stem_fast_kernel(
     const uint8_t* __restrict__ in, bf16_t* __restrict__ out, const bf16_t* __restrict__ w,
     const float* __restrict__ bias, int Hin, int Win, int Hc, int Wc, int off_t, int off_l, float fill_raw,
     float inv_std, int H1, int W1, int ldo) {
-  __shared__ __attribute__((aligned(16))) uint32_t stile[kSfIH * kSfIW * 2];   // [17][68] x 4 bf16
+  static_assert(TH == 8 || TH == 16, "8 or 16 output rows per tile");
+  static_assert(!WIDE || TH == 8, "the 16-B store path pairs the two half-rows of an 8-row tile");
+  constexpr int kSfIH = 2 * TH + 1;              // input rows (17 / 33)
+  constexpr int RPW = TH / 4;                    // output rows per wave
+  __shared__ __attribute__((aligned(16))) uint32_t stile[kSfIH * kSfIW * 2];   // [kSfIH][68] x 4 bf16
   const int tid = threadIdx.x, b = blockIdx.z, lane = tid & 63, wave = tid >> 6;
-  const int oy0 = blockIdx.y * kSfTH, ox0 = blockIdx.x * kSfTW;
+  const int oy0 = blockIdx.y * TH, ox0 = blockIdx.x * kSfTW;
   const int g0 = (2 * ox0 - 4) >> 2;            // first group: canvas x 2 ox0 - 4 .. 2 ox0 - 1
   const uint8_t* img = in + (long)b * Hin * Win * 3;
   const uint32_t f2 = pack2(fill_raw, fill_raw), fb = f2 & 0xffffu;
@@ -305,12 +308,12 @@ __global__ __launch_bounds__(256) void stem_fast_kernel(
   for (int e = 0; e < 4; ++e) cb[e] = bias ? bias[4 * fq + e] : 0.f;
   // this lane's output pixel (2 wave, fr) of the tile, 32-bit element offsets from the image
   const bf16_t* obase = out + (size_t)b * H1 * W1 * ldo;
-  const int orow = oy0 + 2 * wave, ocol = ox0 + fr;
+  const int orow = oy0 + RPW * wave, ocol = ox0 + fr;
   const uint32_t o0 = (uint32_t)((orow * W1 + ocol) * ldo + 4 * fq);
-  const int lbase = 4 * wave * kSfIW + 2 * fr;              // tile pixel of output (2 wave, fr)
+  const int lbase = 2 * RPW * wave * kSfIW + 2 * fr;        // tile pixel of output (RPW wave, fr)
   if constexpr (!WIDE) {
 #pragma unroll
-    for (int pt = 0; pt < 4; ++pt) {
+    for (int pt = 0; pt < 2 * RPW; ++pt) {
       const int dy = pt >> 1, dx = 16 * (pt & 1);
       const int base = lbase + 2 * dy * kSfIW + 2 * dx;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -704,15 +707,18 @@ extern "C" int aiko_stem_direct(const void* in, void* out, const void* w, const 
       ldo % 8 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
       off_l % 4 == 0 && Wc % 4 == 0 && mean[0] == 0.f && mean[1] == 0.f && mean[2] == 0.f &&
       std[0] == std[1] && std[1] == std[2] && std[0] > 0.f) {
-    dim3 grid((W1 + aiko::kSfTW - 1) / aiko::kSfTW, (H1 + aiko::kSfTH - 1) / aiko::kSfTH, B);
+    const char* th_env = getenv("AIKO_STEM_FAST_TH");         // 8 or 16 output rows per tile
+    const int th = th_env && atoi(th_env) == 16 ? 16 : 8;
     // 16-B stores through v_permlane16_swap pairs: measured no faster on MI355X (69.2-69.8 us
     // narrow vs 70.4-74.2 us wide at B=64, same box), so opt-in
     const char* wide_env = getenv("AIKO_STEM_FAST_WIDE");    // read per call (tests flip it)
     const bool wide = wide_env && *wide_env == '1';
+    dim3 grid((W1 + aiko::kSfTW - 1) / aiko::kSfTW, (H1 + th - 1) / th, B);
     auto go = [&](auto act_tag, auto bgr_tag) {
       constexpr int A = decltype(act_tag)::value;
       constexpr bool G = decltype(bgr_tag)::value;
-      auto kern = wide ? aiko::stem_fast_kernel<A, G, true> : aiko::stem_fast_kernel<A, G, false>;
+      auto kern = th == 16 ? aiko::stem_fast_kernel<A, G, false, 16>
+                           : (wide ? aiko::stem_fast_kernel<A, G, true, 8> : aiko::stem_fast_kernel<A, G, false, 8>);
       kern<<<grid, 256, 0, stream>>>(
           static_cast<const uint8_t*>(in), static_cast<aiko::bf16_t*>(out), static_cast<const aiko::bf16_t*>(w),
           bias, Hin, Win, Hc, Wc, off_t, off_l, fill, 1.f / (255.f * std[0]), H1, W1, ldo);

@@ -167,8 +167,12 @@ def test_fast_stem_wide_stores_identical(native, monkeypatch):
     narrow = m.stem_from_frames(frames).clone()
     monkeypatch.setenv("AIKO_STEM_FAST_WIDE", "1")
     wide = m.stem_from_frames(frames).clone()
+    monkeypatch.setenv("AIKO_STEM_FAST_WIDE", "0")
+    monkeypatch.setenv("AIKO_STEM_FAST_TH", "16")              # 16-row tiles: same values
+    tall = m.stem_from_frames(frames).clone()
     torch.cuda.synchronize()
     assert torch.equal(wide, narrow)
+    assert torch.equal(tall, narrow)
 
 
 def test_yolov8n_fused_stem_detect_matches(native):
