@@ -240,7 +240,10 @@ __global__ __launch_bounds__(256) void stem_direct_kernel(
 //     tile whose rows start 3 pixels early, so a group of 4 lands on 2 aligned ds_write_b128 —
 //     no per-pixel index division, bounds test or byte load;
 //   * letterbox bars / conv padding are decided per group (aligned groups never straddle).
-constexpr int kSfTH = 8, kSfTW = 32;             // default tile: 8 x 32 outputs (TH template: 8 or 16)
+// tile: TH x 32 outputs.  TH = 16 is the default: 65.3-67.5 us against 71.8-72.4 (TH 8) and
+// 68.6-72.1 (TH 32) at B=64 480x640 on MI355X (same box, interleaved) — half the workgroups, half
+// the per-tile weight / bias loads and 3 % input-row halo instead of 6 %
+constexpr int kSfTW = 32;
 constexpr int kSfG = kSfTW / 2 + 1;             // 17 groups of 4 pixels per input row
 constexpr int kSfIW = 4 * kSfG;                 // 68 tile columns (tile col = input x - (2 ox0 - 1) + 3)
 template <int ACT, bool BGR, bool WIDE, int TH = 8>
@@ -248,7 +251,7 @@ __global__ __launch_bounds__(256) void stem_fast_kernel(
     const uint8_t* __restrict__ in, bf16_t* __restrict__ out, const bf16_t* __restrict__ w,
     const float* __restrict__ bias, int Hin, int Win, int Hc, int Wc, int off_t, int off_l, float fill_raw,
     float inv_std, int H1, int W1, int ldo) {
-  static_assert(TH == 8 || TH == 16, "8 or 16 output rows per tile");
+  static_assert(TH == 8 || TH == 16 || TH == 32, "8, 16 or 32 output rows per tile");
   static_assert(!WIDE || TH == 8, "the 16-B store path pairs the two half-rows of an 8-row tile");
   constexpr int kSfIH = 2 * TH + 1;              // input rows (17 / 33)
   constexpr int RPW = TH / 4;                    // output rows per wave
@@ -707,8 +710,9 @@ extern "C" int aiko_stem_direct(const void* in, void* out, const void* w, const 
       ldo % 8 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
       off_l % 4 == 0 && Wc % 4 == 0 && mean[0] == 0.f && mean[1] == 0.f && mean[2] == 0.f &&
       std[0] == std[1] && std[1] == std[2] && std[0] > 0.f) {
-    const char* th_env = getenv("AIKO_STEM_FAST_TH");         // 8 or 16 output rows per tile
-    const int th = th_env && atoi(th_env) == 16 ? 16 : 8;
+    const char* th_env = getenv("AIKO_STEM_FAST_TH");         // 8, 16 or 32 output rows per tile
+    const int th_req = th_env ? atoi(th_env) : 16;
+    const int th = th_req == 8 || th_req == 32 ? th_req : 16;
     // 16-B stores through v_permlane16_swap pairs: measured no faster on MI355X (69.2-69.8 us
     // narrow vs 70.4-74.2 us wide at B=64, same box), so opt-in
     const char* wide_env = getenv("AIKO_STEM_FAST_WIDE");    // read per call (tests flip it)
@@ -717,7 +721,8 @@ extern "C" int aiko_stem_direct(const void* in, void* out, const void* w, const 
     auto go = [&](auto act_tag, auto bgr_tag) {
       constexpr int A = decltype(act_tag)::value;
       constexpr bool G = decltype(bgr_tag)::value;
-      auto kern = th == 16 ? aiko::stem_fast_kernel<A, G, false, 16>
+      auto kern = th == 32 ? aiko::stem_fast_kernel<A, G, false, 32>
+                : th == 16 ? aiko::stem_fast_kernel<A, G, false, 16>
                            : (wide ? aiko::stem_fast_kernel<A, G, true, 8> : aiko::stem_fast_kernel<A, G, false, 8>);
       kern<<<grid, 256, 0, stream>>>(
           static_cast<const uint8_t*>(in), static_cast<aiko::bf16_t*>(out), static_cast<const aiko::bf16_t*>(w),

@@ -164,15 +164,19 @@ def test_fast_stem_wide_stores_identical(native, monkeypatch):
     g = torch.Generator().manual_seed(7)
     frames = torch.randint(0, 256, (2, 480, 640, 3), generator=g, dtype=torch.uint8).to(DEV)
     monkeypatch.setenv("AIKO_STEM_FAST_WIDE", "0")
+    monkeypatch.setenv("AIKO_STEM_FAST_TH", "8")
     narrow = m.stem_from_frames(frames).clone()
-    monkeypatch.setenv("AIKO_STEM_FAST_WIDE", "1")
+    monkeypatch.setenv("AIKO_STEM_FAST_WIDE", "1")              # (8-row tiles only)
     wide = m.stem_from_frames(frames).clone()
     monkeypatch.setenv("AIKO_STEM_FAST_WIDE", "0")
-    monkeypatch.setenv("AIKO_STEM_FAST_TH", "16")              # 16-row tiles: same values
-    tall = m.stem_from_frames(frames).clone()
+    talls = []
+    for th in ("16", "32"):                                    # 16- / 32-row tiles: same values
+        monkeypatch.setenv("AIKO_STEM_FAST_TH", th)
+        talls.append(m.stem_from_frames(frames).clone())
     torch.cuda.synchronize()
     assert torch.equal(wide, narrow)
-    assert torch.equal(tall, narrow)
+    for tall in talls:
+        assert torch.equal(tall, narrow)
 
 
 def test_yolov8n_fused_stem_detect_matches(native):
