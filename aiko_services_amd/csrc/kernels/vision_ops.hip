@@ -243,16 +243,17 @@ __global__ __launch_bounds__(256) void stem_direct_kernel(
 // tile: TH x 32 outputs.  TH = 16 is the default: 65.3-67.5 us against 71.8-72.4 (TH 8) and
 // 68.6-72.1 (TH 32) at B=64 480x640 on MI355X (same box, interleaved) — half the workgroups, half
 // the per-tile weight / bias loads and 3 % input-row halo instead of 6 %
-constexpr int kSfTW = 32;
-constexpr int kSfG = kSfTW / 2 + 1;             // 17 groups of 4 pixels per input row
-constexpr int kSfIW = 4 * kSfG;                 // 68 tile columns (tile col = input x - (2 ox0 - 1) + 3)
-template <int ACT, bool BGR, bool WIDE, int TH = 8>
+template <int ACT, bool BGR, bool WIDE, int TH = 8, int TW = 32>
 __global__ __launch_bounds__(256) void stem_fast_kernel(
     const uint8_t* __restrict__ in, bf16_t* __restrict__ out, const bf16_t* __restrict__ w,
     const float* __restrict__ bias, int Hin, int Win, int Hc, int Wc, int off_t, int off_l, float fill_raw,
     float inv_std, int H1, int W1, int ldo) {
   static_assert(TH == 8 || TH == 16 || TH == 32, "8, 16 or 32 output rows per tile");
-  static_assert(!WIDE || TH == 8, "the 16-B store path pairs the two half-rows of an 8-row tile");
+  static_assert(!WIDE || (TH == 8 && TW == 32), "the 16-B store path pairs the two half-rows of an 8 x 32 tile");
+  static_assert(TW == 32 || TW == 64, "32 or 64 output columns per tile");
+  constexpr int kSfTW = TW;
+  constexpr int kSfG = TW / 2 + 1;               // groups of 4 pixels per input row (17 / 33)
+  constexpr int kSfIW = 4 * kSfG;                // tile columns (tile col = input x - (2 ox0 - 1) + 3)
   constexpr int kSfIH = 2 * TH + 1;              // input rows (17 / 33)
   constexpr int RPW = TH / 4;                    // output rows per wave
   __shared__ __attribute__((aligned(16))) uint32_t stile[kSfIH * kSfIW * 2];   // [kSfIH][68] x 4 bf16
@@ -316,8 +317,8 @@ __global__ __launch_bounds__(256) void stem_fast_kernel(
   const int lbase = 2 * RPW * wave * kSfIW + 2 * fr;        // tile pixel of output (RPW wave, fr)
   if constexpr (!WIDE) {
 #pragma unroll
-    for (int pt = 0; pt < 2 * RPW; ++pt) {
-      const int dy = pt >> 1, dx = 16 * (pt & 1);
+    for (int pt = 0; pt < (TW / 16) * RPW; ++pt) {
+      const int dy = pt / (TW / 16), dx = 16 * (pt % (TW / 16));
       const int base = lbase + 2 * dy * kSfIW + 2 * dx;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -713,15 +714,18 @@ extern "C" int aiko_stem_direct(const void* in, void* out, const void* w, const 
     const char* th_env = getenv("AIKO_STEM_FAST_TH");         // 8, 16 or 32 output rows per tile
     const int th_req = th_env ? atoi(th_env) : 16;
     const int th = th_req == 8 || th_req == 32 ? th_req : 16;
+    const char* tw_env = getenv("AIKO_STEM_FAST_TW");         // 32 or 64 output columns per tile
+    const int tw = tw_env && atoi(tw_env) == 64 ? 64 : 32;
     // 16-B stores through v_permlane16_swap pairs: measured no faster on MI355X (69.2-69.8 us
     // narrow vs 70.4-74.2 us wide at B=64, same box), so opt-in
     const char* wide_env = getenv("AIKO_STEM_FAST_WIDE");    // read per call (tests flip it)
     const bool wide = wide_env && *wide_env == '1';
-    dim3 grid((W1 + aiko::kSfTW - 1) / aiko::kSfTW, (H1 + th - 1) / th, B);
+    dim3 grid((W1 + tw - 1) / tw, (H1 + th - 1) / th, B);
     auto go = [&](auto act_tag, auto bgr_tag) {
       constexpr int A = decltype(act_tag)::value;
       constexpr bool G = decltype(bgr_tag)::value;
-      auto kern = th == 32 ? aiko::stem_fast_kernel<A, G, false, 32>
+      auto kern = tw == 64 ? (th == 8 ? aiko::stem_fast_kernel<A, G, false, 8, 64> : aiko::stem_fast_kernel<A, G, false, 16, 64>)
+                : th == 32 ? aiko::stem_fast_kernel<A, G, false, 32>
                 : th == 16 ? aiko::stem_fast_kernel<A, G, false, 16>
                            : (wide ? aiko::stem_fast_kernel<A, G, true, 8> : aiko::stem_fast_kernel<A, G, false, 8>);
       kern<<<grid, 256, 0, stream>>>(

@@ -170,8 +170,9 @@ def test_fast_stem_wide_stores_identical(native, monkeypatch):
     wide = m.stem_from_frames(frames).clone()
     monkeypatch.setenv("AIKO_STEM_FAST_WIDE", "0")
     talls = []
-    for th in ("16", "32"):                                    # 16- / 32-row tiles: same values
+    for th, tw in (("16", "32"), ("32", "32"), ("8", "64"), ("16", "64")):   # other tiles: same values
         monkeypatch.setenv("AIKO_STEM_FAST_TH", th)
+        monkeypatch.setenv("AIKO_STEM_FAST_TW", tw)
         talls.append(m.stem_from_frames(frames).clone())
     torch.cuda.synchronize()
     assert torch.equal(wide, narrow)
