@@ -83,7 +83,7 @@ int aiko_sppf_pool(void* x, int B, int H, int W, int ld, int c, int k, hipStream
 int aiko_window_shift(const float* src, const float* chunk, float* dst, int B, int W, int n, hipStream_t stream);
 int aiko_conv_narrow(const void* x, const void* w, const float* bias, const void* res, void* y, int H, int W, int C,
                      int Cc, int R, int S, int stride, int pad, int Ho, int Wo, int M, int Cout, int K, int act,
-                     int ldy, int ldr, hipStream_t stream);
+                     int ldy, int ldr, int th, int wreg, hipStream_t stream);
 int aiko_stem_pool_u8(const void* frames, const void* w, const float* bias, void* y, int B, int Hi, int Wi,
                       int Ho, int Wo, int Hm, int Wm, int ldy, const float* mean255, int variant, hipStream_t stream);
 int aiko_stem_pool(const void* x, const void* w, const float* bias, void* y, int B, int Hp, int Wp,
@@ -201,7 +201,7 @@ void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, co
                     (Cc == 16 || Cc == 32) && (Cout == 16 || Cout == 32),
                 "aiko.conv_igemm_out: variant 7 needs a 3x3 / pad 1 / stride 1-2 or 1x1 / stride 1 conv with Cc, Cout in {16, 32}");
     rc = aiko_conv_narrow(x.data_ptr(), w.data_ptr(), bptr, rptr, y.data_ptr(), H, W, C, Cc, R, S, stride, pad, Ho,
-                          Wo, M, Cout, K, act, ldy, ldr, cur_stream());
+                          Wo, M, Cout, K, act, ldy, ldr, bm == 16 ? 16 : 8, bn == 64 ? 1 : 0, cur_stream());
   } else if (variant == 8 || variant == 9 || variant == 11) {
     // 8-wave wide tiles, transposed product, register-direct epilogue (conv_wide.hip)
     TORCH_CHECK(Cc % 64 == 0 && R * S <= 32 && x_extent * 2 < (1LL << 31) - 64 && w.numel() * 2 < (1LL << 31),

@@ -31,10 +31,12 @@ struct NarrowParams {
   int H, W, C, Ho, Wo, K, act, ldy, ldr, tiles_h, tiles_w;
 };
 
-constexpr int kNTH = 8, kNTW = 32;   // output tile rows x cols: 4 waves x 4 blocks of 16 pixels
+constexpr int kNTW = 32;   // output tile cols; rows TH = 8 (4 waves x 4 blocks of 16 pixels) or 16
 
-template <int CC, int COUT, int ST, int FR = 3>
+template <int CC, int COUT, int ST, int FR = 3, int TH = 8, bool WREG = false>
 __global__ __launch_bounds__(256) void conv_narrow_kernel(NarrowParams p) {
+  constexpr int kNTH = TH;
+  constexpr int RPW = TH / 4;                   // output rows per wave
   constexpr int TAPS = FR * FR, PAD = FR / 2;   // 3x3 / pad 1 or 1x1 / pad 0
   constexpr int IH = (kNTH - 1) * ST + FR, IW = (kNTW - 1) * ST + FR;
   constexpr int CH = CC / 8;                    // 16-byte chunks per pixel
@@ -45,8 +47,10 @@ __global__ __launch_bounds__(256) void conv_narrow_kernel(NarrowParams p) {
   constexpr int NT = COUT / 16;                 // 16-channel output tiles
   // Cc 32: the 9-chunk weight set would hold 72 VGPRs per lane for the whole tile; it is staged
   // in LDS instead and read per K chunk (16-B reads, 16 lanes share a row).  Measured on the
-  // YOLOv8-n Cc-32 layers: on par with the igemm kernel (28-32 us), either may win per layer
-  constexpr bool WLDS = CC == 32;
+  // YOLOv8-n Cc-32 layers: on par with the igemm kernel (28-32 us), either may win per layer.
+  // WREG keeps them in registers anyway (80 VGPRs at Cout 32): the per-MFMA A read from LDS
+  // (1.5 LDS reads per MFMA with the B fragment) is what bounds the LDS-staged form
+  constexpr bool WLDS = CC == 32 && !WREG;
   constexpr int WELEMS = WLDS ? COUT * NKC * 32 : 8;
   __shared__ __attribute__((aligned(16))) bf16_t tile[IH * IW * CC];
   __shared__ __attribute__((aligned(16))) bf16_t wlds[WELEMS];
@@ -121,8 +125,8 @@ __global__ __launch_bounds__(256) void conv_narrow_kernel(NarrowParams p) {
   const bool post = (p.act & 16) != 0;
   const int act = p.act & 15;
 #pragma unroll
-  for (int pt = 0; pt < 4; ++pt) {
-    const int ly = 2 * wave + (pt >> 1), lx = 16 * (pt & 1) + fr;
+  for (int pt = 0; pt < 2 * RPW; ++pt) {
+    const int ly = RPW * wave + (pt >> 1), lx = 16 * (pt & 1) + fr;
     const int base = ((ly * ST) * IW + lx * ST) * CC;
     f32x4 acc[NT];
 #pragma unroll
@@ -186,9 +190,10 @@ __global__ __launch_bounds__(256) void conv_narrow_kernel(NarrowParams p) {
 extern "C" int aiko_conv_narrow(const void* x, const void* w, const float* bias, const void* res,
                                 void* y, int H, int W, int C, int Cc, int R, int S, int stride,
                                 int pad, int Ho, int Wo, int M, int Cout, int K, int act, int ldy,
-                                int ldr, hipStream_t stream) {
+                                int ldr, int th, int wreg, hipStream_t stream) {
   using namespace aiko;
   const bool k3 = R == 3 && S == 3 && pad == 1, k1 = R == 1 && S == 1 && pad == 0;
+  if (th != 8 && th != 16) return -1;
   if ((!k3 && !k1) || (stride != 1 && stride != 2) || (Cc != 16 && Cc != 32) ||
       (Cout != 16 && Cout != 32) || K < R * S * Cc || K % 64 || C % 8 || ldy % 4 || ldr % 4 ||
       Ho <= 0 || Wo <= 0 || M % (Ho * Wo))
@@ -200,13 +205,20 @@ extern "C" int aiko_conv_narrow(const void* x, const void* w, const float* bias,
   p.res = static_cast<const bf16_t*>(res);
   p.y = static_cast<bf16_t*>(y);
   p.H = H; p.W = W; p.C = C; p.Ho = Ho; p.Wo = Wo; p.K = K; p.act = act; p.ldy = ldy; p.ldr = ldr;
-  p.tiles_h = (Ho + kNTH - 1) / kNTH;
+  p.tiles_h = (Ho + th - 1) / th;
   p.tiles_w = (Wo + kNTW - 1) / kNTW;
   const long grid = (long)(M / (Ho * Wo)) * p.tiles_h * p.tiles_w;
   if (grid <= 0 || grid > 0x7fffffffL) return -1;
   const dim3 g((unsigned)grid), b(256);
-#define AIKO_NARROW(FR, CC, CO, ST) \
-  if (R == FR && Cc == CC && Cout == CO && stride == ST) { conv_narrow_kernel<CC, CO, ST, FR><<<g, b, 0, stream>>>(p); return (int)hipGetLastError(); }
+#define AIKO_NARROW(FR, CC, CO, ST)                                                                      \
+  if (R == FR && Cc == CC && Cout == CO && stride == ST) {                                                \
+    if (wreg && CC == 32) {                                                                               \
+      if (th == 16) conv_narrow_kernel<CC, CO, ST, FR, 16, true><<<g, b, 0, stream>>>(p);                 \
+      else conv_narrow_kernel<CC, CO, ST, FR, 8, true><<<g, b, 0, stream>>>(p);                           \
+    } else if (th == 16) conv_narrow_kernel<CC, CO, ST, FR, 16><<<g, b, 0, stream>>>(p);                  \
+    else conv_narrow_kernel<CC, CO, ST, FR, 8><<<g, b, 0, stream>>>(p);                                   \
+    return (int)hipGetLastError();                                                                      \
+  }
   AIKO_NARROW(3, 16, 16, 1) AIKO_NARROW(3, 16, 32, 1) AIKO_NARROW(3, 32, 16, 1) AIKO_NARROW(3, 32, 32, 1)
   AIKO_NARROW(3, 16, 16, 2) AIKO_NARROW(3, 16, 32, 2) AIKO_NARROW(3, 32, 16, 2) AIKO_NARROW(3, 32, 32, 2)
   AIKO_NARROW(1, 16, 16, 1) AIKO_NARROW(1, 16, 32, 1) AIKO_NARROW(1, 32, 16, 1) AIKO_NARROW(1, 32, 32, 1)

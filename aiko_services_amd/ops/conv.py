@@ -324,7 +324,10 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False):
     if cout <= 32:
         cands = [t + (0,) for t in NARROW_TILES]
         if narrow_ok:
-            cands.append((8, 32, 7))         # variant 7: tile fixed by the kernel (8 x 32 pixels)
+            cands.append((8, 32, 7))         # variant 7: 8 x 32 output pixels per workgroup
+            cands.append((16, 32, 7))        #            16 x 32
+            cands.append((8, 64, 7))         # bn = 64: Cc-32 weights held in registers, not LDS
+            cands.append((16, 64, 7))
     else:
         cands = [t + (0,) for t in TILES] + [t + (1,) for t in TILES]
         if buf_ok:

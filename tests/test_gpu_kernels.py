@@ -71,6 +71,16 @@ def _nhwc(x_nchw):
     (1, 9, 10, 16, 32, 3, 1, 1, "gelu", True, (8, 32, 7)),
     (2, 21, 45, 32, 32, 1, 1, 0, "silu", True, (8, 32, 7)),
     (1, 16, 32, 16, 32, 1, 1, 0, None, False, (8, 32, 7)),
+    # the same kernel with 16-row output tiles
+    (1, 20, 64, 32, 16, 3, 2, 1, None, False, (16, 32, 7)),
+    (1, 9, 10, 16, 32, 3, 1, 1, "gelu", True, (16, 32, 7)),
+    (2, 21, 45, 32, 32, 1, 1, 0, "silu", True, (16, 32, 7)),
+    (2, 37, 70, 16, 16, 3, 1, 1, "silu", True, (16, 32, 7)),
+    (1, 40, 66, 16, 32, 3, 2, 1, "relu", False, (16, 32, 7)),
+    # Cc-32 weights in registers (bn = 64)
+    (1, 9, 10, 32, 32, 3, 1, 1, "gelu", True, (16, 64, 7)),
+    (2, 21, 45, 32, 16, 3, 2, 1, "silu", True, (8, 64, 7)),
+    (2, 21, 45, 32, 32, 1, 1, 0, "silu", True, (16, 64, 7)),
     # high-occupancy buffer-DMA (variant 3)
     (2, 28, 28, 128, 512, 1, 1, 0, "relu", True, (64, 128, 3)),
     (1, 9, 11, 128, 64, 3, 1, 1, "silu", False, (64, 64, 3)),
