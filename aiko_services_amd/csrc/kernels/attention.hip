@@ -151,7 +151,7 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const u32x4 raw = *reinterpret_cast<const u32x4*>(p.q + (seq0 + qc) * p.ldq + hc + ks * 32 + 8 * g);
-      if constexpr (SM == 1) {
+      if constexpr (SM >= 1) {
         u32x4 w;
 #pragma unroll
         for (int e = 0; e < 4; ++e)
@@ -315,9 +315,9 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
     // bounded by 2^kRescale and the stale max is exact for the final normalisation)
     const float c = p.scale_log2;
     bf16x8 pf[2][2];
-    if constexpr (SM == 1) {
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
+    // SM >= 1 softmax of query tile qt: tile max relative to m_run (v_max3 tree + 2 permlane
+    // swaps), lazy rescale, v_exp straight off the accumulators, bf16 pack
+    auto softmax_qt = [&](int qt) {
         if constexpr (MASK) {
 #pragma unroll
           for (int kt = 0; kt < 4; ++kt)
@@ -356,7 +356,33 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
           u[3] = pack2(fast_exp2(s[2 * ks + 1][qt][2]), fast_exp2(s[2 * ks + 1][qt][3]));
           pf[qt][ks] = as_bf16x8(u);
         }
+    };
+    auto pv_qt = [&](int qt) {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        read_v(d);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          o[d][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vfr[d][ks], pf[qt][ks], o[d][qt], 0, 0, 0);
       }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        lsum[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qt][ks], lsum[qt], 0, 0, 0);
+    };
+    if constexpr (SM == 2) {
+      // ping-pong the two query tiles: query tile 0's PV MFMAs are issued before tile 1's
+      // softmax, so the matrix pipe works on tile 0 while the VALU runs tile 1's exp / pack (V
+      // fragments are re-read for tile 1: +16 LDS reads, no extra VGPRs).  Same operations per
+      // accumulator in the same order as SM = 1: bit-identical output.  Measured (variant 15,
+      // scripts/attn_pp_ab.sh): 141.8-142.6 us against 134.2-134.5 us for SM = 1 — the V re-reads
+      // cost more than the overlap returns; kept opt-in
+      softmax_qt(0);
+      pv_qt(0);
+      softmax_qt(1);
+      pv_qt(1);
+    } else if constexpr (SM == 1) {
+      softmax_qt(0);
+      softmax_qt(1);
     } else {
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
@@ -409,6 +435,7 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
     }
 
     // O^T += V^T P^T (fragments read above / here)
+    if constexpr (SM != 2) {
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       if (d >= VPRE) read_v(d);
@@ -425,6 +452,7 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
         for (int qt = 0; qt < 2; ++qt)
           lsum[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qt][ks], lsum[qt], 0, 0, 0);
     }
+    }
 
     slot = slot == NS - 1 ? 0 : slot + 1;
   };
@@ -433,7 +461,7 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
   for (int it = tb; it < tfull; ++it) tile(it, std::false_type{});
   if (nfull < te) tile(nfull, std::true_type{});
 
-  if constexpr (SM == 1) {
+  if constexpr (SM >= 1) {
     if (piece >= 0) {
       // a key-range piece: publish (m, l, unnormalised O) for its rows; the last of the
       // split_s pieces to arrive merges them: O = sum_i 2^(m_i - M) O_i / sum_i 2^(m_i - M) l_i
@@ -493,7 +521,7 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     float l;
-    if constexpr (SM == 1) {
+    if constexpr (SM >= 1) {
       l = lsum[qt][0];                 // every row of the ones-MFMA result is the row sum
     } else {
       l = l_run[qt];
@@ -536,10 +564,8 @@ extern "C" int aiko_attn_fwd(const void* q, const void* k, const void* v, void* 
   p.split_s = p.split_full = p.split_r = 0;
   p.part = nullptr;
   p.cnt = nullptr;
-  static const int variant = [] {
-    const char* v = getenv("AIKO_ATTN_VARIANT");
-    return v ? atoi(v) : 0;
-  }();
+  const char* variant_env = getenv("AIKO_ATTN_VARIANT");   // read per call (tests flip it)
+  const int variant = variant_env ? atoi(variant_env) : 0;
   // pieces per split item; 0 = no split.  Measured on MI355X at Whisper-small shapes (median of
   // 7 x 50 launches, scripts/attn_split_ab.sh): unsplit 135.1-135.4 us, s=2 133.2-134.4, s=4
   // 147.5-148.3, s=8 134.1-135.4, and the 1-D mapping alone (s=1) 139.7-140.4 — the final-round
@@ -566,7 +592,7 @@ extern "C" int aiko_attn_fwd(const void* q, const void* k, const void* v, void* 
     p.nqb = (T + QB - 1) / QB;
     const long items = (long)p.nqb * H * B;
     const int ntiles = (T + aiko::kKB - 1) / aiko::kKB;
-    if (SM == 1 && work && force_s > 0 && cus >= 8 && items % 8 == 0) {
+    if (SM >= 1 && work && force_s > 0 && cus >= 8 && items % 8 == 0) {
       const long n = items / 8;
       const int slots = (16 / NW) * (cus / 8);          // resident workgroups per XCD
       const int r = (int)(n % slots);
@@ -609,6 +635,7 @@ extern "C" int aiko_attn_fwd(const void* q, const void* k, const void* v, void* 
     case 12: launch(I8{}, V0{}, R1{}, R1{}); break;
     case 13: launch(I4{}, V0{}, R0{}, R1{}); break;
     case 14: launch(I4{}, V2{}, R1{}, R1{}); break;
+    case 15: launch(I8{}, V0{}, R0{}, std::integral_constant<int, 2>{}); break;   // ping-pong query tiles
     default: launch(I8{}, V0{}, R0{}, R1{}); break;
   }
   return (int)hipGetLastError();

@@ -147,6 +147,27 @@ def test_flash_attention_split_tail(native, B, H, T, Tpad, scale_k, pieces, monk
         assert outs[0].view(B, Tpad, d)[:, T:].abs().max().item() == 0
 
 
+def test_flash_attention_pingpong_identical(native, monkeypatch):
+    """Variant 15 (the two query tiles ping-ponged: tile 0's PV MFMAs issued before tile 1's
+    softmax) runs the same operations per accumulator in the same order as the default softmax:
+    bit-identical output, ragged last tile and the lazy-rescale path included."""
+    from aiko_services_amd.ops import transformer as TR
+    g = torch.Generator().manual_seed(5)
+    B, H, T, Tpad = 2, 3, 1000, 1024
+    d = H * 64
+    qkv = torch.randn(B * Tpad, 3 * d, generator=g) * 1.5
+    qkv.view(B, Tpad, 3, H, 64)[:, :, 1] *= torch.linspace(0.3, 6.0, Tpad).view(1, Tpad, 1, 1)
+    qkv = qkv.to(DEV, torch.bfloat16)
+    outs = []
+    for variant in ("0", "15"):
+        monkeypatch.setenv("AIKO_ATTN_VARIANT", variant)
+        o = torch.zeros(B * Tpad, d, dtype=torch.bfloat16, device=DEV)
+        TR.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, B, H, T, Tpad, 0.125)
+        outs.append(o)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_log_mel(native):
     from aiko_services_amd.ops import audio as AU
     g = torch.Generator().manual_seed(3)
