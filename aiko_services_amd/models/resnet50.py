@@ -375,6 +375,9 @@ class ResNet50(WeightsMixin):
         the image must be refreshed here, not lazily at the next eager call)."""
         if getattr(self.stem, "_stem_pool_w", None) is not None:
             C.stem_pool_weight(self.stem)
+        u8 = getattr(self.stem, "_stem_pool_u8_w", None)
+        if u8 is not None:                          # the uint8 stem's 1/(255 std)-scaled image
+            C.stem_pool_u8_weight(self.stem, u8[0][2])
         for b in self.blocks:
             if b.fused is None:
                 continue

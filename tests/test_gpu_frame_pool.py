@@ -51,8 +51,13 @@ def test_frames_in_pool_slots_and_graphs_on_slots(native):
     st = src.frame_pool.stats()
     assert st["acquired"] == 3 + 9 and st["high_water"] <= 3     # 3 fills + 9 frames
     resnet = p.get_element("ResNet50Classifier")
-    graphs = [k for k in resnet._captured if isinstance(k, tuple) and len(k) == 3 and k[0] != "addrs"]
-    assert len(graphs) == 3, graphs                    # one graph per slot address, no copy path
+    # per-address graphs live in the ("graphs", key, lane) LRU; the copy-in fallback is keyed
+    # (key, lane) and must never have been created
+    per_addr = [a for k, g in resnet._captured.items() if isinstance(k, tuple) and k[:1] == ("graphs",)
+                for a in g]
+    assert len(per_addr) == 3, per_addr                # one graph per slot address
+    copy_in = [k for k in resnet._captured if isinstance(k, tuple) and len(k) == 2 and k[0] not in ("graphs", "seen")]
+    assert not copy_in, copy_in                        # no copy path
     # same slot -> same frames -> same top-5 (frames 0, 3, 6 used slot 0)
     a, b = results[0].wait(), results[3].wait()
     assert torch.equal(a["top_index"], b["top_index"])
