@@ -44,11 +44,12 @@ def test_pp_rank0_local_share_runs_two_lanes():
     """a stage ending in a remote element may run frame lanes, and rank 0's
     local share of the replicated ResNet stage runs in the enclosing frame's lane.  World-1 plan
     (stage 0 = decode + resize, stage 1 = ResNet-50 + top-k as rank 0's local share, 224²
-    frames): two lanes beat one."""
+    frames, B=256 as in config 3 — at B=128 the host-side plan, not the GPU, sets the pace and
+    the lanes gain only ~3 %): two lanes beat one."""
     vals = {}
     for lanes in (1, 2):
-        r = _torchrun("bench.py", "--parallel", "pp", "--gpus", "1", "--steps", "12", "--warmup", "4",
-                      "--batch", "128", "--lanes", str(lanes), "--height", "224", "--width", "224")
+        r = _torchrun("bench.py", "--parallel", "pp", "--gpus", "1", "--steps", "16", "--warmup", "4",
+                      "--batch", "256", "--lanes", str(lanes), "--height", "224", "--width", "224")
         lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
         assert r.returncode == 0 and lines, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
         out = json.loads(lines[-1])
