@@ -478,6 +478,181 @@ __global__ __launch_bounds__(256, 2) void stem_pool_strip_kernel(StemPoolParams 
   }
 }
 
+// ---- strip variant with half-channel waves (variants 3 / 4): occupancy for lane overlap ----
+//
+// The strip kernel above holds all 64 channels' A fragments per wave (112 VGPRs, 214 in all)
+// and 55 KB of LDS: two workgroups per CU, and while the stem runs (4 rounds of long-lived
+// strips) the other frame lane's conv tiles cannot be resident beside it — the bench measured
+// the stem costing ~170 us of wall time per batch against its 127 us of kernel time.  Here a
+// wave owns 32 channels (2 channel blocks: 56 VGPRs of A fragments) x 8 stem rows instead of
+// 64 channels x 4 rows — the same 112 MFMAs per wave and tile, the same accumulation order per
+// output (so bit-identical to variants 0-2), twice the B-fragment reads (still < half the LDS
+// rate) — and the pool tile is single-buffered with the previous tile's last stem row carried
+// in a 2 x 1 KB side buffer: 40.6 KB of LDS and 124 VGPRs, so 4 workgroups fit a CU (variant 3,
+// two stem rows per MFMA group) and the kernel leaves registers / LDS for a co-resident lane;
+// variant 4 groups four rows (8 accumulators in flight, 3 workgroups per CU).
+constexpr int kSp2HpB = kSpRows * kSpHpRowB;             // 16128 B, single buffer
+constexpr int kSp2CarryB = kSpHpRowB;                    // 1008 B: one stem row of 7 pixels
+
+template <int WGS, int RP>
+__global__ __launch_bounds__(256, WGS) void stem_pool_strip2_kernel(StemPoolParams p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * kSpPatchB + kSp2HpB + 2 * kSp2CarryB];
+  unsigned char* patch0 = smem;
+  unsigned char* hp = smem + 2 * kSpPatchB;
+  unsigned char* carry0 = hp + kSp2HpB;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int chh = wave & 1;                              // channel half: blocks 2 chh, 2 chh + 1
+  const int rh = wave >> 1;                              // stem rows 8 rh .. 8 rh + 7 of a tile
+  const int strips = p.tiles_w;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int img = bid / strips;
+  const int sj = bid - img * strips;
+  const int px0 = sj * 7;
+  const int sx0 = 2 * px0 - 1;
+  const int ix0 = 2 * sx0 - 3;
+  const int xa = ix0 >= 0 ? (ix0 & ~3) : -((3 - ix0) & ~3);
+  const uint8_t* im = p.xu8 + (size_t)img * p.Hi * p.Wi * 3;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  bf16x8 af[7][2];
+  f32x4 bias[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int mb = 2 * chh + j;
+    const int o = mb * 16 + fr;
+#pragma unroll
+    for (int r = 0; r < 7; ++r)
+      af[r][j] = *reinterpret_cast<const bf16x8*>(
+          reinterpret_cast<const unsigned char*>(p.w) + r * 64 * 64 + (o * 4 + (fq ^ ((o >> 2) & 2))) * 16);
+    bias[j] = *reinterpret_cast<const f32x4*>(p.bias + mb * 16 + fq * 4);
+  }
+
+  uint32_t pre[kSpTaskIt][3];
+  auto load_patch = [&](int py0) {
+    const int iy0 = 4 * py0 - 3;
+#pragma unroll
+    for (int k = 0; k < kSpTaskIt; ++k) {
+      const int task = tid + k * 256;
+      const int r = task / kSpGroups, gi = task - r * kSpGroups;
+      const int y = iy0 + r, x = xa + 4 * gi;
+      pre[k][0] = pre[k][1] = pre[k][2] = 0u;
+      if (task < kSpTasks && (unsigned)y < (unsigned)p.Hi && x >= 0 && x + 3 < p.Wi) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(im + ((size_t)y * p.Wi + x) * 3);
+        pre[k][0] = __builtin_nontemporal_load(src);
+        pre[k][1] = __builtin_nontemporal_load(src + 1);
+        pre[k][2] = __builtin_nontemporal_load(src + 2);
+      }
+    }
+  };
+  auto store_patch = [&](unsigned char* patch, int py0) {
+    const int iy0 = 4 * py0 - 3;
+#pragma unroll
+    for (int k = 0; k < kSpTaskIt; ++k) {
+      const int task = tid + k * 256;
+      if (task >= kSpTasks) continue;
+      const int r = task / kSpGroups, gi = task - r * kSpGroups;
+      const int y = iy0 + r, x = xa + 4 * gi;
+      const bool in = (unsigned)y < (unsigned)p.Hi && x >= 0 && x + 3 < p.Wi;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = x + q - ix0;
+        if ((unsigned)j >= (unsigned)kSpPW) continue;
+        uint2 o = {0u, 0u};
+        if (in) {
+          const int e = 3 * q;
+          const float c0 = (float)((pre[k][e >> 2] >> (8 * (e & 3))) & 0xFFu);
+          const float c1 = (float)((pre[k][(e + 1) >> 2] >> (8 * ((e + 1) & 3))) & 0xFFu);
+          const float c2 = (float)((pre[k][(e + 2) >> 2] >> (8 * ((e + 2) & 3))) & 0xFFu);
+          o = make_uint2(pack2(c0 - p.m0, c1 - p.m1), pack2(c2 - p.m2, 0.f));
+        }
+        *reinterpret_cast<uint2*>(patch + r * kSpRowB + j * 8) = o;
+      }
+    }
+  };
+
+  const int b_base = 2 * (8 * rh) * kSpRowB + 16 * fr + 16 * fq;
+  const bool col_ok = (unsigned)(sx0 + fr) < (unsigned)p.Wo;
+  const bool store_lane = (fr & 1) && fr < 15;
+  const int hp_lane = ((fr - 1) >> 1) * kSpHpPitch + fq * 8 + chh * 64;
+
+  load_patch(0);
+  store_patch(patch0, 0);
+  __syncthreads();
+
+  for (int t = 0; t < p.tiles_h; ++t) {
+    const int py0 = t * 8;
+    const int sy0 = 2 * py0;
+    const unsigned char* patch = patch0 + (t & 1) * kSpPatchB + b_base;
+    const bool more = t + 1 < p.tiles_h;
+    if (more) load_patch(py0 + 8);
+
+    // RP stem rows at a time: 2 RP accumulators (RP rows x 2 channel blocks)
+#pragma unroll
+    for (int np = 0; np < 8 / RP; ++np) {
+      f32x4 acc[2][RP];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int nj = 0; nj < RP; ++nj) acc[j][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 7; ++r)
+#pragma unroll
+        for (int nj = 0; nj < RP; ++nj) {
+          const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(patch + (2 * (RP * np + nj) + r) * kSpRowB);
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[j][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[r][j], bfr, acc[j][nj], 0, 0, 0);
+        }
+      if (np == 0) __syncthreads();                      // pool(t - 1) is done with hp
+
+#pragma unroll
+      for (int nj = 0; nj < RP; ++nj) {
+        const int row = 8 * rh + RP * np + nj;
+        const float hi = (col_ok && sy0 + row < p.Ho) ? __builtin_inff() : 0.f;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const f32x2 s01 = f32x2{acc[j][nj][0], acc[j][nj][1]} + f32x2{bias[j][0], bias[j][1]};
+          const f32x2 s23 = f32x2{acc[j][nj][2], acc[j][nj][3]} + f32x2{bias[j][2], bias[j][3]};
+          const uint32_t w01 = pack2(__builtin_amdgcn_fmed3f(s01[0], 0.f, hi), __builtin_amdgcn_fmed3f(s01[1], 0.f, hi));
+          const uint32_t w23 = pack2(__builtin_amdgcn_fmed3f(s23[0], 0.f, hi), __builtin_amdgcn_fmed3f(s23[1], 0.f, hi));
+          const uint32_t h01 = sp_max3_u16x2(w01, sp_dpp_shr1(w01), sp_dpp_shl1(w01));
+          const uint32_t h23 = sp_max3_u16x2(w23, sp_dpp_shr1(w23), sp_dpp_shl1(w23));
+          if (store_lane)
+            *reinterpret_cast<uint2*>(hp + row * kSpHpRowB + hp_lane + j * 32) = make_uint2(h01, h23);
+        }
+      }
+    }
+    if (more) store_patch(patch0 + ((t + 1) & 1) * kSpPatchB, py0 + 8);
+    __syncthreads();
+
+    // vertical max; the thread that reads stem row 15 (pooled row 7) also copies it into the
+    // carry buffer the next tile's pooled row 0 reads (double-buffered by tile parity)
+    const unsigned char* cin = carry0 + (t & 1) * kSp2CarryB;
+    unsigned char* cout_ = carry0 + ((t + 1) & 1) * kSp2CarryB;
+    for (int it = tid; it < 8 * 7 * 8; it += 256) {
+      const int pp = it >> 3, g = it & 7;
+      const int i = pp / 7, jx = pp - i * 7;
+      const int gy = py0 + i, gx = px0 + jx;
+      const int off = jx * kSpHpPitch + g * 16;
+      const u32x4 a = *reinterpret_cast<const u32x4*>(hp + (2 * i) * kSpHpRowB + off);
+      const u32x4 b = *reinterpret_cast<const u32x4*>(hp + (2 * i + 1) * kSpHpRowB + off);
+      u32x4 c = u32x4{0u, 0u, 0u, 0u};
+      if (i > 0)
+        c = *reinterpret_cast<const u32x4*>(hp + (2 * i - 1) * kSpHpRowB + off);
+      else if (t > 0)
+        c = *reinterpret_cast<const u32x4*>(cin + off);
+      if (i == 7) *reinterpret_cast<u32x4*>(cout_ + off) = b;
+      if (gy >= p.Hm || gx >= p.Wm) continue;
+      const u32x4 o = u32x4{sp_max3_u16x2(a.x, b.x, c.x), sp_max3_u16x2(a.y, b.y, c.y),
+                            sp_max3_u16x2(a.z, b.z, c.z), sp_max3_u16x2(a.w, b.w, c.w)};
+      *reinterpret_cast<u32x4*>(p.y + ((size_t)(img * p.Hm + gy) * p.Wm + gx) * p.ldy + g * 8) = o;
+    }
+  }
+}
+
 }  // namespace
 
 }  // namespace aiko
@@ -528,14 +703,19 @@ extern "C" int aiko_stem_pool_u8(const void* frames, const void* w, const float*
   p.bias = bias;
   p.y = static_cast<bf16_t*>(y);
   p.B = B; p.Hp = Hi + 6; p.Wp = Wi + 6; p.Ho = Ho; p.Wo = Wo; p.Hm = Hm; p.Wm = Wm; p.ldy = ldy;
-  if (variant == 2) {
-    // strip kernel: stem rows 2 py0 .. 2 py0 + 15 of every pooled tile must exist in the stem
+  if (variant >= 2 && variant <= 4) {
+    // strip kernels: stem rows 2 py0 .. 2 py0 + 15 of every pooled tile must exist in the stem
     // geometry the pool expects (Ho = 2 Hm or 2 Hm - 1; stem rows past Ho read as zeros)
     p.tiles_h = (Hm + 7) / 8;
     p.tiles_w = (Wm + 6) / 7;
     const long grid = (long)B * p.tiles_w;
     if (grid <= 0 || grid > 0x7fffffffL) return -1;
-    stem_pool_strip_kernel<<<dim3((unsigned)grid), dim3(256), 0, stream>>>(p);
+    if (variant == 2)
+      stem_pool_strip_kernel<<<dim3((unsigned)grid), dim3(256), 0, stream>>>(p);
+    else if (variant == 3)
+      stem_pool_strip2_kernel<4, 2><<<dim3((unsigned)grid), dim3(256), 0, stream>>>(p);
+    else
+      stem_pool_strip2_kernel<3, 4><<<dim3((unsigned)grid), dim3(256), 0, stream>>>(p);
     return (int)hipGetLastError();
   }
   const int tpw = variant == 1 ? 14 : 7;

@@ -445,8 +445,12 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None
 
 STEM_POOL_VARIANT = 0     # 0: 8x7 pooled tiles (4 workgroups/CU); 1: 8x14 (2 workgroups/CU)
 # uint8 stem: 2 = the strip kernel (weights in registers for a 7-column strip of pooled tiles,
-# horizontal max in DPP lanes): 126.6 us vs 136.1 us for the tile kernel at B=256 on MI355X
-STEM_POOL_U8_VARIANT = int(__import__("os").environ.get("AIKO_STEM_U8_VARIANT", "2"))
+# horizontal max in DPP lanes): 126.6 us vs 136.1 us for the tile kernel at B=256 on MI355X;
+# 3 (default) = the strip kernel with half-channel waves (124 VGPRs, 40.6 KB LDS: 4 workgroups
+# per CU instead of 2, room for the other frame lane): 126-128 us vs 143-150 us for variant 2 on
+# the same box, ResNet-50 bench 85.2k / 83.9k vs 81.7k / 83.0k interleaved; 4 = four rows per
+# MFMA group (3 workgroups per CU), not faster
+STEM_POOL_U8_VARIANT = int(__import__("os").environ.get("AIKO_STEM_U8_VARIANT", "3"))
 
 
 def stem_pool_weight(spec: ConvSpec) -> torch.Tensor:

@@ -51,7 +51,7 @@ def main():
         print(f"stem_pool variant {v} {t:8.1f} us  exact={ok}")
     from aiko_services_amd.ops.vision import IMAGENET_MEAN, IMAGENET_STD
     outs = {}
-    for v in (0, 1, 2):
+    for v in (0, 1, 2, 3, 4):
         outs[v] = C.stem_pool_u8(frames, spec, IMAGENET_MEAN, IMAGENET_STD, variant=v).clone()
         t = timed(lambda: C.stem_pool_u8(frames, spec, IMAGENET_MEAN, IMAGENET_STD, out=out, variant=v))
         print(f"stem_pool_u8 variant {v} {t:8.1f} us  same_as_v0={torch.equal(outs[v], outs[0])}")

@@ -434,7 +434,7 @@ def test_stem_pool_fused(native, hw):
     # same values within bf16 rounding of the input / scaled weights, both tile widths
     if hw[1] % 4 == 0:
         outs = []
-        for variant in (0, 1, 2):
+        for variant in (0, 1, 2, 3, 4):
             u8 = C.stem_pool_u8(frames.to(DEV), spec, V.IMAGENET_MEAN, V.IMAGENET_STD, variant=variant)
             torch.cuda.synchronize()
             assert u8.shape == fused.shape
@@ -442,5 +442,7 @@ def test_stem_pool_fused(native, hw):
             assert _rel_err(u8.float(), fused.float()) < 1e-2
             outs.append(u8)
         # the strip kernel (weights in registers, in-register horizontal max) is bit-identical
-        # to the tile kernel: same patch values, same MFMA order per accumulator
+        # to the tile kernel: same patch values, same MFMA order per accumulator; so are the
+        # half-channel-wave strip kernels (variants 3 / 4, carried pool row)
         assert torch.equal(outs[2], outs[0])
+        assert torch.equal(outs[3], outs[0]) and torch.equal(outs[4], outs[0])
