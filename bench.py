@@ -148,7 +148,12 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--batch", type=int, default=256, help="frames per GPU per step")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="frames per GPU per step (default: ResNet-50 320, YOLOv8-n 64, Whisper 16 "
+                         "streams).  ResNet-50's 320 is chosen for the chip's 256 CUs: stage 3 runs "
+                         "M = 320 x 196 = 62720 = 245 tiles of 256 rows (96 %% of the CUs busy in one "
+                         "round) where B=256 gives 196 tiles (77 %%); interleaved on MI355X 86.3-87.9k "
+                         "vs 83.7-84.4k frames/s at B=256 (scripts/batch_quant_ab.sh)")
     ap.add_argument("--height", type=int, default=224)
     ap.add_argument("--width", type=int, default=224)
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture")
@@ -178,10 +183,8 @@ def main(argv=None):
     explicit_hw = "--height" in (argv or sys.argv)
     if (a.parallel == "pp" or a.model == "yolov8n") and not explicit_hw:
         a.height, a.width = 480, 640          # configs 3/4 decode VGA video frames
-    if a.model == "yolov8n" and "--batch" not in (argv or sys.argv):
-        a.batch = 64
-    if a.model.startswith("whisper") and "--batch" not in (argv or sys.argv):
-        a.batch = 16
+    if a.batch is None:
+        a.batch = 64 if a.model == "yolov8n" else 16 if a.model.startswith("whisper") else 320
 
     procs = []
     if a.parallel == "pp":
