@@ -149,8 +149,10 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--batch", type=int, default=None,
-                    help="frames per GPU per step (default: ResNet-50 320, YOLOv8-n 64, Whisper 16 "
-                         "streams).  ResNet-50's 320 is chosen for the chip's 256 CUs: stage 3 runs "
+                    help="frames per GPU per step (default: ResNet-50 320, YOLOv8-n 64, Whisper 14 "
+                         "streams: 14 x 12 heads of query tiles is 1.97 rounds of the attention kernel's 512 "
+                         "resident workgroups where 16 streams was 2.25 — 2.94k-3.05k vs 2.87k-2.88k "
+                         "windows/s at a lower p50, scripts/batch_sweep_cfg45.sh).  ResNet-50's 320 is chosen for the chip's 256 CUs: stage 3 runs "
                          "M = 320 x 196 = 62720 = 245 tiles of 256 rows (96 %% of the CUs busy in one "
                          "round) where B=256 gives 196 tiles (77 %%); interleaved on MI355X 86.3-87.9k "
                          "vs 83.7-84.4k frames/s at B=256 (scripts/batch_quant_ab.sh)")
@@ -184,7 +186,7 @@ def main(argv=None):
     if (a.parallel == "pp" or a.model == "yolov8n") and not explicit_hw:
         a.height, a.width = 480, 640          # configs 3/4 decode VGA video frames
     if a.batch is None:
-        a.batch = 64 if a.model == "yolov8n" else 16 if a.model.startswith("whisper") else 320
+        a.batch = 64 if a.model == "yolov8n" else 14 if a.model.startswith("whisper") else 320
 
     procs = []
     if a.parallel == "pp":
