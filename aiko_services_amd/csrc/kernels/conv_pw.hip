@@ -1,0 +1,303 @@
+// Pointwise (1x1 / stride 1) convolution as a persistent, bandwidth-shaped GEMM (tuner variant 12).
+//
+//   y[m, n] = act(x[m, :] . w[n, :] + bias[n] (+ res[m, n]))      (residual before or after act)
+//
+// For the ResNet expansion convs with a residual (stage 3: M = B*196, K = 256, N = 1024; stage 4:
+// K = 512, N = 2048) every tiled kernel of conv_buf / conv_wide ran at 400-700 TFLOP/s and
+// 3.1-3.6 TB/s counting the residual: a tile is only 4-8 K blocks, so each workgroup pays one
+// L2/HBM round trip to fill its ring, a second for the residual, and drains everything during its
+// epilogue — the bytes in flight per CU, not HBM or the matrix pipe, set the pace.  Here:
+//   * one 512-thread workgroup per CU walks a column of output tiles: its channel block n0 is
+//     fixed (bias in registers, weights L2-resident), its 128-pixel row blocks step by the grid's
+//     group count; the ntn workgroups of one row block are adjacent logical ids, i.e. on the same
+//     XCD (xcd_remap), so each activation row block is fetched from HBM once into that XCD's L2;
+//   * ONE 4-slot ring of 64-deep K blocks streams across tile boundaries (K % 256 == 0, so block
+//     kb always uses slot kb % 4 and every slot address is an immediate): while a tile finishes
+//     its last blocks and runs its epilogue, the next tile's first three blocks are in flight;
+//   * the residual tile is DMA'd (buffer_load ... lds) into its own 32 KB LDS region at the
+//     tile's second K step, source-swizzled so the epilogue's 16-byte reads are conflict-free —
+//     no ordinary global loads are ever waited on while DMAs are in flight;
+//   * the product is transposed (weights on the MFMA A side) and one v_permlane16_swap per fp32
+//     pair gives each lane 8 consecutive channels of one pixel: bias, residual, activation and a
+//     16-byte store straight from registers (conv_wide.hip's epilogue), no LDS bounce;
+//   * every wait is a counted `s_waitcnt vmcnt(N)`, N = the DMA ops issued after the awaited
+//     one (loads retire in order, so the epilogue's stores can only make a wait stricter), and a
+//     raw s_barrier — never __syncthreads() with DMAs in flight.  The last tile waits vmcnt(0).
+// LDS: 4 x 32 KB ring + 32 KB residual = 160 KB, one workgroup per CU.
+//
+// Measured (MI355X, ResNet-50 at B=320, scripts/pw_check.sh, tuner medians): stage-3 expansion
+// M=62720 N=1024 K=256 + residual 77.9 us vs 80 us for the best tiled kernel (picked); stage-4
+// N=2048 K=512 53.8 vs 45.3 us, stage-3 reductions N=256 K=1024 42.4 vs 34 us (not picked).  So
+// the per-tile ring fill / residual round trip was not what held those layers at 3.6 TB/s: with
+// three 32 KB blocks in flight per CU across tile boundaries the kernel still spends ~5 us per
+// 128 x 128 tile (17 % MFMA, ~37 % LDS, 3.8 TB/s HBM).  Kept as a tuner candidate.
+#include "conv_common.h"
+
+namespace aiko {
+
+namespace {
+
+constexpr uint32_t kPwOOB = 0x80000000u;          // offsets >= num_records read as zero
+constexpr uint32_t kPwRecords = 0x7ffffff0u;
+constexpr int kPwBM = 128, kPwBN = 128, kPwBK = 64, kPwNS = 4;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pw_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)kPwRecords, 0x00020000);
+}
+
+__device__ __forceinline__ void pw_dma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, void* lds) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(
+      r, reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(lds)), 16,
+      voff, soff, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void pw_vm_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+struct PwParams {
+  const bf16_t* x;      // [M][ldx], K channels used
+  const bf16_t* w;      // [N][K]
+  const float* bias;    // [N] or nullptr
+  const bf16_t* res;    // [M][ldr] or nullptr
+  bf16_t* y;            // [M][ldy]
+  int M, N, K, ldx, ldy, ldr, act;
+  int ntn, mtiles, groups;
+};
+
+template <bool RES>
+__global__ __launch_bounds__(512, 1) void conv_pw_kernel(PwParams p) {
+  constexpr int BM = kPwBM, BN = kPwBN, BK = kPwBK, NS = kPwNS;
+  constexpr int WGN = 4, WM = 64, WN = 32, MI = WM / 16, NI = WN / 16;
+  constexpr int RPW = 8, RPI = 64;                // tile rows per wave / per workgroup DMA instruction
+  constexpr int APT = BM / RPI, BPT = BN / RPI, P = APT + BPT;
+  constexpr int NR = RES ? BM / 32 : 0;           // residual DMA instructions per thread
+  constexpr int STAGE = (BM + BN) * BK;           // elements per ring slot
+  constexpr int RES_ELEMS = BM * BN;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[NS * STAGE + RES_ELEMS];
+  bf16_t* const resb = lds + NS * STAGE;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WGN, wc = wave % WGN;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile_n = lid % p.ntn, group = lid / p.ntn;
+  if (group >= p.groups) return;                   // (host sizes the grid to ntn * groups)
+  const int n0 = tile_n * BN;
+  const int ntiles = group < p.mtiles ? (p.mtiles - 1 - group) / p.groups + 1 : 0;
+  if (ntiles == 0) return;
+  const int nkb = p.K / BK;                        // multiple of NS (host)
+
+  const __amdgpu_buffer_rsrc_t rx = pw_rsrc(p.x);
+  const __amdgpu_buffer_rsrc_t rw = pw_rsrc(p.w);
+  const __amdgpu_buffer_rsrc_t rr = pw_rsrc(RES ? p.res : p.x);
+
+  const int lrow = wave * RPW + (lane >> 3);
+  const int lp = (lane & 7) ^ (lane >> 3);        // source-side swizzle of the 128-B rows
+  uint32_t b_off[BPT];
+#pragma unroll
+  for (int i = 0; i < BPT; ++i) b_off[i] = (uint32_t)(((n0 + lrow + RPI * i) * p.K + lp * 8) * 2);
+  // residual DMA: 16 pieces (256 B) per tile row, 4 rows per wave instruction; the piece a lane
+  // writes at LDS position lane & 15 of row rrow is logical piece (lane & 15) ^ (rrow & 15)
+  const int rrow0 = wave * 4 + (lane >> 4);
+  const int rpiece = (lane & 15) ^ (rrow0 & 15);   // (rrow0 + 32 r) & 15 == rrow0 & 15
+
+  // ---- bias for the fixed channel block, consumed before any DMA is in flight ----
+  const int fr = lane & 15, fq = lane >> 4;
+  const int coff = ((fq & 1) << 4) | ((fq >> 1) << 3);
+  const int nl = wc * WN + coff;                   // tile-local first channel of this lane's 8
+  float e_bias[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) e_bias[e] = 0.f;
+  if (p.bias) {
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(p.bias + n0 + nl);
+    const f32x4 b1 = *reinterpret_cast<const f32x4*>(p.bias + n0 + nl + 4);
+    e_bias[0] = b0[0]; e_bias[1] = b0[1]; e_bias[2] = b0[2]; e_bias[3] = b0[3];
+    e_bias[4] = b1[0]; e_bias[5] = b1[1]; e_bias[6] = b1[2]; e_bias[7] = b1[3];
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) asm volatile("" ::"v"(e_bias[e]));   // retire the loads here
+
+  auto issue = [&](int f, auto slot_tag) {         // flat K block f = tile * nkb + kb
+    constexpr int SLOT = decltype(slot_tag)::value;
+    const int t = f / nkb, kb = f - t * nkb;
+    if (t >= ntiles) return;
+    const int m0 = (group + t * p.groups) * BM;
+    bf16_t* Xs = lds + SLOT * STAGE;
+    bf16_t* Ws = Xs + BM * BK;
+    const uint32_t sb = (uint32_t)(kb * BK * 2);
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) pw_dma16(rw, b_off[i], sb, Ws + (i * RPI + wave * RPW) * BK);
+#pragma unroll
+    for (int i = 0; i < APT; ++i) {
+      const int m = m0 + lrow + RPI * i;
+      const uint32_t off = m < p.M ? (uint32_t)((m * p.ldx + lp * 8) * 2) : kPwOOB;
+      pw_dma16(rx, off, sb, Xs + (i * RPI + wave * RPW) * BK);
+    }
+  };
+  auto issue_res = [&](int t) {
+    const int m0 = (group + t * p.groups) * BM;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int m = m0 + rrow0 + 32 * r;
+      const uint32_t off = m < p.M ? (uint32_t)((m * p.ldr + n0 + rpiece * 8) * 2) : kPwOOB;
+      pw_dma16(rr, off, 0u, resb + (r * 32 + wave * 4) * BN);
+    }
+  };
+
+  const int sw = fr & 7;
+  int w_rd[NI], x_rd[MI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) w_rd[j] = BM * BK + (wc * WN + j * 16 + fr) * BK;
+#pragma unroll
+  for (int i = 0; i < MI; ++i) x_rd[i] = (wr * WM + i * 16 + fr) * BK;
+
+  f32x4 acc[NI][MI];
+  auto compute = [&](auto slot_tag) {
+    constexpr int SLOT = decltype(slot_tag)::value;
+    const bf16_t* St = lds + SLOT * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int pc = ((fq + 4 * kk) ^ sw) << 3;
+      bf16x8 wf[NI], xf[MI];
+#pragma unroll
+      for (int j = 0; j < NI; ++j) wf[j] = *reinterpret_cast<const bf16x8*>(St + w_rd[j] + pc);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) xf[i] = *reinterpret_cast<const bf16x8*>(St + x_rd[i] + pc);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
+    }
+  };
+
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  using S2 = std::integral_constant<int, 2>;
+  using S3 = std::integral_constant<int, 3>;
+  issue(0, S0{});
+  issue(1, S1{});
+  issue(2, S2{});
+
+  const bool post = (p.act & 16) != 0;
+  const int act = p.act & 15;
+  for (int t = 0; t < ntiles; ++t) {
+    const bool last = t + 1 == ntiles;
+    const int m0 = (group + t * p.groups) * BM;
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int i = 0; i < MI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kq = 0; kq < nkb; kq += NS) {
+      const int f = t * nkb + kq;
+      // block f + s: younger DMA ops = the next two blocks (+ this tile's residual, issued at
+      // step 1 before block f + 4, while it is outstanding behind blocks (t, 2) and (t, 3))
+      if (last && kq + NS >= nkb) pw_vm_barrier<0>(); else pw_vm_barrier<2 * P>();
+      issue(f + 3, S3{});
+      compute(S0{});
+      if (last && kq + NS >= nkb) pw_vm_barrier<0>(); else pw_vm_barrier<2 * P>();
+      if (RES && kq == 0) issue_res(t);
+      issue(f + 4, S0{});
+      compute(S1{});
+      if (last && kq + NS >= nkb) pw_vm_barrier<0>();
+      else if (RES && kq == 0) pw_vm_barrier<2 * P + NR>();
+      else pw_vm_barrier<2 * P>();
+      issue(f + 5, S1{});
+      compute(S2{});
+      if (last && kq + NS >= nkb) pw_vm_barrier<0>();
+      else if (RES && kq == 0) pw_vm_barrier<2 * P + NR>();
+      else pw_vm_barrier<2 * P>();
+      issue(f + 6, S2{});
+      compute(S3{});
+    }
+    // residual landed (younger: the nkb - 1 blocks issued since) and visible to every wave
+    if (RES) {
+      if (last) pw_vm_barrier<0>();
+      else if (nkb == 4) pw_vm_barrier<3 * P>();
+      else pw_vm_barrier<0>();
+    }
+
+    // ---- register-direct epilogue ----
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int ml = wr * WM + i * 16 + fr;
+      const int m = m0 + ml;
+      f32x4 lo = acc[0][i], hi = acc[1][i];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(lo[e]), __float_as_uint(hi[e]), false, false);
+        lo[e] = __uint_as_float(s[0]);
+        hi[e] = __uint_as_float(s[1]);
+      }
+      u32x4 r = {0u, 0u, 0u, 0u};
+      if constexpr (RES) r = *reinterpret_cast<const u32x4*>(resb + ml * BN + (((nl >> 3) ^ fr) << 3));
+      if (m >= p.M) continue;
+      float v[8] = {lo[0] + e_bias[0], lo[1] + e_bias[1], lo[2] + e_bias[2], lo[3] + e_bias[3],
+                    hi[0] + e_bias[4], hi[1] + e_bias[5], hi[2] + e_bias[6], hi[3] + e_bias[7]};
+      if (RES && !post) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[2 * e] += __uint_as_float(r[e] << 16);
+          v[2 * e + 1] += __uint_as_float(r[e] & 0xffff0000u);
+        }
+      }
+      if (act == 1) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      } else if (act == 2) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = silu(v[e]);
+      } else if (act == 3) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+      }
+      if (RES && post) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[2 * e] += __uint_as_float(r[e] << 16);
+          v[2 * e + 1] += __uint_as_float(r[e] & 0xffff0000u);
+        }
+      }
+      u32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = pack2(v[2 * e], v[2 * e + 1]);
+      *reinterpret_cast<u32x4*>(p.y + (size_t)m * p.ldy + n0 + nl) = o;
+    }
+  }
+}
+
+}  // namespace
+
+}  // namespace aiko
+
+// 1x1 / stride-1 conv over x [M][ldx] (first K channels): K % 256 == 0, N % 128 == 0, ldx / ldy /
+// ldr multiples of 8, 16-byte aligned operands, every operand < 2^31 bytes (host checks).
+// ``cus``: compute units to size the persistent grid for.
+extern "C" int aiko_conv_pw(const void* x, const void* w, const float* bias, const void* res, void* y, int M,
+                            int N, int K, int ldx, int ldy, int ldr, int act, int cus, hipStream_t stream) {
+  using namespace aiko;
+  if (K % (kPwBK * kPwNS) || N % kPwBN || M <= 0 || ldx % 8 || ldy % 8 || (res && ldr % 8) || ldx < K)
+    return -1;
+  PwParams p;
+  p.x = static_cast<const bf16_t*>(x);
+  p.w = static_cast<const bf16_t*>(w);
+  p.bias = bias;
+  p.res = static_cast<const bf16_t*>(res);
+  p.y = static_cast<bf16_t*>(y);
+  p.M = M; p.N = N; p.K = K; p.ldx = ldx; p.ldy = ldy; p.ldr = ldr; p.act = act;
+  p.ntn = N / kPwBN;
+  p.mtiles = (M + kPwBM - 1) / kPwBM;
+  int groups = (cus > 0 ? cus : 256) / p.ntn;
+  if (groups < 1) groups = 1;
+  if (groups > p.mtiles) groups = p.mtiles;
+  p.groups = groups;
+  const dim3 grid((unsigned)(groups * p.ntn));
+  if (res)
+    conv_pw_kernel<true><<<grid, 512, 0, stream>>>(p);
+  else
+    conv_pw_kernel<false><<<grid, 512, 0, stream>>>(p);
+  return (int)hipGetLastError();
+}

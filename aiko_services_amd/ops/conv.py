@@ -268,6 +268,9 @@ WIDE_OCC_TILES = ((128, 128), (256, 64), (128, 64), (64, 128), (64, 64))
 # Measured on the ResNet-50 layers (MI355X, round 3): never the tuner's pick against variant 8,
 # i.e. the 2-slot 64-deep ring is not what limits those tiles; kept as a candidate
 WIDE_DEEP_TILES = ((256, 256), (256, 128), (128, 256))
+# variant 12 (conv_pw.hip): persistent pointwise GEMM for 1x1/s1 convs with K % 256 == 0 — one
+# 4-slot K-block ring across tile boundaries, residual DMA'd into LDS, fixed channel block per
+# workgroup; 77.9 vs 80 us on the stage-3 expansion at B=320 (the tuner's pick there)
 
 
 def buf_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = None) -> bool:
@@ -311,6 +314,15 @@ def patch_weight(spec: ConvSpec) -> torch.Tensor:
     return img
 
 
+def pw_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = None) -> bool:
+    """Whether the persistent pointwise kernel (variant 12, conv_pw.hip) applies: a 1x1 / stride 1
+    single-source conv with K % 256 == 0 (4-slot ring of 64-deep K blocks), Cout % 128 == 0 and
+    16-byte aligned pixel rows."""
+    return (spec.kind != "stem" and x2 is None and spec.K1 is None and spec.R == 1 and spec.S == 1
+            and spec.stride == 1 and spec.pad == 0 and spec.Cc == spec.K and spec.K % 256 == 0
+            and spec.cout % 128 == 0 and x.stride(2) % 8 == 0)
+
+
 def narrow_variant_ok(spec: ConvSpec, x2: torch.Tensor | None = None) -> bool:
     """Whether the direct narrow-layer kernel (variant 7, conv_narrow.hip) applies: a 3x3 / pad 1
     / stride 1-2 or 1x1 / stride 1 conv with 16 or 32 input and output channels, no second source."""
@@ -320,7 +332,7 @@ def narrow_variant_ok(spec: ConvSpec, x2: torch.Tensor | None = None) -> bool:
             and spec.Cc in (16, 32) and spec.cout in (16, 32))
 
 
-def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False):
+def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, pw_ok=False):
     if cout <= 32:
         cands = [t + (0,) for t in NARROW_TILES]
         if narrow_ok:
@@ -339,6 +351,8 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False):
             cands += [t + (11,) for t in WIDE_DEEP_TILES]
         if patch_ok:
             cands.append((8, 64, 10))        # variant 10: tile fixed by the kernel (8 rows x W)
+        if pw_ok:
+            cands.append((128, 128, 12))     # variant 12: persistent pointwise GEMM (conv_pw.hip)
     skip = {int(v) for v in __import__("os").environ.get("AIKO_CONV_SKIP", "").split(",") if v.strip()}
     if skip:                                   # A/B runs: exclude variants from the tuner
         cands = [t for t in cands if (t[2] if len(t) > 2 else 0) not in skip] or cands
@@ -436,7 +450,8 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None
         if tile is None:
             if _tuning:
                 tile = _tune(key, M, spec.cout, launch, buf_variant_ok(spec, x, x2), narrow_variant_ok(spec, x2),
-                             patch_variant_ok(spec, x, residual, x2, out) and not residual_after_act)
+                             patch_variant_ok(spec, x, residual, x2, out) and not residual_after_act,
+                             pw_variant_ok(spec, x, x2))
             else:
                 tile = pick_tile(M, spec.cout)
     launch(tile)

@@ -118,6 +118,15 @@ def _nhwc(x_nchw):
     (2, 7, 7, 512, 512, 3, 1, 1, "relu", False, (128, 256, 11)),
     (1, 9, 11, 128, 200, 3, 1, 1, "silu", True, (256, 128, 11)),
     (2, 30, 30, 64, 64, 3, 1, 1, "relu", True, (128, 256, 11)),
+    # variant 12: persistent pointwise GEMM (1x1 / s1, K % 256 == 0, Cout % 128 == 0) — M tails,
+    # several tiles per workgroup (B=64), K = 512 (8 blocks per tile), no residual, one column
+    (3, 14, 14, 256, 1024, 1, 1, 0, None, True, (128, 128, 12)),
+    (2, 14, 14, 256, 1024, 1, 1, 0, "relu", True, (128, 128, 12)),
+    (64, 14, 14, 256, 1024, 1, 1, 0, "relu", True, (128, 128, 12)),
+    (1, 7, 7, 512, 2048, 1, 1, 0, "relu", True, (128, 128, 12)),
+    (64, 7, 7, 512, 2048, 1, 1, 0, "relu", True, (128, 128, 12)),
+    (2, 28, 28, 256, 128, 1, 1, 0, "relu", False, (128, 128, 12)),
+    (40, 14, 14, 256, 512, 1, 1, 0, "gelu", True, (128, 128, 12)),
 ])
 def test_conv_igemm_matches_torch(native, B, H, W, cin, cout, k, stride, pad, act, res, tile):
     from aiko_services_amd.ops import conv as C
