@@ -27,7 +27,7 @@ int aiko_conv_wide(const void* x, const void* w, const float* bias, const void* 
                    int M, int Cout, int K, int act, int ldy, int ldr, int bm, int bn, const void* x2,
                    int K1, int H2, int W2, int C2, int stride2, int occ, hipStream_t stream);
 int aiko_conv_pw(const void* x, const void* w, const float* bias, const void* res, void* y, int M, int N,
-                 int K, int ldx, int ldy, int ldr, int act, int cus, hipStream_t stream);
+                 int K, int ldx, int ldy, int ldr, int act, int cus, int mode, hipStream_t stream);
 int aiko_conv_persist(const void* x, const void* w, const float* bias, const void* res, void* y,
                       int H, int W, int C, int Cc, int R, int S, int stride, int pad, int Ho, int Wo,
                       int M, int Cout, int K, int act, int ldy, int ldr, int bm, int bn, const void* x2,
@@ -214,11 +214,11 @@ void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, co
     rc = aiko_conv_wide(x.data_ptr(), w.data_ptr(), bptr, rptr, y.data_ptr(), H, W, C, Cc, R, S, stride,
                         pad, Ho, Wo, M, Cout, K, act, ldy, ldr, bm, bn, x2ptr, K1, H2, W2, C2, stride2,
                         variant == 11 ? 11 : (variant == 9 ? 2 : 1), cur_stream());
-  } else if (variant == 12) {
+  } else if (variant == 12 || variant == 13) {
     // persistent pointwise GEMM (conv_pw.hip): 1x1 / stride 1 / one source, K % 256 == 0,
     // Cout % 128 == 0, x rows = pixels at pitch C
     TORCH_CHECK(!dual && R == 1 && S == 1 && stride == 1 && pad == 0 && Cc == K && K % 256 == 0 &&
-                    Cout % 128 == 0 && C % 8 == 0 && x_extent * 2 < (1LL << 31) - 64 && w.numel() * 2 < (1LL << 31) &&
+                    Cout % 128 == 0 && C % 8 == 0 && (variant == 12 || K == 256) && x_extent * 2 < (1LL << 31) - 64 && w.numel() * 2 < (1LL << 31) &&
                     avail_elems(y) * 2 < (1LL << 31),
                 "aiko.conv_igemm_out: variant 12 needs a 1x1/s1 single-source conv with K % 256 == 0, "
                 "Cout % 128 == 0 and operands < 2 GiB");
@@ -234,7 +234,7 @@ void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, co
       cus = n;
     }
     rc = aiko_conv_pw(x.data_ptr(), w.data_ptr(), bptr, rptr, y.data_ptr(), M, Cout, K, C, ldy, ldr, act, cus,
-                      cur_stream());
+                      variant == 13 ? 1 : 0, cur_stream());
   } else if (variant == 4) {
     // persistent buffer-LDS-DMA kernel: one K-block stream across each workgroup's run of tiles
     TORCH_CHECK(Cc % 64 == 0 && R * S <= 32 && K % 64 == 0 && x_extent * 2 < (1LL << 31) - 64 &&

@@ -269,18 +269,227 @@ __global__ __launch_bounds__(512, 1) void conv_pw_kernel(PwParams p) {
   }
 }
 
+// ---- resident-weight variant (tuner variant 13): K == 256 only ----
+//
+// conv_pw_kernel keeps three 32 KB blocks in flight per CU: ~1 us of MFMA work to cover a ~2 us
+// L2 / HBM round trip, so every K step stalls.  With the workgroup's channel block fixed, its
+// 128 x 256 weight block (64 KB) is loaded into LDS once; the ring then carries only activation
+// blocks of a 64-pixel tile (8 KB each) and 8 slots fit beside the weights and a 16 KB residual
+// tile (144 KB): seven blocks in flight, the lookahead in time doubled at a quarter of the bytes
+// per block.  Slots cycle every two tiles (block kb of tile t uses slot 4 (t & 1) + kb), so the
+// tile loop is unrolled by two and every slot address is an immediate.
+// Measured (MI355X, B=320, scripts/pw_check.sh): stage-3 expansion M=62720 N=1024 K=256 + residual
+// 65.6 us (500 TF, 4.4 TB/s with the residual) against 77.9 us for conv_pw_kernel and 80 us for the
+// best tiled kernel — the longer lookahead, not the ring restart, was the lever.
+template <bool RES>
+__global__ __launch_bounds__(512, 1) void conv_pw_rb_kernel(PwParams p) {
+  constexpr int BM = 64, BN = 128, BK = 64, NS = 8, KW = 256;
+  constexpr int WGN = 4, WM = 32, WN = 32, MI = WM / 16, NI = WN / 16;
+  constexpr int NR = RES ? 2 : 0;                 // residual DMA instructions per thread
+  constexpr int SLOT = BM * BK;                   // elements per ring slot (8 KB)
+  constexpr int W_ELEMS = BN * KW;                // resident weights (64 KB)
+  __shared__ __attribute__((aligned(16))) bf16_t lds[W_ELEMS + NS * SLOT + BM * BN];
+  bf16_t* const wres = lds;
+  bf16_t* const ring = lds + W_ELEMS;
+  bf16_t* const resb = ring + NS * SLOT;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WGN, wc = wave % WGN;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile_n = lid % p.ntn, group = lid / p.ntn;
+  if (group >= p.groups) return;
+  const int n0 = tile_n * BN;
+  const int ntiles = group < p.mtiles ? (p.mtiles - 1 - group) / p.groups + 1 : 0;
+  if (ntiles == 0) return;
+
+  const __amdgpu_buffer_rsrc_t rx = pw_rsrc(p.x);
+  const __amdgpu_buffer_rsrc_t rw = pw_rsrc(p.w);
+  const __amdgpu_buffer_rsrc_t rr = pw_rsrc(RES ? p.res : p.x);
+
+  const int fr = lane & 15, fq = lane >> 4;
+  const int coff = ((fq & 1) << 4) | ((fq >> 1) << 3);
+  const int nl = wc * WN + coff;
+  float e_bias[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) e_bias[e] = 0.f;
+  if (p.bias) {
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(p.bias + n0 + nl);
+    const f32x4 b1 = *reinterpret_cast<const f32x4*>(p.bias + n0 + nl + 4);
+    e_bias[0] = b0[0]; e_bias[1] = b0[1]; e_bias[2] = b0[2]; e_bias[3] = b0[3];
+    e_bias[4] = b1[0]; e_bias[5] = b1[1]; e_bias[6] = b1[2]; e_bias[7] = b1[3];
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) asm volatile("" ::"v"(e_bias[e]));
+
+  // resident weights: 32 16-B pieces per 512-B row, two rows per wave instruction; LDS position
+  // pos of row n holds logical piece (pos & ~7) | ((pos & 7) ^ (n & 7))
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = (i * 8 + wave) * 2 + (lane >> 5);
+    const int pos = lane & 31;
+    const int lpc = (pos & ~7) | ((pos & 7) ^ (row & 7));
+    pw_dma16(rw, (uint32_t)(((n0 + row) * KW + lpc * 8) * 2), 0u, wres + (i * 8 + wave) * 2 * KW);
+  }
+
+  const int lrow = wave * 8 + (lane >> 3);         // activation DMA: 8 rows per wave, 64 per block
+  const int lp = (lane & 7) ^ (lane >> 3);
+  const int rrow0 = wave * 4 + (lane >> 4);
+  const int rpiece = (lane & 15) ^ (rrow0 & 15);
+
+  auto issue = [&](int f, auto slot_tag) {
+    constexpr int S = decltype(slot_tag)::value;
+    const int t = f >> 2, kb = f & 3;
+    if (t >= ntiles) return;
+    const int m = (group + t * p.groups) * BM + lrow;
+    const uint32_t off = m < p.M ? (uint32_t)((m * p.ldx + lp * 8) * 2) : kPwOOB;
+    pw_dma16(rx, off, (uint32_t)(kb * BK * 2), ring + S * SLOT + wave * 8 * BK);
+  };
+  auto issue_res = [&](int t) {
+    const int m0 = (group + t * p.groups) * BM;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int m = m0 + rrow0 + 32 * r;
+      const uint32_t off = m < p.M ? (uint32_t)((m * p.ldr + n0 + rpiece * 8) * 2) : kPwOOB;
+      pw_dma16(rr, off, 0u, resb + (r * 32 + wave * 4) * BN);
+    }
+  };
+
+  const int sw = fr & 7;
+  int w_rd[NI], x_rd[MI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) w_rd[j] = (wc * WN + j * 16 + fr) * KW;
+#pragma unroll
+  for (int i = 0; i < MI; ++i) x_rd[i] = (wr * WM + i * 16 + fr) * BK;
+
+  f32x4 acc[NI][MI];
+  auto compute = [&](auto slot_tag, auto kb_tag) {
+    constexpr int S = decltype(slot_tag)::value, KB = decltype(kb_tag)::value;
+    const bf16_t* Xs = ring + S * SLOT;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int pc = ((fq + 4 * kk) ^ sw) << 3;
+      bf16x8 wf[NI], xf[MI];
+#pragma unroll
+      for (int j = 0; j < NI; ++j) wf[j] = *reinterpret_cast<const bf16x8*>(wres + w_rd[j] + KB * 64 + pc);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) xf[i] = *reinterpret_cast<const bf16x8*>(Xs + x_rd[i] + pc);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
+    }
+  };
+
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  using I4 = std::integral_constant<int, 4>;
+  using I5 = std::integral_constant<int, 5>;
+  using I6 = std::integral_constant<int, 6>;
+  using I7 = std::integral_constant<int, 7>;
+  issue(0, I0{}); issue(1, I1{}); issue(2, I2{}); issue(3, I3{});
+  issue(4, I4{}); issue(5, I5{}); issue(6, I6{});
+
+  const bool post = (p.act & 16) != 0;
+  const int act = p.act & 15;
+  // one tile: H = slot half (tile parity).  Waits: block f has the six next blocks younger, plus
+  // this tile's residual (issued at step 0, before block f + 7) for steps 1-3; the last two
+  // tiles of the walk (fewer blocks issued behind them) wait for everything.
+  auto tile = [&](int t, auto half_tag) {
+    constexpr int H = decltype(half_tag)::value;
+    const bool tail = t + 2 >= ntiles;
+    const int f = 4 * t;
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int i = 0; i < MI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (tail) pw_vm_barrier<0>(); else pw_vm_barrier<6>();
+    if (RES) issue_res(t);
+    issue(f + 7, std::integral_constant<int, (4 * H + 7) % 8>{});
+    compute(std::integral_constant<int, 4 * H + 0>{}, I0{});
+    if (tail) pw_vm_barrier<0>(); else pw_vm_barrier<6 + NR>();
+    issue(f + 8, std::integral_constant<int, (4 * H + 8) % 8>{});
+    compute(std::integral_constant<int, 4 * H + 1>{}, I1{});
+    if (tail) pw_vm_barrier<0>(); else pw_vm_barrier<6 + NR>();
+    issue(f + 9, std::integral_constant<int, (4 * H + 9) % 8>{});
+    compute(std::integral_constant<int, 4 * H + 2>{}, I2{});
+    if (tail) pw_vm_barrier<0>(); else pw_vm_barrier<6 + NR>();
+    issue(f + 10, std::integral_constant<int, (4 * H + 10) % 8>{});
+    compute(std::integral_constant<int, 4 * H + 3>{}, I3{});
+    if (RES) {                                     // residual: younger = the 4 blocks issued since
+      if (tail) pw_vm_barrier<0>(); else pw_vm_barrier<4>();
+    }
+    const int m0 = (group + t * p.groups) * BM;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int ml = wr * WM + i * 16 + fr;
+      const int m = m0 + ml;
+      f32x4 lo = acc[0][i], hi = acc[1][i];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(lo[e]), __float_as_uint(hi[e]), false, false);
+        lo[e] = __uint_as_float(s[0]);
+        hi[e] = __uint_as_float(s[1]);
+      }
+      u32x4 r = {0u, 0u, 0u, 0u};
+      if constexpr (RES) r = *reinterpret_cast<const u32x4*>(resb + ml * BN + (((nl >> 3) ^ fr) << 3));
+      if (m >= p.M) continue;
+      float v[8] = {lo[0] + e_bias[0], lo[1] + e_bias[1], lo[2] + e_bias[2], lo[3] + e_bias[3],
+                    hi[0] + e_bias[4], hi[1] + e_bias[5], hi[2] + e_bias[6], hi[3] + e_bias[7]};
+      if (RES && !post) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[2 * e] += __uint_as_float(r[e] << 16);
+          v[2 * e + 1] += __uint_as_float(r[e] & 0xffff0000u);
+        }
+      }
+      if (act == 1) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      } else if (act == 2) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = silu(v[e]);
+      } else if (act == 3) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+      }
+      if (RES && post) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[2 * e] += __uint_as_float(r[e] << 16);
+          v[2 * e + 1] += __uint_as_float(r[e] & 0xffff0000u);
+        }
+      }
+      u32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = pack2(v[2 * e], v[2 * e + 1]);
+      *reinterpret_cast<u32x4*>(p.y + (size_t)m * p.ldy + n0 + nl) = o;
+    }
+  };
+  for (int t = 0; t < ntiles; t += 2) {
+    tile(t, I0{});
+    if (t + 1 < ntiles) tile(t + 1, I1{});
+  }
+}
+
 }  // namespace
 
 }  // namespace aiko
 
 // 1x1 / stride-1 conv over x [M][ldx] (first K channels): K % 256 == 0, N % 128 == 0, ldx / ldy /
 // ldr multiples of 8, 16-byte aligned operands, every operand < 2^31 bytes (host checks).
-// ``cus``: compute units to size the persistent grid for.
+// ``cus``: compute units to size the persistent grid for; ``mode`` 1: resident-weight kernel (K == 256).
 extern "C" int aiko_conv_pw(const void* x, const void* w, const float* bias, const void* res, void* y, int M,
-                            int N, int K, int ldx, int ldy, int ldr, int act, int cus, hipStream_t stream) {
+                            int N, int K, int ldx, int ldy, int ldr, int act, int cus, int mode,
+                            hipStream_t stream) {
   using namespace aiko;
   if (K % (kPwBK * kPwNS) || N % kPwBN || M <= 0 || ldx % 8 || ldy % 8 || (res && ldr % 8) || ldx < K)
     return -1;
+  if (mode == 1 && K != 256) return -1;      // resident weights: one 128 x 256 block per workgroup
   PwParams p;
   p.x = static_cast<const bf16_t*>(x);
   p.w = static_cast<const bf16_t*>(w);
@@ -289,15 +498,22 @@ extern "C" int aiko_conv_pw(const void* x, const void* w, const float* bias, con
   p.y = static_cast<bf16_t*>(y);
   p.M = M; p.N = N; p.K = K; p.ldx = ldx; p.ldy = ldy; p.ldr = ldr; p.act = act;
   p.ntn = N / kPwBN;
-  p.mtiles = (M + kPwBM - 1) / kPwBM;
+  const int bm = mode == 1 ? 64 : kPwBM;
+  p.mtiles = (M + bm - 1) / bm;
   int groups = (cus > 0 ? cus : 256) / p.ntn;
   if (groups < 1) groups = 1;
   if (groups > p.mtiles) groups = p.mtiles;
   p.groups = groups;
   const dim3 grid((unsigned)(groups * p.ntn));
-  if (res)
+  if (mode == 1) {
+    if (res)
+      conv_pw_rb_kernel<true><<<grid, 512, 0, stream>>>(p);
+    else
+      conv_pw_rb_kernel<false><<<grid, 512, 0, stream>>>(p);
+  } else if (res) {
     conv_pw_kernel<true><<<grid, 512, 0, stream>>>(p);
-  else
+  } else {
     conv_pw_kernel<false><<<grid, 512, 0, stream>>>(p);
+  }
   return (int)hipGetLastError();
 }

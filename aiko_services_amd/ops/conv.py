@@ -270,7 +270,9 @@ WIDE_OCC_TILES = ((128, 128), (256, 64), (128, 64), (64, 128), (64, 64))
 WIDE_DEEP_TILES = ((256, 256), (256, 128), (128, 256))
 # variant 12 (conv_pw.hip): persistent pointwise GEMM for 1x1/s1 convs with K % 256 == 0 — one
 # 4-slot K-block ring across tile boundaries, residual DMA'd into LDS, fixed channel block per
-# workgroup; 77.9 vs 80 us on the stage-3 expansion at B=320 (the tuner's pick there)
+# workgroup; 77.9 vs 80 us on the stage-3 expansion at B=320.  Variant 13 (K == 256): the
+# workgroup's 128 x 256 weight block resident in LDS, 64-pixel tiles through an 8-slot ring (seven
+# blocks in flight): 65.6 us there (the tuner's pick; 500 TF, 4.4 TB/s counting the residual)
 
 
 def buf_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = None) -> bool:
@@ -320,7 +322,7 @@ def pw_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = Non
     16-byte aligned pixel rows."""
     return (spec.kind != "stem" and x2 is None and spec.K1 is None and spec.R == 1 and spec.S == 1
             and spec.stride == 1 and spec.pad == 0 and spec.Cc == spec.K and spec.K % 256 == 0
-            and spec.cout % 128 == 0 and x.stride(2) % 8 == 0)
+            and spec.cout % 128 == 0 and x.stride(2) % 8 == 0) and ("k256" if spec.K == 256 else True)
 
 
 def narrow_variant_ok(spec: ConvSpec, x2: torch.Tensor | None = None) -> bool:
@@ -353,6 +355,8 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, p
             cands.append((8, 64, 10))        # variant 10: tile fixed by the kernel (8 rows x W)
         if pw_ok:
             cands.append((128, 128, 12))     # variant 12: persistent pointwise GEMM (conv_pw.hip)
+            if pw_ok == "k256":
+                cands.append((64, 128, 13))  # variant 13: the same with the weight block resident in LDS
     skip = {int(v) for v in __import__("os").environ.get("AIKO_CONV_SKIP", "").split(",") if v.strip()}
     if skip:                                   # A/B runs: exclude variants from the tuner
         cands = [t for t in cands if (t[2] if len(t) > 2 else 0) not in skip] or cands

@@ -127,6 +127,13 @@ def _nhwc(x_nchw):
     (64, 7, 7, 512, 2048, 1, 1, 0, "relu", True, (128, 128, 12)),
     (2, 28, 28, 256, 128, 1, 1, 0, "relu", False, (128, 128, 12)),
     (40, 14, 14, 256, 512, 1, 1, 0, "gelu", True, (128, 128, 12)),
+    # variant 13: resident 128 x 256 weight block, 64-pixel tiles, 8-slot ring (K == 256 only):
+    # M tails, many tiles per workgroup (odd and even counts), no residual, one channel column
+    (3, 14, 14, 256, 1024, 1, 1, 0, None, True, (64, 128, 13)),
+    (64, 14, 14, 256, 1024, 1, 1, 0, "relu", True, (64, 128, 13)),
+    (65, 14, 14, 256, 1024, 1, 1, 0, "relu", True, (64, 128, 13)),
+    (2, 28, 28, 256, 128, 1, 1, 0, "relu", False, (64, 128, 13)),
+    (40, 14, 14, 256, 512, 1, 1, 0, "gelu", True, (64, 128, 13)),
 ])
 def test_conv_igemm_matches_torch(native, B, H, W, cin, cout, k, stride, pad, act, res, tile):
     from aiko_services_amd.ops import conv as C
