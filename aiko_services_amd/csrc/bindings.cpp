@@ -218,7 +218,7 @@ void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, co
     // persistent pointwise GEMM (conv_pw.hip): 1x1 / stride 1 / one source, K % 256 == 0,
     // Cout % 128 == 0, x rows = pixels at pitch C
     TORCH_CHECK(!dual && R == 1 && S == 1 && stride == 1 && pad == 0 && Cc == K && K % 256 == 0 &&
-                    Cout % 128 == 0 && C % 8 == 0 && (variant == 12 || K == 256) && x_extent * 2 < (1LL << 31) - 64 && w.numel() * 2 < (1LL << 31) &&
+                    Cout % 128 == 0 && C % 8 == 0 && (variant == 12 || K == 256 || K == 512) && x_extent * 2 < (1LL << 31) - 64 && w.numel() * 2 < (1LL << 31) &&
                     avail_elems(y) * 2 < (1LL << 31),
                 "aiko.conv_igemm_out: variant 12 needs a 1x1/s1 single-source conv with K % 256 == 0, "
                 "Cout % 128 == 0 and operands < 2 GiB");

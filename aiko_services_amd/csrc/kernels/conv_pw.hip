@@ -269,7 +269,7 @@ __global__ __launch_bounds__(512, 1) void conv_pw_kernel(PwParams p) {
   }
 }
 
-// ---- resident-weight variant (tuner variant 13): K == 256 only ----
+// ---- resident-weight variant (tuner variant 13): K == 256 or 512 ----
 //
 // conv_pw_kernel keeps three 32 KB blocks in flight per CU: ~1 us of MFMA work to cover a ~2 us
 // L2 / HBM round trip, so every K step stalls.  With the workgroup's channel block fixed, its
@@ -280,12 +280,23 @@ __global__ __launch_bounds__(512, 1) void conv_pw_kernel(PwParams p) {
 // tile loop is unrolled by two and every slot address is an immediate.
 // Measured (MI355X, B=320, scripts/pw_check.sh): stage-3 expansion M=62720 N=1024 K=256 + residual
 // 65.6 us (500 TF, 4.4 TB/s with the residual) against 77.9 us for conv_pw_kernel and 80 us for the
-// best tiled kernel — the longer lookahead, not the ring restart, was the lever.
-template <bool RES>
+// best tiled kernel — the longer lookahead, not the ring restart, was the lever.  The K = 512 form
+// (64-channel blocks, half the FLOPs per activation byte, so half the lookahead in time) measured
+// slower than the tiled kernels on every ResNet layer it applies to (512 -> 128: 75 vs 62 us,
+// 512 -> 256: 154 vs 97, stage-4 expansion 82 vs 47) — a tuner candidate the tuner does not pick.
+// KW = 512 (stage-4 expansions, 512 -> 256/128 reductions): a 64 x 512 weight block (BN = 64),
+// one tile per ring cycle (block kb in slot kb), 4 x 2 waves of 16 x 32.
+template <bool RES, int KW>
 __global__ __launch_bounds__(512, 1) void conv_pw_rb_kernel(PwParams p) {
-  constexpr int BM = 64, BN = 128, BK = 64, NS = 8, KW = 256;
-  constexpr int WGN = 4, WM = 32, WN = 32, MI = WM / 16, NI = WN / 16;
-  constexpr int NR = RES ? 2 : 0;                 // residual DMA instructions per thread
+  static_assert(KW == 256 || KW == 512, "K = 256 or 512");
+  constexpr int BN = KW == 256 ? 128 : 64;
+  constexpr int BM = 64, BK = 64, NS = 8, NKB = KW / BK;
+  constexpr int WGN = KW == 256 ? 4 : 2, WM = BM / (8 / WGN), WN = BN / WGN, MI = WM / 16, NI = WN / 16;
+  constexpr int RPC = BN / 8;                     // 16-B pieces per residual row (16 / 8)
+  constexpr int RMASK = RPC - 1;
+  constexpr int NR = RES ? BM * RPC / 512 : 0;    // residual DMA instructions per thread (2 / 1)
+  constexpr int LA = NS - 1;                      // blocks in flight
+  constexpr int TAIL = (NKB + LA - 1) / NKB;      // tiles the lookahead reaches ahead (2 / 1)
   constexpr int SLOT = BM * BK;                   // elements per ring slot (8 KB)
   constexpr int W_ELEMS = BN * KW;                // resident weights (64 KB)
   __shared__ __attribute__((aligned(16))) bf16_t lds[W_ELEMS + NS * SLOT + BM * BN];
@@ -323,24 +334,26 @@ __global__ __launch_bounds__(512, 1) void conv_pw_rb_kernel(PwParams p) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) asm volatile("" ::"v"(e_bias[e]));
 
-  // resident weights: 32 16-B pieces per 512-B row, two rows per wave instruction; LDS position
-  // pos of row n holds logical piece (pos & ~7) | ((pos & 7) ^ (n & 7))
+  // resident weights: KW / 8 16-B pieces per row (2 rows / 1 row per wave instruction); LDS
+  // position pos of row n holds logical piece (pos & ~7) | ((pos & 7) ^ (n & 7))
+  constexpr int WROWS = 64 / (KW / 8);            // rows per wave instruction
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int row = (i * 8 + wave) * 2 + (lane >> 5);
-    const int pos = lane & 31;
+    const int row = (i * 8 + wave) * WROWS + lane / (KW / 8);
+    const int pos = lane % (KW / 8);
     const int lpc = (pos & ~7) | ((pos & 7) ^ (row & 7));
-    pw_dma16(rw, (uint32_t)(((n0 + row) * KW + lpc * 8) * 2), 0u, wres + (i * 8 + wave) * 2 * KW);
+    pw_dma16(rw, (uint32_t)(((n0 + row) * KW + lpc * 8) * 2), 0u, wres + (i * 8 + wave) * WROWS * KW);
   }
 
   const int lrow = wave * 8 + (lane >> 3);         // activation DMA: 8 rows per wave, 64 per block
   const int lp = (lane & 7) ^ (lane >> 3);
-  const int rrow0 = wave * 4 + (lane >> 4);
-  const int rpiece = (lane & 15) ^ (rrow0 & 15);
+  constexpr int RRW = 64 / RPC;                   // residual rows per wave instruction (4 / 8)
+  const int rrow0 = wave * RRW + lane / RPC;
+  const int rpiece = (lane % RPC) ^ (rrow0 & RMASK);
 
   auto issue = [&](int f, auto slot_tag) {
     constexpr int S = decltype(slot_tag)::value;
-    const int t = f >> 2, kb = f & 3;
+    const int t = f / NKB, kb = f % NKB;
     if (t >= ntiles) return;
     const int m = (group + t * p.groups) * BM + lrow;
     const uint32_t off = m < p.M ? (uint32_t)((m * p.ldx + lp * 8) * 2) : kPwOOB;
@@ -350,9 +363,9 @@ __global__ __launch_bounds__(512, 1) void conv_pw_rb_kernel(PwParams p) {
     const int m0 = (group + t * p.groups) * BM;
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
-      const int m = m0 + rrow0 + 32 * r;
+      const int m = m0 + rrow0 + 8 * RRW * r;
       const uint32_t off = m < p.M ? (uint32_t)((m * p.ldr + n0 + rpiece * 8) * 2) : kPwOOB;
-      pw_dma16(rr, off, 0u, resb + (r * 32 + wave * 4) * BN);
+      pw_dma16(rr, off, 0u, resb + (r * 8 * RRW + wave * RRW) * BN);
     }
   };
 
@@ -396,32 +409,38 @@ __global__ __launch_bounds__(512, 1) void conv_pw_rb_kernel(PwParams p) {
 
   const bool post = (p.act & 16) != 0;
   const int act = p.act & 15;
-  // one tile: H = slot half (tile parity).  Waits: block f has the six next blocks younger, plus
-  // this tile's residual (issued at step 0, before block f + 7) for steps 1-3; the last two
-  // tiles of the walk (fewer blocks issued behind them) wait for everything.
+  // one tile: H = tile parity (selects the slot half when two tiles share the 8-slot cycle).
+  // Waits: block (t, kb) has the next six blocks younger, plus this tile's residual (issued at
+  // step 0, before block (t, 0) + 7) while it sits between them (kb = 1 .. 6); the tiles the
+  // lookahead runs past the end of the walk wait for everything.
+  auto step = [&](int t, bool tail, auto h_tag, auto kb_tag) {
+    constexpr int H = decltype(h_tag)::value, KB = decltype(kb_tag)::value;
+    constexpr int SL = (NKB == 4 ? 4 * H : 0) + KB;
+    if (tail) pw_vm_barrier<0>();
+    else if (KB >= 1 && KB <= 6) pw_vm_barrier<6 + NR>();
+    else pw_vm_barrier<6>();
+    if (RES && KB == 0) issue_res(t);
+    issue(NKB * t + KB + LA, std::integral_constant<int, (SL + LA) % NS>{});
+    compute(std::integral_constant<int, SL>{}, kb_tag);
+  };
   auto tile = [&](int t, auto half_tag) {
-    constexpr int H = decltype(half_tag)::value;
-    const bool tail = t + 2 >= ntiles;
-    const int f = 4 * t;
+    const bool tail = t + TAIL >= ntiles;
 #pragma unroll
     for (int j = 0; j < NI; ++j)
 #pragma unroll
       for (int i = 0; i < MI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (tail) pw_vm_barrier<0>(); else pw_vm_barrier<6>();
-    if (RES) issue_res(t);
-    issue(f + 7, std::integral_constant<int, (4 * H + 7) % 8>{});
-    compute(std::integral_constant<int, 4 * H + 0>{}, I0{});
-    if (tail) pw_vm_barrier<0>(); else pw_vm_barrier<6 + NR>();
-    issue(f + 8, std::integral_constant<int, (4 * H + 8) % 8>{});
-    compute(std::integral_constant<int, 4 * H + 1>{}, I1{});
-    if (tail) pw_vm_barrier<0>(); else pw_vm_barrier<6 + NR>();
-    issue(f + 9, std::integral_constant<int, (4 * H + 9) % 8>{});
-    compute(std::integral_constant<int, 4 * H + 2>{}, I2{});
-    if (tail) pw_vm_barrier<0>(); else pw_vm_barrier<6 + NR>();
-    issue(f + 10, std::integral_constant<int, (4 * H + 10) % 8>{});
-    compute(std::integral_constant<int, 4 * H + 3>{}, I3{});
-    if (RES) {                                     // residual: younger = the 4 blocks issued since
-      if (tail) pw_vm_barrier<0>(); else pw_vm_barrier<4>();
+    step(t, tail, half_tag, I0{});
+    step(t, tail, half_tag, I1{});
+    step(t, tail, half_tag, I2{});
+    step(t, tail, half_tag, I3{});
+    if constexpr (NKB == 8) {
+      step(t, tail, half_tag, I4{});
+      step(t, tail, half_tag, I5{});
+      step(t, tail, half_tag, I6{});
+      step(t, tail, half_tag, I7{});
+    }
+    if (RES) {                                     // residual: younger = the NKB blocks issued since
+      if (tail) pw_vm_barrier<0>(); else pw_vm_barrier<NKB>();
     }
     const int m0 = (group + t * p.groups) * BM;
 #pragma unroll
@@ -436,7 +455,7 @@ __global__ __launch_bounds__(512, 1) void conv_pw_rb_kernel(PwParams p) {
         hi[e] = __uint_as_float(s[1]);
       }
       u32x4 r = {0u, 0u, 0u, 0u};
-      if constexpr (RES) r = *reinterpret_cast<const u32x4*>(resb + ml * BN + (((nl >> 3) ^ fr) << 3));
+      if constexpr (RES) r = *reinterpret_cast<const u32x4*>(resb + ml * BN + (((nl >> 3) ^ (fr & RMASK)) << 3));
       if (m >= p.M) continue;
       float v[8] = {lo[0] + e_bias[0], lo[1] + e_bias[1], lo[2] + e_bias[2], lo[3] + e_bias[3],
                     hi[0] + e_bias[4], hi[1] + e_bias[5], hi[2] + e_bias[6], hi[3] + e_bias[7]};
@@ -489,7 +508,7 @@ extern "C" int aiko_conv_pw(const void* x, const void* w, const float* bias, con
   using namespace aiko;
   if (K % (kPwBK * kPwNS) || N % kPwBN || M <= 0 || ldx % 8 || ldy % 8 || (res && ldr % 8) || ldx < K)
     return -1;
-  if (mode == 1 && K != 256) return -1;      // resident weights: one 128 x 256 block per workgroup
+  if (mode == 1 && K != 256 && K != 512) return -1;   // resident weights: a 64 KB block per workgroup
   PwParams p;
   p.x = static_cast<const bf16_t*>(x);
   p.w = static_cast<const bf16_t*>(w);
@@ -497,7 +516,7 @@ extern "C" int aiko_conv_pw(const void* x, const void* w, const float* bias, con
   p.res = static_cast<const bf16_t*>(res);
   p.y = static_cast<bf16_t*>(y);
   p.M = M; p.N = N; p.K = K; p.ldx = ldx; p.ldy = ldy; p.ldr = ldr; p.act = act;
-  p.ntn = N / kPwBN;
+  p.ntn = N / (mode == 1 && K == 512 ? 64 : kPwBN);
   const int bm = mode == 1 ? 64 : kPwBM;
   p.mtiles = (M + bm - 1) / bm;
   int groups = (cus > 0 ? cus : 256) / p.ntn;
@@ -505,11 +524,16 @@ extern "C" int aiko_conv_pw(const void* x, const void* w, const float* bias, con
   if (groups > p.mtiles) groups = p.mtiles;
   p.groups = groups;
   const dim3 grid((unsigned)(groups * p.ntn));
-  if (mode == 1) {
+  if (mode == 1 && K == 512) {
     if (res)
-      conv_pw_rb_kernel<true><<<grid, 512, 0, stream>>>(p);
+      conv_pw_rb_kernel<true, 512><<<grid, 512, 0, stream>>>(p);
     else
-      conv_pw_rb_kernel<false><<<grid, 512, 0, stream>>>(p);
+      conv_pw_rb_kernel<false, 512><<<grid, 512, 0, stream>>>(p);
+  } else if (mode == 1) {
+    if (res)
+      conv_pw_rb_kernel<true, 256><<<grid, 512, 0, stream>>>(p);
+    else
+      conv_pw_rb_kernel<false, 256><<<grid, 512, 0, stream>>>(p);
   } else if (res) {
     conv_pw_kernel<true><<<grid, 512, 0, stream>>>(p);
   } else {

@@ -322,7 +322,7 @@ def pw_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = Non
     16-byte aligned pixel rows."""
     return (spec.kind != "stem" and x2 is None and spec.K1 is None and spec.R == 1 and spec.S == 1
             and spec.stride == 1 and spec.pad == 0 and spec.Cc == spec.K and spec.K % 256 == 0
-            and spec.cout % 128 == 0 and x.stride(2) % 8 == 0) and ("k256" if spec.K == 256 else True)
+            and spec.cout % 128 == 0 and x.stride(2) % 8 == 0) and ("resident" if spec.K in (256, 512) else True)
 
 
 def narrow_variant_ok(spec: ConvSpec, x2: torch.Tensor | None = None) -> bool:
@@ -355,7 +355,7 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, p
             cands.append((8, 64, 10))        # variant 10: tile fixed by the kernel (8 rows x W)
         if pw_ok:
             cands.append((128, 128, 12))     # variant 12: persistent pointwise GEMM (conv_pw.hip)
-            if pw_ok == "k256":
+            if pw_ok == "resident":
                 cands.append((64, 128, 13))  # variant 13: the same with the weight block resident in LDS
     skip = {int(v) for v in __import__("os").environ.get("AIKO_CONV_SKIP", "").split(",") if v.strip()}
     if skip:                                   # A/B runs: exclude variants from the tuner

@@ -7,7 +7,7 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -q -k "conv_igem
 tail -1 gpurun_out/pw_t.log
 AIKO_TUNE_VERBOSE=1 timeout -k 10 300 python scripts/model_layers.py --batch 320 > gpurun_out/tune_pw.txt 2>&1 || { tail -20 gpurun_out/tune_pw.txt; exit 1; }
 grep -E "1[23]\): " gpurun_out/tune_pw.txt | head -20
-grep -E "^ +(13|16|19|29|31|34|37) M" gpurun_out/tune_pw.txt
+grep -E "^ +(6|11|13|16|19|29|31|34|37) M" gpurun_out/tune_pw.txt
 tail -1 gpurun_out/tune_pw.txt
 for i in 1 2; do
   echo -n "bench default: "; timeout -k 10 200 python bench.py --steps 30 --warmup 6 2>&1 | grep -o '"value": [0-9.]*' || exit 1

@@ -134,6 +134,11 @@ def _nhwc(x_nchw):
     (65, 14, 14, 256, 1024, 1, 1, 0, "relu", True, (64, 128, 13)),
     (2, 28, 28, 256, 128, 1, 1, 0, "relu", False, (64, 128, 13)),
     (40, 14, 14, 256, 512, 1, 1, 0, "gelu", True, (64, 128, 13)),
+    # K = 512: a 64 x 512 weight block per workgroup, one tile per ring cycle
+    (1, 7, 7, 512, 2048, 1, 1, 0, "relu", True, (64, 128, 13)),
+    (64, 7, 7, 512, 2048, 1, 1, 0, "relu", True, (64, 128, 13)),
+    (8, 28, 28, 512, 128, 1, 1, 0, "relu", False, (64, 128, 13)),
+    (9, 14, 14, 512, 256, 1, 1, 0, None, True, (64, 128, 13)),
 ])
 def test_conv_igemm_matches_torch(native, B, H, W, cin, cout, k, stride, pad, act, res, tile):
     from aiko_services_amd.ops import conv as C
