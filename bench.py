@@ -143,19 +143,21 @@ def pp_definition(batch: int, graph: bool, height: int, width: int, world: int, 
     return d
 
 
-def main(argv=None):
+def parse_args(argv=None) -> argparse.Namespace:
+    """Command line -> options with the per-model defaults applied (batch, frame size)."""
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--batch", type=int, default=None,
                     help="frames per GPU per step (default: ResNet-50 320, YOLOv8-n 64, Whisper 14 "
-                         "streams: 14 x 12 heads of query tiles is 1.97 rounds of the attention kernel's 512 "
-                         "resident workgroups where 16 streams was 2.25 — 2.94k-3.05k vs 2.87k-2.88k "
-                         "windows/s at a lower p50, scripts/batch_sweep_cfg45.sh).  ResNet-50's 320 is chosen for the chip's 256 CUs: stage 3 runs "
+                         "streams).  ResNet-50's 320 is chosen for the chip's 256 CUs: stage 3 runs "
                          "M = 320 x 196 = 62720 = 245 tiles of 256 rows (96 %% of the CUs busy in one "
                          "round) where B=256 gives 196 tiles (77 %%); interleaved on MI355X 86.3-87.9k "
-                         "vs 83.7-84.4k frames/s at B=256 (scripts/batch_quant_ab.sh)")
+                         "vs 83.7-84.4k frames/s at B=256 (scripts/batch_quant_ab.sh).  Whisper's 14 "
+                         "streams x 12 heads x 6 query tiles are 1.97 rounds of the attention kernel's "
+                         "512 resident workgroups where 16 streams were 2.25: 2.94k-3.05k vs "
+                         "2.87k-2.88k windows/s at a lower p50 (scripts/batch_sweep_cfg45.sh)")
     ap.add_argument("--height", type=int, default=224)
     ap.add_argument("--width", type=int, default=224)
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture")
@@ -182,11 +184,16 @@ def main(argv=None):
     ap.add_argument("--element-times", default=None,
                     help="(pp) JSON {element: ms per batch} for the stage balancer")
     a = ap.parse_args(argv)
-    explicit_hw = "--height" in (argv or sys.argv)
+    explicit_hw = "--height" in (sys.argv[1:] if argv is None else argv)
     if (a.parallel == "pp" or a.model == "yolov8n") and not explicit_hw:
         a.height, a.width = 480, 640          # configs 3/4 decode VGA video frames
     if a.batch is None:
         a.batch = 64 if a.model == "yolov8n" else 14 if a.model.startswith("whisper") else 320
+    return a
+
+
+def main(argv=None):
+    a = parse_args(argv)
 
     procs = []
     if a.parallel == "pp":
