@@ -467,3 +467,29 @@ def test_stem_pool_fused(native, hw):
         # half-channel-wave strip kernels (variants 3 / 4, carried pool row)
         assert torch.equal(outs[2], outs[0])
         assert torch.equal(outs[3], outs[0]) and torch.equal(outs[4], outs[0])
+
+
+@pytest.mark.parametrize("tile", [(128, 128, 12), (64, 128, 13)])
+def test_conv_pw_slices_and_post_residual(native, tile):
+    """conv_pw (variants 12 / 13): input from a channel slice (pitch 384 != K), output into a
+    slice of a concat buffer, residual added after the activation (YOLO bottleneck form) — the
+    same result as the register-staged kernel within bf16 rounding, nothing outside the slice."""
+    from aiko_services_amd.ops import conv as C
+    from aiko_services_amd.ops import reference as R
+    g = torch.Generator().manual_seed(17)
+    B, H, W, K, N = 9, 14, 14, 256, 256
+    big = torch.randn(B, H, W, 384, generator=g).to(torch.bfloat16).to(DEV)
+    xin = big[..., 64:64 + K]
+    w = torch.randn(N, K, 1, 1, generator=g) / 16
+    b = torch.randn(N, generator=g) * 0.1
+    spec = C.make_conv_spec(w, b, act="silu", device=DEV)
+    res = torch.randn(B, H, W, N, generator=g).to(torch.bfloat16).to(DEV)
+    cat = torch.zeros(B, H, W, 448, dtype=torch.bfloat16, device=DEV)
+    C.conv2d(xin, spec, residual=res, out=cat[..., 128:128 + N], tile=tile, residual_after_act=True)
+    ref_out = torch.zeros_like(cat)
+    C.conv2d(xin, spec, residual=res, out=ref_out[..., 128:128 + N], tile=(128, 128, 0), residual_after_act=True)
+    torch.cuda.synchronize()
+    ref = R.conv_ref(xin.permute(0, 3, 1, 2).float(), spec) + res.permute(0, 3, 1, 2).float()
+    assert _rel_err(cat[..., 128:128 + N].permute(0, 3, 1, 2), ref) < 1e-2
+    assert _rel_err(cat.float(), ref_out.float()) < 1e-2
+    assert cat[..., :128].abs().max().item() == 0 and cat[..., 128 + N:].abs().max().item() == 0
