@@ -46,6 +46,9 @@ int aiko_stem_direct(const void* in, void* out, const void* w, const float* bias
                      int act, hipStream_t stream);
 int aiko_conv3x3_patch(const void* x, const void* wimg, const float* bias, void* y, int B, int H, int W, int ldy,
                        int act, int grid, hipStream_t stream);
+int aiko_bneck_fused(const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
+                     const void* w3, const float* b3, void* y, int B, int H, int W, int cin, int grid,
+                     unsigned* dbg, hipStream_t stream);
 int aiko_conv_chain(const void* A, const void* W1, const float* b1, const void* R, void* Y, const void* W2,
                     const float* b2, void* Z, const void* A2, int M, int K1, int N1, int N2, int grid,
                     hipStream_t stream);
@@ -375,6 +378,48 @@ void conv_chain_out(const at::Tensor& A, const at::Tensor& W1, const at::Tensor&
                                Y.data_ptr(), W2.data_ptr(), b2.data_ptr<float>(), Z.data_ptr(),
                                dual ? R.data_ptr() : nullptr, M, K1, N1, N2, grid, cur_stream()),
                "conv_chain");
+}
+
+// A whole ResNet stage-1 bottleneck in one launch (bneck_fused.hip): x [B, H, 56, cin] ->
+// y [B, H, 56, 256]; cin 256 = identity block (w3 [256, 64]), cin 64 = projection block with
+// w3 = [conv3 | shortcut] [256, 128] (K-concatenated, ops.conv.fuse_shortcut).
+void bneck_fused_out(const at::Tensor& x, const at::Tensor& w1, const at::Tensor& b1, const at::Tensor& w2,
+                     const at::Tensor& b2, const at::Tensor& w3, const at::Tensor& b3, at::Tensor& y, int64_t grid,
+                     const c10::optional<at::Tensor>& dbg) {
+  for (const at::Tensor* t : {&x, &w1, &b1, &w2, &b2, &w3, &b3, (const at::Tensor*)&y}) {
+    check_cuda(*t, "bneck_fused operand");
+    TORCH_CHECK(t->is_contiguous() && reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
+                "aiko.bneck_fused_out: operands must be contiguous and 16-byte aligned");
+  }
+  for (const at::Tensor* t : {&x, &w1, &w2, &w3, (const at::Tensor*)&y})
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16, "aiko.bneck_fused_out: bf16 activations / weights");
+  for (const at::Tensor* t : {&b1, &b2, &b3})
+    TORCH_CHECK(t->scalar_type() == at::kFloat, "aiko.bneck_fused_out: fp32 biases");
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4, "aiko.bneck_fused_out: x / y NHWC");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), cin = x.size(3);
+  TORCH_CHECK(W == 56 && (cin == 256 || cin == 64), "aiko.bneck_fused_out: x must be [B, H, 56, 256 | 64]");
+  TORCH_CHECK(y.size(0) == B && y.size(1) == H && y.size(2) == W && y.size(3) == 256,
+              "aiko.bneck_fused_out: y must be [B, H, 56, 256]");
+  const int64_t k3 = cin == 64 ? 128 : 64;
+  TORCH_CHECK(w1.dim() == 2 && w1.size(0) == 64 && w1.size(1) == cin, "aiko.bneck_fused_out: w1 [64, cin]");
+  TORCH_CHECK(w2.dim() == 2 && w2.size(0) == 64 && w2.size(1) == 576, "aiko.bneck_fused_out: w2 [64, 576] (3x3, tap-major)");
+  TORCH_CHECK(w3.dim() == 2 && w3.size(0) == 256 && w3.size(1) == k3, "aiko.bneck_fused_out: w3 [256, ", k3, "]");
+  TORCH_CHECK(b1.numel() == 64 && b2.numel() == 64 && b3.numel() == 256, "aiko.bneck_fused_out: biases [64], [64], [256]");
+  TORCH_CHECK(x.data_ptr() != y.data_ptr(), "aiko.bneck_fused_out: in place is not supported");
+  TORCH_CHECK(grid >= 0, "aiko.bneck_fused_out: grid must be >= 0 (0: one workgroup per CU)");
+  unsigned* dbg_ptr = nullptr;
+  if (dbg.has_value()) {                // diagnostics: [grid, B * H / grid + 1, 8] int32 stamps
+    check_cuda(*dbg, "bneck_fused dbg");
+    TORCH_CHECK(grid > 0 && dbg->scalar_type() == at::kInt && dbg->is_contiguous() &&
+                    dbg->numel() >= grid * ((x.size(0) * x.size(1)) / grid + 1) * 8,
+                "aiko.bneck_fused_out: dbg must be int32 [grid, B*H/grid + 1, 8] with an explicit grid");
+    dbg_ptr = reinterpret_cast<unsigned*>(dbg->data_ptr());
+  }
+  TORCH_CHECK(B * H * W * 256 < INT_MAX, "aiko.bneck_fused_out: batch too large for 32-bit pixel indices");
+  check_launch(aiko_bneck_fused(x.data_ptr(), w1.data_ptr(), b1.data_ptr<float>(), w2.data_ptr(), b2.data_ptr<float>(),
+                                w3.data_ptr(), b3.data_ptr<float>(), y.data_ptr(), (int)B, (int)H, (int)W, (int)cin,
+                                (int)grid, dbg_ptr, cur_stream()),
+               "bneck_fused");
 }
 
 // uint8 frames -> letterbox/normalise -> k x k stem conv (+bias, act) -> bf16 NHWC ``out``
@@ -1084,6 +1129,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("stem_direct_out(Tensor frames, Tensor w, Tensor? bias, Tensor(a!) out, int[] geom, float fill, float[] mean, float[] std, bool bgr) -> ()");
   m.def("conv3x3_patch_out(Tensor x, Tensor wimg, Tensor? bias, Tensor(a!) y, int act, int grid=0) -> ()");
   m.def("conv_chain_out(Tensor A, Tensor W1, Tensor b1, Tensor? R, Tensor(a!) Y, Tensor W2, Tensor b2, Tensor(b!) Z, int grid=0, Tensor? A2=None) -> ()");
+  m.def("bneck_fused_out(Tensor x, Tensor w1, Tensor b1, Tensor w2, Tensor b2, Tensor w3, Tensor b3, Tensor(a!) y, int grid=0, Tensor? dbg=None) -> ()");
   m.def("maxpool_out(Tensor x, Tensor(a!) y, int k, int s, int p) -> ()");
   m.def("avgpool_out(Tensor x, Tensor(a!) y) -> ()");
   m.def("mean_rows_out(Tensor x, Tensor(a!) y) -> ()");
@@ -1109,6 +1155,7 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("preprocess_out", &preprocess_out);
   m.impl("maxpool_out", &maxpool_out);
   m.impl("conv_chain_out", &conv_chain_out);
+  m.impl("bneck_fused_out", &bneck_fused_out);
   m.impl("conv3x3_patch_out", &conv3x3_patch_out);
   m.impl("stem_direct_out", &stem_direct_out);
   m.impl("upsample2x_out", &upsample2x_out);

@@ -99,6 +99,8 @@ class ResNet50(WeightsMixin):
         self.mall_blocks = int(os.environ.get("AIKO_RESNET_MALL_BLOCKS", "3"))
         # conv_chain: identity block's 1x1 expansion + next block's 1x1 reduction in one launch
         self.chain = os.environ.get("AIKO_RESNET_CHAIN", "1") != "0"
+        # stage-1 bottlenecks as ONE launch each (bneck_fused.hip: t1 / t2 stay in LDS)
+        self.bneck = os.environ.get("AIKO_RESNET_BNECK", "1") != "0"
         # uint8 frames of the model's own size go straight into the fused stem (it normalises
         # while filling its LDS patch): no pre-processing kernel, no bf16 stem buffer
         self.stem_u8 = os.environ.get("AIKO_STEM_U8", "1") != "0"
@@ -207,6 +209,11 @@ class ResNet50(WeightsMixin):
         blk = self.blocks[bi]
         H, W = x.shape[1], x.shape[2]
         sl = slice(c0, c0 + ch)
+        conv3 = blk.fused if blk.fused is not None and self.fuse_shortcut else blk.conv3
+        if (self.bneck and t1 is None and (blk.down is None or conv3 is blk.fused)
+                and C.bneck_ok(x, blk.conv1, blk.conv2, conv3)):
+            out = self._buf(tag + ("xa" if bi % 2 == 0 else "xb"), (B, H, W, conv3.cout))[sl]
+            return C.bneck_fused(x, blk.conv1, blk.conv2, conv3, out=out), None
         if t1 is None:
             t1 = C.conv2d(x, blk.conv1, out=self._buf(tag + "t1", (B, H, W, blk.conv1.cout))[sl])
         Ho, Wo = blk.conv2.out_hw(H, W)

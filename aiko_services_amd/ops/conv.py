@@ -619,6 +619,42 @@ def chain_dual_ok(fused: ConvSpec, spec1: ConvSpec) -> bool:
             and spec1.weight.shape == (64, 256) and spec1.bias is not None and spec1.act == ACT_RELU)
 
 
+def bneck_ok(x: torch.Tensor, conv1: ConvSpec, conv2: ConvSpec, conv3: ConvSpec) -> bool:
+    """Can this ResNet bottleneck run as ONE ``bneck_fused`` launch (``bneck_fused.hip``)?
+    Stage-1 geometry: x NHWC [B, H, 56, 256] with an identity residual (``conv3`` 64 -> 256), or
+    x [B, H, 56, 64] with ``conv3`` the K-concatenated conv3 + 1x1 projection (``fuse_shortcut``:
+    weight [256, 128]); conv1 1x1 -> 64, conv2 3x3 / stride 1 / pad 1 64 -> 64; every conv with
+    a bias and ReLU."""
+    def relu_bias(s):
+        return s.kind == "conv" and s.bias is not None and s.act == ACT_RELU
+    if not (x.dim() == 4 and x.is_contiguous() and x.dtype == torch.bfloat16 and x.shape[2] == 56
+            and relu_bias(conv1) and relu_bias(conv2) and relu_bias(conv3)):
+        return False
+    cin = x.shape[3]
+    k3 = 128 if cin == 64 else 64
+    return (cin in (64, 256) and conv1.R == conv1.S == 1 and conv1.stride == 1 and conv1.K1 is None
+            and tuple(conv1.weight.shape) == (64, cin) and conv2.R == conv2.S == 3 and conv2.stride == 1
+            and conv2.pad == 1 and tuple(conv2.weight.shape) == (64, 576) and conv3.R == conv3.S == 1
+            and conv3.stride == 1 and tuple(conv3.weight.shape) == (256, k3)
+            and (conv3.K1 is None if cin == 256 else (conv3.K1 == 64 and conv3.stride2 == 1)))
+
+
+def bneck_fused(x: torch.Tensor, conv1: ConvSpec, conv2: ConvSpec, conv3: ConvSpec, out: torch.Tensor | None = None,
+                grid: int = 0) -> torch.Tensor:
+    """A whole stage-1 ResNet bottleneck in one kernel: ``relu(conv3(relu(conv2(relu(conv1(x)))))
+    + x)`` (identity block) or ``relu([conv2 out | x] . W3^T + b)`` with ``conv3`` the fused
+    conv3 + projection (entry block).  The 64-channel intermediates never leave LDS.  Persistent:
+    ``grid`` workgroups (0 = one per CU) each stream a contiguous range of the B * H output rows
+    across image boundaries."""
+    if not bneck_ok(x, conv1, conv2, conv3):
+        raise ValueError("bneck_fused: shapes not eligible (see bneck_ok)")
+    if out is None:
+        out = torch.empty(*x.shape[:3], 256, dtype=torch.bfloat16, device=x.device)
+    torch.ops.aiko.bneck_fused_out(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias, conv3.weight,
+                                   conv3.bias, out, grid)
+    return out
+
+
 def conv_chain(x: torch.Tensor, spec3: ConvSpec, residual: torch.Tensor | None, out_y: torch.Tensor,
                spec1: ConvSpec, out_z: torch.Tensor, grid: int = 0, x2: torch.Tensor | None = None):
     """``out_y = relu(conv1x1(x, spec3) + residual)``, ``out_z = relu(conv1x1(out_y, spec1))`` in

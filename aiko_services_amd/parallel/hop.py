@@ -52,49 +52,17 @@ import torch
 import torch.distributed as tdist
 
 from . import dist as D
+from .hop_state import (FLOAT_TOKEN, RESULT_KEY, TOKEN, NoCredit, StageFailure, is_token,  # noqa: F401
+                        needs_decode, plane, set_plane)
 
 __all__ = ["HopPlane", "StageFailure", "NoCredit", "init_plane", "plane", "shutdown_plane", "is_token",
            "needs_decode", "mark_frame_held", "TOKEN", "FLOAT_TOKEN"]
 
-TOKEN = "T@"
-FLOAT_TOKEN = "F@"
-RESULT_KEY = "_device_result"
 _ALIGN = 256
 _DTYPES = {str(dt).split(".")[-1]: dt for dt in
            (torch.uint8, torch.int8, torch.int16, torch.int32, torch.int64, torch.float16,
             torch.float32, torch.float64, torch.bfloat16, torch.bool)}
 _DTYPE_NAMES = {dt: name for name, dt in _DTYPES.items()}
-
-
-class StageFailure(RuntimeError):
-    """A peer rank of the hop plane is gone (registrar removal, last will or transport error)."""
-
-    def __init__(self, peer: int, cause=None):
-        super().__init__(f"hop: stage rank {peer} failed" + (f": {cause}" if cause else ""))
-        self.peer = peer
-
-
-class NoCredit(RuntimeError):
-    """Every staging slot toward the peer holds an unacknowledged frame."""
-
-
-def is_token(v) -> bool:
-    return isinstance(v, str) and (v.startswith(TOKEN) or v.startswith(FLOAT_TOKEN))
-
-
-def needs_decode(stream_dict, values) -> bool:
-    """Whether a ``process_frame`` / ``process_frame_response`` message went through
-    :meth:`HopPlane.encode`: the stream dict names a hop rank (forward hops), or a value is a
-    tensor / float token or an encoded DeviceResult (responses).  Plain nested-dict swag values
-    of reference pipelines never enter the token scanner."""
-    if isinstance(stream_dict, dict) and stream_dict.get("hop_rank") is not None:
-        return True
-    if not isinstance(values, dict):
-        return False
-    for v in values.values():
-        if is_token(v) or (isinstance(v, dict) and RESULT_KEY in v):
-            return True
-    return False
 
 
 def _nbytes(dtype, shape) -> int:
@@ -791,21 +759,14 @@ class HopPlane:
             torch.cuda.synchronize(self.device)
 
 
-_plane: HopPlane | None = None
-
-
 def init_plane(links, device=None, depth: int = 4) -> HopPlane:
-    global _plane
-    _plane = HopPlane(links, device=device, depth=depth)
-    return _plane
-
-
-def plane() -> HopPlane | None:
-    return _plane
+    p = HopPlane(links, device=device, depth=depth)
+    set_plane(p)
+    return p
 
 
 def shutdown_plane():
-    global _plane
-    if _plane is not None:
-        _plane.close()
-    _plane = None
+    p = plane()
+    if p is not None:
+        p.close()
+    set_plane(None)

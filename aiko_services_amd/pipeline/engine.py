@@ -37,7 +37,7 @@ from ..runtime.context import Interface, compose_instance, pipeline_args, pipeli
 from ..runtime.lease import Lease
 from ..runtime.process import aiko
 from ..runtime.service import ServiceFilter, ServiceProtocol, ServiceTags
-from ..parallel import hop as _hop
+from ..parallel import hop_state as _hop     # torch-free: control-plane processes stay light
 from ..utils import fault as _fault
 from ..utils import trace as _trace
 from ..utils.configuration import get_gpu_configuration
@@ -659,6 +659,12 @@ class PipelineImpl(Pipeline):
         if lease is not None:
             lease.terminate()
             lease.stream.state = StreamState.STOP if lease.stream.state != StreamState.ERROR else StreamState.ERROR
+            # frames still in flight (a non-graceful destroy, or an error) leave with the stream:
+            # their hop / FramePool slots and admission credits come back now — a response that
+            # arrives later finds "stream not found" and is dropped
+            for frame_id in list(lease.stream.frames):
+                self._release_frame(lease.stream, frame_id)
+        self._admit_release_stream(stream_id)
         hop = _hop.plane()
         if hop is not None:
             self.logger.info(f"Stream {stream_id} destroyed: hop {hop.stats()} redispatched "
@@ -824,6 +830,8 @@ class PipelineImpl(Pipeline):
         lease = self.stream_leases.get(stream_id)
         if lease is None:
             self.logger.warning(f"{header} stream not found")
+            if new_frame:
+                self._admit_release((stream_id, frame_id))   # admitted, but it never existed
             return None, None
         lease.extend()
         stream = lease.stream
@@ -1157,6 +1165,16 @@ class PipelineImpl(Pipeline):
                 self._admitted.discard(key)
                 self._admit_cv.notify_all()
 
+    def _admit_release_stream(self, stream_id):
+        """Every admission credit a destroyed stream still holds (frames admitted but rejected
+        before they existed, or never released): the window is shared by the whole pipeline."""
+        stream_id = str(stream_id)
+        with self._admit_cv:
+            stale = [k for k in self._admitted if k[0] == stream_id]
+            if stale:
+                self._admitted.difference_update(stale)
+                self._admit_cv.notify_all()
+
     # ---- remote hops: credits, dispatch, failure ------------------------------------------------
     def _param_float(self, name, default):
         v, found = self.get_parameter(name)
@@ -1331,6 +1349,7 @@ class PipelineImpl(Pipeline):
         self._inflight.pop(key, None)
         lease = self.stream_leases.get(str(key[0]))
         if lease is None:
+            self._admit_release(key)     # its stream is gone: only the admission credit is left
             return
         stream = lease.stream
         self._release_frame(stream, key[1])

@@ -18,6 +18,8 @@ def main():
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("--top", type=int, default=12)
     ap.add_argument("--clock-ghz", type=float, default=2.4)
+    ap.add_argument("--lds", action="store_true",
+                    help="add LDS-array utilisation (SQ_LDS_IDX_ACTIVE / (cycles x 256 CUs)) and per-wave counts")
     a = ap.parse_args()
     cnt = defaultdict(lambda: defaultdict(list))
     dur = defaultdict(dict)
@@ -39,13 +41,22 @@ def main():
         conf = m("SQ_LDS_BANK_CONFLICT") / m("SQ_LDS_IDX_ACTIVE") if m("SQ_LDS_IDX_ACTIVE") else 0.0
         fetch, write = m("FETCH_SIZE"), m("WRITE_SIZE")
         bw = (fetch + write) * 1e3 / (us * 1e-6) / 1e12 if us else float("nan")
+        waves = max(1.0, m("SQ_WAVES")) if cs.get("SQ_WAVES") else float("nan")
+        extra = (m("SQ_LDS_IDX_ACTIVE") / (cyc * 256) if cyc else float("nan"),
+                 m("SQ_INSTS_LDS") / waves, m("SQ_INSTS_MFMA") / waves, m("SQ_INSTS_VALU") / waves)
         rows.append((us * calls, key, calls, us, mfma, conf, fetch / 1e3, write / 1e3, bw,
-                     m("SQ_INSTS_VALU") / max(1.0, m("SQ_INSTS_MFMA"))))
+                     m("SQ_INSTS_VALU") / max(1.0, m("SQ_INSTS_MFMA")), extra))
     rows.sort(reverse=True)
-    print("| kernel | grid | n | us | MFMA busy | LDS conflict | fetch MB | write MB | TB/s | VALU/MFMA |")
-    print("|---|---|---|---|---|---|---|---|---|---|")
-    for tot, (name, grid), n, us, mf, cf, fe, wr, bw, vm in rows[:a.top]:
-        print(f"| `{name}` | {grid} | {n} | {us:.1f} | {mf:.2f} | {cf:.3f} | {fe:.1f} | {wr:.1f} | {bw:.2f} | {vm:.2f} |")
+    hdr = "| kernel | grid | n | us | MFMA busy | LDS conflict | fetch MB | write MB | TB/s | VALU/MFMA |"
+    if a.lds:
+        hdr += " LDS active | LDS/wave | MFMA/wave | VALU/wave |"
+    print(hdr)
+    print("|---" * (hdr.count("|") - 1) + "|")
+    for tot, (name, grid), n, us, mf, cf, fe, wr, bw, vm, ex in rows[:a.top]:
+        line = f"| `{name}` | {grid} | {n} | {us:.1f} | {mf:.2f} | {cf:.3f} | {fe:.1f} | {wr:.1f} | {bw:.2f} | {vm:.2f} |"
+        if a.lds:
+            line += f" {ex[0]:.2f} | {ex[1]:.0f} | {ex[2]:.0f} | {ex[3]:.0f} |"
+        print(line)
 
 
 if __name__ == "__main__":

@@ -28,14 +28,35 @@ def summarize(db, top=40, by_grid=False):
     return "\n".join(out)
 
 
+def sequence(db, last=80):
+    """The last ``last`` dispatches in launch order with their durations (one forward of an
+    in-order single-stream trace: isolated per-kernel times, attributable to layers)."""
+    con = sqlite3.connect(db)
+    cur = con.cursor()
+    cols = [r[1] for r in cur.execute("pragma table_info(kernels)")]
+    name_col = "kernel_name" if "kernel_name" in cols else "name"
+    rows = cur.execute(f"select {name_col}, start, end, grid_x from kernels order by start").fetchall()[-last:]
+    out = ["| # | kernel | grid | us |", "|---|---|---|---|"]
+    tot = 0.0
+    for i, (name, s, e, gx) in enumerate(rows):
+        d = (e - s) / 1e3
+        tot += d
+        short = name if len(name) < 80 else name[:77] + "..."
+        out.append(f"| {i} | `{short}` | {gx} | {d:.1f} |")
+    span = (rows[-1][2] - rows[0][1]) / 1e3 if rows else 0.0
+    out.append(f"\nsum {tot:.1f} us, span {span:.1f} us over {len(rows)} dispatches")
+    return "\n".join(out)
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
     ap.add_argument("--out")
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--by-grid", action="store_true", help="split kernels by grid size (layer shapes)")
+    ap.add_argument("--sequence", type=int, default=0, help="list the last N dispatches in order instead")
     a = ap.parse_args()
-    s = summarize(a.db, a.top, a.by_grid)
+    s = sequence(a.db, a.sequence) if a.sequence else summarize(a.db, a.top, a.by_grid)
     print(s)
     if a.out:
         with open(a.out, "w") as f:

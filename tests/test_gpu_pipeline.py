@@ -223,6 +223,7 @@ def test_resnet50_chain_matches_unchained(native):
     g = torch.Generator().manual_seed(6)
     frames = torch.randint(0, 256, (16, 224, 224, 3), generator=g, dtype=torch.uint8).to("cuda")
     m = ResNet50(device="cuda")
+    m.bneck = False              # stage 1 on the chained / patch kernels (bneck_fused replaces them)
     m.chain = False
     ref = m.logits(frames).float().clone()
     m.chain = True

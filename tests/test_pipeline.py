@@ -638,3 +638,35 @@ def test_aruco_original_dictionary_ids(aiko_process):
     assert sorted(got) == sorted(placed)
     for mid, tl in placed.items():
         assert got[mid] == tl, (mid, got[mid], tl)
+
+
+def test_destroy_stream_returns_admission_credits(aiko_process):
+    """the admission window is shared by the whole pipeline, so a stream
+    destroyed with frames in flight (or with admitted frames that never came to exist) must
+    return every credit, or later streams starve at admit_frame."""
+    from aiko_services_amd.pipeline.stream import Frame
+    d = json.loads(json.dumps(DIAMOND))
+    d["parameters"]["frame_window"] = 2
+    pipeline, q = _create(d, stream_id="w1")
+    assert pipeline.frame_window() == 2
+    released = []
+    # two frames in flight on stream w1: admitted and present in the stream, never completed
+    for fid in (0, 1):
+        assert pipeline.admit_frame("w1", fid, timeout=0)
+        frame = Frame()
+        frame.on_complete.append(lambda fid=fid: released.append(fid))
+        pipeline.stream_leases["w1"].stream.frames[fid] = frame
+    assert not pipeline.admit_frame("w2", 0, timeout=0)           # window full
+    event.call_on_loop(lambda: pipeline.destroy_stream("w1"))
+    assert sorted(released) == [0, 1]                              # their slots came back
+    assert pipeline.admit_frame("w2", 0, timeout=0)                # and so did the credits
+    # a frame admitted for a stream that no longer exists is rejected AND un-admitted
+    assert pipeline.admit_frame("gone", 7, timeout=0)
+    event.call_on_loop(lambda: pipeline.process_frame({"stream_id": "gone", "frame_id": 7}, {"b": 1}))
+    assert ("gone", 7) not in pipeline._admitted
+    # credits held by a stream whose frames never reached the engine go with the stream
+    pipeline._admit_release(("w2", 0))
+    assert pipeline.admit_frame("w3", 0, timeout=0) and pipeline.admit_frame("w3", 1, timeout=0)
+    event.call_on_loop(lambda: pipeline.create_stream("w3"))
+    event.call_on_loop(lambda: pipeline.destroy_stream("w3"))
+    assert not any(k[0] == "w3" for k in pipeline._admitted)
