@@ -154,7 +154,7 @@ __global__ __launch_bounds__(64 * kBnNW, 1) void bneck_fused_kernel(BnParams p) 
   constexpr int KS1 = CIN / 32, KS2 = 9 * kBnMid / 32, K3 = DUAL ? 2 * kBnMid : kBnMid, KS3 = K3 / 32;
   constexpr int ST = 2 * kBnTPW;                   // y stores per wave per row
   constexpr int X_BYTES = 4 * XB, T1_BYTES = 3 * kBnTB;
-  constexpr int LDS_BYTES = X_BYTES + T1_BYTES + kBnTB + 1024;
+  constexpr int LDS_BYTES = X_BYTES + T1_BYTES + kBnTB;
   // conv1 / conv3 read x units up to 7 past a row image (odd chunk, pixel slots 56..63): for the
   // last ring slot they fall into the t1 ring, still inside the allocation
   static_assert(LDS_BYTES <= 160 * 1024, "LDS");
@@ -162,7 +162,6 @@ __global__ __launch_bounds__(64 * kBnNW, 1) void bneck_fused_kernel(BnParams p) 
   unsigned char* const xr = lds;
   unsigned char* const t1r = lds + X_BYTES;
   unsigned char* const t2b = lds + X_BYTES + T1_BYTES;
-  float* const b3s = reinterpret_cast<float*>(lds + X_BYTES + T1_BYTES + kBnTB);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -198,7 +197,13 @@ __global__ __launch_bounds__(64 * kBnNW, 1) void bneck_fused_kernel(BnParams p) 
     bias1[e] = p.b1[16 * cg + 4 * fq + e];
     bias2[e] = p.b2[16 * cg + 4 * fq + e];
   }
-  if (tid < kBnOut) b3s[tid] = p.b3[tid];
+  // conv3's bias: the C input of each tile's first MFMA, held in registers (an LDS re-read per
+  // pixel tile cost 8 ds_read_b128 per wave and row in the LDS-bound phase B)
+  f32x4 bias3[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bias3[t][e] = p.b3[64 * cg + 32 * (t >> 1) + 8 * fq + 4 * (t & 1) + e];
   // one-hot A fragments of the identity residual (tile parity tp): row 4q + e of the tile is
   // channel 8q + 4tp + e of the 32-channel slice the B fragment (x's chunk run) holds
   bf16x8 eye[2];
@@ -222,7 +227,7 @@ __global__ __launch_bounds__(64 * kBnNW, 1) void bneck_fused_kernel(BnParams p) 
     const int s = min(u / XPU, kBnW - 1);
     const int c = min(u - (u / XPU) * XPU, NC - 1);           // the pad units: a duplicate chunk
     goff[q] = s * CIN * 2 + c * 16;
-    gok[q] = u < XU && wv + kBnNW * q < NI;
+    gok[q] = u < XU && wv + kBnNW * q < NI && u - (u / XPU) * XPU < NC;   // no request for pad units
   }
   int dw = 0;                                      // this wave's DMA instructions per row
 #pragma unroll
@@ -337,7 +342,6 @@ __global__ __launch_bounds__(64 * kBnNW, 1) void bneck_fused_kernel(BnParams p) 
   auto conv3 = [&](int vc, int n, int r) {
     const unsigned char* xres = xr + (vc & 3) * XB + xlb;
     const unsigned char* t2r = t2b + tlb;
-    const float* bb = b3s + 64 * cg + 8 * fq;
     bf16_t* yrow = p.y + ((long)(n * H + r) * kBnW + 16 * pt0 + fr) * kBnOut + 64 * cg + 8 * fq;
 #pragma unroll
     for (int t8 = 0; t8 < kBnTPW; ++t8) {          // pixel tile pt0 + t8
@@ -354,12 +358,10 @@ __global__ __launch_bounds__(64 * kBnNW, 1) void bneck_fused_kernel(BnParams p) 
       }
       f32x4 a3[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t)                  // bias of rows 4 fq + e: channels 64 cg + 32 (t>>1) + 8 fq + 4 (t&1) + e
-        a3[t] = *reinterpret_cast<const f32x4*>(bb + 32 * (t >> 1) + 4 * (t & 1));
-#pragma unroll
       for (int ks = 0; ks < KS3; ++ks)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) a3[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w3f[t][ks], bf[ks], a3[t], 0, 0, 0);
+        for (int t = 0; t < 4; ++t)
+          a3[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w3f[t][ks], bf[ks], ks == 0 ? bias3[t] : a3[t], 0, 0, 0);
       if constexpr (!DUAL) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) a3[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(eye[t & 1], rv[t >> 1], a3[t], 0, 0, 0);
@@ -371,6 +373,9 @@ __global__ __launch_bounds__(64 * kBnNW, 1) void bneck_fused_kernel(BnParams p) 
                        bn_relu2(pack2(a3[2 * h + 1][2], a3[2 * h + 1][3]))};
         if (p.mode & 128) {                        // ablation: no store (keep the values live)
           if (ov[0] == 0x7fc07fc0u && ov[1] == ov[2] && ov[3] == 1u) bn_store16(yrow, ov);
+        } else if (p.mode & 256) {                 // ablation: same bytes, lane-contiguous addresses
+          bf16_t* yr = p.y + ((long)(n * H + r) * kBnW) * kBnOut;
+          bn_store16(yr + (long)(((cg * 2 + (pt0 >> 1)) * 4 + t8 * 2 + h) % 28) * 512 + lane * 8, ov);
         } else if (16 * (pt0 + t8) + fr < kBnW) {
           bn_store16(yrow + 16 * t8 * kBnOut + 32 * h, ov);
         }
@@ -428,9 +433,15 @@ __global__ __launch_bounds__(64 * kBnNW, 1) void bneck_fused_kernel(BnParams p) 
     stamp(3);
     if (!(p.mode & 16)) bn_barrier();
     stamp(4);
-    if (!(p.mode & 2) && vc + 2 <= vlast) conv1(vc + 2);
-    stamp(5);
-    if (!(p.mode & 4)) conv3(vc, n, r);
+    if (p.mode & 512) {                            // A/B: conv3 (and its stores) first
+      if (!(p.mode & 4)) conv3(vc, n, r);
+      stamp(5);
+      if (!(p.mode & 2) && vc + 2 <= vlast) conv1(vc + 2);
+    } else {
+      if (!(p.mode & 2) && vc + 2 <= vlast) conv1(vc + 2);
+      stamp(5);
+      if (!(p.mode & 4)) conv3(vc, n, r);
+    }
     stamp(6);
     if (!(p.mode & 16)) bn_barrier();
     stamp(7);

@@ -390,24 +390,75 @@ class HopPlane:
                         pass
         return keys
 
+    # ---- stream ordering -------------------------------------------------------------------
+    def ready_event(self):
+        """An event on the current HIP stream (None off-GPU): recorded where a frame's tensors
+        were produced, it lets :meth:`encode` run from any other stream — another frame's lane,
+        the event-loop thread — and still copy / send them only once they are written."""
+        if self.device.type != "cuda":
+            return None
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        return ev
+
+    def _order_after(self, events) -> None:
+        if self.device.type != "cuda":
+            return
+        cur = torch.cuda.current_stream(self.device)
+        for ev in events:
+            if ev is not None:
+                cur.wait_event(ev)
+
+    def hold_inputs(self, values: dict):
+        """A frame's hop inputs made safe to send LATER from another stream (a frame waiting for
+        a credit): device tensors that are not frame-held (:func:`mark_frame_held`) are copied
+        into storage the queue owns — the producer may rewrite its buffer for its next frame —
+        and DeviceResults' device tensors likewise once their event passed.  Returns (values,
+        event after the copies) — the event goes to :meth:`encode` as ``ready``."""
+        from ..gpu.element import DeviceResult
+        if self.device.type != "cuda" or not isinstance(values, dict):
+            return values, None
+        cur = torch.cuda.current_stream(self.device)
+
+        def own(t):
+            return t.clone() if t.device.type == "cuda" and not _frame_held(t) else t
+
+        out = {}
+        for k, v in values.items():
+            if isinstance(v, torch.Tensor):
+                out[k] = own(v)
+            elif isinstance(v, DeviceResult):
+                if v.event is not None:
+                    cur.wait_event(v.event)
+                # host tensors (pinned HostRing sets) stay by reference: a set is reused only
+                # once the DeviceResult carrying it is dropped, and the queue holds it
+                out[k] = DeviceResult({n: own(t) if isinstance(t, torch.Tensor) else t for n, t in v.tensors.items()},
+                                      v.event, t_submit=v.t_submit, meta=v.meta)
+            else:
+                out[k] = v
+        return out, self.ready_event()
+
     # ---- encode (sender) -------------------------------------------------------------------
-    def encode(self, dst: int, values: dict, key=None) -> dict:
+    def encode(self, dst: int, values: dict, key=None, ready=None) -> dict:
         """``values`` with every tensor / DeviceResult / float replaced by tokens; the tensors
         are packed and sent to ``dst``.  ``key`` (forward hops): hold the staging slot until
         :meth:`ack` (raises :class:`NoCredit` when none is free).  Non-tensor values pass
-        through unchanged."""
-        return self._encode_many(dst, [values], key)[0]
+        through unchanged.  ``ready``: events of the streams that produced the tensors (see
+        :meth:`ready_event`); the staging copy and the send are ordered after them and after
+        every DeviceResult's own event.  Without them the tensors must come from the current
+        stream."""
+        return self._encode_many(dst, [values], key, ready)[0]
 
-    def encode_group(self, dst: int, values_list, keys=None) -> list:
+    def encode_group(self, dst: int, values_list, keys=None, ready=None) -> list:
         """Several messages (frames) toward ``dst`` in ONE transfer: one staging slot, one
         send, one per-link sequence number; returns one token dict per message.  ``keys``
         (forward hops, one per frame): the slot is ONE credit, held until every member is
         acknowledged or dropped — control-plane cost per frame falls with the group size."""
         if keys is None:
-            return self._encode_many(dst, values_list, None)
+            return self._encode_many(dst, values_list, None, ready)
         gk = ("group", self._group_seq)
         self._group_seq += 1
-        outs = self._encode_many(dst, values_list, gk)
+        outs = self._encode_many(dst, values_list, gk, ready)
         rec = self._held.get(gk)
         if rec is not None:
             rec[6] = {k: i for i, k in enumerate(keys)}
@@ -415,7 +466,7 @@ class HopPlane:
                 self._member_of[k] = gk
         return outs
 
-    def _encode_many(self, dst, values_list, key):
+    def _encode_many(self, dst, values_list, key, ready=None):
         from ..gpu.element import DeviceResult
         dst = int(dst)
         link = self.send_links.get(dst)
@@ -424,6 +475,7 @@ class HopPlane:
                 raise StageFailure(dst)
             raise RuntimeError(f"hop: no send link {self.rank} -> {dst} in this plan")
         tensors = []
+        events = list(ready or ())
 
         def tok(v):
             if isinstance(v, torch.Tensor):
@@ -438,6 +490,7 @@ class HopPlane:
             out = {}
             for k, v in values.items():
                 if isinstance(v, DeviceResult):
+                    events.append(v.event)
                     d = {RESULT_KEY: "1"}
                     t = v.t_submit
                     if isinstance(t, torch.Tensor):
@@ -466,6 +519,9 @@ class HopPlane:
         slot, buf = link.take(total, key if key is not None else (), staging=not direct)
         seq = link.seq
         link.seq += 1
+        # the copy below and the send (RCCL's stream waits on the current one) read the tensors:
+        # order the current stream after the streams that wrote them
+        self._order_after(events)
         if direct:
             buf = t0.reshape(-1).view(torch.uint8)
             self.counters["zero_copy"] += 1
@@ -479,8 +535,9 @@ class HopPlane:
                                + "x".join(map(str, shape)))
         self._post(link, slot, buf, total, dst)
         if key is not None:
-            # [dst, slot, total, specs, templates, buf, members (groups), slot reusable]
-            self._held[key] = [dst, slot, total, specs, outs, buf, None, True]
+            # [dst, slot, total, specs, templates, buf, members (groups), slot reusable,
+            #  event after the staging copy (a re-send from another stream waits on it)]
+            self._held[key] = [dst, slot, total, specs, outs, buf, None, True, self.ready_event()]
         else:
             link.release(slot)                       # ring slot: free once its transfer is done
         return outs
@@ -490,7 +547,9 @@ class HopPlane:
         if dst == self.rank:
             # loopback: the message's own copy of its bytes — the staging slot may be reused
             # (ring / ack) before the receiver decodes, so the queue must not alias it
-            self._loop.append(buf[:total].clone())
+            # (its event: the receiver's stream is ordered after this copy, as an RCCL receive is
+            # after the send it matches)
+            self._loop.append((buf[:total].clone(), self.ready_event()))
             link.work[slot] = None
         else:
             # the link's process group directly: tdist.isend re-validates group and rank per call
@@ -520,9 +579,10 @@ class HopPlane:
         slot, _ = link.take(0, key, staging=False)
         seq = link.seq
         link.seq += 1
+        self._order_after([rec[8]])                   # the bytes were staged on another stream
         self._post(link, slot, buf, total, dst)
         out = _retoken(templates[0], seq)
-        self._held[key] = [dst, slot, total, specs, [out], buf, None, True]
+        self._held[key] = [dst, slot, total, specs, [out], buf, None, True, rec[8]]
         self.counters["resent"] += 1
         return out
 
@@ -539,6 +599,7 @@ class HopPlane:
             rec = self._held[key]
         _dst, _slot, total, specs, templates, buf = rec[:6]
         offs, _ = _layout(specs)
+        self._order_after([rec[8]])                   # staged on another stream
         return self._materialize(templates[index], buf, offs)
 
     def _materialize(self, template, buf, offs):
@@ -699,7 +760,9 @@ class HopPlane:
         D._account("hop_recv", total)
         work = None
         if src == self.rank:
-            buf[:total].copy_(self._loop.popleft()[:total], non_blocking=True)
+            data, ev = self._loop.popleft()
+            self._order_after([ev])
+            buf[:total].copy_(data[:total], non_blocking=True)
         elif link.group is not None:
             try:
                 work = link.group.recv([buf[:total]], link.grank, 0)

@@ -741,16 +741,18 @@ class PipelineImpl(Pipeline):
         no receive slot is reused under them)."""
         hop = _hop.plane()
         groups: dict = {}
-        for topic, reply, info, data, stream, frame_id in batch:
-            groups.setdefault((topic, reply), []).append((info, data))
+        for topic, reply, info, data, ready, stream, frame_id in batch:
+            groups.setdefault((topic, reply), []).append((info, data, ready))
         try:
+            # this runs after the members' lane scopes closed: every member's response is
+            # ordered after the event recorded on its own lane when it completed
             for (topic, reply), items in groups.items():
                 proxy = get_actor_mqtt(topic, Pipeline)
                 if len(items) == 1:
-                    proxy.process_frame_response(items[0][0], hop.encode(reply, items[0][1]))
+                    proxy.process_frame_response(items[0][0], hop.encode(reply, items[0][1], ready=[items[0][2]]))
                 else:
-                    outs = hop.encode_group(reply, [data for _, data in items])
-                    proxy.process_frame_responses([info for info, _ in items], outs)
+                    outs = hop.encode_group(reply, [data for _, data, _ in items], ready=[r for *_, r in items])
+                    proxy.process_frame_responses([info for info, _, _ in items], outs)
         finally:
             for *_, stream, frame_id in batch:
                 self._release_frame(stream, frame_id)
@@ -1025,7 +1027,7 @@ class PipelineImpl(Pipeline):
                     if hop is not None and reply is not None and self._response_batch is not None:
                         # member of a group message: answered with the group, released after
                         self._response_batch.append((stream.topic_response, reply, stream_info, frame_data_out,
-                                                     stream, frame_id))
+                                                     hop.ready_event(), stream, frame_id))
                         frame_complete = False
                     else:
                         if hop is not None and reply is not None:
@@ -1195,10 +1197,12 @@ class PipelineImpl(Pipeline):
             return True
         return sum(1 for f in self._inflight.values() if f["target"] is proxy) < window
 
-    def _dispatch(self, element, target, node_name, stream_id, frame_id, inputs, held=False):
+    def _dispatch(self, element, target, node_name, stream_id, frame_id, inputs, held=False, ready=None):
         """Send frame ``(stream_id, frame_id)`` (paused at ``node_name``) to ``target``: metadata
         over MQTT, tensors over RCCL holding one of the target link's credits until the response
-        (``held``: the frame's bytes are already staged — a re-dispatch).  A LocalStage target runs
+        (``held``: the frame's bytes are already staged — a re-dispatch).  ``ready``: the event
+        of the stream that produced ``inputs`` when this runs from another stream (a queued
+        frame dispatched from another frame's lane or the event loop).  A LocalStage target runs
         in-process and resumes the frame through ``process_frame_response``."""
         key = (stream_id, frame_id)
         if isinstance(target, LocalStage):
@@ -1222,18 +1226,23 @@ class PipelineImpl(Pipeline):
             # metadata over MQTT, tensors over RCCL to the remote's rank
             stream_info["hop_rank"] = hop.rank
             try:
-                out = hop.resend(key, rank) if held else hop.encode(rank, inputs, key=key)
+                out = hop.resend(key, rank) if held else \
+                    hop.encode(rank, inputs, key=key, ready=None if ready is None else [ready])
             except _hop.StageFailure as exc:
                 self._replica_lost_rank(exc.peer)
                 if not held:
-                    self._queue_hop(element, node_name, stream_id, frame_id, inputs)
+                    self._queue_hop(element, node_name, stream_id, frame_id, inputs, ready=ready)
                 return
         self._inflight[key] = {"element": element, "target": target, "node": node_name, "rank": rank,
                                "inputs": inputs if rank is None else None, "t": time.monotonic()}
         self._watch_hops()
         target.process_frame(stream_info, **out)
 
-    def _queue_hop(self, element, node_name, stream_id, frame_id, inputs, held=False):
+    def _queue_hop(self, element, node_name, stream_id, frame_id, inputs, held=False, ready=None):
+        """Frame ``(stream_id, frame_id)`` waits for a credit of ``node_name``.  Its inputs are
+        sent later from whichever stream drains the queue, so they are captured here, on the
+        producing stream: tensors the producer may rewrite are copied into queue-owned
+        storage and an event marks them written (``ready``: inputs already captured)."""
         limit = int(self._param_float("remote_pending", 256))
         if self._pending_total() >= limit:
             self.frames_dropped += 1
@@ -1247,10 +1256,13 @@ class PipelineImpl(Pipeline):
             if lease is not None:
                 self._release_frame(lease.stream, frame_id)
             return
+        hop = _hop.plane()
+        if hop is not None and not held and ready is None:
+            inputs, ready = hop.hold_inputs(inputs)
         self._pending_hops.setdefault(node_name, deque()).append({
                                    "element": element, "node": node_name, "stream_id": stream_id,
                                    "frame_id": frame_id, "inputs": inputs, "held": held,
-                                   "t": time.monotonic()})
+                                   "ready": ready, "t": time.monotonic()})
         self._watch_hops()
 
     @property
@@ -1295,7 +1307,7 @@ class PipelineImpl(Pipeline):
                                 group.append(q)
                     if len(group) == 1:
                         self._dispatch(element, target, node_name, p["stream_id"], p["frame_id"], p["inputs"],
-                                       held=p["held"])
+                                       held=p["held"], ready=p.get("ready"))
                     else:
                         self._dispatch_group(element, target, node_name, group)
                 if not fifo and self._pending_hops.get(node_name) is fifo:
@@ -1313,11 +1325,13 @@ class PipelineImpl(Pipeline):
         rank = target.hop_rank
         keys = [(g["stream_id"], g["frame_id"]) for g in group]
         try:
-            outs = hop.encode_group(rank, [g["inputs"] for g in group], keys)
+            outs = hop.encode_group(rank, [g["inputs"] for g in group], keys,
+                                    ready=[g.get("ready") for g in group])
         except _hop.StageFailure as exc:
             self._replica_lost_rank(exc.peer)
             for g in group:
-                self._queue_hop(element, node_name, g["stream_id"], g["frame_id"], g["inputs"])
+                self._queue_hop(element, node_name, g["stream_id"], g["frame_id"], g["inputs"],
+                                ready=g.get("ready"))
             return
         now = time.monotonic()
         for key in keys:
