@@ -30,7 +30,8 @@ class TensorFrames(GpuPipelineElement):
         limit, found = self.get_parameter("frames")
         if found and limit:
             stream.variables["tensor_frames_left"] = int(limit)
-            self.create_frames(stream, self.frame_generator)
+            rate, _ = self.get_parameter("rate")          # frames per second (None: as fast as admitted)
+            self.create_frames(stream, self.frame_generator, rate=float(rate) if rate else None)
         return StreamEvent.OKAY, None
 
     def frame_generator(self, stream, frame_id):

@@ -31,6 +31,7 @@ __all__ = ["init", "is_initialized", "world_size", "rank", "local_rank", "barrie
 
 _backend = None
 _comm: dict = {}          # op -> [calls, bytes]
+_identity = None          # (rank, world) of a re-admitted rank: no default process group exists
 
 
 def _account(op: str, nbytes: int):
@@ -67,11 +68,24 @@ def is_initialized() -> bool:
 
 
 def world_size() -> int:
+    if _identity is not None:
+        return _identity[1]
     return tdist.get_world_size() if is_initialized() else 1
 
 
 def rank() -> int:
+    if _identity is not None:
+        return _identity[0]
     return tdist.get_rank() if is_initialized() else 0
+
+
+def set_identity(rank_: int, world: int, backend_name: str) -> None:
+    """A restarted rank re-admitted into a running plan (``parallel/launch.py`` supervisor): it
+    cannot join the original default process group, so its rank / world / backend are set
+    here and its hop links are fresh 2-rank groups (``HopPlane`` rejoin mode)."""
+    global _identity, _backend
+    _identity = (int(rank_), int(world))
+    _backend = backend_name
 
 
 def local_rank() -> int:

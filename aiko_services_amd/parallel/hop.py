@@ -45,6 +45,7 @@ tokens and are rebuilt (with a completion event) on the receiver.
 """
 from __future__ import annotations
 
+import datetime
 import weakref
 from collections import deque
 
@@ -265,7 +266,10 @@ class HopPlane:
     ``depth``: staging slots = credits per forward link = half the receive pool.
     """
 
-    def __init__(self, links, device=None, depth: int = 4):
+    def __init__(self, links, device=None, depth: int = 4, rejoin=None):
+        """``rejoin``: ``{"store": TCPStore client, "epoch": k}`` for a restarted rank joining a
+        running plan: no default-group collectives here; :meth:`connect_rejoin` then builds
+        its links as fresh 2-rank groups, as the survivors do in :meth:`readmit_connect`."""
         self.rank = D.rank()
         self.world = D.world_size()
         if device is None:
@@ -283,6 +287,19 @@ class HopPlane:
         self._waits = None                 # finish_later queue (host transfers), thread on first use
         self._member_of: dict = {}         # frame key -> group key (encode_group)
         self._group_seq = 0
+        self._rejoin = rejoin
+        self._readmit_callbacks: list = []  # fn(rank) after a restarted peer's links are back
+        self.epochs: dict = {}             # peer rank -> epoch of its current links (0: original)
+        self.counters = {"sent_msgs": 0, "sent_bytes": 0, "recv_msgs": 0, "recv_bytes": 0,
+                         "pool_overflow": 0, "pool_waits": 0, "resent": 0, "dead_peers": 0, "zero_copy": 0,
+                         "readmitted": 0}
+        if rejoin is not None:
+            for src, dst in self.links:
+                if src == dst == self.rank:
+                    self.send_links[dst] = _SendLink(dst, None, self.device, self.depth)
+                    self.recv_links[src] = _RecvLink(src, None, self.device, self.depth)
+            self.control = None
+            return
         for src, dst in self.links:
             if src == dst:
                 if src == self.rank:
@@ -313,8 +330,83 @@ class HopPlane:
             torch.cuda.synchronize(self.device)
         # host-side control group (gloo) for start-up barriers issued from helper threads
         self.control = tdist.new_group(backend="gloo") if D.is_initialized() else None
-        self.counters = {"sent_msgs": 0, "sent_bytes": 0, "recv_msgs": 0, "recv_bytes": 0,
-                         "pool_overflow": 0, "pool_waits": 0, "resent": 0, "dead_peers": 0, "zero_copy": 0}
+
+    # ---- re-admission of a restarted peer -----------------------------------------------------
+    def _pair_links(self, peer: int, store, epoch: int, timeout_s: float):
+        """Fresh 2-rank groups for every plan link between this rank and ``peer`` (a
+        ``PrefixStore`` per link and epoch on the running group's store), brought up with the
+        same one-element exchange as at start-up, in plan order on both sides.  Blocking."""
+        from torch.distributed import PrefixStore
+        backend = D.backend() or ("nccl" if self.device.type == "cuda" else "gloo")
+        timeout = datetime.timedelta(seconds=timeout_s)
+        send, recv, groups = {}, {}, {}
+        for src, dst in self.links:
+            if src == dst or {src, dst} != {self.rank, peer}:
+                continue
+            members = sorted({src, dst})
+            ps = PrefixStore(f"aiko/hop/epoch{epoch}/{src}-{dst}", store)
+            me = members.index(self.rank)
+            if backend == "nccl":
+                group = tdist.ProcessGroupNCCL(ps, me, 2, timeout)
+            else:
+                group = tdist.ProcessGroupGloo(ps, me, 2, timeout)
+            groups[(src, dst)] = group
+            other = members.index(peer)
+            t = torch.zeros(1, dtype=torch.int64, device=self.device)
+            if src == self.rank:
+                send[dst] = _SendLink(dst, group, self.device, self.depth, other)
+                group.send([t], other, 0).wait()
+            else:
+                recv[src] = _RecvLink(src, group, self.device, self.depth, other)
+                group.recv([t], other, 0).wait()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        return {"peer": peer, "epoch": epoch, "send": send, "recv": recv, "groups": groups}
+
+    def connect_rejoin(self, timeout_s: float = 120.0) -> list:
+        """Restarted rank: bring up its links to every peer (each survivor does its side in
+        :meth:`readmit_connect` once it hears the rejoin announcement).  Blocking; returns
+        the peers connected."""
+        if self._rejoin is None:
+            raise RuntimeError("hop: connect_rejoin on a plane that did not start in rejoin mode")
+        peers = []
+        for src, dst in self.links:
+            for peer in (src, dst):
+                if peer != self.rank and self.rank in (src, dst) and peer not in peers:
+                    peers.append(peer)
+        for peer in peers:
+            self.readmit_install(self._pair_links(peer, self._rejoin["store"], self._rejoin["epoch"], timeout_s))
+        return peers
+
+    def links_with(self, rank: int) -> bool:
+        return any(self.rank in (s, d) and int(rank) in (s, d) and s != d for s, d in self.links)
+
+    def readmit_connect(self, rank: int, epoch: int, timeout_s: float = 120.0):
+        """Survivor side of a restarted peer's links, on the running group's store (blocking:
+        run it off the actor thread, then :meth:`readmit_install` on it)."""
+        from .rendezvous import group_store
+        store = group_store()              # the raw TCPStore the restarted rank connects to
+        if store is None:
+            from torch.distributed.distributed_c10d import _get_default_store
+            store = _get_default_store()
+        return self._pair_links(int(rank), store, int(epoch), timeout_s)
+
+    def readmit_install(self, pending) -> None:
+        """Swap in a peer's fresh links (credits full, sequence numbers 0) and forget that it
+        was dead; then tell the listeners (the engine re-adds the peer's replica)."""
+        peer = pending["peer"]
+        self.send_links.update(pending["send"])
+        self.recv_links.update(pending["recv"])
+        self._groups.update(pending["groups"])
+        self.epochs[peer] = pending["epoch"]
+        if peer in self.dead:
+            self.dead.discard(peer)
+            self.counters["readmitted"] += 1
+        for fn in list(self._readmit_callbacks):
+            fn(peer)
+
+    def on_readmit(self, fn) -> None:
+        self._readmit_callbacks.append(fn)
 
     # ---- credits / failure ------------------------------------------------------------------
     def credit(self, dst: int) -> int:
@@ -822,8 +914,8 @@ class HopPlane:
             torch.cuda.synchronize(self.device)
 
 
-def init_plane(links, device=None, depth: int = 4) -> HopPlane:
-    p = HopPlane(links, device=device, depth=depth)
+def init_plane(links, device=None, depth: int = 4, rejoin=None) -> HopPlane:
+    p = HopPlane(links, device=device, depth=depth, rejoin=rejoin)
     set_plane(p)
     return p
 

@@ -19,6 +19,17 @@ in the reference is by hand, ``examples/pipeline/multitude/run_large.sh``):
 
 Frames then flow as in the reference — ``process_frame`` to the remote, ``process_frame_
 response`` back — with the tensors on xGMI.  Workers exit when their parent process goes.
+
+Supervision (``AIKO_SUPERVISE=N``: up to N restarts per rank): the ProcessManager's exit
+callback restarts a worker that died as a FRESH child process (never an exec of a process that
+touched the GPU) with ``AIKO_REJOIN_EPOCH`` / ``AIKO_REJOIN_STORE``.  The restarted rank cannot
+join the original default process group, so :func:`rejoin` gives it its identity, announces
+``(rejoin rank epoch)`` on ``{namespace}/rendezvous/{group}/rejoin`` and brings its hop links up
+as fresh 2-rank groups on the running group's TCPStore; every survivor with a link to it does
+its side (:func:`_on_rejoin`), and rank 0's engine re-adds the replica only once those links are
+up (reference model: a re-appearing remote is re-bound on the registrar ``add``,
+``/root/reference/src/aiko_services/main/pipeline.py:985-1006``; process supervision as in
+``/root/reference/src/aiko_services/main/lifecycle.py:144-288``).
 """
 from __future__ import annotations
 
@@ -42,26 +53,64 @@ def backend_for() -> str:
     return "nccl" if torch.cuda.is_available() else "gloo"
 
 
-def spawn_workers(plan: Plan, plan_path: str | None = None, env: dict | None = None):
-    """Start ranks 1..world-1 (``python -m aiko_services_amd.parallel.launch worker``)."""
+def spawn_workers(plan: Plan, plan_path: str | None = None, env: dict | None = None,
+                  max_restarts: int | None = None):
+    """Start ranks 1..world-1 (``python -m aiko_services_amd.parallel.launch worker``);
+    ``max_restarts`` (default ``AIKO_SUPERVISE``, 0) per rank: see the module docstring."""
     from ..control.process_manager import ProcessManager
     if plan_path is None:
         fd, plan_path = tempfile.mkstemp(prefix="aiko_plan_", suffix=".json")
         with os.fdopen(fd, "w") as f:
             f.write(plan.to_json())
-    manager = ProcessManager()
     base_env = dict(os.environ if env is None else env)
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     base_env["PYTHONPATH"] = root + os.pathsep + base_env.get("PYTHONPATH", "")
-    for spec in plan.ranks:
-        if spec.rank == 0:
-            continue
-        child = dict(base_env, LOCAL_RANK=str(spec.device), RANK=str(spec.rank),
-                     WORLD_SIZE=str(plan.world), AIKO_PARENT_PID=str(os.getpid()))
+    if max_restarts is None:
+        max_restarts = int(base_env.get("AIKO_SUPERVISE", "0") or 0)
+    state = {"stopping": False, "restarts": {}}
+
+    def child_env(spec, epoch=0):
+        e = dict(base_env, LOCAL_RANK=str(spec.device), RANK=str(spec.rank),
+                 WORLD_SIZE=str(plan.world), AIKO_PARENT_PID=str(os.getpid()))
+        if epoch:
+            from .rendezvous import store_address
+            host, port = store_address()
+            e.update(AIKO_REJOIN_EPOCH=str(epoch), AIKO_REJOIN_STORE=f"{host}:{port}")
+            e.pop("AIKO_FAULTS", None)          # an injected fault is not re-injected
+        return e
+
+    def start(spec, epoch=0):
         manager.create(f"rank{spec.rank}", sys.executable,
                        ["-m", "aiko_services_amd.parallel.launch", "worker", plan_path, str(spec.rank)],
-                       env=child)
-    atexit.register(manager.terminate_all)
+                       env=child_env(spec, epoch))
+
+    def on_exit(id, data):
+        """ProcessManager monitor thread: a worker exited."""
+        if state["stopping"] or not str(id).startswith("rank"):
+            return
+        rank = int(str(id)[4:])
+        n = state["restarts"].get(rank, 0)
+        from .rendezvous import store_address
+        if n >= max_restarts or store_address() is None:
+            if max_restarts:
+                print(f"aiko supervisor: rank {rank} exited ({data.get('return_code')}), not restarted "
+                      f"({n} restarts)", file=sys.stderr, flush=True)
+            return
+        state["restarts"][rank] = n + 1
+        print(f"aiko supervisor: rank {rank} exited ({data.get('return_code')}): restarting it, epoch {n + 1}",
+              file=sys.stderr, flush=True)
+        start(plan.ranks[rank], epoch=n + 1)
+
+    manager = ProcessManager(process_exit_handler=on_exit)
+    manager.supervisor_state = state
+    for spec in plan.ranks:
+        if spec.rank != 0:
+            start(spec)
+
+    def stop():
+        state["stopping"] = True
+        manager.terminate_all()
+    atexit.register(stop)
     atexit.register(lambda: os.path.exists(plan_path) and os.unlink(plan_path))
     return manager, plan_path
 
@@ -78,6 +127,88 @@ def join(plan: Plan, rank: int, timeout_s: float = 120.0):
         rendezvous_init(plan.group, rank, plan.world, host, port, backend=backend, timeout_s=timeout_s)
     depth = int(os.environ.get("AIKO_HOP_DEPTH", "4"))
     plane = hop.init_plane(plan.links, depth=depth)
+    _listen_rejoin(plan, plane)
+
+    def report():
+        print(f"hop rank {rank} stats: {plane.stats()}", file=sys.stderr, flush=True)
+    atexit.register(report)
+    return plane
+
+
+def _rejoin_topic(plan: Plan) -> str:
+    from .rendezvous import rendezvous_topic
+    return rendezvous_topic(plan.group) + "/rejoin"
+
+
+def _listen_rejoin(plan: Plan, plane) -> None:
+    """Every rank: on ``(rejoin rank epoch)`` for a peer this rank has links with, bring those
+    links up again (off the event loop: it blocks until the peer's side connects), then swap
+    them in on the event loop."""
+    from ..runtime import event
+    from ..runtime.process import aiko
+    from ..utils.sexpr import parse
+
+    def handler(_aiko, _topic, payload):
+        try:
+            cmd, params = parse(payload)
+            peer, epoch = int(params[0]), int(params[1])
+        except Exception:                               # noqa: BLE001 — not ours
+            return False
+        if cmd != "rejoin" or peer == plane.rank or not plane.links_with(peer) \
+                or plane.epochs.get(peer, 0) >= epoch:
+            return False
+
+        def work():
+            deadline = time.time() + 30.0
+            while peer not in plane.dead and time.time() < deadline:
+                time.sleep(0.05)                        # its death reaches this rank first
+            try:
+                pending = plane.readmit_connect(peer, epoch)
+            except Exception as exc:                    # noqa: BLE001
+                print(f"hop rank {plane.rank}: re-admitting rank {peer} failed: {exc}", file=sys.stderr, flush=True)
+                return
+            event.call_soon(plane.readmit_install, pending)
+        threading.Thread(target=work, daemon=True, name=f"hop-readmit-{peer}").start()
+        return False
+    aiko.process.add_message_handler(handler, _rejoin_topic(plan))
+
+
+def rejoin(plan: Plan, rank: int, timeout_s: float = 120.0):
+    """A restarted rank (``AIKO_REJOIN_EPOCH`` / ``AIKO_REJOIN_STORE``): identity without a
+    default process group, a hop plane in rejoin mode, the announcement, then (helper thread)
+    its links as fresh 2-rank groups.  The stage pipeline is created meanwhile; the survivors
+    only route frames to it once the links are up."""
+    from ..message.mqtt_client import MQTTClient
+    from ..utils.configuration import get_mqtt_host
+    from ..utils.sexpr import generate
+    from . import dist as D
+    from . import hop
+    from .rendezvous import connect_store
+    os.environ.setdefault("LOCAL_RANK", str(plan.ranks[rank].device))
+    epoch = int(os.environ["AIKO_REJOIN_EPOCH"])
+    backend = backend_for()
+    if backend == "nccl":
+        import torch
+        torch.cuda.set_device(torch.device("cuda", D.local_rank() % max(1, torch.cuda.device_count())))
+    D.set_identity(rank, plan.world, backend)
+    store = connect_store(os.environ["AIKO_REJOIN_STORE"], timeout_s)
+    depth = int(os.environ.get("AIKO_HOP_DEPTH", "4"))
+    plane = hop.init_plane(plan.links, depth=depth, rejoin={"store": store, "epoch": epoch})
+    _listen_rejoin(plan, plane)
+    _, host, port = get_mqtt_host()
+    client = MQTTClient(client_id=f"aiko-rejoin-{rank}-{epoch}")
+    client.connect(host, port)
+    client.publish(_rejoin_topic(plan), generate("rejoin", [rank, epoch]), qos=1, wait=True)
+    time.sleep(0.05)
+    client.disconnect()
+
+    def connect():
+        try:
+            peers = plane.connect_rejoin(timeout_s)
+            print(f"hop rank {rank}: re-admitted (epoch {epoch}), links to {peers}", file=sys.stderr, flush=True)
+        except Exception as exc:                        # noqa: BLE001
+            print(f"hop rank {rank}: rejoin failed: {exc}", file=sys.stderr, flush=True)
+    threading.Thread(target=connect, daemon=True, name="hop-rejoin").start()
 
     def report():
         print(f"hop rank {rank} stats: {plane.stats()}", file=sys.stderr, flush=True)
@@ -88,7 +219,7 @@ def join(plan: Plan, rank: int, timeout_s: float = 120.0):
 def create_rank_pipeline(plan: Plan, rank: int, stream_id=None, parameters=None, frame_id=0,
                          frame_data=None, grace_time=60, queue_response=None, name=None,
                          graph_path=None, stream_reset=False, definition_pathname="<parallel>",
-                         auto_start=True):
+                         auto_start=True, extra_tags=()):
     """This rank's stage Pipeline; on rank 0 also binds replicated / local stage members.
     ``auto_start``: a helper thread waits until the stage is ready, joins the start barrier and
     (rank 0) creates the stream — embedders that drive frames themselves pass False."""
@@ -103,7 +234,7 @@ def create_rank_pipeline(plan: Plan, rank: int, stream_id=None, parameters=None,
         grace_time = int(plan.stream.get("grace_time", grace_time))
     pipeline = PipelineImpl.create_pipeline(definition_pathname, definition, name or spec.name, graph_path,
                                             None, [], frame_id, None, grace_time,
-                                            queue_response=queue_response, tags=list(spec.tags))
+                                            queue_response=queue_response, tags=list(spec.tags) + list(extra_tags))
     if plan.mode != "dp" and spec.stage + 1 < len(plan.stages):
         remote = f"Stage{spec.stage + 1}"
         local_def = None
@@ -207,8 +338,14 @@ def worker_main(argv=None):
     with open(argv[1]) as f:
         plan = Plan.from_json(f.read())
     rank = int(argv[2])
-    join(plan, rank)
-    pipeline = create_rank_pipeline(plan, rank)
+    if os.environ.get("AIKO_REJOIN_EPOCH"):
+        rejoin(plan, rank)
+        # no start barrier (the original group started long ago): the stage just serves
+        pipeline = create_rank_pipeline(plan, rank, auto_start=False,
+                                        extra_tags=[f"epoch={os.environ['AIKO_REJOIN_EPOCH']}"])
+    else:
+        join(plan, rank)
+        pipeline = create_rank_pipeline(plan, rank)
     _watch_parent()
     if os.environ.get("AIKO_WORKER_SAMPLE"):             # sampled main-thread stacks -> DIR/worker_R.txt
         _sample_main_thread(os.path.join(os.environ["AIKO_WORKER_SAMPLE"], f"worker_{rank}.txt"))

@@ -26,7 +26,27 @@ from ..utils.configuration import get_namespace
 from ..utils.sexpr import generate, parse
 from . import dist as D
 
-__all__ = ["rendezvous_topic", "rendezvous_init", "free_port"]
+__all__ = ["rendezvous_topic", "rendezvous_init", "free_port", "store_address", "connect_store"]
+
+_STORE_ADDR = None        # (host, port) of the group's TCPStore (rank 0 is its master)
+_STORE = None             # this rank's handle on it (re-admission groups use raw keys on it)
+
+
+def group_store():
+    """This rank's TCPStore of the MQTT-bootstrapped group (None: not bootstrapped here)."""
+    return _STORE
+
+
+def store_address():
+    """(host, port) of this process's group store, or None: what a restarted rank connects to
+    (the rank-0 supervisor passes it in ``AIKO_REJOIN_STORE``)."""
+    return _STORE_ADDR
+
+
+def connect_store(address: str, timeout_s: float = 60.0):
+    """A client of the running group's TCPStore (``host:port``), for a re-admitted rank."""
+    host, port = address.rsplit(":", 1)
+    return tdist.TCPStore(host, int(port), is_master=False, timeout=datetime.timedelta(seconds=timeout_s))
 
 
 def rendezvous_topic(group: str) -> str:
@@ -77,6 +97,8 @@ def rendezvous_init(group: str, rank: int, world_size: int, mqtt_host="127.0.0.1
             port = free_port("0.0.0.0" if host != "127.0.0.1" else "127.0.0.1")
             store = tdist.TCPStore(host, port, world_size, is_master=True, wait_for_workers=False,
                                    timeout=datetime.timedelta(seconds=timeout_s))
+            global _STORE_ADDR
+            _STORE_ADDR = (host, port)
             client.publish(topic, generate("rendezvous", [group, host, port, world_size, uuid.uuid4().hex[:8]]),
                            retain=True, qos=1, wait=True)
         else:
@@ -85,6 +107,8 @@ def rendezvous_init(group: str, rank: int, world_size: int, mqtt_host="127.0.0.1
                 raise TimeoutError(f"rendezvous {group}: no leader on {topic} after {timeout_s}s")
             store = tdist.TCPStore(got["host"], got["port"], world_size, is_master=False,
                                    timeout=datetime.timedelta(seconds=timeout_s))
+        global _STORE
+        _STORE = store
         kwargs = {}
         if backend == "nccl":
             dev = torch.device("cuda", D.local_rank() % max(1, torch.cuda.device_count()))

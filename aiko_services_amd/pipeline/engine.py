@@ -363,6 +363,8 @@ class PipelineImpl(Pipeline):
         self.hop_groups = 0                # group messages sent (hop_batch > 1)
         self._draining = False
         self._response_batch = None        # replica: responses of a group message, sent as one
+        self._deferred_adds: dict = {}     # hop rank -> registrar add of a restarted replica
+        self._readmit_hooked = False
         self.pipeline_graph = self._create_pipeline_graph(context.definition)
         self.share["element_count"] = self.pipeline_graph.element_count
         self.share["streams"] = 0
@@ -542,12 +544,33 @@ class PipelineImpl(Pipeline):
         if command == "add":
             tags = ServiceTags.parse_tags(service_details[5] if len(service_details) > 5
                                           and isinstance(service_details[5], list) else [])
+            rank = tags.get("rank")
+            hop = _hop.plane()
+            if hop is not None and rank not in (None, "") and hop.is_dead(int(rank)):
+                # a restarted replica on a rank whose links were retired: it stays absent until
+                # its fresh links are up (parallel/launch.py rejoin), then this add runs again
+                self._deferred_adds[int(rank)] = (command, service_details)
+                if not self._readmit_hooked:
+                    hop.on_readmit(lambda peer: self._post_message(
+                        ActorTopic.IN, "hop_readmitted", [peer], target_function=self._hop_readmitted))
+                    self._readmit_hooked = True
+                self.logger.info(f"remote {element_name}: rank {rank} re-registered "
+                                 f"(epoch {tags.get('epoch', '?')}): waiting for its data-plane links")
+                return
             proxy = get_actor_mqtt(topic_path, PipelineRemote)
             proxy.definition = element_instance.definition
-            rank = tags.get("rank")
             proxy.hop_rank = int(rank) if rank not in (None, "") else None
             replicas.add(topic_path, proxy, weight=float(tags.get("weight", 1) or 1))
             element_instance.set_remote_absent(False)
+            # a member that appears while streams run (a restarted replica, a late registrar add)
+            # gets each of them first: on its topic the create_stream precedes any frame
+            for sid, lease in list(self.stream_leases.items()):
+                st = lease.stream
+                on_path = any(PipelineGraph.get_element(n)[1] == element_name
+                              for n in self.pipeline_graph.get_path(Graph.path_local(st.graph_path)))
+                if on_path:
+                    proxy.create_stream(sid, Graph.path_remote(st.graph_path), st.parameters,
+                                        getattr(lease, "grace_time", GRACE_TIME), None, self.topic_in)
         else:
             if topic_path not in replicas._members:
                 return
@@ -561,6 +584,15 @@ class PipelineImpl(Pipeline):
             element_instance.set_remote_absent(True)
             node.element = element_instance
         self._update_lifecycle_state()
+
+    def _hop_readmitted(self, rank):
+        """A restarted peer's hop links are up again: its deferred registrar add now binds it."""
+        pending = self._deferred_adds.pop(int(rank), None)
+        if pending is not None:
+            self.logger.info(f"hop rank {rank} re-admitted: replica bound again")
+            self._pipeline_element_change_handler(*pending)
+            if self._pending_hops:
+                self._drain_pending()
 
     # ---- streams -------------------------------------------------------------------------------
     def create_stream(self, stream_id, graph_path=None, parameters=None, grace_time=GRACE_TIME,
@@ -583,6 +615,7 @@ class PipelineImpl(Pipeline):
             self.logger.error(f"Create stream: Unknown Pipeline Graph Path: {graph_path}")
             return False
         lease = Lease(int(float(grace_time)), stream_id, lease_expired_handler=self.destroy_stream)
+        lease.grace_time = grace_time
         lease.stream = Stream(stream_id=stream_id, graph_path=graph_path,
                               parameters=parameters if isinstance(parameters, dict) else {},
                               queue_response=queue_response, topic_response=topic_response)

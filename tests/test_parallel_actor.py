@@ -301,3 +301,35 @@ def test_hop_group_loopback_credit_and_shared_slot():
     assert handle.count == 1 and pool.free_count() == free0
     plane.release([handle])
     assert handle.count == 0 and plane.stats()["held_frames"] == 0
+
+
+def test_restarted_replica_is_readmitted(cluster):
+    """rank 2 (a stage-1 replica of tensor_ppdp.json) dies after its 2nd
+    frame; the supervisor (``AIKO_SUPERVISE``) restarts it as a fresh process, which re-joins the
+    running plan (fresh 2-rank hop links on the group's store, announced over MQTT) — rank 0
+    keeps it absent until those links are up, then binds it again, and frames after the
+    restart are served by the new rank-2 process.  Every output matches the single-process
+    run (reference: a re-appearing remote is re-bound on the registrar add,
+    /root/reference/src/aiko_services/main/pipeline.py:985-1006)."""
+    frames = 96
+    path, d = _variant(os.path.join(DEFS, "tensor_ppdp.json"), frames=frames, rate=12, hop_timeout=30)
+    env = dict(cluster["env"], AIKO_FAULTS="kill=2@rank2", AIKO_SUPERVISE="1", AIKO_LOG_LEVEL="INFO")
+    try:
+        r, par = _create(env, path, frames, timeout=170)
+    finally:
+        os.unlink(path)
+    text = r.stdout + r.stderr
+    assert len(par) == frames, (r.returncode, text[-4000:])
+    assert "rank 2 exited" in text and "restarting it, epoch 1" in text, text[-3000:]
+    assert "hop rank 2: re-admitted (epoch 1)" in text, text[-3000:]
+    rank0 = re.search(r"hop rank 0 stats: (\{.*\})", text)
+    assert rank0 and "'readmitted': 1" in rank0.group(1) and "'dead'" not in rank0.group(1), text[-3000:]
+    # stage-1 traffic by destination topic, in order of first use: rank 1, the first rank-2
+    # process, then the restarted rank-2 process (a new topic: new pid)
+    sent = {}
+    for topic, p in cluster["payloads"]:
+        if (p.startswith(b"(process_frame ") or p.startswith(b"(process_frames ")) and b"T@0/" in p:
+            sent[topic] = sent.get(topic, 0) + 1
+    assert len(sent) == 3, sent
+    assert list(sent.values())[-1] >= 3, sent          # the restarted replica served frames
+    assert _single(cluster, d, frames) == par
