@@ -30,6 +30,15 @@ def _int(v, d):
         return d
 
 
+def spmd(element) -> bool:
+    """Whether the element's pipeline runs SPMD (``parallel: {mode: dp}``): its collectives
+    pair up across ranks.  A replicated-stage plan of the same definition
+    (``parallel: {mode: dp, replicated: true}``, ``parallel/placement.py``) sets the pipeline
+    parameter ``spmd`` false: every frame then visits ONE replica, so fan-out / gather are
+    pass-throughs."""
+    return str(element.get_parameter("spmd", True)[0]).lower() not in ("false", "0", "no")
+
+
 def _bool(v):
     return str(v).lower() in ("true", "1", "yes")
 
@@ -50,7 +59,7 @@ class FrameFanout(GpuPipelineElement):
     def process_frame(self, stream, images=None):
         from ...parallel import dist as D
         ws, rank = D.world_size(), D.rank()
-        if ws == 1:
+        if ws == 1 or not spmd(self):
             return StreamEvent.OKAY, {"images": images}
         B = _int(self.get_parameter("batch", 1)[0], 1)
         H = _int(self.get_parameter("height", 480)[0], 480)
@@ -146,7 +155,7 @@ class DetectionsGather(GpuPipelineElement):
 
     def process_frame(self, stream, detections, counts, t_submit=None):
         from ...parallel import dist as D
-        world = D.world_size() if self.gather else 1
+        world = D.world_size() if self.gather and spmd(self) else 1
         b = self._buffers(tuple(detections.shape), world)
         det, cnt = detections, counts
         if world > 1:

@@ -81,7 +81,8 @@ class SyntheticFrames(GpuPipelineElement):
             self.frame_pool.release_after(s)
 
     def _frames(self):
-        glob = str(self.get_parameter("global", False)[0]).lower() in ("true", "1", "yes")
+        glob = str(self.get_parameter("global", False)[0]).lower() in ("true", "1", "yes") \
+            and str(self.get_parameter("spmd", True)[0]).lower() not in ("false", "0", "no")
         if glob:
             # data-parallel ingest: rank ``src`` decodes the node's whole batch (N x batch),
             # the other ranks get theirs from FrameFanout
@@ -102,6 +103,11 @@ class SyntheticFrames(GpuPipelineElement):
     def start_stream(self, stream, stream_id):
         limit, found = self.get_parameter("frames")
         if found and limit:
+            if self.pipeline is not None and hasattr(self.pipeline, "limit_frames"):
+                # the credit window must be known before the generator admits its first frame
+                # (the pool itself is made on the first frame): else a burst of admitted frames
+                # waits on the actor thread for slots only their own responses could free
+                self.pipeline.limit_frames(self.name, max(1, _int(self.get_parameter("pool", 2)[0], 2)))
             stream.variables["synthetic_left"] = int(limit)
             rate, _ = self.get_parameter("rate", None)
             self.create_frames(stream, self.frame_generator, rate=float(rate) if rate else None)

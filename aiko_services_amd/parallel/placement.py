@@ -213,6 +213,36 @@ def _dp_plan(definition: dict, gpus: int, group: str | None) -> Plan:
                 local_share=0.0, ranks=ranks, links=[])
 
 
+def _dp_replicated_plan(definition: dict, gpus: int, group: str | None) -> Plan:
+    """``mode: dp`` + ``replicated: true`` — data parallelism on the replicated-stage
+    machinery instead of SPMD collectives: stage 0 = the ingest prefix (through the fan-out
+    element, or the source alone) on rank 0; stage 1 = the rest, one replica per other GPU
+    plus rank 0's local share (``local_share`` = rank 0's fraction of the frames, default
+    1 / gpus: rank 0 detects as much as each replica).  Frames are dealt to replicas by the hop credits; a dead replica's frames are
+    re-dispatched to the survivors (``pipeline/engine.py`` ``_replica_lost``) instead of
+    hanging a collective, and a restarted one is re-admitted.  The definition's collective
+    elements become pass-throughs (pipeline parameter ``spmd`` false: each frame visits one
+    replica).  BASELINE config 4's topology with rank loss survivable; plain ``mode: dp``
+    keeps the SPMD fast path."""
+    par = definition.get("parallel") or {}
+    order = element_order(definition)
+    by = {e["name"]: e for e in definition["elements"]}
+
+    def cls(n):
+        return by[n]["deploy"].get("local", {}).get("class_name") or n
+    cut = next((i for i, n in enumerate(order) if cls(n) == "FrameFanout"), 0) + 1
+    cut = min(cut, len(order) - 1)
+    d = copy.deepcopy(definition)
+    d["parameters"] = dict(d.get("parameters") or {}, spmd=False)
+    d["parallel"] = {k: v for k, v in par.items() if k not in ("mode", "replicated")}
+    d["parallel"]["mode"] = "pp"
+    for e in d["elements"]:
+        e.get("deploy", {}).get("local", {}).pop("stage", None)
+    share = float(par.get("local_share", 1.0 / max(1, gpus)))
+    return make_plan(d, gpus=gpus, stages=[order[:cut], order[cut:]], replicas=[1, max(0, gpus - 1)],
+                     local_share=share if gpus > 1 else 1.0, group=group)
+
+
 def boundary_ms_from_bytes(boundary_bytes: dict, link_gbps: float) -> dict:
     """Transfer cost of each element's output over one xGMI link: ``bytes / link rate`` (ms
     per frame batch) — the balancer's ``boundary_ms``."""
@@ -228,6 +258,8 @@ def make_plan(definition: dict, gpus: int | None = None, stages=None, replicas=N
     par = definition.get("parallel") or {}
     mode = par.get("mode", "pp")
     gpus = int(gpus or par.get("gpus", 1))
+    if mode == "dp" and par.get("replicated"):
+        return _dp_replicated_plan(definition, gpus, group)
     if mode == "dp":
         return _dp_plan(definition, gpus, group)
     if replicas is None and par.get("replicas") is not None:

@@ -333,3 +333,38 @@ def test_restarted_replica_is_readmitted(cluster):
     assert len(sent) == 3, sent
     assert list(sent.values())[-1] >= 3, sent          # the restarted replica served frames
     assert _single(cluster, d, frames) == par
+
+
+@pytest.mark.parametrize("kill", [False, True])
+def test_dp_replicated_survives_rank_loss(cluster, kill):
+    """config 4's DP shape (ingest -> fan-out -> detector -> gather) as
+    ``parallel: {mode: dp, replicated: true}``: rank 0 ingests, each frame batch goes to ONE
+    detector replica (ranks 1, 2 or rank 0's local share) over hop credits.  With
+    ``kill=2@rank2`` one replica dies mid-stream; its frames are re-dispatched and every frame
+    completes with the single-process values (SPMD ``mode: dp`` would hang its collectives)."""
+    frames = 12
+    path, d = _variant(os.path.join(DEFS, "tensor_dp3_replicated.json"), frames=frames, hop_timeout=30)
+    env = dict(cluster["env"], AIKO_LOG_LEVEL="INFO")
+    if kill:
+        env["AIKO_FAULTS"] = "kill=2@rank2"
+    try:
+        t0 = time.time()
+        r, par = _create(env, path, frames, timeout=150)
+        elapsed = time.time() - t0
+    finally:
+        os.unlink(path)
+    text = r.stdout + r.stderr
+    assert len(par) == frames, (r.returncode, text[-4000:])
+    assert elapsed < 120
+    sent = {}
+    for topic, p in cluster["payloads"]:
+        if p.startswith(b"(process_frame ") and b"T@0/" in p:
+            sent[topic] = sent.get(topic, 0) + 1
+    assert len(sent) == 2, sent                       # both remote replicas got frames
+    if kill:
+        rank0 = re.search(r"hop rank 0 stats: (\{.*\})", text)
+        assert rank0 and "'dead': [2]" in rank0.group(1), text[-3000:]
+    # SyntheticFrames serves pre-filled pool slots in completion order, so which slot a frame id
+    # gets depends on timing: every parallel output must be one of the single-process outputs
+    single = _single(cluster, d, frames)
+    assert set(par.values()) <= set(single.values()), (par, single)
