@@ -47,3 +47,32 @@ def test_frame_pool_under_sanitizers(tmp_path, san):
     assert "ERROR: AddressSanitizer" not in out and "runtime error" not in out
     assert "WARNING: ThreadSanitizer" not in out, out[-4000:]
     assert "bad=0" in out
+
+
+def test_sexpr_codec_under_asan_ubsan(tmp_path):
+    """the native S-expression codec parses every inbound MQTT payload, so
+    it runs here built with ``-fsanitize=address,undefined`` (the CPython extension, loaded
+    into an uninstrumented interpreter with the ASan runtime preloaded and PYTHONMALLOC=malloc
+    so Python objects are ASan allocations too) over a seeded random corpus, deep nesting past
+    the 512 limit, huge / malformed canonical lengths and long tokens, each result compared
+    with the pure-Python codec (tests/native/sexpr_asan_driver.py)."""
+    import sysconfig
+    src = ROOT / "aiko_services_amd" / "csrc" / "host" / "sexpr.c"
+    so = tmp_path / "_sexpr.so"
+    cc = "gcc"
+    cmd = [cc, "-O1", "-g", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+           "-fno-sanitize-recover=undefined", "-shared", "-fPIC", "-I", sysconfig.get_paths()["include"],
+           str(src), "-o", str(so)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        pytest.fail(f"sanitizer build failed:\n{r.stderr[-3000:]}")
+    asan = subprocess.run([cc, "-print-file-name=libasan.so"], capture_output=True, text=True).stdout.strip()
+    env = dict(os.environ, LD_PRELOAD=asan, PYTHONMALLOC="malloc",
+               ASAN_OPTIONS="detect_leaks=0:abort_on_error=0:verify_asan_link_order=0",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([sys.executable, str(ROOT / "tests" / "native" / "sexpr_asan_driver.py"), str(so), str(ROOT)],
+                       capture_output=True, text=True, timeout=600, env=env)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "ERROR: AddressSanitizer" not in out and "runtime error" not in out, out[-4000:]
+    assert "SEXPR_ASAN_OK" in out, out[-2000:]

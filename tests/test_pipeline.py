@@ -670,3 +670,31 @@ def test_destroy_stream_returns_admission_credits(aiko_process):
     event.call_on_loop(lambda: pipeline.create_stream("w3"))
     event.call_on_loop(lambda: pipeline.destroy_stream("w3"))
     assert not any(k[0] == "w3" for k in pipeline._admitted)
+
+
+def test_dict_swag_never_enters_hop_decode(aiko_process, monkeypatch):
+    """with a hop data plane up, reference-style frames whose swag holds
+    plain nested dicts (no tensor tokens, no encoded DeviceResult, no hop_rank) are never
+    handed to ``HopPlane.decode`` — only messages that went through ``HopPlane.encode`` are."""
+    from aiko_services_amd.parallel import hop, hop_state
+    assert not hop_state.needs_decode({"stream_id": "1", "frame_id": 0}, {"b": {"x": 1, "y": [1, 2]}})
+    assert not hop_state.needs_decode({}, {"s": "T not a token", "m": {"k": "v"}})
+    assert hop_state.needs_decode({"hop_rank": 0}, {})
+    assert hop_state.needs_decode({}, {"x": "T@0/0/0/float32/2x3"})
+    assert hop_state.needs_decode({}, {"r": {hop_state.RESULT_KEY: "1"}})
+    plane = hop.init_plane([(0, 0)], device="cpu", depth=2)
+    calls = []
+
+    def boom(*a, **k):
+        calls.append(a)
+        raise AssertionError("hop.decode called for a plain reference frame")
+    monkeypatch.setattr(hop.HopPlane, "decode", boom)
+    monkeypatch.setattr(hop.HopPlane, "decode_async", boom)
+    try:
+        pipeline, q = _create(DIAMOND, stream_id="sw")
+        pipeline.create_frame({"stream_id": "sw", "frame_id": 0}, {"b": 2, "meta": {"camera": {"id": 3}}})
+        info, data = q.get(timeout=5)
+        assert info["state"] == 0 and "f" in data and not calls
+    finally:
+        hop.shutdown_plane()
+    assert hop_state.plane() is None
