@@ -8,6 +8,10 @@
   like a hardware decoder writing into device memory; no host upload on the hot path).  In a
   stream it can also run as a frame generator (``frames``, ``rate``).  With ``global: true``
   only rank ``src`` produces frames — ``world x batch`` of them — for a FrameFanout.
+* ``FrameUpload`` — host frames (a decoder / camera / file reader in host memory, or
+  ``SyntheticFrames`` with ``host: true``) -> a FramePool slot in HBM: pinned staging, the
+  H2D copy on the element's own copy stream (it overlaps the previous frames' compute), the
+  frame's lane ordered after it by an event, the slot held until the frame completes.
 * ``ImagePreprocess`` — fused bilinear resize + ImageNet normalise + NHWC->padded-4-channel
   layout in one HIP kernel (output: the ResNet stem buffer).
 * ``ResNet50Classifier`` — ResNet-50 on the igemm MFMA kernels; accepts uint8 frames (then
@@ -25,7 +29,8 @@ import torch
 from ...gpu.element import DeviceResult, FramePool, GpuPipelineElement, HostRing
 from ...pipeline.stream import StreamEvent
 
-__all__ = ["SyntheticFrames", "FrameResize", "ImagePreprocess", "ResNet50Classifier", "ClassifierTopK"]
+__all__ = ["SyntheticFrames", "FrameUpload", "FrameResize", "ImagePreprocess", "ResNet50Classifier",
+           "ClassifierTopK"]
 
 
 def _int(v, d):
@@ -80,7 +85,27 @@ class SyntheticFrames(GpuPipelineElement):
         for s in slots:
             self.frame_pool.release_after(s)
 
+    def _host_frames(self):
+        """``host: true`` — the decoder's output in pinned HOST memory (``pool`` pre-filled
+        batches served in rotation, read-only), for a FrameUpload to bring into HBM."""
+        if self.frame_pool is None:
+            B = _int(self.get_parameter("batch", 1)[0], 1)
+            H = _int(self.get_parameter("height", 224)[0], 224)
+            W = _int(self.get_parameter("width", 224)[0], 224)
+            n = max(1, _int(self.get_parameter("pool", 2)[0], 2))
+            g = torch.Generator().manual_seed(_int(self.get_parameter("seed", 0)[0], 0))
+            pin = torch.cuda.is_available()
+            self.frame_pool = [torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, generator=g).pin_memory()
+                               if pin else torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, generator=g)
+                               for _ in range(n)]
+            self._next = 0
+        frames = self.frame_pool[self._next]
+        self._next = (self._next + 1) % len(self.frame_pool)
+        return frames
+
     def _frames(self):
+        if str(self.get_parameter("host", False)[0]).lower() in ("true", "1", "yes"):
+            return self._host_frames()
         glob = str(self.get_parameter("global", False)[0]).lower() in ("true", "1", "yes") \
             and str(self.get_parameter("spmd", True)[0]).lower() not in ("false", "0", "no")
         if glob:
@@ -127,6 +152,101 @@ class SyntheticFrames(GpuPipelineElement):
             self.share["frames_dropped"] = self.dropped
             return StreamEvent.DROP_FRAME, {"diagnostic": "frame pool exhausted"}
         return StreamEvent.OKAY, {"images": frames, "t_submit": kwargs.get("t_submit", time.perf_counter())}
+
+
+class FrameUpload(GpuPipelineElement):
+    """Host -> HBM ingest of a frame batch (SURVEY K11 "synthetic-frame source + upload"; the
+    reference decodes into host memory and hands numpy images on,
+    ``/root/reference/src/aiko_services/elements/media/video_io.py:124-166``,
+    ``image_io.py:180-191``).
+
+    ``images``: a host uint8 tensor [B, H, W, 3] (pinned or pageable), one HxWx3 image, or a
+    list of them (numpy arrays from ``VideoReadFile`` / ``ImageReadFile`` / ``VideoReadWebcam``).
+    Pageable input is first copied into a pinned staging set (a ring of ``staging`` sets, each
+    reused once its previous upload finished).  The H2D copy runs on this element's copy
+    stream into a FramePool slot (``pool`` slots of the batch's size), the frame's lane waits
+    on the copy's event, and the slot is held until the frame completes — so the upload of
+    frame k+1 overlaps the compute of frame k, and a hop can send the slot zero-copy
+    (``mark_frame_held``).  Output ``images``: the device batch, uint8 [B, H, W, 3]."""
+    lane_safe = True
+
+    def __init__(self, context):
+        context.set_protocol("frame_upload:0")
+        super().__init__(context)
+        self.pool_slots = max(2, _int(self.get_parameter("pool", 6)[0], 6))
+        self.staging_sets = max(2, _int(self.get_parameter("staging", 4)[0], 4))
+        self._pools = {}
+        self._staging = {}
+        self._copy_stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+        self.bytes_uploaded = 0
+
+    @staticmethod
+    def _as_batch(images):
+        import numpy as np
+        if isinstance(images, torch.Tensor):
+            return images if images.dim() == 4 else images.unsqueeze(0)
+        if isinstance(images, np.ndarray):
+            t = torch.from_numpy(np.ascontiguousarray(images))
+            return t if t.dim() == 4 else t.unsqueeze(0)
+        if isinstance(images, (list, tuple)) and images:
+            return [torch.from_numpy(np.ascontiguousarray(i)) if isinstance(i, np.ndarray) else i for i in images]
+        raise ValueError("FrameUpload: images must be a uint8 tensor / array [B, H, W, 3] or a list of HxWx3")
+
+    def _pinned(self, batch, shape):
+        """A pinned host set holding ``batch`` (a tensor or a list of images)."""
+        if isinstance(batch, torch.Tensor) and (batch.is_pinned() or self.device.type != "cuda"):
+            return batch.contiguous()
+        ring = self._staging.get(shape)
+        if ring is None:
+            ring = self._staging[shape] = {"sets": [torch.empty(shape, dtype=torch.uint8, pin_memory=True)
+                                                    for _ in range(self.staging_sets)],
+                                           "events": [None] * self.staging_sets, "next": 0}
+        i = ring["next"]
+        ring["next"] = (i + 1) % self.staging_sets
+        ev = ring["events"][i]
+        if ev is not None:
+            ev.synchronize()                      # its upload (staging_sets frames ago) is done
+        host = ring["sets"][i]
+        if isinstance(batch, torch.Tensor):
+            host.copy_(batch)
+        else:
+            for j, img in enumerate(batch):
+                host[j].copy_(img)
+        ring["current"] = i
+        return host
+
+    def process_frame(self, stream, images):
+        from ...parallel.hop import mark_frame_held
+        batch = self._as_batch(images)
+        first = batch if isinstance(batch, torch.Tensor) else batch[0]
+        shape = (len(batch),) + tuple(first.shape[-3:]) if not isinstance(batch, torch.Tensor) else tuple(batch.shape)
+        if len(shape) != 4 or shape[3] != 3:
+            raise ValueError(f"FrameUpload: expected [B, H, W, 3] frames, got {shape}")
+        if self.device.type != "cuda":
+            out = batch if isinstance(batch, torch.Tensor) else torch.stack(batch)
+            return StreamEvent.OKAY, {"images": out.to(torch.uint8)}
+        nbytes = shape[0] * shape[1] * shape[2] * 3
+        pool = self._pools.get(shape)
+        if pool is None:
+            pool = self._pools[shape] = FramePool(self.pool_slots, nbytes, device=self.device)
+        slot = pool.acquire(30.0)
+        if slot < 0:
+            return StreamEvent.DROP_FRAME, {"diagnostic": "upload pool exhausted"}
+        host = self._pinned(batch, shape)
+        dst = pool.view(slot, shape, torch.uint8)
+        cur = torch.cuda.current_stream(self.device)
+        ev = torch.cuda.Event()
+        with torch.cuda.stream(self._copy_stream):
+            dst.copy_(host, non_blocking=True)
+            ev.record(self._copy_stream)
+        cur.wait_event(ev)                        # the frame's next kernels follow the upload
+        ring = self._staging.get(shape)
+        if ring is not None and host is ring["sets"][ring.get("current", 0)]:
+            ring["events"][ring["current"]] = ev  # the staging set is free once this copy is
+        self.hold_for_frame(pool, slot)
+        self.bytes_uploaded += nbytes
+        self.share["bytes_uploaded"] = self.bytes_uploaded
+        return StreamEvent.OKAY, {"images": mark_frame_held(dst)}
 
 
 class FrameResize(GpuPipelineElement):

@@ -163,6 +163,31 @@ def plan_stages(order, times_ms: dict, gpus: int, replicate: bool = True, local:
     return stages, reps, share, per_rank
 
 
+def plan_ingest(order, times_ms: dict, gpus: int, ingest_ms: float, boundary_ms: dict | None = None):
+    """Where frames enter HBM when they come from the host (decode / camera / files): the
+    PCIe term of the balancer.  ``ingest_ms`` = upload time of one frame batch over one
+    rank's PCIe link.
+
+    * ``rank0``: the source stage on rank 0 decodes AND uploads every batch of the node (its
+      time grows by ``ingest_ms`` per batch) and the stage cut ships frames over xGMI — the
+      best :func:`plan_stages` plan with that cost;
+    * ``per_rank``: every rank decodes and uploads its own batches over its own PCIe link
+      (data parallel: the whole chain per rank, nothing crosses xGMI): per-rank time per node
+      batch = (chain + ingest) / gpus.
+
+    Returns ``(choice, per-rank ms, plan_stages result or None)``: the choice with the lower
+    busiest-rank time (ms per frame batch of the node)."""
+    times0 = dict(times_ms)
+    times0[order[0]] = float(times0.get(order[0], 0.0)) + float(ingest_ms)
+    pp = plan_stages(order, times0, gpus, boundary_ms=boundary_ms)
+    rank0_ms = max(pp[3])
+    chain = sum(float(times_ms.get(e, 0.0)) for e in order) + float(ingest_ms)
+    per_rank_ms = chain / max(1, gpus)
+    if per_rank_ms < rank0_ms:
+        return "per_rank", [per_rank_ms] * gpus, None
+    return "rank0", pp[3], pp
+
+
 def _compositions(total, parts):
     """Positive integer tuples of length ``parts`` summing to at most ``total``."""
     for k in range(parts, total + 1):

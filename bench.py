@@ -60,6 +60,24 @@ def definition(batch: int, graph: bool, height: int, width: int, lanes: int = 1)
 DETECT = "aiko_services_amd.elements.gpu.detect"
 
 
+def host_ingest(d: dict) -> dict:
+    """``--ingest host``: the source makes its frames in pinned HOST memory (a decoder's
+    output) and a FrameUpload element brings each batch into an HBM FramePool slot on its own
+    copy stream — the PCIe upload of configs 3/4 modelled on every rank."""
+    d = json.loads(json.dumps(d))
+    src = d["elements"][0]
+    assert src["name"] == "SyntheticFrames"
+    src["parameters"]["host"] = True
+    src["parameters"].pop("global", None)
+    up = {"name": "FrameUpload", "input": [{"name": "images", "type": "tensor"}],
+          "output": [{"name": "images", "type": "tensor"}],
+          "parameters": {"pool": src["parameters"].get("pool", 6)}, "deploy": {"local": {"module": ELEMENTS}}}
+    d["elements"].insert(1, up)
+    g = d["graph"][0]
+    d["graph"] = [g.replace("(SyntheticFrames ", "(SyntheticFrames FrameUpload ", 1)]
+    return d
+
+
 def yolo_definition(batch: int, graph: bool, height: int, width: int, fanout: str, lanes: int = 1) -> dict:
     """BASELINE config 4: ingest rank decodes the node's frames, RCCL fan-out, YOLOv8-n +
     NMS kernels per GPU, RCCL all-gather of fixed-size detections."""
@@ -181,6 +199,9 @@ def parse_args(argv=None) -> argparse.Namespace:
                     help="dp: every GPU runs the whole pipeline (config 2/headline); "
                          "pp: config 3 as balanced multi-GPU actor pipelines (stages + replicas, "
                          "MQTT metadata, RCCL P2P tensors)")
+    ap.add_argument("--ingest", choices=["hbm", "host"], default="hbm",
+                    help="hbm: frames born in HBM (a hardware decoder); host: frames in pinned host "
+                         "memory, uploaded per rank by FrameUpload on a copy stream (PCIe ingest)")
     ap.add_argument("--element-times", default=None,
                     help="(pp) JSON {element: ms per batch} for the stage balancer")
     a = ap.parse_args(argv)
@@ -226,16 +247,22 @@ def main(argv=None):
                      "pipeline": d.graph[0], "gpu_lanes": a.lanes}
         metric, unit = WHISPER_METRIC, "windows/s"
     elif a.model == "yolov8n":
-        d = parse_pipeline_definition_dict(yolo_definition(a.batch, not a.no_graph, a.height, a.width, a.fanout, a.lanes))
+        yd = yolo_definition(a.batch, not a.no_graph, a.height, a.width, a.fanout, a.lanes)
+        if a.ingest == "host":          # per-rank ingest: each rank uploads its own batch, no fan-out
+            yd = host_ingest(yd)
+            yd["parameters"]["spmd"] = False
+        d = parse_pipeline_definition_dict(yd)
         result_key, model_cfg = "detections", {"model": "yolov8n", "image_size": [640, 640],
                                                "frame_size": [a.height, a.width], "fanout": a.fanout,
                                                "pipeline": d.graph[0], "gpu_lanes": a.lanes}
         metric = YOLO_METRIC
     else:
-        d = parse_pipeline_definition_dict(definition(a.batch, not a.no_graph, a.height, a.width, a.lanes))
+        rd = definition(a.batch, not a.no_graph, a.height, a.width, a.lanes)
+        if a.ingest == "host":
+            rd = host_ingest(rd)
+        d = parse_pipeline_definition_dict(rd)
         result_key, model_cfg = "topk", {"model": "resnet50", "image_size": [a.height, a.width],
-                                         "pipeline": "(SyntheticFrames ResNet50Classifier ClassifierTopK)",
-                                         "gpu_lanes": a.lanes}
+                                         "pipeline": rd["graph"][0], "gpu_lanes": a.lanes}
     responses: queue.Queue = queue.Queue()
     pipeline = PipelineImpl.create_pipeline("<bench>", d, None, None, "bench", [], 0, None, 3600,
                                             queue_response=responses)
@@ -301,11 +328,13 @@ def main(argv=None):
             "dtype": "fp8 linears / bf16 conv+attention" if a.model.startswith("whisper") else "bf16",
             "data": (f"synthetic ({a.batch} streams of {a.chunk:g} s 16 kHz chunks generated in HBM; random-init weights)"
                      if a.model.startswith("whisper") else
-                     f"synthetic (random uint8 {a.height}x{a.width} frames generated in HBM; random-init weights)"),
+                     f"synthetic (random uint8 {a.height}x{a.width} frames "
+                     + ("in pinned host memory, uploaded per step over PCIe" if a.ingest == "host" else "generated in HBM")
+                     + "; random-init weights)"),
             "p50_latency_ms": round(p50 * 1e3, 3),
             "p99_latency_ms": round(p99 * 1e3, 3),
             "config": dict({"global_batch": ws * a.batch, "seq_len": None, "per_gpu_batch": a.batch,
-                            "parallelism": f"dp{ws}", "hipgraph": not a.no_graph,
+                            "parallelism": f"dp{ws}", "hipgraph": not a.no_graph, "ingest": a.ingest,
                             "setup_frames": SETUP_FRAMES}, **model_cfg),
         }
         if a.model.startswith("whisper"):
@@ -325,7 +354,8 @@ PP_ELEMENT_MS = {"SyntheticFrames": 0.01, "FrameResize": 0.06, "ResNet50Classifi
 
 def pp_boundary_bytes(batch: int, height: int, width: int) -> dict:
     """Bytes each element hands to the next per frame batch (the hop payload if cut there)."""
-    return {"SyntheticFrames": batch * height * width * 3, "FrameResize": batch * 224 * 224 * 3,
+    return {"SyntheticFrames": batch * height * width * 3, "FrameUpload": batch * height * width * 3,
+            "FrameResize": batch * 224 * 224 * 3,
             "ResNet50Classifier": batch * 1000 * 2, "ClassifierTopK": batch * 5 * 8}
 
 
@@ -373,12 +403,16 @@ def run_pp(a, device, procs):
     ws, rank = D.world_size(), D.rank()
     times = dict(PP_ELEMENT_MS, **(json.loads(a.element_times) if a.element_times else {}))
     d = pp_definition(a.batch, not a.no_graph, a.height, a.width, ws, a.lanes)
+    if a.ingest == "host":
+        d = host_ingest(d)
     from aiko_services_amd.parallel.placement import boundary_ms_from_bytes
     boundary = boundary_ms_from_bytes(pp_boundary_bytes(a.batch, a.height, a.width), a.link_gbps)
     if ws == 1:
         # one GPU: the two-stage actor topology with the ResNet stage as rank 0's local share
         # (exercises the hop-free LocalStage path, frame lanes across the stage boundary)
-        plan = make_plan(d, gpus=1, stages=[["SyntheticFrames", "FrameResize"], ["ResNet50Classifier", "ClassifierTopK"]],
+        order = [e["name"] for e in d["elements"]]
+        cut = order.index("ResNet50Classifier")
+        plan = make_plan(d, gpus=1, stages=[order[:cut], order[cut:]],
                          replicas=[1, 0], local_share=1.0, group=f"bench{os.environ.get('MASTER_PORT', '0')}")
     else:
         plan = make_plan(d, gpus=ws, times_ms=times, group=f"bench{os.environ.get('MASTER_PORT', '0')}",

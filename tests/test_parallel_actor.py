@@ -368,3 +368,23 @@ def test_dp_replicated_survives_rank_loss(cluster, kill):
     # gets depends on timing: every parallel output must be one of the single-process outputs
     single = _single(cluster, d, frames)
     assert set(par.values()) <= set(single.values()), (par, single)
+
+
+def test_planner_prices_pcie_ingest():
+    """with frames coming from the host, rank-0 ingest pays the PCIe upload
+    of the whole node's batches on one link (and ships them over xGMI); per-rank ingest uploads
+    each rank's own batches on its own link.  Priced at PCIe Gen5 x16 (~50 GB/s) the 236 MB of a
+    256-frame VGA batch cost ~4.7 ms: the planner must choose per-rank ingest at 2..8 GPUs,
+    and rank-0 ingest when the upload is free (frames already in HBM)."""
+    import bench
+    from aiko_services_amd.parallel.placement import boundary_ms_from_bytes, plan_ingest
+    order = ["SyntheticFrames", "FrameUpload", "FrameResize", "ResNet50Classifier", "ClassifierTopK"]
+    times = dict(bench.PP_ELEMENT_MS, FrameUpload=0.0)
+    boundary = boundary_ms_from_bytes(bench.pp_boundary_bytes(256, 480, 640), 50.0)
+    pcie_ms = 256 * 480 * 640 * 3 / 50e9 * 1e3
+    assert 4.5 < pcie_ms < 5.0
+    for gpus in (2, 4, 8):
+        choice, per_rank, _ = plan_ingest(order, times, gpus, pcie_ms, boundary_ms=boundary)
+        assert choice == "per_rank", (gpus, per_rank)
+        rank0 = plan_ingest(order, times, gpus, 0.0, boundary_ms=boundary)
+        assert rank0[0] == "rank0" or max(rank0[1]) <= max(per_rank), rank0
