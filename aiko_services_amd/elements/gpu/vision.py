@@ -88,19 +88,19 @@ class SyntheticFrames(GpuPipelineElement):
     def _host_frames(self):
         """``host: true`` — the decoder's output in pinned HOST memory (``pool`` pre-filled
         batches served in rotation, read-only), for a FrameUpload to bring into HBM."""
-        if self.frame_pool is None:
+        if getattr(self, "host_pool", None) is None:
             B = _int(self.get_parameter("batch", 1)[0], 1)
             H = _int(self.get_parameter("height", 224)[0], 224)
             W = _int(self.get_parameter("width", 224)[0], 224)
             n = max(1, _int(self.get_parameter("pool", 2)[0], 2))
             g = torch.Generator().manual_seed(_int(self.get_parameter("seed", 0)[0], 0))
             pin = torch.cuda.is_available()
-            self.frame_pool = [torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, generator=g).pin_memory()
+            self.host_pool = [torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, generator=g).pin_memory()
                                if pin else torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, generator=g)
                                for _ in range(n)]
             self._next = 0
-        frames = self.frame_pool[self._next]
-        self._next = (self._next + 1) % len(self.frame_pool)
+        frames = self.host_pool[self._next]
+        self._next = (self._next + 1) % len(self.host_pool)
         return frames
 
     def _frames(self):

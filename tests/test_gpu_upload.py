@@ -44,9 +44,9 @@ def test_upload_pipeline_frames_bit_equal(native):
         assert img.is_cuda and img.dtype == torch.uint8 and tuple(img.shape) == (8, 96, 128, 3)
         # a kernel on the current stream right after the upload (no synchronize in between)
         sums.append(img.to(torch.int64).sum())
-        host = src.frame_pool[fid % 3]
+        host = src.host_pool[fid % 3]
         assert torch.equal(img.cpu(), host), fid
-    expect = [int(src.frame_pool[f % 3].to(torch.int64).sum()) for f in range(7)]
+    expect = [int(src.host_pool[f % 3].to(torch.int64).sum()) for f in range(7)]
     assert [int(s) for s in sums] == expect
 
 
