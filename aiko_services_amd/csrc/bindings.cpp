@@ -72,7 +72,7 @@ int aiko_linear_splitk(const void* x, const void* w, const float* bias, float* p
                        int ldx, int ldw, int ldy, int S, hipStream_t stream);
 int aiko_attn_fwd(const void* q, const void* k, const void* v, void* o, int ldq, int ldk, int ldv,
                   int ldo, int B, int H, int T, int Tpad, int dh, float scale, void* work, long work_bytes,
-                  hipStream_t stream);
+                  void* oq, void* osc, int ldoq, int osr, hipStream_t stream);
 int aiko_logmel(const float* audio, int B, int N, const float* mel, int n_mels, const int* mel_range,
                 int n_fft, int hop, int F, float* logmel, int* gmax, void* dst, int rows, int pad, int ld,
                 hipStream_t stream);
@@ -923,7 +923,8 @@ void linear_splitk_out(const at::Tensor& x, const at::Tensor& w, const c10::opti
 // q/k/v/o: [B*Tpad, >= H*64] row-major (column slices of a fused QKV buffer allowed)
 void attn_fwd_out(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, at::Tensor& o,
                   int64_t B, int64_t H, int64_t T, int64_t Tpad, double scale,
-                  const c10::optional<at::Tensor>& work) {
+                  const c10::optional<at::Tensor>& work, const c10::optional<at::Tensor>& oq,
+                  const c10::optional<at::Tensor>& osc) {
   for (const at::Tensor* t : {&q, &k, &v, (const at::Tensor*)&o}) {
     check_cuda(*t, "q/k/v/o");
     TORCH_CHECK(t->scalar_type() == at::kBFloat16, "aiko.attn_fwd_out: bf16 tensors required");
@@ -940,8 +941,29 @@ void attn_fwd_out(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
     wp = work->data_ptr();
     wb = (long)(work->numel() * work->element_size());
   }
+  // MX-fp8 output (ops.transformer.mx_buffers layout): e4m3 [B*Tpad, >= H*64] + E8M0 scales
+  // [H*64/128][rows >= B*Tpad][4]; o is then not written
+  void* qp = nullptr;
+  void* sp = nullptr;
+  int ldoq = 0, osr = 0;
+  if (oq.has_value() && oq->defined()) {
+    TORCH_CHECK(osc.has_value() && osc->defined(), "aiko.attn_fwd_out: oq needs osc");
+    check_cuda(*oq, "oq");
+    check_cuda(*osc, "osc");
+    TORCH_CHECK(oq->scalar_type() == at::kByte && oq->dim() == 2 && oq->stride(1) == 1 && oq->size(0) == B * Tpad &&
+                    oq->size(1) >= H * 64 && oq->stride(0) % 4 == 0,
+                "aiko.attn_fwd_out: oq uint8 [B*Tpad, >= H*64] with a 4-byte row pitch");
+    TORCH_CHECK((H * 64) % 128 == 0 && osc->scalar_type() == at::kByte && osc->is_contiguous() && osc->dim() == 3 &&
+                    osc->size(0) == H * 64 / 128 && osc->size(1) >= B * Tpad && osc->size(2) == 4,
+                "aiko.attn_fwd_out: osc uint8 [H*64/128, rows >= B*Tpad, 4]");
+    qp = oq->data_ptr();
+    sp = osc->data_ptr();
+    ldoq = (int)oq->stride(0);
+    osr = (int)osc->size(1);
+  }
   check_launch(aiko_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), q.stride(0), k.stride(0),
-                             v.stride(0), o.stride(0), B, H, T, Tpad, 64, (float)scale, wp, wb, cur_stream()),
+                             v.stride(0), o.stride(0), B, H, T, Tpad, 64, (float)scale, wp, wb, qp, sp, ldoq, osr,
+                             cur_stream()),
                "attn_fwd");
 }
 
@@ -1141,7 +1163,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("gemm_fp8_out(Tensor a, Tensor? sa, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!)? y, int act, int bm, int bn, int variant=0, Tensor? zero=None, Tensor? amx=None, Tensor(b!)? yq=None, Tensor(c!)? ysc=None) -> ()");
   m.def("rownorm_quant_out(Tensor x, Tensor? gamma, Tensor? beta, float eps, Tensor(a!)? yb, Tensor(b!)? q, Tensor(c!)? qs) -> ()");
   m.def("linear_splitk_out(Tensor x, Tensor w, Tensor? bias, Tensor(a!) part, Tensor(b!) y, int K, int S) -> ()");
-  m.def("attn_fwd_out(Tensor q, Tensor k, Tensor v, Tensor(a!) o, int B, int H, int T, int Tpad, float scale, Tensor(b!)? work=None) -> ()");
+  m.def("attn_fwd_out(Tensor q, Tensor k, Tensor v, Tensor(a!) o, int B, int H, int T, int Tpad, float scale, Tensor(b!)? work=None, Tensor(c!)? oq=None, Tensor(d!)? osc=None) -> ()");
   m.def("logmel_out(Tensor audio, Tensor mel, Tensor mel_range, int n_fft, int hop, int F, Tensor(a!) work, Tensor(b!) gmax, Tensor(c!) dst, int rows, int pad) -> ()");
   m.def("softmax_topk_out(Tensor logits, Tensor(a!) prob, Tensor(b!) index, int k) -> ()");
   m.def("embed_tokens_out(Tensor ids, Tensor pos, Tensor tok, Tensor pemb, Tensor(a!) x) -> ()");

@@ -43,6 +43,12 @@ struct AttnParams {
   int prio;             // 1: waves NW/2 .. NW-1 run at s_setprio 1 (static young-half priority)
   float* part;          // [pieces][QB][64] fp32 partial O, then [pieces][QB] (m, l) pairs
   int* cnt;             // [8 * split_r] arrival counters, zero between launches
+  // MX-fp8 output instead of bf16 o (the out-projection's A operand): e4m3 [rows][ldoq] and
+  // E8M0 scales [H*64/128][osr][4], one per 32 consecutive columns — each head's 64 columns
+  // are two whole blocks, so a workgroup quantises its own output (no per-row pass later)
+  uint8_t* oq;
+  uint8_t* osc;
+  int ldoq, osr;
 };
 
 constexpr int kKB = 64, kDH = 64;
@@ -518,6 +524,55 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
   }
 
   // normalise and write O[q][dh]: lane holds dh = d*16 + 4g + j for its query
+  if (p.oq) {
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      float l;
+      if constexpr (SM >= 1) {
+        l = lsum[qt][0];
+      } else {
+        l = l_run[qt];
+        l += __shfl_xor(l, 16, 64);
+        l += __shfl_xor(l, 32, 64);
+      }
+      const float inv = 1.f / l;
+      const int q = q0 + qt * 16 + fr;
+      const bool live = q < p.T;
+      const long row = seq0 + q;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {              // MX block b: dh 32b .. 32b+31 = d 2b, 2b+1
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = o[2 * b][qt][e] * inv;
+          v[4 + e] = o[2 * b + 1][qt][e] * inv;
+        }
+        float amax = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[e]));
+        amax = max_xor16_32(amax);                 // the 4 lanes of this query (g = 0..3)
+        const int ex = mx_exponent(amax);
+        const float s2 = __uint_as_float((uint32_t)(127 - ex) << 23);
+        unsigned w0 = 0u, w1 = 0u;
+        w0 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[0] * s2, -448.f), 448.f),
+                                             fminf(fmaxf(v[1] * s2, -448.f), 448.f), w0, false);
+        w0 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[2] * s2, -448.f), 448.f),
+                                             fminf(fmaxf(v[3] * s2, -448.f), 448.f), w0, true);
+        w1 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[4] * s2, -448.f), 448.f),
+                                             fminf(fmaxf(v[5] * s2, -448.f), 448.f), w1, false);
+        w1 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[6] * s2, -448.f), 448.f),
+                                             fminf(fmaxf(v[7] * s2, -448.f), 448.f), w1, true);
+        if (live) {
+          uint8_t* dq = p.oq + row * p.ldoq + hc + 32 * b;
+          *reinterpret_cast<unsigned*>(dq + 4 * g) = w0;          // dh 32b + 4g .. +3
+          *reinterpret_cast<unsigned*>(dq + 16 + 4 * g) = w1;     // dh 32b + 16 + 4g .. +3
+          const int col = hc + 32 * b;
+          if (g == 0) p.osc[((long)(col >> 7) * p.osr + row) * 4 + ((col >> 5) & 3)] = (uint8_t)(ex + 127);
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     float l;
@@ -551,9 +606,14 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
 // variants) the grid is the plain one.
 extern "C" int aiko_attn_fwd(const void* q, const void* k, const void* v, void* o, int ldq, int ldk,
                              int ldv, int ldo, int B, int H, int T, int Tpad, int dh, float scale,
-                             void* work, long work_bytes, hipStream_t stream) {
+                             void* work, long work_bytes, void* oq, void* osc, int ldoq, int osr,
+                             hipStream_t stream) {
   if (dh != aiko::kDH || T < 1 || Tpad < T) return -1;
   aiko::AttnParams p;
+  p.oq = static_cast<uint8_t*>(oq);
+  p.osc = static_cast<uint8_t*>(osc);
+  p.ldoq = ldoq;
+  p.osr = osr;
   p.q = static_cast<const aiko::bf16_t*>(q);
   p.k = static_cast<const aiko::bf16_t*>(k);
   p.v = static_cast<const aiko::bf16_t*>(v);

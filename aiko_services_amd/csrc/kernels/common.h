@@ -81,6 +81,15 @@ __device__ __forceinline__ void glds16_asm(const void* g, const void* lds_wave_b
                :: "v"(g), "s"(lds) : "memory", "m0");
 }
 
+// E8M0 exponent of an MX-fp8 block with absolute maximum amax (so that amax / 2^e <= 448, the
+// e4m3 range); shared by every epilogue that writes MX activations (fp8 GEMMs, attention)
+__device__ __forceinline__ int mx_exponent(float amax) {
+  const uint32_t bits = __float_as_uint(amax * (1.f / 448.f));
+  int e = (int)((bits >> 23) & 255u) - 127 + ((bits & 0x7fffffu) != 0u);
+  if (amax == 0.f) e = -126;
+  return e < -126 ? -126 : (e > 127 ? 127 : e);
+}
+
 // Bijective XCD-aware remap of a linear workgroup id: consecutive logical ids land on the
 // same XCD (blocks b and b+8 share an XCD under round-robin dispatch), so tiles that share
 // an operand panel share an L2.  Speed only; correctness never depends on placement.

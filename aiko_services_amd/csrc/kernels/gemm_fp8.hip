@@ -48,13 +48,6 @@ struct Fp8GemmParams {
   int ldq, ysr;
 };
 
-// E8M0 exponent for a block with absolute maximum amax (so that amax / 2^e <= 448)
-__device__ __forceinline__ int mx_exponent(float amax) {
-  const uint32_t bits = __float_as_uint(amax * (1.f / 448.f));
-  int e = (int)((bits >> 23) & 255u) - 127 + ((bits & 0x7fffffu) != 0u);
-  if (amax == 0.f) e = -126;
-  return e < -126 ? -126 : (e > 127 ? 127 : e);
-}
 
 
 

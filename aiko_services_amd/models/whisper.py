@@ -21,6 +21,7 @@ attention run in bf16.  Random init (no checkpoints offline), deterministic per 
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -63,6 +64,8 @@ class WhisperEncoder(WeightsMixin):
         d, L, H = SIZES[size]
         self.d, self.layers_n, self.heads = d, L, H
         self.n_ctx = n_ctx
+        # attention writes MX-fp8 for the out-projection (no per-row quantisation pass)
+        self.mx_attention = os.environ.get("AIKO_WHISPER_MX_ATTN", "1") != "0" and d % 128 == 0
         g = torch.Generator().manual_seed(seed)
         dev = self.device
 
@@ -184,12 +187,24 @@ class WhisperEncoder(WeightsMixin):
         if u8 is None:
             u8, usc = TR.mx_buffers(M, 4 * d, self.device)
             self._ws[(self.ws_tag + "u_mx", M, 4 * d)] = (u8, usc)
+        # attention -> out-projection hand-off in MX-fp8 too: the attention epilogue quantises
+        # each head's 64 columns (two E8M0 blocks) itself, so no per-row quantisation pass
+        a8, asc = self._ws.get((self.ws_tag + "a_mx", M, d)) or (None, None)
+        if a8 is None and self.mx_attention:
+            a8, asc = TR.mx_buffers(M, d, self.device)
+            self._ws[(self.ws_tag + "a_mx", M, d)] = (a8, asc)
         for blk in self.blocks:
             TR.rownorm(x, *blk.ln1, q=q8, qs=s8)
             TR.linear_fp8(q8, s8, blk.qkv, out=qkv)
-            TR.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], att, B, H, T, Tp, (d // H) ** -0.5, work=aws)
-            TR.rownorm(att, q=q8, qs=s8)
-            TR.linear_fp8(q8, s8, blk.out, out=x, residual=x)
+            if self.mx_attention:
+                TR.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], att, B, H, T, Tp, (d // H) ** -0.5,
+                             work=aws, out_mx=(a8, asc))
+                TR.linear_fp8(a8, None, blk.out, out=x, residual=x, x_mx=asc)
+            else:
+                TR.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], att, B, H, T, Tp, (d // H) ** -0.5,
+                             work=aws)
+                TR.rownorm(att, q=q8, qs=s8)
+                TR.linear_fp8(q8, s8, blk.out, out=x, residual=x)
             TR.rownorm(x, *blk.ln2, q=q8, qs=s8)
             TR.linear_fp8(q8, s8, blk.fc1, act=TR.ACT_GELU, out_mx=(u8, usc))
             TR.linear_fp8(u8, None, blk.fc2, out=x, residual=x, x_mx=usc)

@@ -207,10 +207,14 @@ def attention_workspace(device) -> torch.Tensor:
 
 
 def attention(q, k, v, out, batch: int, heads: int, T: int, Tpad: int, scale: float,
-              work: torch.Tensor | None = None):
+              work: torch.Tensor | None = None, out_mx: tuple | None = None):
     """Non-causal multi-head attention (head dim 64) over sequences of ``T`` tokens stored
     every ``Tpad`` rows; q/k/v may be column slices of one fused QKV buffer.  ``work``
     (:func:`attention_workspace`, private to the calling stream) lets the kernel cut the items
-    of a partial last round into key ranges merged in-kernel."""
-    torch.ops.aiko.attn_fwd_out(q, k, v, out, batch, heads, T, Tpad, float(scale), work)
+    of a partial last round into key ranges merged in-kernel.  ``out_mx`` = (q, sc) from
+    :func:`mx_buffers`: the output is written as MX-fp8 (each head's 64 columns are two E8M0
+    blocks, quantised in the epilogue) for an out-projection with ``x_mx`` — ``out`` is then
+    not written."""
+    oq, osc = out_mx if out_mx is not None else (None, None)
+    torch.ops.aiko.attn_fwd_out(q, k, v, out, batch, heads, T, Tpad, float(scale), work, oq, osc)
     return out

@@ -257,3 +257,36 @@ def test_gemm_fp8_mx_in_and_out(native, tile):
     assert (osc.cpu()[:, :M] == rsc[:, :M]).float().mean() > 0.98          # same E8M0 scales
     assert _rel(got, full.cpu()) < 4e-2                                    # fp8 rounding only
     assert _rel(got, TR.mx_dequant(rq, rsc)) < 1e-2
+
+
+@pytest.mark.parametrize("B,T,Tpad,H,split", [(2, 1500, 1501, 12, 0), (3, 77, 80, 4, 0), (16, 1500, 1504, 12, 2)])
+def test_flash_attention_mx_output(native, B, T, Tpad, H, split, monkeypatch):
+    """Attention writing MX-fp8 directly (the out-projection's A operand; each head's 64
+    columns = two E8M0 blocks quantised in the epilogue, split-KV merge included): the
+    dequantised output matches the fp32 reference within e4m3 rounding, the scales equal a
+    reference MX quantisation of the bf16 output path, and padding rows stay unwritten."""
+    from aiko_services_amd.ops import transformer as TR
+    if split:
+        monkeypatch.setenv("AIKO_ATTN_SPLIT_S", str(split))
+    g = torch.Generator().manual_seed(T + H)
+    d = H * 64
+    qkv = (torch.randn(B * Tpad, 3 * d, generator=g) * 1.5).to(DEV, torch.bfloat16)
+    ws = TR.attention_workspace(DEV) if split else None
+    out = torch.zeros(B * Tpad, d, dtype=torch.bfloat16, device=DEV)
+    TR.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], out, B, H, T, Tpad, 0.125, work=ws)
+    aq, asc = TR.mx_buffers(B * Tpad, d, DEV)
+    aq.fill_(0x7f)
+    TR.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], torch.empty_like(out), B, H, T, Tpad, 0.125,
+                 work=ws, out_mx=(aq, asc))
+    torch.cuda.synchronize()
+    x = qkv.float().view(B, Tpad, 3, H, 64)[:, :T]
+    q, k, v = (x[:, :, i].transpose(1, 2) for i in range(3))
+    ref = F.scaled_dot_product_attention(q, k, v, scale=0.125).transpose(1, 2).reshape(B, T, d)
+    got = TR.mx_dequant(aq.cpu(), asc.cpu()).view(B, Tpad, d)[:, :T].to(DEV)
+    assert _rel(got, ref) < 4e-2, _rel(got, ref)
+    rq, rsc = TR.mx_quantize_ref(out.float().cpu())
+    valid = torch.zeros(B, Tpad, dtype=torch.bool)
+    valid[:, :T] = True
+    valid = valid.flatten()
+    assert (asc.cpu()[:, :B * Tpad][:, valid] == rsc[:, :B * Tpad][:, valid]).float().mean() > 0.98
+    assert (aq.view(B, Tpad, d)[:, T:] == 0x7f).all()                   # padding rows untouched
