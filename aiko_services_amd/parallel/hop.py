@@ -449,6 +449,13 @@ class HopPlane:
             return False
         link = self.send_links.get(rec[0])
         if link is not None and not link.dead and rec[1] is not None:
+            if not reuse and rec[9] and self.device.type == "cuda":
+                # a dropped zero-copy send still reads the producer's FramePool slot, which the
+                # frame's release (right after this) returns behind an event on the current
+                # stream: order that stream after the send first (RCCL: stream-ordered wait)
+                w = link.work[rec[1]]
+                if w is not None:
+                    w.wait()
             link.release(rec[1], reuse=reuse)
             return True
         return False
@@ -628,8 +635,9 @@ class HopPlane:
         self._post(link, slot, buf, total, dst)
         if key is not None:
             # [dst, slot, total, specs, templates, buf, members (groups), slot reusable,
-            #  event after the staging copy (a re-send from another stream waits on it)]
-            self._held[key] = [dst, slot, total, specs, outs, buf, None, True, self.ready_event()]
+            #  event after the staging copy (a re-send from another stream waits on it),
+            #  sent straight from the producer's frame-held buffer]
+            self._held[key] = [dst, slot, total, specs, outs, buf, None, True, self.ready_event(), direct]
         else:
             link.release(slot)                       # ring slot: free once its transfer is done
         return outs
@@ -674,7 +682,7 @@ class HopPlane:
         self._order_after([rec[8]])                   # the bytes were staged on another stream
         self._post(link, slot, buf, total, dst)
         out = _retoken(templates[0], seq)
-        self._held[key] = [dst, slot, total, specs, [out], buf, None, True, rec[8]]
+        self._held[key] = [dst, slot, total, specs, [out], buf, None, True, rec[8], rec[9]]
         self.counters["resent"] += 1
         return out
 
