@@ -217,14 +217,17 @@ void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, co
     rc = aiko_conv_wide(x.data_ptr(), w.data_ptr(), bptr, rptr, y.data_ptr(), H, W, C, Cc, R, S, stride,
                         pad, Ho, Wo, M, Cout, K, act, ldy, ldr, bm, bn, x2ptr, K1, H2, W2, C2, stride2,
                         variant == 11 ? 11 : (variant == 9 ? 2 : 1), cur_stream());
-  } else if (variant == 12 || variant == 13) {
+  } else if (variant == 12 || variant == 13 || variant == 14) {
     // persistent pointwise GEMM (conv_pw.hip): 1x1 / stride 1 / one source, K % 256 == 0,
     // Cout % 128 == 0, x rows = pixels at pitch C
-    TORCH_CHECK(!dual && R == 1 && S == 1 && stride == 1 && pad == 0 && Cc == K && K % 256 == 0 &&
-                    Cout % 128 == 0 && C % 8 == 0 && (variant == 12 || K == 256 || K == 512) && x_extent * 2 < (1LL << 31) - 64 && w.numel() * 2 < (1LL << 31) &&
+    const bool pw_shape = variant == 12 ? (K % 256 == 0 && Cout % 128 == 0)
+                                        : ((K == 128 && Cout % 256 == 0) || (K == 256 && Cout % 128 == 0) ||
+                                           (K == 512 && Cout % 64 == 0));
+    TORCH_CHECK(!dual && R == 1 && S == 1 && stride == 1 && pad == 0 && Cc == K && pw_shape &&
+                    C % 8 == 0 && x_extent * 2 < (1LL << 31) - 64 && w.numel() * 2 < (1LL << 31) &&
                     avail_elems(y) * 2 < (1LL << 31),
-                "aiko.conv_igemm_out: variant 12 needs a 1x1/s1 single-source conv with K % 256 == 0, "
-                "Cout % 128 == 0 and operands < 2 GiB");
+                "aiko.conv_igemm_out: variants 12/13 need a 1x1/s1 single-source conv with K % 256 == 0 "
+                "(13: K = 128 / 256 / 512), Cout a multiple of the channel block and operands < 2 GiB");
     TORCH_CHECK(ldy % 8 == 0 && (!rptr || (ldr % 8 == 0 && reinterpret_cast<uintptr_t>(rptr) % 16 == 0 &&
                                           avail_elems(*res) * 2 < (1LL << 31) - 64)),
                 "aiko.conv_igemm_out: variant 12 needs 16-B aligned rows");
@@ -237,7 +240,7 @@ void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, co
       cus = n;
     }
     rc = aiko_conv_pw(x.data_ptr(), w.data_ptr(), bptr, rptr, y.data_ptr(), M, Cout, K, C, ldy, ldr, act, cus,
-                      variant == 13 ? 1 : 0, cur_stream());
+                      variant == 13 ? 1 : variant == 14 ? 2 : 0, cur_stream());
   } else if (variant == 4) {
     // persistent buffer-LDS-DMA kernel: one K-block stream across each workgroup's run of tiles
     TORCH_CHECK(Cc % 64 == 0 && R * S <= 32 && K % 64 == 0 && x_extent * 2 < (1LL << 31) - 64 &&

@@ -269,37 +269,93 @@ __global__ __launch_bounds__(512, 1) void conv_pw_kernel(PwParams p) {
   }
 }
 
-// ---- resident-weight variant (tuner variant 13): K == 256 or 512 ----
+// ---- resident-weight variant (tuner variant 13): K == 128, 256 or 512 ----
 //
 // conv_pw_kernel keeps three 32 KB blocks in flight per CU: ~1 us of MFMA work to cover a ~2 us
 // L2 / HBM round trip, so every K step stalls.  With the workgroup's channel block fixed, its
-// 128 x 256 weight block (64 KB) is loaded into LDS once; the ring then carries only activation
-// blocks of a 64-pixel tile (8 KB each) and 8 slots fit beside the weights and a 16 KB residual
-// tile (144 KB): seven blocks in flight, the lookahead in time doubled at a quarter of the bytes
-// per block.  Slots cycle every two tiles (block kb of tile t uses slot 4 (t & 1) + kb), so the
-// tile loop is unrolled by two and every slot address is an immediate.
-// Measured (MI355X, B=320, scripts/pw_check.sh): stage-3 expansion M=62720 N=1024 K=256 + residual
-// 65.6 us (500 TF, 4.4 TB/s with the residual) against 77.9 us for conv_pw_kernel and 80 us for the
-// best tiled kernel — the longer lookahead, not the ring restart, was the lever.  The K = 512 form
-// (64-channel blocks, half the FLOPs per activation byte, so half the lookahead in time) measured
-// slower than the tiled kernels on every ResNet layer it applies to (512 -> 128: 75 vs 62 us,
-// 512 -> 256: 154 vs 97, stage-4 expansion 82 vs 47) — a tuner candidate the tuner does not pick.
-// KW = 512 (stage-4 expansions, 512 -> 256/128 reductions): a 64 x 512 weight block (BN = 64),
-// one tile per ring cycle (block kb in slot kb), 4 x 2 waves of 16 x 32.
-template <bool RES, int KW>
+// weight block (64 KB) is loaded into LDS once; the ring then carries only activation blocks of a
+// 64-pixel tile (8 KB each) beside the weights and two residual tiles.  Slots cycle every two
+// tiles when a tile has fewer K blocks than the ring has slots (block kb of tile t uses slot
+// NKB (t & 1) + kb), so the tile loop is unrolled by two and every slot address is an immediate.
+//   KW = 128 (stage-2 expansions 128 -> 512): a 256 x 128 weight block, 8 waves of 64 x 32, a
+//            4-slot ring (three blocks = 1.5 tiles in flight), two 32 KB residual tiles: 160 KB;
+//   KW = 256 (stage-3 expansions, 256 -> 128 reductions): 128 x 256 weights, 4 x 2 waves of
+//            32 x 32, an 8-slot ring (seven blocks in flight), two 16 KB residual tiles: 160 KB;
+//   KW = 512 (stage-4 expansions, 512 -> 256/128 reductions): 64 x 512 weights, 4 x 2 waves of
+//            16 x 32, one tile per ring cycle, two 8 KB residual tiles: 144 KB.
+// The residual is the largest operand of an expansion (2x-4x the activation bytes) and used only
+// by the epilogue, so it is DMA'd ONE TILE AHEAD into the other residual buffer: tile t + 1's
+// residual is issued at tile t's first K step and has a whole tile (~2-4 us at the HBM pace) to
+// land, where issuing it at its own tile's first step left ~0.5-2 us — an exposed round trip
+// per tile.  Stores go through buffer_store with an out-of-range offset for the ragged rows (never
+// skipped), so the number of vector-memory ops a wave issues per tile is fixed and every
+// `s_waitcnt vmcnt(N)` below is the EXACT count of ops younger than the awaited one (computed at
+// compile time from the issue order by pw_young_*), for the first tiles and the steady state;
+// the tiles the lookahead runs past the end of the walk wait for everything.
+// Measured (MI355X, B=320, scripts/pw_check.sh): with the residual issued at its own tile the
+// stage-3 expansion M=62720 N=1024 K=256 + residual ran 65.6 us (500 TF, 4.4 TB/s with the
+// residual) against 77.9 us for conv_pw_kernel and 80 us for the best tiled kernel.  Round 4, one
+// box: the stage-2 expansion M=250880 N=512 K=128 + residual 105.5 us one tile ahead vs 110.9 us at
+// its own tile (PF = 0, tuner variant 14) and 133 us for the best tiled kernel — 5.6 TB/s counting
+// the residual; K = 256 71.4 vs 71.8 us, K = 512 81.1 vs 79.8 us (no difference there).
+
+// Issue order per wave (virtual steps s < 0 are the prologue): step s of tile t = s / NKB issues
+// [res(t + 1): NR ops if s % NKB == 0] [x block s + LA: 1 op]; after a tile's last step its
+// epilogue issues MI stores.  res(0) sits at virtual step -NKB (or before everything if NKB > LA).
+// With PF == 0 (A/B form, tuner variant 14) step s issues res(t) itself and there is no virtual one.
+__host__ __device__ constexpr bool pw_res_at(int s, int NKB, int LA, int PF = 1) {
+  return s >= 0 ? s % NKB == 0 : (PF == 0 ? false : NKB <= LA ? s == -NKB : s == -LA);
+}
+__host__ __device__ constexpr int pw_res_id(int s, int NKB, int PF = 1) { return s >= 0 ? s / NKB + PF : 0; }
+
+// ops issued after x block f and before step f's wait
+__host__ __device__ constexpr int pw_young_blk(int f, int NKB, int LA, int NR, int MI, int PF = 1) {
+  int cnt = 0;
+  bool on = false;
+  for (int s = -LA; s < f; ++s) {
+    if (NR && pw_res_at(s, NKB, LA, PF) && on) cnt += NR;
+    if (on) cnt += 1;
+    if (s + LA == f) on = true;
+    if (s >= 0 && s % NKB == NKB - 1 && on) cnt += MI;
+  }
+  return cnt;
+}
+
+// ops issued after res(t) and before tile t's epilogue wait (i.e. after its last step's issue)
+__host__ __device__ constexpr int pw_young_res(int t, int NKB, int LA, int NR, int MI, int PF = 1) {
+  int cnt = 0;
+  bool on = false;
+  const int last = NKB * t + NKB - 1;
+  for (int s = -LA; s <= last; ++s) {
+    if (pw_res_at(s, NKB, LA, PF)) {
+      if (on) cnt += NR;
+      if (pw_res_id(s, NKB, PF) == t) on = true;
+    }
+    if (on) cnt += 1;
+    if (s >= 0 && s % NKB == NKB - 1 && s != last && on) cnt += MI;
+  }
+  return cnt;
+}
+
+template <bool RES, int KW, int PF = 1>
 __global__ __launch_bounds__(512, 1) void conv_pw_rb_kernel(PwParams p) {
-  static_assert(KW == 256 || KW == 512, "K = 256 or 512");
-  constexpr int BN = KW == 256 ? 128 : 64;
-  constexpr int BM = 64, BK = 64, NS = 8, NKB = KW / BK;
-  constexpr int WGN = KW == 256 ? 4 : 2, WM = BM / (8 / WGN), WN = BN / WGN, MI = WM / 16, NI = WN / 16;
-  constexpr int RPC = BN / 8;                     // 16-B pieces per residual row (16 / 8)
-  constexpr int RMASK = RPC - 1;
-  constexpr int NR = RES ? BM * RPC / 512 : 0;    // residual DMA instructions per thread (2 / 1)
+  static_assert(KW == 128 || KW == 256 || KW == 512, "K = 128, 256 or 512");
+  static_assert(PF == 0 || PF == 1, "residual issued at its own tile (0) or one tile ahead (1)");
+  constexpr int BN = KW == 128 ? 256 : KW == 256 ? 128 : 64;
+  constexpr int BM = 64, BK = 64, NKB = KW / BK;
+  constexpr int NS = KW == 128 ? 4 : 8;
+  constexpr int WGN = KW == 128 ? 8 : KW == 256 ? 4 : 2;
+  constexpr int WM = BM / (8 / WGN), WN = BN / WGN, MI = WM / 16, NI = WN / 16;
+  static_assert(NI == 2, "the epilogue pairs two 16-channel fragments");
+  constexpr int RPC = BN / 8;                     // 16-B pieces per residual row (32 / 16 / 8)
+  constexpr int RMASK = RPC < 16 ? RPC - 1 : 15;  // residual swizzle: piece ^ (row & RMASK)
+  constexpr int NR = RES ? BM * RPC / 512 : 0;    // residual DMA instructions per thread (4 / 2 / 1)
   constexpr int LA = NS - 1;                      // blocks in flight
-  constexpr int TAIL = (NKB + LA - 1) / NKB;      // tiles the lookahead reaches ahead (2 / 1)
+  constexpr int TAIL = (LA + NKB - 1) / NKB;      // tiles the lookahead reaches ahead (2 / 2 / 1)
   constexpr int SLOT = BM * BK;                   // elements per ring slot (8 KB)
   constexpr int W_ELEMS = BN * KW;                // resident weights (64 KB)
-  __shared__ __attribute__((aligned(16))) bf16_t lds[W_ELEMS + NS * SLOT + BM * BN];
+  constexpr int R_ELEMS = RES ? BM * BN : 0;      // one residual tile
+  __shared__ __attribute__((aligned(16))) bf16_t lds[W_ELEMS + NS * SLOT + 2 * R_ELEMS];
   bf16_t* const wres = lds;
   bf16_t* const ring = lds + W_ELEMS;
   bf16_t* const resb = ring + NS * SLOT;
@@ -318,6 +374,7 @@ __global__ __launch_bounds__(512, 1) void conv_pw_rb_kernel(PwParams p) {
   const __amdgpu_buffer_rsrc_t rx = pw_rsrc(p.x);
   const __amdgpu_buffer_rsrc_t rw = pw_rsrc(p.w);
   const __amdgpu_buffer_rsrc_t rr = pw_rsrc(RES ? p.res : p.x);
+  const __amdgpu_buffer_rsrc_t ry = pw_rsrc(p.y);
 
   const int fr = lane & 15, fq = lane >> 4;
   const int coff = ((fq & 1) << 4) | ((fq >> 1) << 3);
@@ -334,7 +391,7 @@ __global__ __launch_bounds__(512, 1) void conv_pw_rb_kernel(PwParams p) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) asm volatile("" ::"v"(e_bias[e]));
 
-  // resident weights: KW / 8 16-B pieces per row (2 rows / 1 row per wave instruction); LDS
+  // resident weights: KW / 8 16-B pieces per row (4 / 2 / 1 rows per wave instruction); LDS
   // position pos of row n holds logical piece (pos & ~7) | ((pos & 7) ^ (n & 7))
   constexpr int WROWS = 64 / (KW / 8);            // rows per wave instruction
 #pragma unroll
@@ -347,8 +404,8 @@ __global__ __launch_bounds__(512, 1) void conv_pw_rb_kernel(PwParams p) {
 
   const int lrow = wave * 8 + (lane >> 3);         // activation DMA: 8 rows per wave, 64 per block
   const int lp = (lane & 7) ^ (lane >> 3);
-  constexpr int RRW = 64 / RPC;                   // residual rows per wave instruction (4 / 8)
-  const int rrow0 = wave * RRW + lane / RPC;
+  constexpr int RRW = 64 / RPC;                   // residual rows per wave instruction (2 / 4 / 8)
+  const int rrow0 = wave * RRW + lane / RPC;      // (rrow0 + 8 RRW r) & RMASK == rrow0 & RMASK
   const int rpiece = (lane % RPC) ^ (rrow0 & RMASK);
 
   auto issue = [&](int f, auto slot_tag) {
@@ -359,13 +416,15 @@ __global__ __launch_bounds__(512, 1) void conv_pw_rb_kernel(PwParams p) {
     const uint32_t off = m < p.M ? (uint32_t)((m * p.ldx + lp * 8) * 2) : kPwOOB;
     pw_dma16(rx, off, (uint32_t)(kb * BK * 2), ring + S * SLOT + wave * 8 * BK);
   };
-  auto issue_res = [&](int t) {
+  auto issue_res = [&](int t, auto buf_tag) {      // residual of tile t into buffer B
+    constexpr int B = decltype(buf_tag)::value;
+    if (t >= ntiles) return;
     const int m0 = (group + t * p.groups) * BM;
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
       const int m = m0 + rrow0 + 8 * RRW * r;
       const uint32_t off = m < p.M ? (uint32_t)((m * p.ldr + n0 + rpiece * 8) * 2) : kPwOOB;
-      pw_dma16(rr, off, 0u, resb + (r * 8 * RRW + wave * RRW) * BN);
+      pw_dma16(rr, off, 0u, resb + B * R_ELEMS + (r * 8 * RRW + wave * RRW) * BN);
     }
   };
 
@@ -398,32 +457,39 @@ __global__ __launch_bounds__(512, 1) void conv_pw_rb_kernel(PwParams p) {
 
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using I3 = std::integral_constant<int, 3>;
-  using I4 = std::integral_constant<int, 4>;
-  using I5 = std::integral_constant<int, 5>;
-  using I6 = std::integral_constant<int, 6>;
-  using I7 = std::integral_constant<int, 7>;
-  issue(0, I0{}); issue(1, I1{}); issue(2, I2{}); issue(3, I3{});
-  issue(4, I4{}); issue(5, I5{}); issue(6, I6{});
+  // prologue = virtual steps -LA .. -1: x blocks 0 .. LA - 1 (block b in slot b), res(0) at its
+  // virtual step
+  auto pro = [&](auto b_tag) {
+    constexpr int B = decltype(b_tag)::value;
+    if constexpr (B < LA) {
+      if constexpr (RES && pw_res_at(B - LA, NKB, LA, PF)) issue_res(0, I0{});
+      issue(B, b_tag);
+    }
+  };
+  pro(I0{}); pro(I1{}); pro(std::integral_constant<int, 2>{}); pro(std::integral_constant<int, 3>{});
+  pro(std::integral_constant<int, 4>{}); pro(std::integral_constant<int, 5>{});
+  pro(std::integral_constant<int, 6>{});
 
   const bool post = (p.act & 16) != 0;
   const int act = p.act & 15;
-  // one tile: H = tile parity (selects the slot half when two tiles share the 8-slot cycle).
-  // Waits: block (t, kb) has the next six blocks younger, plus this tile's residual (issued at
-  // step 0, before block (t, 0) + 7) while it sits between them (kb = 1 .. 6); the tiles the
-  // lookahead runs past the end of the walk wait for everything.
+  // one K step of tile t (H = t & 1): wait for its block, issue the lookahead (and at KB == 0 the
+  // next tile's residual), run the MFMAs
   auto step = [&](int t, bool tail, auto h_tag, auto kb_tag) {
     constexpr int H = decltype(h_tag)::value, KB = decltype(kb_tag)::value;
-    constexpr int SL = (NKB == 4 ? 4 * H : 0) + KB;
+    constexpr int SL = (NKB < NS ? NKB * H : 0) + KB;
+    constexpr int Y0 = pw_young_blk(KB, NKB, LA, NR, MI, PF);
+    constexpr int Y1 = pw_young_blk(NKB + KB, NKB, LA, NR, MI, PF);
+    constexpr int YS = pw_young_blk(NKB * TAIL + KB, NKB, LA, NR, MI, PF);
     if (tail) pw_vm_barrier<0>();
-    else if (KB >= 1 && KB <= 6) pw_vm_barrier<6 + NR>();
-    else pw_vm_barrier<6>();
-    if (RES && KB == 0) issue_res(t);
+    else if (t == 0) pw_vm_barrier<Y0>();
+    else if (TAIL > 1 && t == 1) pw_vm_barrier<Y1>();
+    else pw_vm_barrier<YS>();
+    if constexpr (RES && KB == 0) issue_res(t + PF, std::integral_constant<int, H ^ PF>{});
     issue(NKB * t + KB + LA, std::integral_constant<int, (SL + LA) % NS>{});
     compute(std::integral_constant<int, SL>{}, kb_tag);
   };
   auto tile = [&](int t, auto half_tag) {
+    constexpr int H = decltype(half_tag)::value;
     const bool tail = t + TAIL >= ntiles;
 #pragma unroll
     for (int j = 0; j < NI; ++j)
@@ -431,17 +497,24 @@ __global__ __launch_bounds__(512, 1) void conv_pw_rb_kernel(PwParams p) {
       for (int i = 0; i < MI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     step(t, tail, half_tag, I0{});
     step(t, tail, half_tag, I1{});
-    step(t, tail, half_tag, I2{});
-    step(t, tail, half_tag, I3{});
+    if constexpr (NKB >= 4) {
+      step(t, tail, half_tag, std::integral_constant<int, 2>{});
+      step(t, tail, half_tag, std::integral_constant<int, 3>{});
+    }
     if constexpr (NKB == 8) {
-      step(t, tail, half_tag, I4{});
-      step(t, tail, half_tag, I5{});
-      step(t, tail, half_tag, I6{});
-      step(t, tail, half_tag, I7{});
+      step(t, tail, half_tag, std::integral_constant<int, 4>{});
+      step(t, tail, half_tag, std::integral_constant<int, 5>{});
+      step(t, tail, half_tag, std::integral_constant<int, 6>{});
+      step(t, tail, half_tag, std::integral_constant<int, 7>{});
     }
-    if (RES) {                                     // residual: younger = the NKB blocks issued since
-      if (tail) pw_vm_barrier<0>(); else pw_vm_barrier<NKB>();
+    if constexpr (RES) {                           // this tile's residual landed, every wave
+      constexpr int R0 = pw_young_res(0, NKB, LA, NR, MI, PF);
+      constexpr int RS = pw_young_res(1, NKB, LA, NR, MI, PF);
+      if (tail) pw_vm_barrier<0>();
+      else if (t == 0) pw_vm_barrier<R0>();
+      else pw_vm_barrier<RS>();
     }
+    const bf16_t* const rt = resb + H * R_ELEMS;
     const int m0 = (group + t * p.groups) * BM;
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
@@ -455,8 +528,7 @@ __global__ __launch_bounds__(512, 1) void conv_pw_rb_kernel(PwParams p) {
         hi[e] = __uint_as_float(s[1]);
       }
       u32x4 r = {0u, 0u, 0u, 0u};
-      if constexpr (RES) r = *reinterpret_cast<const u32x4*>(resb + ml * BN + (((nl >> 3) ^ (fr & RMASK)) << 3));
-      if (m >= p.M) continue;
+      if constexpr (RES) r = *reinterpret_cast<const u32x4*>(rt + ml * BN + (((nl >> 3) ^ (ml & RMASK)) << 3));
       float v[8] = {lo[0] + e_bias[0], lo[1] + e_bias[1], lo[2] + e_bias[2], lo[3] + e_bias[3],
                     hi[0] + e_bias[4], hi[1] + e_bias[5], hi[2] + e_bias[6], hi[3] + e_bias[7]};
       if (RES && !post) {
@@ -486,29 +558,35 @@ __global__ __launch_bounds__(512, 1) void conv_pw_rb_kernel(PwParams p) {
       u32x4 o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = pack2(v[2 * e], v[2 * e + 1]);
-      *reinterpret_cast<u32x4*>(p.y + (size_t)m * p.ldy + n0 + nl) = o;
+      // always issued (ragged rows at an out-of-range offset): the vmcnt counts above include it
+      const uint32_t off = m < p.M ? (uint32_t)(((size_t)m * p.ldy + n0 + nl) * 2) : kPwOOB;
+      __builtin_amdgcn_raw_buffer_store_b128(o, ry, off, 0, 0);
     }
   };
   for (int t = 0; t < ntiles; t += 2) {
     tile(t, I0{});
     if (t + 1 < ntiles) tile(t + 1, I1{});
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 }  // namespace
 
 }  // namespace aiko
 
-// 1x1 / stride-1 conv over x [M][ldx] (first K channels): K % 256 == 0, N % 128 == 0, ldx / ldy /
-// ldr multiples of 8, 16-byte aligned operands, every operand < 2^31 bytes (host checks).
-// ``cus``: compute units to size the persistent grid for; ``mode`` 1: resident-weight kernel (K == 256).
+// 1x1 / stride-1 conv over x [M][ldx] (first K channels): K % 256 == 0 (mode 0) or K in {128, 256,
+// 512} (mode 1), N a multiple of the channel block, ldx / ldy / ldr multiples of 8, 16-byte aligned
+// operands, every operand < 2^31 bytes (host checks).
+// ``cus``: compute units to size the persistent grid for; ``mode`` 1: resident-weight kernel, 2: the
+// same with each tile's residual issued at its own first K step (A/B form).
 extern "C" int aiko_conv_pw(const void* x, const void* w, const float* bias, const void* res, void* y, int M,
                             int N, int K, int ldx, int ldy, int ldr, int act, int cus, int mode,
                             hipStream_t stream) {
   using namespace aiko;
-  if (K % (kPwBK * kPwNS) || N % kPwBN || M <= 0 || ldx % 8 || ldy % 8 || (res && ldr % 8) || ldx < K)
-    return -1;
-  if (mode == 1 && K != 256 && K != 512) return -1;   // resident weights: a 64 KB block per workgroup
+  const bool rb = mode == 1 || mode == 2;
+  const int bn = rb ? (K == 128 ? 256 : K == 256 ? 128 : 64) : kPwBN;
+  if (N % bn || M <= 0 || ldx % 8 || ldy % 8 || (res && ldr % 8) || ldx < K) return -1;
+  if (rb ? (K != 128 && K != 256 && K != 512) : K % (kPwBK * kPwNS) != 0) return -1;
   PwParams p;
   p.x = static_cast<const bf16_t*>(x);
   p.w = static_cast<const bf16_t*>(w);
@@ -516,24 +594,27 @@ extern "C" int aiko_conv_pw(const void* x, const void* w, const float* bias, con
   p.res = static_cast<const bf16_t*>(res);
   p.y = static_cast<bf16_t*>(y);
   p.M = M; p.N = N; p.K = K; p.ldx = ldx; p.ldy = ldy; p.ldr = ldr; p.act = act;
-  p.ntn = N / (mode == 1 && K == 512 ? 64 : kPwBN);
-  const int bm = mode == 1 ? 64 : kPwBM;
+  p.ntn = N / bn;
+  const int bm = rb ? 64 : kPwBM;
   p.mtiles = (M + bm - 1) / bm;
   int groups = (cus > 0 ? cus : 256) / p.ntn;
   if (groups < 1) groups = 1;
   if (groups > p.mtiles) groups = p.mtiles;
   p.groups = groups;
   const dim3 grid((unsigned)(groups * p.ntn));
-  if (mode == 1 && K == 512) {
-    if (res)
-      conv_pw_rb_kernel<true, 512><<<grid, 512, 0, stream>>>(p);
-    else
-      conv_pw_rb_kernel<false, 512><<<grid, 512, 0, stream>>>(p);
-  } else if (mode == 1) {
-    if (res)
-      conv_pw_rb_kernel<true, 256><<<grid, 512, 0, stream>>>(p);
-    else
-      conv_pw_rb_kernel<false, 256><<<grid, 512, 0, stream>>>(p);
+  if (mode == 1 || mode == 2) {                     // 2: residual at its own tile (A/B form)
+    auto go = [&](auto kw_tag) {
+      constexpr int KWv = decltype(kw_tag)::value;
+      if (res && mode == 2)
+        conv_pw_rb_kernel<true, KWv, 0><<<grid, 512, 0, stream>>>(p);
+      else if (res)
+        conv_pw_rb_kernel<true, KWv, 1><<<grid, 512, 0, stream>>>(p);
+      else
+        conv_pw_rb_kernel<false, KWv, 1><<<grid, 512, 0, stream>>>(p);
+    };
+    if (K == 128) go(std::integral_constant<int, 128>{});
+    else if (K == 256) go(std::integral_constant<int, 256>{});
+    else go(std::integral_constant<int, 512>{});
   } else if (res) {
     conv_pw_kernel<true><<<grid, 512, 0, stream>>>(p);
   } else {

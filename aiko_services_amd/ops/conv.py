@@ -272,7 +272,13 @@ WIDE_DEEP_TILES = ((256, 256), (256, 128), (128, 256))
 # 4-slot K-block ring across tile boundaries, residual DMA'd into LDS, fixed channel block per
 # workgroup; 77.9 vs 80 us on the stage-3 expansion at B=320.  Variant 13 (K == 256): the
 # workgroup's 128 x 256 weight block resident in LDS, 64-pixel tiles through an 8-slot ring (seven
-# blocks in flight): 65.6 us there (the tuner's pick; 500 TF, 4.4 TB/s counting the residual)
+# blocks in flight): 65.6 us there (the tuner's pick; 500 TF, 4.4 TB/s counting the residual).
+# Round 4: variant 13 also takes K == 128 (256 x 128 weight block, 4-slot ring) and DMAs the residual
+# one tile ahead; variant 14 is the same kernel with the residual issued at its own tile (A/B form,
+# tuned only with AIKO_PW_AB=1).  Measured at B=320 (scripts/pw_check.sh, same box): K=128 -> 512
+# expansion 105.5 (13) vs 110.9 us (14) and vs 133 us for the best tiled kernel (5.6 TB/s counting the
+# residual); K=256 -> 1024 71.4 vs 71.8; K=512 -> 2048 81.1 vs 79.8 (the tiled kernel, 47 us, wins)
+_PW_AB = __import__("os").environ.get("AIKO_PW_AB") == "1"
 
 
 def buf_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = None) -> bool:
@@ -316,13 +322,19 @@ def patch_weight(spec: ConvSpec) -> torch.Tensor:
     return img
 
 
-def pw_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = None) -> bool:
-    """Whether the persistent pointwise kernel (variant 12, conv_pw.hip) applies: a 1x1 / stride 1
-    single-source conv with K % 256 == 0 (4-slot ring of 64-deep K blocks), Cout % 128 == 0 and
-    16-byte aligned pixel rows."""
-    return (spec.kind != "stem" and x2 is None and spec.K1 is None and spec.R == 1 and spec.S == 1
-            and spec.stride == 1 and spec.pad == 0 and spec.Cc == spec.K and spec.K % 256 == 0
-            and spec.cout % 128 == 0 and x.stride(2) % 8 == 0) and ("resident" if spec.K in (256, 512) else True)
+def pw_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = None):
+    """Whether the persistent pointwise kernels (conv_pw.hip) apply to a 1x1 / stride 1
+    single-source conv with 16-byte aligned pixel rows: ``True`` for variant 12 only (K % 256 == 0,
+    Cout % 128 == 0), ``"resident"`` for variants 12 and 13 (K = 256 / 512), ``"resident_only"``
+    for variant 13 alone (K = 128, Cout % 256 == 0: the 256 x 128 resident weight block)."""
+    if not (spec.kind != "stem" and x2 is None and spec.K1 is None and spec.R == 1 and spec.S == 1
+            and spec.stride == 1 and spec.pad == 0 and spec.Cc == spec.K and x.stride(2) % 8 == 0):
+        return False
+    if spec.K == 128:
+        return "resident_only" if spec.cout % 256 == 0 else False
+    if spec.K % 256 or spec.cout % 128:
+        return False
+    return "resident" if spec.K in (256, 512) else True
 
 
 def narrow_variant_ok(spec: ConvSpec, x2: torch.Tensor | None = None) -> bool:
@@ -334,7 +346,7 @@ def narrow_variant_ok(spec: ConvSpec, x2: torch.Tensor | None = None) -> bool:
             and spec.Cc in (16, 32) and spec.cout in (16, 32))
 
 
-def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, pw_ok=False):
+def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, pw_ok=False, has_res=False):
     if cout <= 32:
         cands = [t + (0,) for t in NARROW_TILES]
         if narrow_ok:
@@ -353,10 +365,12 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, p
             cands += [t + (11,) for t in WIDE_DEEP_TILES]
         if patch_ok:
             cands.append((8, 64, 10))        # variant 10: tile fixed by the kernel (8 rows x W)
-        if pw_ok:
+        if pw_ok and pw_ok != "resident_only":
             cands.append((128, 128, 12))     # variant 12: persistent pointwise GEMM (conv_pw.hip)
-            if pw_ok == "resident":
-                cands.append((64, 128, 13))  # variant 13: the same with the weight block resident in LDS
+        if pw_ok in ("resident", "resident_only"):
+            cands.append((64, 128, 13))      # variant 13: the same with the weight block resident in LDS
+            if has_res and _PW_AB:
+                cands.append((64, 128, 14))  # variant 14: variant 13 with each tile's residual issued at its own tile
     skip = {int(v) for v in __import__("os").environ.get("AIKO_CONV_SKIP", "").split(",") if v.strip()}
     if skip:                                   # A/B runs: exclude variants from the tuner
         cands = [t for t in cands if (t[2] if len(t) > 2 else 0) not in skip] or cands
@@ -455,7 +469,7 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None
             if _tuning:
                 tile = _tune(key, M, spec.cout, launch, buf_variant_ok(spec, x, x2), narrow_variant_ok(spec, x2),
                              patch_variant_ok(spec, x, residual, x2, out) and not residual_after_act,
-                             pw_variant_ok(spec, x, x2))
+                             pw_variant_ok(spec, x, x2), residual is not None)
             else:
                 tile = pick_tile(M, spec.cout)
     launch(tile)

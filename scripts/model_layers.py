@@ -3,7 +3,9 @@
 
     python scripts/model_layers.py [--model resnet50|yolov8n] [--batch 256]
 Records every conv2d call of one forward, then replays each alone (20 iterations) and prints
-layer, GEMM shape, tile/variant, us, TFLOP/s and TB/s, plus the sum vs the whole forward.
+layer, GEMM shape, tile/variant, us, TFLOP/s and TB/s (input + output + residual + fused-shortcut
+source bytes, each counted once; round 3's tables left the residual out), plus the sum vs the whole
+forward.
 """
 import argparse
 import os
@@ -40,7 +42,13 @@ def main():
 
     def rec(x, spec, *args, **kw):
         out = orig(x, spec, *args, **kw)
-        calls.append((spec, x.shape, out.shape, lambda: orig(x, spec, *args, **kw)))
+        res = kw.get("residual", args[0] if args else None)
+        x2 = kw.get("x2")
+        # bytes each call moves at least once: input, output, residual, and the fused shortcut's
+        # second source (K - K1 channels per output pixel)
+        extra = (res.numel() if res is not None else 0) + (out.shape[0] * out.shape[1] * out.shape[2] * (spec.K - spec.K1)
+                                                          if x2 is not None and spec.K1 else 0)
+        calls.append((spec, x.shape, out.shape, lambda: orig(x, spec, *args, **kw), extra))
         return out
     C.conv2d = rec
     import aiko_services_amd.models.resnet50 as R
@@ -64,12 +72,12 @@ def main():
 
     total_fwd = timeit(fwd, a.iters)
     rows, tot = [], 0.0
-    for i, (spec, xs, ys, fn) in enumerate(calls):
+    for i, (spec, xs, ys, fn, extra) in enumerate(calls):
         us = timeit(fn, a.iters)
         tot += us
         M = ys[0] * ys[1] * ys[2]
         flops = 2 * M * spec.cout * spec.K
-        nbytes = (xs[0] * xs[1] * xs[2] * xs[3] + M * spec.cout) * 2
+        nbytes = (xs[0] * xs[1] * xs[2] * min(xs[3], spec.Cc) + M * spec.cout + extra) * 2
         key = [k for k in C._tile_cache if k[0] == M and k[1] == spec.cout and k[2] == spec.K]
         tile = C._tile_cache[key[0]] if key else "?"
         rows.append((us, f"{i:3d} M={M:7d} N={spec.cout:4d} K={spec.K:5d} R={spec.R} s={spec.stride} "

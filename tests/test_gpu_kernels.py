@@ -139,6 +139,17 @@ def _nhwc(x_nchw):
     (64, 7, 7, 512, 2048, 1, 1, 0, "relu", True, (64, 128, 13)),
     (8, 28, 28, 512, 128, 1, 1, 0, "relu", False, (64, 128, 13)),
     (9, 14, 14, 512, 256, 1, 1, 0, None, True, (64, 128, 13)),
+    # K = 128: a 256 x 128 weight block per workgroup, 4-slot ring (1.5 tiles ahead), residual one
+    # tile ahead in two 32 KB buffers — M tails, a single tile, odd / even tile counts, no residual
+    (1, 7, 7, 128, 512, 1, 1, 0, "relu", True, (64, 128, 13)),
+    (3, 28, 28, 128, 512, 1, 1, 0, "relu", True, (64, 128, 13)),
+    (64, 28, 28, 128, 512, 1, 1, 0, "relu", True, (64, 128, 13)),
+    (33, 28, 28, 128, 256, 1, 1, 0, None, True, (64, 128, 13)),
+    (5, 20, 20, 128, 768, 1, 1, 0, "silu", False, (64, 128, 13)),
+    # variant 14: the resident kernels with each tile's residual issued at its own tile
+    (64, 28, 28, 128, 512, 1, 1, 0, "relu", True, (64, 128, 14)),
+    (65, 14, 14, 256, 1024, 1, 1, 0, "relu", True, (64, 128, 14)),
+    (64, 7, 7, 512, 2048, 1, 1, 0, "relu", True, (64, 128, 14)),
 ])
 def test_conv_igemm_matches_torch(native, B, H, W, cin, cout, k, stride, pad, act, res, tile):
     from aiko_services_amd.ops import conv as C
@@ -469,15 +480,15 @@ def test_stem_pool_fused(native, hw):
         assert torch.equal(outs[3], outs[0]) and torch.equal(outs[4], outs[0])
 
 
-@pytest.mark.parametrize("tile", [(128, 128, 12), (64, 128, 13)])
-def test_conv_pw_slices_and_post_residual(native, tile):
+@pytest.mark.parametrize("tile,K", [((128, 128, 12), 256), ((64, 128, 13), 256), ((64, 128, 13), 128)])
+def test_conv_pw_slices_and_post_residual(native, tile, K):
     """conv_pw (variants 12 / 13): input from a channel slice (pitch 384 != K), output into a
     slice of a concat buffer, residual added after the activation (YOLO bottleneck form) — the
     same result as the register-staged kernel within bf16 rounding, nothing outside the slice."""
     from aiko_services_amd.ops import conv as C
     from aiko_services_amd.ops import reference as R
     g = torch.Generator().manual_seed(17)
-    B, H, W, K, N = 9, 14, 14, 256, 256
+    B, H, W, N = 9, 14, 14, 256
     big = torch.randn(B, H, W, 384, generator=g).to(torch.bfloat16).to(DEV)
     xin = big[..., 64:64 + K]
     w = torch.randn(N, K, 1, 1, generator=g) / 16
