@@ -28,6 +28,9 @@ int aiko_conv_wide(const void* x, const void* w, const float* bias, const void* 
                    int K1, int H2, int W2, int C2, int stride2, int occ, hipStream_t stream);
 int aiko_conv_pw(const void* x, const void* w, const float* bias, const void* res, void* y, int M, int N,
                  int K, int ldx, int ldy, int ldr, int act, int cus, int mode, hipStream_t stream);
+int aiko_conv_pw_dual(const void* x, const void* x2, const void* w, const float* bias, void* y, int M, int N,
+                      int ldx, int ldx2, int ldy, int act, int Ho, int Wo, int H2, int W2, int s2, int cus,
+                      hipStream_t stream);
 int aiko_conv_persist(const void* x, const void* w, const float* bias, const void* res, void* y,
                       int H, int W, int C, int Cc, int R, int S, int stride, int pad, int Ho, int Wo,
                       int M, int Cout, int K, int act, int ldy, int ldr, int bm, int bn, const void* x2,
@@ -217,6 +220,20 @@ void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, co
     rc = aiko_conv_wide(x.data_ptr(), w.data_ptr(), bptr, rptr, y.data_ptr(), H, W, C, Cc, R, S, stride,
                         pad, Ho, Wo, M, Cout, K, act, ldy, ldr, bm, bn, x2ptr, K1, H2, W2, C2, stride2,
                         variant == 11 ? 11 : (variant == 9 ? 2 : 1), cur_stream());
+  } else if (variant == 13 && dual) {
+    // fused projection on the resident-weight pointwise kernel (conv_pw.hip): 1x1 main source of
+    // 128 channels + a 1x1 / stride-s2 second source of 256 channels
+    TORCH_CHECK(R == 1 && S == 1 && stride == 1 && pad == 0 && Cc == 128 && K1 == 128 && K == 384 &&
+                    Cout % 128 == 0 && C % 8 == 0 && !rptr && x_extent * 2 < (1LL << 31) - 64 &&
+                    avail_elems(*x2) * 2 < (1LL << 31) - 64 && avail_elems(y) * 2 < (1LL << 31) && ldy % 8 == 0,
+                "aiko.conv_igemm_out: variant 13 with a second source needs a 128 + 256 column 1x1 projection, "
+                "Cout % 128 == 0, no residual and operands < 2 GiB");
+    TORCH_CHECK(!bptr || reinterpret_cast<uintptr_t>(bptr) % 16 == 0, "aiko.conv_igemm_out: bias alignment");
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    rc = aiko_conv_pw_dual(x.data_ptr(), x2ptr, w.data_ptr(), bptr, y.data_ptr(), M, Cout, C, C2, ldy, act, Ho, Wo,
+                           H2, W2, stride2, cus, cur_stream());
   } else if (variant == 12 || variant == 13 || variant == 14) {
     // persistent pointwise GEMM (conv_pw.hip): 1x1 / stride 1 / one source, K % 256 == 0,
     // Cout % 128 == 0, x rows = pixels at pitch C
@@ -814,8 +831,10 @@ void gemm_fp8_out(const at::Tensor& a, const c10::optional<at::Tensor>& sa_opt, 
   } else {
     TORCH_CHECK(yp != nullptr, "aiko.gemm_fp8_out: y (or yq) required");
   }
-  TORCH_CHECK(!(mx_in || mx_out) || (variant == 1 && bn == 128) || (variant == 3 && bm == 256 && bn == 256 && N % 256 == 0),
-              "aiko.gemm_fp8_out: MX paths need variant 1 with BN 128, or variant 3 (256 x 256, N % 256 == 0)");
+  TORCH_CHECK(!(mx_in || mx_out) || (variant == 1 && bn == 128) || (variant == 3 && bm == 256 && bn == 256 && N % 256 == 0) ||
+                  (variant == 4 && !mx_in && bm == 256 && bn == 256 && N % 256 == 0),
+              "aiko.gemm_fp8_out: MX paths need variant 1 with BN 128, variant 3 (256 x 256, N % 256 == 0) or "
+              "variant 4 (persistent 256 x 256, MX output only)");
   const float* bp = nullptr;
   if (bias.has_value() && bias->defined()) {
     check_cuda(*bias, "bias");

@@ -57,13 +57,19 @@ __device__ __forceinline__ void pw_vm_barrier() {
 }
 
 struct PwParams {
-  const bf16_t* x;      // [M][ldx], K channels used
+  const bf16_t* x;      // [M][ldx], K channels used (the first KA of them with a second source)
   const bf16_t* w;      // [N][K]
   const float* bias;    // [N] or nullptr
   const bf16_t* res;    // [M][ldr] or nullptr
   bf16_t* y;            // [M][ldy]
   int M, N, K, ldx, ldy, ldr, act;
   int ntn, mtiles, groups;
+  // optional second source (K columns [KA, K)): a 1x1 / stride-s2 conv over x2 [B][H2][W2][ldx2]
+  // sampled at output pixel (n, ho, wo) -> (n, s2 ho, s2 wo): the ResNet projection shortcut
+  const bf16_t* x2;
+  int ldx2, hw, wo, h2, w2, s2;
+  uint32_t mhw, mwo;
+  int lhw, lwo;
 };
 
 template <bool RES>
@@ -337,14 +343,15 @@ __host__ __device__ constexpr int pw_young_res(int t, int NKB, int LA, int NR, i
   return cnt;
 }
 
-template <bool RES, int KW, int PF = 1>
+template <bool RES, int KW, int PF = 1, int KA = KW>
 __global__ __launch_bounds__(512, 1) void conv_pw_rb_kernel(PwParams p) {
-  static_assert(KW == 128 || KW == 256 || KW == 512, "K = 128, 256 or 512");
+  static_assert(KW == 128 || KW == 256 || KW == 384 || KW == 512, "K = 128, 256, 384 or 512");
   static_assert(PF == 0 || PF == 1, "residual issued at its own tile (0) or one tile ahead (1)");
-  constexpr int BN = KW == 128 ? 256 : KW == 256 ? 128 : 64;
-  constexpr int BM = 64, BK = 64, NKB = KW / BK;
-  constexpr int NS = KW == 128 ? 4 : 8;
-  constexpr int WGN = KW == 128 ? 8 : KW == 256 ? 4 : 2;
+  static_assert(KA == KW || (KW == 384 && KA == 128 && !RES), "second source: 128 + 256 columns, no residual");
+  constexpr int BN = KW == 128 ? 256 : KW == 512 ? 64 : 128;
+  constexpr int BM = 64, BK = 64, NKB = KW / BK, NKA = KA / BK;
+  constexpr int NS = KW == 128 ? 4 : KW == 384 ? 6 : 8;
+  constexpr int WGN = KW == 128 ? 8 : KW == 512 ? 2 : 4;
   constexpr int WM = BM / (8 / WGN), WN = BN / WGN, MI = WM / 16, NI = WN / 16;
   static_assert(NI == 2, "the epilogue pairs two 16-channel fragments");
   constexpr int RPC = BN / 8;                     // 16-B pieces per residual row (32 / 16 / 8)
@@ -375,6 +382,7 @@ __global__ __launch_bounds__(512, 1) void conv_pw_rb_kernel(PwParams p) {
   const __amdgpu_buffer_rsrc_t rw = pw_rsrc(p.w);
   const __amdgpu_buffer_rsrc_t rr = pw_rsrc(RES ? p.res : p.x);
   const __amdgpu_buffer_rsrc_t ry = pw_rsrc(p.y);
+  const __amdgpu_buffer_rsrc_t rx2 = pw_rsrc(KA < KW ? p.x2 : p.x);
 
   const int fr = lane & 15, fq = lane >> 4;
   const int coff = ((fq & 1) << 4) | ((fq >> 1) << 3);
@@ -391,15 +399,16 @@ __global__ __launch_bounds__(512, 1) void conv_pw_rb_kernel(PwParams p) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) asm volatile("" ::"v"(e_bias[e]));
 
-  // resident weights: KW / 8 16-B pieces per row (4 / 2 / 1 rows per wave instruction); LDS
+  // resident weights: KW / 8 16-B pieces per row, 64 consecutive pieces per wave instruction; LDS
   // position pos of row n holds logical piece (pos & ~7) | ((pos & 7) ^ (n & 7))
-  constexpr int WROWS = 64 / (KW / 8);            // rows per wave instruction
+  constexpr int WI = BN * KW / 8 / 512;           // weight DMA instructions per thread (8 / 8 / 12 / 8)
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int row = (i * 8 + wave) * WROWS + lane / (KW / 8);
-    const int pos = lane % (KW / 8);
+  for (int i = 0; i < WI; ++i) {
+    const int idx = (i * 8 + wave) * 64 + lane;
+    const int row = idx / (KW / 8);
+    const int pos = idx % (KW / 8);
     const int lpc = (pos & ~7) | ((pos & 7) ^ (row & 7));
-    pw_dma16(rw, (uint32_t)(((n0 + row) * KW + lpc * 8) * 2), 0u, wres + (i * 8 + wave) * WROWS * KW);
+    pw_dma16(rw, (uint32_t)(((n0 + row) * KW + lpc * 8) * 2), 0u, wres + (i * 8 + wave) * 64 * 8);
   }
 
   const int lrow = wave * 8 + (lane >> 3);         // activation DMA: 8 rows per wave, 64 per block
@@ -413,8 +422,17 @@ __global__ __launch_bounds__(512, 1) void conv_pw_rb_kernel(PwParams p) {
     const int t = f / NKB, kb = f % NKB;
     if (t >= ntiles) return;
     const int m = (group + t * p.groups) * BM + lrow;
-    const uint32_t off = m < p.M ? (uint32_t)((m * p.ldx + lp * 8) * 2) : kPwOOB;
-    pw_dma16(rx, off, (uint32_t)(kb * BK * 2), ring + S * SLOT + wave * 8 * BK);
+    if (KA == KW || kb < NKA) {
+      const uint32_t off = m < p.M ? (uint32_t)((m * p.ldx + lp * 8) * 2) : kPwOOB;
+      pw_dma16(rx, off, (uint32_t)(kb * BK * 2), ring + S * SLOT + wave * 8 * BK);
+    } else {                                       // the strided second source
+      const int n = fdiv(m, p.mhw, p.lhw);
+      const int r = m - n * p.hw;
+      const int ho = fdiv(r, p.mwo, p.lwo);
+      const int row2 = (n * p.h2 + ho * p.s2) * p.w2 + (r - ho * p.wo) * p.s2;
+      const uint32_t off = m < p.M ? (uint32_t)((row2 * p.ldx2 + lp * 8) * 2) : kPwOOB;
+      pw_dma16(rx2, off, (uint32_t)((kb - NKA) * BK * 2), ring + S * SLOT + wave * 8 * BK);
+    }
   };
   auto issue_res = [&](int t, auto buf_tag) {      // residual of tile t into buffer B
     constexpr int B = decltype(buf_tag)::value;
@@ -501,9 +519,11 @@ __global__ __launch_bounds__(512, 1) void conv_pw_rb_kernel(PwParams p) {
       step(t, tail, half_tag, std::integral_constant<int, 2>{});
       step(t, tail, half_tag, std::integral_constant<int, 3>{});
     }
-    if constexpr (NKB == 8) {
+    if constexpr (NKB >= 6) {
       step(t, tail, half_tag, std::integral_constant<int, 4>{});
       step(t, tail, half_tag, std::integral_constant<int, 5>{});
+    }
+    if constexpr (NKB == 8) {
       step(t, tail, half_tag, std::integral_constant<int, 6>{});
       step(t, tail, half_tag, std::integral_constant<int, 7>{});
     }
@@ -620,5 +640,35 @@ extern "C" int aiko_conv_pw(const void* x, const void* w, const float* bias, con
   } else {
     conv_pw_kernel<false><<<grid, 512, 0, stream>>>(p);
   }
+  return (int)hipGetLastError();
+}
+
+// Fused ResNet projection (stage-2 entry): y = act(x[:, :128] . w[:, :128] + x2(strided)[:, :256] .
+// w[:, 128:] + bias) over the resident-weight kernel with a 128 x 384 weight block (96 KB) and a
+// 6-slot ring (one tile per cycle): x [M][ldx] is the block's 3x3 output at (Ho, Wo), x2
+// [B][H2][W2][ldx2] the block input sampled at stride s2.  N % 128 == 0, no residual.
+extern "C" int aiko_conv_pw_dual(const void* x, const void* x2, const void* w, const float* bias, void* y, int M,
+                                 int N, int ldx, int ldx2, int ldy, int act, int Ho, int Wo, int H2, int W2, int s2,
+                                 int cus, hipStream_t stream) {
+  using namespace aiko;
+  if (N % 128 || M <= 0 || M % (Ho * Wo) || ldx % 8 || ldx2 % 8 || ldy % 8 || ldx < 128 || ldx2 < 256) return -1;
+  PwParams p{};
+  p.x = static_cast<const bf16_t*>(x);
+  p.x2 = static_cast<const bf16_t*>(x2);
+  p.w = static_cast<const bf16_t*>(w);
+  p.bias = bias;
+  p.res = nullptr;
+  p.y = static_cast<bf16_t*>(y);
+  p.M = M; p.N = N; p.K = 384; p.ldx = ldx; p.ldy = ldy; p.ldr = 0; p.act = act;
+  p.ldx2 = ldx2; p.hw = Ho * Wo; p.wo = Wo; p.h2 = H2; p.w2 = W2; p.s2 = s2;
+  fastdiv_init(Ho * Wo, &p.mhw, &p.lhw);
+  fastdiv_init(Wo, &p.mwo, &p.lwo);
+  p.ntn = N / 128;
+  p.mtiles = (M + 63) / 64;
+  int groups = (cus > 0 ? cus : 256) / p.ntn;
+  if (groups < 1) groups = 1;
+  if (groups > p.mtiles) groups = p.mtiles;
+  p.groups = groups;
+  conv_pw_rb_kernel<false, 384, 1, 128><<<dim3((unsigned)(groups * p.ntn)), 512, 0, stream>>>(p);
   return (int)hipGetLastError();
 }

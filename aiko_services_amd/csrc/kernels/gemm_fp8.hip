@@ -741,6 +741,204 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_big_kernel(Fp8GemmParams p, c
 }
 
 // ---------------------------------------------------------------------------------------------
+// Persistent 256 x 256 kernel (tuner variant 4) for the short-K encoder GEMMs (qkv: N = 2304,
+// fc1: N = 3072, K = 768 — six K blocks per tile).  gemm_fp8_big_kernel pays, per tile, an
+// unhidden first-block round trip, an fp32 epilogue staged through LDS in two halves behind
+// __syncthreads, and the tile-quantisation tail of a one-shot grid; at K = 768 that is about as
+// long as the six blocks of MFMA work, so the tuner picked the 2-workgroups-per-CU 128 x 128
+// kernel (~1.1 PFLOP/s) instead.  Here one workgroup per CU walks tiles lid, lid + G, ... with
+// ONE 2-slot ring of 64 KB K blocks running across tile boundaries (the next tile's first block
+// is in flight during the current tile's last block and its epilogue), and the epilogue goes
+// straight from registers: the product is transposed (weights on the MFMA A side), so lane l
+// holds four consecutive output COLUMNS of row l & 15 and one v_permlane16_swap per fp32 pair
+// gives it eight — per-channel scale and bias come from LDS (loaded once per workgroup for the
+// whole N), then GELU, then a 16-B bf16 store or MX-fp8 quantisation (32-column blocks = the
+// four lane rows of one fragment pair: two permlane swaps for the block max).  Stores are
+// buffer stores with an out-of-range offset for rows past M (always issued), so the only vmcnt
+// wait that is not 0 — the first block of a tile, whose younger ops are exactly the previous
+// tile's NST stores — is exact.  N % 256 == 0, N <= 3072, K % 128 == 0, K >= 256, per-row A
+// scales (no MX input), no residual.
+template <bool MXO>
+__global__ __launch_bounds__(512, 1) void gemm_fp8_pers_kernel(Fp8GemmParams p, const uint8_t* zero, int tiles_n,
+                                                               int ntiles) {
+  constexpr int BM = 256, BN = 256, BK = 128, WGN = 4, WM = 128, WN = 64, MI = WM / 16, NI = WN / 16;
+  constexpr int APT = BM / 64, BPT = BN / 64;
+  constexpr int STAGE_BYTES = (BM + BN) * BK;  // 64 KB
+  constexpr int MAXN = 3072;
+  constexpr int NST = MXO ? 2 * MI * (NI / 2) : MI * (NI / 2);   // store instructions per tile per wave
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE_BYTES + 2 * MAXN * 4];
+  float* const s_sb = reinterpret_cast<float*>(smem + 2 * STAGE_BYTES);
+  float* const s_bias = s_sb + MAXN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WGN, wc = wave % WGN;
+  const int G = gridDim.x;
+  const int lid = xcd_remap(blockIdx.x, G);
+  if (lid >= ntiles) return;
+  const int my_tiles = (ntiles - 1 - lid) / G + 1;
+  const int nkb = p.K / BK;
+  const int lrow = wave * 8 + (lane >> 3);
+  const int lp = (lane & 7) ^ (lane >> 3);
+  const int fr = lane & 15, fg = lane >> 4;
+  const int coff = ((fg & 1) << 4) | ((fg >> 1) << 3);
+
+  // per-channel scales and bias for the whole N, once (retired by the first block's wait)
+  for (int n = tid; n < p.N; n += 512) {
+    s_sb[n] = p.sb[n];
+    s_bias[n] = p.bias ? p.bias[n] : 0.f;
+  }
+
+  auto issue = [&](int f) {                          // flat K block f of this workgroup's walk
+    const int k = f / nkb, kb = f - k * nkb;
+    if (k >= my_tiles) return;
+    const int tau = lid + k * G;
+    const int m0 = (tau / tiles_n) * BM, n0 = (tau % tiles_n) * BN;
+    unsigned char* As = smem + (f & 1) * STAGE_BYTES;
+    unsigned char* Bs = As + BM * BK;
+    const int k0 = kb * BK;
+#pragma unroll
+    for (int i = 0; i < APT; ++i) {
+      const int m = m0 + lrow + 64 * i;
+      glds16_u8(m < p.M ? p.a + (long)m * p.lda + lp * 16 + k0 : zero, As + (i * 64 + wave * 8) * BK);
+    }
+#pragma unroll
+    for (int i = 0; i < BPT; ++i)
+      glds16_u8(p.b + (long)(n0 + lrow + 64 * i) * p.K + lp * 16 + k0, Bs + (i * 64 + wave * 8) * BK);
+  };
+
+  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(MXO ? (void*)p.yq : (void*)p.y, (short)0,
+                                                                      0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc(MXO ? (void*)p.ysc : (void*)p.y, (short)0,
+                                                                       0x7ffffff0, 0x00020000);
+  const int off_lo = (fg ^ (fr & 7)) << 4, off_hi = ((fg + 4) ^ (fr & 7)) << 4;
+
+  issue(0);
+  f32x4 acc[MI][NI];
+  float rs[MI];
+  for (int k = 0; k < my_tiles; ++k) {
+    const int tau = lid + k * G;
+    const int m0 = (tau / tiles_n) * BM, n0 = (tau % tiles_n) * BN;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kb = 0; kb < nkb; ++kb) {
+      const int f = k * nkb + kb;
+      if (kb == 0 && k > 0) fp8_wait_vm_barrier<NST>();   // younger: the previous tile's stores
+      else fp8_wait_vm_barrier<0>();
+      if (kb == 0) {                                 // row scales, older than the next block's DMA
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int m = m0 + wr * WM + i * 16 + fr;
+          rs[i] = p.sa && m < p.M ? p.sa[m] : 1.f;
+        }
+      }
+      issue(f + 1);
+      const unsigned char* As = smem + (f & 1) * STAGE_BYTES + (wr * WM + fr) * BK;
+      const unsigned char* Bs = smem + (f & 1) * STAGE_BYTES + BM * BK + (wc * WN + fr) * BK;
+      i32x8 bfr[NI];
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const u32x4 lo = *reinterpret_cast<const u32x4*>(Bs + j * 16 * BK + off_lo);
+        const u32x4 hi = *reinterpret_cast<const u32x4*>(Bs + j * 16 * BK + off_hi);
+        bfr[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const u32x4 lo = *reinterpret_cast<const u32x4*>(As + i * 16 * BK + off_lo);
+        const u32x4 hi = *reinterpret_cast<const u32x4*>(As + i * 16 * BK + off_hi);
+        const i32x8 af = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int j = 0; j < NI; ++j)   // transposed: weights first, so lanes end with 4 consecutive columns
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], af, acc[i][j], 0, 0, 0, 127, 0, 127);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    // ---- register-direct epilogue (the ring is not touched: no barrier) ----
+#pragma unroll
+    for (int pp = 0; pp < NI / 2; ++pp) {
+      const int nb = n0 + wc * WN + pp * 32;         // first column of this fragment pair
+      const int n = nb + coff;                       // this lane's 8 columns
+      const f32x4 sc0 = *reinterpret_cast<const f32x4*>(s_sb + n);
+      const f32x4 sc1 = *reinterpret_cast<const f32x4*>(s_sb + n + 4);
+      const f32x4 bi0 = *reinterpret_cast<const f32x4*>(s_bias + n);
+      const f32x4 bi1 = *reinterpret_cast<const f32x4*>(s_bias + n + 4);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int m = m0 + wr * WM + i * 16 + fr;
+        f32x4 lo = acc[i][2 * pp], hi = acc[i][2 * pp + 1];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(lo[e]), __float_as_uint(hi[e]), false, false);
+          lo[e] = __uint_as_float(sw[0]);
+          hi[e] = __uint_as_float(sw[1]);
+        }
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = lo[e] * rs[i] * sc0[e] + bi0[e];
+          v[e + 4] = hi[e] * rs[i] * sc1[e] + bi1[e];
+        }
+        if (p.act == 1) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+        } else if (p.act == 2) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = silu(v[e]);
+        } else if (p.act == 3) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const f32x2 g = gelu_erf2(f32x2{v[2 * e], v[2 * e + 1]});
+            v[2 * e] = g[0];
+            v[2 * e + 1] = g[1];
+          }
+        }
+        const bool live = m < p.M;
+        if constexpr (MXO) {
+          float amax = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[e]));
+          {
+            const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(amax), __float_as_uint(amax), false, false);
+            amax = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+          }
+          {
+            const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(amax), __float_as_uint(amax), false, false);
+            amax = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+          }
+          const int ex = mx_exponent(amax);
+          const float inv = __uint_as_float((uint32_t)(127 - ex) << 23);
+          unsigned w0 = 0u, w1 = 0u;
+          w0 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[0] * inv, -448.f), 448.f),
+                                               fminf(fmaxf(v[1] * inv, -448.f), 448.f), w0, false);
+          w0 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[2] * inv, -448.f), 448.f),
+                                               fminf(fmaxf(v[3] * inv, -448.f), 448.f), w0, true);
+          w1 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[4] * inv, -448.f), 448.f),
+                                               fminf(fmaxf(v[5] * inv, -448.f), 448.f), w1, false);
+          w1 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[6] * inv, -448.f), 448.f),
+                                               fminf(fmaxf(v[7] * inv, -448.f), 448.f), w1, true);
+          typedef __attribute__((ext_vector_type(2))) unsigned u32x2v;
+          const uint32_t qoff = live ? (uint32_t)((long)m * p.ldq + n) : 0x80000000u;
+          __builtin_amdgcn_raw_buffer_store_b64(u32x2v{w0, w1}, ry, qoff, 0, 0);
+          const uint32_t soff = live && fg == 0 ? (uint32_t)(((long)(nb >> 7) * p.ysr + m) * 4 + ((nb >> 5) & 3))
+                                                : 0x80000000u;
+          __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(ex + 127), rsc, soff, 0, 0);
+        } else {
+          u32x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = pack2(v[2 * e], v[2 * e + 1]);
+          const uint32_t yoff = live ? (uint32_t)(((long)m * p.ldy + n) * 2) : 0x80000000u;
+          __builtin_amdgcn_raw_buffer_store_b128(o, ry, yoff, 0, 0);
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------------------------
 // Row-wise LayerNorm and/or fp8 quantisation, one wave per row (wave64 reductions):
 //   z = gamma ? (x - mean) * rstd * gamma + beta : x
 //   yb (optional) = bf16(z);  q (optional) = e4m3(z / s), s = amax(|z|) / 448 per row.
@@ -891,7 +1089,7 @@ extern "C" int aiko_gemm_fp8(const void* a, const void* b, const float* sa, cons
   p.ysc = static_cast<uint8_t*>(ysc);
   p.ldq = ldq;
   p.ysr = ysr;
-  if ((amx || yq) && variant != 1 && variant != 3) return -1;   // MX paths: LDS-DMA kernels
+  if ((amx || yq) && variant != 1 && variant != 3 && variant != 4) return -1;   // MX paths: LDS-DMA kernels
   p.a = static_cast<const uint8_t*>(a);
   p.b = static_cast<const uint8_t*>(b);
   p.sa = sa; p.sb = sb; p.bias = bias;
@@ -899,6 +1097,22 @@ extern "C" int aiko_gemm_fp8(const void* a, const void* b, const float* sa, cons
   p.y = static_cast<bf16_t*>(y);
   p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldy = ldy; p.ldr = ldr; p.act = act;
   dim3 grid(((M + bm - 1) / bm) * ((N + bn - 1) / bn)), block(256);
+  if (variant == 4) {                   // persistent 256 x 256 (short-K qkv / fc1 shapes)
+    const uint8_t* z = static_cast<const uint8_t*>(zero);
+    if (!z || amx || res || bm != 256 || bn != 256 || N % 256 || N > 3072 || K % 128 || K < 256) return -1;
+    if ((long)M * (yq ? ldq : 2L * ldy) >= 0x7ffffff0L || (yq && (long)(N / 128) * ysr * 4 >= 0x7ffffff0L)) return -1;
+    static int cus = 0;
+    if (cus == 0) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    }
+    const int tiles_n = N / 256, ntiles = ((M + 255) / 256) * tiles_n;
+    const dim3 pg((unsigned)(ntiles < cus ? ntiles : cus));
+    if (yq) gemm_fp8_pers_kernel<true><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles);
+    else gemm_fp8_pers_kernel<false><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles);
+    return (int)hipGetLastError();
+  }
   if (variant == 3) {
     const uint8_t* z = static_cast<const uint8_t*>(zero);
     if (!z || bm != 256 || bn != 256) return -1;

@@ -279,6 +279,8 @@ WIDE_DEEP_TILES = ((256, 256), (256, 128), (128, 256))
 # expansion 105.5 (13) vs 110.9 us (14) and vs 133 us for the best tiled kernel (5.6 TB/s counting the
 # residual); K=256 -> 1024 71.4 vs 71.8; K=512 -> 2048 81.1 vs 79.8 (the tiled kernel, 47 us, wins)
 _PW_AB = __import__("os").environ.get("AIKO_PW_AB") == "1"
+# variant 13 as the fused stage-2 projection (conv_pw_rb_kernel<false, 384, 1, 128>) in the tuner
+_PW_DUAL = __import__("os").environ.get("AIKO_PW_DUAL", "0") == "1"
 
 
 def buf_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = None) -> bool:
@@ -326,7 +328,12 @@ def pw_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = Non
     """Whether the persistent pointwise kernels (conv_pw.hip) apply to a 1x1 / stride 1
     single-source conv with 16-byte aligned pixel rows: ``True`` for variant 12 only (K % 256 == 0,
     Cout % 128 == 0), ``"resident"`` for variants 12 and 13 (K = 256 / 512), ``"resident_only"``
-    for variant 13 alone (K = 128, Cout % 256 == 0: the 256 x 128 resident weight block)."""
+    for variant 13 alone (K = 128, Cout % 256 == 0: the 256 x 128 resident weight block), ``"dual"``
+    for variant 13 as a fused stage-2 projection (128 main + 256 strided shortcut columns)."""
+    if x2 is not None:
+        return "dual" if (spec.kind != "stem" and spec.K1 == 128 and spec.K == 384 and spec.Cc == 128
+                          and spec.R == 1 and spec.S == 1 and spec.stride == 1 and spec.pad == 0
+                          and spec.cout % 128 == 0 and x.stride(2) % 8 == 0 and x2.stride(2) % 8 == 0) else False
     if not (spec.kind != "stem" and x2 is None and spec.K1 is None and spec.R == 1 and spec.S == 1
             and spec.stride == 1 and spec.pad == 0 and spec.Cc == spec.K and x.stride(2) % 8 == 0):
         return False
@@ -365,9 +372,9 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, p
             cands += [t + (11,) for t in WIDE_DEEP_TILES]
         if patch_ok:
             cands.append((8, 64, 10))        # variant 10: tile fixed by the kernel (8 rows x W)
-        if pw_ok and pw_ok != "resident_only":
+        if pw_ok and pw_ok not in ("resident_only", "dual"):
             cands.append((128, 128, 12))     # variant 12: persistent pointwise GEMM (conv_pw.hip)
-        if pw_ok in ("resident", "resident_only"):
+        if pw_ok in ("resident", "resident_only") or (pw_ok == "dual" and not has_res and _PW_DUAL):
             cands.append((64, 128, 13))      # variant 13: the same with the weight block resident in LDS
             if has_res and _PW_AB:
                 cands.append((64, 128, 14))  # variant 14: variant 13 with each tile's residual issued at its own tile

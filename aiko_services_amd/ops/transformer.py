@@ -166,6 +166,8 @@ def _tune_fp8(key, launch, mx=False):
             cands.append((256, 128, 2))  # 8-wave LDS-DMA kernel (one workgroup per CU)
     if key[1] % 256 == 0:
         cands.append((256, 256, 3))      # 256 x 256 tile, 8 waves of 128 x 64 (MX in / out too)
+        if key[1] <= 3072 and not key[4] and not key[6] and os.environ.get("AIKO_FP8_PERSIST", "0") == "1":
+            cands.append((256, 256, 4))  # persistent 256 x 256, register-direct epilogue (no residual / MX input)
     skip = {s.strip() for s in os.environ.get("AIKO_FP8_SKIP", "").split(",") if s.strip()}
     cands = [t for t in cands if ",".join(map(str, t)) not in skip] or cands
     for t in cands:
@@ -183,6 +185,8 @@ def _tune_fp8(key, launch, mx=False):
             e1.synchronize()
             times.append(e0.elapsed_time(e1))
         ms = sorted(times)[2]
+        if _conv._TUNE_VERBOSE:
+            print(f"[tune fp8] M={key[0]} N={key[1]} K={key[2]} {t}: {ms * 1e3:.1f} us", flush=True)
         if best_t is None or ms < best_t:
             best, best_t = t, ms
     _tile_cache[key] = best

@@ -414,6 +414,33 @@ def test_fused_projection_shortcut(native, B, H, cin_main, cin_sc, cout, stride,
     assert _rel_err(y.permute(0, 3, 1, 2), ref) < 1e-2
 
 
+@pytest.mark.parametrize("B,H,cout,stride", [(2, 56, 512, 2), (3, 56, 512, 2), (1, 28, 128, 1), (5, 18, 384, 2),
+                                             (40, 56, 512, 2)])
+def test_fused_projection_pw_dual(native, B, H, cout, stride):
+    """Variant 13 with a second source (conv_pw.hip, K = 128 main + 256 strided shortcut columns,
+    128 x 384 resident weight block): M tails, one / many tiles per workgroup, stride 1 and 2, odd
+    output sizes (Ho = 9), every output written."""
+    from aiko_services_amd.ops import conv as C
+    from aiko_services_amd.ops import reference as R
+    g = torch.Generator().manual_seed(B * 100 + H + cout)
+    Ho = (H - 1) // stride + 1
+    w3 = torch.randn(cout, 128, 1, 1, generator=g) / 128 ** 0.5
+    wd = torch.randn(cout, 256, 1, 1, generator=g) / 256 ** 0.5
+    b3, bd = torch.randn(cout, generator=g), torch.randn(cout, generator=g)
+    main = C.make_conv_spec(w3, b3, act="relu", device=DEV)
+    down = C.make_conv_spec(wd, bd, stride=stride, device=DEV)
+    fused = C.fuse_shortcut(main, down)
+    t = torch.randn(B, Ho, Ho, 128, generator=g).to(torch.bfloat16).to(DEV)
+    x = torch.randn(B, H, H, 256, generator=g).to(torch.bfloat16).to(DEV)
+    out = torch.full((B, Ho, Ho, cout), float("nan"), dtype=torch.bfloat16, device=DEV)
+    y = C.conv2d(t, fused, x2=x, out=out, tile=(64, 128, 13))
+    torch.cuda.synchronize()
+    assert torch.isfinite(y.float()).all()
+    idn = R.conv_ref(x.permute(0, 3, 1, 2).float(), down)
+    ref = R.conv_ref(t.permute(0, 3, 1, 2).float(), main, idn)
+    assert _rel_err(y.permute(0, 3, 1, 2), ref) < 1e-2
+
+
 def test_resize_u8(native):
     from aiko_services_amd.ops import vision as V
     frames = torch.randint(0, 256, (2, 37, 53, 3), dtype=torch.uint8, device=DEV)

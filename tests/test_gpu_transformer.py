@@ -33,6 +33,45 @@ def test_gemm_fp8(native, tile, act):
     assert _rel(y, ref) < 5e-3
 
 
+@pytest.mark.parametrize("M,N,K,act", [(333, 512, 768, 0), (333, 512, 768, 3), (3000, 2304, 768, 0),
+                                       (21014, 3072, 768, 3), (700, 768, 3072, 0), (1, 256, 256, 0)])
+def test_gemm_fp8_persistent(native, M, N, K, act):
+    """Variant 4 (persistent 256 x 256, transposed product, register-direct epilogue): M tails,
+    one and several tiles per workgroup (21014 x 3072: 996 tiles on the CUs), a single-row M,
+    long K; rows past M untouched."""
+    from aiko_services_amd.ops import transformer as TR
+    g = torch.Generator().manual_seed(M + N + act)
+    x = torch.randn(M, K, generator=g)
+    lin = TR.make_fp8_linear(torch.randn(N, K, generator=g) / 30, torch.randn(N, generator=g) * 0.1, DEV)
+    xq, xs = TR.quantize_rows_ref(x)
+    out = torch.full((M + 3, N), 7.0, dtype=torch.bfloat16, device=DEV)
+    TR.linear_fp8(xq.to(DEV), xs.to(DEV), lin, out=out[:M], act=act, tile=(256, 256, 4))
+    ref = (xq.view(torch.float8_e4m3fn).float() * xs[:, None]).to(DEV) @ lin.ref_weight.T.to(DEV) + lin.bias
+    if act == 3:
+        ref = F.gelu(ref)
+    assert _rel(out[:M], ref) < 5e-3
+    assert bool((out[M:] == 7.0).all())
+
+
+@pytest.mark.parametrize("M,N", [(300, 512), (5000, 3072)])
+def test_gemm_fp8_persistent_mx_out(native, M, N):
+    """Variant 4 with GELU + MX-fp8 output (the fc1 -> fc2 hand-off): block max over the four
+    lane rows of a fragment pair (two permlane swaps), same E8M0 scales as the reference."""
+    from aiko_services_amd.ops import transformer as TR
+    g = torch.Generator().manual_seed(N + 5)
+    K = 768
+    lin = TR.make_fp8_linear(torch.randn(N, K, generator=g) / 20, torch.randn(N, generator=g) * 0.1, DEV)
+    xq, xs = TR.quantize_rows_ref(torch.randn(M, K, generator=g))
+    oq, osc = TR.mx_buffers(M, N, DEV)
+    TR.linear_fp8(xq.to(DEV), xs.to(DEV), lin, act=TR.ACT_GELU, out_mx=(oq, osc), tile=(256, 256, 4))
+    full = F.gelu((xq.view(torch.float8_e4m3fn).float() * xs[:, None]).to(DEV) @ lin.ref_weight.T.to(DEV) + lin.bias)
+    rq, rsc = TR.mx_quantize_ref(full.cpu())
+    got = TR.mx_dequant(oq.cpu(), osc.cpu())
+    assert (osc.cpu()[:, :M] == rsc[:, :M]).float().mean() > 0.98
+    assert _rel(got, full.cpu()) < 4e-2
+    assert _rel(got, TR.mx_dequant(rq, rsc)) < 1e-2
+
+
 def test_rownorm_quant(native):
     from aiko_services_amd.ops import transformer as TR
     g = torch.Generator().manual_seed(2)
