@@ -279,7 +279,9 @@ WIDE_DEEP_TILES = ((256, 256), (256, 128), (128, 256))
 # expansion 105.5 (13) vs 110.9 us (14) and vs 133 us for the best tiled kernel (5.6 TB/s counting the
 # residual); K=256 -> 1024 71.4 vs 71.8; K=512 -> 2048 81.1 vs 79.8 (the tiled kernel, 47 us, wins)
 _PW_AB = __import__("os").environ.get("AIKO_PW_AB") == "1"
-# variant 13 as the fused stage-2 projection (conv_pw_rb_kernel<false, 384, 1, 128>) in the tuner
+# variant 13 as the fused stage-2 projection (conv_pw_rb_kernel<false, 384, 1, 128>) in the tuner:
+# numerics-tested but measured slower than conv_wide's 256 x 256 tile (167 vs 154 us at B=320 — the
+# strided second source streams from HBM behind a 5-block lookahead), so opt-in
 _PW_DUAL = __import__("os").environ.get("AIKO_PW_DUAL", "0") == "1"
 
 
