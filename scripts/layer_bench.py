@@ -21,6 +21,7 @@ LAYERS = {
     "b1.conv3": (64, 256, 1, 1, 56, True, 0),
     "b3.conv1": (256, 128, 1, 1, 56, False, 0),
     "b3.conv2": (128, 128, 3, 2, 56, False, 0),
+    "b4.conv2": (128, 128, 3, 1, 28, False, 0),
     "b4.conv3": (128, 512, 1, 1, 28, True, 0),
     "b8.conv2": (256, 256, 3, 1, 14, False, 0),
     "b8.conv3": (256, 1024, 1, 1, 14, True, 0),
