@@ -266,7 +266,10 @@ WIDE_OCC_TILES = ((128, 128), (256, 64), (128, 64), (64, 128), (64, 64))
 # variant 11: the same kernel with 32-deep K blocks in a 4-slot ring (three blocks in flight
 # across each barrier instead of one for the 256-wide tiles) — the long-K compute-bound layers.
 # Measured on the ResNet-50 layers (MI355X, round 3): never the tuner's pick against variant 8,
-# i.e. the 2-slot 64-deep ring is not what limits those tiles; kept as a candidate
+# i.e. the 2-slot 64-deep ring is not what limits those tiles; kept as a candidate.  Round 4: a
+# 256 x 256 form with split rings (3 activation slots + 2 weight slots = 160 KB, activations two
+# blocks ahead) measured 70.8 vs 68.0 us on the stage-3 3x3 (PMC of variant 11 vs 8: wait share
+# 37 vs 40 %, twice the L2 requests at 64-B rows) — dropped
 WIDE_DEEP_TILES = ((256, 256), (256, 128), (128, 256))
 # variant 12 (conv_pw.hip): persistent pointwise GEMM for 1x1/s1 convs with K % 256 == 0 — one
 # 4-slot K-block ring across tile boundaries, residual DMA'd into LDS, fixed channel block per
