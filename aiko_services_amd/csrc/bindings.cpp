@@ -47,6 +47,8 @@ int aiko_stem_direct(const void* in, void* out, const void* w, const float* bias
                      int Ho, int Wo, int Hc, int Wc, int off_t, int off_l, float fill, const float* mean,
                      const float* std, int bgr, int H1, int W1, int Cout, int ldo, int k, int stride, int pad,
                      int act, hipStream_t stream);
+int aiko_conv3x3_patchw(const void* x, const void* wimg, const float* bias, void* y, int B, int H, int W, int ldx,
+                        int ldy, int act, int grid, hipStream_t stream);
 int aiko_conv3x3_patch(const void* x, const void* wimg, const float* bias, void* y, int B, int H, int W, int ldy,
                        int act, int grid, hipStream_t stream);
 int aiko_bneck_fused(const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
@@ -356,6 +358,40 @@ void conv3x3_patch_out(const at::Tensor& x, const at::Tensor& wimg, const c10::o
   check_launch(aiko_conv3x3_patch(x.data_ptr(), wimg.data_ptr(), bptr, y.data_ptr(), (int)B, (int)H, (int)W,
                                   (int)y.stride(2), (int)act, (int)grid, cur_stream()),
                "conv3x3_patch");
+}
+
+// 3x3 / stride 1 / pad 1 conv, 128 -> 128 channels, W = 28, patch per 14-row tile with streamed
+// weights (conv_patchw.hip).  x [B, H, 28, >= 128] NHWC (16-B aligned pixel pitch); wimg the
+// [4, 9, 8, 64, 8] fragment image (ops.conv.patchw_weight); y [B, H, 28, >= 128] NHWC.
+void conv3x3_patchw_out(const at::Tensor& x, const at::Tensor& wimg, const c10::optional<at::Tensor>& bias,
+                        at::Tensor& y, int64_t act, int64_t grid) {
+  check_cuda(x, "x");
+  check_cuda(wimg, "wimg");
+  check_cuda(y, "y");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && wimg.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16,
+              "aiko.conv3x3_patchw_out: bf16 tensors");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) >= 128 && x.size(2) == 28 && x.stride(3) == 1 && x.stride(2) % 8 == 0 &&
+                  x.stride(1) == 28 * x.stride(2) && x.stride(0) == x.size(1) * x.stride(1) &&
+                  reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "aiko.conv3x3_patchw_out: x must be [B, H, 28, >= 128] NHWC with a 16-B aligned pixel pitch");
+  TORCH_CHECK(wimg.is_contiguous() && wimg.numel() == 9 * 128 * 128, "aiko.conv3x3_patchw_out: wimg must be the 147456-element image");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2);
+  TORCH_CHECK(y.dim() == 4 && y.size(0) == B && y.size(1) == H && y.size(2) == W && y.size(3) == 128 && y.stride(3) == 1 &&
+                  y.stride(2) % 8 == 0 && y.stride(1) == W * y.stride(2) && y.stride(0) == H * W * y.stride(2) &&
+                  reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0,
+              "aiko.conv3x3_patchw_out: y must be [B, H, 28, 128] NHWC (16-B aligned pixel pitch)");
+  TORCH_CHECK(avail_elems(x) * 2 < (1LL << 31) - 64 && avail_elems(y) * 2 < (1LL << 31) - 64,
+              "aiko.conv3x3_patchw_out: tensors too large for 32-bit offsets");
+  TORCH_CHECK(act == 0 || act == 1, "aiko.conv3x3_patchw_out: act none / relu");
+  const float* bptr = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    check_cuda(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == 128, "aiko.conv3x3_patchw_out: bias fp32 [128]");
+    bptr = bias->data_ptr<float>();
+  }
+  check_launch(aiko_conv3x3_patchw(x.data_ptr(), wimg.data_ptr(), bptr, y.data_ptr(), (int)B, (int)H, (int)W,
+                                   (int)x.stride(2), (int)y.stride(2), (int)act, (int)grid, cur_stream()),
+               "conv3x3_patchw");
 }
 
 // Chained 1x1 convs at a bottleneck boundary (conv_chain.hip):
@@ -1172,6 +1208,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("topk_nms_out(Tensor boxes, Tensor scores, Tensor cls, int max_cand, float[] params, Tensor(a!) det, Tensor(b!) count) -> ()");
   m.def("stem_direct_out(Tensor frames, Tensor w, Tensor? bias, Tensor(a!) out, int[] geom, float fill, float[] mean, float[] std, bool bgr) -> ()");
   m.def("conv3x3_patch_out(Tensor x, Tensor wimg, Tensor? bias, Tensor(a!) y, int act, int grid=0) -> ()");
+  m.def("conv3x3_patchw_out(Tensor x, Tensor wimg, Tensor? bias, Tensor(a!) y, int act, int grid=0) -> ()");
   m.def("conv_chain_out(Tensor A, Tensor W1, Tensor b1, Tensor? R, Tensor(a!) Y, Tensor W2, Tensor b2, Tensor(b!) Z, int grid=0, Tensor? A2=None) -> ()");
   m.def("bneck_fused_out(Tensor x, Tensor w1, Tensor b1, Tensor w2, Tensor b2, Tensor w3, Tensor b3, Tensor(a!) y, int grid=0, Tensor? dbg=None) -> ()");
   m.def("maxpool_out(Tensor x, Tensor(a!) y, int k, int s, int p) -> ()");
@@ -1201,6 +1238,7 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("conv_chain_out", &conv_chain_out);
   m.impl("bneck_fused_out", &bneck_fused_out);
   m.impl("conv3x3_patch_out", &conv3x3_patch_out);
+  m.impl("conv3x3_patchw_out", &conv3x3_patchw_out);
   m.impl("stem_direct_out", &stem_direct_out);
   m.impl("upsample2x_out", &upsample2x_out);
   m.impl("resize_u8_out", &resize_u8_out);

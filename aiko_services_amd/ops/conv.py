@@ -329,6 +329,37 @@ def patch_weight(spec: ConvSpec) -> torch.Tensor:
     return img
 
 
+def patchw_variant_ok(spec: ConvSpec, x: torch.Tensor, residual=None, x2=None, out=None) -> bool:
+    """Whether the streamed-weight patch 3x3 kernel (variant 16, conv_patchw.hip) applies: a 3x3 /
+    stride 1 / pad 1 conv 128 -> 128 channels on an NHWC [B, H, 28, >= 128] input (the ResNet
+    stage-2 shape), no residual, no second source, activation none / ReLU."""
+    return (spec.kind == "conv" and spec.R == 3 and spec.S == 3 and spec.stride == 1 and spec.pad == 1
+            and spec.Cc == 128 and spec.cout == 128 and spec.K == 1152 and spec.K1 is None
+            and residual is None and x2 is None and spec.act in (ACT_NONE, ACT_RELU)
+            and x.dim() == 4 and x.shape[2] == 28 and x.shape[3] >= 128 and x.stride(3) == 1
+            and x.stride(2) % 8 == 0 and (out is None or (out.stride(3) == 1 and out.stride(2) % 8 == 0)))
+
+
+def patchw_weight(spec: ConvSpec) -> torch.Tensor:
+    """[4, 9, 8, 64, 8] MFMA fragment image of a 3x3 128 -> 128 weight for conv_patchw.hip:
+    (32-channel chunk, tap, 16-output-channel block, lane = 16 (k group) + output row, 8
+    channels) — each (chunk, tap) block is the 8 KB the kernel streams per step.  Cached on the
+    spec and re-derived in place when the weight changes (as patch_weight)."""
+    key = (spec.weight.data_ptr(), spec.weight._version)
+    cached = getattr(spec, "_patchw_w", None)
+    if cached is not None and cached[0] == key:
+        return cached[1]
+    w = spec.weight.view(8, 16, 9, 4, 4, 8)                  # [nb, fr, tap, chunk, fq, e]
+    img = w.permute(3, 2, 0, 4, 1, 5).reshape(4, 9, 8, 64, 8)
+    if cached is not None:
+        cached[1].copy_(img)
+        img = cached[1]
+    else:
+        img = img.contiguous()
+    spec._patchw_w = (key, img)
+    return img
+
+
 def pw_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = None):
     """Whether the persistent pointwise kernels (conv_pw.hip) apply to a 1x1 / stride 1
     single-source conv with 16-byte aligned pixel rows: ``True`` for variant 12 only (K % 256 == 0,
@@ -358,7 +389,8 @@ def narrow_variant_ok(spec: ConvSpec, x2: torch.Tensor | None = None) -> bool:
             and spec.Cc in (16, 32) and spec.cout in (16, 32))
 
 
-def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, pw_ok=False, has_res=False):
+def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, pw_ok=False, has_res=False,
+          patchw_ok=False):
     if cout <= 32:
         cands = [t + (0,) for t in NARROW_TILES]
         if narrow_ok:
@@ -377,6 +409,8 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, p
             cands += [t + (11,) for t in WIDE_DEEP_TILES]
         if patch_ok:
             cands.append((8, 64, 10))        # variant 10: tile fixed by the kernel (8 rows x W)
+        if patchw_ok:
+            cands.append((392, 128, 16))     # variant 16: 14-row patch tiles, streamed weights
         if pw_ok and pw_ok not in ("resident_only", "dual"):
             cands.append((128, 128, 12))     # variant 12: persistent pointwise GEMM (conv_pw.hip)
         if pw_ok in ("resident", "resident_only") or (pw_ok == "dual" and not has_res and _PW_DUAL):
@@ -471,6 +505,11 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None
                 raise ValueError("conv2d: variant 10 needs a 3x3/s1/p1 64->64 conv on a contiguous W<=56 input")
             torch.ops.aiko.conv3x3_patch_out(x, patch_weight(spec), spec.bias, out, spec.act, 0)
             return
+        if v == 16:
+            if not patchw_variant_ok(spec, x, residual, x2, out):
+                raise ValueError("conv2d: variant 16 needs a 3x3/s1/p1 128->128 conv on a [B, H, 28, >=128] input")
+            torch.ops.aiko.conv3x3_patchw_out(x, patchw_weight(spec), spec.bias, out, spec.act, 0)
+            return
         torch.ops.aiko.conv_igemm_out(x, x2, spec.weight, spec.bias, residual, out,
                                       head + [t[0], t[1]] + src2 + [v], zero_page(x.device) if v == 1 else None)
 
@@ -481,7 +520,8 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None
             if _tuning:
                 tile = _tune(key, M, spec.cout, launch, buf_variant_ok(spec, x, x2), narrow_variant_ok(spec, x2),
                              patch_variant_ok(spec, x, residual, x2, out) and not residual_after_act,
-                             pw_variant_ok(spec, x, x2), residual is not None)
+                             pw_variant_ok(spec, x, x2), residual is not None,
+                             patchw_variant_ok(spec, x, residual, x2, out) and not residual_after_act)
             else:
                 tile = pick_tile(M, spec.cout)
     launch(tile)
