@@ -407,6 +407,7 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, p
             cands += [t + (6,) for t in WIDE4_TILES]
             cands += [t + (8,) for t in WIDE8_TILES] + [t + (9,) for t in WIDE_OCC_TILES]
             cands += [t + (11,) for t in WIDE_DEEP_TILES]
+
         if patch_ok:
             cands.append((8, 64, 10))        # variant 10: tile fixed by the kernel (8 rows x W)
         if patchw_ok:
@@ -420,6 +421,10 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, p
     skip = {int(v) for v in __import__("os").environ.get("AIKO_CONV_SKIP", "").split(",") if v.strip()}
     if skip:                                   # A/B runs: exclude variants from the tuner
         cands = [t for t in cands if (t[2] if len(t) > 2 else 0) not in skip] or cands
+    skip_t = {tuple(int(v) for v in e.split("x")) for e in __import__("os").environ.get("AIKO_CONV_SKIP_TILES", "").split(",")
+              if e.strip()}                    # exact tiles, e.g. AIKO_CONV_SKIP_TILES=256x192x8
+    if skip_t:
+        cands = [t for t in cands if tuple(t) not in skip_t] or cands
     # each candidate: 2 warm launches, then the median of 5 individually timed ones (a 3-launch
     # sum was noisy enough to rank a 56 us kernel behind an 80 us one on a fresh box)
     best, best_t = None, None
