@@ -761,7 +761,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_big_kernel(Fp8GemmParams p, c
 // scales (no MX input), no residual.
 template <bool MXO>
 __global__ __launch_bounds__(512, 1) void gemm_fp8_pers_kernel(Fp8GemmParams p, const uint8_t* zero, int tiles_n,
-                                                               int ntiles) {
+                                                               int ntiles, int diag) {
   constexpr int BM = 256, BN = 256, BK = 128, WGN = 4, WM = 128, WN = 64, MI = WM / 16, NI = WN / 16;
   constexpr int APT = BM / 64, BPT = BN / 64;
   constexpr int STAGE_BYTES = (BM + BN) * BK;  // 64 KB
@@ -793,6 +793,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers_kernel(Fp8GemmParams p, 
   auto issue = [&](int f) {                          // flat K block f of this workgroup's walk
     const int k = f / nkb, kb = f - k * nkb;
     if (k >= my_tiles) return;
+    if ((diag & 1) && f > 1) return;                 // timing diagnostic: MFMA + LDS on stale blocks
     const int tau = lid + k * G;
     const int m0 = (tau / tiles_n) * BM, n0 = (tau % tiles_n) * BN;
     unsigned char* As = smem + (f & 1) * STAGE_BYTES;
@@ -931,7 +932,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers_kernel(Fp8GemmParams p, 
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = pack2(v[2 * e], v[2 * e + 1]);
           const uint32_t yoff = live ? (uint32_t)(((long)m * p.ldy + n) * 2) : 0x80000000u;
-          __builtin_amdgcn_raw_buffer_store_b128(o, ry, yoff, 0, 0);
+          if (!(diag & 2)) __builtin_amdgcn_raw_buffer_store_b128(o, ry, yoff, 0, 0);
         }
       }
     }
@@ -1239,8 +1240,12 @@ extern "C" int aiko_gemm_fp8(const void* a, const void* b, const float* sa, cons
     }
     const int tiles_n = N / 256, ntiles = ((M + 255) / 256) * tiles_n;
     const dim3 pg((unsigned)(ntiles < cus ? ntiles : cus));
-    if (yq) gemm_fp8_pers_kernel<true><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles);
-    else gemm_fp8_pers_kernel<false><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles);
+    static const int diag = [] {                     // AIKO_FP8_DIAG: timing diagnostics only (1: no K-block DMAs
+      const char* e = getenv("AIKO_FP8_DIAG");       // after the first two, 2: no epilogue stores) — wrong results
+      return e ? atoi(e) : 0;
+    }();
+    if (yq) gemm_fp8_pers_kernel<true><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles, diag);
+    else gemm_fp8_pers_kernel<false><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles, diag);
     return (int)hipGetLastError();
   }
   if (variant == 3) {
