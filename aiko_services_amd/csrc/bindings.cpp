@@ -47,6 +47,8 @@ int aiko_stem_direct(const void* in, void* out, const void* w, const float* bias
                      int Ho, int Wo, int Hc, int Wc, int off_t, int off_l, float fill, const float* mean,
                      const float* std, int bgr, int H1, int W1, int Cout, int ldo, int k, int stride, int pad,
                      int act, hipStream_t stream);
+int aiko_conv3x3_rows(const void* x, const void* wimg, const float* bias, const void* res, void* y, int B, int H,
+                      int W, int ldx, int ldy, int ldr, int act, int grid, hipStream_t stream);
 int aiko_conv3x3_patchw(const void* x, const void* wimg, const float* bias, void* y, int B, int H, int W, int ldx,
                         int ldy, int act, int grid, hipStream_t stream);
 int aiko_conv3x3_patch(const void* x, const void* wimg, const float* bias, void* y, int B, int H, int W, int ldy,
@@ -392,6 +394,46 @@ void conv3x3_patchw_out(const at::Tensor& x, const at::Tensor& wimg, const c10::
   check_launch(aiko_conv3x3_patchw(x.data_ptr(), wimg.data_ptr(), bptr, y.data_ptr(), (int)B, (int)H, (int)W,
                                    (int)x.stride(2), (int)y.stride(2), (int)act, (int)grid, cur_stream()),
                "conv3x3_patchw");
+}
+
+// 3x3 / stride 1 / pad 1 conv, 32 -> 32 channels, W = 80, as a persistent row stream
+// (conv_rows.hip).  x / res / y: [B, H, 80, >= 32] NHWC views whose rows are uniformly strided
+// (channel slices of wider buffers are fine); wimg the [9, 2, 64, 8] fragment image
+// (ops.conv.rows_weight).  act bits 0-3: none / ReLU / SiLU, bit 4: residual after the activation.
+void conv3x3_rows_out(const at::Tensor& x, const at::Tensor& wimg, const c10::optional<at::Tensor>& bias,
+                      const c10::optional<at::Tensor>& res, at::Tensor& y, int64_t act, int64_t grid) {
+  check_cuda(x, "x");
+  check_cuda(wimg, "wimg");
+  check_cuda(y, "y");
+  auto rows_ok = [](const at::Tensor& t, int64_t B, int64_t H) {
+    return t.dim() == 4 && t.size(0) == B && t.size(1) == H && t.size(2) == 80 && t.size(3) >= 32 && t.stride(3) == 1 &&
+           t.stride(2) % 8 == 0 && t.stride(1) == 80 * t.stride(2) && t.stride(0) == H * t.stride(1) &&
+           reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0 && t.scalar_type() == at::kBFloat16 &&
+           avail_elems(t) * 2 < (1LL << 31) - 64;
+  };
+  const int64_t B = x.size(0), H = x.size(1);
+  TORCH_CHECK(rows_ok(x, B, H), "aiko.conv3x3_rows_out: x must be [B, H, 80, >= 32] bf16 with uniformly strided rows");
+  TORCH_CHECK(rows_ok(y, B, H) && y.size(3) == 32, "aiko.conv3x3_rows_out: y must be [B, H, 80, 32] bf16 (a slice is fine)");
+  TORCH_CHECK(wimg.is_contiguous() && wimg.numel() == 9 * 32 * 32 && wimg.scalar_type() == at::kBFloat16,
+              "aiko.conv3x3_rows_out: wimg must be the 9216-element bf16 image");
+  const void* rptr = nullptr;
+  int64_t ldr = 0;
+  if (res.has_value() && res->defined()) {
+    check_cuda(*res, "res");
+    TORCH_CHECK(rows_ok(*res, B, H), "aiko.conv3x3_rows_out: res must be [B, H, 80, >= 32] bf16 with uniformly strided rows");
+    rptr = res->data_ptr();
+    ldr = res->stride(2);
+  }
+  TORCH_CHECK((act & 15) <= 2 && (act & ~31) == 0, "aiko.conv3x3_rows_out: act none / relu / silu (+16: residual after)");
+  const float* bptr = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    check_cuda(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == 32, "aiko.conv3x3_rows_out: bias fp32 [32]");
+    bptr = bias->data_ptr<float>();
+  }
+  check_launch(aiko_conv3x3_rows(x.data_ptr(), wimg.data_ptr(), bptr, rptr, y.data_ptr(), (int)B, (int)H, 80,
+                                 (int)x.stride(2), (int)y.stride(2), (int)ldr, (int)act, (int)grid, cur_stream()),
+               "conv3x3_rows");
 }
 
 // Chained 1x1 convs at a bottleneck boundary (conv_chain.hip):
@@ -1209,6 +1251,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("stem_direct_out(Tensor frames, Tensor w, Tensor? bias, Tensor(a!) out, int[] geom, float fill, float[] mean, float[] std, bool bgr) -> ()");
   m.def("conv3x3_patch_out(Tensor x, Tensor wimg, Tensor? bias, Tensor(a!) y, int act, int grid=0) -> ()");
   m.def("conv3x3_patchw_out(Tensor x, Tensor wimg, Tensor? bias, Tensor(a!) y, int act, int grid=0) -> ()");
+  m.def("conv3x3_rows_out(Tensor x, Tensor wimg, Tensor? bias, Tensor? res, Tensor(a!) y, int act, int grid=0) -> ()");
   m.def("conv_chain_out(Tensor A, Tensor W1, Tensor b1, Tensor? R, Tensor(a!) Y, Tensor W2, Tensor b2, Tensor(b!) Z, int grid=0, Tensor? A2=None) -> ()");
   m.def("bneck_fused_out(Tensor x, Tensor w1, Tensor b1, Tensor w2, Tensor b2, Tensor w3, Tensor b3, Tensor(a!) y, int grid=0, Tensor? dbg=None) -> ()");
   m.def("maxpool_out(Tensor x, Tensor(a!) y, int k, int s, int p) -> ()");
@@ -1239,6 +1282,7 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("bneck_fused_out", &bneck_fused_out);
   m.impl("conv3x3_patch_out", &conv3x3_patch_out);
   m.impl("conv3x3_patchw_out", &conv3x3_patchw_out);
+  m.impl("conv3x3_rows_out", &conv3x3_rows_out);
   m.impl("stem_direct_out", &stem_direct_out);
   m.impl("upsample2x_out", &upsample2x_out);
   m.impl("resize_u8_out", &resize_u8_out);

@@ -360,6 +360,44 @@ def patchw_weight(spec: ConvSpec) -> torch.Tensor:
     return img
 
 
+def _rows_strided(t: torch.Tensor | None, B: int, H: int) -> bool:
+    return (t is not None and t.dim() == 4 and t.shape[0] == B and t.shape[1] == H and t.shape[2] == 80
+            and t.stride(3) == 1 and t.stride(2) % 8 == 0 and t.stride(1) == 80 * t.stride(2)
+            and t.stride(0) == H * t.stride(1))
+
+
+def rows_variant_ok(spec: ConvSpec, x: torch.Tensor, residual=None, x2=None, out=None) -> bool:
+    """Whether the row-stream kernel (variant 17, conv_rows.hip) applies: a 3x3 / stride 1 / pad 1
+    conv 32 -> 32 channels on 80-wide NHWC views with uniformly strided rows (YOLOv8-n's C2f
+    bottleneck convs at the P3 level), activation none / ReLU / SiLU, optional residual."""
+    if not (spec.kind == "conv" and spec.R == 3 and spec.S == 3 and spec.stride == 1 and spec.pad == 1
+            and spec.Cc == 32 and spec.cout == 32 and spec.K1 is None and x2 is None
+            and spec.act in (ACT_NONE, ACT_RELU, ACT_SILU) and x.dim() == 4):
+        return False
+    B, H = x.shape[0], x.shape[1]
+    return (_rows_strided(x, B, H) and (residual is None or _rows_strided(residual, B, H))
+            and (out is None or _rows_strided(out, B, H)))
+
+
+def rows_weight(spec: ConvSpec) -> torch.Tensor:
+    """[9, 2, 64, 8] MFMA fragment image of a 3x3 32 -> 32 weight for conv_rows.hip: (tap,
+    16-output-channel block, lane = 16 (k group) + output row, 8 channels).  Cached on the spec
+    (re-derived in place when the weight changes)."""
+    key = (spec.weight.data_ptr(), spec.weight._version)
+    cached = getattr(spec, "_rows_w", None)
+    if cached is not None and cached[0] == key:
+        return cached[1]
+    w = spec.weight[:, :288].reshape(2, 16, 9, 4, 8)      # [j, fr, tap, fq, e]
+    img = w.permute(2, 0, 3, 1, 4).reshape(9, 2, 64, 8)
+    if cached is not None:
+        cached[1].copy_(img)
+        img = cached[1]
+    else:
+        img = img.contiguous()
+    spec._rows_w = (key, img)
+    return img
+
+
 def pw_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = None):
     """Whether the persistent pointwise kernels (conv_pw.hip) apply to a 1x1 / stride 1
     single-source conv with 16-byte aligned pixel rows: ``True`` for variant 12 only (K % 256 == 0,
@@ -390,7 +428,7 @@ def narrow_variant_ok(spec: ConvSpec, x2: torch.Tensor | None = None) -> bool:
 
 
 def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, pw_ok=False, has_res=False,
-          patchw_ok=False):
+          patchw_ok=False, rows_ok=False):
     if cout <= 32:
         cands = [t + (0,) for t in NARROW_TILES]
         if narrow_ok:
@@ -398,6 +436,8 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, p
             cands.append((16, 32, 7))        #            16 x 32
             cands.append((8, 64, 7))         # bn = 64: Cc-32 weights held in registers, not LDS
             cands.append((16, 64, 7))
+        if rows_ok:
+            cands.append((1, 32, 17))        # variant 17: persistent row stream (80-wide 32 -> 32 3x3)
     else:
         cands = [t + (0,) for t in TILES] + [t + (1,) for t in TILES]
         if buf_ok:
@@ -510,6 +550,11 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None
                 raise ValueError("conv2d: variant 10 needs a 3x3/s1/p1 64->64 conv on a contiguous W<=56 input")
             torch.ops.aiko.conv3x3_patch_out(x, patch_weight(spec), spec.bias, out, spec.act, 0)
             return
+        if v == 17:
+            if not rows_variant_ok(spec, x, residual, x2, out):
+                raise ValueError("conv2d: variant 17 needs a 3x3/s1/p1 32->32 conv on 80-wide row-strided views")
+            torch.ops.aiko.conv3x3_rows_out(x, rows_weight(spec), spec.bias, residual, out, act, 0)
+            return
         if v == 16:
             if not patchw_variant_ok(spec, x, residual, x2, out):
                 raise ValueError("conv2d: variant 16 needs a 3x3/s1/p1 128->128 conv on a [B, H, 28, >=128] input")
@@ -526,7 +571,8 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, residual: torch.Tensor | None = None
                 tile = _tune(key, M, spec.cout, launch, buf_variant_ok(spec, x, x2), narrow_variant_ok(spec, x2),
                              patch_variant_ok(spec, x, residual, x2, out) and not residual_after_act,
                              pw_variant_ok(spec, x, x2), residual is not None,
-                             patchw_variant_ok(spec, x, residual, x2, out) and not residual_after_act)
+                             patchw_variant_ok(spec, x, residual, x2, out) and not residual_after_act,
+                             rows_variant_ok(spec, x, residual, x2, out))
             else:
                 tile = pick_tile(M, spec.cout)
     launch(tile)

@@ -171,6 +171,48 @@ def test_conv_igemm_matches_torch(native, B, H, W, cin, cout, k, stride, pad, ac
     assert err < 1e-2, err
 
 
+@pytest.mark.parametrize("B,H,act,res,slices,grid", [
+    (2, 80, "silu", None, False, 0), (3, 80, "silu", "after", True, 0), (1, 7, "relu", "before", False, 0),
+    (4, 3, "silu", None, True, 5), (2, 1, None, "after", False, 1), (64, 80, "silu", "after", True, 0),
+    (5, 80, "silu", None, False, 7)])
+def test_conv3x3_rows_matches_torch(native, B, H, act, res, slices, grid):
+    """Variant 17 (row-stream kernel, conv_rows.hip): 80-wide 32 -> 32 3x3 convs, row ranges that
+    cross image boundaries (H = 7 / 3 / 1, grids of 1 / 5 / 7 workgroups), residual before / after
+    the activation, channel-slice input, residual and output (the C2f layout)."""
+    from aiko_services_amd.ops import conv as C
+    from aiko_services_amd.ops import reference as R
+    g = torch.Generator().manual_seed(B * 31 + H)
+    w = torch.randn(32, 32, 3, 3, generator=g) / (32 * 9) ** 0.5
+    b = torch.randn(32, generator=g) * 0.1
+    spec = C.make_conv_spec(w, b, stride=1, pad=1, act=act, device=DEV)
+    x = torch.randn(B, 32, H, 80, generator=g).to(torch.bfloat16)
+    r = torch.randn(B, 32, H, 80, generator=g).to(torch.bfloat16) if res else None
+    if slices:
+        cat = torch.zeros(B, H, 80, 96, dtype=torch.bfloat16)
+        cat[..., 32:64] = _nhwc(x)
+        if r is not None:
+            cat[..., 64:96] = _nhwc(r)
+        cat = cat.to(DEV)
+        xin, rin = cat[..., 32:64], (cat[..., 64:96] if r is not None else None)
+        ybig = torch.full((B, H, 80, 128), float("nan"), dtype=torch.bfloat16, device=DEV)
+        out = ybig[..., 96:128]
+    else:
+        xin = _nhwc(x).to(DEV)
+        rin = _nhwc(r).to(DEV) if r is not None else None
+        out = torch.full((B, H, 80, 32), float("nan"), dtype=torch.bfloat16, device=DEV)
+    assert C.rows_variant_ok(spec, xin, rin, None, out)
+    act_code = spec.act | (C.ACT_RESIDUAL_AFTER if res == "after" else 0)
+    torch.ops.aiko.conv3x3_rows_out(xin, C.rows_weight(spec), spec.bias, rin, out, act_code, grid)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out.float()).all(), "unwritten output pixels"
+    ref = R.conv_ref(x.float().to(DEV), spec, None if (r is None or res == "after") else r.float().to(DEV))
+    if res == "after":
+        ref = ref + r.float().to(DEV)
+    assert _rel_err(out.permute(0, 3, 1, 2), ref) < 1e-2
+    if slices:
+        assert torch.isnan(ybig[..., :96].float()).all()
+
+
 @pytest.mark.parametrize("B,H,act,slices,grid", [(2, 28, "relu", False, 0), (3, 28, None, False, 0),
                                                  (1, 30, "relu", False, 0), (2, 5, "relu", True, 0),
                                                  (5, 28, "relu", True, 3), (33, 28, "relu", False, 0),
