@@ -35,7 +35,6 @@ constexpr int HALF_BYTES = (TH + 2) * PWMAX * 64;         // 40 KB per half-patc
 constexpr int W_BYTES = 9 * 2 * 4 * 1024;                 // weight image: 72 KB
 constexpr int P_DMA = HALF_BYTES / 1024 / 8;              // DMA instructions per wave per half (5)
 constexpr int W_DMA = W_BYTES / 1024 / 8;                 // 9
-constexpr int MI = 7;                                     // 16-pixel blocks per wave (4 x 7 x 16 = 448)
 constexpr uint32_t kOOB = 0x80000000u;
 constexpr uint32_t kRecords = 0x7ffffff0u;
 
@@ -55,6 +54,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_patch_kernel(
     bf16_t* __restrict__ y, int B, int H, int ldy, int act) {
   using namespace patch;
   constexpr int PW = W + 8;
+  constexpr int MIW = (TH * W + 63) / 64;                  // 16-pixel blocks per wave (W 56: 7, 40: 5, 24: 3)
   static_assert(PW % 8 == 0 && PW <= PWMAX, "patch pitch");
   // LDS: [half-patch 0 | half-patch 1 | weights]: patch reads take immediate offsets < 64 KB
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * HALF_BYTES + W_BYTES];
@@ -97,11 +97,11 @@ __global__ __launch_bounds__(512, 2) void conv3x3_patch_kernel(
   // ---- per-lane output pixels: block i of group wr -> p = (7 wr + i) 16 + fr (a pixel past the
   // tile reads patch pixel 0 and its store is dropped).  addr[i][s]: LDS byte address of the
   // pixel's tap-(0, s) input chunk; tap (r, s) adds the immediate r PW 64.
-  int addr[MI][3];
-  int prel[MI];
+  int addr[MIW][3];
+  int prel[MIW];
 #pragma unroll
-  for (int i = 0; i < MI; ++i) {
-    const int p = (MI * wr + i) * 16 + fr;
+  for (int i = 0; i < MIW; ++i) {
+    const int p = (MIW * wr + i) * 16 + fr;
     const bool valid = p < TH * W;
     const int ohl = p / W, ow = p - ohl * W;
     const int q0 = valid ? ohl * PW + ow : 0;
@@ -125,16 +125,16 @@ __global__ __launch_bounds__(512, 2) void conv3x3_patch_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   for (; tile < ntiles; tile += gridDim.x) {
-    f32x4 acc[2][MI];
+    f32x4 acc[2][MIW];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int i = 0; i < MI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < MIW; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      // h = 0: this half's DMAs are older than the previous tile's MI stores; h = 1: nothing younger
+      // h = 0: this half's DMAs are older than the previous tile's MIW stores; h = 1: nothing younger
       if (h == 0)
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(MI) : "memory");
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(MIW) : "memory");
       else
         asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if (h == 0) {
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_patch_kernel(
           const bf16x8 wf0 = *reinterpret_cast<const bf16x8*>(wp);
           const bf16x8 wf1 = *reinterpret_cast<const bf16x8*>(wp + 1024);
 #pragma unroll
-          for (int i = 0; i < MI; ++i) {
+          for (int i = 0; i < MIW; ++i) {
             const bf16x8 xf = *reinterpret_cast<const bf16x8*>(P + addr[i][s] + r * PW * 64);
             acc[0][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf0, xf, acc[0][i], 0, 0, 0);
             acc[1][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1, xf, acc[1][i], 0, 0, 0);
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_patch_kernel(
     const int pix0 = (img * H + oh0) * W;
     const int valid_px = min(TH, H - oh0) * W;
 #pragma unroll
-    for (int i = 0; i < MI; ++i) {
+    for (int i = 0; i < MIW; ++i) {
       f32x4 lo = acc[0][i], hi = acc[1][i];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_patch_kernel(
 }  // namespace aiko
 
 // x: [B, H, W, 64] bf16 contiguous; wimg: [9][2][4][64][8] bf16 fragment image (ops.conv.patch_weight);
-// y: [B, H, W, >= 64] with pixel pitch ldy.  W in {56, 24} (compile-time patch pitch); every byte
+// y: [B, H, W, >= 64] with pixel pitch ldy.  W in {56, 40, 24} (compile-time patch pitch); every byte
 // offset < 2^31.
 extern "C" int aiko_conv3x3_patch(const void* x, const void* wimg, const float* bias, void* y, int B, int H,
                                   int W, int ldy, int act, int grid, hipStream_t stream) {
@@ -210,6 +210,8 @@ extern "C" int aiko_conv3x3_patch(const void* x, const void* wimg, const float* 
   auto yp = static_cast<bf16_t*>(y);
   if (W == 56)
     hipLaunchKernelGGL(conv3x3_patch_kernel<56>, dim3(grid), dim3(512), 0, stream, xp, wp, bias, yp, B, H, ldy, act);
+  else if (W == 40)
+    hipLaunchKernelGGL(conv3x3_patch_kernel<40>, dim3(grid), dim3(512), 0, stream, xp, wp, bias, yp, B, H, ldy, act);
   else if (W == 24)
     hipLaunchKernelGGL(conv3x3_patch_kernel<24>, dim3(grid), dim3(512), 0, stream, xp, wp, bias, yp, B, H, ldy, act);
   else

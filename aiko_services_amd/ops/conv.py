@@ -300,13 +300,13 @@ def buf_variant_ok(spec: ConvSpec, x: torch.Tensor, x2: torch.Tensor | None = No
 
 def patch_variant_ok(spec: ConvSpec, x: torch.Tensor, residual=None, x2=None, out=None) -> bool:
     """Whether the LDS-resident-patch 3x3 kernel (variant 10, conv_patch.hip) applies: a 3x3 /
-    stride 1 / pad 1 conv 64 -> 64 channels on a contiguous [B, H, W, 64] input (W = 56 or 24:
+    stride 1 / pad 1 conv 64 -> 64 channels on a contiguous [B, H, W, 64] input (W = 56, 40 or 24:
     the kernel's patch pitch is a compile-time constant), no residual,
     no second source, activation none / ReLU / SiLU."""
     return (spec.kind == "conv" and spec.R == 3 and spec.S == 3 and spec.stride == 1 and spec.pad == 1
             and spec.Cc == 64 and spec.cout == 64 and spec.K == 576 and spec.K1 is None
             and residual is None and x2 is None and spec.act in (ACT_NONE, ACT_RELU, ACT_SILU)
-            and x.dim() == 4 and x.shape[3] == 64 and x.is_contiguous() and x.shape[2] in (56, 24)
+            and x.dim() == 4 and x.shape[3] == 64 and x.is_contiguous() and x.shape[2] in (56, 40, 24)
             and (out is None or (out.stride(3) == 1 and out.stride(2) % 8 == 0)))
 
 

@@ -251,7 +251,8 @@ def test_conv3x3_patchw_matches_torch(native, B, H, act, slices, grid):
     assert _rel_err(y.permute(0, 3, 1, 2), ref) < 1e-2
 
 
-@pytest.mark.parametrize("B,H,W,act", [(2, 56, 56, "relu"), (3, 13, 24, "silu"), (1, 30, 24, None),
+@pytest.mark.parametrize("B,H,W,act", [(2, 56, 56, "relu"), (3, 13, 24, "silu"), (1, 30, 24, None), (3, 40, 40, "silu"),
+                                          (2, 13, 40, "relu"),
                                           (2, 17, 56, "relu"), (1, 8, 56, "relu"), (3, 1, 24, "relu")])
 def test_conv3x3_patch_matches_torch(native, B, H, W, act):
     """Variant 10 (LDS-resident input patch, conv_patch.hip): partial row tiles, narrow images,
