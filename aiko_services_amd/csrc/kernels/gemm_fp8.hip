@@ -827,7 +827,8 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers_kernel(Fp8GemmParams p, 
       for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int kb = 0; kb < nkb; ++kb) {
       const int f = k * nkb + kb;
-      if (kb == 0 && k > 0) fp8_wait_vm_barrier<NST>();   // younger: the previous tile's stores
+      if (diag & 4) asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");   // diag: no barrier
+      else if (kb == 0 && k > 0) fp8_wait_vm_barrier<NST>();   // younger: the previous tile's stores
       else fp8_wait_vm_barrier<0>();
       if (kb == 0) {                                 // row scales, older than the next block's DMA
 #pragma unroll
@@ -839,23 +840,34 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers_kernel(Fp8GemmParams p, 
       issue(f + 1);
       const unsigned char* As = smem + (f & 1) * STAGE_BYTES + (wr * WM + fr) * BK;
       const unsigned char* Bs = smem + (f & 1) * STAGE_BYTES + BM * BK + (wc * WN + fr) * BK;
+      auto frag = [&](const unsigned char* base) {
+        const u32x4 lo = *reinterpret_cast<const u32x4*>(base + off_lo);
+        const u32x4 hi = *reinterpret_cast<const u32x4*>(base + off_hi);
+        return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+      };
+      // software-pipelined fragment reads: A fragment i + 1 is read while the MFMAs on fragment
+      // i run, so only the weight fragments and A0 are exposed after the barrier, and 2 A
+      // fragments (not MI) are live.  The sched_group_barriers pin that order: left alone the
+      // scheduler hoists all 24 reads above the first MFMA and waits on lgkmcnt(0).
       i32x8 bfr[NI];
 #pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        const u32x4 lo = *reinterpret_cast<const u32x4*>(Bs + j * 16 * BK + off_lo);
-        const u32x4 hi = *reinterpret_cast<const u32x4*>(Bs + j * 16 * BK + off_hi);
-        bfr[j] = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
-      }
+      for (int j = 0; j < NI; ++j) bfr[j] = frag(Bs + j * 16 * BK);
+      i32x8 acur = frag(As);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * NI + 2, 0);
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
-        const u32x4 lo = *reinterpret_cast<const u32x4*>(As + i * 16 * BK + off_lo);
-        const u32x4 hi = *reinterpret_cast<const u32x4*>(As + i * 16 * BK + off_hi);
-        const i32x8 af = i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+        i32x8 anxt = acur;
+        if (i + 1 < MI) {
+          anxt = frag(As + (i + 1) * 16 * BK);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        }
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int j = 0; j < NI; ++j)   // transposed: weights first, so lanes end with 4 consecutive columns
-          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], af, acc[i][j], 0, 0, 0, 127, 0, 127);
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], acur, acc[i][j], 0, 0, 0, 127, 0, 127);
+        __builtin_amdgcn_sched_group_barrier(0x008, NI, 0);
         __builtin_amdgcn_s_setprio(0);
+        acur = anxt;
       }
     }
     // ---- register-direct epilogue (the ring is not touched: no barrier) ----
@@ -1241,8 +1253,8 @@ extern "C" int aiko_gemm_fp8(const void* a, const void* b, const float* sa, cons
     const int tiles_n = N / 256, ntiles = ((M + 255) / 256) * tiles_n;
     const dim3 pg((unsigned)(ntiles < cus ? ntiles : cus));
     static const int diag = [] {                     // AIKO_FP8_DIAG: timing diagnostics only (1: no K-block DMAs
-      const char* e = getenv("AIKO_FP8_DIAG");       // after the first two, 2: no epilogue stores) — wrong results
-      return e ? atoi(e) : 0;
+      const char* e = getenv("AIKO_FP8_DIAG");       // after the first two, 2: no epilogue stores, 4: no barrier)
+      return e ? atoi(e) : 0;                        // — wrong results by design
     }();
     if (yq) gemm_fp8_pers_kernel<true><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles, diag);
     else gemm_fp8_pers_kernel<false><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles, diag);
