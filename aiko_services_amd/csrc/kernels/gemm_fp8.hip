@@ -358,6 +358,42 @@ __device__ __forceinline__ void fp8_wait_vm_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
+template <int I, int N, typename F>
+__device__ __forceinline__ void fp8_static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    fp8_static_for<I + 1, N>(f);
+  }
+}
+
+// LDS fragment reads the compiler does not see: their completion is waited for by hand with a
+// counted lgkmcnt (fp8_lgkm_tie), which names the fragments as in/out operands so no use of them
+// can be scheduled above the wait.  (The compiler's own waits on these reads were lgkmcnt(0)
+// every other MFMA group, draining the read-ahead.)
+template <int OFF>
+__device__ __forceinline__ u32x4 fp8_lds_rd128(uint32_t addr) {
+  u32x4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF) : "memory");
+  return v;
+}
+template <int N>
+__device__ __forceinline__ void fp8_lgkm_tie(u32x4& a, u32x4& b) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void fp8_lgkm_tie(u32x4 (&l)[4], u32x4 (&h)[4], u32x4& a, u32x4& b) {
+  asm volatile("s_waitcnt lgkmcnt(%10)"
+               : "+v"(l[0]), "+v"(l[1]), "+v"(l[2]), "+v"(l[3]), "+v"(h[0]), "+v"(h[1]), "+v"(h[2]), "+v"(h[3]),
+                 "+v"(a), "+v"(b)
+               : "n"(N) : "memory");
+}
+__device__ __forceinline__ void fp8_pin(const f32x4 (&a)[4]) {
+  asm volatile("" ::"v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]));
+}
+__device__ __forceinline__ i32x8 fp8_frag(const u32x4& lo, const u32x4& hi) {
+  return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+}
+
 template <int BM, int BN, bool MXA = false, bool MXO = false>
 __global__ __launch_bounds__(256, 2) void gemm_fp8_glds_kernel(Fp8GemmParams p, const uint8_t* zero) {
   constexpr int BK = 128;
@@ -871,6 +907,10 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers_kernel(Fp8GemmParams p, 
       }
     }
     // ---- register-direct epilogue (the ring is not touched: no barrier) ----
+    if (diag & 8) {                                  // timing diagnostic: no epilogue at all
+      if (acc[0][0][0] == 12345.f) __builtin_amdgcn_s_sleep(1);   // keeps the MFMAs live
+      continue;
+    }
 #pragma unroll
     for (int pp = 0; pp < NI / 2; ++pp) {
       const int nb = n0 + wc * WN + pp * 32;         // first column of this fragment pair
@@ -947,6 +987,244 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers_kernel(Fp8GemmParams p, 
           if (!(diag & 2)) __builtin_amdgcn_raw_buffer_store_b128(o, ry, yoff, 0, 0);
         }
       }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Epilogue of one 16-row fragment group of the persistent kernels' 128 x 64 wave tile: both
+// 32-column fragment pairs (lane l: row l & 15, eight consecutive columns after the permlane
+// swap), per-channel scale + bias from LDS, activation, bf16 or MX-fp8 store.
+template <bool MXO, int ACT>
+__device__ __forceinline__ void fp8_pers_epi(const Fp8GemmParams& p, const f32x4 (&acc)[4], float rs, int m, int nw,
+                                             int coff, int fg, const float* s_sb, const float* s_bias,
+                                             __amdgpu_buffer_rsrc_t ry, __amdgpu_buffer_rsrc_t rsc) {
+#pragma unroll
+  for (int pp = 0; pp < 2; ++pp) {
+    const int nb = nw + pp * 32, n = nb + coff;
+    const f32x4 sc0 = *reinterpret_cast<const f32x4*>(s_sb + n);
+    const f32x4 sc1 = *reinterpret_cast<const f32x4*>(s_sb + n + 4);
+    const f32x4 bi0 = *reinterpret_cast<const f32x4*>(s_bias + n);
+    const f32x4 bi1 = *reinterpret_cast<const f32x4*>(s_bias + n + 4);
+    f32x4 lo = acc[2 * pp], hi = acc[2 * pp + 1];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(lo[e]), __float_as_uint(hi[e]), false, false);
+      lo[e] = __uint_as_float(sw[0]);
+      hi[e] = __uint_as_float(sw[1]);
+    }
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = lo[e] * rs * sc0[e] + bi0[e];
+      v[e + 4] = hi[e] * rs * sc1[e] + bi1[e];
+    }
+    if constexpr (ACT == 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    } else if constexpr (ACT == 2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = silu(v[e]);
+    } else if constexpr (ACT == 3) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const f32x2 g = gelu_erf2(f32x2{v[2 * e], v[2 * e + 1]});
+        v[2 * e] = g[0];
+        v[2 * e + 1] = g[1];
+      }
+    }
+    const bool live = m < p.M;
+    if constexpr (MXO) {
+      float amax = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[e]));
+      {
+        const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(amax), __float_as_uint(amax), false, false);
+        amax = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+      }
+      {
+        const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(amax), __float_as_uint(amax), false, false);
+        amax = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+      }
+      const int ex = mx_exponent(amax);
+      const float inv = __uint_as_float((uint32_t)(127 - ex) << 23);
+      unsigned w0 = 0u, w1 = 0u;
+      w0 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[0] * inv, -448.f), 448.f),
+                                           fminf(fmaxf(v[1] * inv, -448.f), 448.f), w0, false);
+      w0 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[2] * inv, -448.f), 448.f),
+                                           fminf(fmaxf(v[3] * inv, -448.f), 448.f), w0, true);
+      w1 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[4] * inv, -448.f), 448.f),
+                                           fminf(fmaxf(v[5] * inv, -448.f), 448.f), w1, false);
+      w1 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[6] * inv, -448.f), 448.f),
+                                           fminf(fmaxf(v[7] * inv, -448.f), 448.f), w1, true);
+      typedef __attribute__((ext_vector_type(2))) unsigned u32x2v;
+      const uint32_t qoff = live ? (uint32_t)((long)m * p.ldq + n) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2v{w0, w1}, ry, qoff, 0, 0);
+      const uint32_t soff = live && fg == 0 ? (uint32_t)(((long)(nb >> 7) * p.ysr + m) * 4 + ((nb >> 5) & 3))
+                                            : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(ex + 127), rsc, soff, 0, 0);
+    } else {
+      u32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = pack2(v[2 * e], v[2 * e + 1]);
+      const uint32_t yoff = live ? (uint32_t)(((long)m * p.ldy + n) * 2) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b128(o, ry, yoff, 0, 0);
+    }
+  }
+}
+
+// Persistent 256 x 256 fp8 GEMM, epilogue overlapped with MFMA work (tuner variant 4 with
+// AIKO_FP8_OVERLAP=1; otherwise gemm_fp8_pers_kernel above).  Same walk, ring and store layout, two
+// changes in the schedule:
+//   - the epilogue of tile k runs interleaved with the first K block of tile k + 1: fragment
+//     group i is stored, then its accumulators take the next tile's group-i MFMAs (started from
+//     zero), so the epilogue's VALU and store issue overlap the matrix pipe instead of leaving it
+//     idle for ~20 % of the kernel (AIKO_FP8_DIAG=8 on the kernel above: 36.8 -> 29.9 us, qkv);
+//   - the fragment reads are issued by hand (fp8_lds_rd128) with counted lgkmcnt waits, A
+//     fragment i + LA in flight while the MFMAs on fragment i run.
+// vmcnt: block (k, 1)'s DMA is issued right after the fused block's barrier, before that
+// block's stores, so its wait is vmcnt(NST); every other wait is vmcnt(0).
+template <bool MXO, int ACT>
+__global__ __launch_bounds__(512, 1) void gemm_fp8_pers2_kernel(Fp8GemmParams p, const uint8_t* zero, int tiles_n,
+                                                                int ntiles, int diag) {
+  constexpr int BM = 256, BN = 256, BK = 128, WGN = 4, WM = 128, WN = 64, MI = WM / 16, NI = WN / 16;
+  constexpr int APT = BM / 64, BPT = BN / 64;
+  constexpr int STAGE_BYTES = (BM + BN) * BK;  // 64 KB
+  constexpr int MAXN = 3072;
+  constexpr int NST = MXO ? 2 * MI * (NI / 2) : MI * (NI / 2);   // store instructions per tile per wave
+  constexpr int LA = MXO && ACT == 3 ? 1 : 2;        // A fragments read ahead (1: GELU + MX registers)
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE_BYTES + 2 * MAXN * 4];
+  float* const s_sb = reinterpret_cast<float*>(smem + 2 * STAGE_BYTES);
+  float* const s_bias = s_sb + MAXN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WGN, wc = wave % WGN;
+  const int G = gridDim.x;
+  const int lid = xcd_remap(blockIdx.x, G);
+  if (lid >= ntiles) return;
+  const int my_tiles = (ntiles - 1 - lid) / G + 1;
+  const int nkb = p.K / BK;
+  const int lrow = wave * 8 + (lane >> 3);
+  const int lp = (lane & 7) ^ (lane >> 3);
+  const int fr = lane & 15, fg = lane >> 4;
+  const int coff = ((fg & 1) << 4) | ((fg >> 1) << 3);
+
+  for (int n = tid; n < p.N; n += 512) {
+    s_sb[n] = p.sb[n];
+    s_bias[n] = p.bias ? p.bias[n] : 0.f;
+  }
+
+  auto issue = [&](int f) {                          // flat K block f of this workgroup's walk
+    const int k = f / nkb, kb = f - k * nkb;
+    if (k >= my_tiles) return;
+    if ((diag & 1) && f > 1) return;                 // timing diagnostic: MFMA + LDS on stale blocks
+    const int tau = lid + k * G;
+    const int m0 = (tau / tiles_n) * BM, n0 = (tau % tiles_n) * BN;
+    unsigned char* As = smem + (f & 1) * STAGE_BYTES;
+    unsigned char* Bs = As + BM * BK;
+    const int k0 = kb * BK;
+#pragma unroll
+    for (int i = 0; i < APT; ++i) {
+      const int m = m0 + lrow + 64 * i;
+      glds16_u8(m < p.M ? p.a + (long)m * p.lda + lp * 16 + k0 : zero, As + (i * 64 + wave * 8) * BK);
+    }
+#pragma unroll
+    for (int i = 0; i < BPT; ++i)
+      glds16_u8(p.b + (long)(n0 + lrow + 64 * i) * p.K + lp * 16 + k0, Bs + (i * 64 + wave * 8) * BK);
+  };
+  // per-row A scales of tile k, loaded one K block before they are used: branch-free buffer
+  // loads (rows past M read out of range -> 0); no per-row scales -> 1, applied at the use
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)p.sa, (short)0,
+                                                                       p.sa ? p.M * 4 : 0, 0x00020000);
+  auto load_rs = [&](int k, float (&r)[MI]) {
+    const int m0 = ((lid + k * G) / tiles_n) * BM;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+      r[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsa, (m0 + wr * WM + i * 16 + fr) * 4, 0, 0));
+  };
+
+  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(MXO ? (void*)p.yq : (void*)p.y, (short)0,
+                                                                      0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc(MXO ? (void*)p.ysc : (void*)p.y, (short)0,
+                                                                       0x7ffffff0, 0x00020000);
+  const int off_lo = (fg ^ (fr & 7)) << 4, off_hi = ((fg + 4) ^ (fr & 7)) << 4;
+
+  f32x4 acc[MI][NI];
+  // MFMAs of flat K block f; Z: start from zero; pre(i) runs before fragment group i's MFMAs
+  auto kblock = [&](int f, auto ztag, auto&& pre) {
+    constexpr bool Z = decltype(ztag)::value;
+    const uint32_t la = (uint32_t)reinterpret_cast<uintptr_t>(smem + (f & 1) * STAGE_BYTES + (wr * WM + fr) * BK);
+    const uint32_t lb = la + (uint32_t)(BM * BK + (wc * WN - wr * WM) * BK);
+    const uint32_t alo = la + off_lo, ahi = la + off_hi, blo = lb + off_lo, bhi = lb + off_hi;
+    u32x4 bl[NI], bh[NI], al[MI], ah[MI];
+    fp8_static_for<0, NI>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      bl[j] = fp8_lds_rd128<j * 16 * BK>(blo);
+      bh[j] = fp8_lds_rd128<j * 16 * BK>(bhi);
+    });
+    fp8_static_for<0, LA>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      al[i] = fp8_lds_rd128<i * 16 * BK>(alo);
+      ah[i] = fp8_lds_rd128<i * 16 * BK>(ahi);
+    });
+    fp8_static_for<0, MI>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      constexpr int last = i + LA < MI ? i + LA : MI - 1;
+      if constexpr (i + LA < MI) {
+        al[i + LA] = fp8_lds_rd128<(i + LA) * 16 * BK>(alo);
+        ah[i + LA] = fp8_lds_rd128<(i + LA) * 16 * BK>(ahi);
+      }
+      pre(I);
+      if constexpr (i == 0) fp8_lgkm_tie<2 * (last - i)>(bl, bh, al[0], ah[0]);
+      else fp8_lgkm_tie<2 * (last - i)>(al[i], ah[i]);
+      const i32x8 af = fp8_frag(al[i], ah[i]);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+            fp8_frag(bl[j], bh[j]), af, Z ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][j], 0, 0, 0, 127, 0, 127);
+      __builtin_amdgcn_s_setprio(0);
+      // pin the previous group's MFMAs here (a use, 4 MFMAs after them: no wait states): in the
+      // fused block their results are next read a K block later, and the compiler sank them
+      // below the epilogue
+      if constexpr (i > 0) fp8_pin(acc[i - 1]);
+    });
+    fp8_pin(acc[MI - 1]);
+  };
+  auto nop = [](auto) {};
+
+  float rs[MI], rsn[MI];
+  issue(0);
+  fp8_wait_vm_barrier<0>();                          // block 0 landed; scale / bias table written
+  load_rs(0, rs);
+  issue(1);
+  kblock(0, std::true_type{}, nop);
+  for (int k = 0; k < my_tiles; ++k) {
+    const int tau = lid + k * G;
+    const int m0 = (tau / tiles_n) * BM, n0 = (tau % tiles_n) * BN;
+    for (int kb = 1; kb < nkb; ++kb) {
+      const int f = k * nkb + kb;
+      if (kb == 1 && k > 0) fp8_wait_vm_barrier<NST>();   // younger: the previous tile's stores
+      else fp8_wait_vm_barrier<0>();
+      if (kb == nkb - 1 && k + 1 < my_tiles) load_rs(k + 1, rsn);   // older than the next DMA
+      issue(f + 1);
+      kblock(f, std::false_type{}, nop);
+    }
+    const int mw = m0 + wr * WM + fr, nw = n0 + wc * WN;
+    auto epi = [&](auto I) {
+      constexpr int i = decltype(I)::value;
+      fp8_pers_epi<MXO, ACT>(p, acc[i], p.sa ? rs[i] : 1.f, mw + i * 16, nw, coff, fg, s_sb, s_bias, ry, rsc);
+    };
+    if (k + 1 < my_tiles) {                          // epilogue fused with the next tile's block 0
+      const int f = (k + 1) * nkb;
+      fp8_wait_vm_barrier<0>();
+      issue(f + 1);
+      kblock(f, std::true_type{}, epi);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) rs[i] = rsn[i];
+    } else {
+      fp8_static_for<0, MI>(epi);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1253,10 +1531,29 @@ extern "C" int aiko_gemm_fp8(const void* a, const void* b, const float* sa, cons
     const int tiles_n = N / 256, ntiles = ((M + 255) / 256) * tiles_n;
     const dim3 pg((unsigned)(ntiles < cus ? ntiles : cus));
     static const int diag = [] {                     // AIKO_FP8_DIAG: timing diagnostics only (1: no K-block DMAs
-      const char* e = getenv("AIKO_FP8_DIAG");       // after the first two, 2: no epilogue stores, 4: no barrier)
-      return e ? atoi(e) : 0;                        // — wrong results by design
+      const char* e = getenv("AIKO_FP8_DIAG");       // after the first two, 2: no epilogue stores, 4: no barrier,
+      return e ? atoi(e) : 0;                        // 8: no epilogue) — wrong results by design
     }();
-    if (yq) gemm_fp8_pers_kernel<true><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles, diag);
+    static const bool ov = [] {                      // AIKO_FP8_OVERLAP=1: epilogue overlapped
+      const char* e = getenv("AIKO_FP8_OVERLAP");    // with the next tile's first K block
+      return e && e[0] == '1';
+    }();
+    if (ov) {                                        // activation as a template argument: the
+      auto go = [&](auto mxo, auto act) {            // epilogue's registers are those of one path
+        gemm_fp8_pers2_kernel<decltype(mxo)::value, decltype(act)::value>
+            <<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles, diag);
+      };
+      auto by_act = [&](auto mxo) {
+        switch (p.act) {
+          case 1: go(mxo, std::integral_constant<int, 1>{}); break;
+          case 2: go(mxo, std::integral_constant<int, 2>{}); break;
+          case 3: go(mxo, std::integral_constant<int, 3>{}); break;
+          default: go(mxo, std::integral_constant<int, 0>{}); break;
+        }
+      };
+      if (yq) by_act(std::true_type{});
+      else by_act(std::false_type{});
+    } else if (yq) gemm_fp8_pers_kernel<true><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles, diag);
     else gemm_fp8_pers_kernel<false><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles, diag);
     return (int)hipGetLastError();
   }

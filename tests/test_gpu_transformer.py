@@ -34,7 +34,8 @@ def test_gemm_fp8(native, tile, act):
 
 
 @pytest.mark.parametrize("M,N,K,act", [(333, 512, 768, 0), (333, 512, 768, 3), (3000, 2304, 768, 0),
-                                       (21014, 3072, 768, 3), (700, 768, 3072, 0), (1, 256, 256, 0)])
+                                       (21014, 3072, 768, 3), (700, 768, 3072, 0), (1, 256, 256, 0),
+                                       (3000, 1024, 512, 1), (600, 256, 256, 2)])
 def test_gemm_fp8_persistent(native, M, N, K, act):
     """Variant 4 (persistent 256 x 256, transposed product, register-direct epilogue): M tails,
     one and several tiles per workgroup (21014 x 3072: 996 tiles on the CUs), a single-row M,
@@ -47,8 +48,7 @@ def test_gemm_fp8_persistent(native, M, N, K, act):
     out = torch.full((M + 3, N), 7.0, dtype=torch.bfloat16, device=DEV)
     TR.linear_fp8(xq.to(DEV), xs.to(DEV), lin, out=out[:M], act=act, tile=(256, 256, 4))
     ref = (xq.view(torch.float8_e4m3fn).float() * xs[:, None]).to(DEV) @ lin.ref_weight.T.to(DEV) + lin.bias
-    if act == 3:
-        ref = F.gelu(ref)
+    ref = {0: ref, 1: F.relu(ref), 2: F.silu(ref), 3: F.gelu(ref)}[act]
     assert _rel(out[:M], ref) < 5e-3
     assert bool((out[M:] == 7.0).all())
 
