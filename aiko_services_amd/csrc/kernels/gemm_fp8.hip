@@ -1073,8 +1073,10 @@ __device__ __forceinline__ void fp8_pers_epi(const Fp8GemmParams& p, const f32x4
   }
 }
 
-// Persistent 256 x 256 fp8 GEMM, epilogue overlapped with MFMA work (tuner variant 4 with
-// AIKO_FP8_OVERLAP=1; otherwise gemm_fp8_pers_kernel above).  Same walk, ring and store layout, two
+// Persistent 256 x 256 fp8 GEMM, epilogue overlapped with MFMA work (tuner variant 4;
+// AIKO_FP8_OVERLAP=0 selects gemm_fp8_pers_kernel above).  qkv 56.3 -> 51.5 us, fc1 (GELU + MX
+// out) 75.1 -> 68.0 us, Whisper-small 14-stream bench 3,076 / 3,125 -> 3,208 / 3,226 windows/s
+// (scripts/fp8_diag.sh, interleaved).  Same walk, ring and store layout, two
 // changes in the schedule:
 //   - the epilogue of tile k runs interleaved with the first K block of tile k + 1: fragment
 //     group i is stored, then its accumulators take the next tile's group-i MFMAs (started from
@@ -1534,9 +1536,9 @@ extern "C" int aiko_gemm_fp8(const void* a, const void* b, const float* sa, cons
       const char* e = getenv("AIKO_FP8_DIAG");       // after the first two, 2: no epilogue stores, 4: no barrier,
       return e ? atoi(e) : 0;                        // 8: no epilogue) — wrong results by design
     }();
-    static const bool ov = [] {                      // AIKO_FP8_OVERLAP=1: epilogue overlapped
-      const char* e = getenv("AIKO_FP8_OVERLAP");    // with the next tile's first K block
-      return e && e[0] == '1';
+    static const bool ov = [] {                      // AIKO_FP8_OVERLAP=0: epilogue after the K
+      const char* e = getenv("AIKO_FP8_OVERLAP");    // loop (gemm_fp8_pers_kernel)
+      return !(e && e[0] == '0');
     }();
     if (ov) {                                        // activation as a template argument: the
       auto go = [&](auto mxo, auto act) {            // epilogue's registers are those of one path

@@ -14,3 +14,10 @@ for op in gemm_qkv gemm_fc1; do
     done
   done
 done
+# Whisper-small encoder bench (14 streams) A/B over the overlap switch, interleaved
+for i in $(seq ${WHISPER_AB:-0}); do
+  for a in 0 1; do
+    echo -n "whisper overlap=$a: "
+    AIKO_FP8_OVERLAP=$a timeout -k 10 300 python bench.py --model whisper-small --steps 20 --warmup 5 2>&1 | grep -o '"value": [0-9.]*' || exit 1
+  done
+done
