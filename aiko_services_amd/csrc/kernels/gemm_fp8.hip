@@ -995,10 +995,11 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers_kernel(Fp8GemmParams p, 
 // Epilogue of one 16-row fragment group of the persistent kernels' 128 x 64 wave tile: both
 // 32-column fragment pairs (lane l: row l & 15, eight consecutive columns after the permlane
 // swap), per-channel scale + bias from LDS, activation, bf16 or MX-fp8 store.
-template <bool MXO, int ACT>
+template <bool MXO, int ACT, bool RES>
 __device__ __forceinline__ void fp8_pers_epi(const Fp8GemmParams& p, const f32x4 (&acc)[4], float rs, int m, int nw,
                                              int coff, int fg, const float* s_sb, const float* s_bias,
-                                             __amdgpu_buffer_rsrc_t ry, __amdgpu_buffer_rsrc_t rsc) {
+                                             __amdgpu_buffer_rsrc_t ry, __amdgpu_buffer_rsrc_t rsc,
+                                             const u32x4 (&rv)[2]) {
 #pragma unroll
   for (int pp = 0; pp < 2; ++pp) {
     const int nb = nw + pp * 32, n = nb + coff;
@@ -1031,6 +1032,13 @@ __device__ __forceinline__ void fp8_pers_epi(const Fp8GemmParams& p, const f32x4
         const f32x2 g = gelu_erf2(f32x2{v[2 * e], v[2 * e + 1]});
         v[2 * e] = g[0];
         v[2 * e + 1] = g[1];
+      }
+    }
+    if constexpr (RES) {                             // residual (8 bf16, prefetched), after the activation
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[2 * e] += __uint_as_float(rv[pp][e] << 16);
+        v[2 * e + 1] += __uint_as_float(rv[pp][e] & 0xffff0000u);
       }
     }
     const bool live = m < p.M;
@@ -1086,15 +1094,17 @@ __device__ __forceinline__ void fp8_pers_epi(const Fp8GemmParams& p, const f32x4
 //     fragment i + LA in flight while the MFMAs on fragment i run.
 // vmcnt: block (k, 1)'s DMA is issued right after the fused block's barrier, before that
 // block's stores, so its wait is vmcnt(NST); every other wait is vmcnt(0).
-template <bool MXO, int ACT>
+template <int BM, bool MXO, int ACT, bool MXA, bool RES>
 __global__ __launch_bounds__(512, 1) void gemm_fp8_pers2_kernel(Fp8GemmParams p, const uint8_t* zero, int tiles_n,
                                                                 int ntiles, int diag) {
-  constexpr int BM = 256, BN = 256, BK = 128, WGN = 4, WM = 128, WN = 64, MI = WM / 16, NI = WN / 16;
+  constexpr int BN = 256, BK = 128, WGN = 4, WM = BM / 2, WN = 64, MI = WM / 16, NI = WN / 16;
   constexpr int APT = BM / 64, BPT = BN / 64;
-  constexpr int STAGE_BYTES = (BM + BN) * BK;  // 64 KB
+  constexpr int TILE_BYTES = (BM + BN) * BK;
+  constexpr int STAGE_BYTES = TILE_BYTES + (MXA ? BM * 4 : 0);   // + the MX scale tile of A
   constexpr int MAXN = 3072;
   constexpr int NST = MXO ? 2 * MI * (NI / 2) : MI * (NI / 2);   // store instructions per tile per wave
   constexpr int LA = MXO && ACT == 3 ? 1 : 2;        // A fragments read ahead (1: GELU + MX registers)
+  constexpr int NRL = RES ? 2 * MI : 0;              // residual loads per tile per wave (always issued)
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE_BYTES + 2 * MAXN * 4];
   float* const s_sb = reinterpret_cast<float*>(smem + 2 * STAGE_BYTES);
   float* const s_bias = s_sb + MAXN;
@@ -1134,6 +1144,11 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers2_kernel(Fp8GemmParams p,
 #pragma unroll
     for (int i = 0; i < BPT; ++i)
       glds16_u8(p.b + (long)(n0 + lrow + 64 * i) * p.K + lp * 16 + k0, Bs + (i * 64 + wave * 8) * BK);
+    if constexpr (MXA) {   // scale rows m0 .. m0 + BM - 1 (4 B each): wave w takes BM / 8 rows
+      const int r0 = m0 + wave * (BM / 8);           // (the scale tensor holds M rounded up to 128 rows)
+      const uint8_t* src = r0 < p.mxr ? p.amx + ((long)kb * p.mxr + r0) * 4 + lane * 16 : zero;
+      if (lane < BM / 32) glds16_u8(src, As + TILE_BYTES + wave * (BM / 2));
+    }
   };
   // per-row A scales of tile k, loaded one K block before they are used: branch-free buffer
   // loads (rows past M read out of range -> 0); no per-row scales -> 1, applied at the use
@@ -1150,6 +1165,8 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers2_kernel(Fp8GemmParams p,
                                                                       0x7ffffff0, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc(MXO ? (void*)p.ysc : (void*)p.y, (short)0,
                                                                        0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rres_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.res, (short)0, 0x7ffffff0,
+                                                                             0x00020000);
   const int off_lo = (fg ^ (fr & 7)) << 4, off_hi = ((fg + 4) ^ (fr & 7)) << 4;
 
   f32x4 acc[MI][NI];
@@ -1157,6 +1174,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers2_kernel(Fp8GemmParams p,
   auto kblock = [&](int f, auto ztag, auto&& pre) {
     constexpr bool Z = decltype(ztag)::value;
     const uint32_t la = (uint32_t)reinterpret_cast<uintptr_t>(smem + (f & 1) * STAGE_BYTES + (wr * WM + fr) * BK);
+    const uint32_t* scw = reinterpret_cast<const uint32_t*>(smem + (f & 1) * STAGE_BYTES + TILE_BYTES) + wr * WM + fr;
     const uint32_t lb = la + (uint32_t)(BM * BK + (wc * WN - wr * WM) * BK);
     const uint32_t alo = la + off_lo, ahi = la + off_hi, blo = lb + off_lo, bhi = lb + off_hi;
     u32x4 bl[NI], bh[NI], al[MI], ah[MI];
@@ -1181,11 +1199,13 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers2_kernel(Fp8GemmParams p,
       if constexpr (i == 0) fp8_lgkm_tie<2 * (last - i)>(bl, bh, al[0], ah[0]);
       else fp8_lgkm_tie<2 * (last - i)>(al[i], ah[i]);
       const i32x8 af = fp8_frag(al[i], ah[i]);
+      int asc = 127;                                 // E8M0 scale of this lane's A block (byte fg)
+      if constexpr (MXA) asc = (int)(scw[i * 16] >> (8 * fg));
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int j = 0; j < NI; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-            fp8_frag(bl[j], bh[j]), af, Z ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][j], 0, 0, 0, 127, 0, 127);
+            fp8_frag(bl[j], bh[j]), af, Z ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][j], 0, 0, 0, 127, 0, asc);
       __builtin_amdgcn_s_setprio(0);
       // pin the previous group's MFMAs here (a use, 4 MFMAs after them: no wait states): in the
       // fused block their results are next read a K block later, and the compiler sank them
@@ -1207,25 +1227,41 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers2_kernel(Fp8GemmParams p,
     const int m0 = (tau / tiles_n) * BM, n0 = (tau % tiles_n) * BN;
     for (int kb = 1; kb < nkb; ++kb) {
       const int f = k * nkb + kb;
-      if (kb == 1 && k > 0) fp8_wait_vm_barrier<NST>();   // younger: the previous tile's stores
+      if (kb == 1 && k > 0) fp8_wait_vm_barrier<NST + NRL>();   // younger: the previous tile's stores
+                                                                  // and residual loads
       else fp8_wait_vm_barrier<0>();
       if (kb == nkb - 1 && k + 1 < my_tiles) load_rs(k + 1, rsn);   // older than the next DMA
       issue(f + 1);
       kblock(f, std::false_type{}, nop);
     }
     const int mw = m0 + wr * WM + fr, nw = n0 + wc * WN;
+    u32x4 rres[MI][2];                               // residual of fragment group i, loaded a group ahead
+    auto ldres = [&](int i) {
+      if constexpr (RES) {
+        const int m = mw + i * 16;
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+          const uint32_t off = m < p.M ? (uint32_t)(((long)m * p.ldr + nw + pp * 32 + coff) * 2) : 0x80000000u;
+          rres[i][pp] = __builtin_amdgcn_raw_buffer_load_b128(rres_rsrc, off, 0, 0);
+        }
+      }
+    };
     auto epi = [&](auto I) {
       constexpr int i = decltype(I)::value;
-      fp8_pers_epi<MXO, ACT>(p, acc[i], p.sa ? rs[i] : 1.f, mw + i * 16, nw, coff, fg, s_sb, s_bias, ry, rsc);
+      if constexpr (i + 1 < MI) ldres(i + 1);
+      fp8_pers_epi<MXO, ACT, RES>(p, acc[i], p.sa ? rs[i] : 1.f, mw + i * 16, nw, coff, fg, s_sb, s_bias, ry, rsc,
+                                  rres[i]);
     };
     if (k + 1 < my_tiles) {                          // epilogue fused with the next tile's block 0
       const int f = (k + 1) * nkb;
       fp8_wait_vm_barrier<0>();
       issue(f + 1);
+      ldres(0);
       kblock(f, std::true_type{}, epi);
 #pragma unroll
       for (int i = 0; i < MI; ++i) rs[i] = rsn[i];
     } else {
+      ldres(0);
       fp8_static_for<0, MI>(epi);
     }
   }
@@ -1512,7 +1548,7 @@ extern "C" int aiko_gemm_fp8(const void* a, const void* b, const float* sa, cons
   p.ysc = static_cast<uint8_t*>(ysc);
   p.ldq = ldq;
   p.ysr = ysr;
-  if ((amx || yq) && variant != 1 && variant != 3 && variant != 4) return -1;   // MX paths: LDS-DMA kernels
+  if ((amx || yq) && variant != 1 && variant != 3 && variant != 4 && variant != 5) return -1;   // MX: LDS-DMA kernels
   p.a = static_cast<const uint8_t*>(a);
   p.b = static_cast<const uint8_t*>(b);
   p.sa = sa; p.sb = sb; p.bias = bias;
@@ -1520,29 +1556,40 @@ extern "C" int aiko_gemm_fp8(const void* a, const void* b, const float* sa, cons
   p.y = static_cast<bf16_t*>(y);
   p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldy = ldy; p.ldr = ldr; p.act = act;
   dim3 grid(((M + bm - 1) / bm) * ((N + bn - 1) / bn)), block(256);
-  if (variant == 4) {                   // persistent 256 x 256 (short-K qkv / fc1 shapes)
+  if (variant == 4 || variant == 5) {   // persistent 256 x 256 / 128 x 256 (short-K encoder shapes)
     const uint8_t* z = static_cast<const uint8_t*>(zero);
-    if (!z || amx || res || bm != 256 || bn != 256 || N % 256 || N > 3072 || K % 128 || K < 256) return -1;
+    const int BMv = variant == 4 ? 256 : 128;
+    const bool mxres = amx && res && act == 0 && !yq;   // variant 5: MX-fp8 A + residual (out-proj, fc2)
+    if (!z || bm != BMv || bn != 256 || N % 256 || N > 3072 || K % 128 || K < 256) return -1;
+    if ((amx || res) && !(variant == 5 && mxres)) return -1;
     if ((long)M * (yq ? ldq : 2L * ldy) >= 0x7ffffff0L || (yq && (long)(N / 128) * ysr * 4 >= 0x7ffffff0L)) return -1;
+    if (res && ((long)M * ldr * 2 >= 0x7ffffff0L || ldr % 8 || reinterpret_cast<uintptr_t>(res) % 16)) return -1;
+    if (!yq && (ldy % 8 || reinterpret_cast<uintptr_t>(y) % 16)) return -1;   // 16-B row stores
     static int cus = 0;
     if (cus == 0) {
       int dev = 0;
       (void)hipGetDevice(&dev);
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
     }
-    const int tiles_n = N / 256, ntiles = ((M + 255) / 256) * tiles_n;
+    const int tiles_n = N / 256, ntiles = ((M + BMv - 1) / BMv) * tiles_n;
     const dim3 pg((unsigned)(ntiles < cus ? ntiles : cus));
     static const int diag = [] {                     // AIKO_FP8_DIAG: timing diagnostics only (1: no K-block DMAs
       const char* e = getenv("AIKO_FP8_DIAG");       // after the first two, 2: no epilogue stores, 4: no barrier,
       return e ? atoi(e) : 0;                        // 8: no epilogue) — wrong results by design
     }();
     static const bool ov = [] {                      // AIKO_FP8_OVERLAP=0: epilogue after the K
-      const char* e = getenv("AIKO_FP8_OVERLAP");    // loop (gemm_fp8_pers_kernel)
+      const char* e = getenv("AIKO_FP8_OVERLAP");    // loop (gemm_fp8_pers_kernel, variant 4 only)
       return !(e && e[0] == '0');
     }();
-    if (ov) {                                        // activation as a template argument: the
+    if (variant == 5) {
+      if (mxres) gemm_fp8_pers2_kernel<128, false, 0, true, true><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles, diag);
+      else if (yq && act == 3) gemm_fp8_pers2_kernel<128, true, 3, false, false><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles, diag);
+      else if (!yq && act == 0) gemm_fp8_pers2_kernel<128, false, 0, false, false><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles, diag);
+      else if (!yq && act == 3) gemm_fp8_pers2_kernel<128, false, 3, false, false><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles, diag);
+      else return -1;
+    } else if (ov) {                                 // activation as a template argument: the
       auto go = [&](auto mxo, auto act) {            // epilogue's registers are those of one path
-        gemm_fp8_pers2_kernel<decltype(mxo)::value, decltype(act)::value>
+        gemm_fp8_pers2_kernel<256, decltype(mxo)::value, decltype(act)::value, false, false>
             <<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles, diag);
       };
       auto by_act = [&](auto mxo) {

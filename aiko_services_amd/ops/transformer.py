@@ -171,6 +171,14 @@ def _tune_fp8(key, launch, mx=False):
             # the 14-stream shapes (M = 21014, K = 768): qkv 62.8 -> 56.8 us (1.31 PF), fc1 + GELU +
             # MX out 104.8 -> 97.7 us against the best earlier kernel
             cands.append((256, 256, 4))
+        if key[1] <= 3072 and os.environ.get("AIKO_FP8_V5", "1") == "1" and (
+                (not key[4] and not key[6] and key[5] in (0, 3) and (key[5] == 3 or not key[7]))
+                or (key[4] and key[6] and key[5] == 0 and not key[7])):
+            # persistent 128 x 256 (two row tiles per CU at N = 768): no residual / MX input, or the
+            # out-projection / fc2 form (MX-fp8 A + residual, no activation, bf16 out).  Isolated
+            # at the 14-stream shapes: out-proj 27.8 vs 28.6 us (best earlier), fc2 68.9 vs 62.0,
+            # qkv 57.3 vs 51.6 (variant 4) — the tuner keeps it where it wins (scripts/fp8_v5_check.sh)
+            cands.append((128, 256, 5))
     skip = {s.strip() for s in os.environ.get("AIKO_FP8_SKIP", "").split(",") if s.strip()}
     cands = [t for t in cands if ",".join(map(str, t)) not in skip] or cands
     for t in cands:

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Run one op repeatedly at Whisper-small encoder shapes (for rocprofv3 --pmc / timing).
 
-    python scripts/op_bench.py attn|rownorm|gemm_qkv|gemm_fc1|gemm_fc2|gemm_out|fc1_gelu_mx [--batch 16] [--iters 20]
+    python scripts/op_bench.py attn|rownorm|gemm_qkv|gemm_fc1|gemm_fc2|gemm_out|fc1_gelu_mx|out_mxr|fc2_mxr
+                               [--batch 16] [--iters 20] [--tile bm,bn,variant]
 fc1_gelu_mx is the encoder's fc1 as run: GELU + MX-fp8 output quantisation in the epilogue.
 """
 import argparse
@@ -42,7 +43,8 @@ def main():
         flops = 4 * B * H * T * T * 64
     else:
         K, N = {"gemm_qkv": (d, 3 * d), "gemm_fc1": (d, 4 * d), "gemm_fc2": (4 * d, d), "gemm_out": (d, d),
-                "fc1_gelu_mx": (d, 4 * d), "fc1_gelu": (d, 4 * d), "fc1_mx": (d, 4 * d)}[a.op]
+                "fc1_gelu_mx": (d, 4 * d), "fc1_gelu": (d, 4 * d), "fc1_mx": (d, 4 * d),
+                "out_mxr": (d, d), "fc2_mxr": (4 * d, d)}[a.op]
         x = torch.randn(M, K, device=dev)
         xq, xs = TR.quantize_rows_ref(x.cpu())
         xq, xs = xq.to(dev), xs.to(dev)
@@ -53,6 +55,11 @@ def main():
             u8, usc = TR.mx_buffers(M, N, dev)
             act = TR.ACT_GELU if a.op == "fc1_gelu_mx" else TR.ACT_NONE
             fn = lambda: TR.linear_fp8(xq, xs, lin, act=act, out_mx=(u8, usc), tile=tile)  # noqa: E731
+        elif a.op in ("out_mxr", "fc2_mxr"):           # MX-fp8 input + bf16 residual (encoder form)
+            q8, qsc = TR.mx_quantize_ref(x.cpu())
+            q8, qsc = q8.to(dev), qsc.to(dev)
+            res = torch.randn(M, N, device=dev).to(torch.bfloat16)
+            fn = lambda: TR.linear_fp8(q8, None, lin, out=out, residual=res, x_mx=qsc, tile=tile)  # noqa: E731
         elif a.op == "fc1_gelu":
             fn = lambda: TR.linear_fp8(xq, xs, lin, act=TR.ACT_GELU, out=out, tile=tile)  # noqa: E731
         else:

@@ -329,3 +329,45 @@ def test_flash_attention_mx_output(native, B, T, Tpad, H, split, monkeypatch):
     valid = valid.flatten()
     assert (asc.cpu()[:, :B * Tpad][:, valid] == rsc[:, :B * Tpad][:, valid]).float().mean() > 0.98
     assert (aq.view(B, Tpad, d)[:, T:] == 0x7f).all()                   # padding rows untouched
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 768, 768), (2000, 768, 3072), (21014, 768, 768), (1, 256, 256)])
+def test_gemm_fp8_persistent_128_mx_in_residual(native, M, N, K):
+    """Variant 5 (persistent 128 x 256, epilogue overlapped with the next tile): the out-projection
+    / fc2 form — MX-fp8 activations (E8M0 scale tile DMA'd with each K block into the MFMA's B-side
+    scale) plus a bf16 residual prefetched a fragment group ahead; M tails, one and several tiles
+    per workgroup, rows past M untouched."""
+    from aiko_services_amd.ops import transformer as TR
+    g = torch.Generator().manual_seed(M + K)
+    lin = TR.make_fp8_linear(torch.randn(N, K, generator=g) / 20, torch.randn(N, generator=g) * 0.1, DEV)
+    x = torch.randn(M, K, generator=g) * torch.exp2(torch.randint(-6, 6, (M, K // 32), generator=g).float()
+                                                    ).repeat_interleave(32, dim=1)
+    q, sc = TR.mx_quantize_ref(x)
+    res = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    out = torch.full((M + 3, N), 7.0, dtype=torch.bfloat16, device=DEV)
+    TR.linear_fp8(q.to(DEV), None, lin, out=out[:M], residual=res, x_mx=sc.to(DEV), tile=(128, 256, 5))
+    ref = TR.mx_dequant(q, sc).to(DEV) @ lin.ref_weight.T.to(DEV) + lin.bias + res.float()
+    assert _rel(out[:M], ref) < 5e-3
+    assert bool((out[M:] == 7.0).all())
+
+
+@pytest.mark.parametrize("M,N,act,mxo", [(3000, 768, 0, False), (333, 2304, 3, False), (5000, 3072, 3, True)])
+def test_gemm_fp8_persistent_128(native, M, N, act, mxo):
+    """Variant 5 without MX input / residual: bf16 out (none / GELU) and GELU + MX-fp8 out."""
+    from aiko_services_amd.ops import transformer as TR
+    g = torch.Generator().manual_seed(N + act)
+    K = 768
+    lin = TR.make_fp8_linear(torch.randn(N, K, generator=g) / 20, torch.randn(N, generator=g) * 0.1, DEV)
+    xq, xs = TR.quantize_rows_ref(torch.randn(M, K, generator=g))
+    full = (xq.view(torch.float8_e4m3fn).float() * xs[:, None]).to(DEV) @ lin.ref_weight.T.to(DEV) + lin.bias
+    if act == 3:
+        full = F.gelu(full)
+    if mxo:
+        oq, osc = TR.mx_buffers(M, N, DEV)
+        TR.linear_fp8(xq.to(DEV), xs.to(DEV), lin, act=act, out_mx=(oq, osc), tile=(128, 256, 5))
+        rq, rsc = TR.mx_quantize_ref(full.cpu())
+        assert (osc.cpu()[:, :M] == rsc[:, :M]).float().mean() > 0.98
+        assert _rel(TR.mx_dequant(oq.cpu(), osc.cpu()), TR.mx_dequant(rq, rsc)) < 1e-2
+    else:
+        y = TR.linear_fp8(xq.to(DEV), xs.to(DEV), lin, act=act, tile=(128, 256, 5))
+        assert _rel(y, full) < 5e-3
