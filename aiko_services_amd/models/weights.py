@@ -83,7 +83,29 @@ def load_state_dict(model, sd: dict, strict: bool = True) -> list:
     on_load = getattr(model, "_weights_loaded", None)
     if on_load is not None:
         on_load()
+    from ..ops.conv import refresh_derived
+    for spec in _walk_specs(model, set(), 0):       # incl. fused specs outside named_layers
+        refresh_derived(spec)
     return missing
+
+
+def _walk_specs(obj, seen: set, depth: int):
+    """Every ConvSpec reachable from ``obj`` through this package's objects, lists and dicts."""
+    from ..ops.conv import ConvSpec
+    if id(obj) in seen or depth > 5 or isinstance(obj, torch.Tensor):
+        return
+    seen.add(id(obj))
+    if isinstance(obj, ConvSpec):
+        yield obj
+    elif isinstance(obj, (list, tuple)):
+        for o in obj:
+            yield from _walk_specs(o, seen, depth + 1)
+    elif isinstance(obj, dict):
+        for o in obj.values():
+            yield from _walk_specs(o, seen, depth + 1)
+    elif type(obj).__module__.startswith("aiko_services_amd") and hasattr(obj, "__dict__"):
+        for o in vars(obj).values():
+            yield from _walk_specs(o, seen, depth + 1)
 
 
 def save_weights(model, path: str, with_reference: bool = False) -> None:

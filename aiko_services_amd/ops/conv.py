@@ -360,6 +360,15 @@ def patchw_weight(spec: ConvSpec) -> torch.Tensor:
     return img
 
 
+def refresh_derived(spec: ConvSpec) -> None:
+    """Re-derive, in place, every lazily built weight image this spec already holds (patch /
+    patchw / rows kernels).  Called by ``models.weights.load_state_dict``: a captured hipGraph
+    replays these images without re-entering Python, so they cannot wait for the next eager call."""
+    for attr, derive in (("_patch_w", patch_weight), ("_patchw_w", patchw_weight), ("_rows_w", rows_weight)):
+        if getattr(spec, attr, None) is not None:
+            derive(spec)
+
+
 def _rows_strided(t: torch.Tensor | None, B: int, H: int) -> bool:
     return (t is not None and t.dim() == 4 and t.shape[0] == B and t.shape[1] == H and t.shape[2] == 80
             and t.stride(3) == 1 and t.stride(2) % 8 == 0 and t.stride(1) == 80 * t.stride(2)
