@@ -910,10 +910,10 @@ void gemm_fp8_out(const at::Tensor& a, const c10::optional<at::Tensor>& sa_opt, 
     TORCH_CHECK(yp != nullptr, "aiko.gemm_fp8_out: y (or yq) required");
   }
   TORCH_CHECK(!(mx_in || mx_out) || (variant == 1 && bn == 128) || (variant == 3 && bm == 256 && bn == 256 && N % 256 == 0) ||
-                  (variant == 4 && !mx_in && bm == 256 && bn == 256 && N % 256 == 0) ||
+                  (variant == 4 && bm == 256 && bn == 256 && N % 256 == 0) ||
                   (variant == 5 && bm == 128 && bn == 256 && N % 256 == 0),
               "aiko.gemm_fp8_out: MX paths need variant 1 with BN 128, variant 3 (256 x 256, N % 256 == 0), "
-              "variant 4 (persistent 256 x 256, MX output only) or variant 5 (persistent 128 x 256)");
+              "variant 4 (persistent 256 x 256) or variant 5 (persistent 128 x 256)");
   const float* bp = nullptr;
   if (bias.has_value() && bias->defined()) {
     check_cuda(*bias, "bias");

@@ -1103,7 +1103,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers2_kernel(Fp8GemmParams p,
   constexpr int STAGE_BYTES = TILE_BYTES + (MXA ? BM * 4 : 0);   // + the MX scale tile of A
   constexpr int MAXN = 3072;
   constexpr int NST = MXO ? 2 * MI * (NI / 2) : MI * (NI / 2);   // store instructions per tile per wave
-  constexpr int LA = MXO && ACT == 3 ? 1 : 2;        // A fragments read ahead (1: GELU + MX registers)
+  constexpr int LA = (MXO && ACT == 3) || (BM == 256 && RES) ? 1 : 2;   // A fragments read ahead (1: registers)
   constexpr int NRL = RES ? 2 * MI : 0;              // residual loads per tile per wave (always issued)
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE_BYTES + 2 * MAXN * 4];
   float* const s_sb = reinterpret_cast<float*>(smem + 2 * STAGE_BYTES);
@@ -1559,9 +1559,9 @@ extern "C" int aiko_gemm_fp8(const void* a, const void* b, const float* sa, cons
   if (variant == 4 || variant == 5) {   // persistent 256 x 256 / 128 x 256 (short-K encoder shapes)
     const uint8_t* z = static_cast<const uint8_t*>(zero);
     const int BMv = variant == 4 ? 256 : 128;
-    const bool mxres = amx && res && act == 0 && !yq;   // variant 5: MX-fp8 A + residual (out-proj, fc2)
+    const bool mxres = amx && res && act == 0 && !yq;   // MX-fp8 A + residual (out-proj, fc2)
     if (!z || bm != BMv || bn != 256 || N % 256 || N > 3072 || K % 128 || K < 256) return -1;
-    if ((amx || res) && !(variant == 5 && mxres)) return -1;
+    if ((amx || res) && !mxres) return -1;
     if ((long)M * (yq ? ldq : 2L * ldy) >= 0x7ffffff0L || (yq && (long)(N / 128) * ysr * 4 >= 0x7ffffff0L)) return -1;
     if (res && ((long)M * ldr * 2 >= 0x7ffffff0L || ldr % 8 || reinterpret_cast<uintptr_t>(res) % 16)) return -1;
     if (!yq && (ldy % 8 || reinterpret_cast<uintptr_t>(y) % 16)) return -1;   // 16-B row stores
@@ -1587,6 +1587,8 @@ extern "C" int aiko_gemm_fp8(const void* a, const void* b, const float* sa, cons
       else if (!yq && act == 0) gemm_fp8_pers2_kernel<128, false, 0, false, false><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles, diag);
       else if (!yq && act == 3) gemm_fp8_pers2_kernel<128, false, 3, false, false><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles, diag);
       else return -1;
+    } else if (mxres) {
+      gemm_fp8_pers2_kernel<256, false, 0, true, true><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles, diag);
     } else if (ov) {                                 // activation as a template argument: the
       auto go = [&](auto mxo, auto act) {            // epilogue's registers are those of one path
         gemm_fp8_pers2_kernel<256, decltype(mxo)::value, decltype(act)::value, false, false>

@@ -166,8 +166,11 @@ def _tune_fp8(key, launch, mx=False):
             cands.append((256, 128, 2))  # 8-wave LDS-DMA kernel (one workgroup per CU)
     if key[1] % 256 == 0:
         cands.append((256, 256, 3))      # 256 x 256 tile, 8 waves of 128 x 64 (MX in / out too)
-        if key[1] <= 3072 and not key[4] and not key[6] and os.environ.get("AIKO_FP8_PERSIST", "1") == "1":
-            # persistent 256 x 256, register-direct epilogue (no residual / MX input).  Measured at
+        if key[1] <= 3072 and os.environ.get("AIKO_FP8_PERSIST", "1") == "1" and (
+                (not key[4] and not key[6]) or (key[4] and key[6] and key[5] == 0 and not key[7]
+                                                  and os.environ.get("AIKO_FP8_V4MX", "0") == "1")):
+            # persistent 256 x 256, register-direct epilogue (no residual / MX input, or MX input +
+            # residual with no activation: the out-projection / fc2 form).  Measured at
             # the 14-stream shapes (M = 21014, K = 768): qkv 62.8 -> 56.8 us (1.31 PF), fc1 + GELU +
             # MX out 104.8 -> 97.7 us against the best earlier kernel
             cands.append((256, 256, 4))
@@ -179,8 +182,9 @@ def _tune_fp8(key, launch, mx=False):
             # at the 14-stream shapes: out-proj 27.8 vs 28.6 us (best earlier), fc2 68.9 vs 62.0,
             # qkv 57.3 vs 51.6 (variant 4) — the tuner keeps it where it wins (scripts/fp8_v5_check.sh)
             cands.append((128, 256, 5))
+    # AIKO_FP8_SKIP="256x256x4,128x256x5": candidates (BM x BN x variant) the tuner leaves out
     skip = {s.strip() for s in os.environ.get("AIKO_FP8_SKIP", "").split(",") if s.strip()}
-    cands = [t for t in cands if ",".join(map(str, t)) not in skip] or cands
+    cands = [t for t in cands if "x".join(map(str, t)) not in skip] or cands
     for t in cands:
         try:
             launch(t)

@@ -331,8 +331,9 @@ def test_flash_attention_mx_output(native, B, T, Tpad, H, split, monkeypatch):
     assert (aq.view(B, Tpad, d)[:, T:] == 0x7f).all()                   # padding rows untouched
 
 
+@pytest.mark.parametrize("tile", [(128, 256, 5), (256, 256, 4)])
 @pytest.mark.parametrize("M,N,K", [(300, 768, 768), (2000, 768, 3072), (21014, 768, 768), (1, 256, 256)])
-def test_gemm_fp8_persistent_128_mx_in_residual(native, M, N, K):
+def test_gemm_fp8_persistent_128_mx_in_residual(native, M, N, K, tile):
     """Variant 5 (persistent 128 x 256, epilogue overlapped with the next tile): the out-projection
     / fc2 form — MX-fp8 activations (E8M0 scale tile DMA'd with each K block into the MFMA's B-side
     scale) plus a bf16 residual prefetched a fragment group ahead; M tails, one and several tiles
@@ -345,7 +346,7 @@ def test_gemm_fp8_persistent_128_mx_in_residual(native, M, N, K):
     q, sc = TR.mx_quantize_ref(x)
     res = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
     out = torch.full((M + 3, N), 7.0, dtype=torch.bfloat16, device=DEV)
-    TR.linear_fp8(q.to(DEV), None, lin, out=out[:M], residual=res, x_mx=sc.to(DEV), tile=(128, 256, 5))
+    TR.linear_fp8(q.to(DEV), None, lin, out=out[:M], residual=res, x_mx=sc.to(DEV), tile=tile)
     ref = TR.mx_dequant(q, sc).to(DEV) @ lin.ref_weight.T.to(DEV) + lin.bias + res.float()
     assert _rel(out[:M], ref) < 5e-3
     assert bool((out[M:] == 7.0).all())
