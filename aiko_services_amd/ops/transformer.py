@@ -168,7 +168,7 @@ def _tune_fp8(key, launch, mx=False):
         cands.append((256, 256, 3))      # 256 x 256 tile, 8 waves of 128 x 64 (MX in / out too)
         if key[1] <= 3072 and os.environ.get("AIKO_FP8_PERSIST", "1") == "1" and (
                 (not key[4] and not key[6]) or (key[4] and key[6] and key[5] == 0 and not key[7]
-                                                  and os.environ.get("AIKO_FP8_V4MX", "0") == "1")):
+                                                  and os.environ.get("AIKO_FP8_V4MX", "1") == "1")):
             # persistent 256 x 256, register-direct epilogue (no residual / MX input, or MX input +
             # residual with no activation: the out-projection / fc2 form).  Measured at
             # the 14-stream shapes (M = 21014, K = 768): qkv 62.8 -> 56.8 us (1.31 PF), fc1 + GELU +
