@@ -57,6 +57,10 @@ class SyntheticFrames(GpuPipelineElement):
         self.frame_pool = None
         self._shape = None
         self.dropped = 0
+        # ``stamp: true`` (tests): the frame id goes into the first 8 bytes of its slot, so a
+        # frame's pixels — and every output computed from them — depend on the frame id alone,
+        # not on which slot it was served from
+        self._stamp = str(self.get_parameter("stamp", False)[0]).lower() in ("true", "1", "yes")
 
     def _ensure_pool(self, glob):
         if self.frame_pool is not None:
@@ -79,9 +83,13 @@ class SyntheticFrames(GpuPipelineElement):
         self.frame_pool = FramePool(n, B * H * W * 3, device=self.device)
         g = torch.Generator(device=self.device).manual_seed(seed)
         slots = [self.frame_pool.acquire(0) for _ in range(n)]
+        same = None
+        if self._stamp:                       # every slot the same pixels: only the stamp differs
+            same = torch.randint(0, 256, self._shape, dtype=torch.uint8, device=self.device, generator=g)
         for s in slots:
             v = self.frame_pool.view(s, self._shape, torch.uint8)
-            v.copy_(torch.randint(0, 256, self._shape, dtype=torch.uint8, device=self.device, generator=g))
+            v.copy_(same if same is not None else
+                    torch.randint(0, 256, self._shape, dtype=torch.uint8, device=self.device, generator=g))
         for s in slots:
             self.frame_pool.release_after(s)
 
@@ -103,7 +111,7 @@ class SyntheticFrames(GpuPipelineElement):
         self._next = (self._next + 1) % len(self.host_pool)
         return frames
 
-    def _frames(self):
+    def _frames(self, stream=None):
         if str(self.get_parameter("host", False)[0]).lower() in ("true", "1", "yes"):
             return self._host_frames()
         glob = str(self.get_parameter("global", False)[0]).lower() in ("true", "1", "yes") \
@@ -123,7 +131,13 @@ class SyntheticFrames(GpuPipelineElement):
         if slot < 0:
             return False
         self.hold_for_frame(self.frame_pool, slot)
-        return self.frame_pool.view(slot, self._shape, torch.uint8)
+        from ...parallel.hop import mark_frame_held
+        v = self.frame_pool.view(slot, self._shape, torch.uint8)
+        if self._stamp:
+            stamp = torch.tensor([int(getattr(stream, "frame_id", 0) or 0)], dtype=torch.int64).view(torch.uint8)
+            v.view(-1)[:8].copy_(stamp.to(self.device, non_blocking=False))
+        # the slot is the frame's until it completes: a hop may send it zero-copy
+        return mark_frame_held(v)
 
     def start_stream(self, stream, stream_id):
         limit, found = self.get_parameter("frames")
@@ -146,7 +160,7 @@ class SyntheticFrames(GpuPipelineElement):
         return StreamEvent.OKAY, {"t_submit": time.perf_counter()}
 
     def process_frame(self, stream, **kwargs):
-        frames = self._frames()
+        frames = self._frames(stream)
         if frames is False:
             self.dropped += 1
             self.share["frames_dropped"] = self.dropped
@@ -214,6 +228,14 @@ class FrameUpload(GpuPipelineElement):
                 host[j].copy_(img)
         ring["current"] = i
         return host
+
+    def start_stream(self, stream, stream_id):
+        # each frame holds one upload slot until it completes (longer when a hop sends the slot
+        # zero-copy): the pipeline's frame window must not exceed the slots, or the actor would
+        # wait in acquire() for a slot only a later response on this same thread frees
+        if self.pipeline is not None and hasattr(self.pipeline, "limit_frames"):
+            self.pipeline.limit_frames(self.name, self.pool_slots)
+        return StreamEvent.OKAY, None
 
     def process_frame(self, stream, images):
         from ...parallel.hop import mark_frame_held

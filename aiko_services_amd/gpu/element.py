@@ -106,6 +106,10 @@ class FramePool:
     def free_count(self):
         return self._pool.free_count()
 
+    def unheld_count(self) -> int:
+        """Slots no frame holds: free ones plus releases still waiting on their GPU event."""
+        return self._pool.free_count() + len(self._pending)
+
     def stats(self) -> dict:
         cap, used, hw, acq, exh = self._pool.stats()
         return {"capacity": cap, "in_use": used, "high_water": hw, "acquired": acq, "exhausted": exh}

@@ -45,6 +45,11 @@ def _rand_conv(g: torch.Generator, cout: int, cin: int, k: int) -> torch.Tensor:
     return torch.randn(cout, cin, k, k, generator=g) * math.sqrt(2.0 / fan_in)
 
 
+# workgroups of the persistent stage-1 kernel (0 = one per CU); fewer leave CUs to the other
+# frame lane's compute-bound layers while stage 1 streams HBM
+_BN_GRID = int(os.environ.get("AIKO_BN_GRID", "0") or 0)
+
+
 @dataclass
 class Bottleneck:
     conv1: C.ConvSpec
@@ -213,7 +218,7 @@ class ResNet50(WeightsMixin):
         if (self.bneck and t1 is None and (blk.down is None or conv3 is blk.fused)
                 and C.bneck_ok(x, blk.conv1, blk.conv2, conv3)):
             out = self._buf(tag + ("xa" if bi % 2 == 0 else "xb"), (B, H, W, conv3.cout))[sl]
-            return C.bneck_fused(x, blk.conv1, blk.conv2, conv3, out=out), None
+            return C.bneck_fused(x, blk.conv1, blk.conv2, conv3, out=out, grid=_BN_GRID), None
         if t1 is None:
             t1 = C.conv2d(x, blk.conv1, out=self._buf(tag + "t1", (B, H, W, blk.conv1.cout))[sl])
         Ho, Wo = blk.conv2.out_hw(H, W)

@@ -37,7 +37,10 @@ Failure.  :meth:`mark_dead` (registrar ``remove`` / last will of the peer's proc
 transport error) retires every link to and from that rank: pending transfers are dropped, never
 waited on (an RCCL send to a dead rank never completes and a ``wait()`` on it would stall this
 GPU's stream), the per-link communicators are aborted, their staging buffers are not reused, and
-any later use raises :class:`StageFailure`.
+any later use raises :class:`StageFailure`.  A frame abandoned while its peer is ALIVE
+(:meth:`drop`: hop timeout, stream destroyed) never makes a stream wait on its send either: a
+transfer still in flight keeps its slot and credit — and, zero-copy, its producer's FramePool
+slot (:class:`Dropped`) — until :meth:`poll_dropped` sees it complete or the peer is retired.
 
 Python floats (``t_submit`` stamps) travel as ``F@<repr>`` tokens so they keep their type;
 :class:`~aiko_services_amd.gpu.element.DeviceResult` values travel as a nested dict of tensor
@@ -56,7 +59,7 @@ from . import dist as D
 from .hop_state import (FLOAT_TOKEN, RESULT_KEY, TOKEN, NoCredit, StageFailure, is_token,  # noqa: F401
                         needs_decode, plane, set_plane)
 
-__all__ = ["HopPlane", "StageFailure", "NoCredit", "init_plane", "plane", "shutdown_plane", "is_token",
+__all__ = ["HopPlane", "Dropped", "StageFailure", "NoCredit", "init_plane", "plane", "shutdown_plane", "is_token",
            "needs_decode", "mark_frame_held", "TOKEN", "FLOAT_TOKEN"]
 
 _ALIGN = 256
@@ -200,6 +203,17 @@ class _SendLink:
             self.work[slot] = None
             self.bufs[slot] = None
 
+    def pending(self, slot):
+        """The slot's transfer if it may still be reading its buffer (None once it finished)."""
+        w = self.work[slot]
+        if w is None:
+            return None
+        try:
+            done = w.is_completed()
+        except Exception:                    # noqa: BLE001 — a failed transfer reads nothing more
+            done = True
+        return None if done else w
+
     def retire(self):
         """Dead peer: forget every pending transfer (never wait on them) and every buffer."""
         self.dead = True
@@ -250,6 +264,51 @@ class _RecvLink:
         return (pool, s), pool.view(s, (pool.slot_bytes,), torch.uint8)
 
 
+class Dropped:
+    """A dropped forward frame whose transfer may still be reading its bytes (the peer is alive
+    but has not posted the matching receive — stopped, hung, or just slow).  Its send slot and
+    credit stay taken, and — for a zero-copy send out of the producer's FramePool slot — the
+    callbacks the frame's owner hands over (:meth:`then`) are held back too, until
+    :meth:`HopPlane.poll_dropped` sees the transfer complete or :meth:`HopPlane.mark_dead`
+    retires the peer.  No stream ever waits on the transfer."""
+    __slots__ = ("peer", "link", "slot", "work", "callbacks", "done")
+
+    def __init__(self, peer, link, slot, work, host: bool = False):
+        self.peer, self.link, self.slot, self.work = peer, link, slot, work
+        self.callbacks: list = []
+        self.done = None
+        if host:
+            # gloo: a send's Work only reports completion through wait(), which blocks until
+            # the peer receives — so a daemon thread waits and flags it (RCCL: is_completed()
+            # queries the transfer's end event, no thread)
+            import threading
+            self.done = False
+
+            def waiter():
+                try:
+                    work.wait()
+                except Exception:            # noqa: BLE001 — failed or aborted: reads nothing more
+                    pass
+                self.done = True
+            threading.Thread(target=waiter, daemon=True, name="hop-dropped").start()
+
+    def completed(self) -> bool:
+        if self.done is not None:
+            return self.done
+        return self.link.pending(self.slot) is None
+
+    def then(self, fn) -> None:
+        self.callbacks.append(fn)
+
+    def _finish(self, reuse):
+        if reuse and not self.link.dead:
+            self.link.work[self.slot] = None
+            self.link.release(self.slot, reuse=True)
+        callbacks, self.callbacks = self.callbacks, []
+        for fn in callbacks:
+            fn()
+
+
 class _SharedSlot:
     """A receive slot shared by the members of a group message: free after the last release."""
     __slots__ = ("pool", "slot", "count")
@@ -281,6 +340,7 @@ class HopPlane:
         self.recv_links: dict = {}
         self.links = [tuple(int(x) for x in l) for l in links]
         self.dead: set = set()
+        self.suspect: set = set()          # alive but unresponsive peers (see suspend)
         self._held: dict = {}              # frame / group key -> record (see _encode_many)
         self._loop: deque = deque()        # loopback link (src == dst): staged buffers in order
         self._groups: dict = {}            # (src, dst) -> process group
@@ -290,9 +350,12 @@ class HopPlane:
         self._rejoin = rejoin
         self._readmit_callbacks: list = []  # fn(rank) after a restarted peer's links are back
         self.epochs: dict = {}             # peer rank -> epoch of its current links (0: original)
+        self._rejoined: dict = {}          # peer rank -> epoch it announced all links up at
         self.counters = {"sent_msgs": 0, "sent_bytes": 0, "recv_msgs": 0, "recv_bytes": 0,
                          "pool_overflow": 0, "pool_waits": 0, "resent": 0, "dead_peers": 0, "zero_copy": 0,
-                         "readmitted": 0}
+                         "readmitted": 0, "dropped_inflight": 0, "dropped_completed": 0,
+                         "suspended": 0}
+        self._dropped: list = []           # Dropped transfers still in flight (see drop)
         if rejoin is not None:
             for src, dst in self.links:
                 if src == dst == self.rank:
@@ -393,15 +456,32 @@ class HopPlane:
 
     def readmit_install(self, pending) -> None:
         """Swap in a peer's fresh links (credits full, sequence numbers 0) and forget that it
-        was dead; then tell the listeners (the engine re-adds the peer's replica)."""
+        was dead.  The listeners (the engine re-adds the peer's replica) hear of it once the
+        restarted peer has ALSO announced that every one of its links is up
+        (:meth:`mark_rejoined`) — a middle stage must reach its downstream peers before it is
+        given frames.  On the restarted rank itself they hear of it at once."""
         peer = pending["peer"]
         self.send_links.update(pending["send"])
         self.recv_links.update(pending["recv"])
         self._groups.update(pending["groups"])
         self.epochs[peer] = pending["epoch"]
+        self._alive(peer)
         if peer in self.dead:
             self.dead.discard(peer)
             self.counters["readmitted"] += 1
+        if self._rejoin is not None:
+            self._notify_readmit(peer)
+        elif self._rejoined.get(peer) == pending["epoch"]:
+            self._notify_readmit(peer)
+
+    def mark_rejoined(self, peer: int, epoch: int) -> None:
+        """The restarted ``peer`` (at ``epoch``) has every link of the plan up again."""
+        peer, epoch = int(peer), int(epoch)
+        self._rejoined[peer] = epoch
+        if self.epochs.get(peer) == epoch and peer not in self.dead:
+            self._notify_readmit(peer)
+
+    def _notify_readmit(self, peer) -> None:
         for fn in list(self._readmit_callbacks):
             fn(peer)
 
@@ -411,8 +491,22 @@ class HopPlane:
     # ---- credits / failure ------------------------------------------------------------------
     def credit(self, dst: int) -> int:
         """Frames that may still be sent toward ``dst`` before one is acknowledged."""
-        link = self.send_links.get(int(dst))
-        return 0 if link is None else link.credit()
+        dst = int(dst)
+        link = self.send_links.get(dst)
+        return 0 if link is None or dst in self.suspect else link.credit()
+
+    def suspend(self, rank: int) -> None:
+        """A hop to ``rank`` timed out although the peer is not known dead (stopped, hung,
+        overloaded): it gets no credit — no new frames — until it shows life again: a message
+        from it arrives, a dropped transfer toward it completes, or it is re-admitted."""
+        rank = int(rank)
+        if rank != self.rank and rank not in self.dead and rank not in self.suspect:
+            self.suspect.add(rank)
+            self.counters["suspended"] += 1
+
+    def _alive(self, rank: int) -> None:
+        if self.suspect:
+            self.suspect.discard(rank)
 
     def is_dead(self, rank: int) -> bool:
         return int(rank) in self.dead
@@ -425,40 +519,71 @@ class HopPlane:
         """The response of forward frame ``key`` arrived: its staging slot is a credit again
         (a group's slot once every member is acknowledged or dropped).  True if a credit
         returned."""
-        return self._settle(key, reuse=True)
+        return self._settle(key, reuse=True)[0]
 
-    def drop(self, key) -> None:
-        """Abandon forward frame ``key`` (ERROR / timeout): its slot is not reused while its
-        transfer might still be reading it."""
-        self._settle(key, reuse=False)
+    def drop(self, key):
+        """Abandon forward frame ``key`` (ERROR / timeout / stream destroyed).  A transfer that
+        has finished gives its slot and credit back at once.  One that may still be reading
+        (the peer never posted its receive) keeps both until it completes or the peer is
+        retired (:meth:`poll_dropped`, :meth:`mark_dead`) — nothing waits on it.  Returns the
+        :class:`Dropped` handle when the frame was sent zero-copy out of its producer's buffer
+        and the caller must hold that buffer back (``handle.then(release)``); else None."""
+        return self._settle(key, reuse=False)[1]
 
     def _settle(self, key, reuse):
+        """-> (credit returned, Dropped handle of a zero-copy send still in flight or None)."""
         gk = self._member_of.pop(key, None)
         if gk is not None:
             rec = self._held.get(gk)
             if rec is None:
-                return False
+                return False, None
             members = rec[6]
             members.pop(key, None)
             rec[7] = rec[7] and reuse
             if members:
-                return False
+                return False, None
             key, reuse = gk, rec[7]
         rec = self._held.pop(key, None)
         if rec is None:
-            return False
+            return False, None
         link = self.send_links.get(rec[0])
-        if link is not None and not link.dead and rec[1] is not None:
-            if not reuse and rec[9] and self.device.type == "cuda":
-                # a dropped zero-copy send still reads the producer's FramePool slot, which the
-                # frame's release (right after this) returns behind an event on the current
-                # stream: order that stream after the send first (RCCL: stream-ordered wait)
-                w = link.work[rec[1]]
-                if w is not None:
-                    w.wait()
-            link.release(rec[1], reuse=reuse)
-            return True
-        return False
+        if link is None or link.dead or rec[1] is None:
+            return False, None
+        if not reuse:
+            # RCCL: the end event says whether the transfer finished; gloo: only a wait can tell
+            w = link.work[rec[1]] if self.host_transfers else link.pending(rec[1])
+            if w is not None:
+                # the transfer may outlive the frame: the slot (and, zero-copy, the producer's
+                # buffer) stays taken until it completes — a stuck peer runs out of credits
+                # instead of receiving more frames
+                d = Dropped(rec[0], link, rec[1], w, host=self.host_transfers)
+                self._dropped.append(d)
+                self.counters["dropped_inflight"] += 1
+                return False, (d if rec[9] else None)
+        link.release(rec[1], reuse=True)       # the transfer finished: slot reusable as is
+        return True, None
+
+    def poll_dropped(self) -> int:
+        """Finish every dropped transfer that completed: its slot becomes a credit again and
+        the held callbacks run (e.g. the producer's FramePool slot release).  Returns how many
+        are still in flight.  Called from the engine's hop timer and on responses."""
+        if not self._dropped:
+            return 0
+        still = []
+        for d in self._dropped:
+            if d.link.dead or d.completed():
+                if not d.link.dead:
+                    self._alive(d.peer)         # it received again
+                d._finish(reuse=True)
+                self.counters["dropped_completed"] += 1
+            else:
+                still.append(d)
+        self._dropped = still
+        return len(still)
+
+    @property
+    def dropped_inflight(self) -> int:
+        return len(self._dropped)
 
     def mark_dead(self, rank: int) -> list:
         """Retire every link to / from ``rank``; returns the keys of the forward frames it held
@@ -487,6 +612,15 @@ class HopPlane:
                         _abort_process_group(group)
                     except Exception:       # noqa: BLE001 — best effort
                         pass
+        # dropped transfers toward it will never complete: their held callbacks run now (the
+        # link is retired, so nothing is reused under an RCCL kernel that the abort stopped)
+        keep = []
+        for d in self._dropped:
+            if d.peer == rank:
+                d._finish(reuse=False)
+            else:
+                keep.append(d)
+        self._dropped = keep
         return keys
 
     # ---- stream ordering -------------------------------------------------------------------
@@ -570,8 +704,9 @@ class HopPlane:
         dst = int(dst)
         link = self.send_links.get(dst)
         if link is None:
-            if dst in self.dead:
-                raise StageFailure(dst)
+            if dst in self.dead or (self.rank, dst) in self.links:
+                # a plan link that is not up (yet): a restarted rank before its rejoin finished
+                raise StageFailure(dst, "link not connected")
             raise RuntimeError(f"hop: no send link {self.rank} -> {dst} in this plan")
         tensors = []
         events = list(ready or ())
@@ -842,6 +977,7 @@ class HopPlane:
         src, seq = srcs.pop(), seqs.pop()
         if src in self.dead:
             raise StageFailure(src, "message of a retired peer")
+        self._alive(src)
         link = self.recv_links.get(src)
         if link is None:
             raise RuntimeError(f"hop: no receive link {src} -> {self.rank} in this plan")
@@ -904,6 +1040,7 @@ class HopPlane:
     def stats(self) -> dict:
         s = dict(self.counters)
         s["held_frames"] = sum(1 if rec[6] is None else len(rec[6]) for rec in self._held.values())
+        s["dropped_pending"] = len(self._dropped)
         for dst, link in self.send_links.items():
             s[f"credit_to_{dst}"] = link.credit()
         for src, link in self.recv_links.items():
@@ -911,6 +1048,8 @@ class HopPlane:
                 s[f"pool_free_from_{src}"] = link.pool.free_count()
         if self.dead:
             s["dead"] = sorted(self.dead)
+        if self.suspect:
+            s["suspect"] = sorted(self.suspect)
         return s
 
     def close(self):

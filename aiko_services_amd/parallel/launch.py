@@ -67,7 +67,8 @@ def spawn_workers(plan: Plan, plan_path: str | None = None, env: dict | None = N
     base_env["PYTHONPATH"] = root + os.pathsep + base_env.get("PYTHONPATH", "")
     if max_restarts is None:
         max_restarts = int(base_env.get("AIKO_SUPERVISE", "0") or 0)
-    state = {"stopping": False, "restarts": {}}
+    # epochs are unique across ranks (one counter): a rank's fresh links are keyed by it
+    state = {"stopping": False, "restarts": {}, "epoch": 0}
 
     def child_env(spec, epoch=0):
         e = dict(base_env, LOCAL_RANK=str(spec.device), RANK=str(spec.rank),
@@ -85,8 +86,11 @@ def spawn_workers(plan: Plan, plan_path: str | None = None, env: dict | None = N
                        env=child_env(spec, epoch))
 
     def on_exit(id, data):
-        """ProcessManager monitor thread: a worker exited."""
+        """ProcessManager monitor thread: a worker exited.  Only a failure is restarted (a
+        non-zero or signal exit code); a clean exit is part of a shutdown."""
         if state["stopping"] or not str(id).startswith("rank"):
+            return
+        if not data.get("return_code"):
             return
         rank = int(str(id)[4:])
         n = state["restarts"].get(rank, 0)
@@ -97,9 +101,10 @@ def spawn_workers(plan: Plan, plan_path: str | None = None, env: dict | None = N
                       f"({n} restarts)", file=sys.stderr, flush=True)
             return
         state["restarts"][rank] = n + 1
-        print(f"aiko supervisor: rank {rank} exited ({data.get('return_code')}): restarting it, epoch {n + 1}",
-              file=sys.stderr, flush=True)
-        start(plan.ranks[rank], epoch=n + 1)
+        state["epoch"] += 1
+        print(f"aiko supervisor: rank {rank} exited ({data.get('return_code')}): restarting it, "
+              f"epoch {state['epoch']}", file=sys.stderr, flush=True)
+        start(plan.ranks[rank], epoch=state["epoch"])
 
     manager = ProcessManager(process_exit_handler=on_exit)
     manager.supervisor_state = state
@@ -140,10 +145,31 @@ def _rejoin_topic(plan: Plan) -> str:
     return rendezvous_topic(plan.group) + "/rejoin"
 
 
+def _set_device(plane) -> None:
+    """Helper threads that touch the data plane run on the plane's GPU (HIP's current device
+    is per thread)."""
+    if plane.device.type == "cuda":
+        import torch
+        torch.cuda.set_device(plane.device)
+
+
+def _announce(plan: Plan, command: str, rank: int, epoch: int) -> None:
+    from ..message.mqtt_client import MQTTClient
+    from ..utils.configuration import get_mqtt_host
+    from ..utils.sexpr import generate
+    _, host, port = get_mqtt_host()
+    client = MQTTClient(client_id=f"aiko-{command}-{rank}-{epoch}")
+    client.connect(host, port)
+    client.publish(_rejoin_topic(plan), generate(command, [rank, epoch]), qos=1, wait=True)
+    time.sleep(0.05)
+    client.disconnect()
+
+
 def _listen_rejoin(plan: Plan, plane) -> None:
     """Every rank: on ``(rejoin rank epoch)`` for a peer this rank has links with, bring those
     links up again (off the event loop: it blocks until the peer's side connects), then swap
-    them in on the event loop."""
+    them in on the event loop; on ``(rejoined rank epoch)`` — every link of the restarted rank
+    is up — let the engine bind it again (:meth:`HopPlane.mark_rejoined`)."""
     from ..runtime import event
     from ..runtime.process import aiko
     from ..utils.sexpr import parse
@@ -154,11 +180,23 @@ def _listen_rejoin(plan: Plan, plane) -> None:
             peer, epoch = int(params[0]), int(params[1])
         except Exception:                               # noqa: BLE001 — not ours
             return False
-        if cmd != "rejoin" or peer == plane.rank or not plane.links_with(peer) \
-                or plane.epochs.get(peer, 0) >= epoch:
+        if peer == plane.rank or not plane.links_with(peer):
             return False
+        if cmd == "rejoined":
+            event.call_soon(plane.mark_rejoined, peer, epoch)
+            return False
+        if cmd != "rejoin" or plane.epochs.get(peer, 0) >= epoch:
+            return False
+        # the stage right before the peer's binds it as a remote element: its engine must see
+        # the old process's registrar remove (retire links, re-queue held frames) before the
+        # fresh links go in.  Any other neighbour (downstream: it only answered the old process)
+        # never hears of that death — the announcement itself proves it, so retire them now.
+        binds_it = plan.ranks[plane.rank].stage + 1 == plan.ranks[peer].stage
+        if not binds_it and peer not in plane.dead:
+            event.call_soon(plane.mark_dead, peer)
 
         def work():
+            _set_device(plane)
             deadline = time.time() + 30.0
             while peer not in plane.dead and time.time() < deadline:
                 time.sleep(0.05)                        # its death reaches this rank first
@@ -178,9 +216,6 @@ def rejoin(plan: Plan, rank: int, timeout_s: float = 120.0):
     default process group, a hop plane in rejoin mode, the announcement, then (helper thread)
     its links as fresh 2-rank groups.  The stage pipeline is created meanwhile; the survivors
     only route frames to it once the links are up."""
-    from ..message.mqtt_client import MQTTClient
-    from ..utils.configuration import get_mqtt_host
-    from ..utils.sexpr import generate
     from . import dist as D
     from . import hop
     from .rendezvous import connect_store
@@ -195,16 +230,14 @@ def rejoin(plan: Plan, rank: int, timeout_s: float = 120.0):
     depth = int(os.environ.get("AIKO_HOP_DEPTH", "4"))
     plane = hop.init_plane(plan.links, depth=depth, rejoin={"store": store, "epoch": epoch})
     _listen_rejoin(plan, plane)
-    _, host, port = get_mqtt_host()
-    client = MQTTClient(client_id=f"aiko-rejoin-{rank}-{epoch}")
-    client.connect(host, port)
-    client.publish(_rejoin_topic(plan), generate("rejoin", [rank, epoch]), qos=1, wait=True)
-    time.sleep(0.05)
-    client.disconnect()
+    _announce(plan, "rejoin", rank, epoch)
 
     def connect():
+        _set_device(plane)
         try:
             peers = plane.connect_rejoin(timeout_s)
+            # every link is up: the upstream stage may bind this replica again
+            _announce(plan, "rejoined", rank, epoch)
             print(f"hop rank {rank}: re-admitted (epoch {epoch}), links to {peers}", file=sys.stderr, flush=True)
         except Exception as exc:                        # noqa: BLE001
             print(f"hop rank {rank}: rejoin failed: {exc}", file=sys.stderr, flush=True)

@@ -84,7 +84,7 @@ class PipelineGraph(Graph):
     def get_element(cls, node):
         element = node.element
         if isinstance(element, RemoteReplicas):
-            return element, node.name, False, "ready" if element.members else "absent"
+            return element, node.name, False, "ready" if element.members or element.awaiting else "absent"
         if type(element).__name__ == "ServiceRemoteProxy":
             return element, node.name, False, "ready"
         lifecycle = element.share["lifecycle"]
@@ -608,7 +608,12 @@ class PipelineImpl(Pipeline):
             return False
         stream_id = str(stream_id)
         if stream_id in self.stream_leases:
-            self.logger.error(f"Create stream: {stream_id} already exists")
+            if topic_response is not None:
+                # another upstream replica (or a restarted one) opening the same stream: its
+                # frames carry their own reply topic (``reply_to``), nothing to do
+                self.logger.info(f"Create stream: {stream_id} already exists (upstream {topic_response})")
+            else:
+                self.logger.error(f"Create stream: {stream_id} already exists")
             return False
         graph_path = graph_path or self.share["graph_path"]
         if graph_path and Graph.path_local(graph_path) not in self.pipeline_graph.head_nodes:
@@ -694,9 +699,22 @@ class PipelineImpl(Pipeline):
             lease.stream.state = StreamState.STOP if lease.stream.state != StreamState.ERROR else StreamState.ERROR
             # frames still in flight (a non-graceful destroy, or an error) leave with the stream:
             # their hop / FramePool slots and admission credits come back now — a response that
-            # arrives later finds "stream not found" and is dropped
+            # arrives later finds "stream not found" and is dropped.  A frame still out on a
+            # remote hop is dropped first: a zero-copy send keeps its producer slot until the
+            # transfer has completed (hop.drop), a queued one simply leaves its queue.
+            hop = _hop.plane()
+            pending = {}
+            for key in [k for k in self._inflight if str(k[0]) == stream_id]:
+                f = self._inflight.pop(key)
+                if hop is not None and f["rank"] is not None:
+                    pending[key[1]] = hop.drop(key)
+            for node_name, fifo in list(self._pending_hops.items()):
+                for p in [p for p in fifo if str(p["stream_id"]) == stream_id]:
+                    fifo.remove(p)
+                    if p["held"] and hop is not None:
+                        pending[p["frame_id"]] = hop.drop((p["stream_id"], p["frame_id"]))
             for frame_id in list(lease.stream.frames):
-                self._release_frame(lease.stream, frame_id)
+                self._release_frame(lease.stream, frame_id, after=pending.get(frame_id))
         self._admit_release_stream(stream_id)
         hop = _hop.plane()
         if hop is not None:
@@ -852,6 +870,8 @@ class PipelineImpl(Pipeline):
             frame.hop_handles.append(hop_handle)
         if new_frame and stream_dict.get("hop_rank") is not None:
             frame.hop_reply = int(stream_dict["hop_rank"])
+        if new_frame and stream_dict.get("reply_to"):
+            frame.reply_to = str(stream_dict["reply_to"])
         return graph, stream, frame_data_in
 
     def _process_initialize_stream(self, stream, stream_dict, frame_data_in, new_frame):
@@ -1054,19 +1074,22 @@ class PipelineImpl(Pipeline):
                     if getattr(self, "response_swag", False):   # pipeline-parallel stage hand-off
                         frame_data_out = dict(frame.swag)
                     stream.queue_response.put((stream_info, frame_data_out))
-                elif stream.topic_response:
+                elif stream.topic_response or getattr(stream.frames.get(frame_id), "reply_to", None):
                     hop = _hop.plane()
-                    reply = getattr(stream.frames.get(frame_id), "hop_reply", None)
+                    done = stream.frames.get(frame_id)
+                    reply = getattr(done, "hop_reply", None)
+                    # the sender of THIS frame (a stage fed by several upstream replicas, or by a
+                    # restarted one, answers each frame to its own sender)
+                    topic = getattr(done, "reply_to", None) or stream.topic_response
                     if hop is not None and reply is not None and self._response_batch is not None:
                         # member of a group message: answered with the group, released after
-                        self._response_batch.append((stream.topic_response, reply, stream_info, frame_data_out,
+                        self._response_batch.append((topic, reply, stream_info, frame_data_out,
                                                      hop.ready_event(), stream, frame_id))
                         frame_complete = False
                     else:
                         if hop is not None and reply is not None:
                             frame_data_out = hop.encode(reply, frame_data_out)
-                        get_actor_mqtt(stream.topic_response, Pipeline).process_frame_response(stream_info,
-                                                                                               frame_data_out)
+                        get_actor_mqtt(topic, Pipeline).process_frame_response(stream_info, frame_data_out)
                 else:
                     aiko.message.publish(self.topic_out, generate("process_frame", (stream_info, frame_data_out)))
         finally:
@@ -1130,16 +1153,28 @@ class PipelineImpl(Pipeline):
             return StreamState.ERROR
         return StreamState.RUN
 
-    def _release_frame(self, stream, frame_id):
+    def _release_frame(self, stream, frame_id, after=None):
         """A frame leaves the pipeline (completed, dropped or failed): its hop receive slots and
-        FramePool slots go back (event-gated) and its admission credit is returned."""
+        FramePool slots go back (event-gated) and its admission credit is returned.  ``after``:
+        the :class:`~aiko_services_amd.parallel.hop.Dropped` handle of a zero-copy send that
+        may still read the frame's FramePool slot — its callbacks and admission credit are then
+        handed to the hop plane, which runs them once that transfer completed (no wait)."""
         done = stream.frames.pop(frame_id, None)
+        callbacks = []
         if done is not None:
             if done.hop_handles:
                 _hop.plane().release(done.hop_handles)     # event-gated slot release
-            for callback in done.on_complete:               # e.g. FramePool slots
-                callback()
-        self._admit_release((stream.stream_id, frame_id))
+            callbacks.extend(done.on_complete)              # e.g. FramePool slots
+        key = (stream.stream_id, frame_id)
+        if after is not None:
+            for callback in callbacks:
+                after.then(callback)
+            after.then(lambda: self._admit_release(key))
+            self._watch_hops()                              # the hop timer polls the transfer
+            return
+        for callback in callbacks:
+            callback()
+        self._admit_release(key)
 
     # ---- admission window (credits for generated frames) -----------------------------------------
     @property
@@ -1258,6 +1293,7 @@ class PipelineImpl(Pipeline):
         if hop is not None and rank is not None:
             # metadata over MQTT, tensors over RCCL to the remote's rank
             stream_info["hop_rank"] = hop.rank
+            stream_info["reply_to"] = self.topic_in
             try:
                 out = hop.resend(key, rank) if held else \
                     hop.encode(rank, inputs, key=key, ready=None if ready is None else [ready])
@@ -1281,13 +1317,11 @@ class PipelineImpl(Pipeline):
             self.frames_dropped += 1
             self.logger.warning(f"remote {node_name}: {limit} frames already wait for a credit: dropping "
                                 f"<{stream_id}:{frame_id}>")
-            if held:
-                hop = _hop.plane()
-                if hop is not None:
-                    hop.drop((stream_id, frame_id))
+            hop = _hop.plane()
+            pending = hop.drop((stream_id, frame_id)) if held and hop is not None else None
             lease = self.stream_leases.get(str(stream_id))
             if lease is not None:
-                self._release_frame(lease.stream, frame_id)
+                self._release_frame(lease.stream, frame_id, after=pending)
             return
         hop = _hop.plane()
         if hop is not None and not held and ready is None:
@@ -1372,7 +1406,8 @@ class PipelineImpl(Pipeline):
                                    "inputs": None, "t": now}
         self.hop_groups += 1
         self._watch_hops()
-        target.process_frames([{"stream_id": s, "frame_id": f, "hop_rank": hop.rank} for s, f in keys], outs)
+        target.process_frames([{"stream_id": s, "frame_id": f, "hop_rank": hop.rank, "reply_to": self.topic_in}
+                               for s, f in keys], outs)
 
     def _remote_done(self, key):
         f = self._inflight.pop(key, None)
@@ -1382,6 +1417,8 @@ class PipelineImpl(Pipeline):
         freed = True
         if hop is not None and f["rank"] is not None:
             freed = hop.ack(key)         # a group's credit returns with its last member
+            if hop.dropped_inflight and hop.poll_dropped() == 0:
+                freed = True             # dropped transfers finished: their credits are back
         if freed and self._pending_hops:
             self._drain_pending()
 
@@ -1391,15 +1428,18 @@ class PipelineImpl(Pipeline):
         that errors (``/root/reference/src/aiko_services/main/pipeline.py:1229-1263``)."""
         self.hops_failed += 1
         hop = _hop.plane()
-        if hop is not None:
-            hop.drop(key)
+        pending = hop.drop(key) if hop is not None else None
         self._inflight.pop(key, None)
         lease = self.stream_leases.get(str(key[0]))
         if lease is None:
-            self._admit_release(key)     # its stream is gone: only the admission credit is left
+            # its stream is gone: only the admission credit is left
+            if pending is not None:
+                pending.then(lambda: self._admit_release(key))
+            else:
+                self._admit_release(key)
             return
         stream = lease.stream
-        self._release_frame(stream, key[1])
+        self._release_frame(stream, key[1], after=pending)
         self.logger.error(f"Frame <{key[0]}:{key[1]}>: {diagnostic}")
         if stream.state != StreamState.ERROR:
             stream.state = StreamState.ERROR
@@ -1437,7 +1477,9 @@ class PipelineImpl(Pipeline):
         if hop is not None and rank is not None:
             hop.mark_dead(rank)
         node = self.pipeline_graph.get_node(element_name)
-        if replicas.members:
+        if replicas.members or (rank is not None and _supervised()):
+            # (supervised: the dead rank is restarted — its frames wait for it, up to hop_timeout)
+            replicas.awaiting = not replicas.members
             node.element = replicas
         else:
             element_instance.set_remote_absent(True)
@@ -1470,8 +1512,15 @@ class PipelineImpl(Pipeline):
         never comes ends with StreamEvent.ERROR instead of holding its stream forever."""
         timeout = self._param_float("hop_timeout", 60.0)
         now = time.monotonic()
+        hop = _hop.plane()
+        if hop is not None and hop.dropped_inflight:
+            before = hop.dropped_inflight
+            if hop.poll_dropped() < before and self._pending_hops:
+                self._drain_pending()    # credits of finished dropped transfers came back
         for key, f in list(self._inflight.items()):
             if now - f["t"] > timeout:
+                if hop is not None and f["rank"] is not None:
+                    hop.suspend(f["rank"])   # alive but unresponsive: no new frames for it
                 self._fail_frame(key, f"remote hop to {f['node']} timed out after {timeout:g}s")
         if self._pending_hops:
             self._drain_pending()
@@ -1483,7 +1532,7 @@ class PipelineImpl(Pipeline):
                                          f"no replica of {p['node']} had a credit for {timeout:g}s")
             for node_name in [n for n, f in self._pending_hops.items() if not f]:
                 del self._pending_hops[node_name]
-        if not self._inflight and not self._pending_hops:
+        if not self._inflight and not self._pending_hops and not (hop is not None and hop.dropped_inflight):
             self._hop_watch = False
             event.remove_timer_handler(self._hop_timer)
 
@@ -1538,6 +1587,14 @@ class PipelineImpl(Pipeline):
 
 # ---- remote element placeholder --------------------------------------------------------------
 
+def _supervised() -> bool:
+    """Whether dead ranks are restarted (``AIKO_SUPERVISE``, see ``parallel/launch.py``)."""
+    try:
+        return int(os.environ.get("AIKO_SUPERVISE", "0") or 0) > 0
+    except ValueError:
+        return False
+
+
 class RemoteReplicas:
     """The discovered instances of one remote PipelineElement.
 
@@ -1552,6 +1609,8 @@ class RemoteReplicas:
         self.definition = definition
         self.expected = expected        # members needed before the element counts as ready
         self._members: "OrderedDict[str, list]" = OrderedDict()    # topic_path -> [proxy, weight, credit]
+        self.awaiting = False           # every member lost, a supervised restart will bring one back
+
 
     @property
     def members(self):
@@ -1559,6 +1618,7 @@ class RemoteReplicas:
 
     def add(self, topic_path, proxy, weight: float = 1.0):
         self._members[topic_path] = [proxy, max(1e-6, float(weight)), 0.0]
+        self.awaiting = False
 
     def remove(self, topic_path) -> bool:
         return self._members.pop(topic_path, None) is not None

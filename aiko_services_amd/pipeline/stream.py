@@ -59,6 +59,7 @@ class Frame:
     swag: Dict[str, Any] = field(default_factory=dict)
     hop_handles: list = field(default_factory=list)   # RCCL receive slots held by this frame
     hop_reply: int = None          # rank to send the response tensors to (remote hop)
+    reply_to: str = None           # topic of the upstream stage that sent this frame
     on_complete: list = field(default_factory=list)   # callbacks when the frame completes
     lane: int = None               # frame lane (gpu_lanes > 1): a hop's response resumes on it
 

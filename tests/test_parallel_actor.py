@@ -335,6 +335,31 @@ def test_restarted_replica_is_readmitted(cluster):
     assert _single(cluster, d, frames) == par
 
 
+def test_restarted_middle_stage_is_readmitted(cluster):
+    """the MIDDLE rank of the 3-stage chain (tensor_pp3.json) dies after its 2nd
+    frame and is restarted.  Rank 0 binds it as a remote, rank 2 only answered it: rank 2
+    retires the old links on the rejoin announcement itself (it never sees a registrar remove
+    of a remote of its own), and rank 0 re-binds the new rank 1 only once it announced that ALL
+    its links — including the one to rank 2 — are up.  Frames held by the dead rank are re-sent
+    to the new one and every output matches the single-process run."""
+    frames = 40
+    path, d = _variant(os.path.join(DEFS, "tensor_pp3.json"), frames=frames, rate=12, hop_timeout=40)
+    env = dict(cluster["env"], AIKO_FAULTS="kill=2@rank1", AIKO_SUPERVISE="1", AIKO_LOG_LEVEL="INFO")
+    try:
+        t0 = time.time()
+        r, par = _create(env, path, frames, timeout=170)
+        elapsed = time.time() - t0
+    finally:
+        os.unlink(path)
+    text = r.stdout + r.stderr
+    assert len(par) == frames, (r.returncode, text[-4000:])
+    assert "rank 1 exited" in text and "restarting it, epoch 1" in text, text[-3000:]
+    assert "hop rank 1: re-admitted (epoch 1)" in text, text[-3000:]
+    assert "rejoin failed" not in text and "re-admitting rank 1 failed" not in text, text[-3000:]
+    assert elapsed < 60, elapsed          # no survivor waited out the 30 s death grace
+    assert _single(cluster, d, frames) == par
+
+
 @pytest.mark.parametrize("kill", [False, True])
 def test_dp_replicated_survives_rank_loss(cluster, kill):
     """config 4's DP shape (ingest -> fan-out -> detector -> gather) as
@@ -364,10 +389,11 @@ def test_dp_replicated_survives_rank_loss(cluster, kill):
     if kill:
         rank0 = re.search(r"hop rank 0 stats: (\{.*\})", text)
         assert rank0 and "'dead': [2]" in rank0.group(1), text[-3000:]
-    # SyntheticFrames serves pre-filled pool slots in completion order, so which slot a frame id
-    # gets depends on timing: every parallel output must be one of the single-process outputs
+    # SyntheticFrames stamps the frame id into its slot (``stamp: true``): a frame's output
+    # depends on its id alone, whichever slot / replica served it — compared frame by frame
     single = _single(cluster, d, frames)
-    assert set(par.values()) <= set(single.values()), (par, single)
+    assert len(set(single.values())) == frames, single
+    assert par == single, (par, single)
 
 
 def test_planner_prices_pcie_ingest():
