@@ -5,7 +5,8 @@ bit-reproducible, so a pipeline split over processes (``parallel/placement.py``,
 over RCCL / gloo) must produce exactly the outputs of the single-process run.
 
 * ``TensorFrames`` — frame generator (``frames`` per stream): ``x`` float32 [batch, width],
-  a function of the frame id, plus ``t_submit``;
+  a function of the frame id, plus ``t_submit`` (``gpu_sleep``: GPU cycles spent before ``x``
+  is written — a slow producer for stream-ordering tests);
 * ``TensorAffine`` — ``x * scale + shift`` (float32, element-wise);
 * ``TensorStats``  — per-row sum and max as a :class:`DeviceResult` (``stats``).
 """
@@ -22,6 +23,8 @@ __all__ = ["TensorFrames", "TensorAffine", "TensorStats"]
 
 
 class TensorFrames(GpuPipelineElement):
+    lane_safe = True          # no device state kept across frames
+
     def __init__(self, context):
         context.set_protocol("tensor_frames:0")
         super().__init__(context)
@@ -45,12 +48,18 @@ class TensorFrames(GpuPipelineElement):
         _, frame_id = self.get_stream()
         B = int(self.get_parameter("batch", 4)[0])
         W = int(self.get_parameter("width", 256)[0])
+        sleep = int(self.get_parameter("gpu_sleep", 0)[0] or 0)
+        if sleep and self.device.type == "cuda":
+            # a slow producer (GPU cycles before x is written): stream-ordering tests
+            torch.cuda._sleep(sleep)
         x = torch.arange(B * W, dtype=torch.float32, device=self.device).reshape(B, W)
         x = torch.sin(x * 0.01 + float(frame_id))
         return StreamEvent.OKAY, {"x": x, "t_submit": kwargs.get("t_submit", time.perf_counter())}
 
 
 class TensorAffine(GpuPipelineElement):
+    lane_safe = True          # no device state kept across frames
+
     def __init__(self, context):
         context.set_protocol("tensor_affine:0")
         super().__init__(context)
@@ -62,6 +71,8 @@ class TensorAffine(GpuPipelineElement):
 
 
 class TensorStats(GpuPipelineElement):
+    lane_safe = True          # no device state kept across frames
+
     def __init__(self, context):
         context.set_protocol("tensor_stats:0")
         super().__init__(context)

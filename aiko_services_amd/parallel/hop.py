@@ -498,15 +498,18 @@ class HopPlane:
     def suspend(self, rank: int) -> None:
         """A hop to ``rank`` timed out although the peer is not known dead (stopped, hung,
         overloaded): it gets no credit — no new frames — until it shows life again: a message
-        from it arrives, a dropped transfer toward it completes, or it is re-admitted."""
+        from it arrives (:meth:`mark_alive`) or it is re-admitted."""
         rank = int(rank)
         if rank != self.rank and rank not in self.dead and rank not in self.suspect:
             self.suspect.add(rank)
             self.counters["suspended"] += 1
 
-    def _alive(self, rank: int) -> None:
+    def mark_alive(self, rank: int) -> None:
+        """``rank`` sent something (a message, a response): it is not stuck."""
         if self.suspect:
-            self.suspect.discard(rank)
+            self.suspect.discard(int(rank))
+
+    _alive = mark_alive
 
     def is_dead(self, rank: int) -> bool:
         return int(rank) in self.dead
@@ -572,8 +575,7 @@ class HopPlane:
         still = []
         for d in self._dropped:
             if d.link.dead or d.completed():
-                if not d.link.dead:
-                    self._alive(d.peer)         # it received again
+                # (not proof of life: a receive the peer posted before it stopped completes too)
                 d._finish(reuse=True)
                 self.counters["dropped_completed"] += 1
             else:
@@ -750,7 +752,13 @@ class HopPlane:
         # the producer's buffer (its credit still bounds the frames in flight)
         direct = (key is not None and len(tensors) == 1 and t0.device == self.device and t0.is_contiguous()
                   and dst != self.rank and _frame_held(t0))
-        slot, buf = link.take(total, key if key is not None else (), staging=not direct)
+        if dst == self.rank and key is None:
+            # a loopback RESPONSE: the message owns its bytes (no ring slot, no credit — on the
+            # loopback link the forward frames hold every credit of this same link object, and
+            # in a multi-rank plan responses travel on the other direction's link)
+            slot, buf = None, torch.empty(max(total, 1), dtype=torch.uint8, device=self.device)
+        else:
+            slot, buf = link.take(total, key if key is not None else (), staging=not direct)
         seq = link.seq
         link.seq += 1
         # the copy below and the send (RCCL's stream waits on the current one) read the tensors:
@@ -774,7 +782,8 @@ class HopPlane:
             #  sent straight from the producer's frame-held buffer]
             self._held[key] = [dst, slot, total, specs, outs, buf, None, True, self.ready_event(), direct]
         else:
-            link.release(slot)                       # ring slot: free once its transfer is done
+            if slot is not None:
+                link.release(slot)                   # ring slot: free once its transfer is done
         return outs
 
     def _post(self, link, slot, buf, total, dst):
@@ -784,8 +793,9 @@ class HopPlane:
             # (ring / ack) before the receiver decodes, so the queue must not alias it
             # (its event: the receiver's stream is ordered after this copy, as an RCCL receive is
             # after the send it matches)
-            self._loop.append((buf[:total].clone(), self.ready_event()))
-            link.work[slot] = None
+            self._loop.append((buf[:total] if slot is None else buf[:total].clone(), self.ready_event()))
+            if slot is not None:
+                link.work[slot] = None
         else:
             # the link's process group directly: tdist.isend re-validates group and rank per call
             link.work[slot] = link.group.send([buf[:total]], link.grank, 0) if link.group is not None \

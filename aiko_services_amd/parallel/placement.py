@@ -32,7 +32,7 @@ from dataclasses import asdict, dataclass, field
 
 from ..pipeline.definition import parse_pipeline_definition_dict
 
-__all__ = ["Plan", "RankSpec", "plan_stages", "make_plan", "element_chain", "element_order", "predicted_times",
+__all__ = ["Plan", "RankSpec", "plan_stages", "make_plan", "ingest_ms_of", "size_hop_batch", "hop_pairs_per_s", "HOP_CEILING_FPS", "element_chain", "element_order", "predicted_times",
            "boundary_ms_from_bytes",
            "stage_remote_name"]
 
@@ -188,6 +188,43 @@ def plan_ingest(order, times_ms: dict, gpus: int, ingest_ms: float, boundary_ms:
     return "rank0", pp[3], pp
 
 
+# Control-plane ceiling: frames/s that rank 0's event loop sustains through remote hops (one
+# process_frame + process_frame_response pair per message, a message carrying ``hop_batch``
+# frames), flat out, 8-rank shape (7 replicas), measured on the MI355X box's CPUs with
+# ``tools/hop_bench.py`` — profiles/hop_bench_r5_flat_b{1,2,4,8}.json.
+HOP_CEILING_FPS = {1: 3502.0, 2: 7013.0, 4: 9836.0, 8: 10711.0}
+HOP_HEADROOM = 0.6        # plan for at most this fraction of the ceiling
+
+
+def hop_pairs_per_s(batches_per_s: float, remote_fraction: float) -> float:
+    """Remote-hop pairs (frame batches sent to another rank and answered) per second through
+    rank 0: the node's frame-batch rate times the share of batches that leave rank 0."""
+    return max(0.0, float(batches_per_s)) * min(1.0, max(0.0, float(remote_fraction)))
+
+
+def size_hop_batch(pairs_per_s: float, ceiling: dict | None = None, headroom: float = HOP_HEADROOM) -> int:
+    """Smallest ``hop_batch`` (frames per hop message) whose measured control-plane ceiling
+    leaves ``1 / headroom`` room over the rate the plan needs: ``pairs_per_s <= headroom x
+    ceiling[k]``.  Larger groups cost latency (frames wait for a group), so the smallest that
+    fits wins; if none fits, the largest measured one."""
+    ceiling = {int(k): float(v) for k, v in (ceiling or HOP_CEILING_FPS).items()}
+    for k in sorted(ceiling):
+        if pairs_per_s <= headroom * ceiling[k]:
+            return k
+    return max(ceiling)
+
+
+def ingest_ms_of(par: dict) -> float:
+    """PCIe upload time of one frame batch (ms) from a ``parallel`` block: ``ingest_ms``, or
+    ``frame_bytes`` (bytes per batch uploaded) over ``pcie_gbps`` (GB/s of one rank's link);
+    0 when neither is given (frames are born in HBM: nothing to price)."""
+    if par.get("ingest_ms") is not None:
+        return float(par["ingest_ms"])
+    if par.get("frame_bytes") and par.get("pcie_gbps"):
+        return float(par["frame_bytes"]) / (float(par["pcie_gbps"]) * 1e9) * 1e3
+    return 0.0
+
+
 def _compositions(total, parts):
     """Positive integer tuples of length ``parts`` summing to at most ``total``."""
     for k in range(parts, total + 1):
@@ -264,8 +301,23 @@ def _dp_replicated_plan(definition: dict, gpus: int, group: str | None) -> Plan:
     for e in d["elements"]:
         e.get("deploy", {}).get("local", {}).pop("stage", None)
     share = float(par.get("local_share", 1.0 / max(1, gpus)))
-    return make_plan(d, gpus=gpus, stages=[order[:cut], order[cut:]], replicas=[1, max(0, gpus - 1)],
+    hop = None
+    if par.get("times_ms") and gpus > 1:
+        # control-plane headroom: each replica (and rank 0's share) runs stage 1 at its measured
+        # time per frame batch, so the node completes gpus / t batches per second and the
+        # (1 - share) that leave rank 0 are remote-hop pairs through its event loop
+        t1 = sum(float(par["times_ms"].get(n, 0.0)) for n in order[cut:])
+        if t1 > 0:
+            pairs = hop_pairs_per_s(gpus * 1e3 / t1, 1.0 - share)
+            k = int(d["parameters"].get("hop_batch") or 0) or size_hop_batch(pairs, par.get("hop_ceiling"))
+            d["parameters"]["hop_batch"] = k
+            hop = {"hop_pairs_per_s": round(pairs, 1), "hop_batch": k,
+                   "hop_ceiling_fps": (par.get("hop_ceiling") or HOP_CEILING_FPS).get(k)}
+    plan = make_plan(d, gpus=gpus, stages=[order[:cut], order[cut:]], replicas=[1, max(0, gpus - 1)],
                      local_share=share if gpus > 1 else 1.0, group=group)
+    if hop:
+        plan.predicted_ms.update(hop)
+    return plan
 
 
 def boundary_ms_from_bytes(boundary_bytes: dict, link_gbps: float) -> dict:
@@ -281,8 +333,37 @@ def make_plan(definition: dict, gpus: int | None = None, stages=None, replicas=N
     elements' ``deploy.local.stage``, the balancer (``times_ms`` and ``boundary_ms``: per
     element, the cost of shipping its output to the next stage), or one element per stage."""
     par = definition.get("parallel") or {}
+    # (the planner may set pipeline parameters, e.g. hop_batch: never on the caller's dict)
+    definition = dict(definition, parameters=dict(definition.get("parameters") or {}))
     mode = par.get("mode", "pp")
     gpus = int(gpus or par.get("gpus", 1))
+    ingest = par.get("ingest")
+    if mode == "pp" and ingest in ("auto", "per_rank", "rank0") and gpus > 1:
+        # host frames (decode / camera / files): where do they enter HBM?  per_rank = every rank
+        # ingests its own batches over its own PCIe link and runs the whole chain (SPMD data
+        # parallel, nothing on xGMI); rank0 = rank 0 uploads the node's batches and the stage
+        # cut ships them over xGMI (its upload time is priced into its stage)
+        ims = ingest_ms_of(par)
+        times = {k: float(v) for k, v in (times_ms or par.get("times_ms") or {}).items()}
+        bnd = boundary_ms if boundary_ms is not None else \
+            ({k: float(v) for k, v in par["boundary_ms"].items()} if par.get("boundary_ms") else None)
+        choice, per_rank, _ = (plan_ingest(element_order(definition), times, gpus, ims, boundary_ms=bnd)
+                               if ingest == "auto" else (ingest, None, None))
+        rest = {k: v for k, v in par.items() if k not in ("ingest",)}
+        if choice == "per_rank":
+            d = dict(definition, parallel=dict(rest, mode="dp"))
+            plan = _dp_plan(d, gpus, group)
+        else:
+            order0 = element_order(definition)
+            if times:
+                times[order0[0]] = times.get(order0[0], 0.0) + ims
+            d = dict(definition, parallel=dict(rest, times_ms=times) if times else rest)
+            plan = make_plan(d, gpus=gpus, stages=stages, replicas=replicas, local_share=local_share,
+                             group=group, device_offset=device_offset, boundary_ms=boundary_ms)
+        plan.predicted_ms.update(ingest=choice, ingest_ms=round(ims, 4))
+        if per_rank:
+            plan.predicted_ms["ingest_per_rank_ms"] = [round(x, 4) for x in per_rank]
+        return plan
     if mode == "dp" and par.get("replicated"):
         return _dp_replicated_plan(definition, gpus, group)
     if mode == "dp":
@@ -310,6 +391,14 @@ def make_plan(definition: dict, gpus: int | None = None, stages=None, replicas=N
             stages, replicas, local_share, per_rank = plan_stages(order, times_ms, gpus,
                                                                   boundary_ms=boundary_ms)
             predicted = {"per_rank_ms": [round(x, 4) for x in per_rank]}
+            if len(stages) > 1 and max(per_rank) > 0:
+                # every frame batch hops once per stage boundary; rank 0 sends the share of the
+                # stage-1 batches it does not run itself
+                pairs = hop_pairs_per_s(1e3 / max(per_rank), 1.0 - local_share)
+                params = definition.setdefault("parameters", {})
+                k = int(params.get("hop_batch") or 0) or size_hop_batch(pairs, par.get("hop_ceiling"))
+                params["hop_batch"] = k
+                predicted.update(hop_pairs_per_s=round(pairs, 1), hop_batch=k)
             if boundary_ms:
                 predicted["boundary_ms"] = {s[-1]: round(boundary_ms.get(s[-1], 0.0), 4) for s in stages[:-1]}
         else:

@@ -857,6 +857,8 @@ class PipelineImpl(Pipeline):
                 return None, None, None
         if not new_frame:
             # the response of a remote hop: its credit (and held retransmit slot) is free again
+            if hop is not None and stream_dict.get("hop_rank") is not None:
+                hop.mark_alive(int(stream_dict["hop_rank"]))
             self._remote_done((stream.stream_id, stream.frame_id))
         graph, stream = self._process_initialize_stream(stream, stream_dict, frame_data_in, new_frame)
         if graph is None:
@@ -887,6 +889,7 @@ class PipelineImpl(Pipeline):
             self.logger.warning(f"{header} stream not found")
             if new_frame:
                 self._admit_release((stream_id, frame_id))   # admitted, but it never existed
+                self._reject_remote(stream_dict, "stream not found")
             return None, None
         lease.extend()
         stream = lease.stream
@@ -908,6 +911,21 @@ class PipelineImpl(Pipeline):
             return None, None
         frame.swag.update(frame_data_in)
         return graph, stream
+
+    def _reject_remote(self, stream_dict, diagnostic):
+        """A frame sent by an upstream stage cannot run here (its stream is gone — e.g. this
+        process was stopped while the sender timed the frame out and destroyed the stream):
+        answer it with an ERROR response so the sender is not left waiting, and so it hears
+        from this rank (its proof of life, ``HopPlane.mark_alive``)."""
+        reply_to = stream_dict.get("reply_to") if isinstance(stream_dict, dict) else None
+        if not reply_to:
+            return
+        info = {"stream_id": stream_dict.get("stream_id"), "frame_id": stream_dict.get("frame_id"),
+                "state": StreamState.ERROR}
+        hop = _hop.plane()
+        if hop is not None:
+            info["hop_rank"] = hop.rank
+        get_actor_mqtt(str(reply_to), Pipeline).process_frame_response(info, {"diagnostic": diagnostic})
 
     def _frame_lanes(self):
         """(lanes, device) for ``gpu_lanes`` (see ``gpu/lanes.py``); decided on first use."""
@@ -1083,12 +1101,14 @@ class PipelineImpl(Pipeline):
                     topic = getattr(done, "reply_to", None) or stream.topic_response
                     if hop is not None and reply is not None and self._response_batch is not None:
                         # member of a group message: answered with the group, released after
+                        stream_info["hop_rank"] = hop.rank
                         self._response_batch.append((topic, reply, stream_info, frame_data_out,
                                                      hop.ready_event(), stream, frame_id))
                         frame_complete = False
                     else:
                         if hop is not None and reply is not None:
                             frame_data_out = hop.encode(reply, frame_data_out)
+                            stream_info["hop_rank"] = hop.rank     # the responder (proof of life)
                         get_actor_mqtt(topic, Pipeline).process_frame_response(stream_info, frame_data_out)
                 else:
                     aiko.message.publish(self.topic_out, generate("process_frame", (stream_info, frame_data_out)))

@@ -11,6 +11,11 @@ Reference analog: the multitude chain (``/root/reference/src/aiko_services/examp
 multitude/run_large.sh``, ≤ 50 frames/s there).
 
     python -m aiko_services_amd.tools.hop_bench [--replicas 7] [--seconds 10] [--width 16]
+        [--hop-batch K] [--rate FRAMES_PER_S]
+
+``--rate`` offers frames at a fixed cadence (a deployment's frame rate, e.g. config 4 at 8 GPUs:
+~4.1k batches/s through rank 0) instead of flat out, so the p50 reported is the latency at that
+load; flat out gives the ceiling.
 
 Prints one JSON line: pairs/s at rank 0, p50 / p99 frame latency, hop stats.
 """
@@ -59,6 +64,8 @@ def main(argv=None):
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--width", type=int, default=16)
     ap.add_argument("--hop-batch", type=int, default=1, help="frames per hop message (pipeline hop_batch)")
+    ap.add_argument("--rate", type=float, default=0.0,
+                    help="offered frames/s (paced; 0 = flat out through the credit window)")
     a = ap.parse_args(argv)
     if os.environ.get("AIKO_HOP_BENCH_RANK0") == "1":
         return _rank0(a)
@@ -140,17 +147,22 @@ def _rank0(a):
             t_meas = t0 + a.warmup
             t_stop = t_meas + a.seconds
             counted = 0
+            offered = 0
             while True:
                 now = time.perf_counter()
                 if now >= t_stop:
                     break
                 for _ in range(64):
+                    if a.rate > 0 and fid >= (now - t0) * a.rate:
+                        break                   # paced: frame fid is not due yet
                     if not pipeline.admit_frame("hb", fid, timeout=0):
                         break
                     pipeline.create_frame({"stream_id": "hb", "frame_id": fid}, {"t_submit": time.perf_counter()})
                     fid += 1
+                    if now >= t_meas:
+                        offered += 1
                 try:
-                    info, out = q.get(timeout=1.0)
+                    info, out = q.get(timeout=min(1.0, 1.0 / a.rate) if a.rate > 0 else 1.0)
                 except queue.Empty:
                     continue
                 done += 1
@@ -165,7 +177,8 @@ def _rank0(a):
             result["out"] = {
                 "metric": "hop pairs/s at rank 0 (process_frame + process_frame_response, MQTT metadata + gloo tensors)",
                 "value": round(counted / elapsed, 1), "unit": "frames/s", "replicas": a.replicas,
-                "hop_batch": a.hop_batch, "hop_messages_per_s": round(
+                "hop_batch": a.hop_batch, "offered_per_s": round(offered / elapsed, 1) if a.rate > 0 else None,
+                "hop_messages_per_s": round(
                     counted / elapsed / max(1.0, (done / max(1, pipeline.hop_groups)) if a.hop_batch > 1 else 1.0), 1),
                 "window": pipeline.frame_window(), "frames_completed": done,
                 "p50_latency_ms": round(statistics.median(lat) * 1e3, 3) if lat else None,

@@ -203,7 +203,13 @@ def parse_args(argv=None) -> argparse.Namespace:
                     help="hbm: frames born in HBM (a hardware decoder); host: frames in pinned host "
                          "memory, uploaded per rank by FrameUpload on a copy stream (PCIe ingest)")
     ap.add_argument("--element-times", default=None,
-                    help="(pp) JSON {element: ms per batch} for the stage balancer")
+                    help="(pp) JSON {element: ms per batch} for the stage balancer, or @file")
+    ap.add_argument("--write-element-times", default=None,
+                    help="(pp) write the measured per-element GPU ms per batch (rank 0's elements, "
+                         "its local copy of the replicated stage included) to this file")
+    ap.add_argument("--pcie-gbps", type=float, default=50.0,
+                    help="(pp, --ingest host) one rank's host->device rate the planner prices "
+                         "the upload at (PCIe Gen5 x16 ~50 GB/s)")
     a = ap.parse_args(argv)
     explicit_hw = "--height" in (sys.argv[1:] if argv is None else argv)
     if (a.parallel == "pp" or a.model == "yolov8n") and not explicit_hw:
@@ -346,10 +352,29 @@ def main(argv=None):
     D.destroy()
 
 
-# per-element GPU ms per 256-frame batch on one MI355X (VGA frames), the balancer's default input
-# (override: --element-times '{"ResNet50Classifier": 3.3, ...}')
+# per-element GPU ms per frame batch on one MI355X (VGA frames), the balancer's default input:
+# the committed measurement (profiles/element_times_r5.json, written by a world-1
+# `bench.py --parallel pp --write-element-times` run from each element's HIP events), else
+# these round-2 estimates.  Override: --element-times '{"ResNet50Classifier": 3.3, ...}' | @file
 PP_ELEMENT_MS = {"SyntheticFrames": 0.01, "FrameResize": 0.06, "ResNet50Classifier": 3.0,
                  "ClassifierTopK": 0.03}
+_TIMES_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "element_times_r5.json")
+
+
+def _load_times(spec):
+    """--element-times: inline JSON or @file; a file may hold {"element_ms": {...}}."""
+    if not spec:
+        return {}
+    text = open(spec[1:]).read() if spec.startswith("@") else spec
+    d = json.loads(text)
+    return {k: float(v) for k, v in d.get("element_ms", d).items()}
+
+
+if os.path.exists(_TIMES_FILE):
+    try:
+        PP_ELEMENT_MS = dict(PP_ELEMENT_MS, **_load_times("@" + _TIMES_FILE))
+    except (OSError, ValueError):
+        pass
 
 
 def pp_boundary_bytes(batch: int, height: int, width: int) -> dict:
@@ -401,10 +426,15 @@ def run_pp(a, device, procs):
     from aiko_services_amd.parallel.placement import make_plan
     from aiko_services_amd.runtime.process import aiko
     ws, rank = D.world_size(), D.rank()
-    times = dict(PP_ELEMENT_MS, **(json.loads(a.element_times) if a.element_times else {}))
+    times = dict(PP_ELEMENT_MS, **_load_times(a.element_times))
     d = pp_definition(a.batch, not a.no_graph, a.height, a.width, ws, a.lanes)
     if a.ingest == "host":
         d = host_ingest(d)
+        # where the host frames enter HBM is the planner's call (placement.plan_ingest):
+        # per-rank PCIe ingest (SPMD, nothing on xGMI) or rank-0 ingest + a stage cut
+        d["parallel"].update(ingest="auto", frame_bytes=a.batch * a.height * a.width * 3,
+                             pcie_gbps=a.pcie_gbps)
+        times.setdefault("FrameUpload", 0.0)
     from aiko_services_amd.parallel.placement import boundary_ms_from_bytes
     boundary = boundary_ms_from_bytes(pp_boundary_bytes(a.batch, a.height, a.width), a.link_gbps)
     if ws == 1:
@@ -419,7 +449,8 @@ def run_pp(a, device, procs):
                          boundary_ms=boundary)
     plane = hop.init_plane(plan.links, device=device, depth=4)
     responses: queue.Queue = queue.Queue()
-    pipeline = create_rank_pipeline(plan, rank, queue_response=responses if rank == 0 else None,
+    # (per-rank ingest, an SPMD plan: every rank drives and collects its own frames)
+    pipeline = create_rank_pipeline(plan, rank, queue_response=responses if rank == 0 or plan.mode == "dp" else None,
                                     grace_time=3600, auto_start=False)
     result = {}
 
@@ -451,6 +482,27 @@ def run_pp(a, device, procs):
         if result.get("out") is not None:
             result["out"]["config"]["measured_rank_ms"] = [round(sum(g.values()), 4) for g in gathered]
             result["out"]["config"]["measured_element_ms"] = gathered
+            if a.write_element_times and rank == 0:
+                # rank 0's elements (its local copy of the replicated stage at full weight), keyed
+                # by the definition's element names; the HIP-event times of one frame overlap the
+                # other lane's work, so they are scaled to add up to the measured ms per step —
+                # the throughput cost per batch the balancer divides between GPUs
+                names = {e["name"].lower(): e["name"] for e in d["elements"]}
+                el = {}
+                for k, v in gathered[0].items():
+                    if k.startswith("local:"):
+                        k, v = k[len("local:"):], v / (plan.local_share or 1.0)
+                    el.setdefault(names.get(k.lower(), k), v)
+                step = result["out"]["ms_per_step"]
+                scale = step / max(1e-9, sum(el.values()))
+                with open(a.write_element_times, "w") as f:
+                    json.dump({"element_ms": {k: round(v * scale, 4) for k, v in el.items()},
+                               "raw_event_ms": {k: round(v, 4) for k, v in el.items()},
+                               "ms_per_step": step, "batch": a.batch, "frame_size": [a.height, a.width],
+                               "lanes": a.lanes,
+                               "source": "bench.py --parallel pp --write-element-times (world 1): median "
+                                         "HIP-event ms per element and frame batch, scaled to the "
+                                         "measured ms per step"}, f, indent=1)
         aiko.process.terminate(0)
 
     threading.Thread(target=driver, daemon=True, name="bench-driver").start()
@@ -476,7 +528,8 @@ def _drive_pp(a, pipeline, plane, plan, responses, rank, ws):
             raise RuntimeError(f"rank {rank}: stage pipeline not ready (downstream not discovered)")
         time.sleep(0.02)
     plane.barrier()                            # every stage of the plan is up
-    if rank != 0:
+    spmd = plan.mode == "dp"                   # per-rank ingest: every rank runs the whole chain
+    if rank != 0 and not spmd:
         return None
     from aiko_services_amd.runtime.actor import ActorTopic
     pipeline._post_message(ActorTopic.IN, "create_stream", ["bench", None, {}, 3600, responses, None])
@@ -506,13 +559,25 @@ def _drive_pp(a, pipeline, plane, plan, responses, rank, ws):
                 latencies.append(res.latency)
     run(max(a.warmup, 3 * ws), False)          # every replica tunes + captures its graphs
     torch.cuda.synchronize()
+    if spmd:
+        plane.barrier()
     t0 = time.perf_counter()
     run(a.steps, True)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    frames = a.batch * a.steps
+    if spmd and plane.control is not None:
+        # every rank ran its own batches: the node's frames over the slowest rank's time
+        import torch.distributed as tdist
+        got = [None] * ws
+        tdist.all_gather_object(got, elapsed, group=plane.control)
+        elapsed = max(got)
+        frames *= ws
+        if rank != 0:
+            return None
     p50 = statistics.median(latencies) if latencies else 0.0
     return {
-        "metric": METRIC, "value": round(a.batch * a.steps / elapsed, 1), "unit": "frames/s", "n_gpus": ws,
+        "metric": METRIC, "value": round(frames / elapsed, 1), "unit": "frames/s", "n_gpus": ws,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
         "data": f"synthetic (random uint8 {a.height}x{a.width} frames generated in HBM; random-init weights)",
@@ -521,6 +586,7 @@ def _drive_pp(a, pipeline, plane, plan, responses, rank, ws):
                    "image_size": [224, 224], "frame_size": [a.height, a.width],
                    "per_gpu_batch": a.batch, "parallelism": f"pp{ws}", "hipgraph": not a.no_graph,
                    "stages": plan.stages, "replicas": plan.replicas, "local_share": round(plan.local_share, 4),
+                   "ingest": plan.predicted_ms.get("ingest", "hbm"),
                    "predicted_rank_ms": plan.predicted_ms.get("per_rank_ms"),
                    "transport": "actor pipelines: MQTT metadata + RCCL P2P tensors",
                    "hop": plane.stats(),

@@ -91,8 +91,10 @@ def main(path):
                                        "credit_to_2": plane.credit(2)}
             os.kill(rank2, signal.SIGCONT)
             deadline = time.monotonic() + 30
-            while (plane.stats()["dropped_pending"] or pool().unheld_count() < pool().capacity) \
-                    and time.monotonic() < deadline:
+            # the slot comes back once the stuck send completes; the suspicion goes with the
+            # first message from rank 2 (its late responses)
+            while (plane.stats()["dropped_pending"] or pool().unheld_count() < pool().capacity
+                   or plane.suspect) and time.monotonic() < deadline:
                 time.sleep(0.05)
             result["resumed"] = {"dropped_pending": plane.stats()["dropped_pending"],
                                  "pool_free": pool().unheld_count(),

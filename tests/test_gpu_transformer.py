@@ -260,6 +260,24 @@ def test_whisper_tiny_matches_reference(native):
     assert cos > 0.99, cos
 
 
+def test_whisper_small_matches_reference_at_bench_shape(native):
+    """the PRODUCTION encoder (Whisper-small, 30 s windows) at the config-5
+    bench's shape — 14 windows per batch, so the tuner picks what the bench runs (fp8 GEMM
+    variants 4/5 with MX-fp8 A operand + residual, MX-fp8 attention output, persistent rownorm)
+    — against the fp32 PyTorch reference of the same weights: cosine > 0.99 for every window."""
+    from aiko_services_amd.models.whisper import WhisperEncoder
+    enc = WhisperEncoder("small", device=DEV)
+    g = torch.Generator().manual_seed(11)
+    amp = torch.linspace(0.02, 0.3, 14).unsqueeze(1)             # a range of signal levels
+    audio = (amp * torch.randn(14, 480000, generator=g)).to(DEV)
+    y = enc.encode(audio)
+    torch.cuda.synchronize()
+    ref = enc.reference_encode(audio)
+    assert y.shape == ref.shape == (14, 1500, 768)
+    cos = F.cosine_similarity(y.float().flatten(1), ref.flatten(1), dim=1)
+    assert bool((cos > 0.99).all()), cos.tolist()
+
+
 def test_whisper_small_30s(native):
     from aiko_services_amd.models.whisper import WhisperEncoder
     enc = WhisperEncoder("small", device=DEV)

@@ -4,8 +4,9 @@
 Two gloo processes: rank 0 sends a frame-held tensor zero-copy to rank 1, which is alive but
 does not post its receive (a stopped / hung peer).  Rank 0 drops the frame: the send slot, its
 credit and the producer's buffer (the ``Dropped`` callbacks) stay held, nothing blocks, and the
-peer is suspended (no credit).  Once rank 1 receives, ``poll_dropped`` returns the slot, runs the
-callbacks and clears the suspicion; the bytes that arrive are the producer's, unmodified."""
+peer is suspended (no credit).  Once rank 1 receives, ``poll_dropped`` returns the slot and runs the
+callbacks; the suspicion lasts until the peer sends something; the bytes that arrive are the
+producer's, unmodified."""
 import json
 import os
 import socket
@@ -52,6 +53,10 @@ def _worker(rank, port, n):
         while plane.poll_dropped() and time.monotonic() < deadline:
             time.sleep(0.01)
         assert released == [True], "held slot not returned after the transfer completed"
+        # the slot is a credit again, but a completed receive is no proof of life (it may have
+        # been posted before the peer stopped): the peer stays suspect until it sends something
+        assert plane.send_links[1].credit() == 2 and plane.credit(1) == 0
+        plane.mark_alive(1)
         assert plane.credit(1) == 2 and not plane.suspect
         assert plane.stats()["dropped_pending"] == 0 and plane.counters["dropped_completed"] == 1
         assert store.get("got") == b"ok"
