@@ -55,16 +55,25 @@ __device__ __forceinline__ void wide_vm_barrier() {
 // three blocks in flight across every barrier (the 64-deep ring fits only two slots there and
 // retires each block with one block of MFMA work to cover its DMA); 64-B rows swizzled by
 // (row >> 1) & 3.
-template <int BM, int BN, int WGM, int WGN, int NS, bool RES_PF, int OCC, int BK = 64>
+// NR (tuner variant 18, "exact N"): the tile computes only NR <= BN channels — BN is the
+// DMA's row count (whole DMA pieces), NR the channels the MFMAs and epilogue cover and the
+// channel step between tiles — so a layer with N = 80 or 144 (the YOLO heads) runs on a
+// 80- / 144-channel tile instead of wasting 3/8 or 1/4 of a 128 / 192-channel tile's MFMA work.
+// An odd number of 16-channel blocks per wave ends in an unpaired block: its lane holds 4
+// consecutive channels and stores them as 8 bytes.
+template <int BM, int BN, int WGM, int WGN, int NS, bool RES_PF, int OCC, int BK = 64, int NR = 0>
 __global__ __launch_bounds__(64 * WGM * WGN, OCC) void conv_wide_kernel(ConvParams p) {
   constexpr int NW = WGM * WGN;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(BK == 64 || BK == 32, "64- or 32-deep K blocks");
   constexpr int PPR = BK / 8;                    // 16-B pieces per tile row
   constexpr int D = NS - 1;                      // K blocks in flight ahead of the one computed
-  constexpr int WM = BM / WGM, WN = BN / WGN;    // pixels / channels per wave
+  constexpr int BNR = NR ? NR : BN;              // channels computed per tile
+  static_assert(BNR <= BN && BNR % (16 * WGN) == 0, "exact-N tile");
+  constexpr int WM = BM / WGM, WN = BNR / WGN;   // pixels / channels per wave
   constexpr int MI = WM / 16, NI = WN / 16;
-  static_assert(NI % 2 == 0 && MI >= 1, "wave tile: whole 16-pixel blocks, channel blocks in pairs");
+  static_assert((NR != 0 || NI % 2 == 0) && MI >= 1, "wave tile: whole 16-pixel blocks, channel blocks in pairs");
+  constexpr bool TAIL = NI % 2 != 0;             // an unpaired last channel block
   constexpr int RPW = 64 / PPR;                  // tile rows per wave DMA instruction
   constexpr int RPI = RPW * NW;                  // tile rows filled per DMA instruction
   static_assert(BM % RPI == 0 && BN % RPI == 0, "tile rows in whole DMA pieces");
@@ -78,10 +87,10 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCC) void conv_wide_kernel(ConvPara
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave / WGN, wc = wave % WGN;
-  const int ntn = (p.Cout + BN - 1) / BN;
+  const int ntn = (p.Cout + BNR - 1) / BNR;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int tile_n = bid % ntn, tile_m = bid / ntn;
-  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int m0 = tile_m * BM, n0 = tile_n * BNR;
 
   const int lrow = wave * RPW + lane / PPR;
   // source-side swizzle: physical piece (lane % PPR) of the row holds logical piece lp
@@ -140,18 +149,33 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCC) void conv_wide_kernel(ConvPara
       e_bias[q][4] = b1[0]; e_bias[q][5] = b1[1]; e_bias[q][6] = b1[2]; e_bias[q][7] = b1[3];
     }
   }
-  u32x4 e_res[RES_PF ? MI : 1][RES_PF ? NP : 1];
+  // the unpaired block (TAIL): lane holds channels 4 fq .. 4 fq + 3 of pixel fr
+  float e_btail[4] = {0.f, 0.f, 0.f, 0.f};
+  const int ntail = n0 + wc * WN + (NI - 1) * 16 + 4 * fq;
+  if constexpr (TAIL) {
+    if (p.bias && ntail < p.Cout) {
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(p.bias + ntail);
+      e_btail[0] = b0[0]; e_btail[1] = b0[1]; e_btail[2] = b0[2]; e_btail[3] = b0[3];
+    }
+  }
+  u32x4 e_res[RES_PF ? MI : 1][RES_PF && NP > 0 ? NP : 1];
+  uint2 e_rtail[RES_PF && TAIL ? MI : 1];
   if constexpr (RES_PF) {
     if (p.res) {
 #pragma unroll
-      for (int i = 0; i < MI; ++i)
+      for (int i = 0; i < MI; ++i) {
+        const int m = m0 + wr * WM + i * 16 + fr;
 #pragma unroll
         for (int q = 0; q < NP; ++q) {
-          const int m = m0 + wr * WM + i * 16 + fr;
           const int n = n0 + wc * WN + q * 32 + coff;
           const bool ok = m < p.M && n < p.Cout;
           e_res[i][q] = *reinterpret_cast<const u32x4*>(p.res + (ok ? (size_t)m * p.ldr + n : 0));
         }
+        if constexpr (TAIL) {
+          const bool ok = m < p.M && ntail < p.Cout;
+          e_rtail[i] = *reinterpret_cast<const uint2*>(p.res + (ok ? (size_t)m * p.ldr + ntail : 0));
+        }
+      }
     }
   }
   // the bias / residual loads stay in flight under the first K blocks: the loop's counted
@@ -345,6 +369,37 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCC) void conv_wide_kernel(ConvPara
       for (int e = 0; e < 4; ++e) o[e] = pack2(v[2 * e], v[2 * e + 1]);
       *reinterpret_cast<u32x4*>(p.y + (size_t)m * p.ldy + n) = o;
     }
+    if constexpr (TAIL) {                        // 4 consecutive channels, 8-byte store
+      if (m >= p.M || ntail >= p.Cout) continue;
+      const f32x4 a = acc[NI - 1][i];
+      uint2 r = {0u, 0u};
+      if (p.res) {
+        if constexpr (RES_PF) r = e_rtail[i];
+        else r = *reinterpret_cast<const uint2*>(p.res + (size_t)m * p.ldr + ntail);
+      }
+      float v[4] = {a[0] + e_btail[0], a[1] + e_btail[1], a[2] + e_btail[2], a[3] + e_btail[3]};
+      const float rv[4] = {__uint_as_float(r.x << 16), __uint_as_float(r.x & 0xffff0000u),
+                           __uint_as_float(r.y << 16), __uint_as_float(r.y & 0xffff0000u)};
+      if (p.res && !post) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += rv[e];
+      }
+      if (act == 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      } else if (act == 2) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = silu(v[e]);
+      } else if (act == 3) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+      }
+      if (p.res && post) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += rv[e];
+      }
+      *reinterpret_cast<uint2*>(p.y + (size_t)m * p.ldy + ntail) = uint2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+    }
   }
 }
 
@@ -373,7 +428,27 @@ extern "C" int aiko_conv_wide(const void* x, const void* w, const float* bias, c
   p.K1 = x2 ? K1 : K; p.H2 = H2; p.W2 = W2; p.C2 = C2; p.stride2 = stride2;
   conv_params_finalize(p);
   dim3 grid(((M + bm - 1) / bm) * ((Cout + bn - 1) / bn));
-  if (occ <= 1) {                     // 8 waves, one workgroup per CU
+  if (occ == 18) {                    // exact-N tiles: bn = the channels computed per tile
+    if (Cout % 16) return -1;
+    if (bm == 256 && bn == 80)        // 8 waves of 32 pixels x 80 channels (5 blocks), 128-row weight DMA
+      conv_wide_kernel<256, 128, 8, 1, 2, true, 1, 64, 80><<<grid, 512, 0, stream>>>(p);
+    else if (bm == 128 && bn == 80)   // 8 waves of 16 x 80, 2 workgroups per CU
+      conv_wide_kernel<128, 128, 8, 1, 2, true, 2, 64, 80><<<grid, 512, 0, stream>>>(p);
+    else if (bm == 256 && bn == 144)  // 8 waves of 32 x 144 (9 blocks), 192-row weight DMA
+      conv_wide_kernel<256, 192, 8, 1, 2, true, 1, 64, 144><<<grid, 512, 0, stream>>>(p);
+    else if (bm == 128 && bn == 144)  // 8 waves of 16 x 144, 2 workgroups per CU (64 + 64 KB ring)
+      conv_wide_kernel<128, 192, 8, 1, 2, true, 1, 64, 144><<<grid, 512, 0, stream>>>(p);
+    else
+      return -1;
+  } else if (occ == 19) {             // 4 waves of 64 x 64 (half the fragment reads per MFMA of
+                                      // the 8-wave 128 x 128 form), 2-slot ring, 2 workgroups per CU
+    if (bm == 128 && bn == 128)
+      conv_wide_kernel<128, 128, 2, 2, 2, true, 2><<<grid, 256, 0, stream>>>(p);
+    else if (bm == 128 && bn == 256)  // 4 waves of 64 x 128, 1 workgroup per CU (3-slot ring)
+      conv_wide_kernel<128, 256, 2, 2, 3, true, 1><<<grid, 256, 0, stream>>>(p);
+    else
+      return -1;
+  } else if (occ <= 1) {                     // 8 waves, one workgroup per CU
     if (bm == 256 && bn == 256)
       conv_wide_kernel<256, 256, 2, 4, 2, false, 1><<<grid, 512, 0, stream>>>(p);
     else if (bm == 256 && bn == 128)

@@ -261,6 +261,14 @@ WIDE4_TILES = ((256, 128), (128, 256))
 # lane ends with 8 consecutive output channels of one pixel and the epilogue goes straight from
 # registers to memory (no LDS round trip) — tiles up to 256 x 256
 WIDE8_TILES = ((256, 256), (256, 128), (128, 256), (256, 64), (128, 128))
+# variant 19: the same kernel with 4 waves of 64 x 64 (128 x 128 tile, 2 workgroups per CU) or
+# 64 x 128 (128 x 256, one per CU): half / a third fewer fragment reads per MFMA than the 8-wave
+# 128-wide forms, whose 64 x 32 wave tiles read 0.75 fragments per MFMA
+WIDE4_OCC_TILES = ((128, 128), (128, 256))
+# variant 18: the same kernel with an exact-N tile (the MFMAs and epilogue cover exactly
+# these channel counts — the YOLO head's 80-class and 64 + 80 box/class convs — instead of
+# rounding N up to a 128 / 192 tile; odd 16-channel block counts end in an 8-byte store)
+EXACT_N = (80, 144)
 # variant 9: the same kernel at 2-3 workgroups per CU (short-K, bandwidth-bound layers)
 WIDE_OCC_TILES = ((128, 128), (256, 64), (128, 64), (64, 128), (64, 64))
 # variant 11: the same kernel with 32-deep K blocks in a 4-slot ring (three blocks in flight
@@ -282,6 +290,8 @@ WIDE_DEEP_TILES = ((256, 256), (256, 128), (128, 256))
 # expansion 105.5 (13) vs 110.9 us (14) and vs 133 us for the best tiled kernel (5.6 TB/s counting the
 # residual); K=256 -> 1024 71.4 vs 71.8; K=512 -> 2048 81.1 vs 79.8 (the tiled kernel, 47 us, wins)
 _PW_AB = __import__("os").environ.get("AIKO_PW_AB") == "1"
+# opt-in tuner variants (never picked on the measured models): AIKO_CONV_EXTRA="6,11"
+_EXTRA = {int(v) for v in __import__("os").environ.get("AIKO_CONV_EXTRA", "").split(",") if v.strip().isdigit()}
 # variant 13 as the fused stage-2 projection (conv_pw_rb_kernel<false, 384, 1, 128>) in the tuner:
 # numerics-tested but measured slower than conv_wide's 256 x 256 tile (167 vs 154 us at B=320 — the
 # strided second source streams from HBM behind a 5-block lookahead), so opt-in
@@ -453,9 +463,16 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, p
             cands += [t + (2,) for t in TILES + BUF_WIDE_TILES] + [t + (3,) for t in BUF_OCC_TILES]
             cands += [t + (4,) for t in PERSIST_TILES]
             cands += [t + (5,) for t in MF32_TILES]
-            cands += [t + (6,) for t in WIDE4_TILES]
             cands += [t + (8,) for t in WIDE8_TILES] + [t + (9,) for t in WIDE_OCC_TILES]
-            cands += [t + (11,) for t in WIDE_DEEP_TILES]
+            cands += [t + (19,) for t in WIDE4_OCC_TILES]
+            if cout in EXACT_N:
+                cands += [(256, cout, 18), (128, cout, 18)]
+            # variants 6 and 11 were never the tuner's pick on any layer measured (rounds 3-4):
+            # out of default tuning (setup time), kept for other shapes behind AIKO_CONV_EXTRA=6,11
+            if 6 in _EXTRA:
+                cands += [t + (6,) for t in WIDE4_TILES]
+            if 11 in _EXTRA:
+                cands += [t + (11,) for t in WIDE_DEEP_TILES]
 
         if patch_ok:
             cands.append((8, 64, 10))        # variant 10: tile fixed by the kernel (8 rows x W)

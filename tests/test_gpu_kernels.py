@@ -146,6 +146,21 @@ def _nhwc(x_nchw):
     (64, 28, 28, 128, 512, 1, 1, 0, "relu", True, (64, 128, 13)),
     (33, 28, 28, 128, 256, 1, 1, 0, None, True, (64, 128, 13)),
     (5, 20, 20, 128, 768, 1, 1, 0, "silu", False, (64, 128, 13)),
+    # variant 18: exact-N tiles (80 / 144 channels computed per tile, 5 / 9 channel blocks per
+    # wave: the odd last block stores 8 bytes) — YOLO head shapes, 1x1 / 3x3, M tails, residual
+    # (prefetched), several channel tiles (Cout 160 / 288 = 2 tiles)
+    (1, 20, 20, 64, 80, 3, 1, 1, "silu", False, (256, 80, 18)),
+    (2, 10, 10, 64, 80, 3, 1, 1, "silu", True, (128, 80, 18)),
+    (1, 20, 20, 128, 80, 1, 1, 0, None, False, (256, 80, 18)),
+    (1, 17, 19, 64, 160, 3, 1, 1, "relu", True, (256, 80, 18)),
+    (1, 20, 20, 64, 144, 3, 1, 1, "silu", False, (256, 144, 18)),
+    (2, 9, 13, 128, 144, 3, 1, 1, "silu", True, (128, 144, 18)),
+    (1, 11, 11, 64, 288, 1, 1, 0, "gelu", True, (256, 144, 18)),
+    # variant 19: 4-wave 128 x 128 (2 per CU) and 128 x 256 tiles
+    (2, 28, 28, 128, 128, 3, 1, 1, "relu", True, (128, 128, 19)),
+    (1, 13, 9, 192, 72, 3, 2, 1, "gelu", True, (128, 128, 19)),
+    (3, 14, 14, 256, 512, 1, 1, 0, None, False, (128, 256, 19)),
+    (1, 9, 11, 128, 200, 3, 1, 1, "silu", True, (128, 256, 19)),
     # variant 14: the resident kernels with each tile's residual issued at its own tile
     (64, 28, 28, 128, 512, 1, 1, 0, "relu", True, (64, 128, 14)),
     (65, 14, 14, 256, 1024, 1, 1, 0, "relu", True, (64, 128, 14)),
