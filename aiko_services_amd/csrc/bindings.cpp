@@ -215,7 +215,7 @@ void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, co
                 "aiko.conv_igemm_out: variant 7 needs a 3x3 / pad 1 / stride 1-2 or 1x1 / stride 1 conv with Cc, Cout in {16, 32}");
     rc = aiko_conv_narrow(x.data_ptr(), w.data_ptr(), bptr, rptr, y.data_ptr(), H, W, C, Cc, R, S, stride, pad, Ho,
                           Wo, M, Cout, K, act, ldy, ldr, bm == 16 ? 16 : 8, bn == 64 ? 1 : 0, cur_stream());
-  } else if (variant == 8 || variant == 9 || variant == 11 || variant == 18 || variant == 19) {
+  } else if (variant == 8 || variant == 9 || variant == 11 || variant == 18 || variant == 19 || variant == 20) {
     // 8-wave wide tiles, transposed product, register-direct epilogue (conv_wide.hip)
     TORCH_CHECK(Cc % 64 == 0 && R * S <= 32 && x_extent * 2 < (1LL << 31) - 64 && w.numel() * 2 < (1LL << 31),
                 "aiko.conv_igemm_out: variant 8 needs Cc % 64 == 0, R*S <= 32 and operands < 2 GiB");
@@ -224,7 +224,7 @@ void conv_igemm_out(const at::Tensor& x, const c10::optional<at::Tensor>& x2, co
                 "aiko.conv_igemm_out: variant 8 needs 16-B aligned rows");
     rc = aiko_conv_wide(x.data_ptr(), w.data_ptr(), bptr, rptr, y.data_ptr(), H, W, C, Cc, R, S, stride,
                         pad, Ho, Wo, M, Cout, K, act, ldy, ldr, bm, bn, x2ptr, K1, H2, W2, C2, stride2,
-                        variant == 18 ? 18 : variant == 19 ? 19 : variant == 11 ? 11 : (variant == 9 ? 2 : 1), cur_stream());
+                        variant == 18 ? 18 : variant == 19 ? 19 : variant == 20 ? 20 : variant == 11 ? 11 : (variant == 9 ? 2 : 1), cur_stream());
   } else if (variant == 13 && dual) {
     // fused projection on the resident-weight pointwise kernel (conv_pw.hip): 1x1 main source of
     // 128 channels + a 1x1 / stride-s2 second source of 256 channels

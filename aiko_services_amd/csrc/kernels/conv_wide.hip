@@ -18,6 +18,7 @@
 // Staging is conv_buf's (buffer_load_dwordx4 ... lds with a scalar tap cursor, out-of-range
 // offsets as zero padding, XOR-swizzled 128-B rows, counted vmcnt + raw s_barrier, NS-slot
 // ring), at 512 threads and one workgroup per CU, so the tile can be 256 wide on either side.
+#include <cstdlib>
 #include <type_traits>
 
 #include "conv_common.h"
@@ -403,6 +404,276 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCC) void conv_wide_kernel(ConvPara
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Persistent form (tuner variant 20) for the short-K, residual-free layers (ResNet reductions,
+// projections: K = 384..1536, 6-24 K blocks per tile): one workgroup per CU walks tiles lid,
+// lid + G, ... with ONE ring of 64-deep K blocks running across tile boundaries, so the next
+// tile's first block is in flight while the current tile finishes its last block and stores its
+// epilogue — the per-tile ring fill that the one-shot grid pays with every new workgroup is
+// hidden (gemm_fp8_pers2_kernel's walk, applied to the implicit-GEMM conv).  The epilogue stores
+// are buffer stores that are ALWAYS issued (rows / channels past the tensor get an out-of-range
+// offset), so the wait for a tile's first block — whose younger VMEM ops are exactly the previous
+// tile's NST stores (plus the blocks issued after it) — is an exact counted vmcnt, never a
+// drain.  Biases are read from LDS (staged once), so no VGPR-destination global load is ever
+// waited on while DMAs are in flight.
+template <int BM, int BN, int WGM, int WGN, int NS>
+__global__ __launch_bounds__(64 * WGM * WGN, 1) void conv_wide_pers_kernel(ConvParams p) {
+  constexpr int BK = 64, PPR = 8;
+  constexpr int NW = WGM * WGN;
+  static_assert(NW == 8, "8 waves");
+  static_assert(NS == 2 || NS == 3, "2- or 3-slot ring");
+  constexpr int D = NS - 1;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int MI = WM / 16, NI = WN / 16, NP = NI / 2;
+  static_assert(NI % 2 == 0, "channel blocks in pairs");
+  constexpr int RPW = 64 / PPR, RPI = RPW * NW;
+  static_assert(BM % RPI == 0 && BN % RPI == 0, "tile rows in whole DMA pieces");
+  constexpr int APT = BM / RPI, BPT = BN / RPI, PER = APT + BPT;
+  constexpr int NST = MI * NP;                   // epilogue stores per thread and tile
+  constexpr int STAGE_ELEMS = (BM + BN) * BK;
+  constexpr int BIAS_FLOATS = 2048;              // Cout <= 2048 (host check)
+  static_assert(NS * STAGE_ELEMS * 2 + BIAS_FLOATS * 4 <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) bf16_t ring[NS * STAGE_ELEMS + BIAS_FLOATS * 2];
+  float* const sbias = reinterpret_cast<float*>(ring + NS * STAGE_ELEMS);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WGN, wc = wave % WGN;
+  const int ntn = (p.Cout + BN - 1) / BN;
+  const int ntiles = ((p.M + BM - 1) / BM) * ntn;
+  const int G = gridDim.x;
+  const int lid = xcd_remap(blockIdx.x, G);
+  if (lid >= ntiles) return;
+  const int nkb = p.K / BK;
+  const int nblocks = ((ntiles - lid + G - 1) / G) * nkb;   // this workgroup's K blocks, all tiles
+
+  // biases into LDS once (before any DMA: these plain loads are waited for here, nothing else
+  // is in flight yet)
+  for (int c = tid; c < BIAS_FLOATS; c += 64 * NW) sbias[c] = (p.bias && c < p.Cout) ? p.bias[c] : 0.f;
+  __syncthreads();
+
+  const int lrow = wave * RPW + lane / PPR;
+  const int lp = (lane & 7) ^ (lane >> 3);
+  const int HoWo = p.Ho * p.Wo;
+  const __amdgpu_buffer_rsrc_t rx = wide_rsrc(p.x);
+  const __amdgpu_buffer_rsrc_t rw = wide_rsrc(p.w);
+  const __amdgpu_buffer_rsrc_t rx2 = wide_rsrc(p.x2 ? p.x2 : p.x);
+  const __amdgpu_buffer_rsrc_t ry = wide_rsrc(p.y);
+
+  // ---- issue side: the tile whose blocks are being DMA'd (runs up to D blocks ahead) ----
+  int it = lid, ikb = 0;
+  int a_base[APT];
+  uint32_t a_mask[APT], a2_off[APT], b_off[BPT], a_off[APT];
+  int cur_tap = -1, iss_tap = 0, iss_c = 0, iss_r = 0, iss_s = 0;
+  const int K1 = p.x2 ? p.K1 : p.K;
+  auto setup_issue = [&](int t) {
+    const int m0 = (t / ntn) * BM, n0 = (t % ntn) * BN;
+#pragma unroll
+    for (int i = 0; i < APT; ++i) {
+      const int m = m0 + lrow + RPI * i;
+      a_mask[i] = 0u;
+      a_base[i] = 0;
+      a2_off[i] = kWideOOB;
+      a_off[i] = kWideOOB;
+      if (m < p.M) {
+        const int img = fdiv(m, p.mHoWo, p.lHoWo);
+        const int rem = m - img * HoWo;
+        const int oh = fdiv(rem, p.mWo, p.lWo);
+        const int ow = rem - oh * p.Wo;
+        const int ih0 = oh * p.stride - p.pad, iw0 = ow * p.stride - p.pad;
+        a_base[i] = (((img * p.H + ih0) * p.W + iw0) * p.C + lp * 8) * 2;
+        const int r_lo = max(0, -ih0), r_hi = min(p.R, p.H - ih0);
+        const int s_lo = max(0, -iw0), s_hi = min(p.S, p.W - iw0);
+        const uint32_t mr = r_hi > r_lo ? ((1u << r_hi) - 1u) & ~((1u << r_lo) - 1u) : 0u;
+        const uint32_t ms = s_hi > s_lo ? ((1u << s_hi) - 1u) & ~((1u << s_lo) - 1u) : 0u;
+        a_mask[i] = mr | (ms << 16);
+        a2_off[i] = (uint32_t)((((img * p.H2 + oh * p.stride2) * p.W2 + ow * p.stride2) * p.C2 + lp * 8) * 2);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      const int n = n0 + lrow + RPI * i;
+      b_off[i] = n < p.Cout ? (uint32_t)(((long)n * p.K + lp * 8) * 2) : kWideOOB;
+    }
+    cur_tap = -1;
+    iss_tap = iss_c = iss_r = iss_s = 0;
+  };
+  // DMA of block ikb of tile it into ring slot SLOT, then advance (to the next tile after its last)
+  auto issue_next = [&](auto slot_tag) {
+    constexpr int SLOT = decltype(slot_tag)::value;
+    if (it >= ntiles) return;
+    bf16_t* Xs = ring + SLOT * STAGE_ELEMS;
+    bf16_t* Ws = Xs + BM * BK;
+    const int k0 = ikb * BK;
+    const uint32_t sb = (uint32_t)(k0 * 2);
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) wide_dma16(rw, b_off[i], sb, Ws + (i * RPI + wave * RPW) * BK);
+    if (k0 >= K1) {
+      const uint32_t soff = (uint32_t)((k0 - K1) * 2);
+#pragma unroll
+      for (int i = 0; i < APT; ++i) wide_dma16(rx2, a2_off[i], soff, Xs + (i * RPI + wave * RPW) * BK);
+    } else {
+      if (iss_tap != cur_tap) {
+        cur_tap = iss_tap;
+        const int tap_off = ((iss_r * p.W + iss_s) * p.C) * 2;
+        const uint32_t bit = (1u << iss_r) | (1u << (iss_s + 16));
+#pragma unroll
+        for (int i = 0; i < APT; ++i)
+          a_off[i] = (a_mask[i] & bit) == bit ? (uint32_t)(a_base[i] + tap_off) : kWideOOB;
+      }
+      const uint32_t soff = (uint32_t)(iss_c * 2);
+#pragma unroll
+      for (int i = 0; i < APT; ++i) wide_dma16(rx, a_off[i], soff, Xs + (i * RPI + wave * RPW) * BK);
+      iss_c += BK;
+      if (iss_c >= p.Cc) {
+        iss_c = 0;
+        ++iss_tap;
+        if (++iss_s == p.S) {
+          iss_s = 0;
+          ++iss_r;
+        }
+      }
+    }
+    if (++ikb == nkb) {
+      ikb = 0;
+      it += G;
+      if (it < ntiles) setup_issue(it);
+    }
+  };
+
+  // ---- compute side ----
+  const int fr = lane & 15, fq = lane >> 4;
+  const int coff = ((fq & 1) << 4) | ((fq >> 1) << 3);
+  const int sw = fr & 7;
+  int w_rd[NI], x_rd[MI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) w_rd[j] = BM * BK + (wc * WN + j * 16 + fr) * BK;
+#pragma unroll
+  for (int i = 0; i < MI; ++i) x_rd[i] = (wr * WM + i * 16 + fr) * BK;
+  f32x4 acc[NI][MI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j)
+#pragma unroll
+    for (int i = 0; i < MI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](auto slot_tag) {
+    constexpr int SLOT = decltype(slot_tag)::value;
+    const bf16_t* St = ring + SLOT * STAGE_ELEMS;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int pc = ((fq + 4 * kk) ^ sw) << 3;
+      bf16x8 wf[NI], xf[MI];
+#pragma unroll
+      for (int j = 0; j < NI; ++j) wf[j] = *reinterpret_cast<const bf16x8*>(St + w_rd[j] + pc);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) xf[i] = *reinterpret_cast<const bf16x8*>(St + x_rd[i] + pc);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
+    }
+  };
+  const int act = p.act & 15;
+  // epilogue of tile t: NST buffer stores per thread, always issued (out-of-range offset masks)
+  auto epilogue = [&](int t) {
+    const int m0 = (t / ntn) * BM, n0 = (t % ntn) * BN;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = m0 + wr * WM + i * 16 + fr;
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        f32x4 lo = acc[2 * q][i], hi = acc[2 * q + 1][i];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto s2 = __builtin_amdgcn_permlane16_swap(__float_as_uint(lo[e]), __float_as_uint(hi[e]), false, false);
+          lo[e] = __uint_as_float(s2[0]);
+          hi[e] = __uint_as_float(s2[1]);
+        }
+        const int n = n0 + wc * WN + q * 32 + coff;
+        const bool ok = m < p.M && n < p.Cout;
+        const f32x4 b0 = *reinterpret_cast<const f32x4*>(sbias + (ok ? n : 0));
+        const f32x4 b1 = *reinterpret_cast<const f32x4*>(sbias + (ok ? n : 0) + 4);
+        float v[8] = {lo[0] + b0[0], lo[1] + b0[1], lo[2] + b0[2], lo[3] + b0[3],
+                      hi[0] + b1[0], hi[1] + b1[1], hi[2] + b1[2], hi[3] + b1[3]};
+        if (act == 1) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+        } else if (act == 2) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = silu(v[e]);
+        } else if (act == 3) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+        }
+        u32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = pack2(v[2 * e], v[2 * e + 1]);
+        const uint32_t off = ok ? (uint32_t)(((size_t)m * p.ldy + n) * 2) : kWideOOB;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), ry, off, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int i = 0; i < MI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  setup_issue(it);
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  using S2 = std::integral_constant<int, 2>;
+  issue_next(S0{});
+  if constexpr (NS == 3) issue_next(S1{});
+  int ct = lid, ckb = 0;
+  bool epi_prev = false;                        // the previous step ended a tile (NST stores)
+  bool epi_prev2 = false;                       // ... the step before it (NS == 3)
+  // step for global block g: wait for it, publish, issue block g + D, compute, maybe epilogue
+  auto step = [&](int g, auto slot_tag) {
+    constexpr int SLOT = decltype(slot_tag)::value;
+    constexpr int PREV = SLOT == 0 ? NS - 1 : SLOT - 1;
+    // younger VMEM ops than block g: the D - 1 blocks issued after it (if any) and the stores
+    // of an epilogue that ran after its issue; counting fewer is only stricter
+    if constexpr (D == 1) {
+      if (epi_prev) wide_vm_barrier<NST>();
+      else wide_vm_barrier<0>();
+    } else {
+      const bool more = g + 1 < nblocks;        // block g + 1 was issued (at step g - 1)
+      const bool epi = epi_prev || epi_prev2;
+      if (more && epi) wide_vm_barrier<PER + NST>();
+      else if (more) wide_vm_barrier<PER>();
+      else if (epi) wide_vm_barrier<NST>();
+      else wide_vm_barrier<0>();
+    }
+    issue_next(std::integral_constant<int, PREV>{});
+    compute(slot_tag);
+    epi_prev2 = epi_prev;
+    epi_prev = false;
+    if (++ckb == nkb) {
+      epilogue(ct);
+      ct += G;
+      ckb = 0;
+      epi_prev = true;
+    }
+  };
+  int g = 0;
+  if constexpr (NS == 2) {
+    for (; g + 2 <= nblocks; g += 2) {
+      step(g, S0{});
+      step(g + 1, S1{});
+    }
+    if (g < nblocks) step(g, S0{});
+  } else {
+    for (; g + 3 <= nblocks; g += 3) {
+      step(g, S0{});
+      step(g + 1, S1{});
+      step(g + 2, S2{});
+    }
+    if (g < nblocks) step(g, S0{});
+    if (g + 1 < nblocks) step(g + 1, S1{});
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 }  // namespace aiko
 
 // Same arguments as aiko_conv_buf (no occupancy / MFMA-shape options).  Host preconditions
@@ -438,6 +709,23 @@ extern "C" int aiko_conv_wide(const void* x, const void* w, const float* bias, c
       conv_wide_kernel<256, 192, 8, 1, 2, true, 1, 64, 144><<<grid, 512, 0, stream>>>(p);
     else if (bm == 128 && bn == 144)  // 8 waves of 16 x 144, 2 workgroups per CU (64 + 64 KB ring)
       conv_wide_kernel<128, 192, 8, 1, 2, true, 1, 64, 144><<<grid, 512, 0, stream>>>(p);
+    else
+      return -1;
+  } else if (occ == 20) {             // persistent walk, residual-free layers (host checks)
+    if (res != nullptr || Cout > 2048) return -1;
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    const char* cap = getenv("AIKO_CONV_PERS_GRID");   // tests: force several tiles per workgroup
+    if (cap && atoi(cap) > 0) cus = atoi(cap);
+    const int ntiles = (int)grid.x;
+    dim3 pg(ntiles < cus ? ntiles : cus);
+    if (bm == 256 && bn == 256)
+      conv_wide_pers_kernel<256, 256, 2, 4, 2><<<pg, 512, 0, stream>>>(p);
+    else if (bm == 256 && bn == 128)
+      conv_wide_pers_kernel<256, 128, 4, 2, 3><<<pg, 512, 0, stream>>>(p);
+    else if (bm == 128 && bn == 256)
+      conv_wide_pers_kernel<128, 256, 2, 4, 3><<<pg, 512, 0, stream>>>(p);
     else
       return -1;
   } else if (occ == 19) {             // 4 waves of 64 x 64 (half the fragment reads per MFMA of

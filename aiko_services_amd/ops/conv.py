@@ -265,6 +265,10 @@ WIDE8_TILES = ((256, 256), (256, 128), (128, 256), (256, 64), (128, 128))
 # 64 x 128 (128 x 256, one per CU): half / a third fewer fragment reads per MFMA than the 8-wave
 # 128-wide forms, whose 64 x 32 wave tiles read 0.75 fragments per MFMA
 WIDE4_OCC_TILES = ((128, 128), (128, 256))
+# variant 20: persistent conv_wide (one workgroup per CU walks tiles with ONE K-block ring across
+# tile boundaries; epilogue stores always issued, so the next tile's first-block wait is exact)
+# for the short-K layers without a residual (reductions, projections)
+WIDE_PERS_TILES = ((256, 256), (256, 128), (128, 256))
 # variant 18: the same kernel with an exact-N tile (the MFMAs and epilogue cover exactly
 # these channel counts — the YOLO head's 80-class and 64 + 80 box/class convs — instead of
 # rounding N up to a 128 / 192 tile; odd 16-channel block counts end in an 8-byte store)
@@ -465,6 +469,8 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, p
             cands += [t + (5,) for t in MF32_TILES]
             cands += [t + (8,) for t in WIDE8_TILES] + [t + (9,) for t in WIDE_OCC_TILES]
             cands += [t + (19,) for t in WIDE4_OCC_TILES]
+            if not has_res and cout <= 2048:
+                cands += [t + (20,) for t in WIDE_PERS_TILES]
             if cout in EXACT_N:
                 cands += [(256, cout, 18), (128, cout, 18)]
             # variants 6 and 11 were never the tuner's pick on any layer measured (rounds 3-4):

@@ -27,6 +27,8 @@ LAYERS = {
     "b8.conv3": (256, 1024, 1, 1, 14, True, 0),
     "b14.conv3": (512, 2048, 1, 1, 7, True, 0),
     "b14.conv2": (512, 512, 3, 1, 7, False, 0),
+    "b9.conv1": (1024, 256, 1, 1, 14, False, 0),       # stage-3 reduction
+    "b3.conv3f": (128, 512, 1, 1, 28, False, 256),     # stage-2 fused projection (K = 128 + 256)
     "b13.conv1": (1024, 512, 1, 1, 14, False, 0),
     "gemm4k": (4096, 4096, 1, 1, 16, False, 0),       # M = 256*16*16 = 65536: main-loop ceiling
     "gemm4k_3x3": (512, 4096, 3, 1, 16, False, 0),

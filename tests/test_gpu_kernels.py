@@ -161,12 +161,22 @@ def _nhwc(x_nchw):
     (1, 13, 9, 192, 72, 3, 2, 1, "gelu", True, (128, 128, 19)),
     (3, 14, 14, 256, 512, 1, 1, 0, None, False, (128, 256, 19)),
     (1, 9, 11, 128, 200, 3, 1, 1, "silu", True, (128, 256, 19)),
+    # variant 20: persistent walk (no residual) — K from 1 to 36 blocks, 3x3 / strided / dual
+    # source below; several tiles per workgroup via AIKO_CONV_PERS_GRID in the test
+    (2, 28, 28, 128, 256, 3, 1, 1, "relu", False, (256, 256, 20)),
+    (3, 14, 14, 1024, 256, 1, 1, 0, "relu", False, (256, 256, 20)),
+    (5, 14, 14, 256, 512, 1, 1, 0, None, False, (256, 128, 20)),
+    (1, 13, 9, 192, 72, 3, 2, 1, "gelu", False, (256, 128, 20)),
+    (4, 14, 14, 64, 1024, 1, 1, 0, "silu", False, (128, 256, 20)),
+    (2, 7, 7, 512, 512, 3, 1, 1, "relu", False, (128, 256, 20)),
     # variant 14: the resident kernels with each tile's residual issued at its own tile
     (64, 28, 28, 128, 512, 1, 1, 0, "relu", True, (64, 128, 14)),
     (65, 14, 14, 256, 1024, 1, 1, 0, "relu", True, (64, 128, 14)),
     (64, 7, 7, 512, 2048, 1, 1, 0, "relu", True, (64, 128, 14)),
 ])
-def test_conv_igemm_matches_torch(native, B, H, W, cin, cout, k, stride, pad, act, res, tile):
+def test_conv_igemm_matches_torch(native, B, H, W, cin, cout, k, stride, pad, act, res, tile, monkeypatch):
+    if len(tile) > 2 and tile[2] == 20:
+        monkeypatch.setenv("AIKO_CONV_PERS_GRID", "3")    # 3 workgroups: many tiles each, odd tails
     from aiko_services_amd.ops import conv as C
     from aiko_services_amd.ops import reference as R
     g = torch.Generator().manual_seed(1234)
@@ -486,11 +496,13 @@ def test_resnet50_matches_fp32_reference(native):
     assert (i[:, 0].long() == lg.argmax(1)).all()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 8, 11])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 8, 11, 20])
 @pytest.mark.parametrize("B,H,cin_main,cin_sc,cout,stride", [(2, 28, 64, 64, 256, 1), (2, 28, 128, 256, 512, 2),
                                                               (1, 14, 512, 1024, 2048, 2)])
-def test_fused_projection_shortcut(native, B, H, cin_main, cin_sc, cout, stride, variant):
+def test_fused_projection_shortcut(native, B, H, cin_main, cin_sc, cout, stride, variant, monkeypatch):
     """conv3(t) + down(x) (+bias, ReLU) as one K-concatenated igemm with two A sources."""
+    if variant == 20:
+        monkeypatch.setenv("AIKO_CONV_PERS_GRID", "5")    # persistent walk over several tiles
     from aiko_services_amd.ops import conv as C
     from aiko_services_amd.ops import reference as R
     g = torch.Generator().manual_seed(21)
@@ -503,7 +515,7 @@ def test_fused_projection_shortcut(native, B, H, cin_main, cin_sc, cout, stride,
     fused = C.fuse_shortcut(main, down)
     t = torch.randn(B, Ho, Ho, cin_main, generator=g).to(torch.bfloat16).to(DEV)
     x = torch.randn(B, H, H, cin_sc, generator=g).to(torch.bfloat16).to(DEV)
-    y = C.conv2d(t, fused, x2=x, tile=(256, 128, variant) if variant in (8, 11) else (64, 128, variant))
+    y = C.conv2d(t, fused, x2=x, tile=(256, 128, variant) if variant in (8, 11, 20) else (64, 128, variant))
     torch.cuda.synchronize()
     idn = R.conv_ref(x.permute(0, 3, 1, 2).float(), down)
     ref = R.conv_ref(t.permute(0, 3, 1, 2).float(), main, idn)
