@@ -417,7 +417,10 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCC) void conv_wide_kernel(ConvPara
 // tile's NST stores (plus the blocks issued after it) — is an exact counted vmcnt, never a
 // drain.  Biases are read from LDS (staged once), so no VGPR-destination global load is ever
 // waited on while DMAs are in flight.
-template <int BM, int BN, int WGM, int WGN, int NS>
+// RES: a residual added in the epilogue — each tile's residual chunks are buffer-loaded into
+// registers D + 1 steps before its epilogue (after that step's wait, before its DMA issue), so
+// they have D + 1 blocks of compute to land.
+template <int BM, int BN, int WGM, int WGN, int NS, bool RES = false>
 __global__ __launch_bounds__(64 * WGM * WGN, 1) void conv_wide_pers_kernel(ConvParams p) {
   constexpr int BK = 64, PPR = 8;
   constexpr int NW = WGM * WGN;
@@ -460,6 +463,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void conv_wide_pers_kernel(ConvP
   const __amdgpu_buffer_rsrc_t rw = wide_rsrc(p.w);
   const __amdgpu_buffer_rsrc_t rx2 = wide_rsrc(p.x2 ? p.x2 : p.x);
   const __amdgpu_buffer_rsrc_t ry = wide_rsrc(p.y);
+  const __amdgpu_buffer_rsrc_t rr = wide_rsrc(p.res ? p.res : p.y);
 
   // ---- issue side: the tile whose blocks are being DMA'd (runs up to D blocks ahead) ----
   int it = lid, ikb = 0;
@@ -467,7 +471,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void conv_wide_pers_kernel(ConvP
   uint32_t a_mask[APT], a2_off[APT], b_off[BPT], a_off[APT];
   int cur_tap = -1, iss_tap = 0, iss_c = 0, iss_r = 0, iss_s = 0;
   const int K1 = p.x2 ? p.K1 : p.K;
-  auto setup_issue = [&](int t) {
+  auto setup_issue = [&](int t) __attribute__((always_inline)) {
     const int m0 = (t / ntn) * BM, n0 = (t % ntn) * BN;
 #pragma unroll
     for (int i = 0; i < APT; ++i) {
@@ -500,7 +504,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void conv_wide_pers_kernel(ConvP
     iss_tap = iss_c = iss_r = iss_s = 0;
   };
   // DMA of block ikb of tile it into ring slot SLOT, then advance (to the next tile after its last)
-  auto issue_next = [&](auto slot_tag) {
+  auto issue_next = [&](auto slot_tag) __attribute__((always_inline)) {
     constexpr int SLOT = decltype(slot_tag)::value;
     if (it >= ntiles) return;
     bf16_t* Xs = ring + SLOT * STAGE_ELEMS;
@@ -556,7 +560,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void conv_wide_pers_kernel(ConvP
   for (int j = 0; j < NI; ++j)
 #pragma unroll
     for (int i = 0; i < MI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto compute = [&](auto slot_tag) {
+  auto compute = [&](auto slot_tag) __attribute__((always_inline)) {
     constexpr int SLOT = decltype(slot_tag)::value;
     const bf16_t* St = ring + SLOT * STAGE_ELEMS;
 #pragma unroll
@@ -575,8 +579,21 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void conv_wide_pers_kernel(ConvP
     }
   };
   const int act = p.act & 15;
+  const bool post = (p.act & 16) != 0;
+  u32x4 e_res[RES ? MI : 1][RES ? NP : 1];
+  auto load_res = [&](int t) __attribute__((always_inline)) {                  // tile t's residual chunks -> registers
+    const int m0 = (t / ntn) * BM, n0 = (t % ntn) * BN;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        const int m = m0 + wr * WM + i * 16 + fr, n = n0 + wc * WN + q * 32 + coff;
+        const uint32_t off = (m < p.M && n < p.Cout) ? (uint32_t)(((size_t)m * p.ldr + n) * 2) : kWideOOB;
+        e_res[i][q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0));
+      }
+  };
   // epilogue of tile t: NST buffer stores per thread, always issued (out-of-range offset masks)
-  auto epilogue = [&](int t) {
+  auto epilogue = [&](int t) __attribute__((always_inline)) {
     const int m0 = (t / ntn) * BM, n0 = (t % ntn) * BN;
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
@@ -596,6 +613,15 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void conv_wide_pers_kernel(ConvP
         const f32x4 b1 = *reinterpret_cast<const f32x4*>(sbias + (ok ? n : 0) + 4);
         float v[8] = {lo[0] + b0[0], lo[1] + b0[1], lo[2] + b0[2], lo[3] + b0[3],
                       hi[0] + b1[0], hi[1] + b1[1], hi[2] + b1[2], hi[3] + b1[3]};
+        if constexpr (RES) {
+          if (!post) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[2 * e] += __uint_as_float(e_res[i][q][e] << 16);
+              v[2 * e + 1] += __uint_as_float(e_res[i][q][e] & 0xffff0000u);
+            }
+          }
+        }
         if (act == 1) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
@@ -605,6 +631,15 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void conv_wide_pers_kernel(ConvP
         } else if (act == 3) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+        }
+        if constexpr (RES) {
+          if (post) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[2 * e] += __uint_as_float(e_res[i][q][e] << 16);
+              v[2 * e + 1] += __uint_as_float(e_res[i][q][e] & 0xffff0000u);
+            }
+          }
         }
         u32x4 o;
 #pragma unroll
@@ -629,7 +664,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void conv_wide_pers_kernel(ConvP
   bool epi_prev = false;                        // the previous step ended a tile (NST stores)
   bool epi_prev2 = false;                       // ... the step before it (NS == 3)
   // step for global block g: wait for it, publish, issue block g + D, compute, maybe epilogue
-  auto step = [&](int g, auto slot_tag) {
+  auto step = [&](int g, auto slot_tag) __attribute__((always_inline)) {
     constexpr int SLOT = decltype(slot_tag)::value;
     constexpr int PREV = SLOT == 0 ? NS - 1 : SLOT - 1;
     // younger VMEM ops than block g: the D - 1 blocks issued after it (if any) and the stores
@@ -644,6 +679,10 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void conv_wide_pers_kernel(ConvP
       else if (more) wide_vm_barrier<PER>();
       else if (epi) wide_vm_barrier<NST>();
       else wide_vm_barrier<0>();
+    }
+    if constexpr (RES) {
+      // (nkb >= D + 1, host check) the residual of tile ct, D + 1 blocks before its epilogue
+      if (ckb == nkb - 1 - D) load_res(ct);
     }
     issue_next(std::integral_constant<int, PREV>{});
     compute(slot_tag);
@@ -711,8 +750,8 @@ extern "C" int aiko_conv_wide(const void* x, const void* w, const float* bias, c
       conv_wide_kernel<128, 192, 8, 1, 2, true, 1, 64, 144><<<grid, 512, 0, stream>>>(p);
     else
       return -1;
-  } else if (occ == 20) {             // persistent walk, residual-free layers (host checks)
-    if (res != nullptr || Cout > 2048) return -1;
+  } else if (occ == 20) {             // persistent walk (host checks: K >= 3 blocks with a residual)
+    if (Cout > 2048 || (res != nullptr && K < 192)) return -1;
     int dev = 0, cus = 0;
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
@@ -720,12 +759,17 @@ extern "C" int aiko_conv_wide(const void* x, const void* w, const float* bias, c
     if (cap && atoi(cap) > 0) cus = atoi(cap);
     const int ntiles = (int)grid.x;
     dim3 pg(ntiles < cus ? ntiles : cus);
-    if (bm == 256 && bn == 256)
+    const bool r = res != nullptr;
+    if (bm == 256 && bn == 256 && !r)
       conv_wide_pers_kernel<256, 256, 2, 4, 2><<<pg, 512, 0, stream>>>(p);
-    else if (bm == 256 && bn == 128)
+    else if (bm == 256 && bn == 128 && !r)
       conv_wide_pers_kernel<256, 128, 4, 2, 3><<<pg, 512, 0, stream>>>(p);
-    else if (bm == 128 && bn == 256)
+    else if (bm == 128 && bn == 256 && !r)
       conv_wide_pers_kernel<128, 256, 2, 4, 3><<<pg, 512, 0, stream>>>(p);
+    else if (bm == 256 && bn == 128)
+      conv_wide_pers_kernel<256, 128, 4, 2, 3, true><<<pg, 512, 0, stream>>>(p);
+    else if (bm == 128 && bn == 256)
+      conv_wide_pers_kernel<128, 256, 2, 4, 3, true><<<pg, 512, 0, stream>>>(p);
     else
       return -1;
   } else if (occ == 19) {             // 4 waves of 64 x 64 (half the fragment reads per MFMA of

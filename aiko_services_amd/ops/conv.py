@@ -469,8 +469,10 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, p
             cands += [t + (5,) for t in MF32_TILES]
             cands += [t + (8,) for t in WIDE8_TILES] + [t + (9,) for t in WIDE_OCC_TILES]
             cands += [t + (19,) for t in WIDE4_OCC_TILES]
-            if not has_res and cout <= 2048:
+            if cout <= 2048 and not has_res:
                 cands += [t + (20,) for t in WIDE_PERS_TILES]
+            elif cout <= 2048 and key[2] >= 192:     # with a residual: the 3-slot forms
+                cands += [t + (20,) for t in WIDE_PERS_TILES if t != (256, 256)]
             if cout in EXACT_N:
                 cands += [(256, cout, 18), (128, cout, 18)]
             # variants 6 and 11 were never the tuner's pick on any layer measured (rounds 3-4):

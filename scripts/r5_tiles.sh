@@ -12,3 +12,8 @@ for L in b13.conv1 b9.conv1 b3.conv3f; do
     echo -n "$L $t: "; timeout -k 10 120 python scripts/layer_bench.py --layers $L --batch 320 --tile $t --iters 20 2>&1 | grep -o "best.*" || echo fail
   done
 done
+for L in b14.conv3 b8.conv3; do
+  for t in 256,256,8 64,128,13 256,128,20 128,256,20; do
+    echo -n "$L $t: "; timeout -k 10 120 python scripts/layer_bench.py --layers $L --batch 320 --tile $t --iters 20 2>&1 | grep -o "best.*" || echo fail
+  done
+done

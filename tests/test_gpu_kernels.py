@@ -169,6 +169,10 @@ def _nhwc(x_nchw):
     (1, 13, 9, 192, 72, 3, 2, 1, "gelu", False, (256, 128, 20)),
     (4, 14, 14, 64, 1024, 1, 1, 0, "silu", False, (128, 256, 20)),
     (2, 7, 7, 512, 512, 3, 1, 1, "relu", False, (128, 256, 20)),
+    # ... with a residual (3-slot forms, residual loaded D + 1 blocks ahead of each epilogue)
+    (3, 14, 14, 256, 1024, 1, 1, 0, None, True, (256, 128, 20)),
+    (2, 7, 7, 512, 2048, 1, 1, 0, "relu", True, (128, 256, 20)),
+    (1, 13, 9, 192, 72, 3, 2, 1, "gelu", True, (256, 128, 20)),
     # variant 14: the resident kernels with each tile's residual issued at its own tile
     (64, 28, 28, 128, 512, 1, 1, 0, "relu", True, (64, 128, 14)),
     (65, 14, 14, 256, 1024, 1, 1, 0, "relu", True, (64, 128, 14)),
