@@ -263,11 +263,17 @@ WIDE4_TILES = ((256, 128), (128, 256))
 WIDE8_TILES = ((256, 256), (256, 128), (128, 256), (256, 64), (128, 128))
 # variant 19: the same kernel with 4 waves of 64 x 64 (128 x 128 tile, 2 workgroups per CU) or
 # 64 x 128 (128 x 256, one per CU): half / a third fewer fragment reads per MFMA than the 8-wave
-# 128-wide forms, whose 64 x 32 wave tiles read 0.75 fragments per MFMA
+# 128-wide forms, whose 64 x 32 wave tiles read 0.75 fragments per MFMA.  Measured at B=320
+# (round 5, scripts/r5_tiles.sh): stage-2 3x3 84.4 vs 81.2 us (variant 9), stage-3 3x3 79.9 vs
+# 66.0 us (variant 8) — the fragment traffic was not the limit; opt-in (AIKO_CONV_EXTRA=19)
 WIDE4_OCC_TILES = ((128, 128), (128, 256))
 # variant 20: persistent conv_wide (one workgroup per CU walks tiles with ONE K-block ring across
 # tile boundaries; epilogue stores always issued, so the next tile's first-block wait is exact)
-# for the short-K layers without a residual (reductions, projections)
+# for the short-K layers without a residual (reductions, projections).  Measured at B=320 (round
+# 5): fused stage-2 projection 159.6 vs 163.6 us (variant 8), stage-3 reduction 37.4 vs 36.1,
+# stage-3 -> 4 reduction 70.6 vs 66.1 — the tile-boundary fill was not the limit either; the
+# tuner keeps it where it wins.  The residual form (expansions) is opt-in (AIKO_CONV_EXTRA=20):
+# 60-61 vs 49.7 us (stage 4), 87.6 vs 76.7 us (stage 3, resident-weight kernel)
 WIDE_PERS_TILES = ((256, 256), (256, 128), (128, 256))
 # variant 18: the same kernel with an exact-N tile (the MFMAs and epilogue cover exactly
 # these channel counts — the YOLO head's 80-class and 64 + 80 box/class convs — instead of
@@ -468,10 +474,11 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, p
             cands += [t + (4,) for t in PERSIST_TILES]
             cands += [t + (5,) for t in MF32_TILES]
             cands += [t + (8,) for t in WIDE8_TILES] + [t + (9,) for t in WIDE_OCC_TILES]
-            cands += [t + (19,) for t in WIDE4_OCC_TILES]
+            if 19 in _EXTRA:
+                cands += [t + (19,) for t in WIDE4_OCC_TILES]
             if cout <= 2048 and not has_res:
                 cands += [t + (20,) for t in WIDE_PERS_TILES]
-            elif cout <= 2048 and key[2] >= 192:     # with a residual: the 3-slot forms
+            elif cout <= 2048 and key[2] >= 192 and 20 in _EXTRA:   # with a residual: 3-slot forms
                 cands += [t + (20,) for t in WIDE_PERS_TILES if t != (256, 256)]
             if cout in EXACT_N:
                 cands += [(256, cout, 18), (128, cout, 18)]

@@ -179,7 +179,7 @@ def _nhwc(x_nchw):
     (64, 7, 7, 512, 2048, 1, 1, 0, "relu", True, (64, 128, 14)),
 ])
 def test_conv_igemm_matches_torch(native, B, H, W, cin, cout, k, stride, pad, act, res, tile, monkeypatch):
-    if len(tile) > 2 and tile[2] == 20:
+    if tile is not None and len(tile) > 2 and tile[2] == 20:
         monkeypatch.setenv("AIKO_CONV_PERS_GRID", "3")    # 3 workgroups: many tiles each, odd tails
     from aiko_services_amd.ops import conv as C
     from aiko_services_amd.ops import reference as R
