@@ -56,6 +56,7 @@
 // row's DMAs — the stores are inline asm too, so the count is exact and the compiler inserts no
 // vmcnt(0) drains of its own).
 #include <cstdlib>
+#include <type_traits>
 
 #include "conv_common.h"
 
@@ -313,13 +314,17 @@ __global__ __launch_bounds__(64 * kBnNW, 1) void bneck_fused_kernel(BnParams p) 
     }
   };
 
-  // conv2 of the output row centred on virtual row vc: t1 slots of vc - 1, vc, vc + 1 -> t2
-  auto conv2 = [&](int vc) {
+  // conv2 of the output row centred on virtual row vc: t1 slots of vc - 1, vc, vc + 1 -> t2.
+  // k-steps [KB, KE) only, into a2n (ks 0 .. 11 are the taps of rows vc - 1 and vc, 12 .. 17 those
+  // of row vc + 1): the split schedule runs the first part for the NEXT row inside phase B, whose
+  // MFMA pipe the stores / packing of conv3 leave half idle, and only the last taps in phase A
+  f32x4 a2n[kBnTPW];
+  auto conv2_part = [&](int vc, auto kb, auto ke) __attribute__((always_inline)) {
+    constexpr int KB = decltype(kb)::value, KE = decltype(ke)::value;
     const unsigned char* tr[3] = {t1r + ((vc - 1) % 3) * kBnTB + tlb, t1r + (vc % 3) * kBnTB + tlb,
                                   t1r + ((vc + 1) % 3) * kBnTB + tlb};
-    f32x4 a2[kBnTPW];
 #pragma unroll
-    for (int ks = 0; ks < KS2; ++ks) {
+    for (int ks = KB; ks < KE; ++ks) {
       const int tap = ks >> 1, dy = tap / 3, dx = tap % 3 - 1, hk = ks & 1;
       bf16x8 bf[kBnTPW];
 #pragma unroll
@@ -327,16 +332,21 @@ __global__ __launch_bounds__(64 * kBnNW, 1) void bneck_fused_kernel(BnParams p) 
         bf[t] = *reinterpret_cast<const bf16x8*>(tr[dy] + (1 + 256 * hk + 16 * t + dx) * 16);
 #pragma unroll
       for (int t = 0; t < kBnTPW; ++t)
-        a2[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f[ks], bf[t], ks == 0 ? bias2 : a2[t], 0, 0, 0);
+        a2n[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f[ks], bf[t], ks == 0 ? bias2 : a2n[t], 0, 0, 0);
     }
-    bn_pipeline<KS2, kBnTPW, 4>();
+    bn_pipeline<KE - KB, kBnTPW, 4>();
+  };
+  auto conv2_store = [&]() __attribute__((always_inline)) {
     unsigned char* t2w = t2b + twb;
 #pragma unroll
     for (int t = 0; t < kBnTPW; ++t) {
-      const uint2 pk{bn_relu2(pack2(a2[t][0], a2[t][1])), bn_relu2(pack2(a2[t][2], a2[t][3]))};
+      const uint2 pk{bn_relu2(pack2(a2n[t][0], a2n[t][1])), bn_relu2(pack2(a2n[t][2], a2n[t][3]))};
       *reinterpret_cast<uint2*>(t2w + (1 + 16 * t) * 16) = pk;
     }
   };
+  using KB0 = std::integral_constant<int, 0>;
+  using KBS = std::integral_constant<int, 12>;
+  using KBE = std::integral_constant<int, KS2>;
 
   // conv3 (+ residual / projection of x row vc) -> y row (n, r), centred on virtual row vc
   auto conv3 = [&](int vc, int n, int r) {
@@ -403,6 +413,7 @@ __global__ __launch_bounds__(64 * kBnNW, 1) void bneck_fused_kernel(BnParams p) 
   int n = n0, r = h0, vc = h0 + 1;
   const bool stamps = p.dbg != nullptr && wv == 0;
   unsigned st[8];
+  bool pre = false;                                // a2n holds this row's first conv2 taps
   auto stamp = [&](int i) {
     if (stamps) st[i] = (unsigned)__builtin_amdgcn_s_memtime();
   };
@@ -427,12 +438,20 @@ __global__ __launch_bounds__(64 * kBnNW, 1) void bneck_fused_kernel(BnParams p) 
       conv1(vc + 1);
       bn_barrier();
     }
-    if (!(p.mode & 1)) conv2(vc);
+    if (!(p.mode & 1)) {
+      if (pre) conv2_part(vc, KBS{}, KBE{});       // rows vc - 1, vc were done in the last phase B
+      else conv2_part(vc, KB0{}, KBE{});
+      conv2_store();
+    }
     stamp(2);
     if (!(p.mode & 8) && vc + 2 <= vlast) wait_row(vc + 2);
     stamp(3);
     if (!(p.mode & 16)) bn_barrier();
     stamp(4);
+    // split schedule: the next output row's first conv2 taps (t1 rows vc, vc + 1, both complete;
+    // conv1 below writes the slot of vc - 1) when it is in the same image
+    const bool split = (p.mode & 3072) && j + 1 < nrows && r + 1 < H;
+    if (split && (p.mode & 2048)) conv2_part(vc + 1, KB0{}, KBS{});
     if (p.mode & 512) {                            // A/B: conv3 (and its stores) first
       if (!(p.mode & 4)) conv3(vc, n, r);
       stamp(5);
@@ -442,6 +461,8 @@ __global__ __launch_bounds__(64 * kBnNW, 1) void bneck_fused_kernel(BnParams p) 
       stamp(5);
       if (!(p.mode & 4)) conv3(vc, n, r);
     }
+    if (split && !(p.mode & 2048)) conv2_part(vc + 1, KB0{}, KBS{});
+    pre = split;
     stamp(6);
     if (!(p.mode & 16)) bn_barrier();
     stamp(7);
