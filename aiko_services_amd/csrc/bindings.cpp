@@ -75,6 +75,12 @@ int aiko_gemm_fp8(const void* a, const void* b, const float* sa, const float* sb
                   hipStream_t stream);
 int aiko_rownorm_quant(const void* x, int ldx, const float* gamma, const float* beta, float eps,
                        void* yb, int ldyb, void* q, int ldq, float* qs, int M, int D, hipStream_t stream);
+int aiko_gemm_fp8_ln(const void* a, const void* b, const float* sb, const float* bias, const void* res, void* y, int M,
+                     int N, int K, int lda, int ldy, int ldr, int act, const void* zero, const void* amx, int mxr,
+                     void* yq, void* ysc, int ldq, int ysr, float* st, const float* cs, int sts, int stp, int ln_d,
+                     float ln_eps, int ln, hipStream_t stream);
+int aiko_rowstats_mx(const void* x, int ldx, void* q, int ldq, void* qsc, int ysr, float* st, int sts, int P, int M,
+                     int D, hipStream_t stream);
 int aiko_linear_splitk(const void* x, const void* w, const float* bias, float* part, void* y, int M, int N, int K,
                        int ldx, int ldw, int ldy, int S, hipStream_t stream);
 int aiko_attn_fwd(const void* q, const void* k, const void* v, void* o, int ldq, int ldk, int ldv,
@@ -992,6 +998,104 @@ void rownorm_quant_out(const at::Tensor& x, const c10::optional<at::Tensor>& gam
                "rownorm_quant");
 }
 
+// LayerNorm folded across a GEMM pair (gemm_fp8.hip, aiko_gemm_fp8_ln).  a: MX-fp8 [M, K] with
+// E8M0 scales amx [K/128, R >= M rounded to 128, 4]; b fp8 [N, K]; st fp32 [P, R2 >= M, 2] row
+// partials (ln 1 writes P = N / 256 of them, ln 2 reads P = st.size(0)).
+//   ln 1: y = a b^T sb + bias + res (bf16) and its MX copy yq [M, N] / ysc [N/128, >= M, 4]
+//   ln 2: y (bf16, act 0) or yq / ysc (MX, act 3 = GELU) = act(rstd (a b^T sb - mean cs) + bias)
+void gemm_fp8_ln_out(const at::Tensor& a, const at::Tensor& amx, const at::Tensor& b, const at::Tensor& sb,
+                     const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& res,
+                     const c10::optional<at::Tensor>& y, const c10::optional<at::Tensor>& yq,
+                     const c10::optional<at::Tensor>& ysc, at::Tensor& st, const c10::optional<at::Tensor>& cs,
+                     int64_t ln, int64_t act, int64_t ln_d, double eps, const at::Tensor& zero) {
+  for (const at::Tensor* t : {&a, &amx, &b, &sb, (const at::Tensor*)&st, &zero}) check_cuda(*t, "operand");
+  TORCH_CHECK(a.element_size() == 1 && b.element_size() == 1, "aiko.gemm_fp8_ln_out: A and B must be fp8 storage");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(K % 128 == 0 && b.dim() == 2 && b.size(1) == K && b.is_contiguous() && N % 256 == 0,
+              "aiko.gemm_fp8_ln_out: B [N % 256 == 0, K % 128 == 0] contiguous");
+  const int64_t lda = row_pitch(a, K, "gemm_fp8_ln_out", "A");
+  TORCH_CHECK(sb.scalar_type() == at::kFloat && sb.numel() == N && sb.is_contiguous(), "aiko.gemm_fp8_ln_out: sb fp32 [N]");
+  TORCH_CHECK(amx.element_size() == 1 && amx.dim() == 3 && amx.size(0) == K / 128 && amx.size(2) == 4 &&
+                  amx.is_contiguous() && amx.size(1) >= ((M + 127) / 128) * 128,
+              "aiko.gemm_fp8_ln_out: amx uint8 [K/128, rows >= M rounded to 128, 4]");
+  TORCH_CHECK(st.scalar_type() == at::kFloat && st.dim() == 3 && st.size(2) == 2 && st.size(1) >= M && st.is_contiguous(),
+              "aiko.gemm_fp8_ln_out: st fp32 [P, >= M, 2]");
+  TORCH_CHECK(zero.nbytes() >= 16 && reinterpret_cast<uintptr_t>(zero.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0,
+              "aiko.gemm_fp8_ln_out: 16-byte aligned operands and a zero page");
+  const float* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    check_cuda(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == N && bias->is_contiguous(), "aiko.gemm_fp8_ln_out: bias fp32 [N]");
+    bp = bias->data_ptr<float>();
+  }
+  const float* csp = nullptr;
+  if (cs.has_value() && cs->defined()) {
+    check_cuda(*cs, "cs");
+    TORCH_CHECK(cs->scalar_type() == at::kFloat && cs->numel() == N && cs->is_contiguous(), "aiko.gemm_fp8_ln_out: cs fp32 [N]");
+    csp = cs->data_ptr<float>();
+  }
+  const void* rp = nullptr;
+  int64_t ldr = 0;
+  if (res.has_value() && res->defined()) {
+    check_cuda(*res, "residual");
+    TORCH_CHECK(res->scalar_type() == at::kBFloat16 && res->size(0) == M, "aiko.gemm_fp8_ln_out: residual bf16 [M, N]");
+    ldr = row_pitch(*res, N, "gemm_fp8_ln_out", "residual");
+    rp = res->data_ptr();
+  }
+  void* yp = nullptr;
+  int64_t ldy = 0;
+  if (y.has_value() && y->defined()) {
+    check_cuda(*y, "y");
+    TORCH_CHECK(y->scalar_type() == at::kBFloat16 && y->size(0) == M, "aiko.gemm_fp8_ln_out: y bf16 [M, N]");
+    ldy = row_pitch(*y, N, "gemm_fp8_ln_out", "y");
+    yp = y->data_ptr();
+  }
+  void* yqp = nullptr;
+  void* yscp = nullptr;
+  int64_t ldq = 0, ysr = 0;
+  if (yq.has_value() && yq->defined()) {
+    TORCH_CHECK(ysc.has_value() && ysc->defined(), "aiko.gemm_fp8_ln_out: yq needs ysc");
+    check_cuda(*yq, "yq");
+    check_cuda(*ysc, "ysc");
+    TORCH_CHECK(yq->element_size() == 1 && yq->size(0) == M, "aiko.gemm_fp8_ln_out: yq uint8 [M, N]");
+    ldq = row_pitch(*yq, N, "gemm_fp8_ln_out", "yq");
+    TORCH_CHECK(ysc->element_size() == 1 && ysc->dim() == 3 && ysc->size(0) == N / 128 && ysc->size(1) >= M &&
+                    ysc->size(2) == 4 && ysc->is_contiguous(),
+                "aiko.gemm_fp8_ln_out: ysc uint8 [N/128, rows >= M, 4]");
+    yqp = yq->data_ptr();
+    yscp = ysc->data_ptr();
+    ysr = ysc->size(1);
+  }
+  if (ln == 1) TORCH_CHECK(st.size(0) >= N / 256, "aiko.gemm_fp8_ln_out: st needs N / 256 partials");
+  check_launch(aiko_gemm_fp8_ln(a.data_ptr(), b.data_ptr(), sb.data_ptr<float>(), bp, rp, yp, M, N, K, lda, ldy, ldr,
+                                act, zero.data_ptr(), amx.data_ptr(), (int)amx.size(1), yqp, yscp, (int)ldq, (int)ysr,
+                                st.data_ptr<float>(), csp, (int)st.size(1), (int)st.size(0), (int)ln_d, (float)eps,
+                                (int)ln, cur_stream()),
+               "gemm_fp8_ln");
+}
+
+// bf16 rows x [M, D] -> MX-fp8 copy (q [M, D], qsc [D/128, >= M, 4]) + row sum / sum of squares
+// as partial 0 of st [P, >= M, 2] (partials 1 .. P-1 zeroed)
+void rowstats_mx_out(const at::Tensor& x, at::Tensor& q, at::Tensor& qsc, at::Tensor& st) {
+  for (const at::Tensor* t : {&x, (const at::Tensor*)&q, (const at::Tensor*)&qsc, (const at::Tensor*)&st}) check_cuda(*t, "operand");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16, "aiko.rowstats_mx_out: x bf16");
+  const int64_t M = x.size(0), D = x.size(1);
+  const int64_t ldx = row_pitch(x, D, "rowstats_mx_out", "x");
+  TORCH_CHECK(ldx % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "aiko.rowstats_mx_out: 16-B rows");
+  TORCH_CHECK(q.element_size() == 1 && q.size(0) == M && q.size(1) >= D, "aiko.rowstats_mx_out: q uint8 [M, D]");
+  const int64_t ldq = row_pitch(q, D, "rowstats_mx_out", "q");
+  TORCH_CHECK(ldq % 8 == 0 && reinterpret_cast<uintptr_t>(q.data_ptr()) % 8 == 0, "aiko.rowstats_mx_out: 8-B q rows");
+  TORCH_CHECK(qsc.element_size() == 1 && qsc.dim() == 3 && qsc.size(0) == D / 128 && qsc.size(1) >= M && qsc.size(2) == 4 &&
+                  qsc.is_contiguous(),
+              "aiko.rowstats_mx_out: qsc uint8 [D/128, >= M, 4]");
+  TORCH_CHECK(st.scalar_type() == at::kFloat && st.dim() == 3 && st.size(2) == 2 && st.size(1) >= M && st.is_contiguous(),
+              "aiko.rowstats_mx_out: st fp32 [P, >= M, 2]");
+  check_launch(aiko_rowstats_mx(x.data_ptr(), (int)ldx, q.data_ptr(), (int)ldq, qsc.data_ptr(), (int)qsc.size(1),
+                                st.data_ptr<float>(), (int)st.size(1), (int)st.size(0), (int)M, (int)D, cur_stream()),
+               "rowstats_mx");
+}
+
 // Split-K linear (linear_splitk.hip): x [M, >= K] bf16, w [N, >= K] bf16 (row pitch w.stride(0)),
 // bias fp32 [N] or None, part fp32 with >= S*M*N elements, y [M, >= N] bf16.
 void linear_splitk_out(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
@@ -1266,6 +1370,8 @@ TORCH_LIBRARY(aiko, m) {
   m.def("stem_pool_u8_out(Tensor frames, Tensor w, Tensor bias, Tensor(a!) y, float[] mean255, int variant=0) -> ()");
   m.def("gemm_fp8_out(Tensor a, Tensor? sa, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!)? y, int act, int bm, int bn, int variant=0, Tensor? zero=None, Tensor? amx=None, Tensor(b!)? yq=None, Tensor(c!)? ysc=None) -> ()");
   m.def("rownorm_quant_out(Tensor x, Tensor? gamma, Tensor? beta, float eps, Tensor(a!)? yb, Tensor(b!)? q, Tensor(c!)? qs) -> ()");
+  m.def("gemm_fp8_ln_out(Tensor a, Tensor amx, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!)? y, Tensor(b!)? yq, Tensor(c!)? ysc, Tensor(d!) st, Tensor? cs, int ln, int act, int ln_d, float eps, Tensor zero) -> ()");
+  m.def("rowstats_mx_out(Tensor x, Tensor(a!) q, Tensor(b!) qsc, Tensor(c!) st) -> ()");
   m.def("linear_splitk_out(Tensor x, Tensor w, Tensor? bias, Tensor(a!) part, Tensor(b!) y, int K, int S) -> ()");
   m.def("attn_fwd_out(Tensor q, Tensor k, Tensor v, Tensor(a!) o, int B, int H, int T, int Tpad, float scale, Tensor(b!)? work=None, Tensor(c!)? oq=None, Tensor(d!)? osc=None) -> ()");
   m.def("logmel_out(Tensor audio, Tensor mel, Tensor mel_range, int n_fft, int hop, int F, Tensor(a!) work, Tensor(b!) gmax, Tensor(c!) dst, int rows, int pad) -> ()");
@@ -1301,6 +1407,8 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("softmax_topk_out", &softmax_topk_out);
   m.impl("gemm_fp8_out", &gemm_fp8_out);
   m.impl("rownorm_quant_out", &rownorm_quant_out);
+  m.impl("gemm_fp8_ln_out", &gemm_fp8_ln_out);
+  m.impl("rowstats_mx_out", &rowstats_mx_out);
   m.impl("attn_fwd_out", &attn_fwd_out);
   m.impl("linear_splitk_out", &linear_splitk_out);
   m.impl("logmel_out", &logmel_out);

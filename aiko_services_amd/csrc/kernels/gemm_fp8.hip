@@ -47,6 +47,15 @@ struct Fp8GemmParams {
   uint8_t* yq;          // MX output instead of y: e4m3 [M][ldq] + scales [N/128][ysr][4]
   uint8_t* ysc;
   int ldq, ysr;
+  // LayerNorm folded across a GEMM pair (persistent 256 x 256 kernel only; see the comment above
+  // gemm_fp8_pers2_kernel): the producer (LN 1) also writes y's MX-fp8 copy to yq / ysc and the
+  // per-row partial sum / sum of squares of every 256-column tile to st [N / 256][sts] float2;
+  // the consumer (LN 2) reads stp of those partials per row, cs [N] = sum_k W'[n, k] (W' = W
+  // diag(gamma), dequantised), bias = b + W beta, over ln_d columns with ln_eps
+  float* st;
+  const float* cs;
+  int sts, stp, ln_d;
+  float ln_eps;
 };
 
 
@@ -995,11 +1004,21 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers_kernel(Fp8GemmParams p, 
 // Epilogue of one 16-row fragment group of the persistent kernels' 128 x 64 wave tile: both
 // 32-column fragment pairs (lane l: row l & 15, eight consecutive columns after the permlane
 // swap), per-channel scale + bias from LDS, activation, bf16 or MX-fp8 store.
-template <bool MXO, int ACT, bool RES>
-__device__ __forceinline__ void fp8_pers_epi(const Fp8GemmParams& p, const f32x4 (&acc)[4], float rs, int m, int nw,
-                                             int coff, int fg, const float* s_sb, const float* s_bias,
+__device__ __forceinline__ float fp8_h2f(uint32_t bits) {
+  return (float)__builtin_bit_cast(_Float16, (unsigned short)bits);
+}
+
+// LN 2 (LayerNorm-folded consumer): rs = rstd of row m, r2 = -mean * rstd, and s_bias holds
+// (cs, bias) as half2 — v = rstd * (acc * sb - mean * cs) + bias.  LN 1 (producer): after the
+// bf16 store, the stored values' MX-fp8 copy (yq / ysc) and their row sum / sum of squares over
+// this wave's 64 columns into LDS (s_part, lane group 0).
+template <bool MXO, int ACT, bool RES, int LN = 0>
+__device__ __forceinline__ void fp8_pers_epi(const Fp8GemmParams& p, const f32x4 (&acc)[4], float rs, float r2, int m,
+                                             int nw, int coff, int fg, const float* s_sb, const float* s_bias,
                                              __amdgpu_buffer_rsrc_t ry, __amdgpu_buffer_rsrc_t rsc,
-                                             const u32x4 (&rv)[2]) {
+                                             const u32x4 (&rv)[2], __amdgpu_buffer_rsrc_t rq, float* s_part) {
+  [[maybe_unused]] float s1 = 0.f, s2 = 0.f;
+  [[maybe_unused]] int ex2[2] = {0, 0};
 #pragma unroll
   for (int pp = 0; pp < 2; ++pp) {
     const int nb = nw + pp * 32, n = nb + coff;
@@ -1015,10 +1034,21 @@ __device__ __forceinline__ void fp8_pers_epi(const Fp8GemmParams& p, const f32x4
       hi[e] = __uint_as_float(sw[1]);
     }
     float v[8];
+    if constexpr (LN == 2) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      v[e] = lo[e] * rs * sc0[e] + bi0[e];
-      v[e + 4] = hi[e] * rs * sc1[e] + bi1[e];
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t c0 = __float_as_uint(bi0[e]), c1 = __float_as_uint(bi1[e]);   // (cs, bias) half2
+        v[e] = (lo[e] * sc0[e]) * rs + (r2 * fp8_h2f(c0 & 0xffffu) +
+                                        fp8_h2f(c0 >> 16));
+        v[e + 4] = (hi[e] * sc1[e]) * rs + (r2 * fp8_h2f(c1 & 0xffffu) +
+                                            fp8_h2f(c1 >> 16));
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = lo[e] * rs * sc0[e] + bi0[e];
+        v[e + 4] = hi[e] * rs * sc1[e] + bi1[e];
+      }
     }
     if constexpr (ACT == 1) {
 #pragma unroll
@@ -1077,7 +1107,62 @@ __device__ __forceinline__ void fp8_pers_epi(const Fp8GemmParams& p, const f32x4
       for (int e = 0; e < 4; ++e) o[e] = pack2(v[2 * e], v[2 * e + 1]);
       const uint32_t yoff = live ? (uint32_t)(((long)m * p.ldy + n) * 2) : 0x80000000u;
       __builtin_amdgcn_raw_buffer_store_b128(o, ry, yoff, 0, 0);
+      if constexpr (LN == 1) {                       // the stored (bf16-rounded) values
+        float w[8];
+        float amax = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          w[2 * e] = __uint_as_float(o[e] << 16);
+          w[2 * e + 1] = __uint_as_float(o[e] & 0xffff0000u);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          amax = fmaxf(amax, fabsf(w[e]));
+          s1 += w[e];
+          s2 += w[e] * w[e];
+        }
+        {
+          const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(amax), __float_as_uint(amax), false, false);
+          amax = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+        }
+        {
+          const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(amax), __float_as_uint(amax), false, false);
+          amax = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+        }
+        const int ex = mx_exponent(amax);
+        ex2[pp] = ex;
+        const float inv = __uint_as_float((uint32_t)(127 - ex) << 23);
+        unsigned w0 = 0u, w1 = 0u;
+        w0 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(w[0] * inv, -448.f), 448.f),
+                                             fminf(fmaxf(w[1] * inv, -448.f), 448.f), w0, false);
+        w0 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(w[2] * inv, -448.f), 448.f),
+                                             fminf(fmaxf(w[3] * inv, -448.f), 448.f), w0, true);
+        w1 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(w[4] * inv, -448.f), 448.f),
+                                             fminf(fmaxf(w[5] * inv, -448.f), 448.f), w1, false);
+        w1 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(w[6] * inv, -448.f), 448.f),
+                                             fminf(fmaxf(w[7] * inv, -448.f), 448.f), w1, true);
+        typedef __attribute__((ext_vector_type(2))) unsigned u32x2v;
+        const uint32_t qoff = live ? (uint32_t)((long)m * p.ldq + n) : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2v{w0, w1}, rq, qoff, 0, 0);
+      }
     }
+  }
+  if constexpr (LN == 1) {
+    // both 32-column blocks' scale bytes are adjacent (nw % 64 == 0): one 2-byte store
+    const bool live = m < p.M;
+    const uint32_t soff = live && fg == 0 ? (uint32_t)(((long)(nw >> 7) * p.ysr + m) * 4 + ((nw >> 5) & 3))
+                                          : 0x80000000u;
+    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)((ex2[0] + 127) | ((ex2[1] + 127) << 8)), rsc, soff, 0, 0);
+    // row partials over the lane group's four 8-column pieces
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float& u = t ? s2 : s1;
+      const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(u), __float_as_uint(u), false, false);
+      u = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+      const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(u), __float_as_uint(u), false, false);
+      u = __uint_as_float(b[0]) + __uint_as_float(b[1]);
+    }
+    if (fg == 0) *reinterpret_cast<float2*>(s_part) = make_float2(s1, s2);
   }
 }
 
@@ -1094,20 +1179,41 @@ __device__ __forceinline__ void fp8_pers_epi(const Fp8GemmParams& p, const f32x4
 //     fragment i + LA in flight while the MFMAs on fragment i run.
 // vmcnt: block (k, 1)'s DMA is issued right after the fused block's barrier, before that
 // block's stores, so its wait is vmcnt(NST); every other wait is vmcnt(0).
-template <int BM, bool MXO, int ACT, bool MXA, bool RES>
+//
+// LayerNorm folded across a GEMM pair (LN template argument; Whisper's out-proj / fc2 -> qkv / fc1):
+//   LN(x) W^T + b = rstd * (x - mean) (W diag g)^T + (b + W beta)
+//                 = rstd * (x W'^T) - rstd * mean * cs + b',   cs[n] = sum_k W'[n, k]
+// so the consumer (LN 2) multiplies the MX-fp8 copy of the raw residual stream x by the folded
+// weights and applies the row's statistics in its epilogue; no normalised / quantised copy of x
+// is ever materialised.  The producer (LN 1: the GEMM that writes x, with its residual add)
+// quantises its own output tile to MX-fp8 (block scales are local to 32 columns) and reduces the
+// row sum / sum of squares of each 256-column tile: per wave in registers, across the tile's four
+// column waves in LDS, written out one K block into the next tile (after that block's barrier)
+// as st[tile_n][m] — deterministic, no atomics.  The consumer reads the stp partials of its rows
+// a K block ahead (lane group g loads partial g), reduces them across the lane groups and forms
+// (rstd, -mean * rstd).
+template <int BM, bool MXO, int ACT, bool MXA, bool RES, int LN = 0>
 __global__ __launch_bounds__(512, 1) void gemm_fp8_pers2_kernel(Fp8GemmParams p, const uint8_t* zero, int tiles_n,
                                                                 int ntiles, int diag) {
   constexpr int BN = 256, BK = 128, WGN = 4, WM = BM / 2, WN = 64, MI = WM / 16, NI = WN / 16;
   constexpr int APT = BM / 64, BPT = BN / 64;
   constexpr int TILE_BYTES = (BM + BN) * BK;
   constexpr int STAGE_BYTES = TILE_BYTES + (MXA ? BM * 4 : 0);   // + the MX scale tile of A
-  constexpr int MAXN = 3072;
-  constexpr int NST = MXO ? 2 * MI * (NI / 2) : MI * (NI / 2);   // store instructions per tile per wave
+  constexpr int MAXN = LN == 1 ? 1024 : 3072;
+  // store instructions per tile per wave (LN 1: bf16 + MX bytes per 32-column pair, one 2-byte
+  // scale store per fragment group)
+  constexpr int NST = MXO ? 2 * MI * (NI / 2) : LN == 1 ? 5 * MI : MI * (NI / 2);
   constexpr int LA = (MXO && ACT == 3) || (BM == 256 && RES) ? 1 : 2;   // A fragments read ahead (1: registers)
-  constexpr int NRL = RES ? 2 * MI : 0;              // residual loads per tile per wave (always issued)
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE_BYTES + 2 * MAXN * 4];
+  // residual loads (LN 2: row-statistics partials) per tile per wave, always issued
+  constexpr int NRL = RES ? 2 * MI : (LN == 2 ? MI : 0);
+  static_assert(NST + NRL <= 63, "vmcnt is a 6-bit counter");
+  static_assert(LN == 0 || BM == 256, "LayerNorm folding: 256 x 256 tiles");
+  static_assert(LN != 1 || (RES && !MXO && ACT == 0), "LN producer: bf16 out + residual, no activation");
+  constexpr int PART_BYTES = LN == 1 ? BM * 4 * 8 : 0;   // [BM rows][4 column waves] float2
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE_BYTES + 2 * MAXN * 4 + PART_BYTES];
   float* const s_sb = reinterpret_cast<float*>(smem + 2 * STAGE_BYTES);
   float* const s_bias = s_sb + MAXN;
+  [[maybe_unused]] float* const s_part = s_bias + MAXN;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1124,7 +1230,14 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers2_kernel(Fp8GemmParams p,
 
   for (int n = tid; n < p.N; n += 512) {
     s_sb[n] = p.sb[n];
-    s_bias[n] = p.bias ? p.bias[n] : 0.f;
+    if constexpr (LN == 2) {                         // (cs, bias) as half2
+      const float b = p.bias ? p.bias[n] : 0.f;
+      const uint32_t lo = __builtin_bit_cast(unsigned short, (_Float16)p.cs[n]);
+      const uint32_t hi = __builtin_bit_cast(unsigned short, (_Float16)b);
+      s_bias[n] = __uint_as_float(lo | (hi << 16));
+    } else {
+      s_bias[n] = p.bias ? p.bias[n] : 0.f;
+    }
   }
 
   auto issue = [&](int f) {                          // flat K block f of this workgroup's walk
@@ -1160,11 +1273,16 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers2_kernel(Fp8GemmParams p,
     for (int i = 0; i < MI; ++i)
       r[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsa, (m0 + wr * WM + i * 16 + fr) * 4, 0, 0));
   };
+  // LN 1: row partials out; LN 2: in (lane group g loads partial g of its row)
+  const __amdgpu_buffer_rsrc_t rst = __builtin_amdgcn_make_buffer_rsrc(
+      LN ? (void*)p.st : (void*)p.sb, (short)0, LN == 2 ? p.stp * p.sts * 8 : (LN == 1 ? 0x7ffffff0 : 0), 0x00020000);
 
   const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(MXO ? (void*)p.yq : (void*)p.y, (short)0,
                                                                       0x7ffffff0, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc(MXO ? (void*)p.ysc : (void*)p.y, (short)0,
-                                                                       0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc((MXO || LN == 1) ? (void*)p.ysc : (void*)p.y,
+                                                                       (short)0, 0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(LN == 1 ? (void*)p.yq : (void*)p.y, (short)0,
+                                                                      0x7ffffff0, 0x00020000);
   const __amdgpu_buffer_rsrc_t rres_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.res, (short)0, 0x7ffffff0,
                                                                              0x00020000);
   const int off_lo = (fg ^ (fr & 7)) << 4, off_hi = ((fg + 4) ^ (fr & 7)) << 4;
@@ -1216,6 +1334,22 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers2_kernel(Fp8GemmParams p,
   };
   auto nop = [](auto) {};
 
+  // LN 1: tile kp's row partials (its four column waves, in s_part since the barrier just passed)
+  // -> st[tile_n][m]: two threads per row, the even one stores
+  auto part_out = [&](int kp) {
+    if constexpr (LN == 1) {
+      const int tau = lid + kp * G;
+      const int m = (tau / tiles_n) * BM + (tid >> 1);
+      const f32x4 a = *reinterpret_cast<const f32x4*>(s_part + (tid >> 1) * 8 + (tid & 1) * 4);
+      float t1 = a[0] + a[2], t2 = a[1] + a[3];
+      t1 += dpp_f32<0xB1>(t1);
+      t2 += dpp_f32<0xB1>(t2);
+      typedef __attribute__((ext_vector_type(2))) unsigned u32x2v;
+      const uint32_t off = (tid & 1) == 0 && m < p.M ? (uint32_t)(((long)(tau % tiles_n) * p.sts + m) * 8) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2v{__float_as_uint(t1), __float_as_uint(t2)}, rst, off, 0, 0);
+    }
+  };
+
   float rs[MI], rsn[MI];
   issue(0);
   fp8_wait_vm_barrier<0>();                          // block 0 landed; scale / bias table written
@@ -1227,16 +1361,27 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers2_kernel(Fp8GemmParams p,
     const int m0 = (tau / tiles_n) * BM, n0 = (tau % tiles_n) * BN;
     for (int kb = 1; kb < nkb; ++kb) {
       const int f = k * nkb + kb;
-      if (kb == 1 && k > 0) fp8_wait_vm_barrier<NST + NRL>();   // younger: the previous tile's stores
-                                                                  // and residual loads
-      else fp8_wait_vm_barrier<0>();
+      if (kb == 1 && k > 0) {
+        fp8_wait_vm_barrier<NST + NRL>();            // younger: the previous tile's stores and
+        part_out(k - 1);                             // residual loads
+      } else {
+        fp8_wait_vm_barrier<0>();
+      }
       if (kb == nkb - 1 && k + 1 < my_tiles) load_rs(k + 1, rsn);   // older than the next DMA
       issue(f + 1);
       kblock(f, std::false_type{}, nop);
     }
     const int mw = m0 + wr * WM + fr, nw = n0 + wc * WN;
     u32x4 rres[MI][2];                               // residual of fragment group i, loaded a group ahead
+    [[maybe_unused]] float st1[MI], st2[MI];         // LN 2: row partials of group i, likewise
     auto ldres = [&](int i) {
+      if constexpr (LN == 2) {
+        const int m = mw + i * 16;
+        const uint32_t off = fg < p.stp && m < p.M ? (uint32_t)((fg * p.sts + m) * 8) : 0x80000000u;
+        const auto u = __builtin_amdgcn_raw_buffer_load_b64(rst, off, 0, 0);
+        st1[i] = __uint_as_float(u[0]);
+        st2[i] = __uint_as_float(u[1]);
+      }
       if constexpr (RES) {
         const int m = mw + i * 16;
 #pragma unroll
@@ -1249,8 +1394,24 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers2_kernel(Fp8GemmParams p,
     auto epi = [&](auto I) {
       constexpr int i = decltype(I)::value;
       if constexpr (i + 1 < MI) ldres(i + 1);
-      fp8_pers_epi<MXO, ACT, RES>(p, acc[i], p.sa ? rs[i] : 1.f, mw + i * 16, nw, coff, fg, s_sb, s_bias, ry, rsc,
-                                  rres[i]);
+      float r1 = p.sa ? rs[i] : 1.f, r2 = 0.f;
+      if constexpr (LN == 2) {                       // row statistics from the lane groups' partials
+        float t1 = st1[i], t2 = st2[i];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          float& u = t ? t2 : t1;
+          const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(u), __float_as_uint(u), false, false);
+          u = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+          const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(u), __float_as_uint(u), false, false);
+          u = __uint_as_float(b[0]) + __uint_as_float(b[1]);
+        }
+        const float inv_d = 1.f / (float)p.ln_d;
+        const float mean = t1 * inv_d;
+        r1 = rsqrtf(fmaxf(t2 * inv_d - mean * mean, 0.f) + p.ln_eps);
+        r2 = -mean * r1;
+      }
+      fp8_pers_epi<MXO, ACT, RES, LN>(p, acc[i], r1, r2, mw + i * 16, nw, coff, fg, s_sb, s_bias, ry, rsc, rres[i], rq,
+                                      s_part + (wr * WM + i * 16 + fr) * 8 + wc * 2);
     };
     if (k + 1 < my_tiles) {                          // epilogue fused with the next tile's block 0
       const int f = (k + 1) * nkb;
@@ -1263,6 +1424,10 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers2_kernel(Fp8GemmParams p,
     } else {
       ldres(0);
       fp8_static_for<0, MI>(epi);
+      if constexpr (LN == 1) {                       // the last tile's partials
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        part_out(k);
+      }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1533,6 +1698,65 @@ __global__ __launch_bounds__(256) void rownorm_quant_pers_kernel(
   }
 }
 
+// The LayerNorm producer's outputs for a residual stream no GEMM wrote (Whisper's first layer):
+// x [M][ldx] bf16, D columns (D % 32 == 0, D <= 768) -> its MX-fp8 copy q [M][ldq] + E8M0 scales
+// [D/128][ysr][4], and the row sum / sum of squares as partial 0 of st [P][sts] float2 (partials
+// 1 .. P - 1 zeroed, so a consumer reading P partials sees the full row).  32 lanes per row (chunk
+// c of lane l: columns 8 (l + 32 c) ..+ 7; one MX block = 4 adjacent lanes), 8 rows per block.
+__global__ __launch_bounds__(256) void rowstats_mx_kernel(const bf16_t* __restrict__ x, int ldx, uint8_t* __restrict__ q,
+                                                          int ldq, uint8_t* __restrict__ qsc, int ysr,
+                                                          float* __restrict__ st, int sts, int P, int M, int D) {
+  const int lane = threadIdx.x & 31;
+  const int row = blockIdx.x * 8 + (threadIdx.x >> 5);
+  const bool live = row < M;                       // both halves of a wave run the reductions
+  const int nchunk = D >> 3;
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const int ch = lane + 32 * c;
+    const bool ok = live && ch < nchunk;
+    u32x4 u = {0u, 0u, 0u, 0u};
+    if (ok) u = *reinterpret_cast<const u32x4*>(x + (long)row * ldx + ch * 8);
+    float w[8];
+    float amax = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      w[2 * e] = __uint_as_float(u[e] << 16);
+      w[2 * e + 1] = __uint_as_float(u[e] & 0xffff0000u);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s1 += w[e];
+      s2 += w[e] * w[e];
+      amax = fmaxf(amax, fabsf(w[e]));
+    }
+    amax = fmaxf(amax, dpp_f32<0xB1>(amax));       // the 4 lanes of one 32-column block
+    amax = fmaxf(amax, dpp_f32<0x4E>(amax));
+    const int ex = mx_exponent(amax);
+    const float inv = __uint_as_float((uint32_t)(127 - ex) << 23);
+    unsigned w0 = 0u, w1 = 0u;
+    w0 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(w[0] * inv, -448.f), 448.f),
+                                         fminf(fmaxf(w[1] * inv, -448.f), 448.f), w0, false);
+    w0 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(w[2] * inv, -448.f), 448.f),
+                                         fminf(fmaxf(w[3] * inv, -448.f), 448.f), w0, true);
+    w1 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(w[4] * inv, -448.f), 448.f),
+                                         fminf(fmaxf(w[5] * inv, -448.f), 448.f), w1, false);
+    w1 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(w[6] * inv, -448.f), 448.f),
+                                         fminf(fmaxf(w[7] * inv, -448.f), 448.f), w1, true);
+    if (ok) {
+      *reinterpret_cast<uint2*>(q + (long)row * ldq + ch * 8) = make_uint2(w0, w1);
+      const int blk = ch >> 2;
+      if ((lane & 3) == 0) qsc[((long)(blk >> 2) * ysr + row) * 4 + (blk & 3)] = (uint8_t)(ex + 127);
+    }
+  }
+  s1 = group_sum<1>(s1);
+  s2 = group_sum<1>(s2);
+  if (live && lane < P) {
+    const float2 v = lane == 0 ? make_float2(s1, s2) : make_float2(0.f, 0.f);
+    *reinterpret_cast<float2*>(st + ((long)lane * sts + row) * 2) = v;
+  }
+}
+
 }  // namespace aiko
 
 extern "C" int aiko_gemm_fp8(const void* a, const void* b, const float* sa, const float* sb,
@@ -1706,6 +1930,69 @@ extern "C" int aiko_rownorm_quant(const void* x, int ldx, const float* gamma, co
     rownorm_quant_kernel<6><<<grid, block, 0, stream>>>(xp, ldx, gamma, beta, eps, yp, ldyb, qp, ldq, qs, M, D);
   } else if (D <= 64 * 8 * 16) {
     rownorm_quant_kernel<16><<<grid, block, 0, stream>>>(xp, ldx, gamma, beta, eps, yp, ldyb, qp, ldq, qs, M, D);
+  } else {
+    return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int aiko_rowstats_mx(const void* x, int ldx, void* q, int ldq, void* qsc, int ysr, float* st, int sts,
+                                int P, int M, int D, hipStream_t stream) {
+  using namespace aiko;
+  if (M <= 0 || D % 32 || D > 768 || P < 1 || P > 32 || sts < M || ysr < M) return -1;
+  rowstats_mx_kernel<<<dim3((M + 7) / 8), dim3(256), 0, stream>>>(static_cast<const bf16_t*>(x), ldx,
+                                                                 static_cast<uint8_t*>(q), ldq,
+                                                                 static_cast<uint8_t*>(qsc), ysr, st, sts, P, M, D);
+  return (int)hipGetLastError();
+}
+
+// LayerNorm folded across a GEMM pair on the persistent 256 x 256 kernel (gemm_fp8_pers2_kernel,
+// LN argument).  ln 1 (producer): y = A B^T * sb + bias + res (bf16), its MX-fp8 copy yq / ysc and
+// row partials st [N/256][sts] float2; ln 2 (consumer): y (bf16, act 0) or yq / ysc (MX-fp8, act 3
+// = GELU) = act(rstd * (A B^T * sb - mean * cs) + bias) with the statistics of the stp partials
+// in st over ln_d columns.  A is MX-fp8 (amx) in both.
+extern "C" int aiko_gemm_fp8_ln(const void* a, const void* b, const float* sb, const float* bias, const void* res,
+                                void* y, int M, int N, int K, int lda, int ldy, int ldr, int act, const void* zero,
+                                const void* amx, int mxr, void* yq, void* ysc, int ldq, int ysr, float* st,
+                                const float* cs, int sts, int stp, int ln_d, float ln_eps, int ln, hipStream_t stream) {
+  using namespace aiko;
+  if (!zero || !amx || !st || M <= 0 || N % 256 || N > 3072 || K % 128 || K < 256 || sts < M) return -1;
+  Fp8GemmParams p{};
+  p.a = static_cast<const uint8_t*>(a);
+  p.b = static_cast<const uint8_t*>(b);
+  p.sa = nullptr; p.sb = sb; p.bias = bias;
+  p.res = static_cast<const bf16_t*>(res);
+  p.y = static_cast<bf16_t*>(y);
+  p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldy = ldy; p.ldr = ldr; p.act = act;
+  p.amx = static_cast<const uint8_t*>(amx); p.mxr = mxr;
+  p.yq = static_cast<uint8_t*>(yq); p.ysc = static_cast<uint8_t*>(ysc); p.ldq = ldq; p.ysr = ysr;
+  p.st = st; p.cs = cs; p.sts = sts; p.stp = stp; p.ln_d = ln_d; p.ln_eps = ln_eps;
+  if ((long)sts * 8 * (N / 256 > stp ? N / 256 : stp) >= 0x7ffffff0L) return -1;
+  if (yq && ((long)M * ldq >= 0x7ffffff0L || (long)(N / 128) * ysr * 4 >= 0x7ffffff0L || ysr < M)) return -1;
+  if (y && ((long)M * ldy * 2 >= 0x7ffffff0L || ldy % 8 || reinterpret_cast<uintptr_t>(y) % 16)) return -1;
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  const int tiles_n = N / 256, ntiles = ((M + 255) / 256) * tiles_n;
+  const dim3 pg((unsigned)(ntiles < cus ? ntiles : cus));
+  const uint8_t* z = static_cast<const uint8_t*>(zero);
+  if (ln == 1) {
+    if (!res || !y || !yq || !ysc || act != 0 || N > 1024 || ldr % 8 || (long)M * ldr * 2 >= 0x7ffffff0L ||
+        reinterpret_cast<uintptr_t>(res) % 16)
+      return -1;
+    gemm_fp8_pers2_kernel<256, false, 0, true, true, 1><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles, 0);
+  } else if (ln == 2) {
+    if (!cs || res || stp < 1 || stp > 4 || ln_d <= 0) return -1;
+    if (yq && ysc && act == 3 && !y) {
+      gemm_fp8_pers2_kernel<256, true, 3, true, false, 2><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles, 0);
+    } else if (y && !yq && act == 0) {
+      gemm_fp8_pers2_kernel<256, false, 0, true, false, 2><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles, 0);
+    } else {
+      return -1;
+    }
   } else {
     return -1;
   }

@@ -20,7 +20,8 @@ import torch
 
 from . import conv as _conv
 
-__all__ = ["Fp8Linear", "make_fp8_linear", "quantize_rows_ref", "linear_fp8", "rownorm",
+__all__ = ["Fp8Linear", "make_fp8_linear", "make_ln_fp8_linear", "linear_fp8_ln", "rowstats_mx",
+           "quantize_rows_ref", "linear_fp8", "rownorm",
            "attention", "ACT_NONE", "ACT_RELU", "ACT_SILU", "ACT_GELU", "FP8_MAX", "pick_tile"]
 
 ACT_NONE, ACT_RELU, ACT_SILU, ACT_GELU = 0, 1, 2, 3
@@ -40,12 +41,15 @@ class Fp8Linear:
     n: int
     k: int
     ref_weight: torch.Tensor | None = field(default=None, repr=False)   # dequantised fp32 [N, K]
+    cs: torch.Tensor | None = field(default=None, repr=False)   # LayerNorm-folded: sum_k W[n, k] fp32 [N]
 
     def to(self, device):
         self.weight = self.weight.to(device)
         self.scale = self.scale.to(device)
         if self.bias is not None:
             self.bias = self.bias.to(device)
+        if self.cs is not None:
+            self.cs = self.cs.to(device)
         return self
 
     @property
@@ -67,6 +71,53 @@ def make_fp8_linear(w: torch.Tensor, bias: torch.Tensor | None = None, device=No
     lin = Fp8Linear(qp.contiguous(), scale.contiguous(), None if bias is None else bias.float().contiguous(),
                     n, k, ref)
     return lin.to(device) if device is not None else lin
+
+
+def dequant_fp8_linear(lin: Fp8Linear) -> torch.Tensor:
+    """fp32 [N, K] values of ``lin``'s quantised weight (its ``ref_weight`` when held)."""
+    if lin.ref_weight is not None:
+        return lin.ref_weight.float()
+    return lin.weight[:, :lin.k].view(FP8).float() * lin.scale.float()[:, None]
+
+
+def make_ln_fp8_linear(lin: Fp8Linear, gamma: torch.Tensor, beta: torch.Tensor, device=None) -> Fp8Linear:
+    """``lin`` with the preceding LayerNorm's affine folded in, for :func:`linear_fp8_ln` (ln 2):
+    ``LN(x) W^T + b = rstd * (x W'^T - mean * cs) + b'`` with ``W' = W diag(gamma)`` (re-quantised
+    per output channel), ``b' = b + W beta`` and ``cs[n] = sum_k W'[n, k]`` of the quantised W',
+    so the mean term removes exactly what the GEMM accumulates."""
+    w = dequant_fp8_linear(lin).cpu()
+    g, be = gamma.detach().float().cpu(), beta.detach().float().cpu()
+    b = w @ be
+    if lin.bias is not None:
+        b = b + lin.bias.float().cpu()
+    out = make_fp8_linear(w * g[None, :], b)
+    out.cs = out.ref_weight.sum(dim=1).contiguous()
+    return out.to(device) if device is not None else out
+
+
+def linear_fp8_ln(xq: torch.Tensor, x_mx: torch.Tensor, lin: Fp8Linear, st: torch.Tensor, ln: int,
+                  out: torch.Tensor | None = None, residual: torch.Tensor | None = None, act: int = ACT_NONE,
+                  out_mx: tuple | None = None, ln_d: int | None = None, eps: float = 1e-5) -> None:
+    """The two halves of a LayerNorm folded across a GEMM pair (``gemm_fp8.hip``, persistent
+    256 x 256 kernel), MX-fp8 activations ``xq`` / ``x_mx`` in both:
+      ln 1 (producer): ``out = xq W^T + bias + residual`` (bf16), its MX-fp8 copy ``out_mx`` and
+        the per-row partial sums / sums of squares of each 256-column tile into ``st`` [N/256, M, 2];
+      ln 2 (consumer, ``lin`` from :func:`make_ln_fp8_linear`): ``act(LN(x) W^T + b)`` from the
+        producer's MX copy of x and its ``st`` partials (``ln_d`` columns, ``eps``) -> bf16 ``out``
+        (act none) or MX-fp8 ``out_mx`` (act GELU)."""
+    yq, ysc = out_mx if out_mx is not None else (None, None)
+    if ln == 2 and lin.cs is None:
+        raise ValueError("linear_fp8_ln: the consumer needs a LayerNorm-folded linear (make_ln_fp8_linear)")
+    torch.ops.aiko.gemm_fp8_ln_out(xq, x_mx, lin.weight, lin.scale, lin.bias, residual, out, yq, ysc, st,
+                                   lin.cs if ln == 2 else None, int(ln), int(act),
+                                   int(ln_d if ln_d is not None else xq.shape[1]), float(eps),
+                                   _conv.zero_page(xq.device))
+
+
+def rowstats_mx(x: torch.Tensor, q: torch.Tensor, qsc: torch.Tensor, st: torch.Tensor) -> None:
+    """The ln-1 producer outputs for bf16 rows no GEMM wrote: MX-fp8 copy (``q``, ``qsc``) and row
+    sum / sum of squares as partial 0 of ``st`` [P, M, 2] (the other partials zeroed)."""
+    torch.ops.aiko.rowstats_mx_out(x, q, qsc, st)
 
 
 def quantize_rows_ref(x: torch.Tensor):
