@@ -30,6 +30,7 @@ def main():
            for n, (o, i) in {"qkv": (3 * d, d), "out": (d, d), "fc1": (4 * d, d), "fc2": (d, 4 * d)}.items()}
     g, b = 1 + 0.1 * torch.randn(d), 0.1 * torch.randn(d)
     fold = {n: TR.make_ln_fp8_linear(lin[n], g, b, DEV) for n in ("qkv", "fc1")}
+    gd, bd = g.to(DEV), b.to(DEV)
     x = torch.randn(M, d, device=DEV).to(torch.bfloat16)
     xq, xsc = TR.mx_buffers(M, d, DEV)
     a8, asc = TR.mx_buffers(M, d, DEV)
@@ -39,13 +40,13 @@ def main():
     st = torch.zeros(3, M, 2, device=DEV)
     TR.rowstats_mx(x, xq, xsc, st)
     a8.copy_(xq); asc.copy_(xsc)
-    TR.rownorm(x, g.to(DEV), b.to(DEV), q=q8, qs=s8)
+    TR.rownorm(x, gd, bd, q=q8, qs=s8)
     u8.random_(0, 100)
     usc.fill_(120)
     qkv = torch.empty(M, 3 * d, dtype=torch.bfloat16, device=DEV)
     t4 = (256, 256, 4)
     rows = [
-        ("rownorm (ln1/ln2 pass)", lambda: TR.rownorm(x, g.to(DEV), b.to(DEV), q=q8, qs=s8)),
+        ("rownorm (ln1/ln2 pass)", lambda: TR.rownorm(x, gd, bd, q=q8, qs=s8)),
         ("rowstats_mx", lambda: TR.rowstats_mx(x, xq, xsc, st)),
         ("qkv plain v4", lambda: TR.linear_fp8(q8, s8, lin["qkv"], out=qkv, tile=t4)),
         ("qkv MX-A v4 (no LN)", lambda: TR.linear_fp8(xq, None, lin["qkv"], out=qkv, x_mx=xsc, tile=(256, 256, 3))),
