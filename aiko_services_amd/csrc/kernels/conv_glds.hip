@@ -19,10 +19,15 @@
 
 namespace aiko {
 
+// B-tile rows staged per K block: BN rounded up to the 32-row DMA granule (exact-N tiles)
+template <int BN>
+constexpr int glds_bn_pad() {
+  return (BN + 31) / 32 * 32;
+}
 // ring slots: 3 (two stages in flight) where 2 workgroups still fit the 160 KB LDS, else 2
 template <int BM, int BN>
 constexpr int glds_slots() {
-  return (BM + BN) * 64 * 2 * 3 <= 80 * 1024 ? 3 : 2;
+  return (BM + glds_bn_pad<BN>()) * 64 * 2 * 3 <= 80 * 1024 ? 3 : 2;
 }
 template <int BM, int BN>
 constexpr int glds_occupancy() {
@@ -40,17 +45,21 @@ __device__ __forceinline__ void wait_vm_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN>
+// WGM x WGN waves (2 x 2; exact-N tiles such as BN = 80: 4 x 1, each wave all BN columns)
+template <int BM, int BN, int WGM = 2, int WGN = 2>
 __global__ __launch_bounds__(256, (glds_occupancy<BM, BN>())) void conv_glds_kernel(ConvParams p,
                                                                                  const bf16_t* zero) {
+  static_assert(WGM * WGN == 4, "four waves");
   constexpr int BK = 64;
   constexpr int NS = glds_slots<BM, BN>();     // LDS ring slots
   constexpr int D = NS - 1;                    // stages in flight
-  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int MI = WM / 16, NI = WN / 16;
-  constexpr int APT = BM / 32, BPT = BN / 32;  // DMA instructions per thread per stage
+  static_assert(WM % 16 == 0 && WN % 16 == 0, "whole 16 x 16 fragments per wave");
+  constexpr int BNP = glds_bn_pad<BN>();       // staged B rows (rows past BN read the zero page)
+  constexpr int APT = BM / 32, BPT = BNP / 32; // DMA instructions per thread per stage
   constexpr int PER = APT + BPT;
-  constexpr int STAGE_ELEMS = (BM + BN) * BK;
+  constexpr int STAGE_ELEMS = (BM + BNP) * BK;
   constexpr int CPAD = 4;
   constexpr int EPI_BYTES = BM * (BN + CPAD) * 4;
   constexpr int RING_BYTES = NS * STAGE_ELEMS * 2;
@@ -61,7 +70,7 @@ __global__ __launch_bounds__(256, (glds_occupancy<BM, BN>())) void conv_glds_ker
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
+  const int wr = wave / WGN, wc = wave % WGN;
   const int ntn = (p.Cout + BN - 1) / BN;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int tile_n = bid % ntn, tile_m = bid / ntn;
@@ -96,30 +105,38 @@ __global__ __launch_bounds__(256, (glds_occupancy<BM, BN>())) void conv_glds_ker
 #pragma unroll
   for (int i = 0; i < BPT; ++i) {
     const int n = n0 + lrow + 32 * i;
-    b_src[i] = n < p.Cout ? p.w + (long)n * p.K + lp * 8 : nullptr;
+    b_src[i] = n < p.Cout && lrow + 32 * i < BN ? p.w + (long)n * p.K + lp * 8 : nullptr;
   }
 
-  // epilogue operands, prefetched before the K loop (ordinary loads, older than every DMA)
-  constexpr int CPR = BN / 8, CHUNKS = BM * CPR, CPT = CHUNKS / 256, E_ROWS = 256 / CPR;
+  // epilogue operands, prefetched before the K loop (ordinary loads, older than every DMA).
+  // Chunk c = tid + 256 i of the tile's BM x BN / 8 eight-column chunks: row c / CPR, column
+  // chunk c % CPR — for power-of-two CPR every i has the same column chunk (bias loaded once)
+  constexpr int CPR = BN / 8, CHUNKS = BM * CPR, CPT = CHUNKS / 256;
   static_assert(CHUNKS % 256 == 0, "tile must give every thread whole chunks");
-  const int e_cc = tid % CPR, e_row0 = tid / CPR;
-  const int e_n = n0 + e_cc * 8;
-  float e_bias[8];
+  constexpr bool FIXED_CC = 256 % CPR == 0;
+  auto e_cc_of = [&](int i) { return (tid + 256 * i) % CPR; };
+  auto e_row_of = [&](int i) { return (tid + 256 * i) / CPR; };
+  // (otherwise the bias is read per chunk in the epilogue: no registers held over the K loop)
+  auto load_bias = [&](int i, float (&b)[8]) {
+    const int en = n0 + e_cc_of(i) * 8;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) e_bias[e] = 0.f;
-  if (p.bias && e_n < p.Cout) {
-    const f32x4 b0 = *reinterpret_cast<const f32x4*>(p.bias + e_n);
-    const f32x4 b1 = *reinterpret_cast<const f32x4*>(p.bias + e_n + 4);
-    e_bias[0] = b0[0]; e_bias[1] = b0[1]; e_bias[2] = b0[2]; e_bias[3] = b0[3];
-    e_bias[4] = b1[0]; e_bias[5] = b1[1]; e_bias[6] = b1[2]; e_bias[7] = b1[3];
-  }
+    for (int e = 0; e < 8; ++e) b[e] = 0.f;
+    if (p.bias && en < p.Cout) {
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(p.bias + en);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(p.bias + en + 4);
+      b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2]; b[3] = b0[3];
+      b[4] = b1[0]; b[5] = b1[1]; b[6] = b1[2]; b[7] = b1[3];
+    }
+  };
+  float e_bias[8];
+  if constexpr (FIXED_CC) load_bias(0, e_bias);
   u32x4 e_res[CPT];
   if (p.res) {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const int m = m0 + e_row0 + E_ROWS * i;
-      const bool ok = m < p.M && e_n < p.Cout;
-      e_res[i] = *reinterpret_cast<const u32x4*>(p.res + (ok ? (size_t)m * p.ldr + e_n : 0));
+      const int m = m0 + e_row_of(i), en = n0 + e_cc_of(i) * 8;
+      const bool ok = m < p.M && en < p.Cout;
+      e_res[i] = *reinterpret_cast<const u32x4*>(p.res + (ok ? (size_t)m * p.ldr + en : 0));
     }
   }
 
@@ -219,12 +236,13 @@ __global__ __launch_bounds__(256, (glds_occupancy<BM, BN>())) void conv_glds_ker
   const int act = p.act & 15;
 #pragma unroll
   for (int i = 0; i < CPT; ++i) {
-    const int row = e_row0 + E_ROWS * i;
-    const int m = m0 + row;
+    const int row = e_row_of(i), cc = e_cc_of(i);
+    const int m = m0 + row, e_n = n0 + cc * 8;
     if (m >= p.M || e_n >= p.Cout) continue;
-    const f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + e_cc * 8);
-    const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + e_cc * 8 + 4);
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + cc * 8);
+    const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + cc * 8 + 4);
     float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    if constexpr (!FIXED_CC) load_bias(i, e_bias);
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] += e_bias[e];
     if (p.res && !post) {
@@ -289,6 +307,10 @@ extern "C" int aiko_conv_glds(const void* x, const void* w, const float* bias, c
     conv_glds_kernel<64, 64><<<grid, block, 0, stream>>>(p, z);
   } else if (bm == 64 && bn == 128) {
     conv_glds_kernel<64, 128><<<grid, block, 0, stream>>>(p, z);
+  } else if (bm == 128 && bn == 80) {              // exact-N tiles (YOLO's 80-class head convs)
+    conv_glds_kernel<128, 80, 4, 1><<<grid, block, 0, stream>>>(p, z);
+  } else if (bm == 256 && bn == 80) {
+    conv_glds_kernel<256, 80, 4, 1><<<grid, block, 0, stream>>>(p, z);
   } else {
     return -1;
   }

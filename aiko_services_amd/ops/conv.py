@@ -279,6 +279,10 @@ WIDE_PERS_TILES = ((256, 256), (256, 128), (128, 256))
 # these channel counts — the YOLO head's 80-class and 64 + 80 box/class convs — instead of
 # rounding N up to a 128 / 192 tile; odd 16-channel block counts end in an 8-byte store)
 EXACT_N = (80, 144)
+# exact-N tiles of the LDS-DMA igemm (variant 1, conv_glds.hip: 4 x 1 waves, each all N columns)
+# for N = 80 layers whose 80-channel input (Cc = 80) rules out every 64-channel-block kernel: the
+# YOLOv8 class branch (3x3 80 -> 80, 1x1 80 -> 80), where a 128-wide tile wastes 37.5 % of its lanes
+GLDS_EXACT_N = (80,)
 # variant 9: the same kernel at 2-3 workgroups per CU (short-K, bandwidth-bound layers)
 WIDE_OCC_TILES = ((128, 128), (256, 64), (128, 64), (64, 128), (64, 64))
 # variant 11: the same kernel with 32-deep K blocks in a 4-slot ring (three blocks in flight
@@ -469,6 +473,8 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, p
             cands.append((1, 32, 17))        # variant 17: persistent row stream (80-wide 32 -> 32 3x3)
     else:
         cands = [t + (0,) for t in TILES] + [t + (1,) for t in TILES]
+        if cout in GLDS_EXACT_N:
+            cands += [t + (1,) for t in ((128, cout), (256, cout))]
         if buf_ok:
             cands += [t + (2,) for t in TILES + BUF_WIDE_TILES] + [t + (3,) for t in BUF_OCC_TILES]
             cands += [t + (4,) for t in PERSIST_TILES]

@@ -37,6 +37,11 @@ def _nhwc(x_nchw):
     (1, 9, 11, 40, 24, 3, 1, 1, "silu", False, (64, 64, 1)),
     (2, 20, 20, 48, 64, 3, 2, 1, "silu", False, (128, 64, 1)),
     (2, 20, 20, 16, 64, 3, 1, 1, "relu", False, (128, 128, 1)),
+    # exact-N LDS-DMA tiles (4 x 1 waves, N = 80: the YOLO class branch, Cc = 80 input)
+    (2, 20, 20, 80, 80, 3, 1, 1, "silu", False, (128, 80, 1)),
+    (1, 13, 17, 80, 80, 1, 1, 0, None, True, (128, 80, 1)),
+    (2, 20, 20, 80, 80, 3, 1, 1, "silu", True, (256, 80, 1)),
+    (1, 9, 11, 64, 80, 3, 2, 1, "relu", False, (256, 80, 1)),
     # buffer-LDS-DMA variant (Cc % 64 == 0: padding by out-of-range buffer reads)
     (2, 56, 56, 64, 256, 1, 1, 0, "relu", True, (128, 128, 2)),
     (2, 56, 56, 64, 64, 3, 1, 1, "relu", False, (128, 64, 2)),
