@@ -147,4 +147,58 @@ __device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
   return __builtin_elementwise_fma(h, erf, h);
 }
 
+// GELU with a transcendental-free erf, for epilogues that quantise to e4m3 right after (the
+// fc1 -> fc2 MX-fp8 hand-off): erf(x / sqrt2) ~= xc Q(xc^2), xc = clamp(x, +-3 sqrt2), Q a
+// degree-8 least-squares fit (|GELU error| <= 5.2e-5 absolute for every x in fp32 evaluation,
+// far below e4m3's 2^-4 relative step).  Only packed-fp32 multiplies / FMAs: gelu_erf2 spends
+// a v_rcp and a v_exp (quarter-rate transcendentals) per element, which made the fc1 epilogue
+// VALU-bound.
+__device__ __forceinline__ f32x2 gelu_poly2(f32x2 x) {
+  constexpr float C = 4.242640687f;
+  const f32x2 xc = {fminf(fmaxf(x[0], -C), C), fminf(fmaxf(x[1], -C), C)};
+  const f32x2 s = xc * xc;
+  f32x2 q = __builtin_elementwise_fma(f32x2{1.124738094e-10f, 1.124738094e-10f}, s,
+                                      f32x2{-1.074885849e-08f, -1.074885849e-08f});
+  q = __builtin_elementwise_fma(q, s, f32x2{4.542003143e-07f, 4.542003143e-07f});
+  q = __builtin_elementwise_fma(q, s, f32x2{-1.130945777e-05f, -1.130945777e-05f});
+  q = __builtin_elementwise_fma(q, s, f32x2{1.874421164e-04f, 1.874421164e-04f});
+  q = __builtin_elementwise_fma(q, s, f32x2{-2.220934090e-03f, -2.220934090e-03f});
+  q = __builtin_elementwise_fma(q, s, f32x2{1.964535859e-02f, 1.964535859e-02f});
+  q = __builtin_elementwise_fma(q, s, f32x2{-1.327118241e-01f, -1.327118241e-01f});
+  q = __builtin_elementwise_fma(q, s, f32x2{7.978177156e-01f, 7.978177156e-01f});
+  const f32x2 h = f32x2{0.5f, 0.5f} * x;
+  return __builtin_elementwise_fma(h, xc * q, h);
+}
+
+// gelu_poly2 over N independent pairs with the Horner steps interleaved across the pairs: a
+// packed-fp32 op reading the previous one's result needs a wait state, so one chain at a time
+// issued an s_nop after every FMA
+template <int N>
+__device__ __forceinline__ void gelu_poly_n(f32x2 (&x)[N]) {
+  constexpr float C = 4.242640687f;
+  constexpr float Q[9] = {7.978177156e-01f, -1.327118241e-01f, 1.964535859e-02f, -2.220934090e-03f,
+                          1.874421164e-04f, -1.130945777e-05f, 4.542003143e-07f, -1.074885849e-08f,
+                          1.124738094e-10f};
+  f32x2 xc[N], s[N], q[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    xc[i] = f32x2{fminf(fmaxf(x[i][0], -C), C), fminf(fmaxf(x[i][1], -C), C)};
+    s[i] = xc[i] * xc[i];
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) q[i] = __builtin_elementwise_fma(f32x2{Q[8], Q[8]}, s[i], f32x2{Q[7], Q[7]});
+#pragma unroll
+  for (int k = 6; k >= 0; --k) {
+    __builtin_amdgcn_sched_barrier(0);             // keep the steps interleaved (no per-chain nops)
+#pragma unroll
+    for (int i = 0; i < N; ++i) q[i] = __builtin_elementwise_fma(q[i], s[i], f32x2{Q[k], Q[k]});
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const f32x2 h = f32x2{0.5f, 0.5f} * x[i];
+    x[i] = __builtin_elementwise_fma(h, xc[i] * q[i], h);
+  }
+}
+
 }  // namespace aiko

@@ -1004,6 +1004,12 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers_kernel(Fp8GemmParams p, 
 // Epilogue of one 16-row fragment group of the persistent kernels' 128 x 64 wave tile: both
 // 32-column fragment pairs (lane l: row l & 15, eight consecutive columns after the permlane
 // swap), per-channel scale + bias from LDS, activation, bf16 or MX-fp8 store.
+// AIKO_FP8_POLY_GELU=0 at build time (-DAIKO_FP8_POLY_GELU=0): the erf GELU in the MX-out epilogue
+#ifndef AIKO_FP8_POLY_GELU
+#define AIKO_FP8_POLY_GELU 1
+#endif
+constexpr bool kFp8PolyGelu = AIKO_FP8_POLY_GELU != 0;
+
 __device__ __forceinline__ float fp8_h2f(uint32_t bits) {
   return (float)__builtin_bit_cast(_Float16, (unsigned short)bits);
 }
@@ -1056,6 +1062,14 @@ __device__ __forceinline__ void fp8_pers_epi(const Fp8GemmParams& p, const f32x4
     } else if constexpr (ACT == 2) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = silu(v[e]);
+    } else if constexpr (ACT == 3 && MXO && kFp8PolyGelu) {   // MX-fp8 out: transcendental-free GELU
+      f32x2 g[4] = {{v[0], v[1]}, {v[2], v[3]}, {v[4], v[5]}, {v[6], v[7]}};
+      gelu_poly_n<4>(g);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[2 * e] = g[e][0];
+        v[2 * e + 1] = g[e][1];
+      }
     } else if constexpr (ACT == 3) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
