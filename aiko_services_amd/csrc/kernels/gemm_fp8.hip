@@ -1010,6 +1010,15 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers_kernel(Fp8GemmParams p, 
 #endif
 constexpr bool kFp8PolyGelu = AIKO_FP8_POLY_GELU != 0;
 
+// four fp32 -> e4m3 bytes (a in byte 0) divided by the power-of-two MX scale, in two
+// v_cvt_scalef32_pk_fp8_f32 (gfx950)
+__device__ __forceinline__ unsigned mx_pack4(float a, float b, float c, float d, float scale) {
+  typedef __attribute__((ext_vector_type(2))) short v2s;
+  v2s r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(v2s{0, 0}, a, b, scale, false);
+  r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(r, c, d, scale, true);
+  return __builtin_bit_cast(unsigned, r);
+}
+
 __device__ __forceinline__ float fp8_h2f(uint32_t bits) {
   return (float)__builtin_bit_cast(_Float16, (unsigned short)bits);
 }
@@ -1099,16 +1108,10 @@ __device__ __forceinline__ void fp8_pers_epi(const Fp8GemmParams& p, const f32x4
         amax = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
       }
       const int ex = mx_exponent(amax);
-      const float inv = __uint_as_float((uint32_t)(127 - ex) << 23);
-      unsigned w0 = 0u, w1 = 0u;
-      w0 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[0] * inv, -448.f), 448.f),
-                                           fminf(fmaxf(v[1] * inv, -448.f), 448.f), w0, false);
-      w0 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[2] * inv, -448.f), 448.f),
-                                           fminf(fmaxf(v[3] * inv, -448.f), 448.f), w0, true);
-      w1 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[4] * inv, -448.f), 448.f),
-                                           fminf(fmaxf(v[5] * inv, -448.f), 448.f), w1, false);
-      w1 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(v[6] * inv, -448.f), 448.f),
-                                           fminf(fmaxf(v[7] * inv, -448.f), 448.f), w1, true);
+      // one v_cvt_scalef32_pk_fp8_f32 per pair (divides by the 2^ex scale; |v| / 2^ex <= 448 by
+      // the exponent's choice, so no clamp): scripts/probe/cvt_scale_probe.hip
+      const float sc2 = __uint_as_float((uint32_t)(ex + 127) << 23);
+      const unsigned w0 = mx_pack4(v[0], v[1], v[2], v[3], sc2), w1 = mx_pack4(v[4], v[5], v[6], v[7], sc2);
       typedef __attribute__((ext_vector_type(2))) unsigned u32x2v;
       const uint32_t qoff = live ? (uint32_t)((long)m * p.ldq + n) : 0x80000000u;
       __builtin_amdgcn_raw_buffer_store_b64(u32x2v{w0, w1}, ry, qoff, 0, 0);
