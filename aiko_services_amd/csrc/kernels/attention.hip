@@ -102,7 +102,16 @@ __device__ __forceinline__ int v_off(int row, int col) {
 //   * the row sums come out of the MFMA pipe: one extra 16x16x32 MFMA per P fragment with an
 //     all-ones A operand (rowsum(P) in every row of the result, no fp32 add chain and no
 //     end-of-kernel reduction), summing the same bf16 P that enters O.
-template <int NW, int VPRE, int REG = 0, int SM = 0>
+// VA = 1: the V^T fragments are read with ds_read_b64_tr_b16 issued from inline asm and retired
+// by an explicit lgkmcnt(0) tied to them.  Through the builtin, hipcc's waitcnt pass treats the
+// transposed read as possibly aliasing the in-flight LDS-DMA (buffer_load ... lds) writes and puts
+// an s_waitcnt vmcnt(0) in front of it every tile — draining the three-tile K/V prefetch, so each
+// tile waited for the DMA issued at its own top.  The slot being read was retired by the tile's
+// counted vmcnt + barrier, which is the only ordering these reads need.  Measured (round 5,
+// scripts/r5_attn_va.sh, B = 14): 129.7-133.7 us vs 130.4-132.8 us for the builtin reads — the
+// K/V tiles are L2 hits (the query blocks of a head share them), so the drained prefetch was
+// not on the critical path; variants 16-18, opt-in.
+template <int NW, int VPRE, int REG = 0, int SM = 0, int VA = 0>
 __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p) {
   constexpr int NT = 64 * NW;
   constexpr int QB = 32 * NW;
@@ -284,11 +293,29 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const int r0 = 32 * ks + 4 * g + trq;
-        const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) v4i16*)(vb + v_off(r0, d * 16 + 4 * trp)));
-        const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) v4i16*)(vb + v_off(r0 + 16, d * 16 + 4 * trp)));
-        vfr[d][ks] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        if constexpr (VA) {
+          const uint32_t a0 = (uint32_t)reinterpret_cast<uintptr_t>(vb + v_off(r0, d * 16 + 4 * trp));
+          const uint32_t a1 = (uint32_t)reinterpret_cast<uintptr_t>(vb + v_off(r0 + 16, d * 16 + 4 * trp));
+          v4i16 lo, hi;
+          asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a0) : "memory");
+          asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(a1) : "memory");
+          vfr[d][ks] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        } else {
+          const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) v4i16*)(vb + v_off(r0, d * 16 + 4 * trp)));
+          const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) v4i16*)(vb + v_off(r0 + 16, d * 16 + 4 * trp)));
+          vfr[d][ks] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+      }
+    };
+    // VA: every V read issued so far has landed (no use of the fragments above this point)
+    auto wait_v = [&](int d0, int d1) {
+      if constexpr (VA) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        for (int d = d0; d < d1; ++d)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) asm volatile("" : "+v"(vfr[d][ks]));
       }
     };
 
@@ -442,9 +469,13 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
 
     // O^T += V^T P^T (fragments read above / here)
     if constexpr (SM != 2) {
+    if constexpr (VA) wait_v(0, VPRE);
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-      if (d >= VPRE) read_v(d);
+      if (d >= VPRE) {
+        read_v(d);
+        wait_v(d, d + 1);
+      }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -645,9 +676,9 @@ extern "C" int aiko_attn_fwd(const void* q, const void* k, const void* v, void* 
       return 0;
     return n;
   }();
-  auto launch = [&](auto nw_tag, auto vpre_tag, auto reg_tag, auto sm_tag) {
+  auto launch = [&](auto nw_tag, auto vpre_tag, auto reg_tag, auto sm_tag, auto va_tag) {
     constexpr int NW = decltype(nw_tag)::value, VPRE = decltype(vpre_tag)::value;
-    constexpr int REG = decltype(reg_tag)::value, SM = decltype(sm_tag)::value;
+    constexpr int REG = decltype(reg_tag)::value, SM = decltype(sm_tag)::value, VA = decltype(va_tag)::value;
     constexpr int QB = 32 * NW;
     p.nqb = (T + QB - 1) / QB;
     const long items = (long)p.nqb * H * B;
@@ -667,14 +698,16 @@ extern "C" int aiko_attn_fwd(const void* q, const void* k, const void* v, void* 
           p.cnt = static_cast<int*>(work);
           p.part = reinterpret_cast<float*>(static_cast<char*>(work) + cnt_b);
           dim3 grid((unsigned)(8 * (p.split_full + (long)r * sp))), block(64 * NW);
-          aiko::attn_fwd_kernel<NW, VPRE, REG, SM><<<grid, block, 0, stream>>>(p);
+          aiko::attn_fwd_kernel<NW, VPRE, REG, SM, VA><<<grid, block, 0, stream>>>(p);
           return;
         }
       }
     }
     dim3 grid(p.nqb, H, B), block(64 * NW);
-    aiko::attn_fwd_kernel<NW, VPRE, REG, SM><<<grid, block, 0, stream>>>(p);
+    aiko::attn_fwd_kernel<NW, VPRE, REG, SM, VA><<<grid, block, 0, stream>>>(p);
   };
+  using A0 = std::integral_constant<int, 0>;
+  using A1 = std::integral_constant<int, 1>;
   using R0 = std::integral_constant<int, 0>;
   using R1 = std::integral_constant<int, 1>;
   using I8 = std::integral_constant<int, 8>;
@@ -682,21 +715,24 @@ extern "C" int aiko_attn_fwd(const void* q, const void* k, const void* v, void* 
   using V0 = std::integral_constant<int, 0>;
   using V2 = std::integral_constant<int, 2>;
   switch (variant) {
-    case 1: launch(I8{}, V2{}, R0{}, R0{}); break;
-    case 2: launch(I8{}, std::integral_constant<int, 4>{}, R0{}, R0{}); break;
-    case 3: launch(I4{}, V0{}, R0{}, R0{}); break;
-    case 4: launch(I4{}, V2{}, R0{}, R0{}); break;
-    case 5: launch(I8{}, V0{}, R1{}, R0{}); break;
-    case 6: launch(I8{}, V2{}, R1{}, R0{}); break;
-    case 7: launch(I4{}, V0{}, R1{}, R0{}); break;
-    case 8: launch(I4{}, V2{}, R1{}, R0{}); break;
-    case 10: launch(I8{}, V0{}, R0{}, R0{}); break;        // round-2 softmax
-    case 11: launch(I8{}, V2{}, R0{}, R1{}); break;
-    case 12: launch(I8{}, V0{}, R1{}, R1{}); break;
-    case 13: launch(I4{}, V0{}, R0{}, R1{}); break;
-    case 14: launch(I4{}, V2{}, R1{}, R1{}); break;
-    case 15: launch(I8{}, V0{}, R0{}, std::integral_constant<int, 2>{}); break;   // ping-pong query tiles
-    default: launch(I8{}, V0{}, R0{}, R1{}); break;
+    case 1: launch(I8{}, V2{}, R0{}, R0{}, A0{}); break;
+    case 2: launch(I8{}, std::integral_constant<int, 4>{}, R0{}, R0{}, A0{}); break;
+    case 3: launch(I4{}, V0{}, R0{}, R0{}, A0{}); break;
+    case 4: launch(I4{}, V2{}, R0{}, R0{}, A0{}); break;
+    case 5: launch(I8{}, V0{}, R1{}, R0{}, A0{}); break;
+    case 6: launch(I8{}, V2{}, R1{}, R0{}, A0{}); break;
+    case 7: launch(I4{}, V0{}, R1{}, R0{}, A0{}); break;
+    case 8: launch(I4{}, V2{}, R1{}, R0{}, A0{}); break;
+    case 10: launch(I8{}, V0{}, R0{}, R0{}, A0{}); break;        // round-2 softmax
+    case 11: launch(I8{}, V2{}, R0{}, R1{}, A0{}); break;
+    case 12: launch(I8{}, V0{}, R1{}, R1{}, A0{}); break;
+    case 13: launch(I4{}, V0{}, R0{}, R1{}, A0{}); break;
+    case 14: launch(I4{}, V2{}, R1{}, R1{}, A0{}); break;
+    case 15: launch(I8{}, V0{}, R0{}, std::integral_constant<int, 2>{}, A0{}); break;   // ping-pong query tiles
+    case 16: launch(I8{}, V0{}, R0{}, R1{}, A1{}); break;   // asm V reads, per d-block wait
+    case 17: launch(I8{}, std::integral_constant<int, 4>{}, R0{}, R1{}, A1{}); break;   // all V reads before the softmax
+    case 18: launch(I8{}, V2{}, R0{}, R1{}, A1{}); break;
+    default: launch(I8{}, V0{}, R0{}, R1{}, A0{}); break;
   }
   return (int)hipGetLastError();
 }
