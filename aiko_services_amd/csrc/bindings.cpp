@@ -79,6 +79,9 @@ int aiko_gemm_fp8_ln(const void* a, const void* b, const float* sb, const float*
                      int N, int K, int lda, int ldy, int ldr, int act, const void* zero, const void* amx, int mxr,
                      void* yq, void* ysc, int ldq, int ysr, float* st, const float* cs, int sts, int stp, int ln_d,
                      float ln_eps, int ln, hipStream_t stream);
+int aiko_c2f_fused(const void* x, int ldx, const void* w1, const float* b1, int k1, const void* wa, const float* ba,
+                   int ka, const void* wb, const float* bb, int kb, const void* w2, const float* b2, int k2, void* y, int ldy,
+                   int B, int H, int W, int CI, int C, int CO, int shortcut, int rb, hipStream_t stream);
 int aiko_rowstats_mx(const void* x, int ldx, void* q, int ldq, void* qsc, int ysr, float* st, int sts, int P, int M,
                      int D, hipStream_t stream);
 int aiko_linear_splitk(const void* x, const void* w, const float* bias, float* part, void* y, int M, int N, int K,
@@ -483,6 +486,41 @@ void conv_chain_out(const at::Tensor& A, const at::Tensor& W1, const at::Tensor&
                                Y.data_ptr(), W2.data_ptr(), b2.data_ptr<float>(), Z.data_ptr(),
                                dual ? R.data_ptr() : nullptr, M, K1, N1, N2, grid, cur_stream()),
                "conv_chain");
+}
+
+// A YOLOv8 C2f block with one bottleneck in one launch (c2f_fused.hip): x [B, H, W, >= CI] ->
+// y [B, H, W, >= CO]; weights / biases as the four ConvSpecs hold them (cv1, conv a, conv b, cv2:
+// [Cout, K padded] bf16 + fp32 biases, SiLU everywhere).  Shapes without an instantiation fail.
+void c2f_fused_out(const at::Tensor& x, const at::Tensor& w1, const at::Tensor& b1, const at::Tensor& wa,
+                   const at::Tensor& ba, const at::Tensor& wb, const at::Tensor& bb, const at::Tensor& w2,
+                   const at::Tensor& b2, at::Tensor& y, int64_t ci, bool shortcut, int64_t rb) {
+  for (const at::Tensor* t : {&x, &w1, &b1, &wa, &ba, &wb, &bb, &w2, &b2, (const at::Tensor*)&y}) check_cuda(*t, "c2f operand");
+  for (const at::Tensor* t : {&x, &w1, &wa, &wb, &w2, (const at::Tensor*)&y})
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16, "aiko.c2f_fused_out: bf16 activations / weights");
+  for (const at::Tensor* t : {&b1, &ba, &bb, &b2})
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "aiko.c2f_fused_out: fp32 contiguous biases");
+  for (const at::Tensor* t : {&w1, &wa, &wb, &w2})
+    TORCH_CHECK(t->dim() == 2 && t->is_contiguous() && t->size(1) % 8 == 0, "aiko.c2f_fused_out: weights [Cout, K] contiguous");
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.size(0) == y.size(0) && x.size(1) == y.size(1) && x.size(2) == y.size(2),
+              "aiko.c2f_fused_out: x, y [B, H, W, C]");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2);
+  const int64_t C = wa.size(0), CO = w2.size(0), CI = ci;
+  TORCH_CHECK(CI % 32 == 0 && w1.size(1) >= CI, "aiko.c2f_fused_out: cv1 K (input channels) a multiple of 32");
+  TORCH_CHECK(w1.size(0) == 2 * C && wb.size(0) == C && wa.size(1) >= 9 * C && wb.size(1) >= 9 * C &&
+                  ((9 * C + 31) / 32) * 32 <= wa.size(1) && ((9 * C + 31) / 32) * 32 <= wb.size(1) && w2.size(1) >= 3 * C &&
+                  b1.numel() == 2 * C && ba.numel() == C && bb.numel() == C && b2.numel() == CO,
+              "aiko.c2f_fused_out: inconsistent cv1 / bottleneck / cv2 shapes");
+  const int64_t ldx = x.stride(2), ldy = y.stride(2);
+  TORCH_CHECK(x.stride(3) == 1 && y.stride(3) == 1 && x.stride(2) == ldx && y.stride(2) == ldy &&
+                  x.stride(1) == W * ldx && y.stride(1) == W * ldy && x.stride(0) == H * W * ldx &&
+                  y.stride(0) == H * W * ldy && ldx % 8 == 0 && ldy % 4 == 0 && x.size(3) >= CI && y.size(3) >= CO &&
+                  reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(y.data_ptr()) % 8 == 0,
+              "aiko.c2f_fused_out: NHWC views with 16-B aligned pixels");
+  check_launch(aiko_c2f_fused(x.data_ptr(), (int)ldx, w1.data_ptr(), b1.data_ptr<float>(), (int)w1.size(1), wa.data_ptr(),
+                              ba.data_ptr<float>(), (int)wa.size(1), wb.data_ptr(), bb.data_ptr<float>(), (int)wb.size(1),
+                              w2.data_ptr(), b2.data_ptr<float>(), (int)w2.size(1), y.data_ptr(), (int)ldy, (int)B, (int)H,
+                              (int)W, (int)CI, (int)C, (int)CO, shortcut ? 1 : 0, (int)rb, cur_stream()),
+               "c2f_fused");
 }
 
 // A whole ResNet stage-1 bottleneck in one launch (bneck_fused.hip): x [B, H, 56, cin] ->
@@ -1372,6 +1410,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("rownorm_quant_out(Tensor x, Tensor? gamma, Tensor? beta, float eps, Tensor(a!)? yb, Tensor(b!)? q, Tensor(c!)? qs) -> ()");
   m.def("gemm_fp8_ln_out(Tensor a, Tensor amx, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!)? y, Tensor(b!)? yq, Tensor(c!)? ysc, Tensor(d!) st, Tensor? cs, int ln, int act, int ln_d, float eps, Tensor zero) -> ()");
   m.def("rowstats_mx_out(Tensor x, Tensor(a!) q, Tensor(b!) qsc, Tensor(c!) st) -> ()");
+  m.def("c2f_fused_out(Tensor x, Tensor w1, Tensor b1, Tensor wa, Tensor ba, Tensor wb, Tensor bb, Tensor w2, Tensor b2, Tensor(a!) y, int ci, bool shortcut, int rb) -> ()");
   m.def("linear_splitk_out(Tensor x, Tensor w, Tensor? bias, Tensor(a!) part, Tensor(b!) y, int K, int S) -> ()");
   m.def("attn_fwd_out(Tensor q, Tensor k, Tensor v, Tensor(a!) o, int B, int H, int T, int Tpad, float scale, Tensor(b!)? work=None, Tensor(c!)? oq=None, Tensor(d!)? osc=None) -> ()");
   m.def("logmel_out(Tensor audio, Tensor mel, Tensor mel_range, int n_fft, int hop, int F, Tensor(a!) work, Tensor(b!) gmax, Tensor(c!) dst, int rows, int pad) -> ()");
@@ -1409,6 +1448,7 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("rownorm_quant_out", &rownorm_quant_out);
   m.impl("gemm_fp8_ln_out", &gemm_fp8_ln_out);
   m.impl("rowstats_mx_out", &rowstats_mx_out);
+  m.impl("c2f_fused_out", &c2f_fused_out);
   m.impl("attn_fwd_out", &attn_fwd_out);
   m.impl("linear_splitk_out", &linear_splitk_out);
   m.impl("logmel_out", &logmel_out);

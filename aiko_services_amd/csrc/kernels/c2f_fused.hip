@@ -1,0 +1,269 @@
+// Fused YOLOv8 C2f block (one bottleneck, n = 1) as a row stream, for the wide, narrow-channel
+// layers where the unfused chain is bound by HBM round trips (YOLOv8-n l2 at 160 x 160: cv1 1x1
+// 32 -> 32, bottleneck 3x3 16 -> 16 twice + shortcut, cv2 1x1 48 -> 32 — four launches moving
+// ~730 MB at B = 64, against 210 MB for x in and y out):
+//
+//   [a | s] = silu(cv1(x));  t = silu(conv_a(s));  c = silu(conv_b(t)) (+ s);  y = silu(cv2([a, s, c]))
+//
+// (Ultralytics C2f / Bottleneck, /root/reference/src/aiko_services/examples/yolo/yolo.py runs the
+// packaged model).  One workgroup streams a band of RB output rows of one image,
+// full width W, through LDS row rings; one step per row, ONE barrier per step, every phase of a
+// step reading only rows finished in earlier steps:
+//
+//   step v:  cv1(x row v+2) -> A / S rings          (x fragments loaded from HBM a step ahead)
+//            conv_a(S rows v-1..v+1) -> T row v
+//            conv_b(T rows v-3..v-1) + S row v-2 -> c (registers)
+//            cv2(A, S rows v-2 | c) -> y row v-2    (c enters as a 16x16x16 MFMA operand straight
+//                                                     from the conv_b accumulators: same layout)
+//   rings: A, S 5 rows (S with a zero pixel each side), T 4 rows; rows outside the image are zero.
+//
+// Every product is transposed (weights on the MFMA A side, 16 output channels x 32 K, resident
+// in registers for the whole launch): each lane's accumulator holds 4 consecutive channels of
+// one pixel, so results go to the LDS row images (and y to HBM) as 8-byte pieces with bias and
+// SiLU applied in registers.  The 3x3 convs take their K = 9 taps x 16 channels in chunks of two
+// taps (lane groups 0-1: tap 2k, 2-3: tap 2k+1; the tenth tap has zero weights and re-reads tap
+// 8, so the products stay finite).  Wave w owns pixel tiles PT w .. of 16 pixels.
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+
+namespace aiko {
+
+namespace c2f {
+typedef __attribute__((ext_vector_type(4))) short v4s;
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+
+__device__ __forceinline__ f32x4 silu4(f32x4 v) {
+  return f32x4{silu(v[0]), silu(v[1]), silu(v[2]), silu(v[3])};
+}
+__device__ __forceinline__ u32x2 pack4(f32x4 v) { return u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])}; }
+__device__ __forceinline__ f32x4 unpack4(u32x2 u) {
+  return f32x4{__uint_as_float(u[0] << 16), __uint_as_float(u[0] & 0xffff0000u), __uint_as_float(u[1] << 16),
+               __uint_as_float(u[1] & 0xffff0000u)};
+}
+}  // namespace c2f
+
+struct C2fParams {
+  const bf16_t* x;       // [B][H][W][ldx] (CI channels used)
+  const bf16_t* w1;      // cv1 [2C][k1]        (1x1, K = CI)
+  const float* b1;
+  const bf16_t* wa;      // bottleneck conv a [C][ka] (3x3, K = 9 C in (r, s, c) order, zero-padded)
+  const float* ba;
+  const bf16_t* wb;      // bottleneck conv b
+  const float* bb;
+  const bf16_t* w2;      // cv2 [CO][k2]         (1x1, K = 3C: a | s | c)
+  const float* b2;
+  bf16_t* y;             // [B][H][W][ldy] (CO channels written)
+  int B, H, ldx, ldy, k1, ka, kb, k2, rb;
+};
+
+// W: row width (pixels), CI / C / CO: channels (C = 16: two taps per 32-wide K chunk), SC: the
+// bottleneck's shortcut.  Block = W / 32 waves (two 16-pixel tiles each).
+template <int W, int CI, int C, int CO, bool SC>
+__global__ __launch_bounds__(W * 2, 1) void c2f_fused_kernel(C2fParams p) {
+  using namespace c2f;
+  static_assert(C == 16 && CI % 32 == 0 && CO % 16 == 0 && W % 32 == 0, "instantiated shapes");
+  constexpr int NWAVE = W / 32, PT = 2;               // waves, pixel tiles per wave
+  constexpr int KS1 = CI / 32;                         // cv1 K steps
+  constexpr int N1 = 2 * C / 16;                       // cv1 output-channel tiles (a: < C / 16)
+  constexpr int KC3 = (9 * C + 31) / 32;               // 3x3 K chunks (5)
+  constexpr int N2 = CO / 16;
+  constexpr int SW = W + 2;                            // S / T row images: one zero pixel each side
+  constexpr int SROW = SW * C * 2, TROW = SW * C * 2, AROW = W * C * 2;   // bytes
+  constexpr int NS = 5, NA = 5, NT = 4;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NS * SROW + NA * AROW + NT * TROW];
+  unsigned char* const sring = smem;
+  unsigned char* const aring = sring + NS * SROW;
+  unsigned char* const tring = aring + NA * AROW;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nb = p.H / p.rb;
+  const int img = blockIdx.x / nb, r0 = (blockIdx.x % nb) * p.rb, r1 = r0 + p.rb;
+  const int px0 = wave * 32;                           // this wave's first pixel
+
+  // ---- weights (A operands) and biases, resident ----
+  bf16x8 w1f[N1][KS1], waf[KC3], wbf[KC3], w2f[N2];
+  v4s w2c[N2];
+#pragma unroll
+  for (int n = 0; n < N1; ++n)
+#pragma unroll
+    for (int k = 0; k < KS1; ++k)
+      w1f[n][k] = *reinterpret_cast<const bf16x8*>(p.w1 + (long)(16 * n + fr) * p.k1 + 32 * k + 8 * fq);
+#pragma unroll
+  for (int k = 0; k < KC3; ++k) {
+    waf[k] = *reinterpret_cast<const bf16x8*>(p.wa + (long)fr * p.ka + 32 * k + 8 * fq);
+    wbf[k] = *reinterpret_cast<const bf16x8*>(p.wb + (long)fr * p.kb + 32 * k + 8 * fq);
+  }
+#pragma unroll
+  for (int n = 0; n < N2; ++n) {
+    w2f[n] = *reinterpret_cast<const bf16x8*>(p.w2 + (long)(16 * n + fr) * p.k2 + 8 * fq);
+    w2c[n] = *reinterpret_cast<const v4s*>(p.w2 + (long)(16 * n + fr) * p.k2 + 2 * C + 4 * fq);
+  }
+  f32x4 b1v[N1], bav, bbv, b2v[N2];
+#pragma unroll
+  for (int n = 0; n < N1; ++n) b1v[n] = *reinterpret_cast<const f32x4*>(p.b1 + 16 * n + 4 * fq);
+  bav = *reinterpret_cast<const f32x4*>(p.ba + 4 * fq);
+  bbv = *reinterpret_cast<const f32x4*>(p.bb + 4 * fq);
+#pragma unroll
+  for (int n = 0; n < N2; ++n) b2v[n] = *reinterpret_cast<const f32x4*>(p.b2 + 16 * n + 4 * fq);
+
+  // zero the S / T border pixels of every ring slot (never written by the row phases)
+  for (int i = tid; i < (NS + NT) * 2 * (C / 8); i += NWAVE * 64) {
+    const int slot = i / (2 * (C / 8)), rem = i % (2 * (C / 8));
+    const int side = rem / (C / 8), piece = rem % (C / 8);
+    unsigned char* base = slot < NS ? sring + slot * SROW : tring + (slot - NS) * TROW;
+    *reinterpret_cast<u32x4*>(base + (side ? (W + 1) : 0) * C * 2 + piece * 16) = u32x4{0u, 0u, 0u, 0u};
+  }
+
+  // 3x3 B-fragment geometry of this lane for chunk k: tap q = 2k + (fq >> 1) (tap 9 -> tap 8 with
+  // zero weights), channels 8 (fq & 1) .. +7; byte offset inside a row image (border included)
+  // and the tap's row (0..2 = dy + 1)
+  int toff[KC3], trow[KC3];
+#pragma unroll
+  for (int k = 0; k < KC3; ++k) {
+    int q = 2 * k + (fq >> 1);
+    if (q > 8) q = 8;
+    const int dy = q / 3, dx = q % 3 - 1;
+    trow[k] = dy;
+    toff[k] = ((fr + 1 + dx) * C + 8 * (fq & 1)) * 2;
+  }
+
+  // ---- x fragments of one row (B operand of cv1): pixel px0 + 16 t + fr, channels 32 k + 8 fq
+  bf16x8 xf[PT][KS1];
+  auto load_x = [&](int row) __attribute__((always_inline)) {
+    const bool ok = row >= 0 && row < p.H;
+    const bf16_t* src = p.x + (((long)img * p.H + (ok ? row : 0)) * W + px0 + fr) * p.ldx + 8 * fq;
+#pragma unroll
+    for (int t = 0; t < PT; ++t)
+#pragma unroll
+      for (int k = 0; k < KS1; ++k)
+        xf[t][k] = *reinterpret_cast<const bf16x8*>(src + (long)16 * t * p.ldx + 32 * k);
+  };
+
+  // cv1 of row `row` (x fragments in xf) -> A / S ring slots of that row (zeros outside the image)
+  auto cv1 = [&](int row) __attribute__((always_inline)) {
+    const bool ok = row >= 0 && row < p.H;
+    const int slot = (row + 2 * NS) % NS;
+#pragma unroll
+    for (int t = 0; t < PT; ++t) {
+      const int px = px0 + 16 * t + fr;
+#pragma unroll
+      for (int n = 0; n < N1; ++n) {
+        f32x4 acc = b1v[n];
+#pragma unroll
+        for (int k = 0; k < KS1; ++k) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[n][k], xf[t][k], acc, 0, 0, 0);
+        const u32x2 v = ok ? pack4(silu4(acc)) : u32x2{0u, 0u};
+        if (n < C / 16)        // a: channels 16 n + 4 fq
+          *reinterpret_cast<u32x2*>(aring + slot * AROW + (px * C + 16 * n + 4 * fq) * 2) = v;
+        else                   // s
+          *reinterpret_cast<u32x2*>(sring + slot * SROW + ((px + 1) * C + 16 * (n - C / 16) + 4 * fq) * 2) = v;
+      }
+    }
+  };
+
+  // 3x3 conv of the row centred on `row` from ring `ring` (slot stride `rstride`, NSL slots):
+  // returns the accumulators of pixel tile t (bias added, before the activation)
+  auto conv3 = [&](const unsigned char* ring, int nsl, int rstride, int row, const bf16x8 (&wf)[KC3], f32x4 bias,
+                   int t) __attribute__((always_inline)) {
+    const unsigned char* rows[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) rows[d] = ring + ((row - 1 + d + 4 * nsl) % nsl) * rstride + (px0 + 16 * t) * C * 2;
+    f32x4 acc = bias;
+#pragma unroll
+    for (int k = 0; k < KC3; ++k) {
+      const unsigned char* base = trow[k] == 0 ? rows[0] : (trow[k] == 1 ? rows[1] : rows[2]);
+      const bf16x8 b = *reinterpret_cast<const bf16x8*>(base + toff[k]);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[k], b, acc, 0, 0, 0);
+    }
+    return acc;
+  };
+
+  // ---- prologue: cv1 of rows r0-2 .. r0, x fragments of row r0+1 in flight
+  load_x(r0 - 2);
+  cv1(r0 - 2);
+  load_x(r0 - 1);
+  cv1(r0 - 1);
+  load_x(r0);
+  cv1(r0);
+  load_x(r0 + 1);
+
+  for (int v = r0 - 1; v <= r1 + 1; ++v) {
+    // rows of earlier steps complete (LDS only: the x loads and y stores stay in flight)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // cv1(v + 2): its x fragments were loaded last step; then the next row's go out
+    if (v + 2 <= r1 + 1) {
+      cv1(v + 2);
+      if (v + 3 <= r1 + 1) load_x(v + 3);
+    }
+    // conv_a(v) -> T row v
+    if (v <= r1) {
+      const bool ok = v >= 0 && v < p.H;
+      const int slot = (v + 2 * NT) % NT;
+#pragma unroll
+      for (int t = 0; t < PT; ++t) {
+        const f32x4 acc = conv3(sring, NS, SROW, v, waf, bav, t);
+        const u32x2 o = ok ? pack4(silu4(acc)) : u32x2{0u, 0u};
+        *reinterpret_cast<u32x2*>(tring + slot * TROW + ((px0 + 16 * t + fr + 1) * C + 4 * fq) * 2) = o;
+      }
+    }
+    // conv_b(v - 2) (+ shortcut) and cv2 -> y row v - 2
+    const int w = v - 2;
+    if (w >= r0 && w < r1) {
+      const int aslot = (w + 2 * NA) % NA, sslot = (w + 2 * NS) % NS;
+#pragma unroll
+      for (int t = 0; t < PT; ++t) {
+        const int px = px0 + 16 * t + fr;
+        f32x4 c = silu4(conv3(tring, NT, TROW, w, wbf, bbv, t));
+        if constexpr (SC) {
+          const u32x2 s = *reinterpret_cast<const u32x2*>(sring + sslot * SROW + ((px + 1) * C + 4 * fq) * 2);
+          const f32x4 sv = unpack4(s);
+          c = f32x4{c[0] + sv[0], c[1] + sv[1], c[2] + sv[2], c[3] + sv[3]};
+        }
+        const u32x2 cb = pack4(c);
+        const v4s cop = __builtin_bit_cast(v4s, cb);
+        // [a | s] chunk: lane groups 0-1 read a, 2-3 read s (channels 8 (fq & 1) .. +7)
+        const bf16x8 as = fq < 2 ? *reinterpret_cast<const bf16x8*>(aring + aslot * AROW + (px * C + 8 * fq) * 2)
+                                 : *reinterpret_cast<const bf16x8*>(sring + sslot * SROW + ((px + 1) * C + 8 * (fq - 2)) * 2);
+        bf16_t* yrow = p.y + (((long)img * p.H + w) * W + px) * p.ldy;
+#pragma unroll
+        for (int n = 0; n < N2; ++n) {
+          // two independent products summed on the VALU: chaining the 16x16x16 MFMA's SrcC on
+          // the 16x16x32 one's result read its first two accumulator VGPRs stale on gfx950
+          // (measured: output channels 4k, 4k+1 wrong, 4k+2, 4k+3 right)
+          const f32x4 acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f[n], as, b2v[n], 0, 0, 0);
+          const f32x4 acc2 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(w2c[n], cop, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          const f32x4 acc = {acc1[0] + acc2[0], acc1[1] + acc2[1], acc1[2] + acc2[2], acc1[3] + acc2[3]};
+          *reinterpret_cast<u32x2*>(yrow + 16 * n + 4 * fq) = pack4(silu4(acc));
+        }
+      }
+    }
+  }
+}
+
+}  // namespace aiko
+
+// x [B, H, W, ldx] -> y [B, H, W, ldy] through the fused C2f (n = 1); weights as the ConvSpecs
+// hold them ([Cout][K] bf16, K padded).  Returns -1 for shapes without an instantiation.
+extern "C" int aiko_c2f_fused(const void* x, int ldx, const void* w1, const float* b1, int k1, const void* wa,
+                              const float* ba, int ka, const void* wb, const float* bb, int kb, const void* w2,
+                              const float* b2, int k2, void* y, int ldy, int B, int H, int W, int CI, int C, int CO,
+                              int shortcut, int rb, hipStream_t stream) {
+  using namespace aiko;
+  if (rb <= 0 || H % rb || B <= 0) return -1;
+  C2fParams p;
+  p.x = static_cast<const bf16_t*>(x);
+  p.w1 = static_cast<const bf16_t*>(w1); p.b1 = b1;
+  p.wa = static_cast<const bf16_t*>(wa); p.ba = ba;
+  p.wb = static_cast<const bf16_t*>(wb); p.bb = bb;
+  p.w2 = static_cast<const bf16_t*>(w2); p.b2 = b2;
+  p.y = static_cast<bf16_t*>(y);
+  p.B = B; p.H = H; p.ldx = ldx; p.ldy = ldy; p.k1 = k1; p.ka = ka; p.kb = kb; p.k2 = k2; p.rb = rb;
+  const dim3 grid((unsigned)(B * (H / rb)));
+  if (W == 160 && CI == 32 && C == 16 && CO == 32 && shortcut) {
+    c2f_fused_kernel<160, 32, 16, 32, true><<<grid, dim3(320), 0, stream>>>(p);
+  } else {
+    return -1;
+  }
+  return (int)hipGetLastError();
+}

@@ -168,9 +168,31 @@ class YOLOv8(WeightsMixin):
         self._ws.clear()
 
     # ---- blocks -------------------------------------------------------------------------------
+    def _c2f_fused_ok(self, blk: C2f, x, out) -> bool:
+        """The one-launch C2f row stream (``c2f_fused.hip``) has this shape: one bottleneck, 160-wide
+        rows, 32 -> (16 | 16) -> 32 channels with the shortcut (YOLOv8-n l2)."""
+        import os
+        if not x.is_cuda or os.environ.get("AIKO_C2F_FUSED", "1") == "0" or len(blk.m) != 1:
+            return False
+        a, b = blk.m[0]
+        B, H, W, _ = x.shape
+        return (W == 160 and H % self._c2f_rb(H) == 0 and blk.cv1.Cc == 32 and blk.c == 16 and blk.cv2.cout == 32
+                and blk.shortcut and a.R == 3 and b.R == 3 and a.Cc == 16 and b.Cc == 16
+                and x.stride(3) == 1 and out.stride(3) == 1)
+
+    @staticmethod
+    def _c2f_rb(H):
+        import os
+        return int(os.environ.get("AIKO_C2F_RB", "40"))   # 160-row images: 4 bands (bench sweep 32-160: 40 best)
+
     def _run_c2f(self, name, blk: C2f, x, out):
         B, H, W, _ = x.shape
         c, n = blk.c, len(blk.m)
+        if self._c2f_fused_ok(blk, x, out):
+            a, b = blk.m[0]
+            torch.ops.aiko.c2f_fused_out(x, blk.cv1.weight, blk.cv1.bias, a.weight, a.bias, b.weight, b.bias,
+                                         blk.cv2.weight, blk.cv2.bias, out, blk.cv1.Cc, blk.shortcut, self._c2f_rb(H))
+            return out
         cat = self._buf(f"{name}.cat", (B, H, W, (2 + n) * c))
         C.conv2d(x, blk.cv1, out=cat[..., :2 * c])
         tmp = self._buf(f"{name}.tmp", (B, H, W, c))

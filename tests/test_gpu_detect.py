@@ -260,3 +260,26 @@ def test_yolo_weights_roundtrip_bit_exact(native, tmp_path):
     b.load(path)
     det_b, cnt_b = b.detect(frames)
     assert torch.equal(cnt_a, cnt_b) and torch.equal(det_a, det_b)
+
+
+@pytest.mark.parametrize("rb", [10, 20, 160])
+def test_c2f_fused_matches_unfused(native, monkeypatch, rb):
+    """The one-launch C2f row stream (c2f_fused.hip) against the four-launch chain (cv1, bottleneck
+    3x3 pair with the shortcut, cv2) on YOLOv8-n's l2 block: bands of rb rows (zero rows at the
+    image edges, halo rows recomputed at band edges), two images."""
+    from aiko_services_amd.models.yolov8 import YOLOv8
+    m = YOLOv8("n", device=DEV)
+    g = torch.Generator().manual_seed(rb)
+    x = (torch.randn(2, 160, 160, 32, generator=g) * 2).to(DEV, torch.bfloat16)
+    monkeypatch.setenv("AIKO_C2F_RB", str(rb))
+    out_f = torch.full((2, 160, 160, 32), 7.0, dtype=torch.bfloat16, device=DEV)
+    assert m._c2f_fused_ok(m.l2, x, out_f)
+    m._run_c2f("l2f", m.l2, x, out_f)
+    monkeypatch.setenv("AIKO_C2F_FUSED", "0")
+    out_u = torch.empty_like(out_f)
+    m._run_c2f("l2u", m.l2, x, out_u)
+    torch.cuda.synchronize()
+    a, b = out_f.float(), out_u.float()
+    cos = torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()
+    assert cos > 0.9995, cos
+    assert (a - b).abs().max().item() < 0.05 * b.abs().max().item()
