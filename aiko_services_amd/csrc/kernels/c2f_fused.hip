@@ -241,6 +241,176 @@ __global__ __launch_bounds__(W * 2, 1) void c2f_fused_kernel(C2fParams p) {
   }
 }
 
+// The same row stream for wider channel counts (YOLOv8-n l15 at 80 x 80: cv1 1x1 192 -> 64,
+// bottleneck 3x3 32 -> 32 twice, no shortcut, cv2 1x1 96 -> 64): the weights (~77 KB) live in
+// LDS (rows padded by 16 bytes: the 16 rows of a fragment read start on different banks), each
+// 3x3 K chunk is one tap (32 channels), one 16-pixel tile per wave (W / 16 waves), and cv2 takes
+// the C / 16 tiles of c through independent 16x16x16 products summed on the VALU.
+template <int W, int CI, int C, int CO, bool SC>
+__global__ __launch_bounds__(W * 4, 1) void c2f_fused_wl_kernel(C2fParams p) {
+  using namespace c2f;
+  static_assert(C == 32 && CI % 32 == 0 && CO % 16 == 0 && W % 16 == 0, "instantiated shapes");
+  constexpr int NWAVE = W / 16;
+  constexpr int KS1 = CI / 32, N1 = 2 * C / 16, KC3 = 9, N3 = C / 16, N2 = CO / 16, KS2 = 2 * C / 32;
+  constexpr int P1 = CI * 2 + 16, P3 = 9 * C * 2 + 16, P2 = 3 * C * 2 + 16;   // weight row pitches (bytes)
+  constexpr int W1B = 2 * C * P1, W3B = C * P3, W2B = CO * P2;
+  constexpr int SW = W + 2;
+  constexpr int SROW = SW * C * 2, TROW = SW * C * 2, AROW = W * C * 2;
+  constexpr int NS = 5, NA = 5, NT = 4;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[W1B + 2 * W3B + W2B + NS * SROW + NA * AROW + NT * TROW];
+  unsigned char* const lw1 = smem;
+  unsigned char* const lwa = lw1 + W1B;
+  unsigned char* const lwb = lwa + W3B;
+  unsigned char* const lw2 = lwb + W3B;
+  unsigned char* const sring = lw2 + W2B;
+  unsigned char* const aring = sring + NS * SROW;
+  unsigned char* const tring = aring + NA * AROW;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nb = p.H / p.rb;
+  const int img = blockIdx.x / nb, r0 = (blockIdx.x % nb) * p.rb, r1 = r0 + p.rb;
+  const int px0 = wave * 16;
+
+  // ---- weights -> LDS (16-B pieces), biases -> registers
+  auto stage = [&](unsigned char* dst, const bf16_t* src, int rows, int kused, int kpitch, int dpitch) {
+    const int per = kused / 8;
+    for (int i = tid; i < rows * per; i += NWAVE * 64) {
+      const int r = i / per, c = i - r * per;
+      *reinterpret_cast<u32x4*>(dst + r * dpitch + c * 16) =
+          *reinterpret_cast<const u32x4*>(src + (long)r * kpitch + c * 8);
+    }
+  };
+  stage(lw1, p.w1, 2 * C, CI, p.k1, P1);
+  stage(lwa, p.wa, C, 9 * C, p.ka, P3);
+  stage(lwb, p.wb, C, 9 * C, p.kb, P3);
+  stage(lw2, p.w2, CO, 3 * C, p.k2, P2);
+  f32x4 b1v[N1], bav[N3], bbv[N3], b2v[N2];
+#pragma unroll
+  for (int n = 0; n < N1; ++n) b1v[n] = *reinterpret_cast<const f32x4*>(p.b1 + 16 * n + 4 * fq);
+#pragma unroll
+  for (int n = 0; n < N3; ++n) {
+    bav[n] = *reinterpret_cast<const f32x4*>(p.ba + 16 * n + 4 * fq);
+    bbv[n] = *reinterpret_cast<const f32x4*>(p.bb + 16 * n + 4 * fq);
+  }
+#pragma unroll
+  for (int n = 0; n < N2; ++n) b2v[n] = *reinterpret_cast<const f32x4*>(p.b2 + 16 * n + 4 * fq);
+  for (int i = tid; i < (NS + NT) * 2 * (C / 8); i += NWAVE * 64) {
+    const int slot = i / (2 * (C / 8)), rem = i % (2 * (C / 8));
+    const int side = rem / (C / 8), piece = rem % (C / 8);
+    unsigned char* base = slot < NS ? sring + slot * SROW : tring + (slot - NS) * TROW;
+    *reinterpret_cast<u32x4*>(base + (side ? (W + 1) : 0) * C * 2 + piece * 16) = u32x4{0u, 0u, 0u, 0u};
+  }
+  auto wfrag = [&](const unsigned char* lw, int pitch, int n, int koff) __attribute__((always_inline)) {
+    return *reinterpret_cast<const bf16x8*>(lw + (16 * n + fr) * pitch + (koff + 8 * fq) * 2);
+  };
+
+  bf16x8 xf[KS1];
+  auto load_x = [&](int row) __attribute__((always_inline)) {
+    const bool ok = row >= 0 && row < p.H;
+    const bf16_t* src = p.x + (((long)img * p.H + (ok ? row : 0)) * W + px0 + fr) * p.ldx + 8 * fq;
+#pragma unroll
+    for (int k = 0; k < KS1; ++k) xf[k] = *reinterpret_cast<const bf16x8*>(src + 32 * k);
+  };
+  auto cv1 = [&](int row) __attribute__((always_inline)) {
+    const bool ok = row >= 0 && row < p.H;
+    const int slot = (row + 2 * NS) % NS;
+    const int px = px0 + fr;
+#pragma unroll
+    for (int n = 0; n < N1; ++n) {
+      f32x4 acc = b1v[n];
+#pragma unroll
+      for (int k = 0; k < KS1; ++k) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfrag(lw1, P1, n, 32 * k), xf[k], acc, 0, 0, 0);
+      const u32x2 v = ok ? pack4(silu4(acc)) : u32x2{0u, 0u};
+      if (n < C / 16)
+        *reinterpret_cast<u32x2*>(aring + slot * AROW + (px * C + 16 * n + 4 * fq) * 2) = v;
+      else
+        *reinterpret_cast<u32x2*>(sring + slot * SROW + ((px + 1) * C + 16 * (n - C / 16) + 4 * fq) * 2) = v;
+    }
+  };
+  // 3x3: chunk k = tap k (dy = k / 3, dx = k % 3 - 1), channels 8 fq .. +7 of that tap's pixel
+  auto conv3 = [&](const unsigned char* ring, int nsl, int rstride, int row, const unsigned char* lw,
+                   const f32x4 (&bias)[N3], f32x4 (&acc)[N3]) __attribute__((always_inline)) {
+    const unsigned char* rows[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) rows[d] = ring + ((row - 1 + d + 4 * nsl) % nsl) * rstride + (px0 + fr + 1) * C * 2 + 16 * fq;
+#pragma unroll
+    for (int n = 0; n < N3; ++n) acc[n] = bias[n];
+#pragma unroll
+    for (int k = 0; k < KC3; ++k) {
+      const bf16x8 b = *reinterpret_cast<const bf16x8*>(rows[k / 3] + (k % 3 - 1) * C * 2);
+#pragma unroll
+      for (int n = 0; n < N3; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfrag(lw, P3, n, 32 * k), b, acc[n], 0, 0, 0);
+    }
+  };
+
+  load_x(r0 - 2);
+  cv1(r0 - 2);
+  load_x(r0 - 1);
+  cv1(r0 - 1);
+  load_x(r0);
+  cv1(r0);
+  load_x(r0 + 1);
+
+  for (int v = r0 - 1; v <= r1 + 1; ++v) {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (v + 2 <= r1 + 1) {
+      cv1(v + 2);
+      if (v + 3 <= r1 + 1) load_x(v + 3);
+    }
+    if (v <= r1) {
+      const bool ok = v >= 0 && v < p.H;
+      const int slot = (v + 2 * NT) % NT;
+      f32x4 acc[N3];
+      conv3(sring, NS, SROW, v, lwa, bav, acc);
+#pragma unroll
+      for (int n = 0; n < N3; ++n) {
+        const u32x2 o = ok ? pack4(silu4(acc[n])) : u32x2{0u, 0u};
+        *reinterpret_cast<u32x2*>(tring + slot * TROW + ((px0 + fr + 1) * C + 16 * n + 4 * fq) * 2) = o;
+      }
+    }
+    const int w = v - 2;
+    if (w >= r0 && w < r1) {
+      const int aslot = (w + 2 * NA) % NA, sslot = (w + 2 * NS) % NS;
+      const int px = px0 + fr;
+      f32x4 c[N3];
+      conv3(tring, NT, TROW, w, lwb, bbv, c);
+      v4s cop[N3];
+#pragma unroll
+      for (int n = 0; n < N3; ++n) {
+        c[n] = silu4(c[n]);
+        if constexpr (SC) {
+          const f32x4 sv = unpack4(*reinterpret_cast<const u32x2*>(sring + sslot * SROW + ((px + 1) * C + 16 * n + 4 * fq) * 2));
+          c[n] = f32x4{c[n][0] + sv[0], c[n][1] + sv[1], c[n][2] + sv[2], c[n][3] + sv[3]};
+        }
+        cop[n] = __builtin_bit_cast(v4s, pack4(c[n]));
+      }
+      // [a | s] chunks: channel g = 32 k + 8 fq of the concatenation (a below C, s from C)
+      bf16x8 asf[KS2];
+#pragma unroll
+      for (int k = 0; k < KS2; ++k) {
+        const int g = 32 * k + 8 * fq;
+        asf[k] = g < C ? *reinterpret_cast<const bf16x8*>(aring + aslot * AROW + (px * C + g) * 2)
+                       : *reinterpret_cast<const bf16x8*>(sring + sslot * SROW + ((px + 1) * C + g - C) * 2);
+      }
+      bf16_t* yrow = p.y + (((long)img * p.H + w) * W + px) * p.ldy;
+#pragma unroll
+      for (int n = 0; n < N2; ++n) {
+        f32x4 acc = b2v[n];
+#pragma unroll
+        for (int k = 0; k < KS2; ++k) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfrag(lw2, P2, n, 32 * k), asf[k], acc, 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < N3; ++j) {      // independent products (see c2f_fused_kernel)
+          const v4s wc = *reinterpret_cast<const v4s*>(lw2 + (16 * n + fr) * P2 + (2 * C + 16 * j + 4 * fq) * 2);
+          const f32x4 pj = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wc, cop[j], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          acc = f32x4{acc[0] + pj[0], acc[1] + pj[1], acc[2] + pj[2], acc[3] + pj[3]};
+        }
+        *reinterpret_cast<u32x2*>(yrow + 16 * n + 4 * fq) = pack4(silu4(acc));
+      }
+    }
+  }
+}
+
 }  // namespace aiko
 
 // x [B, H, W, ldx] -> y [B, H, W, ldy] through the fused C2f (n = 1); weights as the ConvSpecs
@@ -262,6 +432,8 @@ extern "C" int aiko_c2f_fused(const void* x, int ldx, const void* w1, const floa
   const dim3 grid((unsigned)(B * (H / rb)));
   if (W == 160 && CI == 32 && C == 16 && CO == 32 && shortcut) {
     c2f_fused_kernel<160, 32, 16, 32, true><<<grid, dim3(320), 0, stream>>>(p);
+  } else if (W == 80 && CI == 192 && C == 32 && CO == 64 && !shortcut) {
+    c2f_fused_wl_kernel<80, 192, 32, 64, false><<<grid, dim3(320), 0, stream>>>(p);
   } else {
     return -1;
   }

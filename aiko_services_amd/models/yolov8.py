@@ -176,14 +176,16 @@ class YOLOv8(WeightsMixin):
             return False
         a, b = blk.m[0]
         B, H, W, _ = x.shape
-        return (W == 160 and H % self._c2f_rb(H) == 0 and blk.cv1.Cc == 32 and blk.c == 16 and blk.cv2.cout == 32
-                and blk.shortcut and a.R == 3 and b.R == 3 and a.Cc == 16 and b.Cc == 16
+        shape = (W, blk.cv1.Cc, blk.c, blk.cv2.cout, blk.shortcut)
+        return (shape in ((160, 32, 16, 32, True), (80, 192, 32, 64, False)) and H % self._c2f_rb(H) == 0
+                and a.R == 3 and b.R == 3 and a.Cc == blk.c and b.Cc == blk.c
                 and x.stride(3) == 1 and out.stride(3) == 1)
 
     @staticmethod
     def _c2f_rb(H):
+        """Band height: 160-row images 40 (bench sweep 32-160), 80-row images 20."""
         import os
-        return int(os.environ.get("AIKO_C2F_RB", "40"))   # 160-row images: 4 bands (bench sweep 32-160: 40 best)
+        return int(os.environ.get("AIKO_C2F_RB" if H == 160 else "AIKO_C2F_RB80", "40" if H == 160 else "20"))
 
     def _run_c2f(self, name, blk: C2f, x, out):
         B, H, W, _ = x.shape

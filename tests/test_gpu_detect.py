@@ -283,3 +283,25 @@ def test_c2f_fused_matches_unfused(native, monkeypatch, rb):
     cos = torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()
     assert cos > 0.9995, cos
     assert (a - b).abs().max().item() < 0.05 * b.abs().max().item()
+
+
+@pytest.mark.parametrize("rb", [10, 20, 80])
+def test_c2f_fused_wide_matches_unfused(native, monkeypatch, rb):
+    """The LDS-weights variant (c2f_fused_wl_kernel) on YOLOv8-n's l15 block (80 x 80, cv1 192 -> 64,
+    bottleneck 3x3 32 -> 32 without the shortcut, cv2 96 -> 64) against the four-launch chain."""
+    from aiko_services_amd.models.yolov8 import YOLOv8
+    m = YOLOv8("n", device=DEV)
+    g = torch.Generator().manual_seed(rb)
+    x = (torch.randn(2, 80, 80, 192, generator=g) * 2).to(DEV, torch.bfloat16)
+    monkeypatch.setenv("AIKO_C2F_RB80", str(rb))
+    out_f = torch.full((2, 80, 80, 64), 7.0, dtype=torch.bfloat16, device=DEV)
+    assert m._c2f_fused_ok(m.l15, x, out_f)
+    m._run_c2f("l15f", m.l15, x, out_f)
+    monkeypatch.setenv("AIKO_C2F_FUSED", "0")
+    out_u = torch.empty_like(out_f)
+    m._run_c2f("l15u", m.l15, x, out_u)
+    torch.cuda.synchronize()
+    a, b = out_f.float(), out_u.float()
+    cos = torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()
+    assert cos > 0.9995, cos
+    assert (a - b).abs().max().item() < 0.05 * b.abs().max().item()
