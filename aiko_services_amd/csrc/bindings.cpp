@@ -82,6 +82,8 @@ int aiko_gemm_fp8_ln(const void* a, const void* b, const float* sb, const float*
 int aiko_c2f_fused(const void* x, int ldx, const void* w1, const float* b1, int k1, const void* wa, const float* ba,
                    int ka, const void* wb, const float* bb, int kb, const void* w2, const float* b2, int k2, void* y, int ldy,
                    int B, int H, int W, int CI, int C, int CO, int shortcut, int rb, hipStream_t stream);
+int aiko_c2f_bneck(const void* x, int ldx, const void* wa, const float* ba, int ka, const void* wb, const float* bb,
+                   int kb, void* y, int ldy, int B, int H, int W, int C, int shortcut, int rb, hipStream_t stream);
 int aiko_rowstats_mx(const void* x, int ldx, void* q, int ldq, void* qsc, int ysr, float* st, int sts, int P, int M,
                      int D, hipStream_t stream);
 int aiko_linear_splitk(const void* x, const void* w, const float* bias, float* part, void* y, int M, int N, int K,
@@ -521,6 +523,32 @@ void c2f_fused_out(const at::Tensor& x, const at::Tensor& w1, const at::Tensor& 
                               w2.data_ptr(), b2.data_ptr<float>(), (int)w2.size(1), y.data_ptr(), (int)ldy, (int)B, (int)H,
                               (int)W, (int)CI, (int)C, (int)CO, shortcut ? 1 : 0, (int)rb, cur_stream()),
                "c2f_fused");
+}
+
+// One YOLOv8 C2f bottleneck (3x3 C -> C twice + shortcut) in one launch (c2f_fused.hip):
+// x = s, y = c as NHWC channel-slice views of the C2f's concat buffer.
+void c2f_bneck_out(const at::Tensor& x, const at::Tensor& wa, const at::Tensor& ba, const at::Tensor& wb,
+                   const at::Tensor& bb, at::Tensor& y, bool shortcut, int64_t rb) {
+  for (const at::Tensor* t : {&x, &wa, &ba, &wb, &bb, (const at::Tensor*)&y}) check_cuda(*t, "c2f bottleneck operand");
+  for (const at::Tensor* t : {&x, &wa, &wb, (const at::Tensor*)&y})
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16, "aiko.c2f_bneck_out: bf16 activations / weights");
+  TORCH_CHECK(ba.scalar_type() == at::kFloat && bb.scalar_type() == at::kFloat && ba.is_contiguous() && bb.is_contiguous(),
+              "aiko.c2f_bneck_out: fp32 biases");
+  const int64_t C = wa.size(0);
+  TORCH_CHECK(wa.dim() == 2 && wb.dim() == 2 && wa.is_contiguous() && wb.is_contiguous() && wb.size(0) == C &&
+                  wa.size(1) >= 9 * C && wb.size(1) >= 9 * C && wa.size(1) % 8 == 0 && wb.size(1) % 8 == 0 &&
+                  ba.numel() == C && bb.numel() == C,
+              "aiko.c2f_bneck_out: 3x3 weights [C, >= 9C]");
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.sizes() == y.sizes() && x.size(3) == C, "aiko.c2f_bneck_out: x, y [B, H, W, C]");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), ldx = x.stride(2), ldy = y.stride(2);
+  TORCH_CHECK(x.stride(3) == 1 && y.stride(3) == 1 && x.stride(1) == W * ldx && y.stride(1) == W * ldy &&
+                  x.stride(0) == H * W * ldx && y.stride(0) == H * W * ldy && ldx % 8 == 0 && ldy % 4 == 0 &&
+                  reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(y.data_ptr()) % 8 == 0,
+              "aiko.c2f_bneck_out: NHWC channel-slice views, 16-B aligned pixels");
+  check_launch(aiko_c2f_bneck(x.data_ptr(), (int)ldx, wa.data_ptr(), ba.data_ptr<float>(), (int)wa.size(1), wb.data_ptr(),
+                              bb.data_ptr<float>(), (int)wb.size(1), y.data_ptr(), (int)ldy, (int)B, (int)H, (int)W, (int)C,
+                              shortcut ? 1 : 0, (int)rb, cur_stream()),
+               "c2f_bneck");
 }
 
 // A whole ResNet stage-1 bottleneck in one launch (bneck_fused.hip): x [B, H, 56, cin] ->
@@ -1411,6 +1439,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("gemm_fp8_ln_out(Tensor a, Tensor amx, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!)? y, Tensor(b!)? yq, Tensor(c!)? ysc, Tensor(d!) st, Tensor? cs, int ln, int act, int ln_d, float eps, Tensor zero) -> ()");
   m.def("rowstats_mx_out(Tensor x, Tensor(a!) q, Tensor(b!) qsc, Tensor(c!) st) -> ()");
   m.def("c2f_fused_out(Tensor x, Tensor w1, Tensor b1, Tensor wa, Tensor ba, Tensor wb, Tensor bb, Tensor w2, Tensor b2, Tensor(a!) y, int ci, bool shortcut, int rb) -> ()");
+  m.def("c2f_bneck_out(Tensor x, Tensor wa, Tensor ba, Tensor wb, Tensor bb, Tensor(a!) y, bool shortcut, int rb) -> ()");
   m.def("linear_splitk_out(Tensor x, Tensor w, Tensor? bias, Tensor(a!) part, Tensor(b!) y, int K, int S) -> ()");
   m.def("attn_fwd_out(Tensor q, Tensor k, Tensor v, Tensor(a!) o, int B, int H, int T, int Tpad, float scale, Tensor(b!)? work=None, Tensor(c!)? oq=None, Tensor(d!)? osc=None) -> ()");
   m.def("logmel_out(Tensor audio, Tensor mel, Tensor mel_range, int n_fft, int hop, int F, Tensor(a!) work, Tensor(b!) gmax, Tensor(c!) dst, int rows, int pad) -> ()");
@@ -1449,6 +1478,7 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("gemm_fp8_ln_out", &gemm_fp8_ln_out);
   m.impl("rowstats_mx_out", &rowstats_mx_out);
   m.impl("c2f_fused_out", &c2f_fused_out);
+  m.impl("c2f_bneck_out", &c2f_bneck_out);
   m.impl("attn_fwd_out", &attn_fwd_out);
   m.impl("linear_splitk_out", &linear_splitk_out);
   m.impl("logmel_out", &logmel_out);

@@ -411,6 +411,134 @@ __global__ __launch_bounds__(W * 4, 1) void c2f_fused_wl_kernel(C2fParams p) {
   }
 }
 
+// One C2f bottleneck alone (3x3 C -> C, SiLU, 3x3 C -> C, SiLU, + shortcut) as the same row
+// stream, for blocks with n = 2 whose whole C2f does not fit in LDS (YOLOv8-n l4 at 80 x 80:
+// s and c are channel slices of the C2f's concat buffer): s rows are copied into the S ring a
+// step ahead (one 16-B piece per thread, loaded the step before), conv_a fills the T ring, and
+// conv_b + shortcut goes straight to HBM — the intermediate t never leaves LDS.
+template <int W, int C, bool SC>
+__global__ __launch_bounds__(W * 4, 1) void c2f_bneck_kernel(C2fParams p) {
+  using namespace c2f;
+  static_assert(C == 32 && W % 16 == 0 && (W * C * 2 / 16) % (W * 4) == 0, "instantiated shapes");
+  constexpr int NWAVE = W / 16, NTH = W * 4;
+  constexpr int KC3 = 9, N3 = C / 16;
+  constexpr int P3 = 9 * C * 2 + 16, W3B = C * P3;
+  constexpr int SW = W + 2, SROW = SW * C * 2, TROW = SW * C * 2;
+  constexpr int NS = 5, NT = 4;
+  constexpr int PPR = W * C * 2 / 16, PPT = PPR / NTH;   // 16-B pieces per row / per thread
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * W3B + NS * SROW + NT * TROW];
+  unsigned char* const lwa = smem;
+  unsigned char* const lwb = lwa + W3B;
+  unsigned char* const sring = lwb + W3B;
+  unsigned char* const tring = sring + NS * SROW;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nb = p.H / p.rb;
+  const int img = blockIdx.x / nb, r0 = (blockIdx.x % nb) * p.rb, r1 = r0 + p.rb;
+  const int px0 = wave * 16;
+
+  for (int i = tid; i < C * (9 * C / 8); i += NTH) {
+    const int r = i / (9 * C / 8), c = i - r * (9 * C / 8);
+    *reinterpret_cast<u32x4*>(lwa + r * P3 + c * 16) = *reinterpret_cast<const u32x4*>(p.wa + (long)r * p.ka + c * 8);
+    *reinterpret_cast<u32x4*>(lwb + r * P3 + c * 16) = *reinterpret_cast<const u32x4*>(p.wb + (long)r * p.kb + c * 8);
+  }
+  f32x4 bav[N3], bbv[N3];
+#pragma unroll
+  for (int n = 0; n < N3; ++n) {
+    bav[n] = *reinterpret_cast<const f32x4*>(p.ba + 16 * n + 4 * fq);
+    bbv[n] = *reinterpret_cast<const f32x4*>(p.bb + 16 * n + 4 * fq);
+  }
+  for (int i = tid; i < (NS + NT) * 2 * (C / 8); i += NTH) {
+    const int slot = i / (2 * (C / 8)), rem = i % (2 * (C / 8));
+    const int side = rem / (C / 8), piece = rem % (C / 8);
+    unsigned char* base = slot < NS ? sring + slot * SROW : tring + (slot - NS) * TROW;
+    *reinterpret_cast<u32x4*>(base + (side ? (W + 1) : 0) * C * 2 + piece * 16) = u32x4{0u, 0u, 0u, 0u};
+  }
+
+  // s row pieces of this thread: piece j = tid + NTH i -> pixel j / (C / 8), chunk j % (C / 8)
+  u32x4 sreg[PPT];
+  auto load_s = [&](int row) __attribute__((always_inline)) {
+    const bool ok = row >= 0 && row < p.H;
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int j = tid + NTH * i, px = j / (C / 8), ch = j % (C / 8);
+      sreg[i] = ok ? *reinterpret_cast<const u32x4*>(p.x + (((long)img * p.H + row) * W + px) * p.ldx + 8 * ch)
+                   : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  auto put_s = [&](int row) __attribute__((always_inline)) {
+    const int slot = (row + 2 * NS) % NS;
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int j = tid + NTH * i, px = j / (C / 8), ch = j % (C / 8);
+      *reinterpret_cast<u32x4*>(sring + slot * SROW + ((px + 1) * C + 8 * ch) * 2) = sreg[i];
+    }
+  };
+  auto conv3 = [&](const unsigned char* ring, int nsl, int rstride, int row, const unsigned char* lw,
+                   const f32x4 (&bias)[N3], f32x4 (&acc)[N3]) __attribute__((always_inline)) {
+    const unsigned char* rows[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) rows[d] = ring + ((row - 1 + d + 4 * nsl) % nsl) * rstride + (px0 + fr + 1) * C * 2 + 16 * fq;
+#pragma unroll
+    for (int n = 0; n < N3; ++n) acc[n] = bias[n];
+#pragma unroll
+    for (int k = 0; k < KC3; ++k) {
+      const bf16x8 b = *reinterpret_cast<const bf16x8*>(rows[k / 3] + (k % 3 - 1) * C * 2);
+#pragma unroll
+      for (int n = 0; n < N3; ++n) {
+        const bf16x8 wf = *reinterpret_cast<const bf16x8*>(lw + (16 * n + fr) * P3 + (32 * k + 8 * fq) * 2);
+        acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, b, acc[n], 0, 0, 0);
+      }
+    }
+  };
+
+  // prologue: s rows r0-2 .. r0 in the ring, row r0+1 in registers
+  load_s(r0 - 2);
+  put_s(r0 - 2);
+  load_s(r0 - 1);
+  put_s(r0 - 1);
+  load_s(r0);
+  put_s(r0);
+  load_s(r0 + 1);
+
+  for (int v = r0 - 1; v <= r1 + 1; ++v) {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (v + 2 <= r1 + 1) {                           // s row v + 2 -> ring, row v + 3 -> registers
+      put_s(v + 2);
+      if (v + 3 <= r1 + 1) load_s(v + 3);
+    }
+    if (v <= r1) {                                   // conv_a(v) -> T row v
+      const bool ok = v >= 0 && v < p.H;
+      const int slot = (v + 2 * NT) % NT;
+      f32x4 acc[N3];
+      conv3(sring, NS, SROW, v, lwa, bav, acc);
+#pragma unroll
+      for (int n = 0; n < N3; ++n) {
+        const u32x2 o = ok ? pack4(silu4(acc[n])) : u32x2{0u, 0u};
+        *reinterpret_cast<u32x2*>(tring + slot * TROW + ((px0 + fr + 1) * C + 16 * n + 4 * fq) * 2) = o;
+      }
+    }
+    const int w = v - 2;
+    if (w >= r0 && w < r1) {                         // conv_b(w) (+ s) -> y row w
+      const int sslot = (w + 2 * NS) % NS;
+      const int px = px0 + fr;
+      f32x4 c[N3];
+      conv3(tring, NT, TROW, w, lwb, bbv, c);
+      bf16_t* yrow = p.y + (((long)img * p.H + w) * W + px) * p.ldy;
+#pragma unroll
+      for (int n = 0; n < N3; ++n) {
+        c[n] = silu4(c[n]);
+        if constexpr (SC) {
+          const f32x4 sv = unpack4(*reinterpret_cast<const u32x2*>(sring + sslot * SROW + ((px + 1) * C + 16 * n + 4 * fq) * 2));
+          c[n] = f32x4{c[n][0] + sv[0], c[n][1] + sv[1], c[n][2] + sv[2], c[n][3] + sv[3]};
+        }
+        *reinterpret_cast<u32x2*>(yrow + 16 * n + 4 * fq) = pack4(c[n]);
+      }
+    }
+  }
+}
+
 }  // namespace aiko
 
 // x [B, H, W, ldx] -> y [B, H, W, ldy] through the fused C2f (n = 1); weights as the ConvSpecs
@@ -434,6 +562,28 @@ extern "C" int aiko_c2f_fused(const void* x, int ldx, const void* w1, const floa
     c2f_fused_kernel<160, 32, 16, 32, true><<<grid, dim3(320), 0, stream>>>(p);
   } else if (W == 80 && CI == 192 && C == 32 && CO == 64 && !shortcut) {
     c2f_fused_wl_kernel<80, 192, 32, 64, false><<<grid, dim3(320), 0, stream>>>(p);
+  } else {
+    return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+// One C2f bottleneck (3x3 C -> C twice, SiLU, optional shortcut) over channel-slice views:
+// x = s [B, H, W, pitch ldx], y = c [B, H, W, pitch ldy] (c2f_bneck_kernel).
+extern "C" int aiko_c2f_bneck(const void* x, int ldx, const void* wa, const float* ba, int ka, const void* wb,
+                              const float* bb, int kb, void* y, int ldy, int B, int H, int W, int C, int shortcut,
+                              int rb, hipStream_t stream) {
+  using namespace aiko;
+  if (rb <= 0 || H % rb || B <= 0) return -1;
+  C2fParams p{};
+  p.x = static_cast<const bf16_t*>(x);
+  p.wa = static_cast<const bf16_t*>(wa); p.ba = ba;
+  p.wb = static_cast<const bf16_t*>(wb); p.bb = bb;
+  p.y = static_cast<bf16_t*>(y);
+  p.B = B; p.H = H; p.ldx = ldx; p.ldy = ldy; p.ka = ka; p.kb = kb; p.rb = rb;
+  const dim3 grid((unsigned)(B * (H / rb)));
+  if (W == 80 && C == 32 && shortcut) {
+    c2f_bneck_kernel<80, 32, true><<<grid, dim3(320), 0, stream>>>(p);
   } else {
     return -1;
   }

@@ -198,8 +198,16 @@ class YOLOv8(WeightsMixin):
         cat = self._buf(f"{name}.cat", (B, H, W, (2 + n) * c))
         C.conv2d(x, blk.cv1, out=cat[..., :2 * c])
         tmp = self._buf(f"{name}.tmp", (B, H, W, c))
+        import os
+        fuse_b = (cat.is_cuda and os.environ.get("AIKO_C2F_FUSED", "1") != "0" and W == 80 and c == 32
+                  and blk.shortcut and H % self._c2f_rb(H) == 0)
         for i, (a, b) in enumerate(blk.m):
             src = cat[..., (1 + i) * c:(2 + i) * c]
+            if fuse_b and a.R == 3 and b.R == 3 and a.Cc == c and b.Cc == c:
+                # both 3x3 convs + shortcut in one row-stream launch (t stays in LDS)
+                torch.ops.aiko.c2f_bneck_out(src, a.weight, a.bias, b.weight, b.bias,
+                                             cat[..., (2 + i) * c:(3 + i) * c], blk.shortcut, self._c2f_rb(H))
+                continue
             C.conv2d(src, a, out=tmp)
             C.conv2d(tmp, b, out=cat[..., (2 + i) * c:(3 + i) * c],
                      residual=src if blk.shortcut else None, residual_after_act=True)

@@ -305,3 +305,24 @@ def test_c2f_fused_wide_matches_unfused(native, monkeypatch, rb):
     cos = torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()
     assert cos > 0.9995, cos
     assert (a - b).abs().max().item() < 0.05 * b.abs().max().item()
+
+
+@pytest.mark.parametrize("rb", [10, 20])
+def test_c2f_bneck_fused_matches_unfused(native, monkeypatch, rb):
+    """The fused bottleneck pair (c2f_bneck_kernel) inside YOLOv8-n's l4 C2f (80 x 80, n = 2, the
+    bottlenecks read / write channel slices of the concat buffer) against the unfused chain."""
+    from aiko_services_amd.models.yolov8 import YOLOv8
+    m = YOLOv8("n", device=DEV)
+    g = torch.Generator().manual_seed(rb)
+    x = (torch.randn(2, 80, 80, 64, generator=g) * 2).to(DEV, torch.bfloat16)
+    monkeypatch.setenv("AIKO_C2F_RB80", str(rb))
+    out_f = torch.empty(2, 80, 80, 64, dtype=torch.bfloat16, device=DEV)
+    m._run_c2f("l4f", m.l4, x, out_f)
+    monkeypatch.setenv("AIKO_C2F_FUSED", "0")
+    out_u = torch.empty_like(out_f)
+    m._run_c2f("l4u", m.l4, x, out_u)
+    torch.cuda.synchronize()
+    a, b = out_f.float(), out_u.float()
+    cos = torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()
+    assert cos > 0.9995, cos
+    assert (a - b).abs().max().item() < 0.05 * b.abs().max().item()
