@@ -84,6 +84,10 @@ int aiko_c2f_fused(const void* x, int ldx, const void* w1, const float* b1, int 
                    int B, int H, int W, int CI, int C, int CO, int shortcut, int rb, hipStream_t stream);
 int aiko_c2f_bneck(const void* x, int ldx, const void* wa, const float* ba, int ka, const void* wb, const float* bb,
                    int kb, void* y, int ldy, int B, int H, int W, int C, int shortcut, int rb, hipStream_t stream);
+int aiko_c2f_fused_s2(const void* a0, int lda0, const void* w0, const float* b0, int k0, const void* w1, const float* b1,
+                      int k1, const void* wa, const float* ba, int ka, const void* wb, const float* bb, int kb, const void* w2,
+                      const float* b2, int k2, void* y, int ldy, int B, int H, int W, int CI, int C, int CO, int shortcut,
+                      int rb, hipStream_t stream);
 int aiko_rowstats_mx(const void* x, int ldx, void* q, int ldq, void* qsc, int ysr, float* st, int sts, int P, int M,
                      int D, hipStream_t stream);
 int aiko_linear_splitk(const void* x, const void* w, const float* bias, float* part, void* y, int M, int N, int K,
@@ -523,6 +527,41 @@ void c2f_fused_out(const at::Tensor& x, const at::Tensor& w1, const at::Tensor& 
                               w2.data_ptr(), b2.data_ptr<float>(), (int)w2.size(1), y.data_ptr(), (int)ldy, (int)B, (int)H,
                               (int)W, (int)CI, (int)C, (int)CO, shortcut ? 1 : 0, (int)rb, cur_stream()),
                "c2f_fused");
+}
+
+// The 3x3 / stride-2 conv feeding a C2f and the C2f itself in one launch (c2f_fused.hip,
+// c2f_fused_s2_kernel): a0 [B, 2H, 2W, >= 16] -> y [B, H, W, >= CO]; w0 / b0 the stride-2 conv.
+void c2f_fused_s2_out(const at::Tensor& a0, const at::Tensor& w0, const at::Tensor& b0, const at::Tensor& w1,
+                      const at::Tensor& b1, const at::Tensor& wa, const at::Tensor& ba, const at::Tensor& wb,
+                      const at::Tensor& bb, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& y, bool shortcut,
+                      int64_t rb) {
+  for (const at::Tensor* t : {&a0, &w0, &b0, &w1, &b1, &wa, &ba, &wb, &bb, &w2, &b2, (const at::Tensor*)&y})
+    check_cuda(*t, "c2f_s2 operand");
+  for (const at::Tensor* t : {&a0, &w0, &w1, &wa, &wb, &w2, (const at::Tensor*)&y})
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16, "aiko.c2f_fused_s2_out: bf16 activations / weights");
+  for (const at::Tensor* t : {&b0, &b1, &ba, &bb, &b2})
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "aiko.c2f_fused_s2_out: fp32 contiguous biases");
+  for (const at::Tensor* t : {&w0, &w1, &wa, &wb, &w2})
+    TORCH_CHECK(t->dim() == 2 && t->is_contiguous() && t->size(1) % 8 == 0, "aiko.c2f_fused_s2_out: weights [Cout, K]");
+  const int64_t C = wa.size(0), CO = w2.size(0), CI = w0.size(0);
+  TORCH_CHECK(w0.size(1) >= 160 && b0.numel() == CI && w1.size(0) == 2 * C && w1.size(1) >= CI && wb.size(0) == C &&
+                  wa.size(1) >= 160 && wb.size(1) >= 160 && w2.size(1) >= 3 * C && b1.numel() == 2 * C &&
+                  ba.numel() == C && bb.numel() == C && b2.numel() == CO,
+              "aiko.c2f_fused_s2_out: inconsistent conv / C2f shapes");
+  TORCH_CHECK(a0.dim() == 4 && y.dim() == 4 && a0.size(0) == y.size(0) && a0.size(1) == 2 * y.size(1) &&
+                  a0.size(2) == 2 * y.size(2) && a0.size(3) >= 16 && y.size(3) >= CO,
+              "aiko.c2f_fused_s2_out: a0 [B, 2H, 2W, 16], y [B, H, W, CO]");
+  const int64_t B = y.size(0), H = y.size(1), W = y.size(2), lda = a0.stride(2), ldy = y.stride(2);
+  TORCH_CHECK(a0.stride(3) == 1 && y.stride(3) == 1 && a0.stride(1) == 2 * W * lda && y.stride(1) == W * ldy &&
+                  a0.stride(0) == 2 * H * a0.stride(1) && y.stride(0) == H * W * ldy && lda % 8 == 0 && ldy % 4 == 0 &&
+                  reinterpret_cast<uintptr_t>(a0.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(y.data_ptr()) % 8 == 0,
+              "aiko.c2f_fused_s2_out: NHWC views with 16-B aligned pixels");
+  check_launch(aiko_c2f_fused_s2(a0.data_ptr(), (int)lda, w0.data_ptr(), b0.data_ptr<float>(), (int)w0.size(1),
+                                 w1.data_ptr(), b1.data_ptr<float>(), (int)w1.size(1), wa.data_ptr(), ba.data_ptr<float>(),
+                                 (int)wa.size(1), wb.data_ptr(), bb.data_ptr<float>(), (int)wb.size(1), w2.data_ptr(),
+                                 b2.data_ptr<float>(), (int)w2.size(1), y.data_ptr(), (int)ldy, (int)B, (int)H, (int)W,
+                                 (int)CI, (int)C, (int)CO, shortcut ? 1 : 0, (int)rb, cur_stream()),
+               "c2f_fused_s2");
 }
 
 // One YOLOv8 C2f bottleneck (3x3 C -> C twice + shortcut) in one launch (c2f_fused.hip):
@@ -1439,6 +1478,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("gemm_fp8_ln_out(Tensor a, Tensor amx, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!)? y, Tensor(b!)? yq, Tensor(c!)? ysc, Tensor(d!) st, Tensor? cs, int ln, int act, int ln_d, float eps, Tensor zero) -> ()");
   m.def("rowstats_mx_out(Tensor x, Tensor(a!) q, Tensor(b!) qsc, Tensor(c!) st) -> ()");
   m.def("c2f_fused_out(Tensor x, Tensor w1, Tensor b1, Tensor wa, Tensor ba, Tensor wb, Tensor bb, Tensor w2, Tensor b2, Tensor(a!) y, int ci, bool shortcut, int rb) -> ()");
+  m.def("c2f_fused_s2_out(Tensor a0, Tensor w0, Tensor b0, Tensor w1, Tensor b1, Tensor wa, Tensor ba, Tensor wb, Tensor bb, Tensor w2, Tensor b2, Tensor(a!) y, bool shortcut, int rb) -> ()");
   m.def("c2f_bneck_out(Tensor x, Tensor wa, Tensor ba, Tensor wb, Tensor bb, Tensor(a!) y, bool shortcut, int rb) -> ()");
   m.def("linear_splitk_out(Tensor x, Tensor w, Tensor? bias, Tensor(a!) part, Tensor(b!) y, int K, int S) -> ()");
   m.def("attn_fwd_out(Tensor q, Tensor k, Tensor v, Tensor(a!) o, int B, int H, int T, int Tpad, float scale, Tensor(b!)? work=None, Tensor(c!)? oq=None, Tensor(d!)? osc=None) -> ()");
@@ -1479,6 +1519,7 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("rowstats_mx_out", &rowstats_mx_out);
   m.impl("c2f_fused_out", &c2f_fused_out);
   m.impl("c2f_bneck_out", &c2f_bneck_out);
+  m.impl("c2f_fused_s2_out", &c2f_fused_s2_out);
   m.impl("attn_fwd_out", &attn_fwd_out);
   m.impl("linear_splitk_out", &linear_splitk_out);
   m.impl("logmel_out", &logmel_out);

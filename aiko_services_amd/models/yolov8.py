@@ -181,6 +181,19 @@ class YOLOv8(WeightsMixin):
                 and a.R == 3 and b.R == 3 and a.Cc == blk.c and b.Cc == blk.c
                 and x.stride(3) == 1 and out.stride(3) == 1)
 
+    def _l1l2_fused_ok(self, a0, a2) -> bool:
+        """l1 + l2 in one launch (c2f_fused_s2_kernel).  Numerics-tested, but the bench measured
+        41.4 / 41.6k vs 41.4 / 42.3k frames/s with l1 as its own conv (same box): the longer
+        serial row step at one workgroup per CU costs what the saved a1 round trip gains; opt-in
+        with AIKO_C2F_S2=1."""
+        import os
+        l1 = self.l1
+        return (a0.is_cuda and os.environ.get("AIKO_C2F_FUSED", "1") != "0"
+                and os.environ.get("AIKO_C2F_S2", "0") == "1"      # opt-in: measured no faster (see below)
+                and l1.kind == "conv" and l1.R == 3 and l1.S == 3 and l1.stride == 2 and l1.pad == 1 and l1.Cc == 16
+                and a0.shape[3] == 16 and a0.shape[1] == 2 * a2.shape[1] and a0.shape[2] == 2 * a2.shape[2]
+                and self._c2f_fused_ok(self.l2, a2, a2) and a0.stride(3) == 1)
+
     @staticmethod
     def _c2f_rb(H):
         """Band height: 160-row images 40 (bench sweep 32-160), 80-row images 20."""
@@ -285,8 +298,16 @@ class YOLOv8(WeightsMixin):
         (H1, W1), (H2, W2), (H3, W3), (H4, W4), (H5, W5) = s
         if a0 is None:
             a0 = C.conv2d(x, self.l0, out=self._buf("a0", (B, H1, W1, c1)), image_hw=(S, S))
-        a1 = C.conv2d(a0, self.l1, out=self._buf("a1", (B, H2, W2, c2)))
-        a2 = self._run_c2f("l2", self.l2, a1, self._buf("a2", (B, H2, W2, c2)))
+        a2 = self._buf("a2", (B, H2, W2, c2))
+        if self._l1l2_fused_ok(a0, a2):
+            # l1 (3x3 / 2) and the l2 C2f in one row-stream launch: a1 is never written
+            a, b = self.l2.m[0]
+            torch.ops.aiko.c2f_fused_s2_out(a0, self.l1.weight, self.l1.bias, self.l2.cv1.weight, self.l2.cv1.bias,
+                                            a.weight, a.bias, b.weight, b.bias, self.l2.cv2.weight, self.l2.cv2.bias,
+                                            a2, self.l2.shortcut, self._c2f_rb(H2))
+        else:
+            a1 = C.conv2d(a0, self.l1, out=self._buf("a1", (B, H2, W2, c2)))
+            a2 = self._run_c2f("l2", self.l2, a1, a2)
         a3 = C.conv2d(a2, self.l3, out=self._buf("a3", (B, H3, W3, c3)))
         cat14 = self._buf("cat14", (B, H3, W3, c4 + c3))       # [up(l12) | l4]
         a4 = self._run_c2f("l4", self.l4, a3, cat14[..., c4:])

@@ -326,3 +326,27 @@ def test_c2f_bneck_fused_matches_unfused(native, monkeypatch, rb):
     cos = torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()
     assert cos > 0.9995, cos
     assert (a - b).abs().max().item() < 0.05 * b.abs().max().item()
+
+
+def test_c2f_fused_s2_matches_unfused(native, monkeypatch):
+    """l1 (3x3 / 2, 16 -> 32) fused in front of the l2 C2f (c2f_fused_s2_kernel: a1 never leaves
+    LDS) against l1 as its own conv + the fused C2f, two images."""
+    from aiko_services_amd.models.yolov8 import YOLOv8
+    from aiko_services_amd.ops import conv as C
+    m = YOLOv8("n", device=DEV)
+    g = torch.Generator().manual_seed(3)
+    a0 = (torch.randn(2, 320, 320, 16, generator=g) * 2).to(DEV, torch.bfloat16)
+    out_f = torch.full((2, 160, 160, 32), 7.0, dtype=torch.bfloat16, device=DEV)
+    monkeypatch.setenv("AIKO_C2F_S2", "1")
+    assert m._l1l2_fused_ok(a0, out_f)
+    a, b = m.l2.m[0]
+    torch.ops.aiko.c2f_fused_s2_out(a0, m.l1.weight, m.l1.bias, m.l2.cv1.weight, m.l2.cv1.bias, a.weight, a.bias,
+                                    b.weight, b.bias, m.l2.cv2.weight, m.l2.cv2.bias, out_f, True, 40)
+    a1 = C.conv2d(a0, m.l1)
+    out_u = torch.empty_like(out_f)
+    m._run_c2f("l2u", m.l2, a1, out_u)
+    torch.cuda.synchronize()
+    x, y = out_f.float(), out_u.float()
+    cos = torch.nn.functional.cosine_similarity(x.flatten(), y.flatten(), dim=0).item()
+    assert cos > 0.9995, cos
+    assert (x - y).abs().max().item() < 0.05 * y.abs().max().item()
