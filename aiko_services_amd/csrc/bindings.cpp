@@ -474,7 +474,8 @@ void conv_chain_out(const at::Tensor& A, const at::Tensor& W1, const at::Tensor&
   const int64_t N1 = W1.size(0), K1 = W1.size(1), N2 = W2.size(0);
   const bool shape_ok = dual ? (K1 == 128 && N1 == 256 && N2 == 64)
                              : ((K1 == 64 && N1 == 256 && (N2 == 64 || N2 == 128)) ||
-                                (K1 == 128 && N1 == 512 && (N2 == 128 || N2 == 256)));
+                                (K1 == 128 && N1 == 512 && (N2 == 128 || N2 == 256)) ||
+                                (K1 == 256 && N1 == 1024 && N2 == 256));
   TORCH_CHECK(shape_ok, "aiko.conv_chain_out: unsupported (K1, N1, N2) = (", K1, ", ", N1, ", ", N2, ")", dual ? " dual" : "");
   const int64_t ka = dual ? K1 / 2 : K1;           // width of each A source
   const int64_t M = A.numel() / ka;

@@ -755,6 +755,12 @@ def _chain_stage2() -> bool:
     return __import__("os").environ.get("AIKO_CHAIN_STAGE2", "0") == "1"
 
 
+def _chain_stage3() -> bool:
+    """``AIKO_CHAIN3=1`` admits the stage-3 chain (256 -> 1024 + residual -> 256 on
+    ``conv_chain3.hip``; read at call time)."""
+    return __import__("os").environ.get("AIKO_CHAIN3", "0") == "1"
+
+
 def chain_ok(spec3: ConvSpec, spec1: ConvSpec) -> bool:
     """Can ``spec3`` (1x1 expansion, identity residual) and the next block's ``spec1`` (1x1
     reduction) run as one ``conv_chain`` launch?"""
@@ -768,6 +774,8 @@ def chain_ok(spec3: ConvSpec, spec1: ConvSpec) -> bool:
         shapes[(128, 512)] = (128,)
     if _chain_stage2():
         shapes[(128, 512)] = (128, 256)
+    if _chain_stage3():
+        shapes[(256, 1024)] = (256,)
     k1, n1 = spec3.weight.shape[1], spec3.weight.shape[0]
     return (one_by_one(spec3) and one_by_one(spec1) and spec3.cin == k1 and (k1, n1) in shapes
             and spec1.cin == n1 and spec1.weight.shape[1] == n1 and spec1.cout in shapes[(k1, n1)]
