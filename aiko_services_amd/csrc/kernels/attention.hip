@@ -293,7 +293,7 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const int r0 = 32 * ks + 4 * g + trq;
-        if constexpr (VA) {
+        if constexpr (VA & 1) {
           const uint32_t a0 = (uint32_t)reinterpret_cast<uintptr_t>(vb + v_off(r0, d * 16 + 4 * trp));
           const uint32_t a1 = (uint32_t)reinterpret_cast<uintptr_t>(vb + v_off(r0 + 16, d * 16 + 4 * trp));
           v4i16 lo, hi;
@@ -311,7 +311,7 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
     };
     // VA: every V read issued so far has landed (no use of the fragments above this point)
     auto wait_v = [&](int d0, int d1) {
-      if constexpr (VA) {
+      if constexpr (VA & 1) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         for (int d = d0; d < d1; ++d)
 #pragma unroll
@@ -320,6 +320,12 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
     };
 
   // S^T = K Q^T : 4 key tiles x 2 query tiles
+    // VA & 2: raised wave priority over the MFMA clusters (s_setprio), so that a wave reaching
+    // its matrix work is issued ahead of the co-resident waves' softmax VALU work — the
+    // workgroup's barriers otherwise keep all waves in the same phase.  Measured (round 5,
+    // scripts/r5_attn_prio.sh, B = 14): 129.9-133.2 us vs 129.2-132.6 us (variant 19 vs 0), bench
+    // 3,373 vs 3,329-3,372 windows/s — no effect; variants 19 / 20 opt-in
+    if constexpr ((VA & 2) != 0) __builtin_amdgcn_s_setprio(2);
     f32x4 s[4][2];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
@@ -339,6 +345,7 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
       }
     }
 
+    if constexpr ((VA & 2) != 0) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
     for (int d = 0; d < VPRE; ++d) read_v(d);
 
@@ -469,7 +476,8 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
 
     // O^T += V^T P^T (fragments read above / here)
     if constexpr (SM != 2) {
-    if constexpr (VA) wait_v(0, VPRE);
+    if constexpr ((VA & 2) != 0) __builtin_amdgcn_s_setprio(2);
+    if constexpr (VA & 1) wait_v(0, VPRE);
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       if (d >= VPRE) {
@@ -489,6 +497,7 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
         for (int qt = 0; qt < 2; ++qt)
           lsum[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qt][ks], lsum[qt], 0, 0, 0);
     }
+    if constexpr ((VA & 2) != 0) __builtin_amdgcn_s_setprio(0);
     }
 
     slot = slot == NS - 1 ? 0 : slot + 1;
@@ -732,6 +741,8 @@ extern "C" int aiko_attn_fwd(const void* q, const void* k, const void* v, void* 
     case 16: launch(I8{}, V0{}, R0{}, R1{}, A1{}); break;   // asm V reads, per d-block wait
     case 17: launch(I8{}, std::integral_constant<int, 4>{}, R0{}, R1{}, A1{}); break;   // all V reads before the softmax
     case 18: launch(I8{}, V2{}, R0{}, R1{}, A1{}); break;
+    case 19: launch(I8{}, V0{}, R0{}, R1{}, std::integral_constant<int, 2>{}); break;   // s_setprio over MFMAs
+    case 20: launch(I8{}, V2{}, R0{}, R1{}, std::integral_constant<int, 2>{}); break;
     default: launch(I8{}, V0{}, R0{}, R1{}, A0{}); break;
   }
   return (int)hipGetLastError();
