@@ -35,6 +35,9 @@ int aiko_conv_persist(const void* x, const void* w, const float* bias, const voi
                       int H, int W, int C, int Cc, int R, int S, int stride, int pad, int Ho, int Wo,
                       int M, int Cout, int K, int act, int ldy, int ldr, int bm, int bn, const void* x2,
                       int K1, int H2, int W2, int C2, int stride2, hipStream_t stream);
+int aiko_conv_glds_tail(const void* x, const void* w, const float* bias, int H, int W, int C, int Cc, int R, int S,
+                        int stride, int pad, int Ho, int Wo, int M, int K, int act, const void* w2, const float* b2,
+                        void* y2, int ldy2, int ldw2, const void* zero, hipStream_t stream);
 int aiko_conv_glds(const void* x, const void* w, const float* bias, const void* res, void* y,
                    int H, int W, int C, int Cc, int R, int S, int stride, int pad, int Ho,
                    int Wo, int M, int Cout, int K, int act, int ldy, int ldr, int bm, int bn,
@@ -589,6 +592,43 @@ void c2f_bneck_out(const at::Tensor& x, const at::Tensor& wa, const at::Tensor& 
                               bb.data_ptr<float>(), (int)wb.size(1), y.data_ptr(), (int)ldy, (int)B, (int)H, (int)W, (int)C,
                               shortcut ? 1 : 0, (int)rb, cur_stream()),
                "c2f_bneck");
+}
+
+// R x R conv (Cout 80, exact 128 x 80 tile, LDS-DMA kernel) with a fused trailing 1x1 80 -> 80 + bias
+// (conv_glds.hip, TAIL): y2 = (act(conv(x) + bias)) . w2[:, :80]^T + b2.  x, y2: NHWC channel-slice
+// views; w [80, K] and w2 [80, >= 96] with zero K padding (conv spec layout).
+void conv_glds_tail_out(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, const at::Tensor& w2,
+                        const at::Tensor& b2, at::Tensor& y2, int64_t R, int64_t stride, int64_t pad, int64_t act,
+                        const at::Tensor& zero) {
+  for (const at::Tensor* t : {&x, &w, &bias, &w2, &b2, (const at::Tensor*)&y2, &zero}) check_cuda(*t, "conv tail operand");
+  for (const at::Tensor* t : {&x, &w, &w2, (const at::Tensor*)&y2})
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16, "aiko.conv_glds_tail_out: bf16 activations / weights");
+  TORCH_CHECK(bias.scalar_type() == at::kFloat && b2.scalar_type() == at::kFloat && bias.numel() == 80 &&
+                  b2.numel() == 80 && bias.is_contiguous() && b2.is_contiguous(),
+              "aiko.conv_glds_tail_out: fp32 biases [80]");
+  TORCH_CHECK(x.dim() == 4 && y2.dim() == 4 && x.stride(3) == 1 && y2.stride(3) == 1, "aiko.conv_glds_tail_out: NHWC");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), Cc = x.size(3), C = x.stride(2);
+  TORCH_CHECK(x.stride(1) == W * C && x.stride(0) == H * W * C && C % 8 == 0 && Cc % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "aiko.conv_glds_tail_out: x must be an NHWC (channel-slice) view with 16-B aligned pixels");
+  const int64_t K = (R * R * Cc + 63) / 64 * 64;
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && w.size(0) == 80 && w.size(1) == K,
+              "aiko.conv_glds_tail_out: w must be [80, ceil64(R*R*Cc)]");
+  TORCH_CHECK(w2.dim() == 2 && w2.is_contiguous() && w2.size(0) == 80 && w2.size(1) >= 96 && w2.size(1) % 8 == 0,
+              "aiko.conv_glds_tail_out: w2 must be [80, >= 96] (zero past column 80)");
+  const int64_t Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - R) / stride + 1;
+  const int64_t ldy2 = y2.stride(2);
+  TORCH_CHECK(y2.size(0) == B && y2.size(1) == Ho && y2.size(2) == Wo && y2.size(3) == 80 &&
+                  y2.stride(1) == Wo * ldy2 && y2.stride(0) == Ho * Wo * ldy2 && ldy2 % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(y2.data_ptr()) % 16 == 0,
+              "aiko.conv_glds_tail_out: y2 must be an NHWC [B, Ho, Wo, 80] (channel-slice) view");
+  const int64_t M = B * Ho * Wo;
+  TORCH_CHECK(avail_elems(x) < INT_MAX && avail_elems(y2) < INT_MAX, "aiko.conv_glds_tail_out: 32-bit offsets");
+  check_launch(aiko_conv_glds_tail(x.data_ptr(), w.data_ptr(), bias.data_ptr<float>(), (int)H, (int)W, (int)C, (int)Cc,
+                                   (int)R, (int)R, (int)stride, (int)pad, (int)Ho, (int)Wo, (int)M, (int)K, (int)act,
+                                   w2.data_ptr(), b2.data_ptr<float>(), y2.data_ptr(), (int)ldy2, (int)w2.size(1),
+                                   zero.data_ptr(), cur_stream()),
+               "conv_glds_tail");
 }
 
 // A whole ResNet stage-1 bottleneck in one launch (bneck_fused.hip): x [B, H, 56, cin] ->
@@ -1481,6 +1521,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("c2f_fused_out(Tensor x, Tensor w1, Tensor b1, Tensor wa, Tensor ba, Tensor wb, Tensor bb, Tensor w2, Tensor b2, Tensor(a!) y, int ci, bool shortcut, int rb) -> ()");
   m.def("c2f_fused_s2_out(Tensor a0, Tensor w0, Tensor b0, Tensor w1, Tensor b1, Tensor wa, Tensor ba, Tensor wb, Tensor bb, Tensor w2, Tensor b2, Tensor(a!) y, bool shortcut, int rb) -> ()");
   m.def("c2f_bneck_out(Tensor x, Tensor wa, Tensor ba, Tensor wb, Tensor bb, Tensor(a!) y, bool shortcut, int rb) -> ()");
+  m.def("conv_glds_tail_out(Tensor x, Tensor w, Tensor bias, Tensor w2, Tensor b2, Tensor(a!) y2, int R, int stride, int pad, int act, Tensor zero) -> ()");
   m.def("linear_splitk_out(Tensor x, Tensor w, Tensor? bias, Tensor(a!) part, Tensor(b!) y, int K, int S) -> ()");
   m.def("attn_fwd_out(Tensor q, Tensor k, Tensor v, Tensor(a!) o, int B, int H, int T, int Tpad, float scale, Tensor(b!)? work=None, Tensor(c!)? oq=None, Tensor(d!)? osc=None) -> ()");
   m.def("logmel_out(Tensor audio, Tensor mel, Tensor mel_range, int n_fft, int hop, int F, Tensor(a!) work, Tensor(b!) gmax, Tensor(c!) dst, int rows, int pad) -> ()");
@@ -1520,6 +1561,7 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("rowstats_mx_out", &rowstats_mx_out);
   m.impl("c2f_fused_out", &c2f_fused_out);
   m.impl("c2f_bneck_out", &c2f_bneck_out);
+  m.impl("conv_glds_tail_out", &conv_glds_tail_out);
   m.impl("c2f_fused_s2_out", &c2f_fused_s2_out);
   m.impl("attn_fwd_out", &attn_fwd_out);
   m.impl("linear_splitk_out", &linear_splitk_out);

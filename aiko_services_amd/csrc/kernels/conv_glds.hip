@@ -45,10 +45,22 @@ __device__ __forceinline__ void wait_vm_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
+// TAIL: a following 1x1 conv fused into the epilogue (YOLOv8 detect head: 3x3 80 -> 80 + SiLU,
+// then the 1x1 80 -> 80 class logits).  The activated 3x3 tile is packed to bf16 in LDS (K
+// columns 80..95 zeroed) and never written to HBM; the 1x1's weights ([N2][ldw2], K zero-padded
+// to a multiple of 64 as every conv spec is) come straight from L2 as B fragments.
+struct GldsTail {
+  const bf16_t* w2;
+  const float* b2;
+  bf16_t* y2;
+  int ldy2, ldw2;
+};
+
 // WGM x WGN waves (2 x 2; exact-N tiles such as BN = 80: 4 x 1, each wave all BN columns)
-template <int BM, int BN, int WGM = 2, int WGN = 2>
+template <int BM, int BN, int WGM = 2, int WGN = 2, bool TAIL = false>
 __global__ __launch_bounds__(256, (glds_occupancy<BM, BN>())) void conv_glds_kernel(ConvParams p,
-                                                                                 const bf16_t* zero) {
+                                                                                 const bf16_t* zero,
+                                                                                 GldsTail tl) {
   static_assert(WGM * WGN == 4, "four waves");
   constexpr int BK = 64;
   constexpr int NS = glds_slots<BM, BN>();     // LDS ring slots
@@ -63,7 +75,11 @@ __global__ __launch_bounds__(256, (glds_occupancy<BM, BN>())) void conv_glds_ker
   constexpr int CPAD = 4;
   constexpr int EPI_BYTES = BM * (BN + CPAD) * 4;
   constexpr int RING_BYTES = NS * STAGE_ELEMS * 2;
-  constexpr int LDS_BYTES = EPI_BYTES > RING_BYTES ? EPI_BYTES : RING_BYTES;
+  static_assert(!TAIL || (WGN == 1 && BN == 80), "tail: 4 x 1 waves over the 80-channel tile");
+  constexpr int TP = 104;                      // tail: bf16 row pitch of the activated tile (96 + 8)
+  constexpr int TAIL_BYTES = TAIL ? BM * TP * 2 : 0;
+  constexpr int LDS_NEED = EPI_BYTES + TAIL_BYTES;
+  constexpr int LDS_BYTES = LDS_NEED > RING_BYTES ? LDS_NEED : RING_BYTES;
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
   bf16_t* ring = reinterpret_cast<bf16_t*>(smem);
 
@@ -272,7 +288,63 @@ __global__ __launch_bounds__(256, (glds_occupancy<BM, BN>())) void conv_glds_ker
     u32x4 o;
 #pragma unroll
     for (int e = 0; e < 4; ++e) o[e] = pack2(v[2 * e], v[2 * e + 1]);
-    *reinterpret_cast<u32x4*>(p.y + (size_t)m * p.ldy + e_n) = o;
+    if constexpr (TAIL)
+      *reinterpret_cast<u32x4*>(smem + EPI_BYTES + (row * TP + cc * 8) * 2) = o;
+    else
+      *reinterpret_cast<u32x4*>(p.y + (size_t)m * p.ldy + e_n) = o;
+  }
+  if constexpr (TAIL) {
+    bf16_t* Ts = reinterpret_cast<bf16_t*>(smem + EPI_BYTES);
+    // K columns 80..95 of every row are zero (two 16-B chunks per row); rows past M stay whatever
+    // the skipped chunks left — their outputs are never stored
+    for (int c = tid; c < BM * 2; c += 256)
+      *reinterpret_cast<u32x4*>(Ts + (c >> 1) * TP + 80 + (c & 1) * 8) = u32x4{0u, 0u, 0u, 0u};
+    __syncthreads();                   // activated tile complete; every Cs read done
+    // 1x1: out[32 w + 16 i + 4 fq + e][16 j + fr], K = 96 (three 32-deep steps)
+    constexpr int MI2 = BM / 4 / 16, NI2 = 80 / 16;
+    f32x4 acc2[MI2][NI2];
+#pragma unroll
+    for (int i = 0; i < MI2; ++i)
+#pragma unroll
+      for (int j = 0; j < NI2; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) {
+      bf16x8 af[MI2], bfr[NI2];
+#pragma unroll
+      for (int i = 0; i < MI2; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(Ts + (wave * (BM / 4) + 16 * i + fr) * TP + 32 * ks + 8 * fq);
+#pragma unroll
+      for (int j = 0; j < NI2; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(tl.w2 + (size_t)(16 * j + fr) * tl.ldw2 + 32 * ks + 8 * fq);
+#pragma unroll
+      for (int i = 0; i < MI2; ++i)
+#pragma unroll
+        for (int j = 0; j < NI2; ++j)
+          acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc2[i][j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < MI2; ++i)
+#pragma unroll
+      for (int j = 0; j < NI2; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Cs[(wave * (BM / 4) + i * 16 + fq * 4 + e) * LDC + j * 16 + fr] = acc2[i][j][e];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int row = e_row_of(i), cc = e_cc_of(i);
+      const int m = m0 + row;
+      if (m >= p.M) continue;
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + cc * 8);
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + cc * 8 + 4);
+      const f32x4 c0 = *reinterpret_cast<const f32x4*>(tl.b2 + cc * 8);
+      const f32x4 c1 = *reinterpret_cast<const f32x4*>(tl.b2 + cc * 8 + 4);
+      u32x4 o;
+      o[0] = pack2(v0[0] + c0[0], v0[1] + c0[1]);
+      o[1] = pack2(v0[2] + c0[2], v0[3] + c0[3]);
+      o[2] = pack2(v1[0] + c1[0], v1[1] + c1[1]);
+      o[3] = pack2(v1[2] + c1[2], v1[3] + c1[3]);
+      *reinterpret_cast<u32x4*>(tl.y2 + (size_t)m * tl.ldy2 + cc * 8) = o;
+    }
   }
 }
 
@@ -300,19 +372,45 @@ extern "C" int aiko_conv_glds(const void* x, const void* w, const float* bias, c
   const bf16_t* z = static_cast<const bf16_t*>(zero);
   dim3 grid(((M + bm - 1) / bm) * ((Cout + bn - 1) / bn)), block(256);
   if (bm == 128 && bn == 128) {
-    conv_glds_kernel<128, 128><<<grid, block, 0, stream>>>(p, z);
+    conv_glds_kernel<128, 128><<<grid, block, 0, stream>>>(p, z, GldsTail{});
   } else if (bm == 128 && bn == 64) {
-    conv_glds_kernel<128, 64><<<grid, block, 0, stream>>>(p, z);
+    conv_glds_kernel<128, 64><<<grid, block, 0, stream>>>(p, z, GldsTail{});
   } else if (bm == 64 && bn == 64) {
-    conv_glds_kernel<64, 64><<<grid, block, 0, stream>>>(p, z);
+    conv_glds_kernel<64, 64><<<grid, block, 0, stream>>>(p, z, GldsTail{});
   } else if (bm == 64 && bn == 128) {
-    conv_glds_kernel<64, 128><<<grid, block, 0, stream>>>(p, z);
+    conv_glds_kernel<64, 128><<<grid, block, 0, stream>>>(p, z, GldsTail{});
   } else if (bm == 128 && bn == 80) {              // exact-N tiles (YOLO's 80-class head convs)
-    conv_glds_kernel<128, 80, 4, 1><<<grid, block, 0, stream>>>(p, z);
+    conv_glds_kernel<128, 80, 4, 1><<<grid, block, 0, stream>>>(p, z, GldsTail{});
   } else if (bm == 256 && bn == 80) {
-    conv_glds_kernel<256, 80, 4, 1><<<grid, block, 0, stream>>>(p, z);
+    conv_glds_kernel<256, 80, 4, 1><<<grid, block, 0, stream>>>(p, z, GldsTail{});
   } else {
     return -1;
   }
+  return (int)hipGetLastError();
+}
+
+// 3x3 (or any R x S) conv with an exact 80-channel tile and a fused trailing 1x1 80 -> 80 (+ bias,
+// no activation) in the epilogue: y2 [M][ldy2] = (act(conv(x) + bias)) . w2[:, :80]^T + b2.
+// Same geometry arguments as aiko_conv_glds (no residual, no second source); bm x bn = 128 x 80.
+extern "C" int aiko_conv_glds_tail(const void* x, const void* w, const float* bias, int H, int W, int C, int Cc,
+                                   int R, int S, int stride, int pad, int Ho, int Wo, int M, int K, int act,
+                                   const void* w2, const float* b2, void* y2, int ldy2, int ldw2, const void* zero,
+                                   hipStream_t stream) {
+  using namespace aiko;
+  ConvParams p;
+  p.x = static_cast<const bf16_t*>(x);
+  p.w = static_cast<const bf16_t*>(w);
+  p.bias = bias;
+  p.res = nullptr;
+  p.y = nullptr;
+  p.H = H; p.W = W; p.C = C; p.Cc = Cc; p.R = R; p.S = S;
+  p.stride = stride; p.pad = pad; p.Ho = Ho; p.Wo = Wo; p.M = M; p.Cout = 80; p.K = K;
+  p.act = act; p.ldy = 80; p.ldr = 0;
+  p.x2 = nullptr;
+  p.K1 = K; p.H2 = 1; p.W2 = 1; p.C2 = 8; p.stride2 = 1;
+  conv_params_finalize(p);
+  GldsTail tl{static_cast<const bf16_t*>(w2), b2, static_cast<bf16_t*>(y2), ldy2, ldw2};
+  dim3 grid((M + 127) / 128), block(256);
+  conv_glds_kernel<128, 80, 4, 1, true><<<grid, block, 0, stream>>>(p, static_cast<const bf16_t*>(zero), tl);
   return (int)hipGetLastError();
 }

@@ -35,6 +35,9 @@ SCALES = {"n": (0.33, 0.25, 1024), "s": (0.33, 0.50, 1024), "m": (0.67, 0.75, 76
           "l": (1.00, 1.00, 512), "x": (1.00, 1.25, 512)}
 STRIDES = (8, 16, 32)
 REG_MAX = 16
+# the detect head's class branch as one conv_glds launch with the 1x1 in its epilogue
+# (AIKO_HEAD_TAIL=0: the two separate convs)
+_HEAD_TAIL = __import__("os").environ.get("AIKO_HEAD_TAIL", "1") != "0"
 
 
 def _make_div(x, d=8):
@@ -248,9 +251,13 @@ class YOLOv8(WeightsMixin):
         out = self._buf(f"h{i}.out", (B, H, W, 4 * REG_MAX + self.nc_pad))
         C.conv2d(x, lvl.first, out=h1)
         C.conv2d(h1[..., :cb], lvl.box[1], out=h2[..., :cb])
-        C.conv2d(h1[..., cb:], lvl.cls[1], out=h2[..., cb:])
         C.conv2d(h2[..., :cb], lvl.box[2], out=out[..., :4 * REG_MAX])
-        C.conv2d(h2[..., cb:], lvl.cls[2], out=out[..., 4 * REG_MAX:])
+        if _HEAD_TAIL and C.conv_tail_ok(h1[..., cb:], lvl.cls[1], lvl.cls[2]):
+            # class branch: 3x3 80 -> 80 + SiLU and the 1x1 80 -> 80 logits in one launch
+            C.conv2d_tail(h1[..., cb:], lvl.cls[1], lvl.cls[2], out[..., 4 * REG_MAX:])
+        else:
+            C.conv2d(h1[..., cb:], lvl.cls[1], out=h2[..., cb:])
+            C.conv2d(h2[..., cb:], lvl.cls[2], out=out[..., 4 * REG_MAX:])
         return out
 
     # ---- forward ------------------------------------------------------------------------------

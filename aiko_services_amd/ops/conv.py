@@ -755,6 +755,29 @@ def _chain_stage2() -> bool:
     return __import__("os").environ.get("AIKO_CHAIN_STAGE2", "0") == "1"
 
 
+def conv_tail_ok(x: torch.Tensor, spec: ConvSpec, spec2: ConvSpec) -> bool:
+    """Can ``spec`` (a 3x3 conv to 80 channels) and the following 1x1 ``spec2`` (80 -> 80, bias,
+    no activation) run as ONE ``conv_glds`` launch with the 1x1 in its epilogue (the YOLOv8 detect
+    head's class branch)?"""
+    return (spec.kind == "conv" and spec.R == spec.S == 3 and spec.K1 is None and spec.cout == 80
+            and spec.bias is not None and x.dim() == 4 and x.shape[3] == spec.Cc and spec.Cc % 8 == 0
+            and x.stride(3) == 1 and x.stride(2) % 8 == 0
+            and spec2.kind == "conv" and spec2.R == spec2.S == 1 and spec2.stride == 1 and spec2.pad == 0
+            and spec2.K1 is None and spec2.Cc == 80 and spec2.cout == 80 and spec2.bias is not None
+            and spec2.act == ACT_NONE and spec2.weight.shape[1] >= 96)
+
+
+def conv2d_tail(x: torch.Tensor, spec: ConvSpec, spec2: ConvSpec, out: torch.Tensor) -> torch.Tensor:
+    """``out = conv1x1(act(conv(x, spec)), spec2)`` in one launch (``conv_glds.hip`` TAIL: the
+    activated 3x3 tile stays in LDS and feeds the 1x1's MFMAs; it is never written to HBM).
+    ``x`` / ``out`` may be channel-slice views.  See :func:`conv_tail_ok`."""
+    if not conv_tail_ok(x, spec, spec2):
+        raise ValueError("conv2d_tail: shapes not eligible (see conv_tail_ok)")
+    torch.ops.aiko.conv_glds_tail_out(x, spec.weight, spec.bias, spec2.weight, spec2.bias, out, spec.R, spec.stride,
+                                      spec.pad, spec.act, zero_page(x.device))
+    return out
+
+
 def _chain_stage3() -> bool:
     """``AIKO_CHAIN3=1`` admits the stage-3 chain (256 -> 1024 + residual -> 256 on
     ``conv_chain3.hip``; read at call time)."""

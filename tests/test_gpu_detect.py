@@ -350,3 +350,42 @@ def test_c2f_fused_s2_matches_unfused(native, monkeypatch):
     cos = torch.nn.functional.cosine_similarity(x.flatten(), y.flatten(), dim=0).item()
     assert cos > 0.9995, cos
     assert (x - y).abs().max().item() < 0.05 * y.abs().max().item()
+
+
+@pytest.mark.parametrize("hw", [(80, 80), (40, 40), (20, 20)])
+def test_conv_tail_matches_two_convs(native, monkeypatch, hw):
+    """Detect-head class branch as ONE launch (conv_glds TAIL: 3x3 80 -> 80 + SiLU with the 1x1
+    80 -> 80 logits in the epilogue) against the two separate convs, at the three head levels;
+    input and output are channel slices of the head's [.., 64 + 80] buffers."""
+    from aiko_services_amd.models import yolov8 as Y
+    from aiko_services_amd.ops import conv as C
+    m = Y.YOLOv8("n", device=DEV)
+    lvl = m.heads[0]
+    g = torch.Generator().manual_seed(hw[0])
+    h1 = (torch.randn(2, hw[0], hw[1], 144, generator=g) * 2).to(DEV, torch.bfloat16)
+    out_f = torch.full((2, hw[0], hw[1], 144), 7.0, dtype=torch.bfloat16, device=DEV)
+    assert C.conv_tail_ok(h1[..., 64:], lvl.cls[1], lvl.cls[2])
+    C.conv2d_tail(h1[..., 64:], lvl.cls[1], lvl.cls[2], out_f[..., 64:])
+    t = C.conv2d(h1[..., 64:], lvl.cls[1])
+    ref = C.conv2d(t, lvl.cls[2])
+    torch.cuda.synchronize()
+    assert torch.equal(out_f[..., :64], torch.full_like(out_f[..., :64], 7.0))   # box slice untouched
+    a, b = out_f[..., 64:].float(), ref.float()
+    cos = torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()
+    assert cos > 0.9999, cos
+    assert (a - b).abs().max().item() < 0.02 * b.abs().max().item()
+    # fp32 reference of the same two convs
+    xr = h1[..., 64:].float().permute(0, 3, 1, 2)
+    tr = torch.nn.functional.silu(torch.nn.functional.conv2d(xr, lvl.cls[1].ref_weight.to(DEV), lvl.cls[1].ref_bias.to(DEV), padding=1))
+    yr = torch.nn.functional.conv2d(tr, lvl.cls[2].ref_weight.to(DEV), lvl.cls[2].ref_bias.to(DEV)).permute(0, 2, 3, 1)
+    assert ((a - yr).norm() / yr.norm()).item() < 1e-2
+    # the model's level-0 head with and without the fused class branch
+    p3 = (torch.randn(2, hw[0], hw[1], 64, generator=g) * 2).to(DEV, torch.bfloat16)
+    monkeypatch.setattr(Y, "_HEAD_TAIL", True)
+    o_f = m._run_head(0, lvl, p3).clone()
+    monkeypatch.setattr(Y, "_HEAD_TAIL", False)
+    o_u = m._run_head(0, lvl, p3).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(o_f[..., :64], o_u[..., :64])
+    a, b = o_f[..., 64:].float(), o_u[..., 64:].float()
+    assert torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item() > 0.9999
