@@ -36,7 +36,7 @@ int aiko_conv_persist(const void* x, const void* w, const float* bias, const voi
                       int M, int Cout, int K, int act, int ldy, int ldr, int bm, int bn, const void* x2,
                       int K1, int H2, int W2, int C2, int stride2, hipStream_t stream);
 int aiko_conv_glds_tail(const void* x, const void* w, const float* bias, int H, int W, int C, int Cc, int R, int S,
-                        int stride, int pad, int Ho, int Wo, int M, int K, int act, const void* w2, const float* b2,
+                        int stride, int pad, int Ho, int Wo, int M, int K, int N, int act, const void* w2, const float* b2,
                         void* y2, int ldy2, int ldw2, const void* zero, hipStream_t stream);
 int aiko_conv_glds(const void* x, const void* w, const float* bias, const void* res, void* y,
                    int H, int W, int C, int Cc, int R, int S, int stride, int pad, int Ho,
@@ -594,38 +594,41 @@ void c2f_bneck_out(const at::Tensor& x, const at::Tensor& wa, const at::Tensor& 
                "c2f_bneck");
 }
 
-// R x R conv (Cout 80, exact 128 x 80 tile, LDS-DMA kernel) with a fused trailing 1x1 80 -> 80 + bias
-// (conv_glds.hip, TAIL): y2 = (act(conv(x) + bias)) . w2[:, :80]^T + b2.  x, y2: NHWC channel-slice
-// views; w [80, K] and w2 [80, >= 96] with zero K padding (conv spec layout).
+// R x R conv (Cout N = 64 or 80, exact-N tile, LDS-DMA kernel) with a fused trailing 1x1 N -> N + bias
+// (conv_glds.hip, TAIL): y2 = (act(conv(x) + bias)) . w2[:, :N]^T + b2.  x, y2: NHWC channel-slice
+// views; w [N, K] and w2 [N, >= ceil32(N)] with zero K padding (conv spec layout).
 void conv_glds_tail_out(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, const at::Tensor& w2,
                         const at::Tensor& b2, at::Tensor& y2, int64_t R, int64_t stride, int64_t pad, int64_t act,
                         const at::Tensor& zero) {
   for (const at::Tensor* t : {&x, &w, &bias, &w2, &b2, (const at::Tensor*)&y2, &zero}) check_cuda(*t, "conv tail operand");
   for (const at::Tensor* t : {&x, &w, &w2, (const at::Tensor*)&y2})
     TORCH_CHECK(t->scalar_type() == at::kBFloat16, "aiko.conv_glds_tail_out: bf16 activations / weights");
-  TORCH_CHECK(bias.scalar_type() == at::kFloat && b2.scalar_type() == at::kFloat && bias.numel() == 80 &&
-                  b2.numel() == 80 && bias.is_contiguous() && b2.is_contiguous(),
-              "aiko.conv_glds_tail_out: fp32 biases [80]");
+  const int64_t N = w.size(0);
+  TORCH_CHECK(N == 64 || N == 80, "aiko.conv_glds_tail_out: N = 64 or 80");
+  TORCH_CHECK(bias.scalar_type() == at::kFloat && b2.scalar_type() == at::kFloat && bias.numel() == N &&
+                  b2.numel() == N && bias.is_contiguous() && b2.is_contiguous(),
+              "aiko.conv_glds_tail_out: fp32 biases [N]");
   TORCH_CHECK(x.dim() == 4 && y2.dim() == 4 && x.stride(3) == 1 && y2.stride(3) == 1, "aiko.conv_glds_tail_out: NHWC");
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), Cc = x.size(3), C = x.stride(2);
   TORCH_CHECK(x.stride(1) == W * C && x.stride(0) == H * W * C && C % 8 == 0 && Cc % 8 == 0 &&
                   reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
               "aiko.conv_glds_tail_out: x must be an NHWC (channel-slice) view with 16-B aligned pixels");
   const int64_t K = (R * R * Cc + 63) / 64 * 64;
-  TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && w.size(0) == 80 && w.size(1) == K,
-              "aiko.conv_glds_tail_out: w must be [80, ceil64(R*R*Cc)]");
-  TORCH_CHECK(w2.dim() == 2 && w2.is_contiguous() && w2.size(0) == 80 && w2.size(1) >= 96 && w2.size(1) % 8 == 0,
-              "aiko.conv_glds_tail_out: w2 must be [80, >= 96] (zero past column 80)");
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && w.size(1) == K,
+              "aiko.conv_glds_tail_out: w must be [N, ceil64(R*R*Cc)]");
+  TORCH_CHECK(w2.dim() == 2 && w2.is_contiguous() && w2.size(0) == N && w2.size(1) >= (N + 31) / 32 * 32 &&
+                  w2.size(1) % 8 == 0,
+              "aiko.conv_glds_tail_out: w2 must be [N, >= ceil32(N)] (zero past column N)");
   const int64_t Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - R) / stride + 1;
   const int64_t ldy2 = y2.stride(2);
-  TORCH_CHECK(y2.size(0) == B && y2.size(1) == Ho && y2.size(2) == Wo && y2.size(3) == 80 &&
+  TORCH_CHECK(y2.size(0) == B && y2.size(1) == Ho && y2.size(2) == Wo && y2.size(3) == N &&
                   y2.stride(1) == Wo * ldy2 && y2.stride(0) == Ho * Wo * ldy2 && ldy2 % 8 == 0 &&
                   reinterpret_cast<uintptr_t>(y2.data_ptr()) % 16 == 0,
-              "aiko.conv_glds_tail_out: y2 must be an NHWC [B, Ho, Wo, 80] (channel-slice) view");
+              "aiko.conv_glds_tail_out: y2 must be an NHWC [B, Ho, Wo, N] (channel-slice) view");
   const int64_t M = B * Ho * Wo;
   TORCH_CHECK(avail_elems(x) < INT_MAX && avail_elems(y2) < INT_MAX, "aiko.conv_glds_tail_out: 32-bit offsets");
   check_launch(aiko_conv_glds_tail(x.data_ptr(), w.data_ptr(), bias.data_ptr<float>(), (int)H, (int)W, (int)C, (int)Cc,
-                                   (int)R, (int)R, (int)stride, (int)pad, (int)Ho, (int)Wo, (int)M, (int)K, (int)act,
+                                   (int)R, (int)R, (int)stride, (int)pad, (int)Ho, (int)Wo, (int)M, (int)K, (int)N, (int)act,
                                    w2.data_ptr(), b2.data_ptr<float>(), y2.data_ptr(), (int)ldy2, (int)w2.size(1),
                                    zero.data_ptr(), cur_stream()),
                "conv_glds_tail");

@@ -46,8 +46,9 @@ __device__ __forceinline__ void wait_vm_barrier() {
 }
 
 // TAIL: a following 1x1 conv fused into the epilogue (YOLOv8 detect head: 3x3 80 -> 80 + SiLU,
-// then the 1x1 80 -> 80 class logits).  The activated 3x3 tile is packed to bf16 in LDS (K
-// columns 80..95 zeroed) and never written to HBM; the 1x1's weights ([N2][ldw2], K zero-padded
+// then the 1x1 80 -> 80 class logits; 3x3 64 -> 64, then the 1x1 64 -> 64 box distribution).
+// The activated 3x3 tile is packed to bf16 in LDS (K columns BN..K2 zeroed) and never written to
+// HBM; the 1x1's weights ([N2][ldw2], K zero-padded
 // to a multiple of 64 as every conv spec is) come straight from L2 as B fragments.
 struct GldsTail {
   const bf16_t* w2;
@@ -75,8 +76,9 @@ __global__ __launch_bounds__(256, (glds_occupancy<BM, BN>())) void conv_glds_ker
   constexpr int CPAD = 4;
   constexpr int EPI_BYTES = BM * (BN + CPAD) * 4;
   constexpr int RING_BYTES = NS * STAGE_ELEMS * 2;
-  static_assert(!TAIL || (WGN == 1 && BN == 80), "tail: 4 x 1 waves over the 80-channel tile");
-  constexpr int TP = 104;                      // tail: bf16 row pitch of the activated tile (96 + 8)
+  static_assert(!TAIL || BN == 64 || BN == 80, "tail: 64- or 80-channel tiles");
+  constexpr int K2 = (BN + 31) / 32 * 32;      // tail: the 1x1's K (zero-padded to the MFMA depth)
+  constexpr int TP = K2 + 8;                   // tail: bf16 row pitch of the activated tile
   constexpr int TAIL_BYTES = TAIL ? BM * TP * 2 : 0;
   constexpr int LDS_NEED = EPI_BYTES + TAIL_BYTES;
   constexpr int LDS_BYTES = LDS_NEED > RING_BYTES ? LDS_NEED : RING_BYTES;
@@ -295,20 +297,23 @@ __global__ __launch_bounds__(256, (glds_occupancy<BM, BN>())) void conv_glds_ker
   }
   if constexpr (TAIL) {
     bf16_t* Ts = reinterpret_cast<bf16_t*>(smem + EPI_BYTES);
-    // K columns 80..95 of every row are zero (two 16-B chunks per row); rows past M stay whatever
-    // the skipped chunks left — their outputs are never stored
-    for (int c = tid; c < BM * 2; c += 256)
-      *reinterpret_cast<u32x4*>(Ts + (c >> 1) * TP + 80 + (c & 1) * 8) = u32x4{0u, 0u, 0u, 0u};
+    // K columns BN..K2 of every row are zero (16-B chunks); rows past M stay whatever the
+    // skipped chunks left — their outputs are never stored
+    constexpr int ZC = (K2 - BN) / 8;
+    if constexpr (ZC > 0)
+      for (int c = tid; c < BM * ZC; c += 256)
+        *reinterpret_cast<u32x4*>(Ts + (c / ZC) * TP + BN + (c % ZC) * 8) = u32x4{0u, 0u, 0u, 0u};
     __syncthreads();                   // activated tile complete; every Cs read done
-    // 1x1: out[32 w + 16 i + 4 fq + e][16 j + fr], K = 96 (three 32-deep steps)
-    constexpr int MI2 = BM / 4 / 16, NI2 = 80 / 16;
+    // 1x1: out[(BM / 4) w + 16 i + 4 fq + e][16 j + fr] over K2 (32-deep steps), each wave a
+    // quarter of the rows and all BN columns
+    constexpr int MI2 = BM / 4 / 16, NI2 = BN / 16;
     f32x4 acc2[MI2][NI2];
 #pragma unroll
     for (int i = 0; i < MI2; ++i)
 #pragma unroll
       for (int j = 0; j < NI2; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ks = 0; ks < 3; ++ks) {
+    for (int ks = 0; ks < K2 / 32; ++ks) {
       bf16x8 af[MI2], bfr[NI2];
 #pragma unroll
       for (int i = 0; i < MI2; ++i)
@@ -389,11 +394,12 @@ extern "C" int aiko_conv_glds(const void* x, const void* w, const float* bias, c
   return (int)hipGetLastError();
 }
 
-// 3x3 (or any R x S) conv with an exact 80-channel tile and a fused trailing 1x1 80 -> 80 (+ bias,
-// no activation) in the epilogue: y2 [M][ldy2] = (act(conv(x) + bias)) . w2[:, :80]^T + b2.
-// Same geometry arguments as aiko_conv_glds (no residual, no second source); bm x bn = 128 x 80.
+// R x S conv with an exact N-channel tile (N = 80: 128 x 80, 4 x 1 waves; N = 64: 128 x 64, 2 x 2)
+// and a fused trailing 1x1 N -> N (+ bias, no activation) in the epilogue:
+// y2 [M][ldy2] = (act(conv(x) + bias)) . w2[:, :N]^T + b2.  Geometry as aiko_conv_glds (no residual,
+// no second source).
 extern "C" int aiko_conv_glds_tail(const void* x, const void* w, const float* bias, int H, int W, int C, int Cc,
-                                   int R, int S, int stride, int pad, int Ho, int Wo, int M, int K, int act,
+                                   int R, int S, int stride, int pad, int Ho, int Wo, int M, int K, int N, int act,
                                    const void* w2, const float* b2, void* y2, int ldy2, int ldw2, const void* zero,
                                    hipStream_t stream) {
   using namespace aiko;
@@ -404,13 +410,18 @@ extern "C" int aiko_conv_glds_tail(const void* x, const void* w, const float* bi
   p.res = nullptr;
   p.y = nullptr;
   p.H = H; p.W = W; p.C = C; p.Cc = Cc; p.R = R; p.S = S;
-  p.stride = stride; p.pad = pad; p.Ho = Ho; p.Wo = Wo; p.M = M; p.Cout = 80; p.K = K;
-  p.act = act; p.ldy = 80; p.ldr = 0;
+  p.stride = stride; p.pad = pad; p.Ho = Ho; p.Wo = Wo; p.M = M; p.Cout = N; p.K = K;
+  p.act = act; p.ldy = N; p.ldr = 0;
   p.x2 = nullptr;
   p.K1 = K; p.H2 = 1; p.W2 = 1; p.C2 = 8; p.stride2 = 1;
   conv_params_finalize(p);
   GldsTail tl{static_cast<const bf16_t*>(w2), b2, static_cast<bf16_t*>(y2), ldy2, ldw2};
   dim3 grid((M + 127) / 128), block(256);
-  conv_glds_kernel<128, 80, 4, 1, true><<<grid, block, 0, stream>>>(p, static_cast<const bf16_t*>(zero), tl);
+  if (N == 80)
+    conv_glds_kernel<128, 80, 4, 1, true><<<grid, block, 0, stream>>>(p, static_cast<const bf16_t*>(zero), tl);
+  else if (N == 64)
+    conv_glds_kernel<128, 64, 2, 2, true><<<grid, block, 0, stream>>>(p, static_cast<const bf16_t*>(zero), tl);
+  else
+    return -1;
   return (int)hipGetLastError();
 }

@@ -38,6 +38,8 @@ REG_MAX = 16
 # the detect head's class branch as one conv_glds launch with the 1x1 in its epilogue
 # (AIKO_HEAD_TAIL=0: the two separate convs)
 _HEAD_TAIL = __import__("os").environ.get("AIKO_HEAD_TAIL", "1") != "0"
+# ... and the box branch (3x3 64 -> 64 + 1x1 64 -> 64) the same way (AIKO_HEAD_TAIL_BOX=0: separate)
+_HEAD_TAIL_BOX = __import__("os").environ.get("AIKO_HEAD_TAIL_BOX", "1") != "0"
 
 
 def _make_div(x, d=8):
@@ -250,8 +252,11 @@ class YOLOv8(WeightsMixin):
         h2 = self._buf(f"h{i}.2", (B, H, W, cb + cc))
         out = self._buf(f"h{i}.out", (B, H, W, 4 * REG_MAX + self.nc_pad))
         C.conv2d(x, lvl.first, out=h1)
-        C.conv2d(h1[..., :cb], lvl.box[1], out=h2[..., :cb])
-        C.conv2d(h2[..., :cb], lvl.box[2], out=out[..., :4 * REG_MAX])
+        if _HEAD_TAIL and _HEAD_TAIL_BOX and C.conv_tail_ok(h1[..., :cb], lvl.box[1], lvl.box[2]):
+            C.conv2d_tail(h1[..., :cb], lvl.box[1], lvl.box[2], out[..., :4 * REG_MAX])
+        else:
+            C.conv2d(h1[..., :cb], lvl.box[1], out=h2[..., :cb])
+            C.conv2d(h2[..., :cb], lvl.box[2], out=out[..., :4 * REG_MAX])
         if _HEAD_TAIL and C.conv_tail_ok(h1[..., cb:], lvl.cls[1], lvl.cls[2]):
             # class branch: 3x3 80 -> 80 + SiLU and the 1x1 80 -> 80 logits in one launch
             C.conv2d_tail(h1[..., cb:], lvl.cls[1], lvl.cls[2], out[..., 4 * REG_MAX:])

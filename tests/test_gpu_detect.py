@@ -386,6 +386,17 @@ def test_conv_tail_matches_two_convs(native, monkeypatch, hw):
     monkeypatch.setattr(Y, "_HEAD_TAIL", False)
     o_u = m._run_head(0, lvl, p3).clone()
     torch.cuda.synchronize()
-    assert torch.equal(o_f[..., :64], o_u[..., :64])
-    a, b = o_f[..., 64:].float(), o_u[..., 64:].float()
-    assert torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item() > 0.9999
+    for sl in (slice(0, 64), slice(64, 144)):              # box (64) and class (80) branches
+        a, b = o_f[..., sl].float(), o_u[..., sl].float()
+        assert torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item() > 0.9999
+    # the box branch alone (64 -> 64 tail) against the fp32 reference
+    bo = torch.full((2, hw[0], hw[1], 144), 7.0, dtype=torch.bfloat16, device=DEV)
+    assert C.conv_tail_ok(h1[..., :64], lvl.box[1], lvl.box[2])
+    C.conv2d_tail(h1[..., :64], lvl.box[1], lvl.box[2], bo[..., :64])
+    torch.cuda.synchronize()
+    assert torch.equal(bo[..., 64:], torch.full_like(bo[..., 64:], 7.0))
+    xr = h1[..., :64].float().permute(0, 3, 1, 2)
+    tr = torch.nn.functional.silu(torch.nn.functional.conv2d(xr, lvl.box[1].ref_weight.to(DEV), lvl.box[1].ref_bias.to(DEV), padding=1))
+    yr = torch.nn.functional.conv2d(tr, lvl.box[2].ref_weight.to(DEV), lvl.box[2].ref_bias.to(DEV)).permute(0, 2, 3, 1)
+    a = bo[..., :64].float()
+    assert ((a - yr).norm() / yr.norm()).item() < 1e-2
