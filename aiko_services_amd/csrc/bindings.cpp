@@ -37,7 +37,7 @@ int aiko_conv_persist(const void* x, const void* w, const float* bias, const voi
                       int K1, int H2, int W2, int C2, int stride2, hipStream_t stream);
 int aiko_conv_glds_tail(const void* x, const void* w, const float* bias, int H, int W, int C, int Cc, int R, int S,
                         int stride, int pad, int Ho, int Wo, int M, int K, int N, int act, const void* w2, const float* b2,
-                        void* y2, int ldy2, int ldw2, const void* zero, hipStream_t stream);
+                        void* y2, int ldy2, int ldw2, int act2, const void* zero, hipStream_t stream);
 int aiko_conv_glds(const void* x, const void* w, const float* bias, const void* res, void* y,
                    int H, int W, int C, int Cc, int R, int S, int stride, int pad, int Ho,
                    int Wo, int M, int Cout, int K, int act, int ldy, int ldr, int bm, int bn,
@@ -595,11 +595,12 @@ void c2f_bneck_out(const at::Tensor& x, const at::Tensor& wa, const at::Tensor& 
 }
 
 // R x R conv (Cout N = 64 or 80, exact-N tile, LDS-DMA kernel) with a fused trailing 1x1 N -> N + bias
-// (conv_glds.hip, TAIL): y2 = (act(conv(x) + bias)) . w2[:, :N]^T + b2.  x, y2: NHWC channel-slice
+// (conv_glds.hip, TAIL): y2 = act2((act(conv(x) + bias)) . w2[:, :N]^T + b2).  x, y2: NHWC channel-slice
 // views; w [N, K] and w2 [N, >= ceil32(N)] with zero K padding (conv spec layout).
 void conv_glds_tail_out(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, const at::Tensor& w2,
                         const at::Tensor& b2, at::Tensor& y2, int64_t R, int64_t stride, int64_t pad, int64_t act,
-                        const at::Tensor& zero) {
+                        int64_t act2, const at::Tensor& zero) {
+  TORCH_CHECK(act2 == 0 || act2 == 2, "aiko.conv_glds_tail_out: act2 = 0 (none) or 2 (SiLU)");
   for (const at::Tensor* t : {&x, &w, &bias, &w2, &b2, (const at::Tensor*)&y2, &zero}) check_cuda(*t, "conv tail operand");
   for (const at::Tensor* t : {&x, &w, &w2, (const at::Tensor*)&y2})
     TORCH_CHECK(t->scalar_type() == at::kBFloat16, "aiko.conv_glds_tail_out: bf16 activations / weights");
@@ -630,7 +631,7 @@ void conv_glds_tail_out(const at::Tensor& x, const at::Tensor& w, const at::Tens
   check_launch(aiko_conv_glds_tail(x.data_ptr(), w.data_ptr(), bias.data_ptr<float>(), (int)H, (int)W, (int)C, (int)Cc,
                                    (int)R, (int)R, (int)stride, (int)pad, (int)Ho, (int)Wo, (int)M, (int)K, (int)N, (int)act,
                                    w2.data_ptr(), b2.data_ptr<float>(), y2.data_ptr(), (int)ldy2, (int)w2.size(1),
-                                   zero.data_ptr(), cur_stream()),
+                                   (int)act2, zero.data_ptr(), cur_stream()),
                "conv_glds_tail");
 }
 
@@ -1524,7 +1525,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("c2f_fused_out(Tensor x, Tensor w1, Tensor b1, Tensor wa, Tensor ba, Tensor wb, Tensor bb, Tensor w2, Tensor b2, Tensor(a!) y, int ci, bool shortcut, int rb) -> ()");
   m.def("c2f_fused_s2_out(Tensor a0, Tensor w0, Tensor b0, Tensor w1, Tensor b1, Tensor wa, Tensor ba, Tensor wb, Tensor bb, Tensor w2, Tensor b2, Tensor(a!) y, bool shortcut, int rb) -> ()");
   m.def("c2f_bneck_out(Tensor x, Tensor wa, Tensor ba, Tensor wb, Tensor bb, Tensor(a!) y, bool shortcut, int rb) -> ()");
-  m.def("conv_glds_tail_out(Tensor x, Tensor w, Tensor bias, Tensor w2, Tensor b2, Tensor(a!) y2, int R, int stride, int pad, int act, Tensor zero) -> ()");
+  m.def("conv_glds_tail_out(Tensor x, Tensor w, Tensor bias, Tensor w2, Tensor b2, Tensor(a!) y2, int R, int stride, int pad, int act, int act2, Tensor zero) -> ()");
   m.def("linear_splitk_out(Tensor x, Tensor w, Tensor? bias, Tensor(a!) part, Tensor(b!) y, int K, int S) -> ()");
   m.def("attn_fwd_out(Tensor q, Tensor k, Tensor v, Tensor(a!) o, int B, int H, int T, int Tpad, float scale, Tensor(b!)? work=None, Tensor(c!)? oq=None, Tensor(d!)? osc=None) -> ()");
   m.def("logmel_out(Tensor audio, Tensor mel, Tensor mel_range, int n_fft, int hop, int F, Tensor(a!) work, Tensor(b!) gmax, Tensor(c!) dst, int rows, int pad) -> ()");

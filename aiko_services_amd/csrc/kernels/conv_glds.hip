@@ -54,7 +54,7 @@ struct GldsTail {
   const bf16_t* w2;
   const float* b2;
   bf16_t* y2;
-  int ldy2, ldw2;
+  int ldy2, ldw2, act2;   // act2: 0 none, 2 SiLU on the 1x1's output
 };
 
 // WGM x WGN waves (2 x 2; exact-N tiles such as BN = 80: 4 x 1, each wave all BN columns)
@@ -343,11 +343,15 @@ __global__ __launch_bounds__(256, (glds_occupancy<BM, BN>())) void conv_glds_ker
       const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + cc * 8 + 4);
       const f32x4 c0 = *reinterpret_cast<const f32x4*>(tl.b2 + cc * 8);
       const f32x4 c1 = *reinterpret_cast<const f32x4*>(tl.b2 + cc * 8 + 4);
+      float v[8] = {v0[0] + c0[0], v0[1] + c0[1], v0[2] + c0[2], v0[3] + c0[3],
+                    v1[0] + c1[0], v1[1] + c1[1], v1[2] + c1[2], v1[3] + c1[3]};
+      if (tl.act2 == 2) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = silu(v[e]);
+      }
       u32x4 o;
-      o[0] = pack2(v0[0] + c0[0], v0[1] + c0[1]);
-      o[1] = pack2(v0[2] + c0[2], v0[3] + c0[3]);
-      o[2] = pack2(v1[0] + c1[0], v1[1] + c1[1]);
-      o[3] = pack2(v1[2] + c1[2], v1[3] + c1[3]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = pack2(v[2 * e], v[2 * e + 1]);
       *reinterpret_cast<u32x4*>(tl.y2 + (size_t)m * tl.ldy2 + cc * 8) = o;
     }
   }
@@ -396,11 +400,11 @@ extern "C" int aiko_conv_glds(const void* x, const void* w, const float* bias, c
 
 // R x S conv with an exact N-channel tile (N = 80: 128 x 80, 4 x 1 waves; N = 64: 128 x 64, 2 x 2)
 // and a fused trailing 1x1 N -> N (+ bias, no activation) in the epilogue:
-// y2 [M][ldy2] = (act(conv(x) + bias)) . w2[:, :N]^T + b2.  Geometry as aiko_conv_glds (no residual,
+// y2 [M][ldy2] = act2((act(conv(x) + bias)) . w2[:, :N]^T + b2).  Geometry as aiko_conv_glds (no residual,
 // no second source).
 extern "C" int aiko_conv_glds_tail(const void* x, const void* w, const float* bias, int H, int W, int C, int Cc,
                                    int R, int S, int stride, int pad, int Ho, int Wo, int M, int K, int N, int act,
-                                   const void* w2, const float* b2, void* y2, int ldy2, int ldw2, const void* zero,
+                                   const void* w2, const float* b2, void* y2, int ldy2, int ldw2, int act2, const void* zero,
                                    hipStream_t stream) {
   using namespace aiko;
   ConvParams p;
@@ -415,7 +419,7 @@ extern "C" int aiko_conv_glds_tail(const void* x, const void* w, const float* bi
   p.x2 = nullptr;
   p.K1 = K; p.H2 = 1; p.W2 = 1; p.C2 = 8; p.stride2 = 1;
   conv_params_finalize(p);
-  GldsTail tl{static_cast<const bf16_t*>(w2), b2, static_cast<bf16_t*>(y2), ldy2, ldw2};
+  GldsTail tl{static_cast<const bf16_t*>(w2), b2, static_cast<bf16_t*>(y2), ldy2, ldw2, act2};
   dim3 grid((M + 127) / 128), block(256);
   if (N == 80)
     conv_glds_kernel<128, 80, 4, 1, true><<<grid, block, 0, stream>>>(p, static_cast<const bf16_t*>(zero), tl);

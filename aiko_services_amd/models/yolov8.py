@@ -205,16 +205,19 @@ class YOLOv8(WeightsMixin):
         import os
         return int(os.environ.get("AIKO_C2F_RB" if H == 160 else "AIKO_C2F_RB80", "40" if H == 160 else "20"))
 
-    def _run_c2f(self, name, blk: C2f, x, out):
+    def _run_c2f(self, name, blk: C2f, x, out, cat=None):
+        """``cat``: the block's split/concat buffer with cv1's output already in channels
+        [0, 2c) (``x`` then only gives the shape)."""
         B, H, W, _ = x.shape
         c, n = blk.c, len(blk.m)
-        if self._c2f_fused_ok(blk, x, out):
+        if cat is None and self._c2f_fused_ok(blk, x, out):
             a, b = blk.m[0]
             torch.ops.aiko.c2f_fused_out(x, blk.cv1.weight, blk.cv1.bias, a.weight, a.bias, b.weight, b.bias,
                                          blk.cv2.weight, blk.cv2.bias, out, blk.cv1.Cc, blk.shortcut, self._c2f_rb(H))
             return out
-        cat = self._buf(f"{name}.cat", (B, H, W, (2 + n) * c))
-        C.conv2d(x, blk.cv1, out=cat[..., :2 * c])
+        if cat is None:
+            cat = self._buf(f"{name}.cat", (B, H, W, (2 + n) * c))
+            C.conv2d(x, blk.cv1, out=cat[..., :2 * c])
         tmp = self._buf(f"{name}.tmp", (B, H, W, c))
         import os
         fuse_b = (cat.is_cuda and os.environ.get("AIKO_C2F_FUSED", "1") != "0" and W == 80 and c == 32
@@ -320,9 +323,17 @@ class YOLOv8(WeightsMixin):
         else:
             a1 = C.conv2d(a0, self.l1, out=self._buf("a1", (B, H2, W2, c2)))
             a2 = self._run_c2f("l2", self.l2, a1, a2)
-        a3 = C.conv2d(a2, self.l3, out=self._buf("a3", (B, H3, W3, c3)))
         cat14 = self._buf("cat14", (B, H3, W3, c4 + c3))       # [up(l12) | l4]
-        a4 = self._run_c2f("l4", self.l4, a3, cat14[..., c4:])
+        a3 = self._buf("a3", (B, H3, W3, c3))
+        if (_HEAD_TAIL and not self._c2f_fused_ok(self.l4, a3, cat14[..., c4:])
+                and C.conv_tail_ok(a2, self.l3, self.l4.cv1)):
+            # l3 (3x3 / 2) with l4's cv1 (1x1 + SiLU) in its epilogue: a3 is never written
+            cat4 = self._buf("l4.cat", (B, H3, W3, (2 + len(self.l4.m)) * self.l4.c))
+            C.conv2d_tail(a2, self.l3, self.l4.cv1, cat4[..., :2 * self.l4.c])
+            a4 = self._run_c2f("l4", self.l4, a3, cat14[..., c4:], cat=cat4)
+        else:
+            C.conv2d(a2, self.l3, out=a3)
+            a4 = self._run_c2f("l4", self.l4, a3, cat14[..., c4:])
         a5 = C.conv2d(a4, self.l5, out=self._buf("a5", (B, H4, W4, c4)))
         cat11 = self._buf("cat11", (B, H4, W4, c5 + c4))       # [up(l9) | l6]
         a6 = self._run_c2f("l6", self.l6, a5, cat11[..., c5:])

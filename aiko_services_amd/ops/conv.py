@@ -756,16 +756,16 @@ def _chain_stage2() -> bool:
 
 
 def conv_tail_ok(x: torch.Tensor, spec: ConvSpec, spec2: ConvSpec) -> bool:
-    """Can ``spec`` (a 3x3 conv to N = 64 or 80 channels) and the following 1x1 ``spec2`` (N -> N,
-    bias, no activation) run as ONE ``conv_glds`` launch with the 1x1 in its epilogue (the YOLOv8
-    detect head's box and class branches)?"""
+    """Can ``spec`` (a 3x3 conv to N = 64 or 80 channels, any stride) and the following 1x1
+    ``spec2`` (N -> N, bias, no activation or SiLU) run as ONE ``conv_glds`` launch with the 1x1
+    in its epilogue (the YOLOv8 detect head's box and class branches; l3 -> l4's C2f cv1)?"""
     n = spec.cout
     return (spec.kind == "conv" and spec.R == spec.S == 3 and spec.K1 is None and n in (64, 80)
             and spec.bias is not None and x.dim() == 4 and x.shape[3] == spec.Cc and spec.Cc % 8 == 0
             and x.stride(3) == 1 and x.stride(2) % 8 == 0
             and spec2.kind == "conv" and spec2.R == spec2.S == 1 and spec2.stride == 1 and spec2.pad == 0
             and spec2.K1 is None and spec2.Cc == n and spec2.cout == n and spec2.bias is not None
-            and spec2.act == ACT_NONE and spec2.weight.shape[1] >= (n + 31) // 32 * 32)
+            and spec2.act in (ACT_NONE, ACT_SILU) and spec2.weight.shape[1] >= (n + 31) // 32 * 32)
 
 
 def conv2d_tail(x: torch.Tensor, spec: ConvSpec, spec2: ConvSpec, out: torch.Tensor) -> torch.Tensor:
@@ -775,7 +775,7 @@ def conv2d_tail(x: torch.Tensor, spec: ConvSpec, spec2: ConvSpec, out: torch.Ten
     if not conv_tail_ok(x, spec, spec2):
         raise ValueError("conv2d_tail: shapes not eligible (see conv_tail_ok)")
     torch.ops.aiko.conv_glds_tail_out(x, spec.weight, spec.bias, spec2.weight, spec2.bias, out, spec.R, spec.stride,
-                                      spec.pad, spec.act, zero_page(x.device))
+                                      spec.pad, spec.act, spec2.act, zero_page(x.device))
     return out
 
 

@@ -400,3 +400,21 @@ def test_conv_tail_matches_two_convs(native, monkeypatch, hw):
     yr = torch.nn.functional.conv2d(tr, lvl.box[2].ref_weight.to(DEV), lvl.box[2].ref_bias.to(DEV)).permute(0, 2, 3, 1)
     a = bo[..., :64].float()
     assert ((a - yr).norm() / yr.norm()).item() < 1e-2
+
+
+def test_yolo_tails_match_unfused(native, monkeypatch):
+    """The whole YOLOv8-n head_outputs with the fused 3x3 + 1x1 launches (l3 -> l4.cv1 with SiLU,
+    detect-head box and class branches) against the same network with every conv separate."""
+    from aiko_services_amd.models import yolov8 as Y
+    m = Y.YOLOv8("n", device=DEV)
+    g = torch.Generator().manual_seed(11)
+    a0 = (torch.randn(2, 320, 320, 16, generator=g) * 2).to(DEV, torch.bfloat16)
+    monkeypatch.setattr(Y, "_HEAD_TAIL", True)
+    fused = [o.clone() for o in m.head_outputs(None, a0=a0)]
+    monkeypatch.setattr(Y, "_HEAD_TAIL", False)
+    plain = [o.clone() for o in m.head_outputs(None, a0=a0)]
+    torch.cuda.synchronize()
+    for a, b in zip(fused, plain):
+        a, b = a.float(), b.float()
+        cos = torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()
+        assert cos > 0.999, cos
