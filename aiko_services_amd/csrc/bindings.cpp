@@ -594,7 +594,7 @@ void c2f_bneck_out(const at::Tensor& x, const at::Tensor& wa, const at::Tensor& 
                "c2f_bneck");
 }
 
-// R x R conv (Cout N = 64 or 80, exact-N tile, LDS-DMA kernel) with a fused trailing 1x1 N -> N + bias
+// R x R conv (Cout N = 64, 80 or 128, exact-N tile, LDS-DMA kernel) with a fused trailing 1x1 N -> N + bias
 // (conv_glds.hip, TAIL): y2 = act2((act(conv(x) + bias)) . w2[:, :N]^T + b2).  x, y2: NHWC channel-slice
 // views; w [N, K] and w2 [N, >= ceil32(N)] with zero K padding (conv spec layout).
 void conv_glds_tail_out(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, const at::Tensor& w2,
@@ -605,7 +605,7 @@ void conv_glds_tail_out(const at::Tensor& x, const at::Tensor& w, const at::Tens
   for (const at::Tensor* t : {&x, &w, &w2, (const at::Tensor*)&y2})
     TORCH_CHECK(t->scalar_type() == at::kBFloat16, "aiko.conv_glds_tail_out: bf16 activations / weights");
   const int64_t N = w.size(0);
-  TORCH_CHECK(N == 64 || N == 80, "aiko.conv_glds_tail_out: N = 64 or 80");
+  TORCH_CHECK(N == 64 || N == 80 || N == 128, "aiko.conv_glds_tail_out: N = 64, 80 or 128");
   TORCH_CHECK(bias.scalar_type() == at::kFloat && b2.scalar_type() == at::kFloat && bias.numel() == N &&
                   b2.numel() == N && bias.is_contiguous() && b2.is_contiguous(),
               "aiko.conv_glds_tail_out: fp32 biases [N]");

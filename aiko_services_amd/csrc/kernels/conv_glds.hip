@@ -76,7 +76,7 @@ __global__ __launch_bounds__(256, (glds_occupancy<BM, BN>())) void conv_glds_ker
   constexpr int CPAD = 4;
   constexpr int EPI_BYTES = BM * (BN + CPAD) * 4;
   constexpr int RING_BYTES = NS * STAGE_ELEMS * 2;
-  static_assert(!TAIL || BN == 64 || BN == 80, "tail: 64- or 80-channel tiles");
+  static_assert(!TAIL || BN == 64 || BN == 80 || BN == 128, "tail: 64-, 80- or 128-channel tiles");
   constexpr int K2 = (BN + 31) / 32 * 32;      // tail: the 1x1's K (zero-padded to the MFMA depth)
   constexpr int TP = K2 + 8;                   // tail: bf16 row pitch of the activated tile
   constexpr int TAIL_BYTES = TAIL ? BM * TP * 2 : 0;
@@ -398,7 +398,8 @@ extern "C" int aiko_conv_glds(const void* x, const void* w, const float* bias, c
   return (int)hipGetLastError();
 }
 
-// R x S conv with an exact N-channel tile (N = 80: 128 x 80, 4 x 1 waves; N = 64: 128 x 64, 2 x 2)
+// R x S conv with an exact N-channel tile (N = 80: 128 x 80, 4 x 1 waves; N = 64: 128 x 64, 2 x 2;
+// N = 128: 64 x 128, 2 x 2)
 // and a fused trailing 1x1 N -> N (+ bias, no activation) in the epilogue:
 // y2 [M][ldy2] = act2((act(conv(x) + bias)) . w2[:, :N]^T + b2).  Geometry as aiko_conv_glds (no residual,
 // no second source).
@@ -425,6 +426,8 @@ extern "C" int aiko_conv_glds_tail(const void* x, const void* w, const float* bi
     conv_glds_kernel<128, 80, 4, 1, true><<<grid, block, 0, stream>>>(p, static_cast<const bf16_t*>(zero), tl);
   else if (N == 64)
     conv_glds_kernel<128, 64, 2, 2, true><<<grid, block, 0, stream>>>(p, static_cast<const bf16_t*>(zero), tl);
+  else if (N == 128)   // 64 x 128 tiles (the 128-row form would hold 102 KB of LDS: one workgroup per CU)
+    conv_glds_kernel<64, 128, 2, 2, true><<<dim3((M + 63) / 64), block, 0, stream>>>(p, static_cast<const bf16_t*>(zero), tl);
   else
     return -1;
   return (int)hipGetLastError();

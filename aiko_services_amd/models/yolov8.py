@@ -334,9 +334,17 @@ class YOLOv8(WeightsMixin):
         else:
             C.conv2d(a2, self.l3, out=a3)
             a4 = self._run_c2f("l4", self.l4, a3, cat14[..., c4:])
-        a5 = C.conv2d(a4, self.l5, out=self._buf("a5", (B, H4, W4, c4)))
         cat11 = self._buf("cat11", (B, H4, W4, c5 + c4))       # [up(l9) | l6]
-        a6 = self._run_c2f("l6", self.l6, a5, cat11[..., c5:])
+        a5 = self._buf("a5", (B, H4, W4, c4))
+        if (_HEAD_TAIL and not self._c2f_fused_ok(self.l6, a5, cat11[..., c5:])
+                and C.conv_tail_ok(a4, self.l5, self.l6.cv1)):
+            # l5 (3x3 / 2) with l6's cv1 in its epilogue: a5 is never written
+            cat6 = self._buf("l6.cat", (B, H4, W4, (2 + len(self.l6.m)) * self.l6.c))
+            C.conv2d_tail(a4, self.l5, self.l6.cv1, cat6[..., :2 * self.l6.c])
+            a6 = self._run_c2f("l6", self.l6, a5, cat11[..., c5:], cat=cat6)
+        else:
+            C.conv2d(a4, self.l5, out=a5)
+            a6 = self._run_c2f("l6", self.l6, a5, cat11[..., c5:])
         a7 = C.conv2d(a6, self.l7, out=self._buf("a7", (B, H5, W5, c5)))
         a8 = self._run_c2f("l8", self.l8, a7, self._buf("a8", (B, H5, W5, c5)))
         cat20 = self._buf("cat20", (B, H5, W5, c4 + c5))       # [l19 | l9]

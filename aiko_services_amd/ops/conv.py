@@ -756,11 +756,12 @@ def _chain_stage2() -> bool:
 
 
 def conv_tail_ok(x: torch.Tensor, spec: ConvSpec, spec2: ConvSpec) -> bool:
-    """Can ``spec`` (a 3x3 conv to N = 64 or 80 channels, any stride) and the following 1x1
+    """Can ``spec`` (a 3x3 conv to N = 64, 80 or 128 channels, any stride) and the following 1x1
     ``spec2`` (N -> N, bias, no activation or SiLU) run as ONE ``conv_glds`` launch with the 1x1
-    in its epilogue (the YOLOv8 detect head's box and class branches; l3 -> l4's C2f cv1)?"""
+    in its epilogue (the YOLOv8 detect head's box and class branches; l3 -> l4's and l5 -> l6's
+    C2f cv1)?"""
     n = spec.cout
-    return (spec.kind == "conv" and spec.R == spec.S == 3 and spec.K1 is None and n in (64, 80)
+    return (spec.kind == "conv" and spec.R == spec.S == 3 and spec.K1 is None and n in (64, 80, 128)
             and spec.bias is not None and x.dim() == 4 and x.shape[3] == spec.Cc and spec.Cc % 8 == 0
             and x.stride(3) == 1 and x.stride(2) % 8 == 0
             and spec2.kind == "conv" and spec2.R == spec2.S == 1 and spec2.stride == 1 and spec2.pad == 0
