@@ -7,12 +7,13 @@ import sqlite3
 import sys
 
 
-def summarize(db, top=40, by_grid=False):
+def summarize(db, top=40, by_grid=False, last_frac=1.0):
     con = sqlite3.connect(db)
     cur = con.cursor()
     cols = [r[1] for r in cur.execute("pragma table_info(kernels)")]
     name_col = "kernel_name" if "kernel_name" in cols else ("name" if "name" in cols else None)
-    rows = cur.execute(f"select {name_col}, start, end, grid_x from kernels").fetchall()
+    rows = cur.execute(f"select {name_col}, start, end, grid_x from kernels order by start").fetchall()
+    rows = rows[int(len(rows) * (1.0 - last_frac)):]    # steady state: skip setup / tuning dispatches
     agg = {}
     for name, s, e, gx in rows:
         d = (e - s) / 1e3  # ns -> us
@@ -55,8 +56,9 @@ if __name__ == "__main__":
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--by-grid", action="store_true", help="split kernels by grid size (layer shapes)")
     ap.add_argument("--sequence", type=int, default=0, help="list the last N dispatches in order instead")
+    ap.add_argument("--last-frac", type=float, default=1.0, help="summarise only the last fraction of dispatches")
     a = ap.parse_args()
-    s = sequence(a.db, a.sequence) if a.sequence else summarize(a.db, a.top, a.by_grid)
+    s = sequence(a.db, a.sequence) if a.sequence else summarize(a.db, a.top, a.by_grid, a.last_frac)
     print(s)
     if a.out:
         with open(a.out, "w") as f:
