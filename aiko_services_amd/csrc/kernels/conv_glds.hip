@@ -158,6 +158,25 @@ __global__ __launch_bounds__(256, (glds_occupancy<BM, BN>())) void conv_glds_ker
     }
   }
 
+  // tail: the 1x1's weight fragments (A operand: 16 output channels x 32 K) and bias, loaded
+  // before the first DMA so they land under the K loop (the first counted wait retires them)
+  constexpr int NI2 = BN / 16, KS2 = K2 / 32;
+  constexpr bool W2_PRE = TAIL && KS2 * NI2 <= 16;
+  bf16x8 w2f[W2_PRE ? KS2 : 1][W2_PRE ? NI2 : 1];
+  f32x4 b2v[TAIL ? NI2 : 1];
+  if constexpr (TAIL) {
+    const int fr0 = lane & 15, fq0 = lane >> 4;
+    if constexpr (W2_PRE) {
+#pragma unroll
+      for (int ks = 0; ks < KS2; ++ks)
+#pragma unroll
+        for (int j = 0; j < NI2; ++j)
+          w2f[ks][j] = *reinterpret_cast<const bf16x8*>(tl.w2 + (size_t)(16 * j + fr0) * tl.ldw2 + 32 * ks + 8 * fq0);
+    }
+#pragma unroll
+    for (int j = 0; j < NI2; ++j) b2v[j] = *reinterpret_cast<const f32x4*>(tl.b2 + 16 * j + 4 * fq0);
+  }
+
   const bf16_t* zp = zero;
   auto issue = [&](int kb, int slot) {
     bf16_t* As = ring + slot * STAGE_ELEMS;
@@ -304,55 +323,48 @@ __global__ __launch_bounds__(256, (glds_occupancy<BM, BN>())) void conv_glds_ker
       for (int c = tid; c < BM * ZC; c += 256)
         *reinterpret_cast<u32x4*>(Ts + (c / ZC) * TP + BN + (c % ZC) * 8) = u32x4{0u, 0u, 0u, 0u};
     __syncthreads();                   // activated tile complete; every Cs read done
-    // 1x1: out[(BM / 4) w + 16 i + 4 fq + e][16 j + fr] over K2 (32-deep steps), each wave a
-    // quarter of the rows and all BN columns
-    constexpr int MI2 = BM / 4 / 16, NI2 = BN / 16;
+    // 1x1, transposed (weights on the A side): out^T[16 j + 4 fq + e][(BM / 4) w + 16 i + fr]
+    // over K2 (32-deep steps), each wave a quarter of the pixels and all BN channels — every lane
+    // ends with 4 consecutive channels of one pixel: bias, activation and an 8-byte store
+    // straight from the accumulators
+    constexpr int MI2 = BM / 4 / 16;
     f32x4 acc2[MI2][NI2];
 #pragma unroll
     for (int i = 0; i < MI2; ++i)
 #pragma unroll
-      for (int j = 0; j < NI2; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NI2; ++j) acc2[i][j] = b2v[j];
 #pragma unroll
-    for (int ks = 0; ks < K2 / 32; ++ks) {
-      bf16x8 af[MI2], bfr[NI2];
+    for (int ks = 0; ks < KS2; ++ks) {
+      bf16x8 tf[MI2], wf[NI2];
 #pragma unroll
       for (int i = 0; i < MI2; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(Ts + (wave * (BM / 4) + 16 * i + fr) * TP + 32 * ks + 8 * fq);
+        tf[i] = *reinterpret_cast<const bf16x8*>(Ts + (wave * (BM / 4) + 16 * i + fr) * TP + 32 * ks + 8 * fq);
 #pragma unroll
-      for (int j = 0; j < NI2; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(tl.w2 + (size_t)(16 * j + fr) * tl.ldw2 + 32 * ks + 8 * fq);
+      for (int j = 0; j < NI2; ++j) {
+        if constexpr (W2_PRE)
+          wf[j] = w2f[ks][j];
+        else
+          wf[j] = *reinterpret_cast<const bf16x8*>(tl.w2 + (size_t)(16 * j + fr) * tl.ldw2 + 32 * ks + 8 * fq);
+      }
 #pragma unroll
       for (int i = 0; i < MI2; ++i)
 #pragma unroll
         for (int j = 0; j < NI2; ++j)
-          acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc2[i][j], 0, 0, 0);
+          acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], tf[i], acc2[i][j], 0, 0, 0);
     }
 #pragma unroll
-    for (int i = 0; i < MI2; ++i)
-#pragma unroll
-      for (int j = 0; j < NI2; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) Cs[(wave * (BM / 4) + i * 16 + fq * 4 + e) * LDC + j * 16 + fr] = acc2[i][j][e];
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int row = e_row_of(i), cc = e_cc_of(i);
-      const int m = m0 + row;
+    for (int i = 0; i < MI2; ++i) {
+      const int m = m0 + wave * (BM / 4) + 16 * i + fr;
       if (m >= p.M) continue;
-      const f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + cc * 8);
-      const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + row * LDC + cc * 8 + 4);
-      const f32x4 c0 = *reinterpret_cast<const f32x4*>(tl.b2 + cc * 8);
-      const f32x4 c1 = *reinterpret_cast<const f32x4*>(tl.b2 + cc * 8 + 4);
-      float v[8] = {v0[0] + c0[0], v0[1] + c0[1], v0[2] + c0[2], v0[3] + c0[3],
-                    v1[0] + c1[0], v1[1] + c1[1], v1[2] + c1[2], v1[3] + c1[3]};
-      if (tl.act2 == 2) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = silu(v[e]);
+      for (int j = 0; j < NI2; ++j) {
+        f32x4 v = acc2[i][j];
+        if (tl.act2 == 2) v = f32x4{silu(v[0]), silu(v[1]), silu(v[2]), silu(v[3])};
+        uint2 o;
+        o.x = pack2(v[0], v[1]);
+        o.y = pack2(v[2], v[3]);
+        *reinterpret_cast<uint2*>(tl.y2 + (size_t)m * tl.ldy2 + 16 * j + 4 * fq) = o;
       }
-      u32x4 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = pack2(v[2 * e], v[2 * e + 1]);
-      *reinterpret_cast<u32x4*>(tl.y2 + (size_t)m * tl.ldy2 + cc * 8) = o;
     }
   }
 }
