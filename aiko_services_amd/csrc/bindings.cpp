@@ -84,7 +84,7 @@ int aiko_gemm_fp8_ln(const void* a, const void* b, const float* sb, const float*
                      float ln_eps, int ln, hipStream_t stream);
 int aiko_c2f_fused(const void* x, int ldx, const void* w1, const float* b1, int k1, const void* wa, const float* ba,
                    int ka, const void* wb, const float* bb, int kb, const void* w2, const float* b2, int k2, void* y, int ldy,
-                   int B, int H, int W, int CI, int C, int CO, int shortcut, int rb, hipStream_t stream);
+                   int B, int H, int W, int CI, int C, int CO, int shortcut, int rb, const void* xu, int ldxu, int cu, hipStream_t stream);
 int aiko_c2f_bneck(const void* x, int ldx, const void* wa, const float* ba, int ka, const void* wb, const float* bb,
                    int kb, void* y, int ldy, int B, int H, int W, int C, int shortcut, int rb, hipStream_t stream);
 int aiko_c2f_fused_s2(const void* a0, int lda0, const void* w0, const float* b0, int k0, const void* w1, const float* b1,
@@ -503,7 +503,8 @@ void conv_chain_out(const at::Tensor& A, const at::Tensor& W1, const at::Tensor&
 // [Cout, K padded] bf16 + fp32 biases, SiLU everywhere).  Shapes without an instantiation fail.
 void c2f_fused_out(const at::Tensor& x, const at::Tensor& w1, const at::Tensor& b1, const at::Tensor& wa,
                    const at::Tensor& ba, const at::Tensor& wb, const at::Tensor& bb, const at::Tensor& w2,
-                   const at::Tensor& b2, at::Tensor& y, int64_t ci, bool shortcut, int64_t rb) {
+                   const at::Tensor& b2, at::Tensor& y, int64_t ci, bool shortcut, int64_t rb,
+                   const c10::optional<at::Tensor>& xu_opt) {
   for (const at::Tensor* t : {&x, &w1, &b1, &wa, &ba, &wb, &bb, &w2, &b2, (const at::Tensor*)&y}) check_cuda(*t, "c2f operand");
   for (const at::Tensor* t : {&x, &w1, &wa, &wb, &w2, (const at::Tensor*)&y})
     TORCH_CHECK(t->scalar_type() == at::kBFloat16, "aiko.c2f_fused_out: bf16 activations / weights");
@@ -526,10 +527,27 @@ void c2f_fused_out(const at::Tensor& x, const at::Tensor& w1, const at::Tensor& 
                   y.stride(0) == H * W * ldy && ldx % 8 == 0 && ldy % 4 == 0 && x.size(3) >= CI && y.size(3) >= CO &&
                   reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(y.data_ptr()) % 8 == 0,
               "aiko.c2f_fused_out: NHWC views with 16-B aligned pixels");
+  // optional in-place 2x upsample source for input channels [0, cu): xu [B, H/2, W/2, cu] (NHWC view)
+  const void* xup = nullptr;
+  int64_t ldxu = 0, cu = 0;
+  if (xu_opt.has_value() && xu_opt->defined()) {
+    const at::Tensor& xu = *xu_opt;
+    check_cuda(xu, "c2f upsample source");
+    TORCH_CHECK(xu.scalar_type() == at::kBFloat16 && xu.dim() == 4 && xu.size(0) == B && 2 * xu.size(1) == H &&
+                    2 * xu.size(2) == W && xu.stride(3) == 1 && xu.stride(1) == xu.size(2) * xu.stride(2) &&
+                    xu.stride(0) == xu.size(1) * xu.stride(1) && xu.stride(2) % 8 == 0 &&
+                    reinterpret_cast<uintptr_t>(xu.data_ptr()) % 16 == 0,
+                "aiko.c2f_fused_out: xu must be an NHWC [B, H/2, W/2, cu] view with 16-B aligned pixels");
+    cu = xu.size(3);
+    TORCH_CHECK(cu % 32 == 0 && cu < CI, "aiko.c2f_fused_out: xu channels a multiple of 32 below ci");
+    xup = xu.data_ptr();
+    ldxu = xu.stride(2);
+  }
   check_launch(aiko_c2f_fused(x.data_ptr(), (int)ldx, w1.data_ptr(), b1.data_ptr<float>(), (int)w1.size(1), wa.data_ptr(),
                               ba.data_ptr<float>(), (int)wa.size(1), wb.data_ptr(), bb.data_ptr<float>(), (int)wb.size(1),
                               w2.data_ptr(), b2.data_ptr<float>(), (int)w2.size(1), y.data_ptr(), (int)ldy, (int)B, (int)H,
-                              (int)W, (int)CI, (int)C, (int)CO, shortcut ? 1 : 0, (int)rb, cur_stream()),
+                              (int)W, (int)CI, (int)C, (int)CO, shortcut ? 1 : 0, (int)rb, xup, (int)ldxu, (int)cu,
+                              cur_stream()),
                "c2f_fused");
 }
 
@@ -1522,7 +1540,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("rownorm_quant_out(Tensor x, Tensor? gamma, Tensor? beta, float eps, Tensor(a!)? yb, Tensor(b!)? q, Tensor(c!)? qs) -> ()");
   m.def("gemm_fp8_ln_out(Tensor a, Tensor amx, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!)? y, Tensor(b!)? yq, Tensor(c!)? ysc, Tensor(d!) st, Tensor? cs, int ln, int act, int ln_d, float eps, Tensor zero) -> ()");
   m.def("rowstats_mx_out(Tensor x, Tensor(a!) q, Tensor(b!) qsc, Tensor(c!) st) -> ()");
-  m.def("c2f_fused_out(Tensor x, Tensor w1, Tensor b1, Tensor wa, Tensor ba, Tensor wb, Tensor bb, Tensor w2, Tensor b2, Tensor(a!) y, int ci, bool shortcut, int rb) -> ()");
+  m.def("c2f_fused_out(Tensor x, Tensor w1, Tensor b1, Tensor wa, Tensor ba, Tensor wb, Tensor bb, Tensor w2, Tensor b2, Tensor(a!) y, int ci, bool shortcut, int rb, Tensor? xu=None) -> ()");
   m.def("c2f_fused_s2_out(Tensor a0, Tensor w0, Tensor b0, Tensor w1, Tensor b1, Tensor wa, Tensor ba, Tensor wb, Tensor bb, Tensor w2, Tensor b2, Tensor(a!) y, bool shortcut, int rb) -> ()");
   m.def("c2f_bneck_out(Tensor x, Tensor wa, Tensor ba, Tensor wb, Tensor bb, Tensor(a!) y, bool shortcut, int rb) -> ()");
   m.def("conv_glds_tail_out(Tensor x, Tensor w, Tensor bias, Tensor w2, Tensor b2, Tensor(a!) y2, int R, int stride, int pad, int act, int act2, Tensor zero) -> ()");

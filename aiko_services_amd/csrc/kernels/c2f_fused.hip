@@ -55,6 +55,10 @@ struct C2fParams {
   const float* b2;
   bf16_t* y;             // [B][H][W][ldy] (CO channels written)
   int B, H, ldx, ldy, k1, ka, kb, k2, rb;
+  // optional (c2f_fused_wl_kernel): input channels [0, cu) come from xu [B][H/2][W/2][ldxu] at
+  // (h / 2, w / 2) — the PAN neck's nearest 2x upsample read in place, never materialised
+  const bf16_t* xu;
+  int ldxu, cu;
 };
 
 // W: row width (pixels), CI / C / CO: channels (C = 16: two taps per 32-wide K chunk), SC: the
@@ -559,9 +563,13 @@ __global__ __launch_bounds__(W * 4, 1) void c2f_fused_wl_kernel(C2fParams p) {
   bf16x8 xf[KS1];
   auto load_x = [&](int row) __attribute__((always_inline)) {
     const bool ok = row >= 0 && row < p.H;
-    const bf16_t* src = p.x + (((long)img * p.H + (ok ? row : 0)) * W + px0 + fr) * p.ldx + 8 * fq;
+    const int r = ok ? row : 0;
+    const bf16_t* src = p.x + (((long)img * p.H + r) * W + px0 + fr) * p.ldx + 8 * fq;
+    const bf16_t* srcu = p.xu ? p.xu + (((long)img * (p.H / 2) + (r >> 1)) * (W / 2) + ((px0 + fr) >> 1)) * p.ldxu + 8 * fq
+                              : src;
 #pragma unroll
-    for (int k = 0; k < KS1; ++k) xf[k] = *reinterpret_cast<const bf16x8*>(src + 32 * k);
+    for (int k = 0; k < KS1; ++k)
+      xf[k] = *reinterpret_cast<const bf16x8*>((32 * k < p.cu ? srcu : src) + 32 * k);
   };
   auto cv1 = [&](int row) __attribute__((always_inline)) {
     const bool ok = row >= 0 && row < p.H;
@@ -797,10 +805,13 @@ __global__ __launch_bounds__(W * 4, 1) void c2f_bneck_kernel(C2fParams p) {
 extern "C" int aiko_c2f_fused(const void* x, int ldx, const void* w1, const float* b1, int k1, const void* wa,
                               const float* ba, int ka, const void* wb, const float* bb, int kb, const void* w2,
                               const float* b2, int k2, void* y, int ldy, int B, int H, int W, int CI, int C, int CO,
-                              int shortcut, int rb, hipStream_t stream) {
+                              int shortcut, int rb, const void* xu, int ldxu, int cu, hipStream_t stream) {
   using namespace aiko;
   if (rb <= 0 || H % rb || B <= 0) return -1;
-  C2fParams p;
+  C2fParams p{};
+  p.xu = static_cast<const bf16_t*>(xu);
+  p.ldxu = ldxu;
+  p.cu = xu ? cu : 0;
   p.x = static_cast<const bf16_t*>(x);
   p.w1 = static_cast<const bf16_t*>(w1); p.b1 = b1;
   p.wa = static_cast<const bf16_t*>(wa); p.ba = ba;
@@ -810,6 +821,7 @@ extern "C" int aiko_c2f_fused(const void* x, int ldx, const void* w1, const floa
   p.B = B; p.H = H; p.ldx = ldx; p.ldy = ldy; p.k1 = k1; p.ka = ka; p.kb = kb; p.k2 = k2; p.rb = rb;
   const dim3 grid((unsigned)(B * (H / rb)));
   if (W == 160 && CI == 32 && C == 16 && CO == 32 && shortcut) {
+    if (xu) return -1;                             // (in-place upsample: the wide-channel kernel only)
     c2f_fused_kernel<160, 32, 16, 32, true><<<grid, dim3(320), 0, stream>>>(p);
   } else if (W == 80 && CI == 192 && C == 32 && CO == 64 && !shortcut) {
     c2f_fused_wl_kernel<80, 192, 32, 64, false><<<grid, dim3(320), 0, stream>>>(p);

@@ -40,6 +40,8 @@ REG_MAX = 16
 _HEAD_TAIL = __import__("os").environ.get("AIKO_HEAD_TAIL", "1") != "0"
 # ... and the box branch (3x3 64 -> 64 + 1x1 64 -> 64) the same way (AIKO_HEAD_TAIL_BOX=0: separate)
 _HEAD_TAIL_BOX = __import__("os").environ.get("AIKO_HEAD_TAIL_BOX", "1") != "0"
+# l15's fused C2f reads the 2x upsample of l12 in place (AIKO_UP_INPLACE=0: upsample2x kernel)
+_UP_INPLACE = __import__("os").environ.get("AIKO_UP_INPLACE", "1") != "0"
 
 
 def _make_div(x, d=8):
@@ -205,16 +207,20 @@ class YOLOv8(WeightsMixin):
         import os
         return int(os.environ.get("AIKO_C2F_RB" if H == 160 else "AIKO_C2F_RB80", "40" if H == 160 else "20"))
 
-    def _run_c2f(self, name, blk: C2f, x, out, cat=None):
+    def _run_c2f(self, name, blk: C2f, x, out, cat=None, xu=None):
         """``cat``: the block's split/concat buffer with cv1's output already in channels
-        [0, 2c) (``x`` then only gives the shape)."""
+        [0, 2c) (``x`` then only gives the shape).  ``xu``: the fused kernel reads x's first
+        ``xu.shape[3]`` channels as the nearest 2x upsample of ``xu`` (only with the fused C2f)."""
         B, H, W, _ = x.shape
         c, n = blk.c, len(blk.m)
         if cat is None and self._c2f_fused_ok(blk, x, out):
             a, b = blk.m[0]
             torch.ops.aiko.c2f_fused_out(x, blk.cv1.weight, blk.cv1.bias, a.weight, a.bias, b.weight, b.bias,
-                                         blk.cv2.weight, blk.cv2.bias, out, blk.cv1.Cc, blk.shortcut, self._c2f_rb(H))
+                                         blk.cv2.weight, blk.cv2.bias, out, blk.cv1.Cc, blk.shortcut, self._c2f_rb(H),
+                                         xu)
             return out
+        if xu is not None:
+            raise ValueError("_run_c2f: an in-place upsample source needs the fused C2f kernel")
         if cat is None:
             cat = self._buf(f"{name}.cat", (B, H, W, (2 + n) * c))
             C.conv2d(x, blk.cv1, out=cat[..., :2 * c])
@@ -352,8 +358,14 @@ class YOLOv8(WeightsMixin):
         DT.upsample2x(a9, out=cat11[..., :c5])
         cat17 = self._buf("cat17", (B, H4, W4, c3 + c4))       # [l16 | l12]
         a12 = self._run_c2f("l12", self.l12, cat11, cat17[..., c3:])
-        DT.upsample2x(a12, out=cat14[..., :c4])
-        p3 = self._run_c2f("l15", self.l15, cat14, self._buf("p3", (B, H3, W3, c3)))
+        p3 = self._buf("p3", (B, H3, W3, c3))
+        if _UP_INPLACE and self._c2f_fused_ok(self.l15, cat14, p3) and W3 == 2 * a12.shape[2]:
+            # l15's fused C2f reads up(l12) straight from a12: the upsampled half of cat14 is
+            # never materialised
+            self._run_c2f("l15", self.l15, cat14, p3, xu=a12)
+        else:
+            DT.upsample2x(a12, out=cat14[..., :c4])
+            self._run_c2f("l15", self.l15, cat14, p3)
         C.conv2d(p3, self.l16, out=cat17[..., :c3])
         p4 = self._run_c2f("l18", self.l18, cat17, self._buf("p4", (B, H4, W4, c4)))
         C.conv2d(p4, self.l19, out=cat20[..., :c4])

@@ -418,3 +418,19 @@ def test_yolo_tails_match_unfused(native, monkeypatch):
         a, b = a.float(), b.float()
         cos = torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()
         assert cos > 0.999, cos
+
+
+def test_yolo_upsample_inplace_matches(native, monkeypatch):
+    """l15's fused C2f reading up(l12) in place from a12 (no upsample2x kernel, the upsampled half
+    of its input buffer never written) gives bit-identical head outputs."""
+    from aiko_services_amd.models import yolov8 as Y
+    m = Y.YOLOv8("n", device=DEV)
+    g = torch.Generator().manual_seed(12)
+    a0 = (torch.randn(2, 320, 320, 16, generator=g) * 2).to(DEV, torch.bfloat16)
+    monkeypatch.setattr(Y, "_UP_INPLACE", True)
+    fused = [o.clone() for o in m.head_outputs(None, a0=a0)]
+    monkeypatch.setattr(Y, "_UP_INPLACE", False)
+    plain = [o.clone() for o in m.head_outputs(None, a0=a0)]
+    torch.cuda.synchronize()
+    for a, b in zip(fused, plain):
+        assert torch.equal(a, b)
