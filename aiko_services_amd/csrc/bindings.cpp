@@ -37,7 +37,8 @@ int aiko_conv_persist(const void* x, const void* w, const float* bias, const voi
                       int K1, int H2, int W2, int C2, int stride2, hipStream_t stream);
 int aiko_conv_glds_tail(const void* x, const void* w, const float* bias, int H, int W, int C, int Cc, int R, int S,
                         int stride, int pad, int Ho, int Wo, int M, int K, int N, int act, const void* w2, const float* b2,
-                        void* y2, int ldy2, int ldw2, int act2, const void* zero, hipStream_t stream);
+                        void* y2, int ldy2, int ldw2, int act2, const void* zero, const int* dec, void* boxes,
+                        float* scores, int* cls, hipStream_t stream);
 int aiko_conv_glds(const void* x, const void* w, const float* bias, const void* res, void* y,
                    int H, int W, int C, int Cc, int R, int S, int stride, int pad, int Ho,
                    int Wo, int M, int Cout, int K, int act, int ldy, int ldr, int bm, int bn,
@@ -649,8 +650,50 @@ void conv_glds_tail_out(const at::Tensor& x, const at::Tensor& w, const at::Tens
   check_launch(aiko_conv_glds_tail(x.data_ptr(), w.data_ptr(), bias.data_ptr<float>(), (int)H, (int)W, (int)C, (int)Cc,
                                    (int)R, (int)R, (int)stride, (int)pad, (int)Ho, (int)Wo, (int)M, (int)K, (int)N, (int)act,
                                    w2.data_ptr(), b2.data_ptr<float>(), y2.data_ptr(), (int)ldy2, (int)w2.size(1),
-                                   (int)act2, zero.data_ptr(), cur_stream()),
+                                   (int)act2, zero.data_ptr(), nullptr, nullptr, nullptr, nullptr, cur_stream()),
                "conv_glds_tail");
+}
+
+// The detect head's box / class branch (R x R conv + 1x1 as above) with the YOLOv8 decode in the
+// epilogue instead of a stored head output: mode 1 (N = 64, 4 x 16 DFL bins) writes xyxy boxes
+// [B, A] float4 at anchors astart + h * W + w, mode 2 (N = 80) sigmoid(max logit over the first nc)
+// and its class into scores / cls [B, A] (ops.detect.yolo_decode semantics, bf16-rounded inputs).
+void conv_glds_tail_decode_out(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, const at::Tensor& w2,
+                               const at::Tensor& b2, at::Tensor& boxes, at::Tensor& scores, at::Tensor& cls, int64_t R,
+                               int64_t pad, int64_t act, int64_t mode, int64_t nc, int64_t level_stride, int64_t astart,
+                               const at::Tensor& zero) {
+  for (const at::Tensor* t : {&x, &w, &bias, &w2, &b2, (const at::Tensor*)&boxes, (const at::Tensor*)&scores,
+                              (const at::Tensor*)&cls, &zero})
+    check_cuda(*t, "conv tail decode operand");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 && w2.scalar_type() == at::kBFloat16,
+              "aiko.conv_glds_tail_decode_out: bf16 activations / weights");
+  TORCH_CHECK(bias.scalar_type() == at::kFloat && b2.scalar_type() == at::kFloat && bias.is_contiguous() && b2.is_contiguous(),
+              "aiko.conv_glds_tail_decode_out: fp32 biases");
+  const int64_t N = w.size(0);
+  TORCH_CHECK((mode == 1 && N == 64) || (mode == 2 && N == 80), "aiko.conv_glds_tail_decode_out: mode 1 needs N = 64, mode 2 N = 80");
+  TORCH_CHECK(bias.numel() == N && b2.numel() == N && nc >= 1 && nc <= N, "aiko.conv_glds_tail_decode_out: biases [N], 1 <= nc <= N");
+  TORCH_CHECK(x.dim() == 4 && x.stride(3) == 1, "aiko.conv_glds_tail_decode_out: NHWC x");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), Cc = x.size(3), C = x.stride(2);
+  TORCH_CHECK(x.stride(1) == W * C && x.stride(0) == H * W * C && C % 8 == 0 && Cc % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "aiko.conv_glds_tail_decode_out: x must be an NHWC (channel-slice) view with 16-B aligned pixels");
+  const int64_t K = (R * R * Cc + 63) / 64 * 64;
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && w.size(1) == K, "aiko.conv_glds_tail_decode_out: w [N, ceil64(R*R*Cc)]");
+  TORCH_CHECK(w2.dim() == 2 && w2.is_contiguous() && w2.size(0) == N && w2.size(1) >= (N + 31) / 32 * 32 && w2.size(1) % 8 == 0,
+              "aiko.conv_glds_tail_decode_out: w2 [N, >= ceil32(N)]");
+  const int64_t Ho = H + 2 * pad - R + 1, Wo = W + 2 * pad - R + 1;
+  TORCH_CHECK(boxes.scalar_type() == at::kFloat && boxes.dim() == 3 && boxes.size(0) == B && boxes.size(2) == 4 &&
+                  boxes.is_contiguous() && scores.scalar_type() == at::kFloat && scores.dim() == 2 && scores.is_contiguous() &&
+                  cls.scalar_type() == at::kInt && cls.dim() == 2 && cls.is_contiguous() && scores.size(0) == B &&
+                  cls.size(0) == B && scores.size(1) == boxes.size(1) && cls.size(1) == boxes.size(1) &&
+                  astart >= 0 && astart + Ho * Wo <= boxes.size(1),
+              "aiko.conv_glds_tail_decode_out: boxes [B, A, 4] f32, scores [B, A] f32, cls [B, A] i32 covering the level");
+  const int dec[5] = {(int)mode, (int)nc, (int)level_stride, (int)astart, (int)boxes.size(1)};
+  check_launch(aiko_conv_glds_tail(x.data_ptr(), w.data_ptr(), bias.data_ptr<float>(), (int)H, (int)W, (int)C, (int)Cc,
+                                   (int)R, (int)R, 1, (int)pad, (int)Ho, (int)Wo, (int)(B * Ho * Wo), (int)K, (int)N, (int)act,
+                                   w2.data_ptr(), b2.data_ptr<float>(), nullptr, 0, (int)w2.size(1), 0, zero.data_ptr(), dec,
+                                   boxes.data_ptr(), scores.data_ptr<float>(), cls.data_ptr<int>(), cur_stream()),
+               "conv_glds_tail_decode");
 }
 
 // A whole ResNet stage-1 bottleneck in one launch (bneck_fused.hip): x [B, H, 56, cin] ->
@@ -1543,6 +1586,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("c2f_fused_out(Tensor x, Tensor w1, Tensor b1, Tensor wa, Tensor ba, Tensor wb, Tensor bb, Tensor w2, Tensor b2, Tensor(a!) y, int ci, bool shortcut, int rb, Tensor? xu=None) -> ()");
   m.def("c2f_fused_s2_out(Tensor a0, Tensor w0, Tensor b0, Tensor w1, Tensor b1, Tensor wa, Tensor ba, Tensor wb, Tensor bb, Tensor w2, Tensor b2, Tensor(a!) y, bool shortcut, int rb) -> ()");
   m.def("c2f_bneck_out(Tensor x, Tensor wa, Tensor ba, Tensor wb, Tensor bb, Tensor(a!) y, bool shortcut, int rb) -> ()");
+  m.def("conv_glds_tail_decode_out(Tensor x, Tensor w, Tensor bias, Tensor w2, Tensor b2, Tensor(a!) boxes, Tensor(b!) scores, Tensor(c!) cls, int R, int pad, int act, int mode, int nc, int level_stride, int astart, Tensor zero) -> ()");
   m.def("conv_glds_tail_out(Tensor x, Tensor w, Tensor bias, Tensor w2, Tensor b2, Tensor(a!) y2, int R, int stride, int pad, int act, int act2, Tensor zero) -> ()");
   m.def("linear_splitk_out(Tensor x, Tensor w, Tensor? bias, Tensor(a!) part, Tensor(b!) y, int K, int S) -> ()");
   m.def("attn_fwd_out(Tensor q, Tensor k, Tensor v, Tensor(a!) o, int B, int H, int T, int Tpad, float scale, Tensor(b!)? work=None, Tensor(c!)? oq=None, Tensor(d!)? osc=None) -> ()");
@@ -1584,6 +1628,7 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("c2f_fused_out", &c2f_fused_out);
   m.impl("c2f_bneck_out", &c2f_bneck_out);
   m.impl("conv_glds_tail_out", &conv_glds_tail_out);
+  m.impl("conv_glds_tail_decode_out", &conv_glds_tail_decode_out);
   m.impl("c2f_fused_s2_out", &c2f_fused_s2_out);
   m.impl("attn_fwd_out", &attn_fwd_out);
   m.impl("linear_splitk_out", &linear_splitk_out);

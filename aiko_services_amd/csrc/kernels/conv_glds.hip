@@ -55,7 +55,37 @@ struct GldsTail {
   const float* b2;
   bf16_t* y2;
   int ldy2, ldw2, act2;   // act2: 0 none, 2 SiLU on the 1x1's output
+  // dmode 1 / 2: YOLOv8 decode in the epilogue instead of storing the 1x1's output (the detect
+  // head's box / class branch): 1 = DFL expectation of the 4 x 16 box bins -> xyxy boxes,
+  // 2 = max / argmax over the first nc class logits -> sigmoid score + class.  Values are rounded
+  // to bf16 first, as the stored head output would be (ops.detect.yolo_decode semantics).
+  int dmode, nc, HW, Wl, lstride, astart, A;
+  float4* boxes;
+  float* scores;
+  int* cls;
 };
+
+// reductions over lanes l, l^16, l^32, l^48 (gfx950 v_permlane16/32_swap with both operands = v
+// return the two halves of the exchange: combining the pair reduces over the xor partner)
+__device__ __forceinline__ float tail_sum4(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+__device__ __forceinline__ float tail_max4(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ int tail_min4(int v) {
+  const auto a = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+  v = min((int)a[0], (int)a[1]);
+  const auto b = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+  return min((int)b[0], (int)b[1]);
+}
+__device__ __forceinline__ float tail_bf16(float x) { return __uint_as_float((pack2(x, 0.f) & 0xffffu) << 16); }
 
 // WGM x WGN waves (2 x 2; exact-N tiles such as BN = 80: 4 x 1, each wave all BN columns)
 template <int BM, int BN, int WGM = 2, int WGN = 2, bool TAIL = false>
@@ -352,6 +382,61 @@ __global__ __launch_bounds__(256, (glds_occupancy<BM, BN>())) void conv_glds_ker
         for (int j = 0; j < NI2; ++j)
           acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], tf[i], acc2[i][j], 0, 0, 0);
     }
+    if (tl.dmode == 1) {                 // box branch: DFL -> xyxy (4 sides x 16 bins = NI2 x 16)
+#pragma unroll
+      for (int i = 0; i < MI2; ++i) {
+        const int m = m0 + wave * (BM / 4) + 16 * i + fr;
+        float dist[NI2];
+#pragma unroll
+        for (int j = 0; j < NI2; ++j) {
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = tail_bf16(acc2[i][j][e]);
+          const float mx = tail_max4(fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+          float se = 0.f, sk = 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float ex = __expf(v[e] - mx);
+            se += ex;
+            sk += ex * (float)(4 * fq + e);
+          }
+          dist[j] = tail_sum4(sk) / tail_sum4(se);
+        }
+        if (m < p.M && fq == 0) {
+          const int b = m / tl.HW, r = m - b * tl.HW, h = r / tl.Wl, w = r - h * tl.Wl;
+          const float sc = (float)tl.lstride, ax = w + 0.5f, ay = h + 0.5f;
+          tl.boxes[(long)b * tl.A + tl.astart + r] =
+              make_float4((ax - dist[0]) * sc, (ay - dist[1]) * sc, (ax + dist[2]) * sc, (ay + dist[3]) * sc);
+        }
+      }
+      return;
+    }
+    if (tl.dmode == 2) {                 // class branch: max / argmax (lowest index on ties)
+#pragma unroll
+      for (int i = 0; i < MI2; ++i) {
+        const int m = m0 + wave * (BM / 4) + 16 * i + fr;
+        float best = -INFINITY;
+        int bi = 0x7fffffff;
+#pragma unroll
+        for (int j = 0; j < NI2; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int c = 16 * j + 4 * fq + e;
+            const float v = tail_bf16(acc2[i][j][e]);
+            if (c < tl.nc && v > best) { best = v; bi = c; }
+          }
+        const float g = tail_max4(best);
+        int cand = tail_min4(best == g ? bi : 0x7fffffff);
+        if (cand == 0x7fffffff) cand = 0;
+        if (m < p.M && fq == 0) {
+          const int b = m / tl.HW, r = m - b * tl.HW;
+          const long idx = (long)b * tl.A + tl.astart + r;
+          tl.scores[idx] = 1.f / (1.f + __expf(-g));
+          tl.cls[idx] = cand;
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < MI2; ++i) {
       const int m = m0 + wave * (BM / 4) + 16 * i + fr;
@@ -418,7 +503,7 @@ extern "C" int aiko_conv_glds(const void* x, const void* w, const float* bias, c
 extern "C" int aiko_conv_glds_tail(const void* x, const void* w, const float* bias, int H, int W, int C, int Cc,
                                    int R, int S, int stride, int pad, int Ho, int Wo, int M, int K, int N, int act,
                                    const void* w2, const float* b2, void* y2, int ldy2, int ldw2, int act2, const void* zero,
-                                   hipStream_t stream) {
+                                   const int* dec, void* boxes, float* scores, int* cls, hipStream_t stream) {
   using namespace aiko;
   ConvParams p;
   p.x = static_cast<const bf16_t*>(x);
@@ -432,7 +517,16 @@ extern "C" int aiko_conv_glds_tail(const void* x, const void* w, const float* bi
   p.x2 = nullptr;
   p.K1 = K; p.H2 = 1; p.W2 = 1; p.C2 = 8; p.stride2 = 1;
   conv_params_finalize(p);
-  GldsTail tl{static_cast<const bf16_t*>(w2), b2, static_cast<bf16_t*>(y2), ldy2, ldw2, act2};
+  GldsTail tl{};
+  tl.w2 = static_cast<const bf16_t*>(w2);
+  tl.b2 = b2;
+  tl.y2 = static_cast<bf16_t*>(y2);
+  tl.ldy2 = ldy2; tl.ldw2 = ldw2; tl.act2 = act2;
+  if (dec) {
+    tl.dmode = dec[0]; tl.nc = dec[1]; tl.HW = Ho * Wo; tl.Wl = Wo; tl.lstride = dec[2]; tl.astart = dec[3];
+    tl.A = dec[4];
+    tl.boxes = static_cast<float4*>(boxes); tl.scores = scores; tl.cls = cls;
+  }
   dim3 grid((M + 127) / 128), block(256);
   if (N == 80)
     conv_glds_kernel<128, 80, 4, 1, true><<<grid, block, 0, stream>>>(p, static_cast<const bf16_t*>(zero), tl);

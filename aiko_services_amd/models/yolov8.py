@@ -40,6 +40,9 @@ REG_MAX = 16
 _HEAD_TAIL = __import__("os").environ.get("AIKO_HEAD_TAIL", "1") != "0"
 # ... and the box branch (3x3 64 -> 64 + 1x1 64 -> 64) the same way (AIKO_HEAD_TAIL_BOX=0: separate)
 _HEAD_TAIL_BOX = __import__("os").environ.get("AIKO_HEAD_TAIL_BOX", "1") != "0"
+# the detect head's tail launches decode in their epilogues (AIKO_DECODE_FUSED=0: head outputs +
+# the yolo_decode kernel)
+_DECODE_FUSED = __import__("os").environ.get("AIKO_DECODE_FUSED", "1") != "0"
 # l15's fused C2f reads the 2x upsample of l12 in place (AIKO_UP_INPLACE=0: upsample2x kernel)
 _UP_INPLACE = __import__("os").environ.get("AIKO_UP_INPLACE", "1") != "0"
 
@@ -305,9 +308,10 @@ class YOLOv8(WeightsMixin):
                                        list(V.YOLO_MEAN), list(V.YOLO_STD), False)
         return out
 
-    def head_outputs(self, x: torch.Tensor | None, a0: torch.Tensor | None = None):
+    def head_outputs(self, x: torch.Tensor | None, a0: torch.Tensor | None = None, decode: bool = False):
         """Stem buffer (or the stem output ``a0``) -> per-level head outputs
-        [B, H/s, W/s, 64 + nc] for s = 8, 16, 32."""
+        [B, H/s, W/s, 64 + nc] for s = 8, 16, 32.  ``decode``: the head branches decode in their
+        epilogues instead (:meth:`_decode_fused_ok`) and this returns (boxes, scores, cls)."""
         B = (x if a0 is None else a0).shape[0]
         S = self.image_size
         c1, c2, c3, c4, c5 = self.ch
@@ -370,7 +374,50 @@ class YOLOv8(WeightsMixin):
         p4 = self._run_c2f("l18", self.l18, cat17, self._buf("p4", (B, H4, W4, c4)))
         C.conv2d(p4, self.l19, out=cat20[..., :c4])
         p5 = self._run_c2f("l21", self.l21, cat20, self._buf("p5", (B, H5, W5, c5)))
+        if decode:
+            A = sum(p.shape[1] * p.shape[2] for p in (p3, p4, p5))
+            boxes = self._buf("boxes", (B, A, 4), torch.float32)
+            scores = self._buf("scores", (B, A), torch.float32)
+            cls = self._buf("cls", (B, A), torch.int32)
+            astart = 0
+            for i, (lvl, p) in enumerate(zip(self.heads, (p3, p4, p5))):
+                self._run_head_decode(i, lvl, p, boxes, scores, cls, STRIDES[i], astart)
+                astart += p.shape[1] * p.shape[2]
+            return boxes, scores, cls
         return [self._run_head(i, lvl, p) for i, (lvl, p) in enumerate(zip(self.heads, (p3, p4, p5)))]
+
+    def _decode_fused_ok(self) -> bool:
+        """Can every detect-head branch run as a tail launch with the decode in its epilogue
+        (box: 4 x 16 DFL bins on the 64-channel branch; class: the 80-channel branch)?"""
+        return (_HEAD_TAIL and _DECODE_FUSED and self.device.type == "cuda" and self.cb == 4 * REG_MAX == 64
+                and self.cc == 80 and self.nc_pad == 80
+                and all(lvl.box[1].cout == 64 and lvl.cls[1].cout == 80 and lvl.box[1].stride == 1
+                        and lvl.cls[1].stride == 1 for lvl in self.heads))
+
+    def _run_head_decode(self, i, lvl: DetectLevel, x, boxes, scores, cls, stride, astart):
+        """Detect head level ``i`` straight to decoded (boxes, scores, cls) rows astart .. of
+        the [B, A] outputs: the first conv, then each branch's 3x3 + 1x1 as one conv_glds tail
+        launch whose epilogue decodes (box: DFL expectation -> xyxy; class: sigmoid(max) /
+        argmax) — the [.., 64 + nc] head output is never written."""
+        B, H, W, _ = x.shape
+        cb = self.cb
+        h1 = self._buf(f"h{i}.1", (B, H, W, cb + self.cc))
+        C.conv2d(x, lvl.first, out=h1)
+        zp = C.zero_page(x.device)
+        for xs, (s1, s2), mode, nc in ((h1[..., :cb], (lvl.box[1], lvl.box[2]), 1, 4 * REG_MAX),
+                                       (h1[..., cb:], (lvl.cls[1], lvl.cls[2]), 2, self.nc_pad)):
+            if not C.conv_tail_ok(xs, s1, s2):
+                raise ValueError("_run_head_decode: head branch not eligible for a tail launch")
+            torch.ops.aiko.conv_glds_tail_decode_out(xs, s1.weight, s1.bias, s2.weight, s2.bias, boxes, scores, cls,
+                                                     s1.R, s1.pad, s1.act, mode, nc, stride, astart, zp)
+
+    def _nms(self, boxes, scores, cls, frame_hw):
+        B = boxes.shape[0]
+        _, _, top, left, gain = self.letterbox(frame_hw)
+        return DT.topk_nms(boxes, scores, cls, self.conf, self.iou, self.max_candidates, self.max_det,
+                           (gain, left, top, frame_hw[1], frame_hw[0]),
+                           det=self._buf("det", (B, self.max_det, 6), torch.float32),
+                           count=self._buf("count", (B,), torch.int32))
 
     def postprocess(self, feats, frame_hw):
         B = feats[0].shape[0]
@@ -386,6 +433,8 @@ class YOLOv8(WeightsMixin):
 
     def detect(self, frames: torch.Tensor):
         H, W = frames.shape[1:3]
+        if self.fused_stem and self._decode_fused_ok():
+            return self._nms(*self.head_outputs(None, a0=self.stem_from_frames(frames), decode=True), (H, W))
         if self.fused_stem:
             return self.postprocess(self.head_outputs(None, a0=self.stem_from_frames(frames)), (H, W))
         return self.postprocess(self.head_outputs(self.preprocess(frames)), (H, W))

@@ -434,3 +434,31 @@ def test_yolo_upsample_inplace_matches(native, monkeypatch):
     torch.cuda.synchronize()
     for a, b in zip(fused, plain):
         assert torch.equal(a, b)
+
+
+def test_yolo_decode_in_tail_matches_decode_kernel(native, monkeypatch):
+    """The detect head's tail launches decoding in their epilogues (DFL -> xyxy boxes, sigmoid(max)
+    / argmax) against the stored head outputs + the yolo_decode kernel, and the final detections."""
+    from aiko_services_amd.models import yolov8 as Y
+    from aiko_services_amd.ops import detect as DT
+    m = Y.YOLOv8("n", device=DEV, cls_bias=0.0)
+    assert m._decode_fused_ok()
+    g = torch.Generator().manual_seed(13)
+    a0 = (torch.randn(2, 320, 320, 16, generator=g) * 2).to(DEV, torch.bfloat16)
+    bf, sf, cf = (t.clone() for t in m.head_outputs(None, a0=a0, decode=True))
+    feats = m.head_outputs(None, a0=a0)
+    A = sum(f.shape[1] * f.shape[2] for f in feats)
+    bd, sd, cd = DT.yolo_decode(feats, Y.STRIDES, m.nc_pad, boxes=torch.empty(2, A, 4, device=DEV),
+                                scores=torch.empty(2, A, device=DEV), cls=torch.empty(2, A, dtype=torch.int32, device=DEV))
+    torch.cuda.synchronize()
+    assert torch.equal(cf, cd)
+    assert torch.equal(sf, sd)
+    assert (bf - bd).abs().max().item() < 1e-3 * bd.abs().max().item()
+    # whole detect(): fused decode vs the decode kernel
+    frames = torch.randint(0, 256, (2, 480, 640, 3), generator=g, dtype=torch.uint8).to(DEV)
+    det_f, cnt_f = (t.clone() for t in m.detect(frames))
+    monkeypatch.setattr(Y, "_DECODE_FUSED", False)
+    det_d, cnt_d = (t.clone() for t in m.detect(frames))
+    torch.cuda.synchronize()
+    assert torch.equal(cnt_f, cnt_d)
+    assert (det_f - det_d).abs().max().item() < 1e-2 * max(1.0, det_d.abs().max().item())
