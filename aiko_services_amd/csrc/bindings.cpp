@@ -35,6 +35,9 @@ int aiko_conv_persist(const void* x, const void* w, const float* bias, const voi
                       int H, int W, int C, int Cc, int R, int S, int stride, int pad, int Ho, int Wo,
                       int M, int Cout, int K, int act, int ldy, int ldr, int bm, int bn, const void* x2,
                       int K1, int H2, int W2, int C2, int stride2, hipStream_t stream);
+int aiko_stem_l1(const void* in, void* out, const void* w0, const float* b0, const void* w1, int k1, const float* b1,
+                 int B, int Hin, int Win, int Hc, int Wc, int off_t, int off_l, float fill_raw, float inv_std, int H0,
+                 int W0, int H1, int W1, int ldo, hipStream_t stream);
 int aiko_conv_glds_tail(const void* x, const void* w, const float* bias, int H, int W, int C, int Cc, int R, int S,
                         int stride, int pad, int Ho, int Wo, int M, int K, int N, int act, const void* w2, const float* b2,
                         void* y2, int ldy2, int ldw2, int act2, const void* zero, const int* dec, void* boxes,
@@ -694,6 +697,39 @@ void conv_glds_tail_decode_out(const at::Tensor& x, const at::Tensor& w, const a
                                    w2.data_ptr(), b2.data_ptr<float>(), nullptr, 0, (int)w2.size(1), 0, zero.data_ptr(), dec,
                                    boxes.data_ptr(), scores.data_ptr<float>(), cls.data_ptr<int>(), cur_stream()),
                "conv_glds_tail_decode");
+}
+
+// YOLOv8 stem (3x3 / 2, 3 -> 16, SiLU, /255) + l1 (3x3 / 2, 16 -> 32, SiLU) from uint8 frames in one
+// launch (stem_l1.hip): a0 never reaches HBM.  geom = [Ho, Wo, Hc, Wc, off_t, off_l] as stem_direct_out
+// (no resize: Ho x Wo = the frame); w0 [16, 64] the direct-stem weight image, w1 [32, >= 160].
+void stem_l1_out(const at::Tensor& frames, const at::Tensor& w0, const at::Tensor& b0, const at::Tensor& w1,
+                 const at::Tensor& b1, at::Tensor& out, at::IntArrayRef geom, double fill, double inv_std) {
+  for (const at::Tensor* t : {&frames, &w0, &b0, &w1, &b1, (const at::Tensor*)&out}) check_cuda(*t, "stem_l1 operand");
+  TORCH_CHECK(frames.scalar_type() == at::kByte && frames.dim() == 4 && frames.size(3) == 3 && frames.is_contiguous(),
+              "aiko.stem_l1_out: frames must be uint8 [B, H, W, 3] contiguous");
+  TORCH_CHECK(geom.size() == 6, "aiko.stem_l1_out: geom = [Ho, Wo, Hc, Wc, off_t, off_l]");
+  const int64_t Ho = geom[0], Wo = geom[1], Hc = geom[2], Wc = geom[3], off_t = geom[4], off_l = geom[5];
+  const int64_t B = frames.size(0), Hin = frames.size(1), Win = frames.size(2);
+  TORCH_CHECK(Ho == Hin && Wo == Win && off_t >= 0 && off_l >= 0 && off_t + Ho <= Hc && off_l + Wo <= Wc &&
+                  off_l % 4 == 0 && Win % 4 == 0 && Wc % 4 == 0 && Hc % 4 == 0,
+              "aiko.stem_l1_out: unresized frame inside the canvas, 4-pixel aligned columns");
+  TORCH_CHECK(w0.scalar_type() == at::kBFloat16 && w0.is_contiguous() && w0.dim() == 2 && w0.size(0) == 16 && w0.size(1) == 64,
+              "aiko.stem_l1_out: w0 bf16 [16, 64]");
+  TORCH_CHECK(w1.scalar_type() == at::kBFloat16 && w1.is_contiguous() && w1.dim() == 2 && w1.size(0) == 32 && w1.size(1) >= 160,
+              "aiko.stem_l1_out: w1 bf16 [32, >= 160]");
+  TORCH_CHECK(b0.scalar_type() == at::kFloat && b0.numel() == 16 && b0.is_contiguous() && b1.scalar_type() == at::kFloat &&
+                  b1.numel() == 32 && b1.is_contiguous(),
+              "aiko.stem_l1_out: fp32 biases [16] / [32]");
+  const int64_t H0 = Hc / 2, W0 = Wc / 2, H1 = H0 / 2, W1 = W0 / 2;
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.dim() == 4 && out.size(0) == B && out.size(1) == H1 &&
+                  out.size(2) == W1 && out.size(3) == 32,
+              "aiko.stem_l1_out: out bf16 [B, Hc / 4, Wc / 4, 32]");
+  const int64_t ldo = pixel_pitch(out, "stem_l1_out");
+  check_launch(aiko_stem_l1(frames.data_ptr(), out.data_ptr(), w0.data_ptr(), b0.data_ptr<float>(), w1.data_ptr(),
+                            (int)w1.size(1), b1.data_ptr<float>(), (int)B, (int)Hin, (int)Win, (int)Hc, (int)Wc, (int)off_t,
+                            (int)off_l, (float)fill, (float)inv_std, (int)H0, (int)W0, (int)H1, (int)W1, (int)ldo,
+                            cur_stream()),
+               "stem_l1");
 }
 
 // A whole ResNet stage-1 bottleneck in one launch (bneck_fused.hip): x [B, H, 56, cin] ->
@@ -1565,6 +1601,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("batchnorm_out(Tensor x, Tensor scale, Tensor shift, Tensor(a!) y, int act) -> ()");
   m.def("yolo_decode_out(Tensor[] feats, int[] strides, int nc, int reg_max, Tensor(a!) boxes, Tensor(b!) scores, Tensor(c!) cls) -> ()");
   m.def("topk_nms_out(Tensor boxes, Tensor scores, Tensor cls, int max_cand, float[] params, Tensor(a!) det, Tensor(b!) count) -> ()");
+  m.def("stem_l1_out(Tensor frames, Tensor w0, Tensor b0, Tensor w1, Tensor b1, Tensor(a!) out, int[] geom, float fill, float inv_std) -> ()");
   m.def("stem_direct_out(Tensor frames, Tensor w, Tensor? bias, Tensor(a!) out, int[] geom, float fill, float[] mean, float[] std, bool bgr) -> ()");
   m.def("conv3x3_patch_out(Tensor x, Tensor wimg, Tensor? bias, Tensor(a!) y, int act, int grid=0) -> ()");
   m.def("conv3x3_patchw_out(Tensor x, Tensor wimg, Tensor? bias, Tensor(a!) y, int act, int grid=0) -> ()");
@@ -1628,6 +1665,7 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("c2f_fused_out", &c2f_fused_out);
   m.impl("c2f_bneck_out", &c2f_bneck_out);
   m.impl("conv_glds_tail_out", &conv_glds_tail_out);
+  m.impl("stem_l1_out", &stem_l1_out);
   m.impl("conv_glds_tail_decode_out", &conv_glds_tail_decode_out);
   m.impl("c2f_fused_s2_out", &c2f_fused_s2_out);
   m.impl("attn_fwd_out", &attn_fwd_out);

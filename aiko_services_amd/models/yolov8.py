@@ -43,6 +43,10 @@ _HEAD_TAIL_BOX = __import__("os").environ.get("AIKO_HEAD_TAIL_BOX", "1") != "0"
 # the detect head's tail launches decode in their epilogues (AIKO_DECODE_FUSED=0: head outputs +
 # the yolo_decode kernel)
 _DECODE_FUSED = __import__("os").environ.get("AIKO_DECODE_FUSED", "1") != "0"
+# letterbox + stem + l1 as one launch, a0 never written (stem_l1.hip).  Measured (round 5,
+# scripts/r5_stem_l1_micro.py, B = 64): 153 us against 60 + 88 us for the two kernels, bench
+# 42.7-43.8k vs 45.2-45.7k with an earlier 174-183 us version — not faster, so opt-in (AIKO_STEM_L1=1)
+_STEM_L1 = __import__("os").environ.get("AIKO_STEM_L1", "0") == "1"
 # l15's fused C2f reads the 2x upsample of l12 in place (AIKO_UP_INPLACE=0: upsample2x kernel)
 _UP_INPLACE = __import__("os").environ.get("AIKO_UP_INPLACE", "1") != "0"
 
@@ -308,11 +312,12 @@ class YOLOv8(WeightsMixin):
                                        list(V.YOLO_MEAN), list(V.YOLO_STD), False)
         return out
 
-    def head_outputs(self, x: torch.Tensor | None, a0: torch.Tensor | None = None, decode: bool = False):
+    def head_outputs(self, x: torch.Tensor | None, a0: torch.Tensor | None = None, decode: bool = False,
+                     a1: torch.Tensor | None = None):
         """Stem buffer (or the stem output ``a0``) -> per-level head outputs
         [B, H/s, W/s, 64 + nc] for s = 8, 16, 32.  ``decode``: the head branches decode in their
         epilogues instead (:meth:`_decode_fused_ok`) and this returns (boxes, scores, cls)."""
-        B = (x if a0 is None else a0).shape[0]
+        B = (a1 if a1 is not None else x if a0 is None else a0).shape[0]
         S = self.image_size
         c1, c2, c3, c4, c5 = self.ch
         h0, w0 = C.stem_out_hw(S, S, 3, 2, 1)
@@ -321,10 +326,12 @@ class YOLOv8(WeightsMixin):
             h, w = s[-1]
             s.append(((h - 1) // 2 + 1, (w - 1) // 2 + 1))
         (H1, W1), (H2, W2), (H3, W3), (H4, W4), (H5, W5) = s
-        if a0 is None:
-            a0 = C.conv2d(x, self.l0, out=self._buf("a0", (B, H1, W1, c1)), image_hw=(S, S))
         a2 = self._buf("a2", (B, H2, W2, c2))
-        if self._l1l2_fused_ok(a0, a2):
+        if a1 is None and a0 is None:
+            a0 = C.conv2d(x, self.l0, out=self._buf("a0", (B, H1, W1, c1)), image_hw=(S, S))
+        if a1 is not None:                  # stem + l1 already ran as one launch (stem_l1_from_frames)
+            a2 = self._run_c2f("l2", self.l2, a1, a2)
+        elif self._l1l2_fused_ok(a0, a2):
             # l1 (3x3 / 2) and the l2 C2f in one row-stream launch: a1 is never written
             a, b = self.l2.m[0]
             torch.ops.aiko.c2f_fused_s2_out(a0, self.l1.weight, self.l1.bias, self.l2.cv1.weight, self.l2.cv1.bias,
@@ -431,8 +438,37 @@ class YOLOv8(WeightsMixin):
                            det=self._buf("det", (B, self.max_det, 6), torch.float32),
                            count=self._buf("count", (B,), torch.int32))
 
+    def _stem_l1_ok(self, frames: torch.Tensor) -> bool:
+        """Can the letterbox + stem + l1 run as ONE launch (stem_l1.hip): an unresized uint8 frame
+        with 4-pixel aligned columns on the canvas, YOLO's /255 normalisation, a 3x3 / 2 16 -> 32 l1."""
+        if not (_STEM_L1 and self.fused_stem and frames.is_cuda and frames.dtype == torch.uint8 and frames.dim() == 4
+                and frames.is_contiguous() and self.ch[0] == 16 and self.ch[1] == 32):
+            return False
+        Ho, Wo, top, left, _ = self.letterbox(frames.shape[1:3])
+        S = self.image_size
+        return ((Ho, Wo) == tuple(frames.shape[1:3]) and left % 4 == 0 and Wo % 4 == 0 and S % 4 == 0
+                and self.l1.R == 3 and self.l1.stride == 2 and self.l1.pad == 1 and self.l1.Cc == 16
+                and self.l1.weight.shape[1] >= 160 and tuple(V.YOLO_MEAN) == (0.0, 0.0, 0.0)
+                and len(set(V.YOLO_STD)) == 1)
+
+    def stem_l1_from_frames(self, frames: torch.Tensor) -> torch.Tensor:
+        """uint8 [B, H, W, 3] -> l1's output [B, S/4, S/4, 32] in ONE kernel (stem_l1_kernel:
+        letterbox + /255 + stem conv + SiLU into LDS, then l1 + SiLU) — a0 never reaches HBM."""
+        B = frames.shape[0]
+        Ho, Wo, top, left, _ = self.letterbox(frames.shape[1:3])
+        S = self.image_size
+        if self._stem_w is None:
+            self._stem_w = torch.zeros(self.l0.cout, 64, dtype=torch.bfloat16, device=self.l0.weight.device)
+            self._derive_stem_w()
+        out = self._buf("a1", (B, S // 4, S // 4, self.ch[1]))
+        torch.ops.aiko.stem_l1_out(frames, self._stem_w, self.l0.bias, self.l1.weight, self.l1.bias, out,
+                                   [Ho, Wo, S, S, top, left], 114.0, 1.0 / (255.0 * V.YOLO_STD[0]))
+        return out
+
     def detect(self, frames: torch.Tensor):
         H, W = frames.shape[1:3]
+        if self._stem_l1_ok(frames) and self._decode_fused_ok():
+            return self._nms(*self.head_outputs(None, a1=self.stem_l1_from_frames(frames), decode=True), (H, W))
         if self.fused_stem and self._decode_fused_ok():
             return self._nms(*self.head_outputs(None, a0=self.stem_from_frames(frames), decode=True), (H, W))
         if self.fused_stem:

@@ -454,7 +454,8 @@ def test_yolo_decode_in_tail_matches_decode_kernel(native, monkeypatch):
     assert torch.equal(cf, cd)
     assert torch.equal(sf, sd)
     assert (bf - bd).abs().max().item() < 1e-3 * bd.abs().max().item()
-    # whole detect(): fused decode vs the decode kernel
+    # whole detect(): fused decode vs the decode kernel (same front end for both)
+    monkeypatch.setattr(Y, "_STEM_L1", False)
     frames = torch.randint(0, 256, (2, 480, 640, 3), generator=g, dtype=torch.uint8).to(DEV)
     det_f, cnt_f = (t.clone() for t in m.detect(frames))
     monkeypatch.setattr(Y, "_DECODE_FUSED", False)
@@ -462,3 +463,29 @@ def test_yolo_decode_in_tail_matches_decode_kernel(native, monkeypatch):
     torch.cuda.synchronize()
     assert torch.equal(cnt_f, cnt_d)
     assert (det_f - det_d).abs().max().item() < 1e-2 * max(1.0, det_d.abs().max().item())
+
+
+@pytest.mark.parametrize("hw", [(480, 640), (640, 480)])
+def test_stem_l1_fused_matches_two_kernels(native, monkeypatch, hw):
+    """Letterbox + stem + l1 in one launch (stem_l1_kernel: a0 only in LDS) against the stem kernel
+    followed by the l1 conv, for landscape and portrait frames (letterbox bars on either axis)."""
+    from aiko_services_amd.models import yolov8 as Y
+    from aiko_services_amd.ops import conv as C
+    m = Y.YOLOv8("n", device=DEV)
+    monkeypatch.setattr(Y, "_STEM_L1", True)
+    g = torch.Generator().manual_seed(hw[0])
+    frames = torch.randint(0, 256, (2, hw[0], hw[1], 3), generator=g, dtype=torch.uint8).to(DEV)
+    assert m._stem_l1_ok(frames)
+    a1f = m.stem_l1_from_frames(frames).clone()
+    a1u = C.conv2d(m.stem_from_frames(frames), m.l1)
+    torch.cuda.synchronize()
+    a, b = a1f.float(), a1u.float()
+    cos = torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()
+    assert cos > 0.99995, cos
+    assert (a - b).abs().max().item() < 0.02 * b.abs().max().item()
+    # whole detect(): fused front vs stem kernel + l1 conv
+    det_f, cnt_f = (t.clone() for t in m.detect(frames))
+    monkeypatch.setattr(Y, "_STEM_L1", False)
+    det_u, cnt_u = (t.clone() for t in m.detect(frames))
+    torch.cuda.synchronize()
+    assert (cnt_f - cnt_u).abs().max().item() <= 2
