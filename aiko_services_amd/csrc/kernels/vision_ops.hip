@@ -761,15 +761,17 @@ extern "C" int aiko_maxpool(const void* x, void* y, int B, int H, int W, int C, 
 
 namespace aiko {
 // Mean over the rows of [B, T, C] bf16 -> [B, C] fp32 (Whisper feature pooling, long T): one
-// 256-thread block per (batch, CL x 8 channels); 256/CL row phases x CL lanes of 8 channels, each
-// lane keeping 4 row loads in flight, then an LDS reduction of the phases in a fixed order.
-// CL = 32 (512 B of each row per block) when B x C/256 blocks fill the chip; CL = 8 (one 128 B
-// line per row) otherwise -- Whisper-small's [16, 1500, 768] gets 192 blocks instead of 48.
-template <int CL>
-__global__ __launch_bounds__(256) void mean_rows_f32_kernel(const bf16_t* __restrict__ x,
-                                                            float* __restrict__ y, int T, int C,
-                                                            long ldb) {
-  constexpr int PH = 256 / CL;
+// NT-thread block per (batch, CL x 8 channels); NT/CL row phases x CL lanes of 8 channels, each
+// lane keeping 4 row loads in flight (guarded, so the tail is batched too), then an LDS reduction
+// of the phases in a fixed order.  CL = 32 (512 B of each row per block) when B x C/256 blocks fill
+// the chip; otherwise CL = 8 (one 128 B line per row) with NT = 1024 — Whisper-small's
+// [14, 1500, 768] is only 168 blocks, so the bytes in flight per block set the pace (256 threads:
+// 58.9 us for 32 MB in the round-5 trace, ~0.55 TB/s).
+template <int CL, int NT>
+__global__ __launch_bounds__(NT) void mean_rows_f32_kernel(const bf16_t* __restrict__ x,
+                                                           float* __restrict__ y, int T, int C,
+                                                           long ldb) {
+  constexpr int PH = NT / CL;
   __shared__ float red[PH][CL][9];
   const int cl = threadIdx.x % CL, ph = threadIdx.x / CL;
   const int C8 = C >> 3;
@@ -778,11 +780,11 @@ __global__ __launch_bounds__(256) void mean_rows_f32_kernel(const bf16_t* __rest
   float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (c8 < C8) {
     const bf16_t* src = x + (long)b * ldb + c8 * 8;      // ldb: batch pitch (rows may be a T-prefix)
-    int i = ph;
-    for (; i + 3 * PH < T; i += 4 * PH) {
+    for (int i = ph; i < T; i += 4 * PH) {
       u32x4 v[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const u32x4*>(src + (long)(i + PH * u) * C);
+      for (int u = 0; u < 4; ++u)
+        v[u] = i + PH * u < T ? *reinterpret_cast<const u32x4*>(src + (long)(i + PH * u) * C) : u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -790,14 +792,6 @@ __global__ __launch_bounds__(256) void mean_rows_f32_kernel(const bf16_t* __rest
           a[2 * e] += __uint_as_float(v[u][e] << 16);
           a[2 * e + 1] += __uint_as_float(v[u][e] & 0xffff0000u);
         }
-    }
-    for (; i < T; i += PH) {
-      const u32x4 v = *reinterpret_cast<const u32x4*>(src + (long)i * C);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        a[2 * e] += __uint_as_float(v[e] << 16);
-        a[2 * e + 1] += __uint_as_float(v[e] & 0xffff0000u);
-      }
     }
   }
 #pragma unroll
@@ -809,7 +803,7 @@ __global__ __launch_bounds__(256) void mean_rows_f32_kernel(const bf16_t* __rest
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float t = 0.f;
-#pragma unroll
+#pragma unroll 8
       for (int q = 0; q < PH; ++q) t += red[q][cl][e];
       o[e] = t * inv;
     }
@@ -839,9 +833,9 @@ extern "C" int aiko_mean_rows_f32(const void* x, float* y, int B, int T, int C, 
   const aiko::bf16_t* xp = static_cast<const aiko::bf16_t*>(x);
   const int C8 = C / 8;
   if ((long)B * ((C8 + 31) / 32) < 256) {
-    aiko::mean_rows_f32_kernel<8><<<dim3((C8 + 7) / 8, B), 256, 0, stream>>>(xp, y, T, C, ldb);
+    aiko::mean_rows_f32_kernel<8, 1024><<<dim3((C8 + 7) / 8, B), 1024, 0, stream>>>(xp, y, T, C, ldb);
   } else {
-    aiko::mean_rows_f32_kernel<32><<<dim3((C8 + 31) / 32, B), 256, 0, stream>>>(xp, y, T, C, ldb);
+    aiko::mean_rows_f32_kernel<32, 256><<<dim3((C8 + 31) / 32, B), 256, 0, stream>>>(xp, y, T, C, ldb);
   }
   return (int)hipGetLastError();
 }
