@@ -482,7 +482,10 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, p
             cands += [t + (8,) for t in WIDE8_TILES] + [t + (9,) for t in WIDE_OCC_TILES]
             if 19 in _EXTRA:
                 cands += [t + (19,) for t in WIDE4_OCC_TILES]
-            if cout <= 2048 and not has_res:
+            # variant 20 wins its layers in isolation but the ResNet bench (two concurrent frame
+            # lanes) runs 1 % faster without it (89.8k vs 90.7k frames/s, 5 + 5 interleaved runs on
+            # two boxes, scripts/r5_skip_ab.sh; YOLO / Whisper unchanged): opt-in, AIKO_CONV_EXTRA=20
+            if cout <= 2048 and not has_res and 20 in _EXTRA:
                 cands += [t + (20,) for t in WIDE_PERS_TILES]
             elif cout <= 2048 and key[2] >= 192 and 20 in _EXTRA:   # with a residual: 3-slot forms
                 cands += [t + (20,) for t in WIDE_PERS_TILES if t != (256, 256)]
