@@ -478,7 +478,11 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, p
         if buf_ok:
             cands += [t + (2,) for t in TILES + BUF_WIDE_TILES] + [t + (3,) for t in BUF_OCC_TILES]
             cands += [t + (4,) for t in PERSIST_TILES]
-            cands += [t + (5,) for t in MF32_TILES]
+            if 5 in _EXTRA:
+                # variant 5 wins some ResNet layers in isolation, but the two-lane bench is ~1 % faster
+                # without it (90.3k vs 91.4k frames/s, 5 + 5 interleaved runs on two boxes,
+                # scripts/r5_skip_ab.sh; YOLO / Whisper never pick it): opt-in, AIKO_CONV_EXTRA=5
+                cands += [t + (5,) for t in MF32_TILES]
             cands += [t + (8,) for t in WIDE8_TILES] + [t + (9,) for t in WIDE_OCC_TILES]
             if 19 in _EXTRA:
                 cands += [t + (19,) for t in WIDE4_OCC_TILES]
