@@ -58,7 +58,7 @@ def test_echo_pipeline_beats_reference(cluster):
     assert res["frames_per_s"] > 50, res      # reference ceiling: 50 frames/s
 
 
-def _snapshot(cluster, service=None, expect=(), timeout=15):
+def _snapshot(cluster, service=None, expect=(), timeout=40):   # generous: returns as soon as seen
     deadline = time.time() + timeout
     out = ""
     while time.time() < deadline:
