@@ -16,6 +16,7 @@ from inspect import getmembers, isfunction
 from ..runtime.actor import Actor
 from ..runtime.context import Interface
 from ..runtime.process import aiko
+from ..message.tensor_payload import encode_message
 from ..utils.sexpr import generate
 from .share import services_cache_create_singleton
 
@@ -86,7 +87,8 @@ def make_proxy_mqtt(target_topic_in, public_method_names):
             parameters = list(args)
             if kwargs:
                 parameters.append(kwargs)
-            aiko.message.publish(target_topic_in, generate(method_name, parameters))
+            # arrays (tensors, ndarrays, DeviceResults) travel as one binary payload
+            aiko.message.publish(target_topic_in, encode_message(method_name, parameters))
         closure.__name__ = method_name
         return closure
 

@@ -252,6 +252,16 @@ static int gen_scalar(Gen *g, PyObject *el, int depth) {
         return _PyUnicodeWriter_WriteStr(&g->w, el);
     }
     if (PyDict_Check(el) || PyList_Check(el) || PyTuple_Check(el)) return gen_expr(g, el, depth + 1, 1);
+    /* arrays never become text (str(tensor) is lossy and unparseable): the caller sends them with
+       message/tensor_payload.py; same rule as sexpr.py _refuse_array */
+    if (!PyLong_Check(el) && !PyFloat_Check(el) &&
+        (PyObject_HasAttrString(el, "__dlpack__") || PyObject_HasAttrString(el, "__array_interface__") ||
+         PyObject_HasAttrString((PyObject *)Py_TYPE(el), "__aiko_device_result__"))) {
+        PyErr_Format(PyExc_TypeError,
+                     "generate(): cannot render %s as an S-expression (use message.tensor_payload.encode_message)",
+                     Py_TYPE(el)->tp_name);
+        return -1;
+    }
     PyObject *s = PyObject_Str(el);
     if (!s) return -1;
     int r = _PyUnicodeWriter_WriteStr(&g->w, s);

@@ -13,7 +13,7 @@ import torch
 from ..pipeline.engine import PipelineElement
 from ..pipeline.stream import StreamEvent
 
-__all__ = ["TensorSource", "TensorAffine", "TensorReduce", "TensorDrop", "FrameStats"]
+__all__ = ["TensorSource", "TensorAffine", "TensorReduce", "TensorDrop", "FrameStats", "TensorEcho"]
 
 
 class _TensorElement(PipelineElement):
@@ -83,3 +83,22 @@ class FrameStats(_TensorElement):
         det[:, 0, 3] = f.mean(dim=(1, 2, 3))
         counts = torch.ones(images.shape[0], dtype=torch.int32, device=images.device)
         return StreamEvent.OKAY, {"detections": det, "counts": counts}
+
+
+class TensorEcho(PipelineElement):
+    """Remote-hop test element: returns its array inputs unchanged plus exact derived values
+    (``x2`` = 2 x, ``u_sum``), on whatever device / container they arrived in (torch tensor or
+    numpy array) — the far end of the binary tensor-payload path (``message/tensor_payload.py``)."""
+    PROTOCOL = "tensor_echo:0"
+
+    def __init__(self, context):
+        context.set_protocol(self.PROTOCOL)
+        context.get_implementation("PipelineElement").__init__(self, context)
+
+    def start_stream(self, stream, stream_id):
+        return StreamEvent.OKAY, None
+
+    def process_frame(self, stream, x, u):
+        device = str(x.device) if isinstance(x, torch.Tensor) else "numpy"
+        return StreamEvent.OKAY, {"x": x, "u": u, "x2": x * 2, "u_sum": int(u.astype("int64").sum()),
+                                  "device_in": device}

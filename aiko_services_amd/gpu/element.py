@@ -119,6 +119,7 @@ class DeviceResult:
     """Tensors produced asynchronously on the GPU plus the event that completes them."""
 
     __slots__ = ("tensors", "event", "t_submit", "t_done", "meta", "__weakref__")
+    __aiko_device_result__ = True       # message/tensor_payload.py: sent as its tensors, re-wrapped
 
     def __init__(self, tensors: dict, event: torch.cuda.Event | None, t_submit: float | None = None, meta=None):
         self.tensors = tensors

@@ -20,6 +20,7 @@ from ..utils import fault as _fault
 from ..utils.configuration import get_mqtt_configuration
 from . import mqtt_codec as C
 from .mqtt_client import MQTTClient, MQTTMessage
+from .websocket import is_websocket_transport
 
 __all__ = ["Message", "Castaway", "Loopback", "LoopbackBus", "MQTT"]
 
@@ -170,6 +171,10 @@ class MQTT(Message):
         self._subscribed: set = set()
         (server_up, self.host, self.port, self.transport, self.username, self.password,
          self.tls) = get_mqtt_configuration()
+        # AIKO_MQTT_TRANSPORT: "tcp" or "websockets" (reference main/message/mqtt.py:87,108); an
+        # unknown value raises here instead of silently trying plain TCP
+        self.websockets = is_websocket_transport(self.transport)
+        self.ws_path = os.environ.get("AIKO_MQTT_WS_PATH", "/mqtt")
         if not server_up:
             raise SystemError(f"Couldn't connect to MQTT server {self.host}:{self.port}")
         self.client = None
@@ -183,7 +188,8 @@ class MQTT(Message):
             client.will_set(self.lwt[0], self.lwt[1], self.lwt[2])
         try:
             client.connect(self.host, self.port, keepalive=int(os.environ.get("AIKO_MQTT_KEEPALIVE", 60)),
-                           username=self.username, password=self.password, tls=self.tls)
+                           username=self.username, password=self.password, tls=self.tls,
+                           transport="websockets" if self.websockets else "tcp", ws_path=self.ws_path)
         except (OSError, ConnectionError) as exc:
             raise SystemError(f"Couldn't connect to MQTT server {self.host}:{self.port}: {exc}")
         self.client = client

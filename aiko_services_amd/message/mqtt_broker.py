@@ -7,7 +7,11 @@ duplicate client id.  Messages are routed with one trie lookup per publish and q
 per-connection output buffers flushed when writable, so one slow subscriber never blocks the
 broker loop.
 
-Run standalone:  ``python -m aiko_services_amd.message.mqtt_broker --port 1883``
+A second listener (``ws_port``) speaks MQTT over WebSockets (RFC 6455, subprotocol ``mqtt``,
+``message/websocket.py``): the HTTP Upgrade and the frame layer sit between the socket and the
+same packet reader / output buffer, so TCP and WebSocket clients share one topic space.
+
+Run standalone:  ``python -m aiko_services_amd.message.mqtt_broker --port 1883 [--ws-port 9001]``
 """
 from __future__ import annotations
 
@@ -20,15 +24,16 @@ import threading
 import time
 
 from . import mqtt_codec as C
+from .websocket import ServerSession
 
 __all__ = ["Broker", "start_broker_thread"]
 
 
 class _Conn:
     __slots__ = ("sock", "reader", "out", "client_id", "will", "keepalive", "last_rx",
-                 "connected", "subs", "closing", "pid")
+                 "connected", "subs", "closing", "pid", "ws")
 
-    def __init__(self, sock):
+    def __init__(self, sock, ws=None):
         self.sock = sock
         self.reader = C.PacketReader()
         self.out = bytearray()
@@ -40,12 +45,15 @@ class _Conn:
         self.subs: dict = {}
         self.closing = False
         self.pid = itertools.count(1)
+        self.ws = ws                     # websocket.ServerSession (WebSocket listener) or None
 
 
 class Broker:
-    def __init__(self, host: str = "127.0.0.1", port: int = 1883):
+    def __init__(self, host: str = "127.0.0.1", port: int = 1883, ws_port: int | None = None):
         self.host = host
         self.port = port
+        self.ws_port = ws_port           # None: no WebSocket listener; 0: any free port
+        self.ws_lsock: socket.socket | None = None
         self.sel = selectors.DefaultSelector()
         self.lsock: socket.socket | None = None
         self.conns: dict = {}            # sock -> _Conn
@@ -57,15 +65,24 @@ class Broker:
         self.stats = {"published": 0, "delivered": 0, "connections": 0}
 
     # ---- lifecycle -------------------------------------------------------------------------
-    def bind(self):
+    def _listen(self, port):
         s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
         s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
-        s.bind((self.host, self.port))
+        s.bind((self.host, port))
         s.listen(256)
         s.setblocking(False)
+        return s
+
+    def bind(self):
+        s = self._listen(self.port)
         self.port = s.getsockname()[1]
         self.lsock = s
         self.sel.register(s, selectors.EVENT_READ, "listen")
+        if self.ws_port is not None:
+            w = self._listen(self.ws_port)
+            self.ws_port = w.getsockname()[1]
+            self.ws_lsock = w
+            self.sel.register(w, selectors.EVENT_READ, "listen_ws")
         self._wake_r.setblocking(False)
         self.sel.register(self._wake_r, selectors.EVENT_READ, "wake")
         return self.port
@@ -87,6 +104,8 @@ class Broker:
                 for key, mask in self.sel.select(timeout=1.0):
                     if key.data == "listen":
                         self._accept()
+                    elif key.data == "listen_ws":
+                        self._accept(websocket=True)
                     elif key.data == "wake":
                         try:
                             self._wake_r.recv(4096)
@@ -108,16 +127,18 @@ class Broker:
             self.sel.close()
             if self.lsock:
                 self.lsock.close()
+            if self.ws_lsock:
+                self.ws_lsock.close()
 
     # ---- connection handling ----------------------------------------------------------------
-    def _accept(self):
+    def _accept(self, websocket=False):
         try:
-            sock, _ = self.lsock.accept()
+            sock, _ = (self.ws_lsock if websocket else self.lsock).accept()
         except OSError:
             return
         sock.setblocking(False)
         sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-        conn = _Conn(sock)
+        conn = _Conn(sock, ServerSession() if websocket else None)
         self.conns[sock] = conn
         self.sel.register(sock, selectors.EVENT_READ, conn)
         self.stats["connections"] += 1
@@ -142,9 +163,11 @@ class Broker:
         except OSError:
             pass
 
-    def _send(self, conn: _Conn, data: bytes):
+    def _send(self, conn: _Conn, data: bytes, raw: bool = False):
         if conn.closing:
             return
+        if conn.ws is not None and not raw:
+            data = conn.ws.wrap(data)                    # one binary frame per MQTT packet
         was_empty = not conn.out
         conn.out += data
         if was_empty:
@@ -177,6 +200,16 @@ class Broker:
             self._close(conn, send_will=True)
             return
         conn.last_rx = time.monotonic()
+        if conn.ws is not None:
+            data, reply, close = conn.ws.feed(data)      # handshake / frames -> MQTT bytes
+            if reply:
+                self._send(conn, reply, raw=True)
+            if close:
+                self._flush(conn)
+                self._close(conn, send_will=not conn.ws.closed)
+                return
+            if not data:
+                return
         conn.reader.feed(data)
         try:
             for ptype, flags, body in conn.reader.packets():
@@ -274,9 +307,10 @@ class Broker:
         self._send(conn, C.publish_packet(topic, payload, qos, retain, pid))
 
 
-def start_broker_thread(host="127.0.0.1", port=0):
-    """Start a broker on a background thread; returns (broker, port)."""
-    broker = Broker(host, port)
+def start_broker_thread(host="127.0.0.1", port=0, ws_port=None):
+    """Start a broker on a background thread; returns (broker, port) (``broker.ws_port``: the
+    WebSocket listener's port when ``ws_port`` is not None)."""
+    broker = Broker(host, port, ws_port)
     port = broker.bind()
     t = threading.Thread(target=broker.serve_forever, name="aiko-mqtt-broker", daemon=True)
     t.start()
@@ -287,10 +321,12 @@ def main(argv=None):
     ap = argparse.ArgumentParser(description="aiko MQTT 3.1.1 broker")
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=1883)
+    ap.add_argument("--ws-port", type=int, default=None, help="also accept MQTT over WebSockets here")
     a = ap.parse_args(argv)
-    b = Broker(a.host, a.port)
+    b = Broker(a.host, a.port, a.ws_port)
     port = b.bind()
-    print(f"aiko MQTT broker listening on {a.host}:{port}", flush=True)
+    ws = f", websockets on {b.ws_port}" if b.ws_port is not None else ""
+    print(f"aiko MQTT broker listening on {a.host}:{port}{ws}", flush=True)
     try:
         b.serve_forever()
     except KeyboardInterrupt:

@@ -5,7 +5,8 @@ message)`` with a paho-compatible ``message`` (``.topic`` str, ``.payload`` byte
 ``.retain``, ``.qos``).  ``publish`` writes directly from the caller's thread under a lock
 (TCP_NODELAY, no busy-wait), ``connect`` waits on a condition for CONNACK instead of the
 reference's 2000 x 1 ms polling loop (``message/mqtt.py:255-289``).  Keep-alive PINGREQs are
-sent by the network thread.  TLS is supported via ``ssl`` when requested.
+sent by the network thread.  TLS is supported via ``ssl`` when requested, and MQTT over
+WebSockets (``transport="websockets"``, ``message/websocket.py``) like paho's transport option.
 """
 from __future__ import annotations
 
@@ -19,6 +20,7 @@ import uuid
 from dataclasses import dataclass
 
 from . import mqtt_codec as C
+from .websocket import client_connect, is_websocket_transport
 
 __all__ = ["MQTTClient", "MQTTMessage"]
 
@@ -58,13 +60,22 @@ class MQTTClient:
         self.will = (topic, payload, retain, qos)
 
     def connect(self, host="127.0.0.1", port=1883, keepalive=60, username=None, password=None,
-                tls=False, timeout=5.0):
+                tls=False, timeout=5.0, transport="tcp", ws_path="/mqtt"):
+        """``transport``: ``tcp`` or ``websockets`` (RFC 6455 Upgrade on ``ws_path``,
+        subprotocol ``mqtt``; over TLS when ``tls``); any other value raises ``ValueError``."""
+        websockets = is_websocket_transport(transport)
         self.host, self.port, self.keepalive = host, port, keepalive
         sock = socket.create_connection((host, port), timeout=timeout)
         sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
         if tls:
             ctx = ssl.create_default_context()
             sock = ctx.wrap_socket(sock, server_hostname=host)
+        if websockets:
+            try:
+                sock = client_connect(sock, host, port, ws_path)
+            except (OSError, ConnectionError):
+                sock.close()
+                raise
         sock.settimeout(None)
         self.sock = sock
         self._stop = False

@@ -43,6 +43,7 @@ from ..utils import trace as _trace
 from ..utils.configuration import get_gpu_configuration
 from ..utils.graph import Graph, Node
 from ..utils.misc import load_module
+from ..message.tensor_payload import encode_message
 from ..utils.sexpr import generate, parse
 from .definition import (PipelineDefinition, PipelineElementDeployLocal, PipelineElementDeployRemote,
                          parse_pipeline_definition)
@@ -1111,7 +1112,7 @@ class PipelineImpl(Pipeline):
                             stream_info["hop_rank"] = hop.rank     # the responder (proof of life)
                         get_actor_mqtt(topic, Pipeline).process_frame_response(stream_info, frame_data_out)
                 else:
-                    aiko.message.publish(self.topic_out, generate("process_frame", (stream_info, frame_data_out)))
+                    aiko.message.publish(self.topic_out, encode_message("process_frame", (stream_info, frame_data_out)))
         finally:
             if frame_complete:
                 self._release_frame(stream, frame_id)

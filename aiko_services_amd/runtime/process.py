@@ -24,6 +24,7 @@ from ..message.mqtt_codec import TopicTrie
 from ..utils.configuration import get_hostname, get_namespace, get_pid, get_username
 from ..utils.logger import DEBUG, LoggingHandlerMQTT, get_logger
 from ..utils.misc import ContextManager, Lock
+from ..message.tensor_payload import encode_message, is_tensor_payload
 from ..utils.sexpr import generate, parse
 from . import event
 from .connection import Connection, ConnectionState
@@ -194,7 +195,8 @@ class ProcessImplementation(ProcessData):
         for t in self.topic_matcher(topic):
             handlers.extend(self._message_handlers.get(t, ()))
             binary = binary or t in self._binary_topics
-        if not binary and isinstance(payload, (bytes, bytearray)):
+        if not binary and isinstance(payload, (bytes, bytearray)) and not is_tensor_payload(payload):
+            # (a tensor payload stays bytes: parse() decodes it, arrays included)
             try:
                 payload = payload.decode("utf-8")
             except UnicodeDecodeError:
@@ -294,4 +296,4 @@ def process_create():
 
 def publish_generate(topic, command, parameters, retain=False):
     """Convenience: publish ``generate(command, parameters)`` on ``topic``."""
-    aiko.message.publish(topic, generate(command, parameters), retain=retain)
+    aiko.message.publish(topic, encode_message(command, parameters), retain=retain)

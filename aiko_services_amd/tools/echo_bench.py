@@ -79,7 +79,7 @@ def _parent(frames: int, window: int, timeout: float, definition: str | None = N
 
 
 def orchestrate(frames=2000, window=8, timeout=60.0, broker_port=None, parent=None, children=None,
-                expect=3):
+                expect=3, extra_env=None):
     """Registrar + child pipeline processes + a parent driving ``frames`` through the chain."""
     from aiko_services_amd.message.mqtt_broker import start_broker_thread
     broker = None
@@ -90,6 +90,7 @@ def orchestrate(frames=2000, window=8, timeout=60.0, broker_port=None, parent=No
                 "AIKO_NAMESPACE": f"echo{uuid.uuid4().hex[:6]}", "AIKO_LOG_MQTT": "false",
                 "AIKO_LOG_LEVEL": "WARNING", "AIKO_REGISTRAR_SEARCH_TIMEOUT": "0.3",
                 "AIKO_MQTT_DISABLE": "0", "PYTHONPATH": str(DEFS.parents[3]) + os.pathsep + env.get("PYTHONPATH", "")})
+    env.update(extra_env or {})          # e.g. AIKO_MQTT_TRANSPORT=websockets
     procs = []
     try:
         procs.append(subprocess.Popen([sys.executable, "-m", "aiko_services_amd.tools.registrar"], env=env))

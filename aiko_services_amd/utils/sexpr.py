@@ -34,6 +34,7 @@ __all__ = ["generate", "parse", "parse_float", "parse_int", "parse_number",
            "generate_s_expression", "parse_list_to_dict"]
 
 _WS = " \t\n\r"
+_TENSOR_MAGIC = b"\x00AIKO-TP1\n"          # message/tensor_payload.py MAGIC
 _DELIMS = set(" \t\n\r()")
 
 
@@ -79,9 +80,21 @@ def _gen(expr, parts: list) -> None:
             _gen(_dict_to_list(el), parts)
         elif isinstance(el, (list, tuple)):
             _gen(el, parts)
+        elif isinstance(el, (int, float)):
+            parts.append(str(el))
         else:
+            _refuse_array(el)
             parts.append(str(el))
     parts.append(")")
+
+
+def _refuse_array(el) -> None:
+    """Arrays never become text: ``str(tensor)`` is lossy and unparseable (send them with
+    ``message.tensor_payload.encode_message``)."""
+    if hasattr(el, "__dlpack__") or hasattr(el, "__array_interface__") \
+            or getattr(type(el), "__aiko_device_result__", False):
+        raise TypeError(f"generate(): cannot render {type(el).__name__} as an S-expression "
+                        "(use message.tensor_payload.encode_message)")
 
 
 def generate_s_expression(expression) -> str:
@@ -184,8 +197,11 @@ class _Scanner:
 
 def parse(payload, dictionaries_flag: bool = True):
     """``"(cmd a (b c) k: v)"`` -> ``("cmd", ["a", ["b", "c"], ...])``."""
-    if isinstance(payload, (bytes, bytearray)):
-        payload = payload.decode("utf-8")
+    if isinstance(payload, (bytes, bytearray, memoryview)):
+        if bytes(payload[:len(_TENSOR_MAGIC)]) == _TENSOR_MAGIC:
+            from ..message.tensor_payload import decode_message
+            return decode_message(payload)          # binary message with arrays (tensor_payload)
+        payload = bytes(payload).decode("utf-8")
     result = _native.scan(payload) if _native is not None else _Scanner(payload).parse_list()
     car, cdr = "", []
     if result:

@@ -162,3 +162,58 @@ def test_transport_reconnects_after_broker_loss(monkeypatch):
             b2.stop()
     finally:
         t.terminate()
+
+
+def test_websocket_clients_share_topics_with_tcp():
+    """MQTT over WebSockets: a WS subscriber and a TCP publisher (and the reverse) on one broker;
+    retained messages, QoS 1 and a 1 MB payload cross the frame layer."""
+    b, port = start_broker_thread("127.0.0.1", 0, ws_port=0)
+    try:
+        ws_sub, q_ws = _client(b.ws_port)
+        ws_sub.connect("127.0.0.1", b.ws_port, transport="websockets")
+        tcp_sub, q_tcp = _client(port)
+        tcp_sub.connect("127.0.0.1", port)
+        ws_sub.subscribe("t/#")
+        tcp_sub.subscribe("w/#")
+        pub, _ = _client(port)
+        pub.connect("127.0.0.1", port)
+        big = bytes(range(256)) * 4096
+        pub.publish("t/a", b"hello", qos=1, wait=True)
+        pub.publish("t/big", big)
+        assert q_ws.get(timeout=5)[:2] == ("t/a", b"hello")
+        assert q_ws.get(timeout=5)[:2] == ("t/big", big)
+        ws_sub.publish("w/x", b"from-ws", qos=1, wait=True)
+        assert q_tcp.get(timeout=5)[:2] == ("w/x", b"from-ws")
+        pub.publish("t/keep", b"kept", retain=True)
+        late, q_late = _client(b.ws_port)
+        late.connect("127.0.0.1", b.ws_port, transport="websockets")
+        late.subscribe("t/keep")
+        assert q_late.get(timeout=5) == ("t/keep", b"kept", True)
+        for c in (ws_sub, tcp_sub, pub, late):
+            c.disconnect()
+    finally:
+        b.stop()
+
+
+def test_websocket_lwt_and_unknown_transport(monkeypatch):
+    b, port = start_broker_thread("127.0.0.1", 0, ws_port=0)
+    try:
+        watcher, q = _client(port)
+        watcher.connect("127.0.0.1", port)
+        watcher.subscribe("lwt/#")
+        c, _ = _client(b.ws_port)
+        c.will_set("lwt/ws", b"(absent)")
+        c.connect("127.0.0.1", b.ws_port, transport="websockets")
+        c.sock.sock.close()                       # abnormal: no DISCONNECT, no close frame
+        assert q.get(timeout=5)[:2] == ("lwt/ws", b"(absent)")
+        watcher.disconnect()
+        from aiko_services_amd.message.message import MQTT
+        monkeypatch.setenv("AIKO_MQTT_HOST", "127.0.0.1")
+        monkeypatch.setenv("AIKO_MQTT_PORT", str(port))
+        monkeypatch.setenv("AIKO_MQTT_TRANSPORT", "quic")
+        with pytest.raises(ValueError):
+            MQTT(message_handler=lambda *a: None)
+        with pytest.raises(ValueError):
+            MQTTClient().connect("127.0.0.1", port, transport="udp")
+    finally:
+        b.stop()

@@ -91,3 +91,71 @@ def test_topic_filters_4_7(filt, topic, match):
     trie = C.TopicTrie()
     trie.add(filt, "sub", 0)
     assert (len(trie.match(topic)) > 0) is match
+
+
+# ---- MQTT over WebSockets (RFC 6455): byte-exact handshake and frame vectors -------------------
+from aiko_services_amd.message import websocket as WS  # noqa: E402
+
+
+def test_ws_accept_key_rfc6455_1_3():
+    # the worked example of RFC 6455 section 1.3
+    assert WS.accept_key("dGhlIHNhbXBsZSBub25jZQ==") == "s3pPLMBiTxaQ9kYGzzhZRbK+xOo="
+
+
+def test_ws_handshake_bytes():
+    req = WS.client_request("broker", 9001, "/mqtt", "dGhlIHNhbXBsZSBub25jZQ==")
+    assert req == (b"GET /mqtt HTTP/1.1\r\nHost: broker:9001\r\nUpgrade: websocket\r\n"
+                   b"Connection: Upgrade\r\nSec-WebSocket-Key: dGhlIHNhbXBsZSBub25jZQ==\r\n"
+                   b"Sec-WebSocket-Version: 13\r\nSec-WebSocket-Protocol: mqtt\r\n\r\n")
+    assert WS.server_response("dGhlIHNhbXBsZSBub25jZQ==") == (
+        b"HTTP/1.1 101 Switching Protocols\r\nUpgrade: websocket\r\nConnection: Upgrade\r\n"
+        b"Sec-WebSocket-Accept: s3pPLMBiTxaQ9kYGzzhZRbK+xOo=\r\nSec-WebSocket-Protocol: mqtt\r\n\r\n")
+    # the broker side answers a client request with exactly that response
+    s = WS.ServerSession()
+    app, reply, close = s.feed(req)
+    assert (app, close) == (b"", False) and reply == WS.server_response("dGhlIHNhbXBsZSBub25jZQ==")
+
+
+KEY = bytes([0x37, 0xFA, 0x21, 0x3D])
+
+
+def test_ws_frames_rfc6455_5_7():
+    # single-frame unmasked text "Hello"
+    assert WS.encode_frame(b"Hello", WS.OP_TEXT) == bytes([0x81, 0x05, 0x48, 0x65, 0x6C, 0x6C, 0x6F])
+    # single-frame masked text "Hello"
+    masked = bytes([0x81, 0x85, 0x37, 0xFA, 0x21, 0x3D, 0x7F, 0x9F, 0x4D, 0x51, 0x58])
+    assert WS.encode_frame(b"Hello", WS.OP_TEXT, KEY) == masked
+    assert WS.FrameDecoder(require_mask=True).feed(masked) == [(WS.OP_TEXT, b"Hello")]
+    # fragmented unmasked text: "Hel" + "lo"
+    frag = bytes([0x01, 0x03, 0x48, 0x65, 0x6C, 0x80, 0x02, 0x6C, 0x6F])
+    assert WS.encode_frame(b"Hel", WS.OP_TEXT, fin=False) + WS.encode_frame(b"lo", WS.OP_CONT) == frag
+    assert WS.FrameDecoder(require_mask=False).feed(frag) == [(WS.OP_TEXT, b"Hello")]
+    # unmasked ping / masked pong
+    assert WS.encode_frame(b"Hello", WS.OP_PING) == bytes([0x89, 0x05]) + b"Hello"
+    assert WS.encode_frame(b"Hello", WS.OP_PONG, KEY) == bytes([0x8A, 0x85, 0x37, 0xFA, 0x21, 0x3D,
+                                                                 0x7F, 0x9F, 0x4D, 0x51, 0x58])
+    # 256 bytes (16-bit length) and 64 KiB (64-bit length) unmasked binary
+    assert WS.encode_frame(bytes(256))[:4] == bytes([0x82, 0x7E, 0x01, 0x00])
+    assert WS.encode_frame(bytes(65536))[:10] == bytes([0x82, 0x7F, 0, 0, 0, 0, 0, 1, 0, 0])
+
+
+def test_ws_decoder_incremental_and_rules():
+    import pytest as _pytest
+    blob = bytes(range(256)) * 300
+    frame = WS.encode_frame(blob, WS.OP_BINARY, KEY)
+    d = WS.FrameDecoder(require_mask=True)
+    got = []
+    for i in range(0, len(frame), 7):                     # byte-dribbled
+        got += d.feed(frame[i:i + 7])
+    assert got == [(WS.OP_BINARY, blob)]
+    with _pytest.raises(ValueError):                      # client frames must be masked
+        WS.FrameDecoder(require_mask=True).feed(WS.encode_frame(b"x"))
+    with _pytest.raises(ValueError):                      # server frames must not be
+        WS.FrameDecoder(require_mask=False).feed(WS.encode_frame(b"x", WS.OP_BINARY, KEY))
+
+
+def test_ws_transport_names():
+    import pytest as _pytest
+    assert WS.is_websocket_transport("websockets") and not WS.is_websocket_transport("tcp")
+    with _pytest.raises(ValueError):
+        WS.is_websocket_transport("carrier-pigeon")

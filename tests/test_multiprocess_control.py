@@ -127,3 +127,27 @@ def test_multitude_chain_three_processes():
     res = run(processes=3, elements=2, frames=100, window=4, timeout=60)
     assert "error" not in res, res
     assert res["frames"] == 100 and res["frames_per_s"] > 50
+
+
+def test_tensor_payload_through_plain_remote(cluster):
+    """A float32 [4, 3, 224, 224] tensor and a uint8 ndarray cross a plain ``deploy.remote``
+    hop (registrar-discovered child, no ``parallel`` block) and come back bit-exact."""
+    from aiko_services_amd.tools.tensor_echo import orchestrate
+    res = orchestrate(frames=3, device="cpu", timeout=60, broker_port=cluster["port"])
+    assert "error" not in res, res
+    assert res["frames"] == 3 and res["mismatches"] == [], res
+    assert res["device_in"] == "cpu"
+
+
+def test_echo_pipeline_over_websockets():
+    """Config 1 (two-process echo pipeline + registrar) with every process on MQTT over
+    WebSockets (AIKO_MQTT_TRANSPORT=websockets; reference main/message/mqtt.py:87,108)."""
+    from aiko_services_amd.tools.echo_bench import orchestrate
+    broker, _port = start_broker_thread("127.0.0.1", 0, ws_port=0)
+    try:
+        res = orchestrate(frames=200, window=4, timeout=40, broker_port=broker.ws_port,
+                          extra_env={"AIKO_MQTT_TRANSPORT": "websockets"})
+    finally:
+        broker.stop()
+    assert "error" not in res, res
+    assert res["frames"] == 200 and res["frames_per_s"] > 50, res
