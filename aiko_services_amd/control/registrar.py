@@ -10,6 +10,9 @@ and sets its last will to ``(primary absent)`` there, so every process learns of
   then ``(sync response_topic)`` on ``{registrar}/out``
 * ``(history response_topic count|*)`` -> removed services, most recent first
 
+Split brain (two primaries, e.g. started together or after a partition): the oldest
+``time_started`` wins, the other demotes itself to secondary (``_resolve_split_brain``).
+
 Process failure: the broker delivers a process's LWT ``(absent)`` on ``{ns}/+/+/+/state``
 and every service of that process is removed.  Fixes vs the reference: an explicit
 ``(remove topic)`` of a single service works (the reference iterated the topic string), and the
@@ -53,6 +56,7 @@ class StateMachineModel:
         {"source": "primary", "trigger": "primary_failed", "dest": "primary_search"},
         {"source": "secondary", "trigger": "primary_failed", "dest": "primary_search"},
         {"source": "secondary", "trigger": "primary_promotion", "dest": "primary"},
+        {"source": "primary", "trigger": "primary_demotion", "dest": "secondary"},
     ]
 
     def __init__(self, service):
@@ -76,8 +80,7 @@ class StateMachineModel:
         # clear the retained boot message, install our LWT, announce ourselves (retained)
         aiko.message.publish(aiko.TOPIC_REGISTRAR_BOOT, "", retain=True)
         aiko.process.set_last_will_and_testament(aiko.TOPIC_REGISTRAR_BOOT, "(primary absent)", True)
-        payload = f"(primary found {self.service.topic_path} {_VERSION} {self.service.time_started})"
-        aiko.message.publish(aiko.TOPIC_REGISTRAR_BOOT, payload, retain=True)
+        self.service.announce()
 
 
 class Registrar(Service):
@@ -110,13 +113,19 @@ class RegistrarImpl(Registrar):
             except ValueError:
                 pass
 
+    def announce(self):
+        payload = f"(primary found {self.topic_path} {_VERSION} {self.time_started})"
+        aiko.message.publish(aiko.TOPIC_REGISTRAR_BOOT, payload, retain=True)
+
     def _registrar_handler(self, action, registrar):
         state = self.state_machine.get_state()
         if action == "found":
+            if registrar and registrar.get("topic_path") == self.topic_path:
+                return
             if state == "primary_search":
-                if registrar and registrar.get("topic_path") == self.topic_path:
-                    return
                 self.state_machine.transition("primary_found", None)
+            elif state == "primary":
+                self._resolve_split_brain(registrar or {})
         elif action == "absent":
             if state == "primary_search":
                 self.state_machine.transition("primary_promotion", None)
@@ -124,6 +133,23 @@ class RegistrarImpl(Registrar):
                 self.services = Services()
                 self.ec_producer.update("service_count", 0)
                 self.state_machine.transition("primary_failed", None)
+
+    def _resolve_split_brain(self, other):
+        """Another registrar announced itself while this one is primary (two promoted at once,
+        or a partition healed; the reference ignores it, main/registrar.py:139-188): the OLDEST
+        (time_started, then topic path) stays primary.  The loser becomes secondary and gives
+        back the "(primary absent)" will (its death must not unseat the winner); the winner
+        re-announces, so the retained boot message and every process's registrar end up on it."""
+        try:
+            theirs = (float(other.get("timestamp")), str(other.get("topic_path")))
+        except (TypeError, ValueError):
+            return
+        if theirs < (float(self.time_started), self.topic_path):
+            _LOGGER.info(f"Registrar {theirs[1]} is older: demoted to secondary")
+            self.state_machine.transition("primary_demotion", None)
+            aiko.process.set_last_will_and_testament(aiko.topic_lwt, aiko.payload_lwt, False)
+        else:
+            self.announce()
 
     def _service_state_handler(self, _aiko, topic, payload_in):
         command, _ = parse(payload_in)
@@ -207,3 +233,4 @@ def main(argv=None):
 
 if __name__ == "__main__":
     main()
+

@@ -180,9 +180,17 @@ class MQTT(Message):
         self.client = None
         self._terminating = False
         self.reconnects = 0
+        self._conn_lock = threading.RLock()   # one live connection: connect / swap / reconnect serialised
         self._connect()
 
     def _connect(self):
+        with self._conn_lock:
+            self._connect_locked()
+
+    def _connect_locked(self):
+        previous = self.client
+        if previous is not None and previous.is_connected():
+            previous.disconnect()              # never two live connections (double delivery)
         client = MQTTClient(on_message=self._on_message, on_disconnect=self._on_disconnect)
         if self.lwt:
             client.will_set(self.lwt[0], self.lwt[1], self.lwt[2])
@@ -206,21 +214,27 @@ class MQTT(Message):
         and replay every subscription (the reference left this as a TODO)."""
         if rc == 0 or self._terminating or client is not self.client:
             return
-        threading.Thread(target=self._reconnect_loop, name="aiko-mqtt-reconnect", daemon=True).start()
+        threading.Thread(target=self._reconnect_loop, args=(client,), name="aiko-mqtt-reconnect",
+                         daemon=True).start()
 
-    def _reconnect_loop(self):
+    def _reconnect_loop(self, lost):
         delay = 0.2
         while not self._terminating:
             time.sleep(delay)
-            try:
-                self._connect()
-                self.reconnects += 1
-                return
-            except SystemError:
-                delay = min(delay * 2, 5.0)
+            with self._conn_lock:
+                if self.client is not lost:        # replaced meanwhile (will swap, another loop)
+                    return
+                try:
+                    self._connect_locked()
+                    self.reconnects += 1
+                    return
+                except SystemError:
+                    delay = min(delay * 2, 5.0)
 
     def _on_message(self, client, userdata, message):
-        if self.message_handler:
+        # only the current connection delivers: a replaced one that the broker has not yet
+        # dropped must not hand the process a second copy of every message
+        if self.message_handler and client is self.client:
             self.message_handler(client, userdata, message)
 
     def is_connected(self):
@@ -259,10 +273,11 @@ class MQTT(Message):
     def set_last_will_and_testament(self, topic_lwt, payload_lwt="(absent)", retain_lwt=False):
         """MQTT fixes the will at CONNECT: reconnect with the new one (as the reference does)."""
         self.lwt = (topic_lwt, payload_lwt, retain_lwt)
-        old = self.client
-        if old is not None:
-            old.disconnect()
-        self._connect()
+        with self._conn_lock:
+            old = self.client
+            if old is not None:
+                old.disconnect()
+            self._connect_locked()
 
     def terminate(self):
         self._terminating = True

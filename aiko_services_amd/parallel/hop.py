@@ -49,6 +49,8 @@ tokens and are rebuilt (with a completion event) on the receiver.
 from __future__ import annotations
 
 import datetime
+import os
+import time
 import weakref
 from collections import deque
 
@@ -341,6 +343,14 @@ class HopPlane:
         self.links = [tuple(int(x) for x in l) for l in links]
         self.dead: set = set()
         self.suspect: set = set()          # alive but unresponsive peers (see suspend)
+        self._suspect_since: dict = {}     # rank -> monotonic time of suspension / last probe
+        self._probes: dict = {}            # rank -> probe frames sent while suspect
+        self._probe_inflight: set = set()  # suspect ranks with a probe frame outstanding
+        # a suspension is bounded: after probe_after_s one PROBE frame is admitted (a peer that
+        # owes nothing would otherwise never be heard from again); after max_probes unanswered
+        # probes suspend() asks the caller to retire the peer (mark_dead -> supervised restart)
+        self.probe_after_s = float(os.environ.get("AIKO_HOP_PROBE_S", 30.0))
+        self.max_probes = int(os.environ.get("AIKO_HOP_MAX_PROBES", 2))
         self._held: dict = {}              # frame / group key -> record (see _encode_many)
         self._loop: deque = deque()        # loopback link (src == dst): staged buffers in order
         self._groups: dict = {}            # (src, dst) -> process group
@@ -354,7 +364,7 @@ class HopPlane:
         self.counters = {"sent_msgs": 0, "sent_bytes": 0, "recv_msgs": 0, "recv_bytes": 0,
                          "pool_overflow": 0, "pool_waits": 0, "resent": 0, "dead_peers": 0, "zero_copy": 0,
                          "readmitted": 0, "dropped_inflight": 0, "dropped_completed": 0,
-                         "suspended": 0}
+                         "suspended": 0, "probes": 0, "escalated": 0}
         self._dropped: list = []           # Dropped transfers still in flight (see drop)
         if rejoin is not None:
             for src, dst in self.links:
@@ -493,21 +503,55 @@ class HopPlane:
         """Frames that may still be sent toward ``dst`` before one is acknowledged."""
         dst = int(dst)
         link = self.send_links.get(dst)
-        return 0 if link is None or dst in self.suspect else link.credit()
+        if link is None:
+            return 0
+        if dst in self.suspect:
+            return min(1, link.credit()) if self._probe_due(dst) else 0
+        return link.credit()
 
-    def suspend(self, rank: int) -> None:
+    def _probe_due(self, rank: int) -> bool:
+        return rank not in self._probe_inflight and \
+            time.monotonic() - self._suspect_since.get(rank, 0.0) >= self.probe_after_s
+
+    def suspend(self, rank: int) -> bool:
         """A hop to ``rank`` timed out although the peer is not known dead (stopped, hung,
         overloaded): it gets no credit — no new frames — until it shows life again: a message
-        from it arrives (:meth:`mark_alive`) or it is re-admitted."""
+        from it arrives (:meth:`mark_alive`) or it is re-admitted.  The suspension is bounded:
+        every ``probe_after_s`` one probe frame is let through (:meth:`credit`); returns True
+        when ``max_probes`` probes went unanswered — the caller then retires the peer."""
         rank = int(rank)
-        if rank != self.rank and rank not in self.dead and rank not in self.suspect:
+        if rank == self.rank or rank in self.dead:
+            return False
+        if rank not in self.suspect:
             self.suspect.add(rank)
+            self._suspect_since[rank] = time.monotonic()
+            self._probes[rank] = 0
             self.counters["suspended"] += 1
+            return False
+        if rank in self._probe_inflight:          # the probe timed out too
+            self._probe_inflight.discard(rank)
+            self._suspect_since[rank] = time.monotonic()
+            if self._probes.get(rank, 0) >= self.max_probes:
+                self.counters["escalated"] += 1
+                return True
+        return False
+
+    def _note_send(self, dst: int) -> None:
+        """A frame (or group) is leaving toward ``dst``: while ``dst`` is suspect it is a probe."""
+        if dst in self.suspect and dst not in self._probe_inflight:
+            self._probe_inflight.add(dst)
+            self._probes[dst] = self._probes.get(dst, 0) + 1
+            self._suspect_since[dst] = time.monotonic()
+            self.counters["probes"] += 1
 
     def mark_alive(self, rank: int) -> None:
         """``rank`` sent something (a message, a response): it is not stuck."""
         if self.suspect:
-            self.suspect.discard(int(rank))
+            rank = int(rank)
+            self.suspect.discard(rank)
+            self._probe_inflight.discard(rank)
+            self._suspect_since.pop(rank, None)
+            self._probes.pop(rank, None)
 
     _alive = mark_alive
 
@@ -710,6 +754,7 @@ class HopPlane:
                 # a plan link that is not up (yet): a restarted rank before its rejoin finished
                 raise StageFailure(dst, "link not connected")
             raise RuntimeError(f"hop: no send link {self.rank} -> {dst} in this plan")
+        self._note_send(dst)
         tensors = []
         events = list(ready or ())
 
@@ -815,6 +860,7 @@ class HopPlane:
         link = self.send_links.get(dst)
         if link is None:
             raise StageFailure(dst) if dst in self.dead else RuntimeError(f"hop: no send link to {dst}")
+        self._note_send(dst)
         old_dst, old_slot, total, specs, templates, buf = rec[:6]
         old = self.send_links.get(old_dst)
         if old is not None and not old.dead and old_slot is not None:

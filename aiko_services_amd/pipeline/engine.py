@@ -356,6 +356,7 @@ class PipelineImpl(Pipeline):
         self._pending_hops: dict = {}      # remote node name -> FIFO of frames waiting for a credit
         self._admit_cv = threading.Condition()
         self._admitted: set = set()
+        self._admit_deferred: set = set()   # credits handed to a Dropped send (released on its completion)
         self._window_limits: dict = {}
         self._hop_watch = False
         self.hops_failed = 0
@@ -1190,6 +1191,10 @@ class PipelineImpl(Pipeline):
         if after is not None:
             for callback in callbacks:
                 after.then(callback)
+            with self._admit_cv:
+                # the credit stays counted until the zero-copy send completes (its FramePool slot
+                # is still read): destroy_stream's bulk release must not hand it out early
+                self._admit_deferred.add((str(key[0]), key[1]))
             after.then(lambda: self._admit_release(key))
             self._watch_hops()                              # the hop timer polls the transfer
             return
@@ -1252,6 +1257,7 @@ class PipelineImpl(Pipeline):
     def _admit_release(self, key):
         key = (str(key[0]), key[1])
         with self._admit_cv:
+            self._admit_deferred.discard(key)
             if key in self._admitted:
                 self._admitted.discard(key)
                 self._admit_cv.notify_all()
@@ -1261,7 +1267,7 @@ class PipelineImpl(Pipeline):
         before they existed, or never released): the window is shared by the whole pipeline."""
         stream_id = str(stream_id)
         with self._admit_cv:
-            stale = [k for k in self._admitted if k[0] == stream_id]
+            stale = [k for k in self._admitted if k[0] == stream_id and k not in self._admit_deferred]
             if stale:
                 self._admitted.difference_update(stale)
                 self._admit_cv.notify_all()
@@ -1540,9 +1546,15 @@ class PipelineImpl(Pipeline):
                 self._drain_pending()    # credits of finished dropped transfers came back
         for key, f in list(self._inflight.items()):
             if now - f["t"] > timeout:
+                escalate = False
                 if hop is not None and f["rank"] is not None:
-                    hop.suspend(f["rank"])   # alive but unresponsive: no new frames for it
+                    # alive but unresponsive: no new frames for it, bar one probe frame every
+                    # AIKO_HOP_PROBE_S; unanswered probes retire it (supervised restart)
+                    escalate = hop.suspend(f["rank"])
                 self._fail_frame(key, f"remote hop to {f['node']} timed out after {timeout:g}s")
+                if escalate:
+                    self.logger.warning(f"remote {f['node']}: rank {f['rank']} answered no probe: retiring it")
+                    self._replica_lost_rank(f["rank"])
         if self._pending_hops:
             self._drain_pending()
             for fifo in list(self._pending_hops.values()):

@@ -371,7 +371,7 @@ def main(argv=None):
     if a.service:
         from ..runtime import event
         for d in services:
-            if _field(d, 1, "name") == a.service:
+            if a.service in (_field(d, 1, "name"), _field(d, 0, "topic_path")):
                 event.call_soon(dash.select, d).result(5)
                 deadline = time.time() + a.timeout
                 while (dash.consumer is None or dash.consumer.cache_state != "ready") and time.time() < deadline:

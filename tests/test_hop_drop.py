@@ -136,3 +136,31 @@ def test_stopped_replica(tmp_path):
     assert held["pool_free"] <= stuck["pool_slots"] - held["dropped_pending"], res   # not reused
     assert res["resumed"] == {"dropped_pending": 0, "pool_free": stuck["pool_slots"], "suspect": []}, res
     assert res["c"] == [12, 0] and res["sent_to_2_in_c"] >= 1, res      # rank 2 serves again
+
+
+def test_suspension_is_bounded_probe_then_escalate(monkeypatch):
+    """a suspended peer that owes nothing is never heard from again, so a
+    suspension must not be permanent.  After AIKO_HOP_PROBE_S one probe frame is admitted; an
+    answered probe (mark_alive) restores the peer; max_probes unanswered probes make suspend()
+    ask the caller to retire it (mark_dead -> supervised restart)."""
+    from aiko_services_amd.parallel import hop as H
+    plane = H.HopPlane([(0, 0)], device="cpu", depth=2)
+    plane.send_links[1] = plane.send_links[0]            # a second peer (logic only)
+    plane.probe_after_s, plane.max_probes = 0.05, 2
+    assert plane.credit(1) == 2
+    assert plane.suspend(1) is False and plane.credit(1) == 0     # suspended: no frames
+    time.sleep(0.06)
+    assert plane.credit(1) == 1                                   # one probe frame is due
+    plane._note_send(1)                                           # (encode / resend call this)
+    assert plane.credit(1) == 0 and plane.counters["probes"] == 1
+    plane.mark_alive(1)                                           # the probe was answered
+    assert plane.credit(1) == 2 and not plane.suspect
+    # a peer that never answers: two probes time out -> escalate
+    assert plane.suspend(1) is False
+    for probe in range(plane.max_probes):
+        time.sleep(0.06)
+        assert plane.credit(1) == 1
+        plane._note_send(1)
+        escalate = plane.suspend(1)                               # the probe's hop timed out
+        assert escalate is (probe == plane.max_probes - 1)
+    assert plane.counters["escalated"] == 1

@@ -204,7 +204,7 @@ def test_websocket_lwt_and_unknown_transport(monkeypatch):
         c, _ = _client(b.ws_port)
         c.will_set("lwt/ws", b"(absent)")
         c.connect("127.0.0.1", b.ws_port, transport="websockets")
-        c.sock.sock.close()                       # abnormal: no DISCONNECT, no close frame
+        c.sock.sock.shutdown(socket.SHUT_RDWR)    # abnormal: no DISCONNECT, no close frame
         assert q.get(timeout=5)[:2] == ("lwt/ws", b"(absent)")
         watcher.disconnect()
         from aiko_services_amd.message.message import MQTT

@@ -151,3 +151,158 @@ def test_echo_pipeline_over_websockets():
         broker.stop()
     assert "error" not in res, res
     assert res["frames"] == 200 and res["frames_per_s"] > 50, res
+
+
+# ---- LifeCycleManager / Registrar failover / Recorder (reference lifecycle.py:434-456,
+#      registrar.py:139-188, recorder.py:76-92) ----------------------------------------------------
+def _vars(cluster, service, expect=(), timeout=40):
+    out = _snapshot(cluster, service=service, expect=expect, timeout=timeout)
+    found = {}
+    for line in out.splitlines():
+        if line.startswith("  ") and " = " in line:
+            k, v = line.strip().split(" = ", 1)
+            found[k] = v
+    return out, found
+
+
+def _wait_vars(cluster, service, pred, timeout=40):
+    deadline = time.time() + timeout
+    out, found = "", {}
+    while time.time() < deadline:
+        out, found = _vars(cluster, service, timeout=5)
+        if pred(found):
+            return out, found
+        time.sleep(0.3)
+    return out, found
+
+
+def test_lifecycle_manager_clients_handshake_kill_and_lease(cluster):
+    import signal
+    import psutil
+    cluster["spawn"]("-m", "aiko_services_amd.tools.registrar")
+    time.sleep(0.8)
+    mgr = cluster["spawn"]("-m", "aiko_services_amd.control.lifecycle", "manager", "4",
+                           "--handshake-lease", "3", "--silent-clients", "3")
+    # three clients complete the (add_client ...) handshake; the silent fourth never does
+    out, v = _wait_vars(cluster, "lifecycle_manager",
+                        lambda v: v.get("lifecycle_manager_clients_active") == "3")
+    assert v.get("lifecycle_manager_clients_active") == "3", out
+    topics = {k: t for k, t in v.items() if k.startswith("lifecycle_manager.")}
+    assert len(topics) == 3, out
+    # the silent client's handshake lease expires: it is deleted (its process ends)
+    out, v = _wait_vars(cluster, "lifecycle_manager",
+                        lambda v: v.get("lifecycle_manager_clients_handshaking") == "0")
+    assert v.get("lifecycle_manager_clients_handshaking") == "0", out
+    def silent_alive():
+        for c in psutil.Process(mgr.pid).children(recursive=True):
+            try:
+                if c.status() != psutil.STATUS_ZOMBIE and "aiko_silent_client" in " ".join(c.cmdline()):
+                    return True
+            except (psutil.NoSuchProcess, psutil.ZombieProcess):
+                pass
+        return False
+
+    deadline = time.time() + 15
+    silent = True
+    while time.time() < deadline and silent:
+        silent = silent_alive()
+        time.sleep(0.2)
+    assert not silent, "silent client was not deleted after its handshake lease"
+    # SIGKILL one active client: its LWT removes it from the registrar -> clients_active drops
+    victim = next(iter(topics.values()))
+    pid = int(victim.split("/")[2])
+    os.kill(pid, signal.SIGKILL)
+    out, v = _wait_vars(cluster, "lifecycle_manager",
+                        lambda v: v.get("lifecycle_manager_clients_active") == "2")
+    assert v.get("lifecycle_manager_clients_active") == "2", out
+    assert victim not in v.values(), out
+
+
+def _registrars(cluster):
+    out = _snapshot(cluster, expect=("registrar",), timeout=10)
+    return [line.split()[0] for line in out.splitlines()[1:] if " registrar " in f" {line} "]
+
+
+def test_registrar_failover_relists_services(cluster):
+    primary = cluster["spawn"]("-m", "aiko_services_amd.tools.registrar")
+    time.sleep(1.0)
+    cluster["spawn"]("-m", "aiko_services_amd.tools.registrar")
+    cluster["spawn"]("-m", "aiko_services_amd.tools.storage", "start", ":memory:")
+    out = _snapshot(cluster, expect=("storage",))
+    assert "storage" in out and len(_registrars(cluster)) == 2, out
+    primary.kill()                                           # SIGKILL: "(primary absent)" LWT
+    t0 = time.time()
+    ok, out = False, ""
+    while time.time() - t0 < 10 and not ok:
+        out = _snapshot(cluster, service="registrar", expect=("lifecycle = primary",), timeout=3)
+        ok = "lifecycle = primary" in out and "storage" in out
+    elapsed = time.time() - t0
+    assert ok, out
+    assert elapsed < 3.0 + 4.0, elapsed       # within 3 s of promotion (+ the snapshot tool's startup)
+    rows = [r for r in out.splitlines() if r and not r.startswith(" ")]
+    assert any("storage" in r for r in rows) and len(_registrars(cluster)) == 1, out
+
+
+def test_registrars_started_together_settle_on_one_primary(cluster):
+    for _ in range(2):
+        cluster["spawn"]("-m", "aiko_services_amd.tools.registrar")
+    deadline = time.time() + 30
+    states = []
+    while time.time() < deadline:
+        tps = _registrars(cluster)
+        if len(tps) == 2:
+            states = [_vars(cluster, tp, timeout=5)[1].get("lifecycle") for tp in tps]
+            if sorted(states) == ["primary", "secondary"]:
+                break
+        time.sleep(0.3)
+    assert sorted(states) == ["primary", "secondary"], states
+
+
+def test_registrar_split_brain_oldest_wins(cluster):
+    """A primary that hears another primary's announcement: older time_started wins."""
+    cluster["spawn"]("-m", "aiko_services_amd.tools.registrar")
+    _, v = _wait_vars(cluster, "registrar", lambda v: v.get("lifecycle") == "primary")
+    assert v.get("lifecycle") == "primary"
+    ns = cluster["env"]["AIKO_NAMESPACE"]
+    boot = f"{ns}/service/registrar"
+    # a NEWER rival: the primary stays primary and re-announces itself (retained)
+    r = cluster["run"]("-m", "aiko_services_amd.tools.mqtt", "pub", boot,
+                       f"(primary found {ns}/rival/1/1 2 {time.time() + 1000})")
+    assert r.returncode == 0, r.stderr
+    time.sleep(1.0)
+    _, v = _vars(cluster, "registrar", timeout=5)
+    assert v.get("lifecycle") == "primary", v
+    # an OLDER rival: the primary demotes itself to secondary
+    r = cluster["run"]("-m", "aiko_services_amd.tools.mqtt", "pub", boot,
+                       f"(primary found {ns}/rival/1/1 2 1.0)")
+    assert r.returncode == 0, r.stderr
+    out, v = _wait_vars(cluster, "registrar", lambda v: v.get("lifecycle") == "secondary", timeout=20)
+    assert v.get("lifecycle") == "secondary", out
+
+
+def test_recorder_keeps_actor_log_lines(cluster):
+    env = dict(cluster["env"], AIKO_LOG_MQTT="all", AIKO_LOG_LEVEL="INFO")
+    cluster["spawn"]("-m", "aiko_services_amd.tools.registrar")
+    time.sleep(0.8)
+    cluster["spawn"]("-m", "aiko_services_amd.tools.recorder")
+    time.sleep(1.0)
+    actor = subprocess.Popen([sys.executable, "-m", "aiko_services_amd.examples.aloha_honua.aloha_honua_0"],
+                             env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    try:
+        topic = None
+        deadline = time.time() + 15
+        while time.time() < deadline and topic is None:
+            line = actor.stdout.readline()
+            if line.startswith("MQTT topic:"):
+                topic = line.split(":", 1)[1].strip()
+        assert topic
+        cluster["run"]("-m", "aiko_services_amd.tools.mqtt", "pub", topic, "(aloha Pele)")
+        log_topic = "/".join(topic.split("/")[:3]) + "/0/log"
+        out, v = _wait_vars(cluster, "recorder", lambda v: any(k.startswith("lru_cache.") and "Pele" in val
+                                                             for k, val in v.items()))
+        hits = {k: val for k, val in v.items() if k.startswith("lru_cache.") and "Pele" in val}
+        assert hits, out
+        assert any(log_topic in k for k in hits), (log_topic, hits)
+    finally:
+        actor.terminate()
+        actor.wait(5)

@@ -672,6 +672,46 @@ def test_destroy_stream_returns_admission_credits(aiko_process):
     assert not any(k[0] == "w3" for k in pipeline._admitted)
 
 
+def test_destroy_stream_keeps_credit_of_stuck_zero_copy_send(aiko_process, monkeypatch):
+    """a destroyed stream's frame whose zero-copy send is still in flight
+    (a Dropped handle owns its FramePool slot) keeps its admission credit until the transfer
+    completes; the bulk release of the stream must not hand that credit out early."""
+    from aiko_services_amd.pipeline.stream import Frame
+    d = json.loads(json.dumps(DIAMOND))
+    d["parameters"]["frame_window"] = 1
+    pipeline, q = _create(d, stream_id="z1")
+    monkeypatch.setattr(pipeline, "_watch_hops", lambda: None)
+
+    class StuckSend:                       # stands in for parallel.hop.Dropped
+        def __init__(self):
+            self.callbacks = []
+
+        def then(self, fn):
+            self.callbacks.append(fn)
+
+        def complete(self):
+            for fn in self.callbacks:
+                fn()
+
+    slot_back = []
+    assert pipeline.admit_frame("z1", 0, timeout=0)
+    frame = Frame()
+    frame.on_complete.append(lambda: slot_back.append(0))
+    lease = pipeline.stream_leases["z1"]
+    lease.stream.frames[0] = frame
+    stuck = StuckSend()
+
+    def destroy():
+        pipeline._release_frame(lease.stream, 0, after=stuck)      # destroy_stream's drop path
+        pipeline._admit_release_stream("z1")
+    event.call_on_loop(destroy)
+    assert slot_back == []                                          # slot still read by the send
+    assert not pipeline.admit_frame("z2", 0, timeout=0.2)            # ... and its credit held
+    stuck.complete()                                                 # poll_dropped: transfer done
+    assert slot_back == [0]
+    assert pipeline.admit_frame("z2", 0, timeout=0)
+
+
 def test_dict_swag_never_enters_hop_decode(aiko_process, monkeypatch):
     """with a hop data plane up, reference-style frames whose swag holds
     plain nested dicts (no tensor tokens, no encoded DeviceResult, no hop_rank) are never
