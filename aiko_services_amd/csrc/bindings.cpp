@@ -35,9 +35,6 @@ int aiko_conv_persist(const void* x, const void* w, const float* bias, const voi
                       int H, int W, int C, int Cc, int R, int S, int stride, int pad, int Ho, int Wo,
                       int M, int Cout, int K, int act, int ldy, int ldr, int bm, int bn, const void* x2,
                       int K1, int H2, int W2, int C2, int stride2, hipStream_t stream);
-int aiko_stem_l1(const void* in, void* out, const void* w0, const float* b0, const void* w1, int k1, const float* b1,
-                 int B, int Hin, int Win, int Hc, int Wc, int off_t, int off_l, float fill_raw, float inv_std, int H0,
-                 int W0, int H1, int W1, int ldo, hipStream_t stream);
 int aiko_conv_glds_tail(const void* x, const void* w, const float* bias, int H, int W, int C, int Cc, int R, int S,
                         int stride, int pad, int Ho, int Wo, int M, int K, int N, int act, const void* w2, const float* b2,
                         void* y2, int ldy2, int ldw2, int act2, const void* zero, const int* dec, void* boxes,
@@ -82,21 +79,11 @@ int aiko_gemm_fp8(const void* a, const void* b, const float* sa, const float* sb
                   hipStream_t stream);
 int aiko_rownorm_quant(const void* x, int ldx, const float* gamma, const float* beta, float eps,
                        void* yb, int ldyb, void* q, int ldq, float* qs, int M, int D, hipStream_t stream);
-int aiko_gemm_fp8_ln(const void* a, const void* b, const float* sb, const float* bias, const void* res, void* y, int M,
-                     int N, int K, int lda, int ldy, int ldr, int act, const void* zero, const void* amx, int mxr,
-                     void* yq, void* ysc, int ldq, int ysr, float* st, const float* cs, int sts, int stp, int ln_d,
-                     float ln_eps, int ln, hipStream_t stream);
 int aiko_c2f_fused(const void* x, int ldx, const void* w1, const float* b1, int k1, const void* wa, const float* ba,
                    int ka, const void* wb, const float* bb, int kb, const void* w2, const float* b2, int k2, void* y, int ldy,
                    int B, int H, int W, int CI, int C, int CO, int shortcut, int rb, const void* xu, int ldxu, int cu, hipStream_t stream);
 int aiko_c2f_bneck(const void* x, int ldx, const void* wa, const float* ba, int ka, const void* wb, const float* bb,
                    int kb, void* y, int ldy, int B, int H, int W, int C, int shortcut, int rb, hipStream_t stream);
-int aiko_c2f_fused_s2(const void* a0, int lda0, const void* w0, const float* b0, int k0, const void* w1, const float* b1,
-                      int k1, const void* wa, const float* ba, int ka, const void* wb, const float* bb, int kb, const void* w2,
-                      const float* b2, int k2, void* y, int ldy, int B, int H, int W, int CI, int C, int CO, int shortcut,
-                      int rb, hipStream_t stream);
-int aiko_rowstats_mx(const void* x, int ldx, void* q, int ldq, void* qsc, int ysr, float* st, int sts, int P, int M,
-                     int D, hipStream_t stream);
 int aiko_linear_splitk(const void* x, const void* w, const float* bias, float* part, void* y, int M, int N, int K,
                        int ldx, int ldw, int ldy, int S, hipStream_t stream);
 int aiko_attn_fwd(const void* q, const void* k, const void* v, void* o, int ldq, int ldk, int ldv,
@@ -555,40 +542,6 @@ void c2f_fused_out(const at::Tensor& x, const at::Tensor& w1, const at::Tensor& 
                "c2f_fused");
 }
 
-// The 3x3 / stride-2 conv feeding a C2f and the C2f itself in one launch (c2f_fused.hip,
-// c2f_fused_s2_kernel): a0 [B, 2H, 2W, >= 16] -> y [B, H, W, >= CO]; w0 / b0 the stride-2 conv.
-void c2f_fused_s2_out(const at::Tensor& a0, const at::Tensor& w0, const at::Tensor& b0, const at::Tensor& w1,
-                      const at::Tensor& b1, const at::Tensor& wa, const at::Tensor& ba, const at::Tensor& wb,
-                      const at::Tensor& bb, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& y, bool shortcut,
-                      int64_t rb) {
-  for (const at::Tensor* t : {&a0, &w0, &b0, &w1, &b1, &wa, &ba, &wb, &bb, &w2, &b2, (const at::Tensor*)&y})
-    check_cuda(*t, "c2f_s2 operand");
-  for (const at::Tensor* t : {&a0, &w0, &w1, &wa, &wb, &w2, (const at::Tensor*)&y})
-    TORCH_CHECK(t->scalar_type() == at::kBFloat16, "aiko.c2f_fused_s2_out: bf16 activations / weights");
-  for (const at::Tensor* t : {&b0, &b1, &ba, &bb, &b2})
-    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "aiko.c2f_fused_s2_out: fp32 contiguous biases");
-  for (const at::Tensor* t : {&w0, &w1, &wa, &wb, &w2})
-    TORCH_CHECK(t->dim() == 2 && t->is_contiguous() && t->size(1) % 8 == 0, "aiko.c2f_fused_s2_out: weights [Cout, K]");
-  const int64_t C = wa.size(0), CO = w2.size(0), CI = w0.size(0);
-  TORCH_CHECK(w0.size(1) >= 160 && b0.numel() == CI && w1.size(0) == 2 * C && w1.size(1) >= CI && wb.size(0) == C &&
-                  wa.size(1) >= 160 && wb.size(1) >= 160 && w2.size(1) >= 3 * C && b1.numel() == 2 * C &&
-                  ba.numel() == C && bb.numel() == C && b2.numel() == CO,
-              "aiko.c2f_fused_s2_out: inconsistent conv / C2f shapes");
-  TORCH_CHECK(a0.dim() == 4 && y.dim() == 4 && a0.size(0) == y.size(0) && a0.size(1) == 2 * y.size(1) &&
-                  a0.size(2) == 2 * y.size(2) && a0.size(3) >= 16 && y.size(3) >= CO,
-              "aiko.c2f_fused_s2_out: a0 [B, 2H, 2W, 16], y [B, H, W, CO]");
-  const int64_t B = y.size(0), H = y.size(1), W = y.size(2), lda = a0.stride(2), ldy = y.stride(2);
-  TORCH_CHECK(a0.stride(3) == 1 && y.stride(3) == 1 && a0.stride(1) == 2 * W * lda && y.stride(1) == W * ldy &&
-                  a0.stride(0) == 2 * H * a0.stride(1) && y.stride(0) == H * W * ldy && lda % 8 == 0 && ldy % 4 == 0 &&
-                  reinterpret_cast<uintptr_t>(a0.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(y.data_ptr()) % 8 == 0,
-              "aiko.c2f_fused_s2_out: NHWC views with 16-B aligned pixels");
-  check_launch(aiko_c2f_fused_s2(a0.data_ptr(), (int)lda, w0.data_ptr(), b0.data_ptr<float>(), (int)w0.size(1),
-                                 w1.data_ptr(), b1.data_ptr<float>(), (int)w1.size(1), wa.data_ptr(), ba.data_ptr<float>(),
-                                 (int)wa.size(1), wb.data_ptr(), bb.data_ptr<float>(), (int)wb.size(1), w2.data_ptr(),
-                                 b2.data_ptr<float>(), (int)w2.size(1), y.data_ptr(), (int)ldy, (int)B, (int)H, (int)W,
-                                 (int)CI, (int)C, (int)CO, shortcut ? 1 : 0, (int)rb, cur_stream()),
-               "c2f_fused_s2");
-}
 
 // One YOLOv8 C2f bottleneck (3x3 C -> C twice + shortcut) in one launch (c2f_fused.hip):
 // x = s, y = c as NHWC channel-slice views of the C2f's concat buffer.
@@ -699,38 +652,6 @@ void conv_glds_tail_decode_out(const at::Tensor& x, const at::Tensor& w, const a
                "conv_glds_tail_decode");
 }
 
-// YOLOv8 stem (3x3 / 2, 3 -> 16, SiLU, /255) + l1 (3x3 / 2, 16 -> 32, SiLU) from uint8 frames in one
-// launch (stem_l1.hip): a0 never reaches HBM.  geom = [Ho, Wo, Hc, Wc, off_t, off_l] as stem_direct_out
-// (no resize: Ho x Wo = the frame); w0 [16, 64] the direct-stem weight image, w1 [32, >= 160].
-void stem_l1_out(const at::Tensor& frames, const at::Tensor& w0, const at::Tensor& b0, const at::Tensor& w1,
-                 const at::Tensor& b1, at::Tensor& out, at::IntArrayRef geom, double fill, double inv_std) {
-  for (const at::Tensor* t : {&frames, &w0, &b0, &w1, &b1, (const at::Tensor*)&out}) check_cuda(*t, "stem_l1 operand");
-  TORCH_CHECK(frames.scalar_type() == at::kByte && frames.dim() == 4 && frames.size(3) == 3 && frames.is_contiguous(),
-              "aiko.stem_l1_out: frames must be uint8 [B, H, W, 3] contiguous");
-  TORCH_CHECK(geom.size() == 6, "aiko.stem_l1_out: geom = [Ho, Wo, Hc, Wc, off_t, off_l]");
-  const int64_t Ho = geom[0], Wo = geom[1], Hc = geom[2], Wc = geom[3], off_t = geom[4], off_l = geom[5];
-  const int64_t B = frames.size(0), Hin = frames.size(1), Win = frames.size(2);
-  TORCH_CHECK(Ho == Hin && Wo == Win && off_t >= 0 && off_l >= 0 && off_t + Ho <= Hc && off_l + Wo <= Wc &&
-                  off_l % 4 == 0 && Win % 4 == 0 && Wc % 4 == 0 && Hc % 4 == 0,
-              "aiko.stem_l1_out: unresized frame inside the canvas, 4-pixel aligned columns");
-  TORCH_CHECK(w0.scalar_type() == at::kBFloat16 && w0.is_contiguous() && w0.dim() == 2 && w0.size(0) == 16 && w0.size(1) == 64,
-              "aiko.stem_l1_out: w0 bf16 [16, 64]");
-  TORCH_CHECK(w1.scalar_type() == at::kBFloat16 && w1.is_contiguous() && w1.dim() == 2 && w1.size(0) == 32 && w1.size(1) >= 160,
-              "aiko.stem_l1_out: w1 bf16 [32, >= 160]");
-  TORCH_CHECK(b0.scalar_type() == at::kFloat && b0.numel() == 16 && b0.is_contiguous() && b1.scalar_type() == at::kFloat &&
-                  b1.numel() == 32 && b1.is_contiguous(),
-              "aiko.stem_l1_out: fp32 biases [16] / [32]");
-  const int64_t H0 = Hc / 2, W0 = Wc / 2, H1 = H0 / 2, W1 = W0 / 2;
-  TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.dim() == 4 && out.size(0) == B && out.size(1) == H1 &&
-                  out.size(2) == W1 && out.size(3) == 32,
-              "aiko.stem_l1_out: out bf16 [B, Hc / 4, Wc / 4, 32]");
-  const int64_t ldo = pixel_pitch(out, "stem_l1_out");
-  check_launch(aiko_stem_l1(frames.data_ptr(), out.data_ptr(), w0.data_ptr(), b0.data_ptr<float>(), w1.data_ptr(),
-                            (int)w1.size(1), b1.data_ptr<float>(), (int)B, (int)Hin, (int)Win, (int)Hc, (int)Wc, (int)off_t,
-                            (int)off_l, (float)fill, (float)inv_std, (int)H0, (int)W0, (int)H1, (int)W1, (int)ldo,
-                            cur_stream()),
-               "stem_l1");
-}
 
 // A whole ResNet stage-1 bottleneck in one launch (bneck_fused.hip): x [B, H, 56, cin] ->
 // y [B, H, 56, 256]; cin 256 = identity block (w3 [256, 64]), cin 64 = projection block with
@@ -1245,103 +1166,7 @@ void rownorm_quant_out(const at::Tensor& x, const c10::optional<at::Tensor>& gam
                "rownorm_quant");
 }
 
-// LayerNorm folded across a GEMM pair (gemm_fp8.hip, aiko_gemm_fp8_ln).  a: MX-fp8 [M, K] with
-// E8M0 scales amx [K/128, R >= M rounded to 128, 4]; b fp8 [N, K]; st fp32 [P, R2 >= M, 2] row
-// partials (ln 1 writes P = N / 256 of them, ln 2 reads P = st.size(0)).
-//   ln 1: y = a b^T sb + bias + res (bf16) and its MX copy yq [M, N] / ysc [N/128, >= M, 4]
-//   ln 2: y (bf16, act 0) or yq / ysc (MX, act 3 = GELU) = act(rstd (a b^T sb - mean cs) + bias)
-void gemm_fp8_ln_out(const at::Tensor& a, const at::Tensor& amx, const at::Tensor& b, const at::Tensor& sb,
-                     const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& res,
-                     const c10::optional<at::Tensor>& y, const c10::optional<at::Tensor>& yq,
-                     const c10::optional<at::Tensor>& ysc, at::Tensor& st, const c10::optional<at::Tensor>& cs,
-                     int64_t ln, int64_t act, int64_t ln_d, double eps, const at::Tensor& zero) {
-  for (const at::Tensor* t : {&a, &amx, &b, &sb, (const at::Tensor*)&st, &zero}) check_cuda(*t, "operand");
-  TORCH_CHECK(a.element_size() == 1 && b.element_size() == 1, "aiko.gemm_fp8_ln_out: A and B must be fp8 storage");
-  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
-  TORCH_CHECK(K % 128 == 0 && b.dim() == 2 && b.size(1) == K && b.is_contiguous() && N % 256 == 0,
-              "aiko.gemm_fp8_ln_out: B [N % 256 == 0, K % 128 == 0] contiguous");
-  const int64_t lda = row_pitch(a, K, "gemm_fp8_ln_out", "A");
-  TORCH_CHECK(sb.scalar_type() == at::kFloat && sb.numel() == N && sb.is_contiguous(), "aiko.gemm_fp8_ln_out: sb fp32 [N]");
-  TORCH_CHECK(amx.element_size() == 1 && amx.dim() == 3 && amx.size(0) == K / 128 && amx.size(2) == 4 &&
-                  amx.is_contiguous() && amx.size(1) >= ((M + 127) / 128) * 128,
-              "aiko.gemm_fp8_ln_out: amx uint8 [K/128, rows >= M rounded to 128, 4]");
-  TORCH_CHECK(st.scalar_type() == at::kFloat && st.dim() == 3 && st.size(2) == 2 && st.size(1) >= M && st.is_contiguous(),
-              "aiko.gemm_fp8_ln_out: st fp32 [P, >= M, 2]");
-  TORCH_CHECK(zero.nbytes() >= 16 && reinterpret_cast<uintptr_t>(zero.data_ptr()) % 16 == 0 &&
-                  reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0,
-              "aiko.gemm_fp8_ln_out: 16-byte aligned operands and a zero page");
-  const float* bp = nullptr;
-  if (bias.has_value() && bias->defined()) {
-    check_cuda(*bias, "bias");
-    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == N && bias->is_contiguous(), "aiko.gemm_fp8_ln_out: bias fp32 [N]");
-    bp = bias->data_ptr<float>();
-  }
-  const float* csp = nullptr;
-  if (cs.has_value() && cs->defined()) {
-    check_cuda(*cs, "cs");
-    TORCH_CHECK(cs->scalar_type() == at::kFloat && cs->numel() == N && cs->is_contiguous(), "aiko.gemm_fp8_ln_out: cs fp32 [N]");
-    csp = cs->data_ptr<float>();
-  }
-  const void* rp = nullptr;
-  int64_t ldr = 0;
-  if (res.has_value() && res->defined()) {
-    check_cuda(*res, "residual");
-    TORCH_CHECK(res->scalar_type() == at::kBFloat16 && res->size(0) == M, "aiko.gemm_fp8_ln_out: residual bf16 [M, N]");
-    ldr = row_pitch(*res, N, "gemm_fp8_ln_out", "residual");
-    rp = res->data_ptr();
-  }
-  void* yp = nullptr;
-  int64_t ldy = 0;
-  if (y.has_value() && y->defined()) {
-    check_cuda(*y, "y");
-    TORCH_CHECK(y->scalar_type() == at::kBFloat16 && y->size(0) == M, "aiko.gemm_fp8_ln_out: y bf16 [M, N]");
-    ldy = row_pitch(*y, N, "gemm_fp8_ln_out", "y");
-    yp = y->data_ptr();
-  }
-  void* yqp = nullptr;
-  void* yscp = nullptr;
-  int64_t ldq = 0, ysr = 0;
-  if (yq.has_value() && yq->defined()) {
-    TORCH_CHECK(ysc.has_value() && ysc->defined(), "aiko.gemm_fp8_ln_out: yq needs ysc");
-    check_cuda(*yq, "yq");
-    check_cuda(*ysc, "ysc");
-    TORCH_CHECK(yq->element_size() == 1 && yq->size(0) == M, "aiko.gemm_fp8_ln_out: yq uint8 [M, N]");
-    ldq = row_pitch(*yq, N, "gemm_fp8_ln_out", "yq");
-    TORCH_CHECK(ysc->element_size() == 1 && ysc->dim() == 3 && ysc->size(0) == N / 128 && ysc->size(1) >= M &&
-                    ysc->size(2) == 4 && ysc->is_contiguous(),
-                "aiko.gemm_fp8_ln_out: ysc uint8 [N/128, rows >= M, 4]");
-    yqp = yq->data_ptr();
-    yscp = ysc->data_ptr();
-    ysr = ysc->size(1);
-  }
-  if (ln == 1) TORCH_CHECK(st.size(0) >= N / 256, "aiko.gemm_fp8_ln_out: st needs N / 256 partials");
-  check_launch(aiko_gemm_fp8_ln(a.data_ptr(), b.data_ptr(), sb.data_ptr<float>(), bp, rp, yp, M, N, K, lda, ldy, ldr,
-                                act, zero.data_ptr(), amx.data_ptr(), (int)amx.size(1), yqp, yscp, (int)ldq, (int)ysr,
-                                st.data_ptr<float>(), csp, (int)st.size(1), (int)st.size(0), (int)ln_d, (float)eps,
-                                (int)ln, cur_stream()),
-               "gemm_fp8_ln");
-}
 
-// bf16 rows x [M, D] -> MX-fp8 copy (q [M, D], qsc [D/128, >= M, 4]) + row sum / sum of squares
-// as partial 0 of st [P, >= M, 2] (partials 1 .. P-1 zeroed)
-void rowstats_mx_out(const at::Tensor& x, at::Tensor& q, at::Tensor& qsc, at::Tensor& st) {
-  for (const at::Tensor* t : {&x, (const at::Tensor*)&q, (const at::Tensor*)&qsc, (const at::Tensor*)&st}) check_cuda(*t, "operand");
-  TORCH_CHECK(x.scalar_type() == at::kBFloat16, "aiko.rowstats_mx_out: x bf16");
-  const int64_t M = x.size(0), D = x.size(1);
-  const int64_t ldx = row_pitch(x, D, "rowstats_mx_out", "x");
-  TORCH_CHECK(ldx % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "aiko.rowstats_mx_out: 16-B rows");
-  TORCH_CHECK(q.element_size() == 1 && q.size(0) == M && q.size(1) >= D, "aiko.rowstats_mx_out: q uint8 [M, D]");
-  const int64_t ldq = row_pitch(q, D, "rowstats_mx_out", "q");
-  TORCH_CHECK(ldq % 8 == 0 && reinterpret_cast<uintptr_t>(q.data_ptr()) % 8 == 0, "aiko.rowstats_mx_out: 8-B q rows");
-  TORCH_CHECK(qsc.element_size() == 1 && qsc.dim() == 3 && qsc.size(0) == D / 128 && qsc.size(1) >= M && qsc.size(2) == 4 &&
-                  qsc.is_contiguous(),
-              "aiko.rowstats_mx_out: qsc uint8 [D/128, >= M, 4]");
-  TORCH_CHECK(st.scalar_type() == at::kFloat && st.dim() == 3 && st.size(2) == 2 && st.size(1) >= M && st.is_contiguous(),
-              "aiko.rowstats_mx_out: st fp32 [P, >= M, 2]");
-  check_launch(aiko_rowstats_mx(x.data_ptr(), (int)ldx, q.data_ptr(), (int)ldq, qsc.data_ptr(), (int)qsc.size(1),
-                                st.data_ptr<float>(), (int)st.size(1), (int)st.size(0), (int)M, (int)D, cur_stream()),
-               "rowstats_mx");
-}
 
 // Split-K linear (linear_splitk.hip): x [M, >= K] bf16, w [N, >= K] bf16 (row pitch w.stride(0)),
 // bias fp32 [N] or None, part fp32 with >= S*M*N elements, y [M, >= N] bf16.
@@ -1601,7 +1426,6 @@ TORCH_LIBRARY(aiko, m) {
   m.def("batchnorm_out(Tensor x, Tensor scale, Tensor shift, Tensor(a!) y, int act) -> ()");
   m.def("yolo_decode_out(Tensor[] feats, int[] strides, int nc, int reg_max, Tensor(a!) boxes, Tensor(b!) scores, Tensor(c!) cls) -> ()");
   m.def("topk_nms_out(Tensor boxes, Tensor scores, Tensor cls, int max_cand, float[] params, Tensor(a!) det, Tensor(b!) count) -> ()");
-  m.def("stem_l1_out(Tensor frames, Tensor w0, Tensor b0, Tensor w1, Tensor b1, Tensor(a!) out, int[] geom, float fill, float inv_std) -> ()");
   m.def("stem_direct_out(Tensor frames, Tensor w, Tensor? bias, Tensor(a!) out, int[] geom, float fill, float[] mean, float[] std, bool bgr) -> ()");
   m.def("conv3x3_patch_out(Tensor x, Tensor wimg, Tensor? bias, Tensor(a!) y, int act, int grid=0) -> ()");
   m.def("conv3x3_patchw_out(Tensor x, Tensor wimg, Tensor? bias, Tensor(a!) y, int act, int grid=0) -> ()");
@@ -1618,10 +1442,7 @@ TORCH_LIBRARY(aiko, m) {
   m.def("stem_pool_u8_out(Tensor frames, Tensor w, Tensor bias, Tensor(a!) y, float[] mean255, int variant=0) -> ()");
   m.def("gemm_fp8_out(Tensor a, Tensor? sa, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!)? y, int act, int bm, int bn, int variant=0, Tensor? zero=None, Tensor? amx=None, Tensor(b!)? yq=None, Tensor(c!)? ysc=None) -> ()");
   m.def("rownorm_quant_out(Tensor x, Tensor? gamma, Tensor? beta, float eps, Tensor(a!)? yb, Tensor(b!)? q, Tensor(c!)? qs) -> ()");
-  m.def("gemm_fp8_ln_out(Tensor a, Tensor amx, Tensor b, Tensor sb, Tensor? bias, Tensor? res, Tensor(a!)? y, Tensor(b!)? yq, Tensor(c!)? ysc, Tensor(d!) st, Tensor? cs, int ln, int act, int ln_d, float eps, Tensor zero) -> ()");
-  m.def("rowstats_mx_out(Tensor x, Tensor(a!) q, Tensor(b!) qsc, Tensor(c!) st) -> ()");
   m.def("c2f_fused_out(Tensor x, Tensor w1, Tensor b1, Tensor wa, Tensor ba, Tensor wb, Tensor bb, Tensor w2, Tensor b2, Tensor(a!) y, int ci, bool shortcut, int rb, Tensor? xu=None) -> ()");
-  m.def("c2f_fused_s2_out(Tensor a0, Tensor w0, Tensor b0, Tensor w1, Tensor b1, Tensor wa, Tensor ba, Tensor wb, Tensor bb, Tensor w2, Tensor b2, Tensor(a!) y, bool shortcut, int rb) -> ()");
   m.def("c2f_bneck_out(Tensor x, Tensor wa, Tensor ba, Tensor wb, Tensor bb, Tensor(a!) y, bool shortcut, int rb) -> ()");
   m.def("conv_glds_tail_decode_out(Tensor x, Tensor w, Tensor bias, Tensor w2, Tensor b2, Tensor(a!) boxes, Tensor(b!) scores, Tensor(c!) cls, int R, int pad, int act, int mode, int nc, int level_stride, int astart, Tensor zero) -> ()");
   m.def("conv_glds_tail_out(Tensor x, Tensor w, Tensor bias, Tensor w2, Tensor b2, Tensor(a!) y2, int R, int stride, int pad, int act, int act2, Tensor zero) -> ()");
@@ -1660,14 +1481,10 @@ TORCH_LIBRARY_IMPL(aiko, CUDA, m) {
   m.impl("softmax_topk_out", &softmax_topk_out);
   m.impl("gemm_fp8_out", &gemm_fp8_out);
   m.impl("rownorm_quant_out", &rownorm_quant_out);
-  m.impl("gemm_fp8_ln_out", &gemm_fp8_ln_out);
-  m.impl("rowstats_mx_out", &rowstats_mx_out);
   m.impl("c2f_fused_out", &c2f_fused_out);
   m.impl("c2f_bneck_out", &c2f_bneck_out);
   m.impl("conv_glds_tail_out", &conv_glds_tail_out);
-  m.impl("stem_l1_out", &stem_l1_out);
   m.impl("conv_glds_tail_decode_out", &conv_glds_tail_decode_out);
-  m.impl("c2f_fused_s2_out", &c2f_fused_s2_out);
   m.impl("attn_fwd_out", &attn_fwd_out);
   m.impl("linear_splitk_out", &linear_splitk_out);
   m.impl("logmel_out", &logmel_out);

@@ -102,16 +102,10 @@ __device__ __forceinline__ int v_off(int row, int col) {
 //   * the row sums come out of the MFMA pipe: one extra 16x16x32 MFMA per P fragment with an
 //     all-ones A operand (rowsum(P) in every row of the result, no fp32 add chain and no
 //     end-of-kernel reduction), summing the same bf16 P that enters O.
-// VA = 1: the V^T fragments are read with ds_read_b64_tr_b16 issued from inline asm and retired
-// by an explicit lgkmcnt(0) tied to them.  Through the builtin, hipcc's waitcnt pass treats the
-// transposed read as possibly aliasing the in-flight LDS-DMA (buffer_load ... lds) writes and puts
-// an s_waitcnt vmcnt(0) in front of it every tile — draining the three-tile K/V prefetch, so each
-// tile waited for the DMA issued at its own top.  The slot being read was retired by the tile's
-// counted vmcnt + barrier, which is the only ordering these reads need.  Measured (round 5,
-// scripts/r5_attn_va.sh, B = 14): 129.7-133.7 us vs 130.4-132.8 us for the builtin reads — the
-// K/V tiles are L2 hits (the query blocks of a head share them), so the drained prefetch was
-// not on the critical path; variants 16-18, opt-in.
-template <int NW, int VPRE, int REG = 0, int SM = 0, int VA = 0>
+// Removed after measurement (round 5, kept in profiles/attn_pmc_r5.md): inline-asm V^T reads with
+// an explicit lgkmcnt (the builtin's vmcnt(0) drain turned out off the critical path: K/V tiles
+// are L2 hits) and s_setprio over the MFMA clusters (no effect) — former variants 16-20.
+template <int NW, int VPRE, int REG = 0, int SM = 0>
 __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p) {
   constexpr int NT = 64 * NW;
   constexpr int QB = 32 * NW;
@@ -293,39 +287,15 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const int r0 = 32 * ks + 4 * g + trq;
-        if constexpr (VA & 1) {
-          const uint32_t a0 = (uint32_t)reinterpret_cast<uintptr_t>(vb + v_off(r0, d * 16 + 4 * trp));
-          const uint32_t a1 = (uint32_t)reinterpret_cast<uintptr_t>(vb + v_off(r0 + 16, d * 16 + 4 * trp));
-          v4i16 lo, hi;
-          asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a0) : "memory");
-          asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(a1) : "memory");
-          vfr[d][ks] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-        } else {
-          const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) v4i16*)(vb + v_off(r0, d * 16 + 4 * trp)));
-          const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) v4i16*)(vb + v_off(r0 + 16, d * 16 + 4 * trp)));
-          vfr[d][ks] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-        }
-      }
-    };
-    // VA: every V read issued so far has landed (no use of the fragments above this point)
-    auto wait_v = [&](int d0, int d1) {
-      if constexpr (VA & 1) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        for (int d = d0; d < d1; ++d)
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks) asm volatile("" : "+v"(vfr[d][ks]));
+        const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4i16*)(vb + v_off(r0, d * 16 + 4 * trp)));
+        const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4i16*)(vb + v_off(r0 + 16, d * 16 + 4 * trp)));
+        vfr[d][ks] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
     };
 
   // S^T = K Q^T : 4 key tiles x 2 query tiles
-    // VA & 2: raised wave priority over the MFMA clusters (s_setprio), so that a wave reaching
-    // its matrix work is issued ahead of the co-resident waves' softmax VALU work — the
-    // workgroup's barriers otherwise keep all waves in the same phase.  Measured (round 5,
-    // scripts/r5_attn_prio.sh, B = 14): 129.9-133.2 us vs 129.2-132.6 us (variant 19 vs 0), bench
-    // 3,373 vs 3,329-3,372 windows/s — no effect; variants 19 / 20 opt-in
-    if constexpr ((VA & 2) != 0) __builtin_amdgcn_s_setprio(2);
     f32x4 s[4][2];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
@@ -345,7 +315,6 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
       }
     }
 
-    if constexpr ((VA & 2) != 0) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
     for (int d = 0; d < VPRE; ++d) read_v(d);
 
@@ -476,14 +445,9 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
 
     // O^T += V^T P^T (fragments read above / here)
     if constexpr (SM != 2) {
-    if constexpr ((VA & 2) != 0) __builtin_amdgcn_s_setprio(2);
-    if constexpr (VA & 1) wait_v(0, VPRE);
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-      if (d >= VPRE) {
-        read_v(d);
-        wait_v(d, d + 1);
-      }
+      if (d >= VPRE) read_v(d);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -497,7 +461,6 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void attn_fwd_kernel(AttnParams p
         for (int qt = 0; qt < 2; ++qt)
           lsum[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[qt][ks], lsum[qt], 0, 0, 0);
     }
-    if constexpr ((VA & 2) != 0) __builtin_amdgcn_s_setprio(0);
     }
 
     slot = slot == NS - 1 ? 0 : slot + 1;
@@ -685,9 +648,9 @@ extern "C" int aiko_attn_fwd(const void* q, const void* k, const void* v, void* 
       return 0;
     return n;
   }();
-  auto launch = [&](auto nw_tag, auto vpre_tag, auto reg_tag, auto sm_tag, auto va_tag) {
+  auto launch = [&](auto nw_tag, auto vpre_tag, auto reg_tag, auto sm_tag) {
     constexpr int NW = decltype(nw_tag)::value, VPRE = decltype(vpre_tag)::value;
-    constexpr int REG = decltype(reg_tag)::value, SM = decltype(sm_tag)::value, VA = decltype(va_tag)::value;
+    constexpr int REG = decltype(reg_tag)::value, SM = decltype(sm_tag)::value;
     constexpr int QB = 32 * NW;
     p.nqb = (T + QB - 1) / QB;
     const long items = (long)p.nqb * H * B;
@@ -707,16 +670,14 @@ extern "C" int aiko_attn_fwd(const void* q, const void* k, const void* v, void* 
           p.cnt = static_cast<int*>(work);
           p.part = reinterpret_cast<float*>(static_cast<char*>(work) + cnt_b);
           dim3 grid((unsigned)(8 * (p.split_full + (long)r * sp))), block(64 * NW);
-          aiko::attn_fwd_kernel<NW, VPRE, REG, SM, VA><<<grid, block, 0, stream>>>(p);
+          aiko::attn_fwd_kernel<NW, VPRE, REG, SM><<<grid, block, 0, stream>>>(p);
           return;
         }
       }
     }
     dim3 grid(p.nqb, H, B), block(64 * NW);
-    aiko::attn_fwd_kernel<NW, VPRE, REG, SM, VA><<<grid, block, 0, stream>>>(p);
+    aiko::attn_fwd_kernel<NW, VPRE, REG, SM><<<grid, block, 0, stream>>>(p);
   };
-  using A0 = std::integral_constant<int, 0>;
-  using A1 = std::integral_constant<int, 1>;
   using R0 = std::integral_constant<int, 0>;
   using R1 = std::integral_constant<int, 1>;
   using I8 = std::integral_constant<int, 8>;
@@ -724,26 +685,21 @@ extern "C" int aiko_attn_fwd(const void* q, const void* k, const void* v, void* 
   using V0 = std::integral_constant<int, 0>;
   using V2 = std::integral_constant<int, 2>;
   switch (variant) {
-    case 1: launch(I8{}, V2{}, R0{}, R0{}, A0{}); break;
-    case 2: launch(I8{}, std::integral_constant<int, 4>{}, R0{}, R0{}, A0{}); break;
-    case 3: launch(I4{}, V0{}, R0{}, R0{}, A0{}); break;
-    case 4: launch(I4{}, V2{}, R0{}, R0{}, A0{}); break;
-    case 5: launch(I8{}, V0{}, R1{}, R0{}, A0{}); break;
-    case 6: launch(I8{}, V2{}, R1{}, R0{}, A0{}); break;
-    case 7: launch(I4{}, V0{}, R1{}, R0{}, A0{}); break;
-    case 8: launch(I4{}, V2{}, R1{}, R0{}, A0{}); break;
-    case 10: launch(I8{}, V0{}, R0{}, R0{}, A0{}); break;        // round-2 softmax
-    case 11: launch(I8{}, V2{}, R0{}, R1{}, A0{}); break;
-    case 12: launch(I8{}, V0{}, R1{}, R1{}, A0{}); break;
-    case 13: launch(I4{}, V0{}, R0{}, R1{}, A0{}); break;
-    case 14: launch(I4{}, V2{}, R1{}, R1{}, A0{}); break;
-    case 15: launch(I8{}, V0{}, R0{}, std::integral_constant<int, 2>{}, A0{}); break;   // ping-pong query tiles
-    case 16: launch(I8{}, V0{}, R0{}, R1{}, A1{}); break;   // asm V reads, per d-block wait
-    case 17: launch(I8{}, std::integral_constant<int, 4>{}, R0{}, R1{}, A1{}); break;   // all V reads before the softmax
-    case 18: launch(I8{}, V2{}, R0{}, R1{}, A1{}); break;
-    case 19: launch(I8{}, V0{}, R0{}, R1{}, std::integral_constant<int, 2>{}); break;   // s_setprio over MFMAs
-    case 20: launch(I8{}, V2{}, R0{}, R1{}, std::integral_constant<int, 2>{}); break;
-    default: launch(I8{}, V0{}, R0{}, R1{}, A0{}); break;
+    case 1: launch(I8{}, V2{}, R0{}, R0{}); break;
+    case 2: launch(I8{}, std::integral_constant<int, 4>{}, R0{}, R0{}); break;
+    case 3: launch(I4{}, V0{}, R0{}, R0{}); break;
+    case 4: launch(I4{}, V2{}, R0{}, R0{}); break;
+    case 5: launch(I8{}, V0{}, R1{}, R0{}); break;
+    case 6: launch(I8{}, V2{}, R1{}, R0{}); break;
+    case 7: launch(I4{}, V0{}, R1{}, R0{}); break;
+    case 8: launch(I4{}, V2{}, R1{}, R0{}); break;
+    case 10: launch(I8{}, V0{}, R0{}, R0{}); break;        // round-2 softmax
+    case 11: launch(I8{}, V2{}, R0{}, R1{}); break;
+    case 12: launch(I8{}, V0{}, R1{}, R1{}); break;
+    case 13: launch(I4{}, V0{}, R0{}, R1{}); break;
+    case 14: launch(I4{}, V2{}, R1{}, R1{}); break;
+    case 15: launch(I8{}, V0{}, R0{}, std::integral_constant<int, 2>{}); break;   // ping-pong query tiles
+    default: launch(I8{}, V0{}, R0{}, R1{}); break;
   }
   return (int)hipGetLastError();
 }

@@ -245,257 +245,6 @@ __global__ __launch_bounds__(W * 2, 1) void c2f_fused_kernel(C2fParams p) {
   }
 }
 
-// The 160-wide C2f with the convolution that feeds it fused in front (YOLOv8-n l1 + l2): x is
-// never written — each step computes x row v + 3 = silu(conv3x3/2(a0 rows 2v+5 .. 2v+7)) into a
-// 2-row X ring (cv0: K = 9 taps x 16 channels in two-tap chunks, stride-2 taps read from a 5-row
-// ring of the 320-wide a0 rows, two new a0 rows per step loaded a step ahead), and cv1 reads its
-// B fragments from X instead of HBM.  Same single barrier per step; the prologue fills the rings
-// with a barrier between each stage.
-struct C2fS2Params {
-  C2fParams c;           // c.x unused (x is computed); c.ldx unused
-  const bf16_t* a0;      // [B][2H][2W][lda0] (16 channels used)
-  const bf16_t* w0;      // cv0 [CI][k0] (3x3 / stride 2, K = 9 x 16)
-  const float* b0;
-  int lda0, k0;
-};
-
-template <int W, int CI, int C, int CO, bool SC>
-__global__ __launch_bounds__(W * 2, 1) void c2f_fused_s2_kernel(C2fS2Params q) {
-  using namespace c2f;
-  const C2fParams& p = q.c;
-  static_assert(W == 160 && CI == 32 && C == 16 && CO == 32, "instantiated shapes");
-  constexpr int C0 = 16;                               // a0 channels
-  constexpr int NWAVE = W / 32, PT = 2, NTH = NWAVE * 64;
-  constexpr int N0 = CI / 16, KC0 = (9 * C0 + 31) / 32;
-  constexpr int KS1 = CI / 32, N1 = 2 * C / 16, KC3 = (9 * C + 31) / 32, N2 = CO / 16;
-  constexpr int SW = W + 2, SROW = SW * C * 2, TROW = SW * C * 2, AROW = W * C * 2;
-  constexpr int W0 = 2 * W, A0W = W0 + 2, A0ROW = A0W * C0 * 2, XROW = W * CI * 2;
-  constexpr int NS = 5, NA = 5, NT = 4, NA0 = 5, NX = 2;
-  constexpr int PPR0 = W0 * C0 * 2 / 16, PPT0 = PPR0 / NTH;   // a0 16-B pieces per row / per thread
-  static_assert(PPR0 % NTH == 0, "whole a0 pieces per thread");
-  __shared__ __attribute__((aligned(16))) unsigned char smem[NS * SROW + NA * AROW + NT * TROW + NA0 * A0ROW + NX * XROW];
-  unsigned char* const sring = smem;
-  unsigned char* const aring = sring + NS * SROW;
-  unsigned char* const tring = aring + NA * AROW;
-  unsigned char* const a0ring = tring + NT * TROW;
-  unsigned char* const xring = a0ring + NA0 * A0ROW;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int fr = lane & 15, fq = lane >> 4;
-  const int H = p.H, H0 = 2 * H;
-  const int nb = H / p.rb;
-  const int img = blockIdx.x / nb, r0 = (blockIdx.x % nb) * p.rb, r1 = r0 + p.rb;
-  const int px0 = wave * 32;
-
-  bf16x8 w0f[N0][KC0], w1f[N1][KS1], waf[KC3], wbf[KC3], w2f[N2];
-  v4s w2c[N2];
-#pragma unroll
-  for (int n = 0; n < N0; ++n)
-#pragma unroll
-    for (int k = 0; k < KC0; ++k)
-      w0f[n][k] = *reinterpret_cast<const bf16x8*>(q.w0 + (long)(16 * n + fr) * q.k0 + 32 * k + 8 * fq);
-#pragma unroll
-  for (int n = 0; n < N1; ++n)
-#pragma unroll
-    for (int k = 0; k < KS1; ++k)
-      w1f[n][k] = *reinterpret_cast<const bf16x8*>(p.w1 + (long)(16 * n + fr) * p.k1 + 32 * k + 8 * fq);
-#pragma unroll
-  for (int k = 0; k < KC3; ++k) {
-    waf[k] = *reinterpret_cast<const bf16x8*>(p.wa + (long)fr * p.ka + 32 * k + 8 * fq);
-    wbf[k] = *reinterpret_cast<const bf16x8*>(p.wb + (long)fr * p.kb + 32 * k + 8 * fq);
-  }
-#pragma unroll
-  for (int n = 0; n < N2; ++n) {
-    w2f[n] = *reinterpret_cast<const bf16x8*>(p.w2 + (long)(16 * n + fr) * p.k2 + 8 * fq);
-    w2c[n] = *reinterpret_cast<const v4s*>(p.w2 + (long)(16 * n + fr) * p.k2 + 2 * C + 4 * fq);
-  }
-  f32x4 b0v[N0], b1v[N1], bav, bbv, b2v[N2];
-#pragma unroll
-  for (int n = 0; n < N0; ++n) b0v[n] = *reinterpret_cast<const f32x4*>(q.b0 + 16 * n + 4 * fq);
-#pragma unroll
-  for (int n = 0; n < N1; ++n) b1v[n] = *reinterpret_cast<const f32x4*>(p.b1 + 16 * n + 4 * fq);
-  bav = *reinterpret_cast<const f32x4*>(p.ba + 4 * fq);
-  bbv = *reinterpret_cast<const f32x4*>(p.bb + 4 * fq);
-#pragma unroll
-  for (int n = 0; n < N2; ++n) b2v[n] = *reinterpret_cast<const f32x4*>(p.b2 + 16 * n + 4 * fq);
-
-  // zero borders: S / T rings (C channels) and the a0 ring (C0 channels)
-  for (int i = tid; i < (NS + NT) * 2 * (C / 8) + NA0 * 2 * (C0 / 8); i += NTH) {
-    if (i < (NS + NT) * 2 * (C / 8)) {
-      const int slot = i / (2 * (C / 8)), rem = i % (2 * (C / 8));
-      const int side = rem / (C / 8), piece = rem % (C / 8);
-      unsigned char* base = slot < NS ? sring + slot * SROW : tring + (slot - NS) * TROW;
-      *reinterpret_cast<u32x4*>(base + (side ? (W + 1) : 0) * C * 2 + piece * 16) = u32x4{0u, 0u, 0u, 0u};
-    } else {
-      const int j = i - (NS + NT) * 2 * (C / 8);
-      const int slot = j / (2 * (C0 / 8)), rem = j % (2 * (C0 / 8));
-      const int side = rem / (C0 / 8), piece = rem % (C0 / 8);
-      *reinterpret_cast<u32x4*>(a0ring + slot * A0ROW + (side ? (W0 + 1) : 0) * C0 * 2 + piece * 16) =
-          u32x4{0u, 0u, 0u, 0u};
-    }
-  }
-
-  // two-tap 3x3 geometry (C = C0 = 16 channels per tap)
-  int toff[KC3], trow[KC3], toff0[KC0];
-#pragma unroll
-  for (int k = 0; k < KC3; ++k) {
-    int t = 2 * k + (fq >> 1);
-    if (t > 8) t = 8;
-    const int dy = t / 3, dx = t % 3 - 1;
-    trow[k] = dy;
-    toff[k] = ((fr + 1 + dx) * C + 8 * (fq & 1)) * 2;
-    toff0[k] = ((2 * fr + 1 + dx) * C0 + 8 * (fq & 1)) * 2;   // stride-2 input pixel of output pixel fr
-  }
-
-  // a0 rows: pieces of this thread (j = tid + NTH i: pixel j / 2, half j % 2)
-  u32x4 a0reg[2][PPT0];
-  auto load_a0 = [&](int slotreg, int row) __attribute__((always_inline)) {
-    const bool ok = row >= 0 && row < H0;
-#pragma unroll
-    for (int i = 0; i < PPT0; ++i) {
-      const int j = tid + NTH * i, px = j >> 1, h = j & 1;
-      a0reg[slotreg][i] = ok ? *reinterpret_cast<const u32x4*>(q.a0 + (((long)img * H0 + row) * W0 + px) * q.lda0 + 8 * h)
-                             : u32x4{0u, 0u, 0u, 0u};
-    }
-  };
-  auto put_a0 = [&](int slotreg, int row) __attribute__((always_inline)) {
-    const int slot = (row + 4 * NA0) % NA0;
-#pragma unroll
-    for (int i = 0; i < PPT0; ++i) {
-      const int j = tid + NTH * i, px = j >> 1, h = j & 1;
-      *reinterpret_cast<u32x4*>(a0ring + slot * A0ROW + ((px + 1) * C0 + 8 * h) * 2) = a0reg[slotreg][i];
-    }
-  };
-  // cv0: x row `xr` from a0 rows 2 xr - 1 .. 2 xr + 1 -> X slot xr % 2
-  auto cv0 = [&](int xr) __attribute__((always_inline)) {
-    const unsigned char* rows[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) rows[d] = a0ring + ((2 * xr - 1 + d + 4 * NA0) % NA0) * A0ROW;
-    unsigned char* xs = xring + ((xr + 2 * NX) % NX) * XROW;
-#pragma unroll
-    for (int t = 0; t < PT; ++t) {
-      const int px = px0 + 16 * t;
-#pragma unroll
-      for (int n = 0; n < N0; ++n) {
-        f32x4 acc = b0v[n];
-#pragma unroll
-        for (int k = 0; k < KC0; ++k) {
-          const unsigned char* base = trow[k] == 0 ? rows[0] : (trow[k] == 1 ? rows[1] : rows[2]);
-          const bf16x8 b = *reinterpret_cast<const bf16x8*>(base + 2 * px * C0 * 2 + toff0[k]);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0f[n][k], b, acc, 0, 0, 0);
-        }
-        *reinterpret_cast<u32x2*>(xs + ((px + fr) * CI + 16 * n + 4 * fq) * 2) = pack4(silu4(acc));
-      }
-    }
-  };
-  auto cv1 = [&](int row) __attribute__((always_inline)) {
-    const bool ok = row >= 0 && row < H;
-    const int slot = (row + 2 * NS) % NS;
-    const unsigned char* xs = xring + ((row + 2 * NX) % NX) * XROW;
-#pragma unroll
-    for (int t = 0; t < PT; ++t) {
-      const int px = px0 + 16 * t + fr;
-      bf16x8 xf[KS1];
-#pragma unroll
-      for (int k = 0; k < KS1; ++k) xf[k] = *reinterpret_cast<const bf16x8*>(xs + (px * CI + 32 * k + 8 * fq) * 2);
-#pragma unroll
-      for (int n = 0; n < N1; ++n) {
-        f32x4 acc = b1v[n];
-#pragma unroll
-        for (int k = 0; k < KS1; ++k) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[n][k], xf[k], acc, 0, 0, 0);
-        const u32x2 v = ok ? pack4(silu4(acc)) : u32x2{0u, 0u};
-        if (n < C / 16)
-          *reinterpret_cast<u32x2*>(aring + slot * AROW + (px * C + 16 * n + 4 * fq) * 2) = v;
-        else
-          *reinterpret_cast<u32x2*>(sring + slot * SROW + ((px + 1) * C + 16 * (n - C / 16) + 4 * fq) * 2) = v;
-      }
-    }
-  };
-  auto conv3 = [&](const unsigned char* ring, int nsl, int rstride, int row, const bf16x8 (&wf)[KC3], f32x4 bias,
-                   int t) __attribute__((always_inline)) {
-    const unsigned char* rows[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) rows[d] = ring + ((row - 1 + d + 4 * nsl) % nsl) * rstride + (px0 + 16 * t) * C * 2;
-    f32x4 acc = bias;
-#pragma unroll
-    for (int k = 0; k < KC3; ++k) {
-      const unsigned char* base = trow[k] == 0 ? rows[0] : (trow[k] == 1 ? rows[1] : rows[2]);
-      const bf16x8 b = *reinterpret_cast<const bf16x8*>(base + toff[k]);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[k], b, acc, 0, 0, 0);
-    }
-    return acc;
-  };
-  auto bar = []() __attribute__((always_inline)) { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
-
-  // ---- prologue: x rows r0-2 .. r0+1 (cv1 of r0-2 .. r0), a0 rows up to 2 r0 + 5 in the ring,
-  // a0 rows 2 r0 + 6, 2 r0 + 7 in registers
-  load_a0(0, 2 * r0 - 5);
-  put_a0(0, 2 * r0 - 5);
-  load_a0(0, 2 * r0 - 4);
-  put_a0(0, 2 * r0 - 4);
-  load_a0(0, 2 * r0 - 3);
-  put_a0(0, 2 * r0 - 3);
-#pragma unroll 1
-  for (int xr = r0 - 2; xr <= r0 + 1; ++xr) {
-    bar();                                           // a0 rows 2 xr - 1 .. 2 xr + 1 in the ring
-    cv0(xr);
-    bar();                                           // X row xr complete; a0 row 2 xr - 1 free
-    if (xr <= r0) cv1(xr);
-    load_a0(0, 2 * xr + 2);
-    load_a0(1, 2 * xr + 3);
-    put_a0(0, 2 * xr + 2);
-    put_a0(1, 2 * xr + 3);
-  }
-  load_a0(0, 2 * r0 + 6);
-  load_a0(1, 2 * r0 + 7);
-
-  for (int v = r0 - 1; v <= r1 + 1; ++v) {
-    bar();
-    // a0 rows 2v+8, 2v+9 into the ring (slots of 2v+3, 2v+4, last read by cv0 of the previous
-    // step), the next two into registers
-    put_a0(0, 2 * v + 8);
-    put_a0(1, 2 * v + 9);
-    load_a0(0, 2 * v + 10);
-    load_a0(1, 2 * v + 11);
-    if (v + 3 <= r1 + 1) cv0(v + 3);               // a0 rows 2v+5 .. 2v+7 (earlier steps) -> X
-    if (v + 2 <= r1 + 1) cv1(v + 2);               // X row v + 2 (previous step)
-    if (v <= r1) {
-      const bool ok = v >= 0 && v < H;
-      const int slot = (v + 2 * NT) % NT;
-#pragma unroll
-      for (int t = 0; t < PT; ++t) {
-        const f32x4 acc = conv3(sring, NS, SROW, v, waf, bav, t);
-        const u32x2 o = ok ? pack4(silu4(acc)) : u32x2{0u, 0u};
-        *reinterpret_cast<u32x2*>(tring + slot * TROW + ((px0 + 16 * t + fr + 1) * C + 4 * fq) * 2) = o;
-      }
-    }
-    const int w = v - 2;
-    if (w >= r0 && w < r1) {
-      const int aslot = (w + 2 * NA) % NA, sslot = (w + 2 * NS) % NS;
-#pragma unroll
-      for (int t = 0; t < PT; ++t) {
-        const int px = px0 + 16 * t + fr;
-        f32x4 c = silu4(conv3(tring, NT, TROW, w, wbf, bbv, t));
-        if constexpr (SC) {
-          const f32x4 sv = unpack4(*reinterpret_cast<const u32x2*>(sring + sslot * SROW + ((px + 1) * C + 4 * fq) * 2));
-          c = f32x4{c[0] + sv[0], c[1] + sv[1], c[2] + sv[2], c[3] + sv[3]};
-        }
-        const v4s cop = __builtin_bit_cast(v4s, pack4(c));
-        const bf16x8 as = fq < 2 ? *reinterpret_cast<const bf16x8*>(aring + aslot * AROW + (px * C + 8 * fq) * 2)
-                                 : *reinterpret_cast<const bf16x8*>(sring + sslot * SROW + ((px + 1) * C + 8 * (fq - 2)) * 2);
-        bf16_t* yrow = p.y + (((long)img * H + w) * W + px) * p.ldy;
-#pragma unroll
-        for (int n = 0; n < N2; ++n) {
-          const f32x4 acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f[n], as, b2v[n], 0, 0, 0);
-          const f32x4 acc2 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(w2c[n], cop, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          const f32x4 acc = {acc1[0] + acc2[0], acc1[1] + acc2[1], acc1[2] + acc2[2], acc1[3] + acc2[3]};
-          *reinterpret_cast<u32x2*>(yrow + 16 * n + 4 * fq) = pack4(silu4(acc));
-        }
-      }
-    }
-  }
-}
-
 // The same row stream for wider channel counts (YOLOv8-n l15 at 80 x 80: cv1 1x1 192 -> 64,
 // bottleneck 3x3 32 -> 32 twice, no shortcut, cv2 1x1 96 -> 64): the weights (~77 KB) live in
 // LDS (rows padded by 16 bytes: the 16 rows of a fragment read start on different banks), each
@@ -853,28 +602,3 @@ extern "C" int aiko_c2f_bneck(const void* x, int ldx, const void* wa, const floa
   return (int)hipGetLastError();
 }
 
-// a0 [B, 2H, 2W, lda0] -> y [B, H, W, ldy]: the 3x3 / stride-2 conv w0 (16 -> CI channels, SiLU)
-// and the C2f after it in one launch (c2f_fused_s2_kernel).
-extern "C" int aiko_c2f_fused_s2(const void* a0, int lda0, const void* w0, const float* b0, int k0, const void* w1,
-                                 const float* b1, int k1, const void* wa, const float* ba, int ka, const void* wb,
-                                 const float* bb, int kb, const void* w2, const float* b2, int k2, void* y, int ldy,
-                                 int B, int H, int W, int CI, int C, int CO, int shortcut, int rb, hipStream_t stream) {
-  using namespace aiko;
-  if (rb <= 0 || H % rb || B <= 0) return -1;
-  C2fS2Params q{};
-  q.c.w1 = static_cast<const bf16_t*>(w1); q.c.b1 = b1;
-  q.c.wa = static_cast<const bf16_t*>(wa); q.c.ba = ba;
-  q.c.wb = static_cast<const bf16_t*>(wb); q.c.bb = bb;
-  q.c.w2 = static_cast<const bf16_t*>(w2); q.c.b2 = b2;
-  q.c.y = static_cast<bf16_t*>(y);
-  q.c.B = B; q.c.H = H; q.c.ldy = ldy; q.c.k1 = k1; q.c.ka = ka; q.c.kb = kb; q.c.k2 = k2; q.c.rb = rb;
-  q.a0 = static_cast<const bf16_t*>(a0); q.lda0 = lda0;
-  q.w0 = static_cast<const bf16_t*>(w0); q.b0 = b0; q.k0 = k0;
-  const dim3 grid((unsigned)(B * (H / rb)));
-  if (W == 160 && CI == 32 && C == 16 && CO == 32 && shortcut) {
-    c2f_fused_s2_kernel<160, 32, 16, 32, true><<<grid, dim3(320), 0, stream>>>(q);
-  } else {
-    return -1;
-  }
-  return (int)hipGetLastError();
-}

@@ -259,10 +259,6 @@ extern "C" int aiko_conv_chain2(const void* A, const void* W1, const float* b1, 
                                 const void* W2, const float* b2, void* Z, int M, int K1, int N1, int N2,
                                 int grid, hipStream_t stream);
 
-extern "C" int aiko_conv_chain3(const void* A, const void* W1, const float* b1, const void* R, void* Y,
-                                const void* W2, const float* b2, void* Z, int M, int K1, int N1, int N2,
-                                int grid, hipStream_t stream);
-
 extern "C" int aiko_conv_chain(const void* A, const void* W1, const float* b1, const void* R, void* Y,
                                const void* W2, const float* b2, void* Z, const void* A2, int M, int K1, int N1, int N2,
                                int grid, hipStream_t stream) {
@@ -289,10 +285,6 @@ extern "C" int aiko_conv_chain(const void* A, const void* W1, const float* b1, c
   // stage 2 -> 128: weights-in-registers kernel (conv_chain2.hip)
   if (!A2 && K1 == 128 && N1 == 512 && N2 == 128)
     return aiko_conv_chain2(A, W1, b1, R, Y, W2, b2, Z, M, K1, N1, N2, grid, stream);
-  AIKO_CHAIN(128, 512, 256)
-  // stage 3 -> 256: channel-chunked kernel (conv_chain3.hip)
-  if (!A2 && K1 == 256 && N1 == 1024 && N2 == 256)
-    return aiko_conv_chain3(A, W1, b1, R, Y, W2, b2, Z, M, K1, N1, N2, grid, stream);
   if (A2 && K1 == 128 && N1 == 256 && N2 == 64) {
     hipLaunchKernelGGL((conv_chain_kernel<128, 256, 64, true>), dim3(grid), dim3(chain::NT), 0, stream, a,
                        static_cast<const bf16_t*>(A2), w1, b1, r, y, w2, b2, z, M);

@@ -1715,65 +1715,6 @@ __global__ __launch_bounds__(256) void rownorm_quant_pers_kernel(
   }
 }
 
-// The LayerNorm producer's outputs for a residual stream no GEMM wrote (Whisper's first layer):
-// x [M][ldx] bf16, D columns (D % 32 == 0, D <= 768) -> its MX-fp8 copy q [M][ldq] + E8M0 scales
-// [D/128][ysr][4], and the row sum / sum of squares as partial 0 of st [P][sts] float2 (partials
-// 1 .. P - 1 zeroed, so a consumer reading P partials sees the full row).  32 lanes per row (chunk
-// c of lane l: columns 8 (l + 32 c) ..+ 7; one MX block = 4 adjacent lanes), 8 rows per block.
-__global__ __launch_bounds__(256) void rowstats_mx_kernel(const bf16_t* __restrict__ x, int ldx, uint8_t* __restrict__ q,
-                                                          int ldq, uint8_t* __restrict__ qsc, int ysr,
-                                                          float* __restrict__ st, int sts, int P, int M, int D) {
-  const int lane = threadIdx.x & 31;
-  const int row = blockIdx.x * 8 + (threadIdx.x >> 5);
-  const bool live = row < M;                       // both halves of a wave run the reductions
-  const int nchunk = D >> 3;
-  float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    const int ch = lane + 32 * c;
-    const bool ok = live && ch < nchunk;
-    u32x4 u = {0u, 0u, 0u, 0u};
-    if (ok) u = *reinterpret_cast<const u32x4*>(x + (long)row * ldx + ch * 8);
-    float w[8];
-    float amax = 0.f;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      w[2 * e] = __uint_as_float(u[e] << 16);
-      w[2 * e + 1] = __uint_as_float(u[e] & 0xffff0000u);
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      s1 += w[e];
-      s2 += w[e] * w[e];
-      amax = fmaxf(amax, fabsf(w[e]));
-    }
-    amax = fmaxf(amax, dpp_f32<0xB1>(amax));       // the 4 lanes of one 32-column block
-    amax = fmaxf(amax, dpp_f32<0x4E>(amax));
-    const int ex = mx_exponent(amax);
-    const float inv = __uint_as_float((uint32_t)(127 - ex) << 23);
-    unsigned w0 = 0u, w1 = 0u;
-    w0 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(w[0] * inv, -448.f), 448.f),
-                                         fminf(fmaxf(w[1] * inv, -448.f), 448.f), w0, false);
-    w0 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(w[2] * inv, -448.f), 448.f),
-                                         fminf(fmaxf(w[3] * inv, -448.f), 448.f), w0, true);
-    w1 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(w[4] * inv, -448.f), 448.f),
-                                         fminf(fmaxf(w[5] * inv, -448.f), 448.f), w1, false);
-    w1 = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(w[6] * inv, -448.f), 448.f),
-                                         fminf(fmaxf(w[7] * inv, -448.f), 448.f), w1, true);
-    if (ok) {
-      *reinterpret_cast<uint2*>(q + (long)row * ldq + ch * 8) = make_uint2(w0, w1);
-      const int blk = ch >> 2;
-      if ((lane & 3) == 0) qsc[((long)(blk >> 2) * ysr + row) * 4 + (blk & 3)] = (uint8_t)(ex + 127);
-    }
-  }
-  s1 = group_sum<1>(s1);
-  s2 = group_sum<1>(s2);
-  if (live && lane < P) {
-    const float2 v = lane == 0 ? make_float2(s1, s2) : make_float2(0.f, 0.f);
-    *reinterpret_cast<float2*>(st + ((long)lane * sts + row) * 2) = v;
-  }
-}
-
 }  // namespace aiko
 
 extern "C" int aiko_gemm_fp8(const void* a, const void* b, const float* sa, const float* sb,
@@ -1947,69 +1888,6 @@ extern "C" int aiko_rownorm_quant(const void* x, int ldx, const float* gamma, co
     rownorm_quant_kernel<6><<<grid, block, 0, stream>>>(xp, ldx, gamma, beta, eps, yp, ldyb, qp, ldq, qs, M, D);
   } else if (D <= 64 * 8 * 16) {
     rownorm_quant_kernel<16><<<grid, block, 0, stream>>>(xp, ldx, gamma, beta, eps, yp, ldyb, qp, ldq, qs, M, D);
-  } else {
-    return -1;
-  }
-  return (int)hipGetLastError();
-}
-
-extern "C" int aiko_rowstats_mx(const void* x, int ldx, void* q, int ldq, void* qsc, int ysr, float* st, int sts,
-                                int P, int M, int D, hipStream_t stream) {
-  using namespace aiko;
-  if (M <= 0 || D % 32 || D > 768 || P < 1 || P > 32 || sts < M || ysr < M) return -1;
-  rowstats_mx_kernel<<<dim3((M + 7) / 8), dim3(256), 0, stream>>>(static_cast<const bf16_t*>(x), ldx,
-                                                                 static_cast<uint8_t*>(q), ldq,
-                                                                 static_cast<uint8_t*>(qsc), ysr, st, sts, P, M, D);
-  return (int)hipGetLastError();
-}
-
-// LayerNorm folded across a GEMM pair on the persistent 256 x 256 kernel (gemm_fp8_pers2_kernel,
-// LN argument).  ln 1 (producer): y = A B^T * sb + bias + res (bf16), its MX-fp8 copy yq / ysc and
-// row partials st [N/256][sts] float2; ln 2 (consumer): y (bf16, act 0) or yq / ysc (MX-fp8, act 3
-// = GELU) = act(rstd * (A B^T * sb - mean * cs) + bias) with the statistics of the stp partials
-// in st over ln_d columns.  A is MX-fp8 (amx) in both.
-extern "C" int aiko_gemm_fp8_ln(const void* a, const void* b, const float* sb, const float* bias, const void* res,
-                                void* y, int M, int N, int K, int lda, int ldy, int ldr, int act, const void* zero,
-                                const void* amx, int mxr, void* yq, void* ysc, int ldq, int ysr, float* st,
-                                const float* cs, int sts, int stp, int ln_d, float ln_eps, int ln, hipStream_t stream) {
-  using namespace aiko;
-  if (!zero || !amx || !st || M <= 0 || N % 256 || N > 3072 || K % 128 || K < 256 || sts < M) return -1;
-  Fp8GemmParams p{};
-  p.a = static_cast<const uint8_t*>(a);
-  p.b = static_cast<const uint8_t*>(b);
-  p.sa = nullptr; p.sb = sb; p.bias = bias;
-  p.res = static_cast<const bf16_t*>(res);
-  p.y = static_cast<bf16_t*>(y);
-  p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldy = ldy; p.ldr = ldr; p.act = act;
-  p.amx = static_cast<const uint8_t*>(amx); p.mxr = mxr;
-  p.yq = static_cast<uint8_t*>(yq); p.ysc = static_cast<uint8_t*>(ysc); p.ldq = ldq; p.ysr = ysr;
-  p.st = st; p.cs = cs; p.sts = sts; p.stp = stp; p.ln_d = ln_d; p.ln_eps = ln_eps;
-  if ((long)sts * 8 * (N / 256 > stp ? N / 256 : stp) >= 0x7ffffff0L) return -1;
-  if (yq && ((long)M * ldq >= 0x7ffffff0L || (long)(N / 128) * ysr * 4 >= 0x7ffffff0L || ysr < M)) return -1;
-  if (y && ((long)M * ldy * 2 >= 0x7ffffff0L || ldy % 8 || reinterpret_cast<uintptr_t>(y) % 16)) return -1;
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  }
-  const int tiles_n = N / 256, ntiles = ((M + 255) / 256) * tiles_n;
-  const dim3 pg((unsigned)(ntiles < cus ? ntiles : cus));
-  const uint8_t* z = static_cast<const uint8_t*>(zero);
-  if (ln == 1) {
-    if (!res || !y || !yq || !ysc || act != 0 || N > 1024 || ldr % 8 || (long)M * ldr * 2 >= 0x7ffffff0L ||
-        reinterpret_cast<uintptr_t>(res) % 16)
-      return -1;
-    gemm_fp8_pers2_kernel<256, false, 0, true, true, 1><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles, 0);
-  } else if (ln == 2) {
-    if (!cs || res || stp < 1 || stp > 4 || ln_d <= 0) return -1;
-    if (yq && ysc && act == 3 && !y) {
-      gemm_fp8_pers2_kernel<256, true, 3, true, false, 2><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles, 0);
-    } else if (y && !yq && act == 0) {
-      gemm_fp8_pers2_kernel<256, false, 0, true, false, 2><<<pg, 512, 0, stream>>>(p, z, tiles_n, ntiles, 0);
-    } else {
-      return -1;
-    }
   } else {
     return -1;
   }

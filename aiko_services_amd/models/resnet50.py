@@ -45,9 +45,9 @@ def _rand_conv(g: torch.Generator, cout: int, cin: int, k: int) -> torch.Tensor:
     return torch.randn(cout, cin, k, k, generator=g) * math.sqrt(2.0 / fan_in)
 
 
-# workgroups of the persistent stage-1 kernel (0 = one per CU); fewer leave CUs to the other
-# frame lane's compute-bound layers while stage 1 streams HBM
-_BN_GRID = int(os.environ.get("AIKO_BN_GRID", "0") or 0)
+# workgroups of the persistent stage-1 kernel: one per CU (fewer, to leave CUs to the other frame
+# lane, measured as noise in round 5: profiles/bneck_r5.md)
+_BN_GRID = 0
 
 
 @dataclass
@@ -99,9 +99,11 @@ class ResNet50(WeightsMixin):
         self._ws: dict = {}
         self.fuse_shortcut = True
         self.fuse_stem_pool = True       # stem conv + ReLU + max-pool in one kernel
-        # Infinity-Cache blocking of the memory-bound early stages (see features_from_stem)
-        self.mall_chunk = int(os.environ.get("AIKO_RESNET_MALL_CHUNK", "0"))
-        self.mall_blocks = int(os.environ.get("AIKO_RESNET_MALL_BLOCKS", "3"))
+        # Infinity-Cache blocking of the memory-bound early stages (see features_from_stem): off —
+        # measured slower than the fused stage-1 kernels (profiles/mall_blocking_resnet50_r1.txt,
+        # round-5 A/B); the attributes stay for the equivalence test
+        self.mall_chunk = 0
+        self.mall_blocks = 3
         # conv_chain: identity block's 1x1 expansion + next block's 1x1 reduction in one launch
         self.chain = os.environ.get("AIKO_RESNET_CHAIN", "1") != "0"
         # stage-1 bottlenecks as ONE launch each (bneck_fused.hip: t1 / t2 stay in LDS)

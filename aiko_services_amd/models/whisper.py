@@ -15,15 +15,9 @@ Whisper-small encoder on streamed audio chunks with fp8 weights.  Execution per 
         LN2 + quantise -> FC1 fp8 GEMM (+bias, GELU) -> quantise -> FC2 fp8 GEMM (+residual) }
   ln_post -> bf16 [B, T, d_model]
 
-With ``ln_fold`` (``AIKO_WHISPER_LN_FOLD=1``) neither LayerNorm is a pass of its own: the GEMM that
-writes the residual stream (conv2 + pos once via ``rowstats_mx``, then out-proj and fc2) also
-writes its MX-fp8 copy and per-row partial sums / sums of squares, and qkv / fc1 run on that
-copy with the LayerNorm's affine folded into their weights and the row statistics applied in
-their epilogue (``ops/transformer.py`` ``linear_fp8_ln``).  Attention writes MX-fp8, fc1 writes
-MX-fp8: the only row-wise pass left is ln_post.  Measured on MI355X at the 14-stream shape
-(profiles/whisper_lnfold_r5.md) it is numerically equivalent but slower — the MX-fp8 A operand
-costs qkv / fc1 7 / 12 us and the producers' extra epilogue 6 / 12 us, more than the two ~13 us
-row-norm passes it removes — so it is opt-in.
+A LayerNorm folded across the GEMM pairs (row statistics from the producer's epilogue, the affine
+folded into the consumer's weights) was built and measured in round 5: numerically equivalent but
+slower (profiles/whisper_lnfold_r5.md), and removed in round 6.
 
 Linear weights are e4m3fn with per-channel scales (see ``ops/transformer.py``); the convs and
 attention run in bf16.  Random init (no checkpoints offline), deterministic per seed.
@@ -76,9 +70,6 @@ class WhisperEncoder(WeightsMixin):
         self.n_ctx = n_ctx
         # attention writes MX-fp8 for the out-projection (no per-row quantisation pass)
         self.mx_attention = os.environ.get("AIKO_WHISPER_MX_ATTN", "1") != "0" and d % 128 == 0
-        # LayerNorms folded into the GEMM pairs (opt-in, AIKO_WHISPER_LN_FOLD=1; see the docstring)
-        self.ln_fold = (self.mx_attention and self.device.type == "cuda" and d % 256 == 0
-                        and os.environ.get("AIKO_WHISPER_LN_FOLD", "0") == "1")
         g = torch.Generator().manual_seed(seed)
         dev = self.device
 
@@ -107,9 +98,6 @@ class WhisperEncoder(WeightsMixin):
                         TR.make_fp8_linear(rnd(d, 4 * d, fan_in=4 * d), small(d), dev))
             self.blocks.append(blk)
         self.ln_post = ((1.0 + 0.1 * torch.randn(d, generator=g)).to(dev), small(d).to(dev))
-        self._folded: list = []          # per block: (qkv, fc1) with ln1 / ln2 folded in
-        if self.ln_fold:
-            self._fold_layernorms()
         self._ws: dict = {}
         self.ws_tag = ""             # workspace key prefix (one workspace per frame lane)
         self._pos_ready: set = set()
@@ -126,24 +114,6 @@ class WhisperEncoder(WeightsMixin):
             yield f"blocks.{i}.fc1", b.fc1
             yield f"blocks.{i}.fc2", b.fc2
         yield "ln_post", self.ln_post
-
-    def _fold_layernorms(self):
-        """(Re)derive the LayerNorm-folded qkv / fc1 linears; in place when they exist, so a
-        captured hipGraph keeps pointing at current weights."""
-        new = [(TR.make_ln_fp8_linear(b.qkv, *b.ln1, device=self.device),
-                TR.make_ln_fp8_linear(b.fc1, *b.ln2, device=self.device)) for b in self.blocks]
-        if len(self._folded) != len(new):
-            self._folded = new
-            return
-        for old_pair, new_pair in zip(self._folded, new):
-            for o, n in zip(old_pair, new_pair):
-                for name in ("weight", "scale", "bias", "cs"):
-                    getattr(o, name).copy_(getattr(n, name))
-                o.ref_weight = n.ref_weight
-
-    def _weights_loaded(self):
-        if self.ln_fold:
-            self._fold_layernorms()
 
     def config(self) -> dict:
         return {"size": self.size, "n_ctx": self.n_ctx}
@@ -227,8 +197,6 @@ class WhisperEncoder(WeightsMixin):
         if a8 is None and self.mx_attention:
             a8, asc = TR.mx_buffers(M, d, self.device)
             self._ws[(self.ws_tag + "a_mx", M, d)] = (a8, asc)
-        if self.ln_fold:
-            return self._encode_folded(x, B, T, Tp, qkv, att, aws, a8, asc, u8, usc)
         for blk in self.blocks:
             TR.rownorm(x, *blk.ln1, q=q8, qs=s8)
             TR.linear_fp8(q8, s8, blk.qkv, out=qkv)
@@ -244,27 +212,6 @@ class WhisperEncoder(WeightsMixin):
             TR.rownorm(x, *blk.ln2, q=q8, qs=s8)
             TR.linear_fp8(q8, s8, blk.fc1, act=TR.ACT_GELU, out_mx=(u8, usc))
             TR.linear_fp8(u8, None, blk.fc2, out=x, residual=x, x_mx=usc)
-        y = self._buf("y", (M, d))
-        TR.rownorm(x, *self.ln_post, out=y)
-        return y.view(B, Tp, d)[:, :T]
-
-    def _encode_folded(self, x, B, T, Tp, qkv, att, aws, a8, asc, u8, usc):
-        """The transformer layers with both LayerNorms folded into the GEMM pairs (class docstring)."""
-        M, d, H = x.shape[0], self.d, self.heads
-        xq, xsc = self._ws.get((self.ws_tag + "x_mx", M, d)) or (None, None)
-        if xq is None:
-            xq, xsc = TR.mx_buffers(M, d, self.device)
-            self._ws[(self.ws_tag + "x_mx", M, d)] = (xq, xsc)
-        st_a = self._buf("ln_st_a", (d // 256, M, 2), torch.float32, zero=True)   # x entering a layer
-        st_b = self._buf("ln_st_b", (d // 256, M, 2), torch.float32, zero=True)   # x after attention
-        TR.rowstats_mx(x, xq, xsc, st_a)
-        for blk, (qkv_f, fc1_f) in zip(self.blocks, self._folded):
-            TR.linear_fp8_ln(xq, xsc, qkv_f, st_a, 2, out=qkv, ln_d=d)
-            TR.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], att, B, H, T, Tp, (d // H) ** -0.5,
-                         work=aws, out_mx=(a8, asc))
-            TR.linear_fp8_ln(a8, asc, blk.out, st_b, 1, out=x, residual=x, out_mx=(xq, xsc))
-            TR.linear_fp8_ln(xq, xsc, fc1_f, st_b, 2, act=TR.ACT_GELU, out_mx=(u8, usc), ln_d=d)
-            TR.linear_fp8_ln(u8, usc, blk.fc2, st_a, 1, out=x, residual=x, out_mx=(xq, xsc))
         y = self._buf("y", (M, d))
         TR.rownorm(x, *self.ln_post, out=y)
         return y.view(B, Tp, d)[:, :T]

@@ -38,17 +38,13 @@ REG_MAX = 16
 # the detect head's class branch as one conv_glds launch with the 1x1 in its epilogue
 # (AIKO_HEAD_TAIL=0: the two separate convs)
 _HEAD_TAIL = __import__("os").environ.get("AIKO_HEAD_TAIL", "1") != "0"
-# ... and the box branch (3x3 64 -> 64 + 1x1 64 -> 64) the same way (AIKO_HEAD_TAIL_BOX=0: separate)
-_HEAD_TAIL_BOX = __import__("os").environ.get("AIKO_HEAD_TAIL_BOX", "1") != "0"
+# (and the box branch, 3x3 64 -> 64 + 1x1 64 -> 64, the same way)
 # the detect head's tail launches decode in their epilogues (AIKO_DECODE_FUSED=0: head outputs +
 # the yolo_decode kernel)
 _DECODE_FUSED = __import__("os").environ.get("AIKO_DECODE_FUSED", "1") != "0"
-# letterbox + stem + l1 as one launch, a0 never written (stem_l1.hip).  Measured (round 5,
-# scripts/r5_stem_l1_micro.py, B = 64): 153 us against 60 + 88 us for the two kernels, bench
-# 42.7-43.8k vs 45.2-45.7k with an earlier 174-183 us version — not faster, so opt-in (AIKO_STEM_L1=1)
-_STEM_L1 = __import__("os").environ.get("AIKO_STEM_L1", "0") == "1"
-# l15's fused C2f reads the 2x upsample of l12 in place (AIKO_UP_INPLACE=0: upsample2x kernel)
-_UP_INPLACE = __import__("os").environ.get("AIKO_UP_INPLACE", "1") != "0"
+# l15's fused C2f reads the 2x upsample of l12 in place (+1.6 % over 5 interleaved bench pairs
+# against the upsample2x kernel, round 5)
+_UP_INPLACE = True
 
 
 def _make_div(x, d=8):
@@ -195,24 +191,10 @@ class YOLOv8(WeightsMixin):
                 and a.R == 3 and b.R == 3 and a.Cc == blk.c and b.Cc == blk.c
                 and x.stride(3) == 1 and out.stride(3) == 1)
 
-    def _l1l2_fused_ok(self, a0, a2) -> bool:
-        """l1 + l2 in one launch (c2f_fused_s2_kernel).  Numerics-tested, but the bench measured
-        41.4 / 41.6k vs 41.4 / 42.3k frames/s with l1 as its own conv (same box): the longer
-        serial row step at one workgroup per CU costs what the saved a1 round trip gains; opt-in
-        with AIKO_C2F_S2=1."""
-        import os
-        l1 = self.l1
-        return (a0.is_cuda and os.environ.get("AIKO_C2F_FUSED", "1") != "0"
-                and os.environ.get("AIKO_C2F_S2", "0") == "1"      # opt-in: measured no faster (see below)
-                and l1.kind == "conv" and l1.R == 3 and l1.S == 3 and l1.stride == 2 and l1.pad == 1 and l1.Cc == 16
-                and a0.shape[3] == 16 and a0.shape[1] == 2 * a2.shape[1] and a0.shape[2] == 2 * a2.shape[2]
-                and self._c2f_fused_ok(self.l2, a2, a2) and a0.stride(3) == 1)
-
     @staticmethod
     def _c2f_rb(H):
         """Band height: 160-row images 40 (bench sweep 32-160), 80-row images 20."""
-        import os
-        return int(os.environ.get("AIKO_C2F_RB" if H == 160 else "AIKO_C2F_RB80", "40" if H == 160 else "20"))
+        return 40 if H == 160 else 20
 
     def _run_c2f(self, name, blk: C2f, x, out, cat=None, xu=None):
         """``cat``: the block's split/concat buffer with cv1's output already in channels
@@ -268,7 +250,7 @@ class YOLOv8(WeightsMixin):
         h2 = self._buf(f"h{i}.2", (B, H, W, cb + cc))
         out = self._buf(f"h{i}.out", (B, H, W, 4 * REG_MAX + self.nc_pad))
         C.conv2d(x, lvl.first, out=h1)
-        if _HEAD_TAIL and _HEAD_TAIL_BOX and C.conv_tail_ok(h1[..., :cb], lvl.box[1], lvl.box[2]):
+        if _HEAD_TAIL and C.conv_tail_ok(h1[..., :cb], lvl.box[1], lvl.box[2]):
             C.conv2d_tail(h1[..., :cb], lvl.box[1], lvl.box[2], out[..., :4 * REG_MAX])
         else:
             C.conv2d(h1[..., :cb], lvl.box[1], out=h2[..., :cb])
@@ -312,12 +294,11 @@ class YOLOv8(WeightsMixin):
                                        list(V.YOLO_MEAN), list(V.YOLO_STD), False)
         return out
 
-    def head_outputs(self, x: torch.Tensor | None, a0: torch.Tensor | None = None, decode: bool = False,
-                     a1: torch.Tensor | None = None):
+    def head_outputs(self, x: torch.Tensor | None, a0: torch.Tensor | None = None, decode: bool = False):
         """Stem buffer (or the stem output ``a0``) -> per-level head outputs
         [B, H/s, W/s, 64 + nc] for s = 8, 16, 32.  ``decode``: the head branches decode in their
         epilogues instead (:meth:`_decode_fused_ok`) and this returns (boxes, scores, cls)."""
-        B = (a1 if a1 is not None else x if a0 is None else a0).shape[0]
+        B = (x if a0 is None else a0).shape[0]
         S = self.image_size
         c1, c2, c3, c4, c5 = self.ch
         h0, w0 = C.stem_out_hw(S, S, 3, 2, 1)
@@ -327,19 +308,10 @@ class YOLOv8(WeightsMixin):
             s.append(((h - 1) // 2 + 1, (w - 1) // 2 + 1))
         (H1, W1), (H2, W2), (H3, W3), (H4, W4), (H5, W5) = s
         a2 = self._buf("a2", (B, H2, W2, c2))
-        if a1 is None and a0 is None:
+        if a0 is None:
             a0 = C.conv2d(x, self.l0, out=self._buf("a0", (B, H1, W1, c1)), image_hw=(S, S))
-        if a1 is not None:                  # stem + l1 already ran as one launch (stem_l1_from_frames)
-            a2 = self._run_c2f("l2", self.l2, a1, a2)
-        elif self._l1l2_fused_ok(a0, a2):
-            # l1 (3x3 / 2) and the l2 C2f in one row-stream launch: a1 is never written
-            a, b = self.l2.m[0]
-            torch.ops.aiko.c2f_fused_s2_out(a0, self.l1.weight, self.l1.bias, self.l2.cv1.weight, self.l2.cv1.bias,
-                                            a.weight, a.bias, b.weight, b.bias, self.l2.cv2.weight, self.l2.cv2.bias,
-                                            a2, self.l2.shortcut, self._c2f_rb(H2))
-        else:
-            a1 = C.conv2d(a0, self.l1, out=self._buf("a1", (B, H2, W2, c2)))
-            a2 = self._run_c2f("l2", self.l2, a1, a2)
+        a1 = C.conv2d(a0, self.l1, out=self._buf("a1", (B, H2, W2, c2)))
+        a2 = self._run_c2f("l2", self.l2, a1, a2)
         cat14 = self._buf("cat14", (B, H3, W3, c4 + c3))       # [up(l12) | l4]
         a3 = self._buf("a3", (B, H3, W3, c3))
         if (_HEAD_TAIL and not self._c2f_fused_ok(self.l4, a3, cat14[..., c4:])
@@ -438,37 +410,8 @@ class YOLOv8(WeightsMixin):
                            det=self._buf("det", (B, self.max_det, 6), torch.float32),
                            count=self._buf("count", (B,), torch.int32))
 
-    def _stem_l1_ok(self, frames: torch.Tensor) -> bool:
-        """Can the letterbox + stem + l1 run as ONE launch (stem_l1.hip): an unresized uint8 frame
-        with 4-pixel aligned columns on the canvas, YOLO's /255 normalisation, a 3x3 / 2 16 -> 32 l1."""
-        if not (_STEM_L1 and self.fused_stem and frames.is_cuda and frames.dtype == torch.uint8 and frames.dim() == 4
-                and frames.is_contiguous() and self.ch[0] == 16 and self.ch[1] == 32):
-            return False
-        Ho, Wo, top, left, _ = self.letterbox(frames.shape[1:3])
-        S = self.image_size
-        return ((Ho, Wo) == tuple(frames.shape[1:3]) and left % 4 == 0 and Wo % 4 == 0 and S % 4 == 0
-                and self.l1.R == 3 and self.l1.stride == 2 and self.l1.pad == 1 and self.l1.Cc == 16
-                and self.l1.weight.shape[1] >= 160 and tuple(V.YOLO_MEAN) == (0.0, 0.0, 0.0)
-                and len(set(V.YOLO_STD)) == 1)
-
-    def stem_l1_from_frames(self, frames: torch.Tensor) -> torch.Tensor:
-        """uint8 [B, H, W, 3] -> l1's output [B, S/4, S/4, 32] in ONE kernel (stem_l1_kernel:
-        letterbox + /255 + stem conv + SiLU into LDS, then l1 + SiLU) — a0 never reaches HBM."""
-        B = frames.shape[0]
-        Ho, Wo, top, left, _ = self.letterbox(frames.shape[1:3])
-        S = self.image_size
-        if self._stem_w is None:
-            self._stem_w = torch.zeros(self.l0.cout, 64, dtype=torch.bfloat16, device=self.l0.weight.device)
-            self._derive_stem_w()
-        out = self._buf("a1", (B, S // 4, S // 4, self.ch[1]))
-        torch.ops.aiko.stem_l1_out(frames, self._stem_w, self.l0.bias, self.l1.weight, self.l1.bias, out,
-                                   [Ho, Wo, S, S, top, left], 114.0, 1.0 / (255.0 * V.YOLO_STD[0]))
-        return out
-
     def detect(self, frames: torch.Tensor):
         H, W = frames.shape[1:3]
-        if self._stem_l1_ok(frames) and self._decode_fused_ok():
-            return self._nms(*self.head_outputs(None, a1=self.stem_l1_from_frames(frames), decode=True), (H, W))
         if self.fused_stem and self._decode_fused_ok():
             return self._nms(*self.head_outputs(None, a0=self.stem_from_frames(frames), decode=True), (H, W))
         if self.fused_stem:

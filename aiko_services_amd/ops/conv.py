@@ -640,7 +640,7 @@ STEM_POOL_VARIANT = 0     # 0: 8x7 pooled tiles (4 workgroups/CU); 1: 8x14 (2 wo
 # per CU instead of 2, room for the other frame lane): 126-128 us vs 143-150 us for variant 2 on
 # the same box, ResNet-50 bench 85.2k / 83.9k vs 81.7k / 83.0k interleaved; 4 = four rows per
 # MFMA group (3 workgroups per CU), not faster
-STEM_POOL_U8_VARIANT = int(__import__("os").environ.get("AIKO_STEM_U8_VARIANT", "3"))
+STEM_POOL_U8_VARIANT = 3
 
 
 def stem_pool_weight(spec: ConvSpec) -> torch.Tensor:
@@ -757,9 +757,6 @@ def linear(x: torch.Tensor, spec: ConvSpec, out: torch.Tensor | None = None,
     return out
 
 
-def _chain_stage2() -> bool:
-    """``AIKO_CHAIN_STAGE2=1`` admits the stage-2 chain shapes (read at call time)."""
-    return __import__("os").environ.get("AIKO_CHAIN_STAGE2", "0") == "1"
 
 
 def conv_tail_ok(x: torch.Tensor, spec: ConvSpec, spec2: ConvSpec) -> bool:
@@ -787,27 +784,16 @@ def conv2d_tail(x: torch.Tensor, spec: ConvSpec, spec2: ConvSpec, out: torch.Ten
     return out
 
 
-def _chain_stage3() -> bool:
-    """``AIKO_CHAIN3=1`` admits the stage-3 chain (256 -> 1024 + residual -> 256 on
-    ``conv_chain3.hip``; read at call time)."""
-    return __import__("os").environ.get("AIKO_CHAIN3", "0") == "1"
-
-
 def chain_ok(spec3: ConvSpec, spec1: ConvSpec) -> bool:
     """Can ``spec3`` (1x1 expansion, identity residual) and the next block's ``spec1`` (1x1
     reduction) run as one ``conv_chain`` launch?"""
     def one_by_one(s):
         return s.kind == "conv" and s.R == 1 and s.S == 1 and s.stride == 1 and s.K1 is None and s.bias is not None
     # (K1, N1) -> allowed N2.  Stage 2 -> 128 runs on conv_chain2.hip (both weight matrices
-    # resident in registers); stage 2 -> 256 (the stage-3 entry reduction) is still the
-    # register-staged kernel, which spills there (519 us against 200 us unchained): opt-in.
-    shapes = {(64, 256): (64, 128)}
-    if __import__("os").environ.get("AIKO_CHAIN2", "1") != "0":
-        shapes[(128, 512)] = (128,)
-    if _chain_stage2():
-        shapes[(128, 512)] = (128, 256)
-    if _chain_stage3():
-        shapes[(256, 1024)] = (256,)
+    # resident in registers).  Measured and removed (round 6 pruning, numbers in profiles/):
+    # stage 2 -> 256 on the register-staged kernel (spills: 519 vs 200 us unchained) and the
+    # stage-3 chain (conv_chain3: 179 vs 101 us, profiles/chain3_stage3_r5.txt).
+    shapes = {(64, 256): (64, 128), (128, 512): (128,)}
     k1, n1 = spec3.weight.shape[1], spec3.weight.shape[0]
     return (one_by_one(spec3) and one_by_one(spec1) and spec3.cin == k1 and (k1, n1) in shapes
             and spec1.cin == n1 and spec1.weight.shape[1] == n1 and spec1.cout in shapes[(k1, n1)]
@@ -867,8 +853,7 @@ def conv_chain(x: torch.Tensor, spec3: ConvSpec, residual: torch.Tensor | None, 
     spec (:func:`chain_dual_ok`): ``out_y = relu([x | x2] . W^T + b)``."""
     ok = chain_dual_ok(spec3, spec1) if x2 is not None else chain_ok(spec3, spec1)
     if not ok:
-        raise ValueError("conv_chain: shapes not eligible (chain_ok / chain_dual_ok); the stage-2 "
-                         "shapes need AIKO_CHAIN_STAGE2=1 (they spill registers and run slower)")
+        raise ValueError("conv_chain: shapes not eligible (chain_ok / chain_dual_ok)")
     torch.ops.aiko.conv_chain_out(x, spec3.weight, spec3.bias, residual, out_y, spec1.weight, spec1.bias,
                                   out_z, grid, x2)
     return out_y, out_z

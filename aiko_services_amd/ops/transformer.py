@@ -20,7 +20,7 @@ import torch
 
 from . import conv as _conv
 
-__all__ = ["Fp8Linear", "make_fp8_linear", "make_ln_fp8_linear", "linear_fp8_ln", "rowstats_mx",
+__all__ = ["Fp8Linear", "make_fp8_linear",
            "quantize_rows_ref", "linear_fp8", "rownorm",
            "attention", "ACT_NONE", "ACT_RELU", "ACT_SILU", "ACT_GELU", "FP8_MAX", "pick_tile"]
 
@@ -78,46 +78,6 @@ def dequant_fp8_linear(lin: Fp8Linear) -> torch.Tensor:
     if lin.ref_weight is not None:
         return lin.ref_weight.float()
     return lin.weight[:, :lin.k].view(FP8).float() * lin.scale.float()[:, None]
-
-
-def make_ln_fp8_linear(lin: Fp8Linear, gamma: torch.Tensor, beta: torch.Tensor, device=None) -> Fp8Linear:
-    """``lin`` with the preceding LayerNorm's affine folded in, for :func:`linear_fp8_ln` (ln 2):
-    ``LN(x) W^T + b = rstd * (x W'^T - mean * cs) + b'`` with ``W' = W diag(gamma)`` (re-quantised
-    per output channel), ``b' = b + W beta`` and ``cs[n] = sum_k W'[n, k]`` of the quantised W',
-    so the mean term removes exactly what the GEMM accumulates."""
-    w = dequant_fp8_linear(lin).cpu()
-    g, be = gamma.detach().float().cpu(), beta.detach().float().cpu()
-    b = w @ be
-    if lin.bias is not None:
-        b = b + lin.bias.float().cpu()
-    out = make_fp8_linear(w * g[None, :], b)
-    out.cs = out.ref_weight.sum(dim=1).contiguous()
-    return out.to(device) if device is not None else out
-
-
-def linear_fp8_ln(xq: torch.Tensor, x_mx: torch.Tensor, lin: Fp8Linear, st: torch.Tensor, ln: int,
-                  out: torch.Tensor | None = None, residual: torch.Tensor | None = None, act: int = ACT_NONE,
-                  out_mx: tuple | None = None, ln_d: int | None = None, eps: float = 1e-5) -> None:
-    """The two halves of a LayerNorm folded across a GEMM pair (``gemm_fp8.hip``, persistent
-    256 x 256 kernel), MX-fp8 activations ``xq`` / ``x_mx`` in both:
-      ln 1 (producer): ``out = xq W^T + bias + residual`` (bf16), its MX-fp8 copy ``out_mx`` and
-        the per-row partial sums / sums of squares of each 256-column tile into ``st`` [N/256, M, 2];
-      ln 2 (consumer, ``lin`` from :func:`make_ln_fp8_linear`): ``act(LN(x) W^T + b)`` from the
-        producer's MX copy of x and its ``st`` partials (``ln_d`` columns, ``eps``) -> bf16 ``out``
-        (act none) or MX-fp8 ``out_mx`` (act GELU)."""
-    yq, ysc = out_mx if out_mx is not None else (None, None)
-    if ln == 2 and lin.cs is None:
-        raise ValueError("linear_fp8_ln: the consumer needs a LayerNorm-folded linear (make_ln_fp8_linear)")
-    torch.ops.aiko.gemm_fp8_ln_out(xq, x_mx, lin.weight, lin.scale, lin.bias, residual, out, yq, ysc, st,
-                                   lin.cs if ln == 2 else None, int(ln), int(act),
-                                   int(ln_d if ln_d is not None else xq.shape[1]), float(eps),
-                                   _conv.zero_page(xq.device))
-
-
-def rowstats_mx(x: torch.Tensor, q: torch.Tensor, qsc: torch.Tensor, st: torch.Tensor) -> None:
-    """The ln-1 producer outputs for bf16 rows no GEMM wrote: MX-fp8 copy (``q``, ``qsc``) and row
-    sum / sum of squares as partial 0 of ``st`` [P, M, 2] (the other partials zeroed)."""
-    torch.ops.aiko.rowstats_mx_out(x, q, qsc, st)
 
 
 def quantize_rows_ref(x: torch.Tensor):
@@ -217,15 +177,14 @@ def _tune_fp8(key, launch, mx=False):
             cands.append((256, 128, 2))  # 8-wave LDS-DMA kernel (one workgroup per CU)
     if key[1] % 256 == 0:
         cands.append((256, 256, 3))      # 256 x 256 tile, 8 waves of 128 x 64 (MX in / out too)
-        if key[1] <= 3072 and os.environ.get("AIKO_FP8_PERSIST", "1") == "1" and (
-                (not key[4] and not key[6]) or (key[4] and key[6] and key[5] == 0 and not key[7]
-                                                  and os.environ.get("AIKO_FP8_V4MX", "1") == "1")):
+        if key[1] <= 3072 and (
+                (not key[4] and not key[6]) or (key[4] and key[6] and key[5] == 0 and not key[7])):
             # persistent 256 x 256, register-direct epilogue (no residual / MX input, or MX input +
             # residual with no activation: the out-projection / fc2 form).  Measured at
             # the 14-stream shapes (M = 21014, K = 768): qkv 62.8 -> 56.8 us (1.31 PF), fc1 + GELU +
             # MX out 104.8 -> 97.7 us against the best earlier kernel
             cands.append((256, 256, 4))
-        if key[1] <= 3072 and os.environ.get("AIKO_FP8_V5", "1") == "1" and (
+        if key[1] <= 3072 and (
                 (not key[4] and not key[6] and key[5] in (0, 3) and (key[5] == 3 or not key[7]))
                 or (key[4] and key[6] and key[5] == 0 and not key[7])):
             # persistent 128 x 256 (two row tiles per CU at N = 768): no residual / MX input, or the

@@ -271,7 +271,7 @@ def test_c2f_fused_matches_unfused(native, monkeypatch, rb):
     m = YOLOv8("n", device=DEV)
     g = torch.Generator().manual_seed(rb)
     x = (torch.randn(2, 160, 160, 32, generator=g) * 2).to(DEV, torch.bfloat16)
-    monkeypatch.setenv("AIKO_C2F_RB", str(rb))
+    monkeypatch.setattr(YOLOv8, "_c2f_rb", staticmethod(lambda H: rb))
     out_f = torch.full((2, 160, 160, 32), 7.0, dtype=torch.bfloat16, device=DEV)
     assert m._c2f_fused_ok(m.l2, x, out_f)
     m._run_c2f("l2f", m.l2, x, out_f)
@@ -293,7 +293,7 @@ def test_c2f_fused_wide_matches_unfused(native, monkeypatch, rb):
     m = YOLOv8("n", device=DEV)
     g = torch.Generator().manual_seed(rb)
     x = (torch.randn(2, 80, 80, 192, generator=g) * 2).to(DEV, torch.bfloat16)
-    monkeypatch.setenv("AIKO_C2F_RB80", str(rb))
+    monkeypatch.setattr(YOLOv8, "_c2f_rb", staticmethod(lambda H: rb))
     out_f = torch.full((2, 80, 80, 64), 7.0, dtype=torch.bfloat16, device=DEV)
     assert m._c2f_fused_ok(m.l15, x, out_f)
     m._run_c2f("l15f", m.l15, x, out_f)
@@ -315,7 +315,7 @@ def test_c2f_bneck_fused_matches_unfused(native, monkeypatch, rb):
     m = YOLOv8("n", device=DEV)
     g = torch.Generator().manual_seed(rb)
     x = (torch.randn(2, 80, 80, 64, generator=g) * 2).to(DEV, torch.bfloat16)
-    monkeypatch.setenv("AIKO_C2F_RB80", str(rb))
+    monkeypatch.setattr(YOLOv8, "_c2f_rb", staticmethod(lambda H: rb))
     out_f = torch.empty(2, 80, 80, 64, dtype=torch.bfloat16, device=DEV)
     m._run_c2f("l4f", m.l4, x, out_f)
     monkeypatch.setenv("AIKO_C2F_FUSED", "0")
@@ -326,30 +326,6 @@ def test_c2f_bneck_fused_matches_unfused(native, monkeypatch, rb):
     cos = torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()
     assert cos > 0.9995, cos
     assert (a - b).abs().max().item() < 0.05 * b.abs().max().item()
-
-
-def test_c2f_fused_s2_matches_unfused(native, monkeypatch):
-    """l1 (3x3 / 2, 16 -> 32) fused in front of the l2 C2f (c2f_fused_s2_kernel: a1 never leaves
-    LDS) against l1 as its own conv + the fused C2f, two images."""
-    from aiko_services_amd.models.yolov8 import YOLOv8
-    from aiko_services_amd.ops import conv as C
-    m = YOLOv8("n", device=DEV)
-    g = torch.Generator().manual_seed(3)
-    a0 = (torch.randn(2, 320, 320, 16, generator=g) * 2).to(DEV, torch.bfloat16)
-    out_f = torch.full((2, 160, 160, 32), 7.0, dtype=torch.bfloat16, device=DEV)
-    monkeypatch.setenv("AIKO_C2F_S2", "1")
-    assert m._l1l2_fused_ok(a0, out_f)
-    a, b = m.l2.m[0]
-    torch.ops.aiko.c2f_fused_s2_out(a0, m.l1.weight, m.l1.bias, m.l2.cv1.weight, m.l2.cv1.bias, a.weight, a.bias,
-                                    b.weight, b.bias, m.l2.cv2.weight, m.l2.cv2.bias, out_f, True, 40)
-    a1 = C.conv2d(a0, m.l1)
-    out_u = torch.empty_like(out_f)
-    m._run_c2f("l2u", m.l2, a1, out_u)
-    torch.cuda.synchronize()
-    x, y = out_f.float(), out_u.float()
-    cos = torch.nn.functional.cosine_similarity(x.flatten(), y.flatten(), dim=0).item()
-    assert cos > 0.9995, cos
-    assert (x - y).abs().max().item() < 0.05 * y.abs().max().item()
 
 
 @pytest.mark.parametrize("hw", [(80, 80), (40, 40), (20, 20)])
@@ -455,7 +431,6 @@ def test_yolo_decode_in_tail_matches_decode_kernel(native, monkeypatch):
     assert torch.equal(sf, sd)
     assert (bf - bd).abs().max().item() < 1e-3 * bd.abs().max().item()
     # whole detect(): fused decode vs the decode kernel (same front end for both)
-    monkeypatch.setattr(Y, "_STEM_L1", False)
     frames = torch.randint(0, 256, (2, 480, 640, 3), generator=g, dtype=torch.uint8).to(DEV)
     det_f, cnt_f = (t.clone() for t in m.detect(frames))
     monkeypatch.setattr(Y, "_DECODE_FUSED", False)
@@ -463,29 +438,3 @@ def test_yolo_decode_in_tail_matches_decode_kernel(native, monkeypatch):
     torch.cuda.synchronize()
     assert torch.equal(cnt_f, cnt_d)
     assert (det_f - det_d).abs().max().item() < 1e-2 * max(1.0, det_d.abs().max().item())
-
-
-@pytest.mark.parametrize("hw", [(480, 640), (640, 480)])
-def test_stem_l1_fused_matches_two_kernels(native, monkeypatch, hw):
-    """Letterbox + stem + l1 in one launch (stem_l1_kernel: a0 only in LDS) against the stem kernel
-    followed by the l1 conv, for landscape and portrait frames (letterbox bars on either axis)."""
-    from aiko_services_amd.models import yolov8 as Y
-    from aiko_services_amd.ops import conv as C
-    m = Y.YOLOv8("n", device=DEV)
-    monkeypatch.setattr(Y, "_STEM_L1", True)
-    g = torch.Generator().manual_seed(hw[0])
-    frames = torch.randint(0, 256, (2, hw[0], hw[1], 3), generator=g, dtype=torch.uint8).to(DEV)
-    assert m._stem_l1_ok(frames)
-    a1f = m.stem_l1_from_frames(frames).clone()
-    a1u = C.conv2d(m.stem_from_frames(frames), m.l1)
-    torch.cuda.synchronize()
-    a, b = a1f.float(), a1u.float()
-    cos = torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()
-    assert cos > 0.99995, cos
-    assert (a - b).abs().max().item() < 0.02 * b.abs().max().item()
-    # whole detect(): fused front vs stem kernel + l1 conv
-    det_f, cnt_f = (t.clone() for t in m.detect(frames))
-    monkeypatch.setattr(Y, "_STEM_L1", False)
-    det_u, cnt_u = (t.clone() for t in m.detect(frames))
-    torch.cuda.synchronize()
-    assert (cnt_f - cnt_u).abs().max().item() <= 2

@@ -390,115 +390,3 @@ def test_gemm_fp8_persistent_128(native, M, N, act, mxo):
     else:
         y = TR.linear_fp8(xq.to(DEV), xs.to(DEV), lin, act=act, tile=(128, 256, 5))
         assert _rel(y, full) < 5e-3
-
-
-@pytest.mark.parametrize("M", [1, 300, 2001])
-def test_rowstats_mx(native, M):
-    """The ln-1 outputs for rows no GEMM wrote: MX-fp8 copy (same bytes / E8M0 scales as the
-    reference quantiser) and the row sum / sum of squares as partial 0 (other partials zeroed)."""
-    from aiko_services_amd.ops import transformer as TR
-    g = torch.Generator().manual_seed(M)
-    d = 768
-    x = (torch.randn(M, d, generator=g) * 3 + 0.5).to(DEV, torch.bfloat16)
-    q, sc = TR.mx_buffers(M, d, DEV)
-    st = torch.full((3, M, 2), 9.0, device=DEV)
-    TR.rowstats_mx(x, q, sc, st)
-    rq, rsc = TR.mx_quantize_ref(x.float().cpu())
-    assert bool((sc.cpu()[:, :M] == rsc[:, :M]).all())
-    assert _rel(TR.mx_dequant(q.cpu(), sc.cpu()), TR.mx_dequant(rq, rsc)) < 1e-6
-    xf = x.float()
-    assert torch.allclose(st[0, :, 0], xf.sum(1), rtol=1e-4, atol=1e-2)
-    assert torch.allclose(st[0, :, 1], (xf * xf).sum(1), rtol=1e-4, atol=1e-2)
-    assert bool((st[1:] == 0).all())
-
-
-@pytest.mark.parametrize("M,K", [(300, 768), (2001, 3072), (21014, 768), (1, 256)])
-def test_gemm_fp8_ln_producer(native, M, K):
-    """ln 1 (out-proj / fc2 with the next LayerNorm folded downstream): bf16 y = A W^T + b + res
-    as the plain kernel, plus y's MX-fp8 copy (bit-equal to quantising y) and the per-row partial
-    sums / sums of squares of each 256-column tile (their sum = the row's statistics)."""
-    from aiko_services_amd.ops import transformer as TR
-    g = torch.Generator().manual_seed(M + K)
-    N = 768
-    lin = TR.make_fp8_linear(torch.randn(N, K, generator=g) / 20, torch.randn(N, generator=g) * 0.1, DEV)
-    x = torch.randn(M, K, generator=g) * torch.exp2(torch.randint(-4, 4, (M, K // 32), generator=g).float()
-                                                    ).repeat_interleave(32, dim=1)
-    q, sc = TR.mx_quantize_ref(x)
-    res = (torch.randn(M, N, generator=g) + 0.3).to(DEV, torch.bfloat16)
-    out = torch.full((M + 3, N), 7.0, dtype=torch.bfloat16, device=DEV)
-    oq, osc = TR.mx_buffers(M, N, DEV)
-    st = torch.zeros(N // 256, M, 2, device=DEV)
-    TR.linear_fp8_ln(q.to(DEV), sc.to(DEV), lin, st, 1, out=out[:M], residual=res, out_mx=(oq, osc))
-    torch.cuda.synchronize()
-    ref = TR.mx_dequant(q, sc).to(DEV) @ lin.ref_weight.T.to(DEV) + lin.bias + res.float()
-    y = out[:M]
-    assert _rel(y, ref) < 5e-3
-    assert bool((out[M:] == 7.0).all())
-    rq, rsc = TR.mx_quantize_ref(y.float().cpu())
-    assert bool((osc.cpu()[:, :M] == rsc[:, :M]).all())
-    assert _rel(TR.mx_dequant(oq.cpu(), osc.cpu()), TR.mx_dequant(rq, rsc)) < 1e-6
-    yf = y.float()
-    for t in range(N // 256):
-        blk = yf[:, 256 * t:256 * (t + 1)]
-        assert torch.allclose(st[t, :, 0], blk.sum(1), rtol=1e-4, atol=1e-2)
-        assert torch.allclose(st[t, :, 1], (blk * blk).sum(1), rtol=1e-4, atol=1e-2)
-
-
-@pytest.mark.parametrize("M,N,act", [(300, 2304, 0), (2001, 3072, 3), (21014, 2304, 0), (1, 768, 3)])
-def test_gemm_fp8_ln_consumer(native, M, N, act):
-    """ln 2 (qkv / fc1 after a folded LayerNorm): act(LN(x) W^T + b) from x's MX-fp8 copy, the
-    folded weights and the producer's row partials — against the fp32 LayerNorm + linear of the
-    dequantised weights (bf16 out for act none, MX-fp8 out for GELU as fc1 writes it)."""
-    from aiko_services_amd.ops import transformer as TR
-    g = torch.Generator().manual_seed(M + N)
-    d = 768
-    lin = TR.make_fp8_linear(torch.randn(N, d, generator=g) / 20, torch.randn(N, generator=g) * 0.1)
-    gamma, beta = 1.0 + 0.2 * torch.randn(d, generator=g), 0.1 * torch.randn(d, generator=g)
-    fold = TR.make_ln_fp8_linear(lin, gamma, beta, DEV)
-    x = ((torch.randn(M, d, generator=g) + 0.4) * (1 + torch.rand(M, 1, generator=g) * 4)).to(DEV, torch.bfloat16)
-    q, sc = TR.mx_buffers(M, d, DEV)
-    st = torch.zeros(3, M, 2, device=DEV)
-    TR.rowstats_mx(x, q, sc, st)
-    ref = F.layer_norm(x.float(), (d,), gamma.to(DEV), beta.to(DEV), 1e-5) @ lin.ref_weight.T.to(DEV) + lin.bias.to(DEV)
-    if act == 3:
-        ref = F.gelu(ref)
-        oq, osc = TR.mx_buffers(M, N, DEV)
-        TR.linear_fp8_ln(q, sc, fold, st, 2, act=3, out_mx=(oq, osc), ln_d=d)
-        got = TR.mx_dequant(oq.cpu(), osc.cpu()).to(DEV)
-        tol = 6e-2
-    else:
-        got = torch.full((M + 2, N), 7.0, dtype=torch.bfloat16, device=DEV)
-        TR.linear_fp8_ln(q, sc, fold, st, 2, out=got[:M], ln_d=d)
-        assert bool((got[M:] == 7.0).all())
-        got = got[:M]
-        tol = 6e-2
-    # MX-fp8 activations and re-quantised folded weights against an unquantised LayerNorm
-    # input and the original weights: a few % of relative error (e4m3 rounding of both operands)
-    assert _rel(got, ref) < tol
-    assert F.cosine_similarity(got.float().flatten(), ref.flatten(), dim=0).item() > 0.998
-
-
-def test_whisper_ln_fold_matches_unfolded(native, monkeypatch):
-    """The folded encoder (AIKO_WHISPER_LN_FOLD=1) against the row-norm-pass encoder of the same weights, and
-    both against the fp32 reference; and a weight reload re-derives the folded linears."""
-    from aiko_services_amd.models.whisper import WhisperEncoder
-    monkeypatch.setenv("AIKO_WHISPER_LN_FOLD", "1")
-    enc = WhisperEncoder("small", device=DEV)
-    assert enc.ln_fold
-    g = torch.Generator().manual_seed(5)
-    audio = (0.1 * torch.randn(3, 160000, generator=g)).to(DEV)
-    y = enc.encode(audio).float().clone()
-    enc.ln_fold = False
-    y0 = enc.encode(audio).float().clone()
-    enc.ln_fold = True
-    ref = enc.reference_encode(audio)
-    for a in (y, y0):
-        cos = F.cosine_similarity(a.flatten(1), ref.flatten(1), dim=1)
-        assert bool((cos > 0.99).all()), cos.tolist()
-    assert F.cosine_similarity(y.flatten(), y0.flatten(), dim=0).item() > 0.995
-    # reload (different weights) -> the folded linears follow
-    other = WhisperEncoder("small", seed=3, device=DEV)
-    enc.load_state_dict(other.state_dict())
-    y1 = enc.encode(audio).float()
-    y2 = other.encode(audio).float()
-    assert F.cosine_similarity(y1.flatten(), y2.flatten(), dim=0).item() > 0.999
