@@ -1475,6 +1475,18 @@ class PipelineImpl(Pipeline):
                                            {"diagnostic": diagnostic}))
             self.destroy_stream(str(key[0]), use_thread_local=False)
 
+    def _rejoin_deadline(self, element_name, element_instance):
+        """``rejoin_timeout`` after a stage lost its last member: still nobody back -> absent."""
+        node = self.pipeline_graph.get_node(element_name)
+        replicas = node.element if isinstance(node.element, RemoteReplicas) else None
+        if replicas is None or not replicas.awaiting or replicas.members:
+            return
+        replicas.awaiting = False
+        self.logger.warning(f"remote {element_name}: no replica rejoined: marking it absent")
+        element_instance.set_remote_absent(True)
+        node.element = element_instance
+        self._update_lifecycle_state()
+
     def _replica_lost_rank(self, rank):
         """A hop peer failed (transport error): drop it from every remote element."""
         for service_name, (name, instance, replicas) in list(self.remote_pipelines.items()):
@@ -1508,6 +1520,13 @@ class PipelineImpl(Pipeline):
             # (supervised: the dead rank is restarted — its frames wait for it, up to hop_timeout)
             replicas.awaiting = not replicas.members
             node.element = replicas
+            if replicas.awaiting:
+                # bounded: if no member is back by rejoin_timeout (the supervisor gave up, or the
+                # restart failed) the element is absent again, so frames fail at once instead of
+                # each waiting out hop_timeout
+                limit = self._param_float("rejoin_timeout", 120.0)
+                self._post_message(ActorTopic.IN, "rejoin_deadline", [element_name, element_instance],
+                                   delay=limit, target_function=self._rejoin_deadline)
         else:
             element_instance.set_remote_absent(True)
             node.element = element_instance
