@@ -187,7 +187,9 @@ class FrameUpload(GpuPipelineElement):
     def __init__(self, context):
         context.set_protocol("frame_upload:0")
         super().__init__(context)
-        self.pool_slots = max(2, _int(self.get_parameter("pool", 6)[0], 6))
+        pool, explicit = self.get_parameter("pool", 6)
+        self.pool_slots = max(2, _int(pool, 6))
+        self.pool_explicit = bool(explicit)
         self.staging_sets = max(2, _int(self.get_parameter("staging", 4)[0], 4))
         self._pools = {}
         self._staging = {}
@@ -229,12 +231,30 @@ class FrameUpload(GpuPipelineElement):
         ring["current"] = i
         return host
 
+    def _credit_window(self) -> int:
+        """Frames a replicated / remote plan keeps in flight: 2 x hop depth x hop_batch x
+        members (the engine's default frame window), 0 without remote elements."""
+        pl = self.pipeline
+        if pl is None or not getattr(pl, "remote_pipelines", None):
+            return 0
+        from ...parallel import hop as _hop
+        hop = _hop.plane()
+        depth = hop.depth if hop is not None else 4
+        return 2 * depth * pl.hop_batch * max(1, pl._remote_member_count())
+
+    def _size_pool(self):
+        # without an explicit ``pool`` the slots follow the plan's credit window, so a rank-0
+        # ingest feeding k replicas keeps every replica busy (ADVICE r5: 6 slots capped them all)
+        if not self.pool_explicit:
+            self.pool_slots = max(self.pool_slots, self._credit_window())
+        if self.pipeline is not None and hasattr(self.pipeline, "limit_frames"):
+            self.pipeline.limit_frames(self.name, self.pool_slots)
+
     def start_stream(self, stream, stream_id):
         # each frame holds one upload slot until it completes (longer when a hop sends the slot
         # zero-copy): the pipeline's frame window must not exceed the slots, or the actor would
         # wait in acquire() for a slot only a later response on this same thread frees
-        if self.pipeline is not None and hasattr(self.pipeline, "limit_frames"):
-            self.pipeline.limit_frames(self.name, self.pool_slots)
+        self._size_pool()
         return StreamEvent.OKAY, None
 
     def process_frame(self, stream, images):
@@ -250,6 +270,7 @@ class FrameUpload(GpuPipelineElement):
         nbytes = shape[0] * shape[1] * shape[2] * 3
         pool = self._pools.get(shape)
         if pool is None:
+            self._size_pool()                     # the plan's members are discovered by now
             pool = self._pools[shape] = FramePool(self.pool_slots, nbytes, device=self.device)
         slot = pool.acquire(30.0)
         if slot < 0:
