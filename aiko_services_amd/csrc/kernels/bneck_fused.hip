@@ -478,279 +478,6 @@ __global__ __launch_bounds__(64 * kBnNW, 1) void bneck_fused_kernel(BnParams p) 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// ---------------------------------------------------------------------------------------------
-// Half-row variant (round 6): the same block, but each workgroup streams ONE HALF of every output
-// row (28 of the 56 pixels, plus a one-pixel halo column on each side), so an x row image is
-// 30 pixels (16 KB instead of 30 KB) and the LDS holds an 8-slot x ring instead of 4.  The full-
-// row kernel keeps ONE x row in flight per CU (rows vc, vc + 1 are still needed as conv3's
-// residual, vc + 2 is conv1's input: 4 slots leave room for one DMA) — 28 KB per CU, which its
-// DMA-only ablation measured at 3.7 TB/s, 54 % of the 6.8 TB/s read roof
-// (profiles/hbm_roof_r6.md).  Here rows vc + 3 .. vc + 7 are in flight: 5 half rows, 80 KB per
-// CU.  The pixel-side MFMA efficiency is unchanged (32 slots per 28 outputs, as 64 per 56): a
-// workgroup is 4 channel slices x 2 pixel tiles of 16 slots, one tile per wave.
-//   pixel slot s of a half row <-> image pixel p0 - 1 + s (p0 = 0 or 28); output slots 1 .. 28
-//   are stored; t1 slots whose pixel is outside the image (the 3x3's zero padding) and slots
-//   30, 31 are written as zeros.
-// Work decomposition: 2 x G2 workgroups (G2 row groups; the two halves of a row group are
-// adjacent logical ids, so on one XCD), each streaming the B * H rows of its group's contiguous
-// range through the same virtual-row sequence (zero halo rows between images) as the full-row
-// kernel.
-constexpr int kHbS = 32;                 // pixel slots per t1 / t2 row plane
-constexpr int kHbX = 30;                 // pixels per x row image (28 + 2 halo columns)
-constexpr int kHbTU = 8 * kHbS + 8;      // t1 / t2 row: guard unit, 8 planes x 32 slots, tail, pad
-constexpr int kHbTB = kHbTU * 16;
-constexpr int kHbRing = 8;               // x ring slots (rows vc .. vc + 7)
-
-template <int CIN>
-__global__ __launch_bounds__(64 * kBnNW, 1) void bneck_half_kernel(BnParams p) {
-  constexpr bool DUAL = CIN == 64;
-  constexpr int NC = CIN / 8;
-  constexpr int XPU = NC + 2;                      // pixel pitch (units): 2 mod 8, conflict-free
-  constexpr int XU = kHbX * XPU;
-  constexpr int XB = XU * 16;
-  constexpr int NI = (XU + 63) / 64;               // 1-KB DMA wave-instructions per x row
-  constexpr int DQ = (NI + kBnNW - 1) / kBnNW;
-  constexpr int KS1 = CIN / 32, KS2 = 9 * kBnMid / 32, K3 = DUAL ? 2 * kBnMid : kBnMid, KS3 = K3 / 32;
-  constexpr int X_BYTES = kHbRing * XB, T1_BYTES = 3 * kHbTB;
-  constexpr int LDS_BYTES = X_BYTES + T1_BYTES + kHbTB;
-  // conv1 / conv3 read x units past a row image for slots 30, 31 (discarded outputs): for the
-  // last ring slot they fall into the t1 ring, still inside the allocation
-  static_assert(LDS_BYTES <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
-  unsigned char* const xr = lds;
-  unsigned char* const t1r = lds + X_BYTES;
-  unsigned char* const t2b = lds + X_BYTES + T1_BYTES;
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int cg = wv & 3;                           // channel slice
-  const int pt = wv >> 2;                          // pixel tile (slots 16 pt .. 16 pt + 15)
-  const int fr = lane & 15, fq = lane >> 4;
-
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  const int half = lid & 1, grp = lid >> 1;
-  const int p0 = 28 * half;
-  const int H = p.H, HV = H + 2;
-  const int R0 = grp * p.rows_per_wg + min(grp, p.rows_rem);
-  const int nrows = p.rows_per_wg + (grp < p.rows_rem ? 1 : 0);
-  if (nrows <= 0) return;
-  const int n0 = R0 / H, h0 = R0 - n0 * H;
-
-  // ---- weights into registers (one channel slice per wave), biases
-  bf16x8 w1f[KS1], w2f[KS2], w3f[4][KS3];
-#pragma unroll
-  for (int ks = 0; ks < KS1; ++ks)
-    w1f[ks] = *reinterpret_cast<const bf16x8*>(p.w1 + (16 * cg + fr) * CIN + 32 * ks + 8 * fq);
-#pragma unroll
-  for (int ks = 0; ks < KS2; ++ks)
-    w2f[ks] = *reinterpret_cast<const bf16x8*>(p.w2 + (16 * cg + fr) * (9 * kBnMid) + 32 * ks + 8 * fq);
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int row = 64 * cg + 32 * (t >> 1) + 8 * (fr >> 2) + 4 * (t & 1) + (fr & 3);
-#pragma unroll
-    for (int ks = 0; ks < KS3; ++ks)
-      w3f[t][ks] = *reinterpret_cast<const bf16x8*>(p.w3 + row * K3 + 32 * ks + 8 * fq);
-  }
-  f32x4 bias1, bias2;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    bias1[e] = p.b1[16 * cg + 4 * fq + e];
-    bias2[e] = p.b2[16 * cg + 4 * fq + e];
-  }
-  f32x4 bias3[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) bias3[t][e] = p.b3[64 * cg + 32 * (t >> 1) + 8 * fq + 4 * (t & 1) + e];
-  bf16x8 eye[2];
-#pragma unroll
-  for (int tp = 0; tp < 2; ++tp)
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      eye[tp][i] = (fq == (fr >> 2) && i == 4 * tp + (fr & 3)) ? (bf16_t)1.0f : (bf16_t)0.0f;
-  if (tid < 3) *reinterpret_cast<u32x4*>(t1r + tid * kHbTB) = u32x4{0u, 0u, 0u, 0u};   // guard units
-  __builtin_amdgcn_s_waitcnt(0x0f70);              // vmcnt(0): weight loads done
-
-  // ---- per-lane DMA source offsets: unit u <- (slot s, chunk c) = image pixel p0 - 1 + s
-  int goff[DQ];
-  bool gok[DQ];
-#pragma unroll
-  for (int q = 0; q < DQ; ++q) {
-    const int u = (wv + kBnNW * q) * 64 + lane;
-    const int s = u / XPU, c = u - (u / XPU) * XPU;
-    const int pix = p0 - 1 + s;
-    goff[q] = min(max(pix, 0), kBnW - 1) * CIN * 2 + min(c, NC - 1) * 16;
-    gok[q] = u < XU && wv + kBnNW * q < NI && c < NC && pix >= 0 && pix < kBnW;
-  }
-  int dw = 0;
-#pragma unroll
-  for (int q = 0; q < DQ; ++q) dw += wv + kBnNW * q < NI ? 1 : 0;
-
-  const int slot = 16 * pt + fr;                   // this lane's pixel slot
-  const int pix = p0 - 1 + slot;                   // its image pixel
-  const bool t1_zero = pix < 0 || pix >= kBnW || slot >= kHbX;
-  const bool y_store = slot >= 1 && slot <= 28;
-  const int xlb = (slot * XPU + fq) * 16;
-  const int tlb = (fq * kHbS + slot) * 16;
-  const int twb = ((2 * cg + (fq >> 1)) * kHbS + slot) * 16 + (fq & 1) * 8;
-
-  constexpr long XROWG = (long)kBnW * CIN * 2;
-  const int nl = (R0 + nrows - 1) / H;
-  const int vlast = (nl - n0) * HV + (R0 + nrows - 1 - nl * H) + 2;
-  int ops = 0;
-  int mk[kHbRing];
-#pragma unroll
-  for (int i = 0; i < kHbRing; ++i) mk[i] = -1;
-  int vdma = h0, dn = n0, dr = h0 - 1;
-  auto set_mk = [&](int v, int m) {
-#pragma unroll
-    for (int i = 0; i < kHbRing; ++i)
-      if ((v & (kHbRing - 1)) == i) mk[i] = m;
-  };
-  auto get_mk = [&](int v) {
-    int m = -1;
-#pragma unroll
-    for (int i = 0; i < kHbRing; ++i)
-      if ((v & (kHbRing - 1)) == i) m = mk[i];
-    return m;
-  };
-  auto dma_next = [&]() {
-    const int v = vdma++;
-    int m = -1;
-    if (dr >= 0 && dr < H) {
-      const unsigned char* src = reinterpret_cast<const unsigned char*>(p.x) + ((long)dn * H + dr) * XROWG;
-      unsigned char* dst = xr + (v & (kHbRing - 1)) * XB;
-#pragma unroll
-      for (int q = 0; q < DQ; ++q) {
-        const int j = wv + kBnNW * q;
-        if (gok[q]) glds16_asm(src + goff[q], dst + j * 1024);
-      }
-      ops += dw;
-      m = ops;
-    }
-    if (++dr > H) {
-      dr = -1;
-      ++dn;
-    }
-    set_mk(v, m);
-  };
-  auto row_valid = [&](int v) { return get_mk(v) >= 0; };
-  auto wait_row = [&](int v) {
-    const int m = get_mk(v);
-    if (m >= 0) bn_vm_wait(__builtin_amdgcn_readfirstlane(ops - m));
-  };
-
-  auto conv1 = [&](int k) {
-    unsigned char* t1w = t1r + (k % 3) * kHbTB + twb;
-    if (!row_valid(k)) {
-      *reinterpret_cast<uint2*>(t1w + 16) = uint2{0u, 0u};
-      return;
-    }
-    const unsigned char* xs = xr + (k & (kHbRing - 1)) * XB + xlb;
-    f32x4 a1;
-#pragma unroll
-    for (int ks = 0; ks < KS1; ++ks) {
-      const bf16x8 bf = *reinterpret_cast<const bf16x8*>(xs + (4 * ks) * 16);
-      a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[ks], bf, ks == 0 ? bias1 : a1, 0, 0, 0);
-    }
-    bn_pipeline<KS1, 1, KS1 >= 4 ? 3 : 1>();
-    uint2 pk{bn_relu2(pack2(a1[0], a1[1])), bn_relu2(pack2(a1[2], a1[3]))};
-    if (t1_zero) pk = uint2{0u, 0u};
-    *reinterpret_cast<uint2*>(t1w + 16) = pk;
-  };
-
-  f32x4 a2;
-  auto conv2 = [&](int vc) {
-    const unsigned char* tr[3] = {t1r + ((vc - 1) % 3) * kHbTB + tlb, t1r + (vc % 3) * kHbTB + tlb,
-                                  t1r + ((vc + 1) % 3) * kHbTB + tlb};
-#pragma unroll
-    for (int ks = 0; ks < KS2; ++ks) {
-      const int tap = ks >> 1, dy = tap / 3, dx = tap % 3 - 1, hk = ks & 1;
-      const bf16x8 bf = *reinterpret_cast<const bf16x8*>(tr[dy] + (1 + 4 * kHbS * hk + dx) * 16);
-      a2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f[ks], bf, ks == 0 ? bias2 : a2, 0, 0, 0);
-    }
-    bn_pipeline<KS2, 1, 4>();
-    const uint2 pk{bn_relu2(pack2(a2[0], a2[1])), bn_relu2(pack2(a2[2], a2[3]))};
-    *reinterpret_cast<uint2*>(t2b + twb + 16) = pk;
-  };
-
-  auto conv3 = [&](int vc, int n, int r) {
-    const unsigned char* xres = xr + (vc & (kHbRing - 1)) * XB + xlb;
-    const unsigned char* t2r = t2b + tlb;
-    bf16_t* yrow = p.y + ((long)(n * H + r) * kBnW + pix) * kBnOut + 64 * cg + 8 * fq;
-    bf16x8 bf[KS3];
-#pragma unroll
-    for (int ks = 0; ks < KS3; ++ks)
-      bf[ks] = ks < 2 ? *reinterpret_cast<const bf16x8*>(t2r + (1 + 4 * kHbS * ks) * 16)
-                      : *reinterpret_cast<const bf16x8*>(xres + (4 * (ks - 2)) * 16);
-    bf16x8 rv[2];
-    if constexpr (!DUAL) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) rv[h] = *reinterpret_cast<const bf16x8*>(xres + (8 * cg + 4 * h) * 16);
-    }
-    f32x4 a3[4];
-#pragma unroll
-    for (int ks = 0; ks < KS3; ++ks)
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-        a3[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w3f[t][ks], bf[ks], ks == 0 ? bias3[t] : a3[t], 0, 0, 0);
-    if constexpr (!DUAL) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t) a3[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(eye[t & 1], rv[t >> 1], a3[t], 0, 0, 0);
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const u32x4 ov{bn_relu2(pack2(a3[2 * h][0], a3[2 * h][1])), bn_relu2(pack2(a3[2 * h][2], a3[2 * h][3])),
-                     bn_relu2(pack2(a3[2 * h + 1][0], a3[2 * h + 1][1])),
-                     bn_relu2(pack2(a3[2 * h + 1][2], a3[2 * h + 1][3]))};
-      if (y_store) bn_store16(yrow + 32 * h, ov);
-    }
-    ops += 2;
-  };
-
-  // ---- prologue: virtual rows h0 .. h0 + 7 in flight, t1 rows of h0 .. h0 + 2
-  while (vdma <= min(h0 + kHbRing - 1, vlast)) dma_next();
-  wait_row(min(h0 + 2, vlast));
-  wait_row(h0 + 1);
-  wait_row(h0);
-  bn_barrier();
-  conv1(h0);
-  conv1(h0 + 1);
-  if (h0 + 2 <= vlast) conv1(h0 + 2);
-  bn_barrier();
-
-  // ---- one output row per iteration: A = conv2(vc); B = conv1(vc + 2) and conv3(vc).  The x
-  //      slot of a row is re-issued only after conv3 read it (rows vc .. vc + 7 at the top)
-  int n = n0, r = h0, vc = h0 + 1;
-  for (int j = 0; j < nrows; ++j) {
-    if (j > 0) {
-      if (++r == H) {
-        r = 0;
-        ++n;
-        vc += 3;
-      } else {
-        ++vc;
-      }
-    }
-    while (vdma <= min(vc + kHbRing - 1, vlast)) dma_next();
-    if (j > 0 && r == 0) {                         // image boundary: t1 rows of vc and vc + 1 first
-      wait_row(vc + 1);
-      wait_row(vc);
-      bn_barrier();
-      conv1(vc);
-      conv1(vc + 1);
-      bn_barrier();
-    }
-    conv2(vc);
-    if (vc + 2 <= vlast) wait_row(vc + 2);
-    bn_barrier();
-    if (vc + 2 <= vlast) conv1(vc + 2);
-    conv3(vc, n, r);
-    bn_barrier();
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
 }  // namespace
 
 }  // namespace aiko
@@ -794,22 +521,6 @@ extern "C" int aiko_bneck_fused(const void* x, const void* w1, const float* b1, 
   p.dbg = dbg;
   const char* mode = getenv("AIKO_BN_MODE");
   p.mode = mode ? atoi(mode) : 0;
-  static const bool half_rows = [] {
-    const char* v = getenv("AIKO_BN_HALF");
-    return !v || atoi(v) != 0;
-  }();
-  if (half_rows && !dbg && p.mode == 0) {
-    // half-row kernel: G / 2 row groups, two workgroups (left / right half) each
-    int G2 = (grid > 0 ? grid : bn_cu_count()) / 2;
-    G2 = G2 < 1 ? 1 : (G2 < R ? G2 : R);
-    p.rows_per_wg = R / G2;
-    p.rows_rem = R % G2;
-    if (cin == 256)
-      hipLaunchKernelGGL(bneck_half_kernel<256>, dim3(2 * G2), dim3(64 * kBnNW), 0, stream, p);
-    else
-      hipLaunchKernelGGL(bneck_half_kernel<64>, dim3(2 * G2), dim3(64 * kBnNW), 0, stream, p);
-    return (int)hipGetLastError();
-  }
   if (cin == 256)
     hipLaunchKernelGGL(bneck_fused_kernel<256>, dim3(G), dim3(64 * kBnNW), 0, stream, p);
   else
