@@ -999,6 +999,7 @@ class PipelineImpl(Pipeline):
             if not metrics:
                 metrics["pipeline_elements"] = {}
                 metrics["time_pipeline_start"] = time.time()
+                metrics["perf_pipeline_start"] = time.perf_counter()   # trace spans: one clock
             tracer = _trace.get_tracer()
             faults = _fault.active()
             frame_data_out = {} if new_frame else frame_data_in
@@ -1087,7 +1088,7 @@ class PipelineImpl(Pipeline):
                     faults.frame_completed()
                 if tracer is not None:
                     end = time.perf_counter()
-                    tracer.span(f"frame {self.name}", end - latency, end, cat="frame",
+                    tracer.span(f"frame {self.name}", metrics.get("perf_pipeline_start", end - latency), end, cat="frame",
                                 args={"stream_id": stream.stream_id, "frame_id": frame_id})
                 stream_info = {"stream_id": stream.stream_id, "frame_id": frame_id, "state": stream.state}
                 if stream.queue_response is not None:
