@@ -193,20 +193,6 @@ NARROW_TILES = ((128, 32), (256, 32), (64, 64), (128, 64))   # Cout <= 32 (YOLO 
 _tile_cache: dict = {}          # geometry key -> (bm, bn), filled by autotune()
 _tuning = False
 _TUNE_VERBOSE = __import__("os").environ.get("AIKO_TUNE_VERBOSE", "0") == "1"
-# cold-cache tuning: before every timed trial a 512 MB buffer is rewritten, so the candidate reads
-# its operands from HBM as it does inside the pipeline (the previous layer's output does not stay
-# in the 256 MB Infinity Cache) instead of from the MALL warmed by the trial before it
-_TUNE_COLD = __import__("os").environ.get("AIKO_TUNE_COLD", "0") == "1"
-_flush_buf = None
-
-
-def _cache_flush():
-    global _flush_buf
-    if _flush_buf is None:
-        _flush_buf = torch.empty(512 << 20, dtype=torch.uint8, device="cuda")
-    _flush_buf.fill_(1)
-
-
 class autotune:
     """Context manager: while active, every conv whose geometry has no cached tile times each
     candidate tile on the GPU (3 runs, HIP events) and keeps the fastest — like a conv
@@ -539,8 +525,6 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, p
         launch(t)
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
         for e0, e1 in evs:
-            if _TUNE_COLD:
-                _cache_flush()
             e0.record()
             launch(t)
             e1.record()
