@@ -92,11 +92,11 @@ int aiko_attn_fwd(const void* q, const void* k, const void* v, void* o, int ldq,
 int aiko_logmel(const float* audio, int B, int N, const float* mel, int n_mels, const int* mel_range,
                 int n_fft, int hop, int F, float* logmel, int* gmax, void* dst, int rows, int pad, int ld,
                 hipStream_t stream);
-size_t aiko_topk_nms_workspace(int B);
 int aiko_topk_nms(const void* boxes, const float* scores, const int* cls, int B, int A,
                   int max_cand, int max_det, float conf, float iou, float max_wh, float gain,
                   float pad_l, float pad_t, float img_w, float img_h, float* det, int* count,
                   void* workspace, hipStream_t stream);
+size_t aiko_topk_nms_workspace(int B);
 int aiko_avgpool(const void* x, void* y, int B, int HW, int C, hipStream_t stream);
 int aiko_mean_rows_f32(const void* x, float* y, int B, int T, int C, long ldb, hipStream_t stream);
 int aiko_zero_border_rows(void* x, int B, int rows, int C, hipStream_t stream);
@@ -918,13 +918,18 @@ void topk_nms_out(const at::Tensor& boxes, const at::Tensor& scores, const at::T
               "aiko.topk_nms_out: 1 <= max_candidates, max_det <= 1024");
   TORCH_CHECK(count.scalar_type() == at::kInt && count.numel() == B && count.is_contiguous(),
               "aiko.topk_nms_out: count int32 [B]");
-  // workspace from the caching allocator (graph-capture safe: a captured graph keeps its pool)
-  at::Tensor ws = at::empty({(int64_t)aiko_topk_nms_workspace((int)B)},
-                            scores.options().dtype(at::kByte));
+  // G > 1 workgroups per image: mask-block workspace + zeroed counters from the caching
+  // allocator (graph-capture safe: the memset is a node of the captured graph)
+  const size_t wsb = aiko_topk_nms_workspace((int)B);
+  at::Tensor ws;
+  if (wsb) {
+    ws = at::empty({(int64_t)wsb}, scores.options().dtype(at::kByte));
+    ws.narrow(0, (int64_t)wsb - 4 * B, 4 * B).zero_();
+  }
   check_launch(aiko_topk_nms(boxes.data_ptr(), scores.data_ptr<float>(), cls.data_ptr<int>(), B, A,
                              max_cand, max_det, params[0], params[1], params[2], params[3], params[4],
                              params[5], params[6], params[7], det.data_ptr<float>(),
-                             count.data_ptr<int>(), ws.data_ptr(), cur_stream()),
+                             count.data_ptr<int>(), wsb ? ws.data_ptr() : nullptr, cur_stream()),
                "topk_nms");
 }
 

@@ -1,34 +1,17 @@
 // Detection kernels for gfx950 (YOLOv8 family): nearest upsample into concat slices, the
 // anchor-free DFL box decode, and a fused per-image "top-k candidates + class-aware NMS".
 //
-// top-k + NMS — three kernels.  Measured (rocprofv3, YOLOv8-n bench batch: B=64 x 8400 anchors,
-// random weights, 1024 candidates per image): the former single 1024-thread workgroup per
-// image took 246 us (IoU bitmask 130 us on 64 CUs, shuffle-bound greedy scan 86 us); now
-// nms_select 24 us + nms_mask 31-32 us + nms_greedy 26 us = 83 us (scripts/nms_phases.py,
-// per-phase stops: scripts/nms_stop.sh):
-//   nms_select (one workgroup per image): keys (5 us), radix select (2 x 12-bit passes over
-//              key - min key, skipped when every live key is a candidate), compaction, sort
-//              (per-wave register bitonic + merge by rank), sorted candidates to a workspace;
-//   nms_mask   (B x 136 waves, balanced): the IoU bitmask over the whole GPU, 4-compare overlap
-//              gate before the exact IoU, plus the transposed diagonal words;
-//   nms_greedy (one workgroup per image): upper-triangle masks staged in LDS (padded rows), the
-//              scan per 64-candidate word as a ballot fixed point, output mapping.
-// Phases:
-//   1. scores above the confidence threshold -> 32-bit keys (float bits are monotone for
-//      positive floats) in LDS;
-//   2. radix select finds the K-th largest key, K = min(max_candidates, #above conf);
-//   3. deterministic compaction (block-wide exclusive scan, ties -> lowest anchor index) and a
-//      sort of the <= 1024 candidates by (score desc, index asc);
-//   4. the IoU suppression bitmask (n x ceil(n/64) 64-bit words) — boxes are offset by
-//      class * max_wh so one pass is class-aware;
-//   5. one wave scans the bitmask 64 candidates at a time: inside a word the suppression chain
-//      is resolved from the diagonal words, then the kept rows' words are OR-ed into the later
-//      words lane-parallel; stops at max_det;
-//   6. kept boxes are mapped back from letterbox to frame coordinates, clipped, and written
-//      as fixed-size [max_det, 6] rows (x1, y1, x2, y2, score, class) + a count, so results can
-//      be all-gathered over RCCL without a size exchange.
-// AIKO_NMS_STOP=<phase> (profiling only) ends the kernels early: 1-4 inside nms_select (then
-// nothing else runs), 5 / 6 inside nms_greedy.
+// top-k + NMS: one launch, up to 4 workgroups per image, the IoU bitmask only where a class run
+// needs it (nms_fused_kernel).  History (YOLOv8-n bench batch, B=64 x 8400 anchors, random
+// weights, 1024 candidates per image): one workgroup per image over the full bitmask 246 us
+// (round 2); three kernels with the full bitmask on the whole GPU, 24 + 31 + 26 = 83 us
+// (rounds 3-5; profiles/nms_r2.md); this kernel 88 us at 4 workgroups per image on that input
+// (3 classes among the candidates, 625 in the largest), far less where classes are many
+// (profiles/nms_r6.md).
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+
 #include "common.h"
 
 namespace aiko {
@@ -229,6 +212,7 @@ constexpr int kNmsThreads = 1024;
 constexpr int kMaxCand = 1024;
 constexpr int kMaxAnchors = 32768;
 constexpr int kMaskWords = kMaxCand / 64;  // 16
+constexpr int kMaxItems = kMaskWords * (kMaskWords + 1) / 2;   // 136 (row block, word) pairs
 
 struct NmsParams {
   const float4* boxes;
@@ -239,24 +223,17 @@ struct NmsParams {
   float gain, pad_l, pad_t, img_w, img_h;  // letterbox -> frame mapping
   float* det;   // [B, max_det, 6]
   int* count;   // [B]
-  int stop;     // profiling: end the kernels early at phase `stop` (99 = run everything)
+  double thr_m; // the division-free IoU threshold (mask_word)
+  int thr_tie;
+  // G > 1: G workgroups per image (each repeats the selection and computes every G-th mask
+  // block into gmask / glow; the last to finish, counted in gcount, runs the scan)
+  int G;
+  unsigned long long* gmask;   // [B][136][64]
+  unsigned long long* glow;    // [B][1024]
+  int* gcount;                 // [B], zero before the launch; the last arriver re-zeroes it
 };
 
-__device__ __forceinline__ unsigned long long shfl64(unsigned long long v, int src) {
-  const unsigned lo = __shfl((unsigned)(v & 0xffffffffull), src, 64);
-  const unsigned hi = __shfl((unsigned)(v >> 32), src, 64);
-  return ((unsigned long long)hi << 32) | lo;
-}
-
-__device__ __forceinline__ float box_iou(float4 a, float4 b) {
-  const float iw = fmaxf(0.f, fminf(a.z, b.z) - fmaxf(a.x, b.x));
-  const float ih = fmaxf(0.f, fminf(a.w, b.w) - fmaxf(a.y, b.y));
-  const float inter = iw * ih;
-  const float area_a = (a.z - a.x) * (a.w - a.y), area_b = (b.z - b.x) * (b.w - b.y);
-  return inter / (area_a + area_b - inter);
-}
-
-// block-wide exclusive scan of one int per thread (1024 threads = 16 waves)
+// block-wide exclusive scan of one int per thread (1024 threads = 16 waves); sh[0..31] scratch
 __device__ int block_exclusive_scan(int v, int* sh) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int x = v;
@@ -278,39 +255,184 @@ __device__ int block_exclusive_scan(int v, int* sh) {
     if (lane < 16) sh[16 + lane] = y - own;
   }
   __syncthreads();
-  return x - v + sh[16 + wave];
+  const int r = x - v + sh[16 + wave];
+  __syncthreads();                                 // sh reusable by the next scan
+  return r;
 }
 
-// Workspace of the three NMS kernels (global memory, per image b):
-//   ckey[b][1024] u64 sorted candidate keys, cbox[b][1024] class-offset boxes, n[b] count,
-//   mask[b][16][1024] u64 IoU suppression words, word-major (word w of row i at [w][i], so
-//   consecutive rows store coalesced); only words on / right of the diagonal are written.
-struct NmsWork {
-  unsigned long long* ckey;
-  float4* cbox;
-  int* n;
-  unsigned long long* mask;
-  unsigned long long* low;   // [b][16][1024]: diagonal word, bits k < i (suppressors of i)
+// Sort buf[0 .. NP) (NP a power of two <= 1024, unique non-zero keys, zero padding) descending
+// with all 1024 threads: a per-wave bitonic sort of 64 keys in registers (21 shuffle passes, no
+// barrier), then a merge by rank — a key's final position is its place in its own wave's list
+// plus, for each other list, the number of keys greater than it (7-step binary search of the
+// LDS copy; the 15 searches are independent).  Padding keys are not written back.
+__device__ void block_sort_desc(unsigned long long* buf, int NP) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  unsigned long long v = tid < NP ? buf[tid] : 0ull;
+  for (int size = 2; size <= 64; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const unsigned lo = __shfl_xor((unsigned)(v & 0xffffffffull), stride, 64);
+      const unsigned hi = __shfl_xor((unsigned)(v >> 32), stride, 64);
+      const unsigned long long c = ((unsigned long long)hi << 32) | lo;
+      const bool desc = size == 64 || (lane & size) == 0, lower = (lane & stride) == 0;
+      v = (desc == lower) ? (v > c ? v : c) : (v < c ? v : c);
+    }
+  }
+  __syncthreads();
+  buf[tid] = v;                                    // [wave][64] sorted descending
+  __syncthreads();
+  int rank = lane;
+  const int nl = (NP + 63) >> 6;
+#pragma unroll 4
+  for (int l = 0; l < nl; ++l) {
+    if (l == wave) continue;
+    const unsigned long long* L = buf + l * 64;
+    int pos = 0;
+#pragma unroll
+    for (int st = 32; st > 0; st >>= 1)
+      if (L[pos + st - 1] > v) pos += st;
+    rank += pos + (L[pos] > v ? 1 : 0);
+  }
+  __syncthreads();
+  if (v != 0ull) buf[rank] = v;
+  __syncthreads();
+}
+
+// v_min / v_max without the NaN canonicalisation fminf / fmaxf carry (two extra v_max per call):
+// box coordinates are finite
+__device__ __forceinline__ float vmin(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float vmax(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+struct IouThrHost {
+  double m;
+  bool tie_up;
 };
 
-// 1. keys, radix select, deterministic compaction and bitonic sort — one 1024-thread
-//    workgroup per image, keys in LDS; writes the sorted candidates to the workspace.
+__host__ inline IouThrHost iou_threshold(float t) {
+  const float s = nextafterf(t, __builtin_inff());
+  IouThrHost r;
+  r.m = ((double)t + (double)s) * 0.5;
+  uint32_t sb;
+  memcpy(&sb, &s, 4);
+  r.tie_up = (sb & 1u) == 0u;
+  return r;
+}
+
+// The reference's decision RN(inter / union) > t (fp32 division, fp32 threshold t >= 0) without
+// the division: with s = the next float above t and m = (t + s) / 2, RN(q) > t  <=>  q > m, or
+// q == m where m rounds to s (ties to even: s's mantissa even).  m has 25 significant bits and
+// union 24, so m * union is exact in double and the comparison inter <=> m * union is exact.
+// (Host side: iou_threshold() below fills NmsParams.thr_m / thr_tie.)
+//
+// IoU > thr bits of row box bi against the 64 column boxes in LDS (bit jj = column jj), one
+// fully unrolled pass: constant bit positions, broadcast LDS reads (FULL: all 64 columns valid,
+// no per-column guard; NEG: negative threshold, every pair tested with the reference's division).
+// A 4-compare overlap test on both axes gates the intersection; pairs of different classes
+// (max_wh apart) stop there.  Products and sums are the reference's roundings (the product is
+// made opaque before the union's subtraction: hipcc contracts a * b - c into an FMA even through
+// __fmul_rn / __fsub_rn), column areas come precomputed, so each bit equals the reference's
+// box_iou > thr.  The test is symmetric bit for bit (min / max and the area sum commute), so the
+// diagonal word's transposed half comes out of the same pass.
+template <bool FULL, bool NEG>
+__device__ __forceinline__ unsigned long long mask_word(const float4* col, const float* carea, float4 bi,
+                                                        float area_i, int je, double thr_m, bool thr_tie,
+                                                        float thr) {
+  unsigned long long hit = 0ull;
+#pragma unroll
+  for (int jj = 0; jj < 64; ++jj) {
+    if (FULL || jj < je) {                                  // wave-uniform
+      const float4 c = col[jj];
+      if (NEG) {
+        const float iw = fmaxf(0.f, __fsub_rn(fminf(bi.z, c.z), fmaxf(bi.x, c.x)));
+        const float ih = fmaxf(0.f, __fsub_rn(fminf(bi.w, c.w), fmaxf(bi.y, c.y)));
+        float inter = __fmul_rn(iw, ih);
+        asm volatile("" : "+v"(inter));                     // no FMA contraction into the union
+        const float iou = __fdiv_rn(inter, __fsub_rn(__fadd_rn(area_i, carea[jj]), inter));
+        if (iou > thr) hit |= 1ull << jj;
+      } else if (bi.z > c.x && c.z > bi.x && bi.w > c.y && c.w > bi.y) {
+        const float iw = __fsub_rn(vmin(bi.z, c.z), vmax(bi.x, c.x));
+        const float ih = __fsub_rn(vmin(bi.w, c.w), vmax(bi.y, c.y));
+        if (iw > 0.f && ih > 0.f) {                         // else the reference's inter is 0
+          float inter = __fmul_rn(iw, ih);
+          asm volatile("" : "+v"(inter));                   // no FMA contraction into the union
+          const float uni = __fsub_rn(__fadd_rn(area_i, carea[jj]), inter);
+          const double d = thr_m * (double)uni;
+          const double in = (double)inter;
+          if (in > d || (thr_tie && in == d)) hit |= 1ull << jj;
+        }
+      }
+    }
+  }
+  return hit;
+}
+
+__device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int l) {
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)(v & 0xffffffffull), l);
+  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(v >> 32), l);
+  return ((unsigned long long)hi << 32) | lo;
+}
+
+// Top-k + class-aware greedy NMS, ONE launch: G 1024-thread workgroups per image (G = CUs / B,
+// at most 4).  Each repeats steps 1-4 (cheaper than a hand-off: no workgroup ever waits for
+// another) and computes every G-th mask block into a global workspace; the last to finish
+// (agent-scope release / acquire around a per-image counter) loads all blocks into LDS and runs
+// steps 6-7.  G = 1 keeps everything in LDS.
+//
+// Class-aware NMS with class-offset boxes (box + class * max_wh, the reference's one-pass trick)
+// never suppresses across classes, so it is an independent greedy NMS per class; the first
+// max_det kept boxes in score order are the same either way.  The kernel therefore re-sorts the
+// score-sorted candidates by (class, score rank) and computes the IoU bitmask only for the
+// 64 x 64 blocks (row block rb, word w >= rb) that hold a same-class pair — the diagonal blocks
+// and, where a class spans blocks, the blocks of that run.  With 80 classes and 1024 candidates
+// that is ~20-30 of the 136 blocks (the three-kernel predecessor computed all 136 on the whole
+// GPU: 31 us of its 83 us); with one class it is all 136, spread over the 16 waves.
+//   1. scores above the confidence threshold -> 32-bit keys (float bits are monotone for
+//      positive floats) in LDS;
+//   2. radix select of the K-th largest key, K = min(max_candidates, #above conf) (12-bit
+//      digits over key - min live key: only as many passes as the live range needs; none when
+//      every live key is a candidate);
+//   3. deterministic compaction (block scan, ties -> lowest anchor index) and a sort of the
+//      <= 1024 candidates by (score desc, index asc) — the score ranks;
+//   4. a second sort by (class, rank): positions; class-offset boxes in position order;
+//   5. the list of same-class (rb, w) blocks; each wave computes its blocks' 64 mask words
+//      (lane = row), the diagonal blocks also the transposed half (suppressors of a row inside
+//      its own block), with the exact division-free IoU test of mask_word;
+//   6. one wave scans the positions 64 at a time: inside a block the suppression chain is a
+//      ballot fixed point over the transposed diagonal words, then the kept rows' words are
+//      OR-ed into the later blocks of the same class, lane-parallel (no max_det stop: kept
+//      flags go to the score ranks);
+//   7. a block scan over the ranks takes the first max_det kept boxes, maps them back from
+//      letterbox to frame coordinates (clipped) and writes fixed-size [max_det, 6] rows
+//      (x1, y1, x2, y2, score, class) + a count, so results can be all-gathered over RCCL
+//      without a size exchange.
+// A negative IoU threshold (every pair suppresses, across classes too) keeps one class run:
+// the second sort then orders by rank alone.
 constexpr int kRadixBits = 12, kRadixBins = 1 << kRadixBits;   // 4096 bins = 4 per thread
-__global__ __launch_bounds__(kNmsThreads) void nms_select_kernel(NmsParams p, NmsWork ws) {
+__global__ __launch_bounds__(kNmsThreads) void nms_fused_kernel(NmsParams p) {
   constexpr int REGION0 = kMaxAnchors * 4;
   __shared__ __attribute__((aligned(16))) unsigned char region0[REGION0];
   __shared__ unsigned long long ckey[kMaxCand];
-  __shared__ unsigned hist[kRadixBins];
-  __shared__ int sh[40];
+  __shared__ __attribute__((aligned(16))) unsigned hist[kRadixBins];
+  __shared__ int sh[48];
 
   unsigned* keys = reinterpret_cast<unsigned*>(region0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int b = blockIdx.x;
+  const int b = blockIdx.x / p.G, g = blockIdx.x - b * p.G;
   const int A = p.A;
   const float* sc = p.scores + (long)b * A;
   const float4* bx = p.boxes + (long)b * A;
   const int* cl = p.cls + (long)b * A;
+  float* det = p.det + (long)b * p.max_det * 6;
+  const float inv = 1.f / p.gain;
 
+  // ---- 1. keys
   if (tid == 0) {
     sh[32] = 0;
     sh[36] = 0;                      // max key
@@ -352,12 +474,19 @@ __global__ __launch_bounds__(kNmsThreads) void nms_select_kernel(NmsParams p, Nm
   __syncthreads();
   const int total = sh[32];
   const int K = min(p.max_cand, total);
-  if (tid == 0) ws.n[b] = K;
-  if (K == 0 || p.stop == 1) return;
+  if (K == 0) {
+    if (g != 0) return;
+    for (int r = tid; r < p.max_det; r += kNmsThreads) {
+      float* o = det + (long)r * 6;
+      o[0] = o[1] = o[2] = o[3] = o[4] = 0.f;
+      o[5] = -1.f;
+    }
+    if (tid == 0) p.count[b] = 0;
+    return;
+  }
 
-  // radix select of the K-th largest key, on d = key - (min live key), 12-bit digits: only as
-  // many as the live range needs (scores in (conf, 1) span ~24 bits -> 2 passes); skipped when
-  // every live key is a candidate.  T = threshold key, remaining = candidates equal to T.
+  // ---- 2. radix select of the K-th largest key; T = threshold key, remaining = candidates
+  // equal to T
   const unsigned klo = (unsigned)sh[37];
   const unsigned range = (unsigned)sh[36] - klo;
   unsigned prefix = 0u, pmask = 0u;
@@ -426,9 +555,8 @@ __global__ __launch_bounds__(kNmsThreads) void nms_select_kernel(NmsParams p, Nm
   const unsigned T = take_all ? 0u : klo + prefix;
   if (take_all) remaining = 0;
   const int n_gt = K - remaining;
-  if (p.stop == 2) return;
 
-  // deterministic compaction (contiguous chunks + block scan) and bitonic sort
+  // ---- 3. deterministic compaction and the score sort (ranks)
   const int chunk = (A + kNmsThreads - 1) / kNmsThreads;
   const int i0 = tid * chunk, i1 = min(A, i0 + chunk);
   int gt = 0, eq = 0;
@@ -453,219 +581,158 @@ __global__ __launch_bounds__(kNmsThreads) void nms_select_kernel(NmsParams p, Nm
   while (NP < K) NP <<= 1;
   if (tid >= K && tid < NP) ckey[tid] = 0ull;
   __syncthreads();
-  if (p.stop == 3) return;
-  // sort = per-wave bitonic sort of 64 keys in registers (21 shuffle passes, no barrier) + merge
-  // by rank: a key's final position is its place in its own wave's sorted list plus, for each of
-  // the other lists, the number of keys greater than it (7-step binary search of the LDS copy;
-  // the 15 searches are independent).  Keys are unique (index in the low word); padding keys
-  // are 0 and are not written.  Two barriers instead of the 55-pass block-wide network's 20.
-  {
-    unsigned long long v = tid < NP ? ckey[tid] : 0ull;
-    for (int size = 2; size <= 64; size <<= 1) {
-      for (int stride = size >> 1; stride > 0; stride >>= 1) {
-        const unsigned lo = __shfl_xor((unsigned)(v & 0xffffffffull), stride, 64);
-        const unsigned hi = __shfl_xor((unsigned)(v >> 32), stride, 64);
-        const unsigned long long c = ((unsigned long long)hi << 32) | lo;
-        const bool desc = size == 64 || (lane & size) == 0, lower = (lane & stride) == 0;
-        v = (desc == lower) ? (v > c ? v : c) : (v < c ? v : c);
-      }
+  block_sort_desc(ckey, NP);                       // ckey[rank], rank 0 = best score
+
+  // ---- 4. (class, rank) order.  region0 (the keys) is free from here:
+  //   cbox   float4[1024]           class-offset boxes by position     16 KB
+  //   masks  u64[136][64]           mask words of the listed blocks    68 KB
+  //   lowd   u64[1024]              transposed diagonal word by row     8 KB
+  //   sbuf   u64[1024]              the second sort's keys              8 KB
+  //   krank  int[1024]              kept flag by score rank             4 KB
+  //   carea  float[1024]            box areas by position               4 KB
+  // and hist: pos_rank int[1024] (rank of position), pcls int[1024] (class of position),
+  // item int[136] ((rb << 8) | w), item_id int[16][16] (-1: block pair without a class run)
+  float4* cbox = reinterpret_cast<float4*>(region0);
+  unsigned long long* masks = reinterpret_cast<unsigned long long*>(region0 + 16384);
+  unsigned long long* lowd = masks + kMaxItems * 64;
+  unsigned long long* sbuf = lowd + kMaxCand;
+  int* krank = reinterpret_cast<int*>(sbuf + kMaxCand);
+  float* carea = reinterpret_cast<float*>(krank + kMaxCand);
+  int* pos_rank = reinterpret_cast<int*>(hist);
+  int* pcls = pos_rank + kMaxCand;
+  int* item = pcls + kMaxCand;
+  int* item_id = item + 256;
+  const bool neg = p.iou < 0.f;
+  if (tid < NP) {
+    unsigned long long k2 = 0ull;
+    if (tid < K) {
+      const int idx = (int)(0xffffffffu - (unsigned)(ckey[tid] & 0xffffffffull));
+      const unsigned c = neg ? 0u : (unsigned)cl[idx];
+      k2 = ~(((unsigned long long)c << 32) | (unsigned)tid);   // descending sort = (class, rank) ascending
     }
-    __syncthreads();
-    ckey[tid] = v;                                   // [wave][64] sorted descending
-    __syncthreads();
-    int rank = lane;
-    const int nl = (NP + 63) >> 6;
-#pragma unroll 4
-    for (int l = 0; l < nl; ++l) {
-      if (l == wave) continue;
-      const unsigned long long* L = ckey + l * 64;
-      int pos = 0;
-#pragma unroll
-      for (int st = 32; st > 0; st >>= 1)
-        if (L[pos + st - 1] > v) pos += st;
-      rank += pos + (L[pos] > v ? 1 : 0);
-    }
-    __syncthreads();
-    if (v != 0ull) ckey[rank] = v;
-    __syncthreads();
+    sbuf[tid] = k2;
   }
-  if (p.stop == 4) return;
-  // sorted keys + class-offset boxes to the workspace
-  for (int i = tid; i < K; i += kNmsThreads) {
-    const unsigned long long ck = ckey[i];
+  if (tid < 256) item_id[tid] = -1;
+  __syncthreads();
+  block_sort_desc(sbuf, NP);
+  if (tid < K) {
+    const int r = (int)(~sbuf[tid] & 0xffffffffull);
+    const unsigned long long ck = ckey[r];
     const int idx = (int)(0xffffffffu - (unsigned)(ck & 0xffffffffull));
-    const float off = cl[idx] * p.max_wh;
+    const int c = cl[idx];
+    float off = __fmul_rn((float)c, p.max_wh);
+    asm volatile("" : "+v"(off));                     // the reference rounds the offset, then adds
     const float4 q = bx[idx];
-    ws.ckey[(long)b * kMaxCand + i] = ck;
-    ws.cbox[(long)b * kMaxCand + i] = make_float4(q.x + off, q.y + off, q.z + off, q.w + off);
+    const float4 o4 = make_float4(__fadd_rn(q.x, off), __fadd_rn(q.y, off), __fadd_rn(q.z, off), __fadd_rn(q.w, off));
+    cbox[tid] = o4;
+    carea[tid] = __fmul_rn(__fsub_rn(o4.z, o4.x), __fsub_rn(o4.w, o4.y));   // (no add to contract)
+    pos_rank[tid] = r;
+    pcls[tid] = neg ? 0 : c;
+    krank[tid] = 0;
   }
-}
+  __syncthreads();
 
-// IoU > thr bits of row box bi against the 64 column boxes in LDS (bit jj = column jj), one
-// fully unrolled pass: constant bit positions, broadcast LDS reads (FULL: all 64 columns valid,
-// no per-column guard; NEG: negative threshold, every pair tested).  Measured alternatives, all
-// slower on the bench inputs (most candidate pairs overlap, so the exact IoU math is the work):
-// LDS reads issued 8 at a time 32.9 us, a division-free fma test with an exact 1-ulp fallback
-// 35 us, a branch-free overlap pass + scalar loop over overlapping columns 50 us, 4 items per
-// workgroup 33 us, partial unroll 33-38 us — against 30.7 us for this form.  A 4-compare overlap test on both axes (a superset of inter > 0)
-// gates the exact intersection + IEEE division, so the decisions are box_iou() > thr bit for
-// bit; most pairs (other classes sit max_wh apart) stop at the 4 compares.  The test is symmetric
-// bit for bit (fminf / fmaxf and the area sum commute), so the diagonal word's transposed half
-// comes out of the same pass.
-template <bool FULL, bool NEG>
-__device__ __forceinline__ unsigned long long mask_word(const float4* col, float4 bi, float area_i,
-                                                        int je, float thr) {
-  unsigned long long hit = 0ull;
-#pragma unroll
-  for (int jj = 0; jj < 64; ++jj) {
-    if (FULL || jj < je) {                                  // wave-uniform
-      const float4 c = col[jj];
-      if (NEG || (bi.z > c.x && c.z > bi.x && bi.w > c.y && c.w > bi.y)) {
-        const float iw = fmaxf(0.f, fminf(bi.z, c.z) - fmaxf(bi.x, c.x));
-        const float ih = fmaxf(0.f, fminf(bi.w, c.w) - fmaxf(bi.y, c.y));
-        const float inter = iw * ih;
-        if (NEG || inter > 0.f) {
-          const float iou = inter / (area_i + (c.z - c.x) * (c.w - c.y) - inter);
-          if (iou > thr) hit |= 1ull << jj;
-        }
+  // ---- 5. same-class block pairs, then their mask words
+  const int W = (K + 63) >> 6;
+  const int npairs = W * (W + 1) / 2;
+  int rb = 0, wq = 0;
+  bool need = false;
+  if (tid < npairs) {
+    int q = tid;
+    while (q >= W - rb) {
+      q -= W - rb;
+      ++rb;
+    }
+    wq = rb + q;
+    need = wq == rb || pcls[wq * 64] == pcls[rb * 64 + 63];
+  }
+  const int slot = block_exclusive_scan(need ? 1 : 0, sh);
+  if (need) {
+    item[slot] = (rb << 8) | wq;
+    item_id[rb * 16 + wq] = slot;
+  }
+  if (tid == npairs - 1) sh[40] = slot + (need ? 1 : 0);
+  __syncthreads();
+  const int nitems = sh[40];
+  const bool split = p.G > 1;
+  unsigned long long* gm = split ? p.gmask + (long)b * kMaxItems * 64 : nullptr;
+  unsigned long long* gl = split ? p.glow + (long)b * kMaxCand : nullptr;
+  for (int j = g + p.G * wave; j < nitems; j += p.G * (kNmsThreads / 64)) {
+    const int rbj = item[j] >> 8, wj = item[j] & 0xff;
+    const int i = rbj * 64 + lane;
+    const int je = min(64, K - wj * 64);
+    unsigned long long bits = 0ull;
+    if (i < K) {
+      const float4 bi = cbox[i];
+      const float area_i = carea[i];
+      const float4* col = cbox + wj * 64;
+      const float* ca = carea + wj * 64;
+      const unsigned long long hit =
+          neg ? mask_word<false, true>(col, ca, bi, area_i, je, p.thr_m, p.thr_tie, p.iou)
+              : (je == 64 ? mask_word<true, false>(col, ca, bi, area_i, je, p.thr_m, p.thr_tie, p.iou)
+                          : mask_word<false, false>(col, ca, bi, area_i, je, p.thr_m, p.thr_tie, p.iou));
+      bits = hit;
+      if (wj == rbj) {
+        bits = lane == 63 ? 0ull : hit & (~0ull << (lane + 1));
+        const unsigned long long lw = hit & ((1ull << lane) - 1ull);
+        if (split) gl[i] = lw;
+        else lowd[i] = lw;
       }
     }
+    if (split) gm[j * 64 + lane] = bits;
+    else masks[j * 64 + lane] = bits;
   }
-  return hit;
-}
-
-// 2. IoU suppression bitmask over the whole GPU: one wave per (image, 64-row block rb, word
-//    w >= rb) — B x 136 equal-sized work items; lane = row, the 64 column boxes of word w sit in
-//    LDS and are read as broadcasts.  The diagonal word also yields its transposed half (bits
-//    k < i: the suppressors of row i inside the word) for the greedy kernel's fixed point.
-constexpr int kMaskPairs = kMaskWords * (kMaskWords + 1) / 2;   // 136 (rb, w) with w >= rb
-constexpr int kMaskWaves = 1;   // work items (waves) per workgroup
-static_assert(kMaskPairs % kMaskWaves == 0, "items of an image fill whole workgroups");
-__global__ __launch_bounds__(64 * kMaskWaves) void nms_mask_kernel(NmsParams p, NmsWork ws) {
-  __shared__ float4 cols[kMaskWaves][64];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int item = blockIdx.x * kMaskWaves + wave;
-  const int b = item / kMaskPairs;
-  int q = item - b * kMaskPairs, rb = 0;
-  while (q >= kMaskWords - rb) {                 // (rb, w) from the triangle index
-    q -= kMaskWords - rb;
-    ++rb;
+  if (split) {
+    // publish this workgroup's blocks; the last of the image's G workgroups takes them all
+    // (release: stores drained, fence, then the counter; acquire: fence, then plain loads)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      sh[42] = __hip_atomic_fetch_add(p.gcount + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (sh[42] != p.G - 1) return;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(p.gcount + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t = tid; t < nitems * 64; t += kNmsThreads) masks[t] = gm[t];
+    if (tid < K) lowd[tid] = gl[tid];
   }
-  const int w = rb + q;
-  const int n = ws.n[b];
-  const int r0 = rb * 64, j0 = w * 64;
-  const bool work = r0 < n && j0 < n;            // wave-uniform; no return before the barrier
-  float4* col = cols[wave];
-  const float4* cb = ws.cbox + (long)b * kMaxCand;
-  if (work && j0 + lane < n) col[lane] = cb[j0 + lane];
-  const int i = r0 + lane;
-  const float4 bi = work && i < n ? cb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
-  if (!work || i >= n) return;
-  const float area_i = (bi.z - bi.x) * (bi.w - bi.y);
-  const int je = min(64, n - j0);
-  const bool diag = w == rb;
-  // (a negative threshold keeps every pair, disjoint ones included: the generic instantiation)
-  const unsigned long long hit =
-      p.iou < 0.f ? mask_word<false, true>(col, bi, area_i, je, p.iou)
-                  : (je == 64 ? mask_word<true, false>(col, bi, area_i, je, p.iou)
-                              : mask_word<false, false>(col, bi, area_i, je, p.iou));
-  unsigned long long bits = hit;
-  if (diag) {
-    bits = lane == 63 ? 0ull : hit & (~0ull << (lane + 1));
-    ws.low[((long)b * kMaskWords + w) * kMaxCand + i] = hit & ((1ull << lane) - 1ull);
-  }
-  ws.mask[((long)b * kMaskWords + w) * kMaxCand + i] = bits;
-}
 
-__device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int l) {
-  const unsigned lo = __builtin_amdgcn_readlane((unsigned)(v & 0xffffffffull), l);
-  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(v >> 32), l);
-  return ((unsigned long long)hi << 32) | lo;
-}
-
-// 3. greedy scan per image.  The mask words at / right of the diagonal are staged into LDS
-//    (row stride padded by one word: the scan's lane-parallel reads hit distinct banks).  (A
-//    chunked variant — 256 rows at a time, next chunk loaded during the scan, stopping at
-//    max_det — measured slower: 26.7 -> 31.6 us.)  The scan: lane w holds the "removed" word w;
-//    inside a 64-candidate word the suppression chain is a ballot fixed point over the
-//    transposed diagonal words, then the kept rows' words are OR-ed lane-parallel into the later
-//    words.  Finally the kept boxes are mapped back from letterbox to frame coordinates.
-constexpr int kGreedyThreads = 1024;
-constexpr int kWordStride = kMaxCand + 1;   // padded: lane w's reads of words[w][row] hit distinct banks
-__global__ __launch_bounds__(kGreedyThreads) void nms_greedy_kernel(NmsParams p, NmsWork ws) {
-  __shared__ unsigned long long words[kMaskWords * kWordStride];  // [w][i]
-  __shared__ unsigned long long lowd[kMaxCand];                  // row i's transposed diagonal word
-  __shared__ int kept[kMaxCand];
-  __shared__ int nk_sh;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int b = blockIdx.x;
-  const int n = ws.n[b];
-  const int W = (n + 63) >> 6;
-  const unsigned long long* mk = ws.mask + (long)b * kMaxCand * kMaskWords;
-  // staging: all 16 loads of a thread are issued before the first LDS store (a load -> store
-  // loop would pay one HBM/L2 latency per word); only the words at / right of the diagonal
-  // (w >= row block), the only ones the scan reads
-  {
-    static_assert(kGreedyThreads == kMaxCand, "one thread per candidate row");
-    const int rb = tid >> 6;
-    unsigned long long tmp[kMaskWords];
-#pragma unroll
-    for (int w = 0; w < kMaskWords; ++w)
-      tmp[w] = (w >= rb && w < W && tid < n) ? mk[(long)w * kMaxCand + tid] : 0ull;
-    const unsigned long long lw =
-        tid < n ? ws.low[((long)b * kMaskWords + rb) * kMaxCand + tid] : 0ull;
-#pragma unroll
-    for (int w = 0; w < kMaskWords; ++w) words[w * kWordStride + tid] = tmp[w];
-    lowd[tid] = lw;
-  }
-  if (tid == 0) nk_sh = 0;
-  __syncthreads();
-  if (p.stop == 5) return;
+  // ---- 6. greedy scan over the positions (one wave; lane w holds the "removed" word w)
   if (tid < 64) {
     unsigned long long removed = 0ull;
-    int nkept = 0;
-    {
-      for (int w = 0; w < W && nkept < p.max_det; ++w) {
-        unsigned long long cur = readlane64(removed, w);
-        const int row = w * 64 + lane;
-        // suppressors of this lane's candidate inside the word (rows k < row, transposed diagonal)
-        const unsigned long long low = row < n ? lowd[row] : 0ull;
-        const int left = n - w * 64;
-        const unsigned long long valid = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
-        const unsigned long long alive = ~cur & valid;
-        const bool me_alive = (alive >> lane) & 1ull;
-        // greedy inside the word as a fixed point: kept = alive minus those with a kept
-        // suppressor.  Candidate c's status is final once all k < c are, so <= 64 rounds; the
-        // first repeat is the (unique) greedy solution.  One ballot per round, not one
-        // dependent step per candidate.
-        unsigned long long keep = alive;
-        for (int it = 0; it <= 64; ++it) {
-          const unsigned long long nk = __ballot(me_alive && !(low & keep));
-          if (nk == keep) break;
-          keep = nk;
-        }
-        const int room = p.max_det - nkept;
-        if (__popcll(keep) > room) {
-          unsigned long long trimmed = 0ull, kk = keep;
-          for (int r = 0; r < room; ++r) {
-            const unsigned long long lowb = kk & (~kk + 1ull);
-            trimmed |= lowb;
-            kk ^= lowb;
-          }
-          keep = trimmed;
-        }
-        if ((keep >> lane) & 1ull) {
-          const unsigned long long below = lane ? (keep & ((1ull << lane) - 1ull)) : 0ull;
-          kept[nkept + __popcll(below)] = row;
-        }
-        nkept += __popcll(keep);
-        // OR the kept rows' words into the later words: 8 LDS reads in flight per round (a
-        // one-read-per-iteration loop exposes the LDS latency for every kept row)
-        unsigned long long kk = keep;
-        unsigned long long acc = 0ull;
-        const bool mine = lane > w && lane < W;
-        const unsigned long long* wl = words + lane * kWordStride + w * 64;
+    for (int w = 0; w < W; ++w) {
+      const unsigned long long cur = readlane64(removed, w);
+      const int row = w * 64 + lane;
+      // suppressors of this lane's candidate inside the block (rows k < row, transposed diagonal)
+      const unsigned long long low = row < K ? lowd[row] : 0ull;
+      const int left = K - w * 64;
+      const unsigned long long valid = left >= 64 ? ~0ull : ((1ull << left) - 1ull);
+      const unsigned long long alive = ~cur & valid;
+      const bool me_alive = (alive >> lane) & 1ull;
+      // greedy inside the block as a fixed point: kept = alive minus those with a kept
+      // suppressor.  Candidate c's status is final once all k < c are, so <= 64 rounds; the
+      // first repeat is the (unique) greedy solution.  One ballot per round.
+      unsigned long long keep = alive;
+      for (int it = 0; it <= 64; ++it) {
+        const unsigned long long nk = __ballot(me_alive && !(low & keep));
+        if (nk == keep) break;
+        keep = nk;
+      }
+      if ((keep >> lane) & 1ull) krank[pos_rank[row]] = 1;
+      // OR the kept rows' words into the later blocks of the same class run: 8 LDS reads in
+      // flight per round
+      const int jl = lane > w && lane < W ? item_id[w * 16 + lane] : -1;
+      if (__ballot(jl >= 0)) {
+        unsigned long long kk = keep, acc = 0ull;
+        const unsigned long long* wl = masks + (jl >= 0 ? jl : 0) * 64;
         while (kk) {
           int bsel[8];
 #pragma unroll
@@ -675,38 +742,38 @@ __global__ __launch_bounds__(kGreedyThreads) void nms_greedy_kernel(NmsParams p,
           }
           unsigned long long v[8];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) v[u] = (mine && bsel[u] >= 0) ? wl[bsel[u]] : 0ull;
+          for (int u = 0; u < 8; ++u) v[u] = (jl >= 0 && bsel[u] >= 0) ? wl[bsel[u]] : 0ull;
 #pragma unroll
           for (int u = 0; u < 8; ++u) acc |= v[u];
         }
         removed |= acc;
       }
     }
-    if (lane == 0) nk_sh = nkept;
   }
   __syncthreads();
-  if (p.stop == 6) return;
-  const int nk = nk_sh;
-  const float4* bx = p.boxes + (long)b * p.A;
-  const int* cl = p.cls + (long)b * p.A;
-  const unsigned long long* ck_all = ws.ckey + (long)b * kMaxCand;
-  const float inv = 1.f / p.gain;
-  for (int r = tid; r < p.max_det; r += kGreedyThreads) {
-    float* o = p.det + ((long)b * p.max_det + r) * 6;
-    if (r < nk) {
-      const unsigned long long ck = ck_all[kept[r]];
-      const int idx = (int)(0xffffffffu - (unsigned)(ck & 0xffffffffull));
-      const float4 q = bx[idx];
-      o[0] = fminf(fmaxf((q.x - p.pad_l) * inv, 0.f), p.img_w);
-      o[1] = fminf(fmaxf((q.y - p.pad_t) * inv, 0.f), p.img_h);
-      o[2] = fminf(fmaxf((q.z - p.pad_l) * inv, 0.f), p.img_w);
-      o[3] = fminf(fmaxf((q.w - p.pad_t) * inv, 0.f), p.img_h);
-      o[4] = __uint_as_float((unsigned)(ck >> 32));
-      o[5] = (float)cl[idx];
-    } else {
-      o[0] = o[1] = o[2] = o[3] = o[4] = 0.f;
-      o[5] = -1.f;
-    }
+
+  // ---- 7. the first max_det kept boxes in score order -> frame coordinates
+  const int kf = tid < K ? krank[tid] : 0;
+  const int out = block_exclusive_scan(kf, sh);
+  if (tid == kNmsThreads - 1) sh[41] = out + kf;
+  __syncthreads();
+  const int nk = min(sh[41], p.max_det);
+  if (kf && out < p.max_det) {
+    const unsigned long long ck = ckey[tid];
+    const int idx = (int)(0xffffffffu - (unsigned)(ck & 0xffffffffull));
+    const float4 q = bx[idx];
+    float* o = det + (long)out * 6;
+    o[0] = fminf(fmaxf((q.x - p.pad_l) * inv, 0.f), p.img_w);
+    o[1] = fminf(fmaxf((q.y - p.pad_t) * inv, 0.f), p.img_h);
+    o[2] = fminf(fmaxf((q.z - p.pad_l) * inv, 0.f), p.img_w);
+    o[3] = fminf(fmaxf((q.w - p.pad_t) * inv, 0.f), p.img_h);
+    o[4] = __uint_as_float((unsigned)(ck >> 32));
+    o[5] = (float)cl[idx];
+  }
+  for (int r = nk + tid; r < p.max_det; r += kNmsThreads) {
+    float* o = det + (long)r * 6;
+    o[0] = o[1] = o[2] = o[3] = o[4] = 0.f;
+    o[5] = -1.f;
   }
   if (tid == 0) p.count[b] = nk;
 }
@@ -770,8 +837,23 @@ extern "C" int aiko_yolo_decode(const void* const* feats, const int* H, const in
   return (int)hipGetLastError();
 }
 
+// workgroups per image: enough to spread the images' mask blocks over the CUs (up to 4)
+extern "C" int aiko_topk_nms_groups(int B) {
+  static int cus = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    return n;
+  }();
+  const int g = cus / (B > 0 ? B : 1);
+  return g < 1 ? 1 : (g > 4 ? 4 : g);
+}
+
+// bytes of the G > 1 workspace (mask blocks, diagonal words, counters), 0 for G == 1; the
+// counters (the last 4 B bytes) must be zero before the launch
 extern "C" size_t aiko_topk_nms_workspace(int B) {
-  return (size_t)B * aiko::kMaxCand * (8 + 16 + 2 * aiko::kMaskWords * 8) + ((size_t)B * 4 + 255) / 256 * 256;
+  if (aiko_topk_nms_groups(B) <= 1) return 0;
+  return (size_t)B * (aiko::kMaxItems * 64 * 8 + aiko::kMaxCand * 8 + 4);
 }
 
 extern "C" int aiko_topk_nms(const void* boxes, const float* scores, const int* cls, int B, int A,
@@ -779,7 +861,7 @@ extern "C" int aiko_topk_nms(const void* boxes, const float* scores, const int* 
                              float gain, float pad_l, float pad_t, float img_w, float img_h,
                              float* det, int* count, void* workspace, hipStream_t stream) {
   if (A > aiko::kMaxAnchors || max_cand < 1 || max_cand > aiko::kMaxCand || max_det < 1 ||
-      max_det > aiko::kMaxCand || workspace == nullptr)
+      max_det > aiko::kMaxCand)
     return -1;
   aiko::NmsParams p;
   p.boxes = static_cast<const float4*>(boxes);
@@ -790,25 +872,14 @@ extern "C" int aiko_topk_nms(const void* boxes, const float* scores, const int* 
   p.gain = gain; p.pad_l = pad_l; p.pad_t = pad_t; p.img_w = img_w; p.img_h = img_h;
   p.det = det;
   p.count = count;
-  static const int stop = [] {                  // profiling hook (scripts/nms_stop.sh), read once
-    const char* e = getenv("AIKO_NMS_STOP");
-    return e ? atoi(e) : 99;
-  }();
-  p.stop = stop;
-  char* w = static_cast<char*>(workspace);
-  aiko::NmsWork ws;
-  ws.mask = reinterpret_cast<unsigned long long*>(w);
-  w += (size_t)B * aiko::kMaxCand * aiko::kMaskWords * 8;
-  ws.ckey = reinterpret_cast<unsigned long long*>(w);
-  w += (size_t)B * aiko::kMaxCand * 8;
-  ws.cbox = reinterpret_cast<float4*>(w);
-  w += (size_t)B * aiko::kMaxCand * 16;
-  ws.n = reinterpret_cast<int*>(w);
-  w += ((size_t)B * 4 + 255) / 256 * 256;
-  ws.low = reinterpret_cast<unsigned long long*>(w);
-  aiko::nms_select_kernel<<<B, aiko::kNmsThreads, 0, stream>>>(p, ws);
-  if (p.stop < 5) return 0;
-  aiko::nms_mask_kernel<<<B * aiko::kMaskPairs / aiko::kMaskWaves, 64 * aiko::kMaskWaves, 0, stream>>>(p, ws);
-  aiko::nms_greedy_kernel<<<B, aiko::kGreedyThreads, 0, stream>>>(p, ws);
+  const aiko::IouThrHost th = aiko::iou_threshold(iou);
+  p.thr_m = th.m;
+  p.thr_tie = th.tie_up;
+  p.G = aiko_topk_nms_groups(B);
+  p.gmask = static_cast<unsigned long long*>(workspace);
+  p.glow = p.gmask ? p.gmask + (size_t)B * aiko::kMaxItems * 64 : nullptr;
+  p.gcount = p.gmask ? reinterpret_cast<int*>(p.glow + (size_t)B * aiko::kMaxCand) : nullptr;
+  if (p.G > 1 && workspace == nullptr) return -1;
+  aiko::nms_fused_kernel<<<B * p.G, aiko::kNmsThreads, 0, stream>>>(p);
   return (int)hipGetLastError();
 }

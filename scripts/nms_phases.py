@@ -1,9 +1,9 @@
-"""Timing of the top-k + NMS kernels on the YOLOv8-n bench inputs (B=64 VGA frames,
+"""Timing of the top-k + NMS kernel on the YOLOv8-n bench inputs (B=64 VGA frames,
 random-init weights: ~6.6k anchors above conf per image, so 1024 candidates each).
 
-Round-2 phase breakdown of the former single-kernel version (phases < k, one run per k):
-keys + radix select 15 us, compaction + sort 15 us, IoU bitmask 130 us, greedy scan 86 us —
-246 us in total; hence the three-kernel split (detect_ops.hip)."""
+History: round 2's single kernel over the full bitmask 246 us (keys + radix select 15 us,
+compaction + sort 15 us, IoU bitmask 130 us, greedy scan 86 us); rounds 3-5's three kernels
+83 us; round 6's single per-class kernel (detect_ops.hip nms_fused_kernel)."""
 import os
 import sys
 
@@ -31,6 +31,12 @@ def main():
     DT.topk_nms = orig
     b, s, c = cap["boxes"], cap["scores"], cap["cls"]
     print("above conf per image:", int((s > 0.25).sum(1).float().mean()))
+    top = s.topk(1024, dim=1).indices
+    tc = torch.gather(c, 1, top)
+    per = [torch.bincount(tc[i].long(), minlength=80) for i in range(tc.shape[0])]
+    mx = torch.stack([q.max() for q in per]).float()
+    nz = torch.stack([(q > 0).sum() for q in per]).float()
+    print(f"classes among the 1024 candidates: {nz.mean():.1f} present, largest run {mx.mean():.0f} (min {mx.min():.0f}, max {mx.max():.0f})")
     for _ in range(3):
         det, cnt = DT.topk_nms(b, s, c)
     torch.cuda.synchronize()

@@ -105,30 +105,36 @@ def test_yolo_decode_tiled_matches_per_anchor(native, monkeypatch):
         assert torch.equal(a, b)
 
 
-def _random_dets(B, A, g, n_centers=40):
+def _random_dets(B, A, g, n_centers=40, n_cls=3):
     centers = torch.rand(B, n_centers, 2, generator=g) * 600
     pick = torch.randint(0, n_centers, (B, A), generator=g)
     c = torch.gather(centers, 1, pick[..., None].expand(B, A, 2)) + torch.randn(B, A, 2, generator=g) * 6
     wh = 20 + torch.rand(B, A, 2, generator=g) * 60
     boxes = torch.cat([c - wh / 2, c + wh / 2], -1)
     scores = (torch.rand(B, A, generator=g) * 256).floor() / 256      # many exact ties
-    cls = torch.randint(0, 3, (B, A), generator=g, dtype=torch.int32)
+    cls = torch.randint(0, n_cls, (B, A), generator=g, dtype=torch.int32)
     return boxes.to(DEV), scores.to(DEV), cls.to(DEV)
 
 
-@pytest.mark.parametrize("A,conf,max_cand,max_det", [(8400, 0.25, 1024, 300), (8400, 0.97, 1024, 300),
-                                                     (2000, 0.1, 256, 50), (33, 0.0, 1024, 300)])
-def test_topk_nms_matches_reference(native, A, conf, max_cand, max_det):
+# n_cls: 3 (class runs spanning several 64-candidate blocks), 1 (every block pair: the whole
+# triangle), 80 (YOLO: mostly diagonal blocks), 1000 (a run per candidate); iou < 0: every pair
+# suppresses, across classes too (one run in rank order)
+@pytest.mark.parametrize("A,conf,max_cand,max_det,n_cls,iou", [
+    (8400, 0.25, 1024, 300, 3, 0.5), (8400, 0.97, 1024, 300, 3, 0.5), (2000, 0.1, 256, 50, 3, 0.5),
+    (33, 0.0, 1024, 300, 3, 0.5), (8400, 0.25, 1024, 300, 1, 0.5), (8400, 0.25, 1024, 1024, 1, 0.3),
+    (8400, 0.25, 1024, 300, 80, 0.5), (8400, 0.25, 1000, 100, 1000, 0.5), (700, 0.1, 1024, 300, 80, -1.0),
+    (6000, 0.5, 777, 13, 7, 0.45)])
+def test_topk_nms_matches_reference(native, A, conf, max_cand, max_det, n_cls, iou):
     from aiko_services_amd.ops import detect as DT
     from aiko_services_amd.ops import reference as R
-    g = torch.Generator().manual_seed(A + max_det)
+    g = torch.Generator().manual_seed(A + max_det + n_cls)
     B = 3
-    boxes, scores, cls = _random_dets(B, A, g)
-    det, count = DT.topk_nms(boxes, scores, cls, conf=conf, iou=0.5, max_candidates=max_cand,
+    boxes, scores, cls = _random_dets(B, A, g, n_cls=n_cls)
+    det, count = DT.topk_nms(boxes, scores, cls, conf=conf, iou=iou, max_candidates=max_cand,
                              max_det=max_det)
     torch.cuda.synchronize()
     for b in range(B):
-        keep = R.nms_ref(boxes[b], scores[b], cls[b], conf, 0.5, max_cand, max_det)
+        keep = R.nms_ref(boxes[b], scores[b], cls[b], conf, iou, max_cand, max_det)
         n = int(count[b])
         assert n == keep.numel(), (b, n, keep.numel())
         ref = torch.cat([boxes[b][keep].clamp(min=0), scores[b][keep, None], cls[b][keep, None].float()], 1)
