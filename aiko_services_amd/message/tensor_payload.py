@@ -28,6 +28,7 @@ instead), a CPU tensor / ndarray on the host, bit-exact.  ``generate()`` itself 
 from __future__ import annotations
 
 import json
+import math
 import os
 import struct
 import sys
@@ -141,6 +142,8 @@ def encode_message(command: str, parameters, codec: str | None = None):
     return b"".join([MAGIC, struct.pack("<I", len(header)), header, b"\x00" * head_pad, *blobs])
 
 
+_MAX_ARRAY_BYTES = 1 << 34                    # 16 GiB: far above any MQTT-borne array
+
 _TORCH_DTYPES = ("float32", "float16", "bfloat16", "float64", "uint8", "int8", "int16", "int32", "int64",
                  "bool", "complex64", "complex128", "float8_e4m3fn", "float8_e5m2", "uint16", "uint32",
                  "uint64")
@@ -152,24 +155,42 @@ def _restore(entry, buf: memoryview, base: int):
     if start < base or start + n > len(buf):
         raise ValueError("tensor payload: blob outside the message")
     raw = buf[start:start + n]
-    if entry.get("codec", "raw") == "zlib":
-        raw = memoryview(zlib.decompress(raw))
-    elif entry["codec"] != "raw":
-        raise ValueError(f"tensor payload: unknown codec {entry['codec']!r}")
     shape = [int(s) for s in entry["shape"]]
-    if entry["kind"] == "numpy":
-        dtype = np.dtype(entry["dtype"])
-        if dtype.hasobject:
+    if any(d < 0 for d in shape):
+        raise ValueError("tensor payload: negative dimension")
+    count = math.prod(shape)
+    kind = entry["kind"]
+    if kind == "numpy":
+        np_dtype = np.dtype(entry["dtype"])
+        if np_dtype.hasobject:
             raise ValueError("tensor payload: object dtype refused")
-        return np.frombuffer(raw, dtype=dtype).reshape(shape).copy()
-    if entry["kind"] != "torch":
-        raise ValueError(f"tensor payload: unknown array kind {entry['kind']!r}")
-    import torch
-    name = entry["dtype"]
-    if name not in _TORCH_DTYPES:
-        raise ValueError(f"tensor payload: dtype {name!r} refused")
-    dtype = getattr(torch, name)
-    if int(np.prod(shape, dtype=np.int64)) == 0:
+        itemsize = np_dtype.itemsize
+    elif kind == "torch":
+        import torch
+        name = entry["dtype"]
+        if name not in _TORCH_DTYPES:
+            raise ValueError(f"tensor payload: dtype {name!r} refused")
+        t_dtype = getattr(torch, name)
+        itemsize = torch.empty((), dtype=t_dtype).element_size()
+    else:
+        raise ValueError(f"tensor payload: unknown array kind {kind!r}")
+    expected = count * itemsize
+    if expected > _MAX_ARRAY_BYTES:
+        raise ValueError(f"tensor payload: {expected} bytes claimed for one array")
+    codec = entry.get("codec", "raw")
+    if codec == "zlib":
+        # bounded: a blob may not inflate past the array it claims to be
+        d = zlib.decompressobj()
+        out = d.decompress(raw, expected + 1)
+        raw = memoryview(out)
+    elif codec != "raw":
+        raise ValueError(f"tensor payload: unknown codec {codec!r}")
+    if raw.nbytes != expected:
+        raise ValueError(f"tensor payload: {raw.nbytes} bytes for a {entry['dtype']} array of shape {shape}")
+    if kind == "numpy":
+        return np.frombuffer(raw, dtype=np_dtype).reshape(shape).copy()
+    dtype = t_dtype
+    if count == 0:
         t = torch.empty(shape, dtype=dtype)
     else:
         t = torch.frombuffer(bytearray(raw), dtype=torch.uint8).view(dtype).reshape(shape)

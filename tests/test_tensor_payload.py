@@ -92,3 +92,37 @@ def test_process_keeps_tensor_payload_bytes():
     proc._message_handlers[M.topic] = [lambda _a, _t, p: seen.append(parse(p))]
     proc.on_message_queue_handler(M, "message")
     assert seen and torch.equal(seen[0][1][1]["x"], torch.arange(4.0))
+
+
+def test_decode_refuses_inconsistent_or_inflated_blobs():
+    """A header whose blob length or inflated size does not match the claimed array is refused
+    (no allocation from the claim alone, no unbounded zlib inflation)."""
+    import json
+    import struct
+    import zlib
+
+    import numpy as np
+    import pytest
+
+    from aiko_services_amd.message.tensor_payload import MAGIC, decode_message, encode_message
+
+    good = encode_message("f", [np.arange(12, dtype=np.int32)])
+    decode_message(good)
+
+    def forge(entry_patch, blob):
+        hdr = {"v": 1, "sexpr": "(f 0:)", "results": [],
+               "arrays": [dict({"path": [0], "kind": "numpy", "dtype": "<i4", "shape": [12], "device": "cpu",
+                                "offset": 0, "nbytes": len(blob), "codec": "raw"}, **entry_patch)]}
+        h = json.dumps(hdr).encode()
+        lead = len(MAGIC) + 4 + len(h)
+        return MAGIC + struct.pack("<I", len(h)) + h + b"\x00" * ((-lead) % 64) + blob
+
+    with pytest.raises(ValueError):                       # 40 bytes for a 48-byte array
+        decode_message(forge({}, b"\x01" * 40))
+    with pytest.raises(ValueError):                       # absurd claimed shape
+        decode_message(forge({"shape": [1 << 40, 1 << 20]}, b"\x01" * 48))
+    bomb = zlib.compress(b"\x00" * (1 << 22))
+    with pytest.raises(ValueError):                       # inflates past the 48 claimed bytes
+        decode_message(forge({"codec": "zlib", "nbytes": len(bomb)}, bomb))
+    with pytest.raises(ValueError):
+        decode_message(forge({"shape": [-1]}, b"\x01" * 48))
