@@ -168,14 +168,17 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--batch", type=int, default=None,
-                    help="frames per GPU per step (default: ResNet-50 320, YOLOv8-n 64, Whisper 14 "
-                         "streams).  ResNet-50's 320 is chosen for the chip's 256 CUs: stage 3 runs "
-                         "M = 320 x 196 = 62720 = 245 tiles of 256 rows (96 %% of the CUs busy in one "
-                         "round) where B=256 gives 196 tiles (77 %%); interleaved on MI355X 86.3-87.9k "
-                         "vs 83.7-84.4k frames/s at B=256 (scripts/batch_quant_ab.sh).  Whisper's 14 "
-                         "streams x 12 heads x 6 query tiles are 1.97 rounds of the attention kernel's "
-                         "512 resident workgroups where 16 streams were 2.25: 2.94k-3.05k vs "
-                         "2.87k-2.88k windows/s at a lower p50 (scripts/batch_sweep_cfg45.sh)")
+                    help="frames per GPU per step (default: ResNet-50 640 (320 for --parallel pp), "
+                         "YOLOv8-n 192, Whisper 28 streams).  Batches are sized for the chip's 256 CUs: "
+                         "ResNet-50 at B = 320 k runs stage 3 as 245 k tiles of 256 rows (96 %% of the "
+                         "CUs busy per round) where B=256 gives 196 tiles (77 %%) and 448 / 768 land "
+                         "on 1.34 / 2.3 rounds.  Round-6 sweep, one MI355X, interleaved x 2 "
+                         "(scripts/batch_ab_r4.sh): B=320 89.0k (p50 7.7-9.0 ms), 448 86.9-87.6k, 512 "
+                         "89.0-90.4k, 640 92.3-92.7k (p50 14 ms), 768 89.5-89.8k, 960 91.3-92.1k, 1280 "
+                         "93.2-93.3k (p50 28-31 ms): 640 takes +3.7 %% for 2x the latency.  YOLOv8-n "
+                         "(scripts/batch_sweep_r6.sh, probe/yolo_batch_sweep.sh): B=64 44.5-46.4k, 128 "
+                         "48.8-48.9k, 192 49.5-50.4k (p50 7.8 ms), 256 50.4k, 320 50.6-51.0k.  "
+                         "Whisper-small: 14 streams 3.36-3.38k, 28 3.42k, 42 3.42k windows/s")
     ap.add_argument("--height", type=int, default=224)
     ap.add_argument("--width", type=int, default=224)
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture")
@@ -215,7 +218,8 @@ def parse_args(argv=None) -> argparse.Namespace:
     if (a.parallel == "pp" or a.model == "yolov8n") and not explicit_hw:
         a.height, a.width = 480, 640          # configs 3/4 decode VGA video frames
     if a.batch is None:
-        a.batch = 64 if a.model == "yolov8n" else 14 if a.model.startswith("whisper") else 320
+        a.batch = (192 if a.model == "yolov8n" else 28 if a.model.startswith("whisper")
+                   else 320 if a.parallel == "pp" else 640)
     return a
 
 

@@ -1,7 +1,7 @@
 """Numerical parity AT THE CREDITED BENCH SHAPES.
 
-The tuner keys its tile picks on the layer geometry, so B = 320 (ResNet-50 headline) and B = 64
-(YOLOv8-n, config 4) run kernels (256 x 256 conv_wide, conv_wide_pers, patchw, chain2,
+The tuner keys its tile picks on the layer geometry, so the bench batches — B = 640 (ResNet-50
+headline) and B = 192 (YOLOv8-n, config 4), ``bench.parse_args`` defaults — run kernels (256 x 256 conv_wide, conv_wide_pers, patchw, chain2,
 conv_pw_rb, the detect-head tail-decode launches) that the small-batch parity tests never reach.
 These tests build the bench pipelines exactly as ``bench.py`` does (``bench.definition`` /
 ``bench.yolo_definition``: tuner picks, 2 frame lanes, hipGraph capture per pool slot and lane),
@@ -52,14 +52,15 @@ def _run(p, q, frame_id, result_key):
     return swag
 
 
-# ---- ResNet-50, B = 320, 2 lanes, hipGraph (BASELINE config 2, the credited headline) ----------
+# ---- ResNet-50 at the bench batch, 2 lanes, hipGraph (BASELINE config 2, the credited headline) --
 RESNET_SETUP = 12          # bench.SETUP_FRAMES: tune + one capture per pool slot (6) and lane (2)
 CHECK_FRAMES = 16          # frames compared per replayed step
 
 
 def _resnet_parity(sabotage: bool):
     import bench
-    p, q = _pipeline(bench.definition(320, True, 224, 224, 2))
+    B = bench.parse_args([]).batch
+    p, q = _pipeline(bench.definition(B, True, 224, 224, 2))
     for fid in range(RESNET_SETUP):
         _run(p, q, fid, "topk")
     model = _element(p, "ResNet50Classifier").model
@@ -97,7 +98,7 @@ def _resnet_ok(results):
 
 def test_resnet50_bench_shape_matches_fp32_reference(native):
     results = _resnet_parity(sabotage=False)
-    print("resnet50 B=320 parity: min cos", [round(r["cos"].min().item(), 7) for r in results])
+    print("resnet50 bench-batch parity: min cos", [round(r["cos"].min().item(), 7) for r in results])
     for r in results:
         assert r["cos"].min().item() > COS_MIN, r["cos"]
         assert bool(r["agree"][r["decisive"]].all()), (r["agree"], r["decisive"])
@@ -110,7 +111,7 @@ def test_resnet50_bench_shape_check_catches_a_wrong_kernel(native):
     assert not _resnet_ok(results)
 
 
-# ---- YOLOv8-n, B = 64, 480 x 640 frames, tail-decode head, 2 lanes, hipGraph (config 4) --------
+# ---- YOLOv8-n at the bench batch, 480 x 640 frames, tail-decode head, 2 lanes, hipGraph (config 4)
 # With random-init weights the detections are a dense band of near-tied scores (~0.3, many exact
 # bf16 ties), so comparing two NMS outputs would test the conditioning of greedy NMS, not the
 # kernels.  The parity is therefore split at the decode: (1) the tail launches' decoded rows
@@ -134,7 +135,8 @@ def _map_back(boxes, frame_hw, geom):
 def _yolo_parity(sabotage: bool):
     import bench
     from aiko_services_amd.ops import reference as R
-    p, q = _pipeline(bench.yolo_definition(64, True, 480, 640, "scatter", 2))
+    B = bench.parse_args(["--model", "yolov8n"]).batch
+    p, q = _pipeline(bench.yolo_definition(B, True, 480, 640, "scatter", 2))
     for fid in range(YOLO_SETUP):
         _run(p, q, fid, "detections")
     m = _element(p, "YoloDetector").model
@@ -153,11 +155,11 @@ def _yolo_parity(sabotage: bool):
         rb, rs, rc = R.yolo_decode_ref(feats, (8, 16, 32), m.nc)
         # the decoded rows stay in the workspace of the lane that ran the frame (the lane is not
         # visible once the frame left the pipeline): the lane whose rows are this frame's
-        lanes = [t for t in ("", "lane1.") if (t + "scores", (64, A), torch.float32) in m._ws]
-        tag = min(lanes, key=lambda t: (m._ws[(t + "scores", (64, A), torch.float32)][:n_images] - rs).abs().mean().item())
-        kb = m._ws[(tag + "boxes", (64, A, 4), torch.float32)][:n_images].clone()
-        ks = m._ws[(tag + "scores", (64, A), torch.float32)][:n_images].clone()
-        kc = m._ws[(tag + "cls", (64, A), torch.int32)][:n_images].clone()
+        lanes = [t for t in ("", "lane1.") if (t + "scores", (B, A), torch.float32) in m._ws]
+        tag = min(lanes, key=lambda t: (m._ws[(t + "scores", (B, A), torch.float32)][:n_images] - rs).abs().mean().item())
+        kb = m._ws[(tag + "boxes", (B, A, 4), torch.float32)][:n_images].clone()
+        ks = m._ws[(tag + "scores", (B, A), torch.float32)][:n_images].clone()
+        kc = m._ws[(tag + "cls", (B, A), torch.int32)][:n_images].clone()
         torch.cuda.synchronize()
         # (1) decode parity over every anchor
         ds = (ks - rs).abs()
@@ -189,7 +191,7 @@ def _yolo_parity(sabotage: bool):
                           d[i:i + 2].tolist() if i < n else None, ref[i:i + 2].tolist() if i < keep.numel() else None,
                           "above conf", int((ks[b] > m.conf).sum()))
                 out["nms_exact"] = False
-    print("yolov8n B=64 parity:", out)
+    print("yolov8n bench-batch parity:", out)
     return out
 
 
