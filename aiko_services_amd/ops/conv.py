@@ -270,8 +270,8 @@ WIDE4_OCC_TILES = ((128, 128), (128, 256))
 # for the short-K layers without a residual (reductions, projections).  Measured at B=320 (round
 # 5): fused stage-2 projection 159.6 vs 163.6 us (variant 8), stage-3 reduction 37.4 vs 36.1,
 # stage-3 -> 4 reduction 70.6 vs 66.1 — the tile-boundary fill was not the limit either; the
-# tuner keeps it where it wins.  The residual form (expansions) is opt-in (AIKO_CONV_EXTRA=20):
-# 60-61 vs 49.7 us (stage 4), 87.6 vs 76.7 us (stage 3, resident-weight kernel)
+# tuner keeps it where it wins (residual form, isolated at B=320: 60-61 vs 49.7 us at stage 4,
+# 87.6 vs 76.7 us at stage 3 against the resident-weight kernel)
 WIDE_PERS_TILES = ((256, 256), (256, 128), (128, 256))
 # variant 18: the same kernel with an exact-N tile (the MFMAs and epilogue cover exactly
 # these channel counts — the YOLO head's 80-class and 64 + 80 box/class convs — instead of
@@ -484,12 +484,13 @@ def _tune(key, M, cout, launch, buf_ok=False, narrow_ok=False, patch_ok=False, p
             cands += [t + (8,) for t in WIDE8_TILES] + [t + (9,) for t in WIDE_OCC_TILES]
             if 19 in _EXTRA:
                 cands += [t + (19,) for t in WIDE4_OCC_TILES]
-            # variant 20 wins its layers in isolation but the ResNet bench (two concurrent frame
-            # lanes) runs 1 % faster without it (89.8k vs 90.7k frames/s, 5 + 5 interleaved runs on
-            # two boxes, scripts/r5_skip_ab.sh; YOLO / Whisper unchanged): opt-in, AIKO_CONV_EXTRA=20
-            if cout <= 2048 and not has_res and 20 in _EXTRA:
+            # variant 20: at B=320 the ResNet bench ran 1 % faster without it (89.8k vs 90.7k,
+            # round 5, scripts/r5_skip_ab.sh); at the round-6 default B=640, interleaved on two
+            # boxes: 94.6k / 94.2k with vs 93.2k / 93.2k without, then 92.63-92.70k vs
+            # 92.64-92.86k (YOLOv8-n 50.0k both): default again, AIKO_CONV_SKIP=20 leaves it out
+            if cout <= 2048 and not has_res:
                 cands += [t + (20,) for t in WIDE_PERS_TILES]
-            elif cout <= 2048 and key[2] >= 192 and 20 in _EXTRA:   # with a residual: 3-slot forms
+            elif cout <= 2048 and key[2] >= 192:   # with a residual: 3-slot forms
                 cands += [t + (20,) for t in WIDE_PERS_TILES if t != (256, 256)]
             if cout in EXACT_N:
                 cands += [(256, cout, 18), (128, cout, 18)]
