@@ -1,0 +1,9 @@
+#!/bin/bash
+# ResNet-50 at the default batch: frame lanes x batches in flight, interleaved
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+for i in 1 2; do
+  for a in "--lanes 2 --depth 2" "--lanes 3 --depth 2" "--lanes 2 --depth 3" "--lanes 3 --depth 3"; do
+    echo -n "$a: "; timeout -k 10 240 python bench.py --steps 20 --warmup 5 $a 2>&1 | grep -o '"value": [0-9.]*\|"p50_latency_ms": [0-9.]*' | tr '\n' ' ' || exit 1
+    echo
+  done
+done
