@@ -444,3 +444,22 @@ def test_yolo_decode_in_tail_matches_decode_kernel(native, monkeypatch):
     torch.cuda.synchronize()
     assert torch.equal(cnt_f, cnt_d)
     assert (det_f - det_d).abs().max().item() < 1e-2 * max(1.0, det_d.abs().max().item())
+
+
+@pytest.mark.parametrize("B", [96, 160])
+def test_topk_nms_workgroups_per_image(native, B):
+    """The fused NMS splits each image over G = CUs / B workgroups (at most 4, last arriver runs
+    the scan): B = 96 gives G = 2 on a 256-CU MI355X, B = 160 gives G = 1 (everything in LDS);
+    B = 3 (test_topk_nms_matches_reference) gives G = 4.  Every image equals nms_ref."""
+    from aiko_services_amd.ops import detect as DT
+    from aiko_services_amd.ops import reference as R
+    g = torch.Generator().manual_seed(B)
+    boxes, scores, cls = _random_dets(B, 3000, g, n_cls=2)
+    det, count = DT.topk_nms(boxes, scores, cls, conf=0.2, iou=0.5, max_candidates=1024, max_det=300)
+    torch.cuda.synchronize()
+    for b in range(0, B, 7):
+        keep = R.nms_ref(boxes[b], scores[b], cls[b], 0.2, 0.5, 1024, 300)
+        n = int(count[b])
+        assert n == keep.numel(), (b, n, keep.numel())
+        ref = torch.cat([boxes[b][keep].clamp(min=0), scores[b][keep, None], cls[b][keep, None].float()], 1)
+        assert torch.allclose(det[b, :n], ref, atol=1e-4), b
