@@ -61,6 +61,8 @@ class Broker:
         self.trie = C.TopicTrie()        # filter -> {conn: qos}
         self.retained: dict = {}         # topic -> (payload, qos)
         self._running = False
+        self._serve_thread = None
+        self._done = threading.Event()   # set once serve_forever closed every socket
         self._wake_r, self._wake_w = socket.socketpair()
         self.stats = {"published": 0, "delivered": 0, "connections": 0}
 
@@ -87,17 +89,23 @@ class Broker:
         self.sel.register(self._wake_r, selectors.EVENT_READ, "wake")
         return self.port
 
-    def stop(self):
+    def stop(self, wait: float = 5.0):
+        """Stop serving; unless called from the serving thread, wait (up to ``wait`` s) until the
+        listening sockets are closed, so the port can be bound again right away."""
         self._running = False
         try:
             self._wake_w.send(b"x")
         except OSError:
             pass
+        if wait and self._serve_thread is not None and threading.current_thread() is not self._serve_thread:
+            self._done.wait(wait)
 
     def serve_forever(self):
         if self.lsock is None:
             self.bind()
         self._running = True
+        self._serve_thread = threading.current_thread()
+        self._done.clear()
         last_sweep = time.monotonic()
         try:
             while self._running:
@@ -129,6 +137,7 @@ class Broker:
                 self.lsock.close()
             if self.ws_lsock:
                 self.ws_lsock.close()
+            self._done.set()
 
     # ---- connection handling ----------------------------------------------------------------
     def _accept(self, websocket=False):
