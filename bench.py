@@ -168,7 +168,7 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--batch", type=int, default=None,
-                    help="frames per GPU per step (default: ResNet-50 640 (320 for --parallel pp), "
+                    help="frames per GPU per step (default: ResNet-50 640 (both --parallel modes), "
                          "YOLOv8-n 192, Whisper 28 streams).  Batches are sized for the chip's 256 CUs: "
                          "ResNet-50 at B = 320 k runs stage 3 as 245 k tiles of 256 rows (96 %% of the "
                          "CUs busy per round) where B=256 gives 196 tiles (77 %%) and 448 / 768 land "
@@ -178,7 +178,8 @@ def parse_args(argv=None) -> argparse.Namespace:
                          "93.2-93.3k (p50 28-31 ms): 640 takes +3.7 %% for 2x the latency.  YOLOv8-n "
                          "(scripts/batch_sweep_r6.sh, probe/yolo_batch_sweep.sh): B=64 44.5-46.4k, 128 "
                          "48.8-48.9k, 192 49.5-50.4k (p50 7.8 ms), 256 50.4k, 320 50.6-51.0k.  "
-                         "Whisper-small: 14 streams 3.36-3.38k, 28 3.42k, 42 3.42k windows/s")
+                         "Whisper-small: 14 streams 3.36-3.38k, 28 3.42k, 42 3.42k windows/s.  Config 3 (--parallel "
+                         "pp, world 1): B=320 79.6-79.9k, 640 83.4-84.1k (scripts/probe/pp_batch_ab.sh)")
     ap.add_argument("--height", type=int, default=224)
     ap.add_argument("--width", type=int, default=224)
     ap.add_argument("--no-graph", action="store_true", help="disable hipGraph capture")
@@ -218,8 +219,7 @@ def parse_args(argv=None) -> argparse.Namespace:
     if (a.parallel == "pp" or a.model == "yolov8n") and not explicit_hw:
         a.height, a.width = 480, 640          # configs 3/4 decode VGA video frames
     if a.batch is None:
-        a.batch = (192 if a.model == "yolov8n" else 28 if a.model.startswith("whisper")
-                   else 320 if a.parallel == "pp" else 640)
+        a.batch = 192 if a.model == "yolov8n" else 28 if a.model.startswith("whisper") else 640
     return a
 
 

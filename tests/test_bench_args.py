@@ -24,5 +24,5 @@ def test_model_defaults_and_explicit_overrides():
     assert bench.parse_args(["--model", "whisper-small"]).batch == 28
     assert bench.parse_args(["--batch", "256"]).batch == 256
     p = bench.parse_args(["--parallel", "pp", "--height", "224", "--width", "224"])
-    assert (p.height, p.width) == (224, 224) and p.batch == 320
+    assert (p.height, p.width) == (224, 224) and p.batch == 640
     assert (bench.parse_args(["--parallel", "pp"]).height, bench.parse_args([]).height) == (480, 224)
