@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-6 bench lines at the final defaults (ResNet-50 B=640, pp world 1 B=320, YOLOv8-n B=192,
+# Round-6 bench lines at the final defaults (ResNet-50 B=640 in both modes, YOLOv8-n B=192,
 # Whisper-small 28 streams), two of each but pp, on one box -> gpurun_out/r6bench/bench_lines.jsonl
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
