@@ -248,10 +248,15 @@ __global__ __launch_bounds__(64 * kBnNW, 1) void bneck_fused_kernel(BnParams p) 
   const int nl = (R0 + nrows - 1) / H;
   const int vlast = (nl - n0) * HV + (R0 + nrows - 1 - nl * H) + 2;
   // VMEM ops this wave has issued (DMAs and y stores; wave-uniform): a DMA issued when the count
-  // became m has landed once vmcnt <= ops - m.  mk[v & 3] = that m for the row in x slot v & 3
-  // (-1: a zero halo row, nothing to wait for; conv1 then writes zeros)
+  // became m has landed once vmcnt <= ops - m.  The marks of the last four virtual rows brought in
+  // (vdma - 1 - d in field d) live in ONE 64-bit register, 16 bits each: bit 15 = a DMA was
+  // issued (clear: a zero halo row, nothing to wait for; conv1 then writes zeros), bits 0..14 =
+  // m mod 2^15 (ops - m is < 64, so the difference mod 2^15 is exact).  Four separate marks
+  // read through the lambdas' captured references were folded into a select of pointers, which
+  // put them in scratch — and the scratch load's vmcnt(0) drained every in-flight DMA at each
+  // wait (rounds 3-5)
   int ops = 0;
-  int mk0 = -1, mk1 = -1, mk2 = -1, mk3 = -1;
+  unsigned long long marks = 0;
   int vdma = h0, dn = n0, dr = h0 - 1;             // next virtual row to bring in = (image, row)
   auto dma_next = [&]() {                          // x row vdma -> ring slot vdma & 3
     const int v = vdma++;
@@ -271,18 +276,15 @@ __global__ __launch_bounds__(64 * kBnNW, 1) void bneck_fused_kernel(BnParams p) 
       dr = -1;
       ++dn;
     }
-    switch (v & 3) {
-      case 0: mk0 = m; break;
-      case 1: mk1 = m; break;
-      case 2: mk2 = m; break;
-      default: mk3 = m; break;
-    }
+    marks = (marks << 16) | (m >= 0 ? 0x8000ull | (unsigned)(m & 0x7fff) : 0ull);
   };
-  auto slot_m = [&](int v) { return (v & 3) == 0 ? mk0 : (v & 3) == 1 ? mk1 : (v & 3) == 2 ? mk2 : mk3; };
-  auto row_valid = [&](int v) { return slot_m(v) >= 0; };    // v is in the ring
+  auto slot_mark = [&](int v) {                    // v in [vdma - 4, vdma)
+    return (unsigned)(marks >> (16 * (vdma - 1 - v))) & 0xffffu;
+  };
+  auto row_valid = [&](int v) { return (slot_mark(v) & 0x8000u) != 0; };    // v is in the ring
   auto wait_row = [&](int v) {                     // this wave's DMA of x row v has landed
-    const int m = slot_m(v);
-    if (m >= 0) bn_vm_wait(__builtin_amdgcn_readfirstlane(ops - m));
+    const unsigned mk = slot_mark(v);
+    if (mk & 0x8000u) bn_vm_wait(__builtin_amdgcn_readfirstlane((int)(((unsigned)ops - mk) & 0x7fffu)));
   };
 
   // conv1: x row v -> t1 slot v % 3 (a zero row for the halo rows)

@@ -41,6 +41,7 @@ def _reference(x_nchw, c1, c2, c3, down):
     (2, 20, False, 1), (2, 20, True, 1),          # one workgroup streaming two images
     (1, 56, False, 1), (2, 13, False, 4),         # one image / uneven split (26 = 7 + 7 + 6 + 6)
     (4, 1, False, 1), (3, 2, True, 2),            # images of one / two rows: a boundary every row or two
+    (40, 56, False, 0), (24, 56, True, 0),        # every CU streaming several rows: counted DMA waits
 ])
 def test_bneck_fused_matches_torch(native, B, H, dual, grid):
     from aiko_services_amd.ops import conv as C
