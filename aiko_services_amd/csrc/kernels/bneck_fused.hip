@@ -87,7 +87,7 @@ struct BnParams {
   int B, H;
   int rows_per_wg, rows_rem;   // output rows R = B * H split into contiguous per-workgroup ranges
   unsigned* dbg;        // diagnostic s_memtime stamps of wave 0, [G][rows_per_wg + 1][8] (null: off)
-  int mode;             // ablation bits for timing studies (AIKO_BN_MODE; 0 = the real kernel)
+  int mode;             // schedule / ablation bits (AIKO_BN_MODE; default 1024 = split conv2 schedule)
 };
 
 __device__ __forceinline__ void bn_barrier() {
@@ -521,8 +521,11 @@ extern "C" int aiko_bneck_fused(const void* x, const void* w1, const float* b1, 
   p.rows_per_wg = R / G;
   p.rows_rem = R % G;
   p.dbg = dbg;
+  // default 1024 = the split conv2 schedule (the next row's first 12 k-steps at the end of phase
+  // B): neutral while every wait drained to vmcnt(0) (round 5), 3 % faster isolated once the
+  // counted waits worked (round 6: 544 vs 561 us identity, 475 vs 486 us projection at B=640)
   const char* mode = getenv("AIKO_BN_MODE");
-  p.mode = mode ? atoi(mode) : 0;
+  p.mode = mode ? atoi(mode) : 1024;
   if (cin == 256)
     hipLaunchKernelGGL(bneck_fused_kernel<256>, dim3(G), dim3(64 * kBnNW), 0, stream, p);
   else
