@@ -1411,7 +1411,10 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_pers2_kernel(Fp8GemmParams p,
     auto epi = [&](auto I) {
       constexpr int i = decltype(I)::value;
       if constexpr (i + 1 < MI) ldres(i + 1);
-      float r1 = p.sa ? rs[i] : 1.f, r2 = 0.f;
+      // MX-fp8 A carries its scales in the blocks (the host refuses sa with amx): with rs dead the
+      // <256, MXA, RES> variant fits its 256 VGPRs (it spilled 24 B, and one reload's vmcnt(0)
+      // inside the fused epilogue drained the next K block's DMA every tile)
+      float r1 = !MXA && p.sa ? rs[i] : 1.f, r2 = 0.f;
       if constexpr (LN == 2) {                       // row statistics from the lane groups' partials
         float t1 = st1[i], t2 = st2[i];
 #pragma unroll
@@ -1731,6 +1734,7 @@ extern "C" int aiko_gemm_fp8(const void* a, const void* b, const float* sa, cons
   p.ldq = ldq;
   p.ysr = ysr;
   if ((amx || yq) && variant != 1 && variant != 3 && variant != 4 && variant != 5) return -1;   // MX: LDS-DMA kernels
+  if (amx && sa) return -1;                          // MX-fp8 A: block scales only, no per-row scales
   p.a = static_cast<const uint8_t*>(a);
   p.b = static_cast<const uint8_t*>(b);
   p.sa = sa; p.sb = sb; p.bias = bias;
