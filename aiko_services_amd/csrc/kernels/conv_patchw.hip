@@ -154,20 +154,22 @@ __global__ __launch_bounds__(512, 1) void conv3x3_patchw_kernel(
   };
 
   // ---- per-lane output pixels: block i of group wr -> tile pixel p = 98 wr + 16 i + fr (past the
-  // group's 98: masked, its store dropped).  addr[i][s]: LDS byte offset of the pixel's tap-(0, s)
-  // input slot; tap (r, s) adds the immediate r * PW * 64.
-  int addr[MI][3];
+  // group's 98: masked, its store dropped).  addr[i]: LDS byte offset of the pixel's tap-(0, 0)
+  // input slot; tap (r, s) reads pixel q0 + s, i.e. addr + 64 s with the slot swizzle of q0 + s:
+  // bit 5 of the offset flips where ((q0 + s) >> 2) & 1 differs from (q0 >> 2) & 1 — bit i + 5 of
+  // sflip[s - 1] for block i — and tap row r adds the immediate r * PW * 64.  (Holding all three
+  // offsets per block cost 14 VGPRs more and spilled 5 dwords, reloaded every tile.)
+  int addr[MI];
+  int sflip[2] = {0, 0};
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int pl = 16 * i + fr;
     const int p = WPX * wr + pl;
     const int ohl = p / W, ow = p - ohl * W;
     const int q0 = pl < WPX ? ohl * PW + ow : 0;
+    addr[i] = q0 * 64 + ((fq ^ (((q0 >> 2) & 1) << 1)) << 4);
 #pragma unroll
-    for (int s = 0; s < 3; ++s) {
-      const int q = q0 + s;
-      addr[i][s] = q * 64 + ((fq ^ (((q >> 2) & 1) << 1)) << 4);
-    }
+    for (int s = 1; s < 3; ++s) sflip[s - 1] |= ((((q0 + s) ^ q0) >> 2) & 1) << (i + 5);
   }
   // bias into LDS (visible after the first group's barrier; read only by the epilogues)
   if (tid < N) s_bias[tid] = bias ? bias[tid] : 0.f;
@@ -194,6 +196,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_patchw_kernel(
       issue_w(nxt % STEPS, k + nxt / STEPS < my_tiles);
     }
     const unsigned char* P = smem + (CH & 1) * P_BYTES + TR * PW * 64;
+    // opaque per group: keeps the compiler from hoisting the tap-1/2 offsets out of the tile loop
+    // (14 more live VGPRs, i.e. the spill this layout removes)
+    int sf[2] = {sflip[0], sflip[1]};
+    asm volatile("" : "+v"(sf[0]), "+v"(sf[1]));
 #pragma unroll
     for (int ts = 0; ts < GS; ++ts) {
       if (ts) __builtin_amdgcn_sched_barrier(0);          // keep the next tap's fragment loads from piling up
@@ -203,7 +209,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_patchw_kernel(
       for (int j = 0; j < 4; ++j) wf[j] = *reinterpret_cast<const bf16x8*>(Wp + j * 1024);
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
-        const bf16x8 xf = *reinterpret_cast<const bf16x8*>(P + addr[i][ts]);
+        const int a = ts == 0 ? addr[i] : (addr[i] ^ ((sf[ts - 1] >> i) & 32)) + 64 * ts;
+        const bf16x8 xf = *reinterpret_cast<const bf16x8*>(P + a);
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf, acc[j][i], 0, 0, 0);
       }

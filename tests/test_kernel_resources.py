@@ -37,6 +37,7 @@ def _functions(asm: str) -> dict:
 @pytest.mark.parametrize("src,pattern,n_min", [
     ("bneck_fused.hip", "bneck_fused_kernel", 2),          # identity and projection blocks
     ("gemm_fp8.hip", "gemm_fp8_pers2_kernel", 10),         # every persistent fp8 GEMM variant
+    ("conv_patchw.hip", "conv3x3_patchw_kernelILi28ELi32E", 1),   # the default patch pitch
 ])
 def test_counted_wait_kernels_use_no_scratch(tmp_path, src, pattern, n_min):
     fns = {k: v for k, v in _functions(_device_asm(src, tmp_path)).items() if pattern in k}
